@@ -1,0 +1,653 @@
+// bucketsort.hip -- MSD bucket sort of level-1 partitions with a fused
+// merge-join count (the sorting_phase + mergejoin_phase of the reference m-way
+// join, src/joins/sortmergejoin_multiway.c:388-460, 559-599, re-designed for
+// MI355X).
+//
+// After the level-1 radix partition (partition.hip) every bucket b holds the
+// tuples whose key falls in one contiguous key range of the RangePlan.
+//
+//   k_tilepass   : every bucket is cut into tiles of TILE2 tuples.  A tile is
+//                  loaded into registers, counted by its level-2 digit d2 in an
+//                  LDS histogram, staged in LDS grouped by d2 and written back
+//                  linearly (fully coalesced), together with the tile's
+//                  exclusive d2 prefix (uint16 per digit).  Traffic: 2w.
+//   k_bucketpass : one workgroup per sub-bucket (b, d2).  It gathers the
+//                  sub-bucket's piece from every tile of bucket b (pieces are
+//                  contiguous runs, read with 64 consecutive lanes), counting-
+//                  sorts the pieces in LDS by the level-3 digit, fixes the few
+//                  equal-digit runs with an in-LDS insertion sort on the full
+//                  (key,payload) order, writes the sorted sub-bucket to its
+//                  final position (coalesced), and -- for a join -- counts the
+//                  matching (r, s) pairs of the R and S sub-buckets that are
+//                  both resident in LDS.  Traffic: 2w, the join reads nothing.
+//
+// Sub-buckets that do not fit the LDS capacity or hold long runs of equal
+// digits (heavy skew, e.g. Zipf hot keys) are queued and sorted by the
+// segmented merge sort (mergesort.hip); their join count uses the merge-path
+// join-count kernel.
+#include "smj_common.hpp"
+#include "smj_internal.hpp"
+
+namespace smj {
+
+constexpr int TP_THREADS = 256;
+constexpr int TP_ITEMS = 16;
+constexpr int TILE2 = TP_THREADS * TP_ITEMS;  // 4096 tuples per tile
+
+constexpr int BP_THREADS = 256;
+#ifdef KEY_8B
+constexpr int BP_CAP = 1024;  // tuples per relation per sub-bucket in LDS
+#else
+constexpr int BP_CAP = 2048;
+#endif
+constexpr int BP_ITEMS = BP_CAP / BP_THREADS;
+constexpr int BP_D3MAX = 10;
+constexpr int BP_PMAX = 512;   // max tiles (pieces) per bucket in the LDS path
+constexpr int BP_RUNMAX = 48;  // longest equal-digit run fixed in LDS
+
+struct TileTable {
+    uint64_t* off;     // tile start in `part`
+    uint32_t* len;     // tile length
+    uint32_t* bucket;  // owning bucket
+    uint32_t* btile0;  // first tile of every bucket (nbuckets + 1)
+    uint16_t* pref;    // [tile][1<<D2] exclusive prefix
+    uint32_t* ntiles;  // device scalar
+};
+
+struct OvfEntry {
+    uint32_t bucket, d2;
+    uint32_t nr[2];
+    uint64_t off[2];  // offset of the sub-bucket inside its bucket
+};
+
+// ---------------------------------------------------------------------------
+// tile table: one workgroup scans the per-bucket tile counts
+__global__ void __launch_bounds__(256)
+k_tiles(const uint64_t* __restrict__ bstart, const int64_t* __restrict__ bcount,
+        uint32_t nb, TileTable tt) {
+    __shared__ uint32_t scr[8];
+    __shared__ uint32_t base_sh;
+    if (threadIdx.x == 0) base_sh = 0;
+    __syncthreads();
+    for (uint32_t b0 = 0; b0 < nb; b0 += 256) {
+        uint32_t b = b0 + threadIdx.x;
+        uint32_t nt = 0;
+        if (b < nb) nt = (uint32_t)((bcount[b] + TILE2 - 1) / TILE2);
+        uint32_t tot;
+        uint32_t ex = block_exclusive_scan(nt, scr, &tot);
+        uint32_t t0 = base_sh + ex;
+        if (b < nb) {
+            tt.btile0[b] = t0;
+            for (uint32_t i = 0; i < nt; i++) {
+                uint64_t o = (uint64_t)i * TILE2;
+                int64_t rem = bcount[b] - (int64_t)o;
+                tt.off[t0 + i] = bstart[b] + o;
+                tt.len[t0 + i] = (uint32_t)(rem < TILE2 ? rem : TILE2);
+                tt.bucket[t0 + i] = b;
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) base_sh += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        tt.btile0[nb] = base_sh;
+        *tt.ntiles = base_sh;
+    }
+}
+
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(TP_THREADS)
+k_tilepass(const Tup* __restrict__ part, Tup* __restrict__ tmp, TileTable tt,
+           const RangePlan* __restrict__ plan_dev, uint32_t nb2) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    const RangePlan P = *plan_dev;
+    Tup* stage = reinterpret_cast<Tup*>(lds_raw);
+    uint32_t* hist = reinterpret_cast<uint32_t*>(lds_raw + TILE2 * sizeof(Tup));
+    uint32_t* scr = hist + nb2;
+
+    const uint32_t t = blockIdx.x;
+    if (t >= *tt.ntiles) return;
+    const uint64_t off = tt.off[t];
+    const uint32_t len = tt.len[t];
+    const uint32_t b = tt.bucket[t];
+
+    for (uint32_t d = threadIdx.x; d < nb2; d += TP_THREADS) hist[d] = 0;
+    Tup v[TP_ITEMS];
+    uint32_t dg[TP_ITEMS];
+#pragma unroll
+    for (int j = 0; j < TP_ITEMS; j++) {
+        uint32_t i = j * TP_THREADS + threadIdx.x;
+        if (i < len) v[j] = part[off + i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < TP_ITEMS; j++) {
+        uint32_t i = j * TP_THREADS + threadIdx.x;
+        if (i < len) {
+            dg[j] = plan_d2(P, plan_rel(P, tup_key(v[j])), b);
+            atomicAdd(&hist[dg[j]], 1u);
+        }
+    }
+    __syncthreads();
+    // exclusive scan of the nb2 bins (contiguous range per thread)
+    const uint32_t per = (nb2 + TP_THREADS - 1) / TP_THREADS;
+    const uint32_t d0 = threadIdx.x * per;
+    uint32_t loc = 0;
+    for (uint32_t k = 0; k < per; k++)
+        if (d0 + k < nb2) loc += hist[d0 + k];
+    uint32_t tot;
+    uint32_t ex = block_exclusive_scan(loc, scr, &tot);
+    uint16_t* pref = tt.pref + (uint64_t)t * nb2;
+    for (uint32_t k = 0; k < per; k++) {
+        uint32_t d = d0 + k;
+        if (d < nb2) {
+            uint32_t c = hist[d];
+            hist[d] = ex;
+            pref[d] = (uint16_t)ex;
+            ex += c;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < TP_ITEMS; j++) {
+        uint32_t i = j * TP_THREADS + threadIdx.x;
+        if (i < len) {
+            uint32_t pos = atomicAdd(&hist[dg[j]], 1u);
+            stage[pos] = v[j];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < TP_ITEMS; j++) {
+        uint32_t i = j * TP_THREADS + threadIdx.x;
+        if (i < len) tmp[off + i] = stage[i];
+    }
+}
+
+// ---------------------------------------------------------------------------
+struct Piece {
+    uint64_t src;
+    uint32_t len;
+    uint32_t dst;
+};
+
+struct BucketPassArgs {
+    const Tup* tmp[2];
+    Tup* out[2];
+    const uint64_t* bstart[2];
+    TileTable tt[2];
+    int nrel;
+    const RangePlan* plan_dev;
+    unsigned long long* count_dev;
+    uint32_t nb2;  // level-2 table stride (>= 1 << plan.D2)
+    OvfEntry* ovf;
+    uint32_t* novf;
+    uint32_t ovf_cap;
+};
+
+// LDS layout (bytes):
+//   B[2]    : 2 * BP_CAP Tups
+//   h[2]    : 2 * 2^D3MAX uint32  (bin starts after scan)
+//   fill    : 2^D3MAX uint32
+//   pieces  : BP_PMAX Piece
+//   misc    : 32 uint32
+constexpr size_t BP_LDS = 2 * BP_CAP * sizeof(Tup) +
+                          3 * (1u << BP_D3MAX) * sizeof(uint32_t) +
+                          BP_PMAX * sizeof(Piece) + 32 * sizeof(uint32_t);
+
+__device__ __forceinline__ uint32_t piece_of(const Piece* pc, uint32_t np,
+                                             uint32_t i) {
+    // last piece with dst <= i (pieces with len 0 share dst; pick any)
+    uint32_t lo = 0, hi = np;  // invariant: pc[lo].dst <= i
+    while (hi - lo > 1) {
+        uint32_t m = (lo + hi) >> 1;
+        if (pc[m].dst <= i) lo = m; else hi = m;
+    }
+    return lo;
+}
+
+// insertion sort of a short run in LDS
+__device__ __forceinline__ void lds_insertion_sort(Tup* a, uint32_t n) {
+    for (uint32_t i = 1; i < n; i++) {
+        Tup x = a[i];
+        uint32_t j = i;
+        while (j > 0 && tup_less(x, a[j - 1])) {
+            a[j] = a[j - 1];
+            j--;
+        }
+        a[j] = x;
+    }
+}
+
+__global__ void __launch_bounds__(BP_THREADS)
+k_bucketpass(BucketPassArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    const RangePlan P = *A.plan_dev;
+    const uint32_t nb2 = A.nb2;
+    const uint32_t nb3 = 1u << P.D3;
+    Tup* B[2];
+    B[0] = reinterpret_cast<Tup*>(lds_raw);
+    B[1] = B[0] + BP_CAP;
+    uint32_t* h[2];
+    h[0] = reinterpret_cast<uint32_t*>(B[1] + BP_CAP);
+    h[1] = h[0] + (1u << BP_D3MAX);
+    uint32_t* fill = h[1] + (1u << BP_D3MAX);
+    Piece* pc = reinterpret_cast<Piece*>(fill + (1u << BP_D3MAX));
+    uint32_t* misc = reinterpret_cast<uint32_t*>(pc + BP_PMAX);
+    // misc[0..7] scan scratch, misc[16..] flags
+
+    const uint32_t b = blockIdx.x / nb2;
+    const uint32_t d2 = blockIdx.x % nb2;
+    const int nrel = A.nrel;
+
+    // ---- phase 1: sizes and offsets of the sub-bucket in every relation
+    uint32_t nsub[2] = {0, 0};
+    uint64_t offsub[2] = {0, 0};
+    bool ovf = false;
+    for (int r = 0; r < nrel; r++) {
+        const TileTable& tt = A.tt[r];
+        const uint32_t t0 = tt.btile0[b], t1 = tt.btile0[b + 1];
+        const uint32_t nt = t1 - t0;
+        if (nt > BP_PMAX) ovf = true;
+        uint32_t mylen = 0;
+        uint64_t mylo = 0;
+        for (uint32_t t = t0 + threadIdx.x; t < t1; t += BP_THREADS) {
+            const uint16_t* pf = tt.pref + (uint64_t)t * nb2;
+            uint32_t lo = pf[d2];
+            uint32_t hi = (d2 + 1 < nb2) ? pf[d2 + 1] : tt.len[t];
+            mylen += hi - lo;
+            mylo += lo;
+        }
+        mylen = wave_sum(mylen);
+        mylo = wave_sum(mylo);
+        if (lane_id() == 0) {
+            misc[(threadIdx.x >> 6)] = mylen;
+            reinterpret_cast<uint64_t*>(misc + 8)[threadIdx.x >> 6] = mylo;
+        }
+        __syncthreads();
+        uint32_t n = 0;
+        uint64_t o = 0;
+        for (int w = 0; w < BP_THREADS / 64; w++) {
+            n += misc[w];
+            o += reinterpret_cast<uint64_t*>(misc + 8)[w];
+        }
+        __syncthreads();
+        nsub[r] = n;
+        offsub[r] = o;
+        if (n > BP_CAP) ovf = true;
+    }
+
+    // ---- phase 2: gather + counting sort by d3 into B[r]
+    int maxrun = 0;
+    if (threadIdx.x == 0) misc[28] = 0;  // any key clamped by the plan?
+    __syncthreads();
+    if (!ovf) {
+        for (int r = 0; r < nrel; r++) {
+            const TileTable& tt = A.tt[r];
+            const uint32_t t0 = tt.btile0[b], t1 = tt.btile0[b + 1];
+            const uint32_t nt = t1 - t0;
+            // piece table
+            uint32_t len = 0;
+            uint64_t src = 0;
+            for (uint32_t base = 0; base < nt; base += BP_THREADS) {
+                uint32_t t = t0 + base + threadIdx.x;
+                len = 0;
+                if (base + threadIdx.x < nt) {
+                    const uint16_t* pf = tt.pref + (uint64_t)t * nb2;
+                    uint32_t lo = pf[d2];
+                    uint32_t hi = (d2 + 1 < nb2) ? pf[d2 + 1] : tt.len[t];
+                    len = hi - lo;
+                    src = tt.off[t] + lo;
+                }
+                uint32_t tot;
+                uint32_t ex = block_exclusive_scan(len, misc, &tot);
+                uint32_t prev = base == 0 ? 0 : misc[20];
+                if (base + threadIdx.x < nt) {
+                    pc[base + threadIdx.x].src = src;
+                    pc[base + threadIdx.x].len = len;
+                    pc[base + threadIdx.x].dst = prev + ex;
+                }
+                __syncthreads();
+                if (threadIdx.x == 0) misc[20] = prev + tot;
+                __syncthreads();
+            }
+            for (uint32_t d = threadIdx.x; d < nb3; d += BP_THREADS) h[r][d] = 0;
+            __syncthreads();
+            const uint32_t n = nsub[r];
+            const uint32_t np = nt;
+            Tup v[BP_ITEMS];
+            uint32_t dg[BP_ITEMS];
+            const uint32_t d12 = (b << P.D2) | d2;
+#pragma unroll
+            for (int j = 0; j < BP_ITEMS; j++) {
+                uint32_t i = j * BP_THREADS + threadIdx.x;
+                if (i < n) {
+                    uint32_t p = piece_of(pc, np, i);
+                    v[j] = A.tmp[r][pc[p].src + (i - pc[p].dst)];
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < BP_ITEMS; j++) {
+                uint32_t i = j * BP_THREADS + threadIdx.x;
+                if (i < n) {
+                    const int64_t k = tup_key(v[j]);
+                    const uint64_t ku = key_u(k), bu = key_u(P.base);
+                    if (ku < bu || ku - bu > P.span) misc[28] = 1;
+                    dg[j] = plan_d3(P, plan_rel(P, k), d12);
+                    atomicAdd(&h[r][dg[j]], 1u);
+                }
+            }
+            __syncthreads();
+            // exclusive scan of bins, record max run
+            const uint32_t per = (nb3 + BP_THREADS - 1) / BP_THREADS;
+            const uint32_t q0 = threadIdx.x * per;
+            uint32_t loc = 0, mx = 0;
+            for (uint32_t k = 0; k < per; k++) {
+                if (q0 + k < nb3) {
+                    uint32_t c = h[r][q0 + k];
+                    loc += c;
+                    mx = c > mx ? c : mx;
+                }
+            }
+            uint32_t tot;
+            uint32_t ex = block_exclusive_scan(loc, misc, &tot);
+            for (uint32_t k = 0; k < per; k++) {
+                uint32_t d = q0 + k;
+                if (d < nb3) {
+                    uint32_t c = h[r][d];
+                    h[r][d] = ex;
+                    fill[d] = ex;
+                    ex += c;
+                }
+            }
+            // max over block
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                uint32_t y = __shfl_xor(mx, o, 64);
+                mx = y > mx ? y : mx;
+            }
+            if (lane_id() == 0) misc[24 + (threadIdx.x >> 6)] = mx;
+            __syncthreads();
+            for (int w = 0; w < BP_THREADS / 64; w++)
+                maxrun = (int)misc[24 + w] > maxrun ? (int)misc[24 + w] : maxrun;
+#pragma unroll
+            for (int j = 0; j < BP_ITEMS; j++) {
+                uint32_t i = j * BP_THREADS + threadIdx.x;
+                if (i < n) {
+                    uint32_t pos = atomicAdd(&fill[dg[j]], 1u);
+                    B[r][pos] = v[j];
+                }
+            }
+            __syncthreads();
+        }
+        if (maxrun > BP_RUNMAX) ovf = true;
+    }
+
+    if (ovf) {
+        if (threadIdx.x == 0) {
+            uint32_t k = atomicAdd(A.novf, 1u);
+            if (k < A.ovf_cap) {
+                OvfEntry e;
+                e.bucket = b;
+                e.d2 = d2;
+                e.nr[0] = nsub[0];
+                e.nr[1] = nsub[1];
+                e.off[0] = offsub[0];
+                e.off[1] = offsub[1];
+                A.ovf[k] = e;
+            }
+        }
+        return;
+    }
+
+    // ---- phase 3: fix equal-digit runs, write out
+    for (int r = 0; r < nrel; r++) {
+        const uint32_t n = nsub[r];
+        for (uint32_t d = threadIdx.x; d < nb3; d += BP_THREADS) {
+            uint32_t s = h[r][d];
+            uint32_t e = (d + 1 < nb3) ? h[r][d + 1] : n;
+            if (e - s > 1) lds_insertion_sort(B[r] + s, e - s);
+        }
+        __syncthreads();
+        Tup* dst = A.out[r] + A.bstart[r][b] + offsub[r];
+        for (uint32_t i = threadIdx.x; i < n; i += BP_THREADS) dst[i] = B[r][i];
+    }
+
+    // ---- phase 4: merge-join count of the two resident sub-buckets
+    if (nrel == 2) {
+        unsigned long long cnt = 0;
+        const uint32_t nR = nsub[0], nS = nsub[1];
+        if (P.s3 == 0 && misc[28] == 0) {
+            // level-3 digit is the exact key: count = sum_k |R_k| * |S_k|
+            for (uint32_t d = threadIdx.x; d < nb3; d += BP_THREADS) {
+                uint32_t cr = ((d + 1 < nb3) ? h[0][d + 1] : nR) - h[0][d];
+                uint32_t cs = ((d + 1 < nb3) ? h[1][d + 1] : nS) - h[1][d];
+                cnt += (unsigned long long)cr * cs;
+            }
+        } else {
+            // generic: for each S run of one key, |R_k| by binary search
+            for (uint32_t i = threadIdx.x; i < nS; i += BP_THREADS) {
+                int64_t k = tup_key(B[1][i]);
+                if (i > 0 && tup_key(B[1][i - 1]) == k) continue;
+                uint32_t e = i + 1;
+                while (e < nS && tup_key(B[1][e]) == k) e++;
+                uint32_t lo = 0, hi = nR;
+                while (lo < hi) {
+                    uint32_t m = (lo + hi) >> 1;
+                    if (tup_key(B[0][m]) < k) lo = m + 1; else hi = m;
+                }
+                uint32_t lb = lo;
+                hi = nR;
+                while (lo < hi) {
+                    uint32_t m = (lo + hi) >> 1;
+                    if (tup_key(B[0][m]) <= k) lo = m + 1; else hi = m;
+                }
+                cnt += (unsigned long long)(lo - lb) * (e - i);
+            }
+        }
+        cnt = wave_sum(cnt);
+        if (lane_id() == 0 && cnt) atomicAdd(A.count_dev, cnt);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// overflow: copy the pieces of a sub-bucket, unsorted, into its output slot
+__global__ void __launch_bounds__(256)
+k_gather_sub(const Tup* __restrict__ tmp, Tup* __restrict__ out,
+             const uint64_t* __restrict__ bstart, TileTable tt,
+             const OvfEntry* __restrict__ ovf, int r, uint32_t nb2) {
+    const OvfEntry e = ovf[blockIdx.x];
+    const uint32_t b = e.bucket, d2 = e.d2;
+    Tup* dst = out + bstart[b] + e.off[r];
+    uint32_t pos = 0;
+    for (uint32_t t = tt.btile0[b]; t < tt.btile0[b + 1]; t++) {
+        const uint16_t* pf = tt.pref + (uint64_t)t * nb2;
+        uint32_t lo = pf[d2];
+        uint32_t hi = (d2 + 1 < nb2) ? pf[d2 + 1] : tt.len[t];
+        const Tup* src = tmp + tt.off[t] + lo;
+        for (uint32_t i = threadIdx.x; i < hi - lo; i += 256) dst[pos + i] = src[i];
+        pos += hi - lo;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// range plan from a strided sample of the relations (or from hints)
+__global__ void __launch_bounds__(256)
+k_plan(const Tup* r0, uint64_t n0, const Tup* r1, uint64_t n1, uint32_t D1,
+       uint32_t D2, int64_t hmin, int64_t hmax, RangePlan* plan) {
+    __shared__ int64_t smin[4], smax[4];
+    int64_t mn = INT64_MAX, mx = INT64_MIN;
+    const int S = 4096;
+    for (int rel = 0; rel < 2; rel++) {
+        const Tup* p = rel ? r1 : r0;
+        uint64_t n = rel ? n1 : n0;
+        if (!p || n == 0) continue;
+        for (int i = threadIdx.x; i < S; i += 256) {
+            // golden-ratio stride sample, deterministic
+            uint64_t idx = __umul64hi((uint64_t)i * 0x9E3779B97F4A7C15ull, n);
+            if (i == 0) idx = 0;
+            if (i == 1) idx = n - 1;
+            int64_t k = tup_key(p[idx]);
+            mn = k < mn ? k : mn;
+            mx = k > mx ? k : mx;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        int64_t a = __shfl_xor(mn, o, 64), c = __shfl_xor(mx, o, 64);
+        mn = a < mn ? a : mn;
+        mx = c > mx ? c : mx;
+    }
+    if (lane_id() == 0) {
+        smin[threadIdx.x >> 6] = mn;
+        smax[threadIdx.x >> 6] = mx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 4; w++) {
+            mn = smin[w] < mn ? smin[w] : mn;
+            mx = smax[w] > mx ? smax[w] : mx;
+        }
+        mn = smin[0] < mn ? smin[0] : mn;
+        mx = smax[0] > mx ? smax[0] : mx;
+        int64_t lo, hi;
+        if (hmin <= hmax) {
+            lo = hmin;
+            hi = hmax;
+        } else if (mn > mx) {
+            lo = 0;
+            hi = 0;
+        } else {
+            // widen the sampled range by 1/64 on both sides (saturating)
+            uint64_t w = key_u(mx) - key_u(mn);
+            uint64_t m = w / 64 + 1;
+            uint64_t lu = key_u(mn) > m ? key_u(mn) - m : 0;
+            uint64_t hu = (~0ull - key_u(mx)) > m ? key_u(mx) + m : ~0ull;
+            lo = (int64_t)(lu ^ 0x8000000000000000ull);
+            hi = (int64_t)(hu ^ 0x8000000000000000ull);
+        }
+        *plan = make_plan(lo, hi, D1, D2, BP_D3MAX);
+    }
+}
+
+void plan_from_sample(Workspace* ws, const Tup* const* rels, const uint64_t* ns,
+                      int nrel, uint32_t D1, uint32_t D2, int64_t hint_min,
+                      int64_t hint_max, RangePlan* plan_dev, hipStream_t st) {
+    (void)ws;
+    hipLaunchKernelGGL(k_plan, dim3(1), dim3(256), 0, st, rels[0], ns[0],
+                       nrel > 1 ? rels[1] : (const Tup*)nullptr,
+                       nrel > 1 ? ns[1] : 0, D1, D2, hint_min, hint_max,
+                       plan_dev);
+    SMJ_CHECK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+void bucket_sort(Workspace* ws, const BucketSortArgs& a, uint32_t D2,
+                 hipStream_t st) {
+    const uint32_t nb = a.nbuckets;
+    const uint32_t nb2 = 1u << D2;
+    TileTable tt[2];
+    static const char* names[2][6] = {
+        {"bs_off0", "bs_len0", "bs_bkt0", "bs_bt00", "bs_pref0", "bs_nt0"},
+        {"bs_off1", "bs_len1", "bs_bkt1", "bs_bt01", "bs_pref1", "bs_nt1"}};
+    uint64_t maxt[2] = {0, 0};
+    for (int r = 0; r < a.nrel; r++) {
+        maxt[r] = (a.n[r] + TILE2 - 1) / TILE2 + nb + 1;
+        tt[r].off = (uint64_t*)ws->scratch(names[r][0], maxt[r] * 8);
+        tt[r].len = (uint32_t*)ws->scratch(names[r][1], maxt[r] * 4);
+        tt[r].bucket = (uint32_t*)ws->scratch(names[r][2], maxt[r] * 4);
+        tt[r].btile0 = (uint32_t*)ws->scratch(names[r][3], (nb + 1) * 4);
+        tt[r].pref = (uint16_t*)ws->scratch(names[r][4], maxt[r] * nb2 * 2);
+        tt[r].ntiles = (uint32_t*)ws->scratch(names[r][5], 4);
+        hipLaunchKernelGGL(k_tiles, dim3(1), dim3(256), 0, st, a.bstart[r],
+                           a.bcount[r], nb, tt[r]);
+    }
+    if (a.ev_tile) SMJ_CHECK(hipEventRecord(a.ev_tile, st));
+    static bool attr = false;
+    if (!attr) {
+        SMJ_CHECK(hipFuncSetAttribute((const void*)k_tilepass,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      160 * 1024));
+        SMJ_CHECK(hipFuncSetAttribute((const void*)k_bucketpass,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      160 * 1024));
+        attr = true;
+    }
+    const size_t tp_lds = TILE2 * sizeof(Tup) + nb2 * 4 + 64;
+    for (int r = 0; r < a.nrel; r++) {
+        TraceScope ts(ws, "k_tilepass", st);
+        hipLaunchKernelGGL(k_tilepass, dim3((uint32_t)maxt[r]), dim3(TP_THREADS),
+                           tp_lds, st, a.part[r], a.tmp[r], tt[r], a.plan_dev, nb2);
+    }
+    if (a.ev_bucket) SMJ_CHECK(hipEventRecord(a.ev_bucket, st));
+
+    const uint32_t nsub = nb * nb2;
+    const uint32_t ovf_cap = nsub;
+    OvfEntry* ovf = (OvfEntry*)ws->scratch("bs_ovf", (size_t)ovf_cap * sizeof(OvfEntry));
+    uint32_t* novf = (uint32_t*)ws->scratch("bs_novf", 4);
+    SMJ_CHECK(hipMemsetAsync(novf, 0, 4, st));
+    BucketPassArgs B;
+    for (int r = 0; r < 2; r++) {
+        int rr = r < a.nrel ? r : 0;
+        B.tmp[r] = a.tmp[rr];
+        B.out[r] = a.out[rr];
+        B.bstart[r] = a.bstart[rr];
+        B.tt[r] = tt[rr];
+    }
+    B.nrel = a.nrel;
+    B.plan_dev = a.plan_dev;
+    B.count_dev = a.count_dev;
+    B.nb2 = nb2;
+    B.ovf = ovf;
+    B.novf = novf;
+    B.ovf_cap = ovf_cap;
+    {
+        TraceScope ts(ws, "k_bucketpass", st);
+        hipLaunchKernelGGL(k_bucketpass, dim3(nsub), dim3(BP_THREADS), BP_LDS, st, B);
+    }
+    SMJ_CHECK(hipGetLastError());
+    if (a.ev_ovf) SMJ_CHECK(hipEventRecord(a.ev_ovf, st));
+
+    // ---- overflow path (synchronises once)
+    uint32_t* h_novf = (uint32_t*)ws->host_pinned("bs_h_novf", 4);
+    SMJ_CHECK(hipMemcpyAsync(h_novf, novf, 4, hipMemcpyDeviceToHost, st));
+    SMJ_CHECK(hipStreamSynchronize(st));
+    const uint32_t no = *h_novf;
+    if (no == 0) return;
+    if (no > ovf_cap) {
+        fprintf(stderr, "[ERROR] smj: overflow table too small\n");
+        abort();
+    }
+    std::vector<OvfEntry> he(no);
+    SMJ_CHECK(hipMemcpyAsync(he.data(), ovf, no * sizeof(OvfEntry),
+                             hipMemcpyDeviceToHost, st));
+    std::vector<uint64_t> hbstart[2];
+    for (int r = 0; r < a.nrel; r++) {
+        hbstart[r].resize(nb);
+        SMJ_CHECK(hipMemcpyAsync(hbstart[r].data(), a.bstart[r], nb * 8,
+                                 hipMemcpyDeviceToHost, st));
+    }
+    SMJ_CHECK(hipStreamSynchronize(st));
+    for (int r = 0; r < a.nrel; r++) {
+        hipLaunchKernelGGL(k_gather_sub, dim3(no), dim3(256), 0, st, a.tmp[r],
+                           a.out[r], a.bstart[r], tt[r], ovf, r, nb2);
+        std::vector<uint64_t> so(no), sl(no);
+        for (uint32_t i = 0; i < no; i++) {
+            so[i] = hbstart[r][he[i].bucket] + he[i].off[r];
+            sl[i] = he[i].nr[r];
+        }
+        segmented_sort(ws, a.out[r], so.data(), sl.data(), no, st);
+    }
+    if (a.nrel == 2) {
+        for (uint32_t i = 0; i < no; i++) {
+            const Tup* rp = a.out[0] + hbstart[0][he[i].bucket] + he[i].off[0];
+            const Tup* sp = a.out[1] + hbstart[1][he[i].bucket] + he[i].off[1];
+            if (he[i].nr[0] && he[i].nr[1])
+                merge_join_count(rp, he[i].nr[0], sp, he[i].nr[1], a.count_dev, st);
+        }
+    }
+    SMJ_CHECK(hipGetLastError());
+}
+
+}  // namespace smj

@@ -1,0 +1,821 @@
+// capi.hip -- the C ABI of libsmj_hip[_k8].so (declared in include/smj.h).
+//
+// Reference-named entry points keep the reference's signatures, pointer-swap
+// conventions and output layout; host pointers are staged through HBM, device
+// pointers are used in place.  Nothing in here computes on the CPU: every
+// sort, partition, merge and join runs in the HIP kernels of this library, and
+// a missing/failed device aborts (fail-fast like the reference).
+#include <math.h>
+#include <string.h>
+#include <sys/time.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../../include/smj.h"
+#include "smj_common.hpp"
+#include "smj_internal.hpp"
+
+namespace smj {
+void gen_pk_nopayload(Tup* out, uint64_t n, uint64_t first, uint64_t total,
+                      uint64_t seed, hipStream_t st);
+}
+
+using namespace smj;
+
+static_assert(sizeof(tuple_t) == sizeof(Tup), "tuple_t / device tuple mismatch");
+
+// ---------------------------------------------------------------------------
+// per-thread device context (the reference's L1 functions are called
+// concurrently from T pthreads on disjoint data, SURVEY.md §8(b) Threading)
+// ---------------------------------------------------------------------------
+struct Ctx {
+    hipStream_t st = nullptr;
+    Workspace ws;
+    int device = -1;
+};
+
+static Ctx& ctx() {
+    thread_local Ctx* c = nullptr;
+    if (!c) {
+        int ndev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+            fprintf(stderr,
+                    "[ERROR] smj: no HIP device visible; the MI355X library has "
+                    "no CPU fallback.\n");
+            abort();
+        }
+        c = new Ctx();
+        SMJ_CHECK(hipGetDevice(&c->device));
+        SMJ_CHECK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+    }
+    return *c;
+}
+
+__global__ void k_setplan(RangePlan* p, RangePlan v) { *p = v; }
+
+static bool is_device_ptr(const void* p) {
+    if (!p) return false;
+    hipPointerAttribute_t a;
+    hipError_t e = hipPointerGetAttributes(&a, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();  // clear
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+}
+
+// Device view of a caller buffer: either the pointer itself or a staged copy.
+struct DevBuf {
+    Tup* d = nullptr;
+    void* host = nullptr;
+    bool staged = false;
+};
+
+static DevBuf dev_in(const void* p, uint64_t ntup, const char* slot,
+                     bool copy_in) {
+    DevBuf b;
+    if (is_device_ptr(p)) {
+        b.d = (Tup*)p;
+        return b;
+    }
+    Ctx& c = ctx();
+    b.d = (Tup*)c.ws.scratch(slot, (ntup ? ntup : 1) * sizeof(Tup));
+    b.host = (void*)p;
+    b.staged = true;
+    if (copy_in && ntup)
+        SMJ_CHECK(hipMemcpyAsync(b.d, p, ntup * sizeof(Tup),
+                                 hipMemcpyHostToDevice, c.st));
+    return b;
+}
+
+static void dev_out(const DevBuf& b, uint64_t ntup) {
+    if (!b.staged || ntup == 0) return;
+    SMJ_CHECK(hipMemcpyAsync(b.host, b.d, ntup * sizeof(Tup),
+                             hipMemcpyDeviceToHost, ctx().st));
+}
+
+static void sync() { SMJ_CHECK(hipStreamSynchronize(ctx().st)); }
+
+// ---------------------------------------------------------------------------
+// device pipelines
+// ---------------------------------------------------------------------------
+static uint32_t ceil_log2(uint64_t x) {
+    uint32_t b = 0;
+    while (b < 63 && (1ull << b) < x) b++;
+    return b;
+}
+
+// level widths: D1 (partition fan-out) and D2 (tile-pass fan-out) so that the
+// expected sub-bucket is a few hundred tuples (fits the in-LDS bucket pass)
+static void choose_levels(uint64_t n, uint32_t want_d1, uint32_t* D1,
+                          uint32_t* D2) {
+    const uint64_t target = (sizeof(Tup) == 16) ? 320 : 640;
+    uint32_t B = n > target ? ceil_log2((n + target - 1) / target) : 0;
+    uint32_t d1 = want_d1 ? want_d1 : 10;
+    if (d1 > B) d1 = B;
+    if (d1 > kNarrowDigitBits) d1 = kNarrowDigitBits;
+    uint32_t d2 = B > d1 ? B - d1 : 0;
+    if (d2 > 9) d2 = 9;
+    *D1 = d1;
+    *D2 = d2;
+}
+
+static void device_sort(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
+                        hipStream_t st) {
+    if (n == 0) return;
+    uint32_t D1, D2;
+    choose_levels(n, 0, &D1, &D2);
+    RangePlan* plan = (RangePlan*)ws->scratch("plan", sizeof(RangePlan));
+    const Tup* rels[1] = {in};
+    uint64_t ns[1] = {n};
+    plan_from_sample(ws, rels, ns, 1, D1, D2, 1, 0, plan, st);
+    const uint32_t nb = 1u << D1;
+    Tup* part = (Tup*)ws->scratch("sort_part", n * sizeof(Tup));
+    uint64_t* starts = (uint64_t*)ws->scratch("sort_starts", nb * 8);
+    int64_t* hist = (int64_t*)ws->scratch("sort_hist", nb * 8);
+    plan_partition(ws, in, n, part, plan, D1, starts, hist, st);
+    BucketSortArgs a;
+    a.part[0] = part;
+    a.bstart[0] = starts;
+    a.bcount[0] = hist;
+    a.tmp[0] = part;
+    a.out[0] = out;
+    a.n[0] = n;
+    a.part[1] = nullptr;
+    a.bstart[1] = nullptr;
+    a.bcount[1] = nullptr;
+    a.tmp[1] = nullptr;
+    a.out[1] = nullptr;
+    a.n[1] = 0;
+    a.nrel = 1;
+    a.nbuckets = nb;
+    a.plan_dev = plan;
+    a.count_dev = nullptr;
+    bucket_sort(ws, a, D2, st);
+}
+
+static void device_join(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
+                        uint64_t nS, Tup* sortedR, Tup* sortedS,
+                        uint32_t fanout_bits, int64_t hint_min,
+                        int64_t hint_max, unsigned long long* count_dev,
+                        hipStream_t st) {
+    ws->events();
+    SMJ_CHECK(hipEventRecord(ws->ev[0], st));
+    SMJ_CHECK(hipMemsetAsync(count_dev, 0, sizeof(unsigned long long), st));
+    uint32_t D1, D2;
+    choose_levels(nR > nS ? nR : nS, fanout_bits, &D1, &D2);
+    RangePlan* plan = (RangePlan*)ws->scratch("plan", sizeof(RangePlan));
+    const Tup* rels[2] = {R, S};
+    uint64_t ns[2] = {nR, nS};
+    plan_from_sample(ws, rels, ns, 2, D1, D2, hint_min, hint_max, plan, st);
+    const uint32_t nb = 1u << D1;
+    Tup* partR = (Tup*)ws->scratch("join_partR", (nR ? nR : 1) * sizeof(Tup));
+    Tup* partS = (Tup*)ws->scratch("join_partS", (nS ? nS : 1) * sizeof(Tup));
+    uint64_t* stR = (uint64_t*)ws->scratch("join_stR", nb * 8);
+    uint64_t* stS = (uint64_t*)ws->scratch("join_stS", nb * 8);
+    int64_t* hR = (int64_t*)ws->scratch("join_hR", nb * 8);
+    int64_t* hS = (int64_t*)ws->scratch("join_hS", nb * 8);
+    plan_partition(ws, R, nR, partR, plan, D1, stR, hR, st);
+    plan_partition(ws, S, nS, partS, plan, D1, stS, hS, st);
+    SMJ_CHECK(hipEventRecord(ws->ev[1], st));
+    BucketSortArgs a;
+    a.part[0] = partR;
+    a.part[1] = partS;
+    a.bstart[0] = stR;
+    a.bstart[1] = stS;
+    a.bcount[0] = hR;
+    a.bcount[1] = hS;
+    a.tmp[0] = partR;
+    a.tmp[1] = partS;
+    a.out[0] = sortedR;
+    a.out[1] = sortedS;
+    a.n[0] = nR;
+    a.n[1] = nS;
+    a.nrel = 2;
+    a.nbuckets = nb;
+    a.plan_dev = plan;
+    a.count_dev = count_dev;
+    a.ev_tile = nullptr;
+    a.ev_bucket = ws->ev[2];
+    a.ev_ovf = ws->ev[3];
+    bucket_sort(ws, a, D2, st);
+    SMJ_CHECK(hipEventRecord(ws->ev[4], st));
+}
+
+// ---------------------------------------------------------------------------
+// partitioning (reference src/partition/partition.c:301-436)
+// ---------------------------------------------------------------------------
+static void partition_common(relation_t** parts, relation_t* input,
+                             relation_t* output, uint32_t nbits,
+                             uint32_t shiftbits, int padded) {
+    Ctx& c = ctx();
+    const uint64_t n = input->num_tuples;
+    const uint32_t fan = 1u << nbits;
+    const uint32_t mask = (uint32_t)(((1ull << nbits) - 1) << shiftbits);
+    DevBuf in = dev_in(input->tuples, n, "api_in", true);
+    // output extent: n plus at most one cache line of padding per partition
+    const uint64_t cap = n + (padded ? (uint64_t)fan * TUPLESPERCACHELINE : 0);
+    DevBuf out = dev_in(output->tuples, cap, "api_out", false);
+    int64_t* hist = (int64_t*)c.ws.scratch("api_hist", fan * 8);
+    int64_t* off = (int64_t*)c.ws.scratch("api_off", fan * 8);
+    Digit32 dig{mask, shiftbits};
+    stable_partition(&c.ws, in.d, n, out.d, dig, nbits, padded, hist, off, c.st);
+    std::vector<int64_t> hh(fan), ho(fan);
+    SMJ_CHECK(hipMemcpyAsync(hh.data(), hist, fan * 8, hipMemcpyDeviceToHost, c.st));
+    SMJ_CHECK(hipMemcpyAsync(ho.data(), off, fan * 8, hipMemcpyDeviceToHost, c.st));
+    sync();
+    const uint64_t extent = fan ? (uint64_t)(ho[fan - 1] + hh[fan - 1]) : 0;
+    dev_out(out, extent);
+    sync();
+    for (uint32_t i = 0; i < fan; i++) {
+        parts[i]->tuples = output->tuples + ho[i];
+        parts[i]->num_tuples = (uint64_t)hh[i];
+    }
+}
+
+extern "C" {
+
+void partition_relation(relation_t** partitions, relation_t* input,
+                        relation_t* output, int radixbits, int shiftbits) {
+    partition_common(partitions, input, output, (uint32_t)radixbits,
+                     (uint32_t)shiftbits, 0);
+}
+
+void partition_relation_optimized(relation_t** partitions, relation_t* input,
+                                  relation_t* output, uint32_t nbits,
+                                  uint32_t shiftbits) {
+    partition_common(partitions, input, output, nbits, shiftbits, 1);
+}
+
+void partition_relation_optimized_V2(relation_t** partitions,
+                                     relation_t* input, relation_t* output,
+                                     uint32_t nbits, uint32_t shiftbits) {
+    partition_common(partitions, input, output, nbits, shiftbits, 1);
+}
+
+void histogram_memcpy_bench(relation_t** partitions, relation_t* input,
+                            relation_t* output, uint32_t nbits) {
+    (void)partitions;
+    Ctx& c = ctx();
+    const uint64_t n = input->num_tuples;
+    DevBuf in = dev_in(input->tuples, n, "api_in", true);
+    DevBuf out = dev_in(output->tuples, n, "api_out", false);
+    hist_memcpy(&c.ws, in.d, n, out.d, nbits, c.st);
+    dev_out(out, n);
+    sync();
+}
+
+// ---------------------------------------------------------------------------
+// sorting (reference src/avxsort/avxsort.c:212-250, avxsort_multiway.c,
+// src/scalarsort/scalarsort.c)
+// ---------------------------------------------------------------------------
+static void sort_tuples_into(const void* inp, void* outp, uint64_t n) {
+    Ctx& c = ctx();
+    DevBuf in = dev_in(inp, n, "api_in", true);
+    DevBuf out = dev_in(outp, n, "api_out", false);
+    device_sort(&c.ws, in.d, n, out.d, c.st);
+    dev_out(out, n);
+    sync();
+}
+
+void avxsort_tuples(tuple_t** inputptr, tuple_t** outputptr, uint64_t nitems) {
+    if (nitems == 0) return;
+    sort_tuples_into(*inputptr, *outputptr, nitems);
+    // sorted items are in *outputptr; *inputptr stays the other buffer
+}
+
+void avxsortmultiway_tuples(tuple_t** inputptr, tuple_t** outputptr,
+                            uint64_t nitems) {
+    if (nitems == 0) return;
+    sort_tuples_into(*inputptr, *outputptr, nitems);
+}
+
+void scalarsort_tuples(tuple_t** inputptr, tuple_t** outputptr,
+                       uint64_t nitems) {
+    // reference sorts in place, then swaps (scalarsort.c:41-50)
+    tuple_t* in = *inputptr;
+    tuple_t* out = *outputptr;
+    if (nitems) sort_tuples_into(in, in, nitems);
+    *inputptr = out;
+    *outputptr = in;
+}
+}  // extern "C"
+
+// ---- int64 / int32 item sorts: items viewed as tuples with key = value
+__global__ void k_expand_i64(const int64_t* __restrict__ a, Tup* __restrict__ t,
+                             uint64_t n) {
+    const uint64_t s = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += s) {
+#ifdef KEY_8B
+        Tup x;
+        x.key = a[i];
+        x.payload = 0;
+        t[i] = x;
+#else
+        t[i] = (uint64_t)a[i];
+#endif
+    }
+}
+__global__ void k_compact_i64(const Tup* __restrict__ t, int64_t* __restrict__ a,
+                              uint64_t n) {
+    const uint64_t s = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += s) {
+#ifdef KEY_8B
+        a[i] = t[i].key;
+#else
+        a[i] = (int64_t)t[i];
+#endif
+    }
+}
+__global__ void k_expand_i32(const int32_t* __restrict__ a, Tup* __restrict__ t,
+                             uint64_t n) {
+    const uint64_t s = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += s) {
+#ifdef KEY_8B
+        Tup x;
+        x.key = a[i];
+        x.payload = 0;
+        t[i] = x;
+#else
+        t[i] = (uint64_t)(uint32_t)a[i] << 32;
+#endif
+    }
+}
+__global__ void k_compact_i32(const Tup* __restrict__ t, int32_t* __restrict__ a,
+                              uint64_t n) {
+    const uint64_t s = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += s)
+        a[i] = (int32_t)tup_key(t[i]);
+}
+
+static uint32_t grid_n(uint64_t n) {
+    uint64_t b = (n + 255) / 256;
+    return (uint32_t)(b < 4096 ? (b ? b : 1) : 4096);
+}
+
+static void sort_int64_into(const int64_t* inp, int64_t* outp, uint64_t n) {
+    if (n == 0) return;
+#ifndef KEY_8B
+    sort_tuples_into(inp, outp, n);  // an 8-byte tuple is an int64 word
+#else
+    Ctx& c = ctx();
+    const bool din = is_device_ptr(inp), dout = is_device_ptr(outp);
+    int64_t* di = (int64_t*)inp;
+    int64_t* dout_p = outp;
+    if (!din) {
+        di = (int64_t*)c.ws.scratch("api_i64_in", n * 8);
+        SMJ_CHECK(hipMemcpyAsync(di, inp, n * 8, hipMemcpyHostToDevice, c.st));
+    }
+    if (!dout) dout_p = (int64_t*)c.ws.scratch("api_i64_out", n * 8);
+    Tup* t = (Tup*)c.ws.scratch("api_i64_t", n * sizeof(Tup));
+    Tup* u = (Tup*)c.ws.scratch("api_i64_u", n * sizeof(Tup));
+    hipLaunchKernelGGL(k_expand_i64, dim3(grid_n(n)), dim3(256), 0, c.st, di, t, n);
+    device_sort(&c.ws, t, n, u, c.st);
+    hipLaunchKernelGGL(k_compact_i64, dim3(grid_n(n)), dim3(256), 0, c.st, u, dout_p, n);
+    if (!dout)
+        SMJ_CHECK(hipMemcpyAsync(outp, dout_p, n * 8, hipMemcpyDeviceToHost, c.st));
+    sync();
+#endif
+}
+
+static void sort_int32_into(const int32_t* inp, int32_t* outp, uint64_t n) {
+    if (n == 0) return;
+    Ctx& c = ctx();
+    const bool din = is_device_ptr(inp), dout = is_device_ptr(outp);
+    int32_t* di = (int32_t*)inp;
+    int32_t* dout_p = outp;
+    if (!din) {
+        di = (int32_t*)c.ws.scratch("api_i32_in", n * 4);
+        SMJ_CHECK(hipMemcpyAsync(di, inp, n * 4, hipMemcpyHostToDevice, c.st));
+    }
+    if (!dout) dout_p = (int32_t*)c.ws.scratch("api_i32_out", n * 4);
+    Tup* t = (Tup*)c.ws.scratch("api_i32_t", n * sizeof(Tup));
+    Tup* u = (Tup*)c.ws.scratch("api_i32_u", n * sizeof(Tup));
+    hipLaunchKernelGGL(k_expand_i32, dim3(grid_n(n)), dim3(256), 0, c.st, di, t, n);
+    device_sort(&c.ws, t, n, u, c.st);
+    hipLaunchKernelGGL(k_compact_i32, dim3(grid_n(n)), dim3(256), 0, c.st, u, dout_p, n);
+    if (!dout)
+        SMJ_CHECK(hipMemcpyAsync(outp, dout_p, n * 4, hipMemcpyDeviceToHost, c.st));
+    sync();
+}
+
+extern "C" {
+
+void avxsort_int64(int64_t** inputptr, int64_t** outputptr, uint64_t nitems) {
+    sort_int64_into(*inputptr, *outputptr, nitems);
+}
+void avxsortmultiway_int64(int64_t** inputptr, int64_t** outputptr,
+                           uint64_t nitems) {
+    sort_int64_into(*inputptr, *outputptr, nitems);
+}
+void avxsort_int32(int32_t** inputptr, int32_t** outputptr, uint64_t nitems) {
+    sort_int32_into(*inputptr, *outputptr, nitems);
+}
+void scalarsort_int64(int64_t** inputptr, int64_t** outputptr, uint64_t nitems) {
+    int64_t* in = *inputptr;
+    int64_t* out = *outputptr;
+    sort_int64_into(in, in, nitems);
+    *inputptr = out;
+    *outputptr = in;
+}
+void scalarsort_int32(int32_t** inputptr, int32_t** outputptr, uint64_t nitems) {
+    int32_t* in = *inputptr;
+    int32_t* out = *outputptr;
+    sort_int32_into(in, in, nitems);
+    *inputptr = out;
+    *outputptr = in;
+}
+
+// ---------------------------------------------------------------------------
+// merging (reference src/merge/merge.c:27-235, avx_multiwaymerge.c:199-338,
+// scalar_multiwaymerge.c)
+// ---------------------------------------------------------------------------
+static uint64_t merge_tuples_common(const void* A, const void* B, void* O,
+                                   uint64_t la, uint64_t lb) {
+    Ctx& c = ctx();
+    DevBuf a = dev_in(A, la, "api_ma", true);
+    DevBuf b = dev_in(B, lb, "api_mb", true);
+    DevBuf o = dev_in(O, la + lb, "api_mo", false);
+    merge2(a.d, la, b.d, lb, o.d, c.st);
+    dev_out(o, la + lb);
+    sync();
+    return la + lb;
+}
+
+uint64_t avx_merge_tuples(tuple_t* const inA, tuple_t* const inB,
+                          tuple_t* const outp, const uint64_t lenA,
+                          const uint64_t lenB) {
+    return merge_tuples_common(inA, inB, outp, lenA, lenB);
+}
+uint64_t scalar_merge_tuples(tuple_t* const inA, tuple_t* const inB,
+                             tuple_t* const outp, const uint64_t lenA,
+                             const uint64_t lenB) {
+    return merge_tuples_common(inA, inB, outp, lenA, lenB);
+}
+
+static uint64_t merge_int64_common(const int64_t* A, const int64_t* B, int64_t* O,
+                                   uint64_t la, uint64_t lb) {
+#ifndef KEY_8B
+    return merge_tuples_common(A, B, O, la, lb);
+#else
+    // 16-byte build: widen, merge, narrow
+    Ctx& c = ctx();
+    const uint64_t n = la + lb;
+    if (n == 0) return 0;
+    int64_t* da = (int64_t*)c.ws.scratch("api_mi_a", (la ? la : 1) * 8);
+    int64_t* db = (int64_t*)c.ws.scratch("api_mi_b", (lb ? lb : 1) * 8);
+    int64_t* dn = (int64_t*)c.ws.scratch("api_mi_o", n * 8);
+    if (la) SMJ_CHECK(hipMemcpyAsync(da, A, la * 8, hipMemcpyDefault, c.st));
+    if (lb) SMJ_CHECK(hipMemcpyAsync(db, B, lb * 8, hipMemcpyDefault, c.st));
+    Tup* ta = (Tup*)c.ws.scratch("api_mi_ta", (la ? la : 1) * sizeof(Tup));
+    Tup* tb = (Tup*)c.ws.scratch("api_mi_tb", (lb ? lb : 1) * sizeof(Tup));
+    Tup* to = (Tup*)c.ws.scratch("api_mi_to", n * sizeof(Tup));
+    if (la) hipLaunchKernelGGL(k_expand_i64, dim3(grid_n(la)), dim3(256), 0, c.st, da, ta, la);
+    if (lb) hipLaunchKernelGGL(k_expand_i64, dim3(grid_n(lb)), dim3(256), 0, c.st, db, tb, lb);
+    merge2(ta, la, tb, lb, to, c.st);
+    hipLaunchKernelGGL(k_compact_i64, dim3(grid_n(n)), dim3(256), 0, c.st, to, dn, n);
+    SMJ_CHECK(hipMemcpyAsync(O, dn, n * 8, hipMemcpyDefault, c.st));
+    sync();
+    return n;
+#endif
+}
+
+uint64_t avx_merge_int64(int64_t* const inA, int64_t* const inB,
+                         int64_t* const outp, const uint64_t lenA,
+                         const uint64_t lenB) {
+    return merge_int64_common(inA, inB, outp, lenA, lenB);
+}
+uint64_t scalar_merge_int64(int64_t* const inA, int64_t* const inB,
+                            int64_t* const outp, const uint64_t lenA,
+                            const uint64_t lenB) {
+    return merge_int64_common(inA, inB, outp, lenA, lenB);
+}
+
+static uint64_t multiway_common(tuple_t* output, relation_t** parts,
+                                uint32_t nparts) {
+    Ctx& c = ctx();
+    std::vector<const Tup*> runs(nparts);
+    std::vector<uint64_t> lens(nparts);
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < nparts; i++) total += parts[i]->num_tuples;
+    // stage host runs into one packed device buffer
+    bool all_dev = is_device_ptr(output);
+    for (uint32_t i = 0; i < nparts && all_dev; i++)
+        if (parts[i]->num_tuples && !is_device_ptr(parts[i]->tuples)) all_dev = false;
+    Tup* packed = nullptr;
+    if (!all_dev) packed = (Tup*)c.ws.scratch("api_mw_in", (total ? total : 1) * sizeof(Tup));
+    uint64_t o = 0;
+    for (uint32_t i = 0; i < nparts; i++) {
+        lens[i] = parts[i]->num_tuples;
+        if (all_dev) {
+            runs[i] = (const Tup*)parts[i]->tuples;
+        } else {
+            runs[i] = packed + o;
+            if (lens[i])
+                SMJ_CHECK(hipMemcpyAsync(packed + o, parts[i]->tuples,
+                                         lens[i] * sizeof(Tup), hipMemcpyDefault,
+                                         c.st));
+            o += lens[i];
+        }
+    }
+    Tup* out = all_dev ? (Tup*)output
+                       : (Tup*)c.ws.scratch("api_mw_out", (total ? total : 1) * sizeof(Tup));
+    multiway_merge(&c.ws, runs.data(), lens.data(), nparts, out, c.st);
+    if (!all_dev && total)
+        SMJ_CHECK(hipMemcpyAsync(output, out, total * sizeof(Tup),
+                                 hipMemcpyDeviceToHost, c.st));
+    sync();
+    // the reference consumes its inputs (avx_multiwaymerge.c:268-272)
+    for (uint32_t i = 0; i < nparts; i++) {
+        parts[i]->tuples += parts[i]->num_tuples;
+        parts[i]->num_tuples = 0;
+    }
+    return total;
+}
+
+uint64_t avx_multiway_merge(tuple_t* output, relation_t** parts,
+                            uint32_t nparts, tuple_t* fifobuffer,
+                            uint32_t bufntuples) {
+    (void)fifobuffer;
+    (void)bufntuples;
+    return multiway_common(output, parts, nparts);
+}
+uint64_t scalar_multiway_merge(tuple_t* output, relation_t** parts,
+                               uint32_t nparts, tuple_t* fifobuffer,
+                               uint32_t bufntuples) {
+    (void)fifobuffer;
+    (void)bufntuples;
+    return multiway_common(output, parts, nparts);
+}
+uint64_t scalar_multiway_merge_modulo(tuple_t* output, relation_t** parts,
+                                      uint32_t nparts, tuple_t* fifobuffer,
+                                      uint32_t bufntuples) {
+    (void)fifobuffer;
+    (void)bufntuples;
+    return multiway_common(output, parts, nparts);
+}
+uint64_t scalar_multiway_merge_bitand(tuple_t* output, relation_t** parts,
+                                      uint32_t nparts, tuple_t* fifobuffer,
+                                      uint32_t bufntuples) {
+    (void)fifobuffer;
+    (void)bufntuples;
+    return multiway_common(output, parts, nparts);
+}
+
+// ---------------------------------------------------------------------------
+// joins (reference src/joins/joincommon.c:239-312,
+// src/joins/sortmergejoin_multiway.c:50-61)
+// ---------------------------------------------------------------------------
+uint64_t merge_join(tuple_t* rtuples, tuple_t* stuples, const uint64_t numR,
+                    const uint64_t numS, void* output) {
+    if (output) {
+        fprintf(stderr, "[ERROR] smj: join materialisation is not supported "
+                        "(the reference's tuple_buffer.h is absent too)\n");
+        abort();
+    }
+    Ctx& c = ctx();
+    DevBuf r = dev_in(rtuples, numR, "api_jr", true);
+    DevBuf s = dev_in(stuples, numS, "api_js", true);
+    unsigned long long* cnt =
+        (unsigned long long*)c.ws.scratch("api_cnt", sizeof(unsigned long long));
+    SMJ_CHECK(hipMemsetAsync(cnt, 0, 8, c.st));
+    merge_join_count(r.d, numR, s.d, numS, cnt, c.st);
+    unsigned long long h = 0;
+    SMJ_CHECK(hipMemcpyAsync(&h, cnt, 8, hipMemcpyDeviceToHost, c.st));
+    sync();
+    return h;
+}
+
+static result_t* join_api(relation_t* relR, relation_t* relS,
+                          joinconfig_t* joincfg, const char* name) {
+    if ((joincfg->NTHREADS & (joincfg->NTHREADS - 1)) != 0) {
+        fprintf(stdout, "[ERROR] %s sort-merge join runs with a power of 2 "
+                        "#threads.\n", name);
+        return 0;
+    }
+    Ctx& c = ctx();
+    struct timeval t0, t1;
+    gettimeofday(&t0, NULL);
+    const uint64_t nR = relR->num_tuples, nS = relS->num_tuples;
+    DevBuf r = dev_in(relR->tuples, nR, "api_jr", true);
+    DevBuf s = dev_in(relS->tuples, nS, "api_js", true);
+    Tup* sR = (Tup*)c.ws.scratch("api_sortedR", (nR ? nR : 1) * sizeof(Tup));
+    Tup* sS = (Tup*)c.ws.scratch("api_sortedS", (nS ? nS : 1) * sizeof(Tup));
+    unsigned long long* cnt =
+        (unsigned long long*)c.ws.scratch("api_cnt", sizeof(unsigned long long));
+    uint32_t fb = 0;
+    if (joincfg->PARTFANOUT > 0) fb = ceil_log2((uint64_t)joincfg->PARTFANOUT);
+    // the reference fan-out (128 by default) only sizes the level-1 pass here;
+    // at least 10 bits keep the sub-buckets LDS sized
+    if (fb < 10) fb = 10;
+    device_join(&c.ws, r.d, nR, s.d, nS, sR, sS, fb, 1, 0, cnt, c.st);
+    unsigned long long h = 0;
+    SMJ_CHECK(hipMemcpyAsync(&h, cnt, 8, hipMemcpyDeviceToHost, c.st));
+    sync();
+    gettimeofday(&t1, NULL);
+    result_t* res = (result_t*)malloc(sizeof(result_t));
+    res->totalresults = (int64_t)h;
+    res->nthreads = joincfg->NTHREADS;
+    res->resultlist =
+        (threadresult_t*)calloc(joincfg->NTHREADS > 0 ? joincfg->NTHREADS : 1,
+                                sizeof(threadresult_t));
+    res->resultlist[0].nresults = (int64_t)h;
+    if (!getenv("SMJ_QUIET")) {
+        float ms[5];
+        smj_join_phase_ms((smj_workspace*)&c.ws, ms);
+        // same shape as the reference's stats lines (joincommon.c:176-196);
+        // phase values are device nanoseconds instead of TSC cycles
+        fprintf(stdout, "Total, Partitioning, Sort, First-Merge, Merge, Join\n");
+        fprintf(stdout, "%llu, %llu, %llu, %llu, %llu, %llu\n",
+                (unsigned long long)(ms[4] * 1e6), (unsigned long long)(ms[0] * 1e6),
+                (unsigned long long)((ms[0] + ms[1]) * 1e6),
+                (unsigned long long)((ms[0] + ms[1]) * 1e6),
+                (unsigned long long)((ms[0] + ms[1]) * 1e6),
+                (unsigned long long)(ms[4] * 1e6));
+        double us = (t1.tv_sec - t0.tv_sec) * 1e6 + (t1.tv_usec - t0.tv_usec);
+        fprintf(stderr, "NUM-TUPLES = %lld TOTAL-TIME-USECS = %.4lf ",
+                (long long)nS, us);
+        fprintf(stderr, "TUPLES-PER-SECOND = %.4lf ", nS / (us / 1e6));
+        fflush(stdout);
+        fflush(stderr);
+    }
+    return res;
+}
+
+result_t* sortmergejoin_multiway(relation_t* relR, relation_t* relS,
+                                 joinconfig_t* joincfg) {
+    return join_api(relR, relS, joincfg, "m-way");
+}
+
+result_t* sortmergejoin_mpsm(relation_t* relR, relation_t* relS,
+                             joinconfig_t* joincfg) {
+    return join_api(relR, relS, joincfg, "mpsm");
+}
+
+// ---------------------------------------------------------------------------
+// device-resident API
+// ---------------------------------------------------------------------------
+int smj_tuple_bytes(void) { return (int)sizeof(Tup); }
+
+const char* smj_device_name(void) {
+    static char name[256] = {0};
+    if (!name[0]) {
+        Ctx& c = ctx();
+        hipDeviceProp_t p;
+        SMJ_CHECK(hipGetDeviceProperties(&p, c.device));
+        snprintf(name, sizeof(name), "%s (%s)", p.name, p.gcnArchName);
+    }
+    return name;
+}
+
+smj_workspace* smj_workspace_create(void) {
+    ctx();
+    return (smj_workspace*)new Workspace();
+}
+void smj_workspace_destroy(smj_workspace* ws) { delete (Workspace*)ws; }
+
+void smj_dev_partition(smj_workspace* ws, const tuple_t* in, uint64_t n,
+                       tuple_t* out, uint32_t nbits, uint32_t shiftbits,
+                       int padded, int64_t* hist_out, int64_t* off_out,
+                       smj_stream_t stream) {
+    const uint32_t mask = (uint32_t)(((1ull << nbits) - 1) << shiftbits);
+    Digit32 dig{mask, shiftbits};
+    stable_partition((Workspace*)ws, (const Tup*)in, n, (Tup*)out, dig, nbits,
+                     padded, hist_out, off_out, (hipStream_t)stream);
+}
+
+void smj_dev_sort(smj_workspace* ws, const tuple_t* in, uint64_t n,
+                  tuple_t* out, smj_stream_t stream) {
+    device_sort((Workspace*)ws, (const Tup*)in, n, (Tup*)out,
+                (hipStream_t)stream);
+}
+
+void smj_dev_merge2(const tuple_t* a, uint64_t na, const tuple_t* b,
+                    uint64_t nb, tuple_t* out, smj_stream_t stream) {
+    merge2((const Tup*)a, na, (const Tup*)b, nb, (Tup*)out, (hipStream_t)stream);
+}
+
+void smj_dev_multiway_merge_host(smj_workspace* ws, const tuple_t* const* runs,
+                                 const uint64_t* lens, uint32_t k,
+                                 tuple_t* out, smj_stream_t stream) {
+    multiway_merge((Workspace*)ws, (const Tup* const*)runs, lens, k, (Tup*)out,
+                   (hipStream_t)stream);
+}
+
+void smj_dev_merge_join_count(const tuple_t* r, uint64_t nr, const tuple_t* s,
+                              uint64_t ns, unsigned long long* count_dev,
+                              smj_stream_t stream) {
+    merge_join_count((const Tup*)r, nr, (const Tup*)s, ns, count_dev,
+                     (hipStream_t)stream);
+}
+
+void smj_dev_join(smj_workspace* ws, const tuple_t* R, uint64_t nR,
+                  const tuple_t* S, uint64_t nS, tuple_t* sortedR,
+                  tuple_t* sortedS, uint32_t fanout_bits, int64_t key_min,
+                  int64_t key_max, unsigned long long* count_dev,
+                  smj_stream_t stream) {
+    device_join((Workspace*)ws, (const Tup*)R, nR, (const Tup*)S, nS,
+                (Tup*)sortedR, (Tup*)sortedS, fanout_bits, key_min, key_max,
+                count_dev, (hipStream_t)stream);
+}
+
+void smj_join_phase_ms(smj_workspace* wsp, float* ms5) {
+    Workspace* ws = (Workspace*)wsp;
+    for (int i = 0; i < 5; i++) ms5[i] = 0.f;
+    if (!ws->ev_init) return;
+    SMJ_CHECK(hipEventSynchronize(ws->ev[4]));
+    float a = 0, b = 0, cc = 0, d = 0;
+    SMJ_CHECK(hipEventElapsedTime(&a, ws->ev[0], ws->ev[1]));
+    SMJ_CHECK(hipEventElapsedTime(&b, ws->ev[1], ws->ev[2]));
+    SMJ_CHECK(hipEventElapsedTime(&cc, ws->ev[2], ws->ev[3]));
+    SMJ_CHECK(hipEventElapsedTime(&d, ws->ev[3], ws->ev[4]));
+    ms5[0] = a;
+    ms5[1] = b;
+    ms5[2] = cc;
+    ms5[3] = d;
+    ms5[4] = a + b + cc + d;
+}
+
+void smj_dev_gen_pk(tuple_t* out, uint64_t n, uint64_t first, uint64_t total,
+                    uint64_t seed, int with_payload, smj_stream_t stream) {
+    if (with_payload)
+        gen_pk((Tup*)out, n, first, total, seed, (hipStream_t)stream);
+    else
+        gen_pk_nopayload((Tup*)out, n, first, total, seed, (hipStream_t)stream);
+}
+
+void smj_dev_gen_fk(tuple_t* out, uint64_t n, uint64_t first, uint64_t total,
+                    uint64_t maxid, uint64_t seed, smj_stream_t stream) {
+    gen_fk((Tup*)out, n, first, total, maxid, seed, (hipStream_t)stream);
+}
+
+void smj_dev_gen_zipf(smj_workspace* ws, tuple_t* out, uint64_t n,
+                      uint64_t first, uint64_t maxid, double theta,
+                      uint64_t seed, smj_stream_t stream) {
+    gen_zipf((Workspace*)ws, (Tup*)out, n, first, maxid, theta, seed,
+             (hipStream_t)stream);
+}
+
+void smj_dev_synchronize(smj_stream_t stream) {
+    SMJ_CHECK(hipStreamSynchronize((hipStream_t)stream));
+}
+
+void smj_dev_partition_range(smj_workspace* wsp, const tuple_t* in, uint64_t n,
+                             tuple_t* out, uint32_t nbits, int64_t key_min,
+                             int64_t key_max, int64_t* hist_out,
+                             smj_stream_t stream) {
+    Workspace* ws = (Workspace*)wsp;
+    hipStream_t st = (hipStream_t)stream;
+    RangePlan* plan = (RangePlan*)ws->scratch("range_plan", sizeof(RangePlan));
+    RangePlan h = make_plan(key_min, key_max, nbits, 0, 0);
+    hipLaunchKernelGGL(k_setplan, dim3(1), dim3(1), 0, st, plan, h);
+    uint64_t* starts = (uint64_t*)ws->scratch("range_starts", (1u << nbits) * 8);
+    plan_partition(ws, (const Tup*)in, n, (Tup*)out, plan, nbits, starts,
+                   hist_out, st);
+}
+
+void smj_trace_enable(smj_workspace* wsp, int on) {
+    ((Workspace*)wsp)->trace_on = on != 0;
+}
+
+void smj_trace_reset(smj_workspace* wsp) { ((Workspace*)wsp)->trace_n = 0; }
+
+// Aggregate the traced kernels by name: returns the number of names written;
+// names are '\n'-separated in `names` (capacity `cap` bytes).
+int smj_trace_read(smj_workspace* wsp, char* names, int cap, float* ms_sum,
+                   int* launches, int max) {
+    Workspace* ws = (Workspace*)wsp;
+    if (ws->trace_n == 0) return 0;
+    SMJ_CHECK(hipEventSynchronize(ws->trace[ws->trace_n - 1].b));
+    std::vector<std::string> nm;
+    std::vector<float> ms;
+    std::vector<int> cnt;
+    for (size_t i = 0; i < ws->trace_n; i++) {
+        float t = 0;
+        SMJ_CHECK(hipEventElapsedTime(&t, ws->trace[i].a, ws->trace[i].b));
+        size_t k = 0;
+        while (k < nm.size() && nm[k] != ws->trace[i].name) k++;
+        if (k == nm.size()) {
+            nm.push_back(ws->trace[i].name);
+            ms.push_back(0);
+            cnt.push_back(0);
+        }
+        ms[k] += t;
+        cnt[k]++;
+    }
+    int w = 0, pos = 0;
+    for (size_t k = 0; k < nm.size() && w < max; k++, w++) {
+        int l = (int)nm[k].size();
+        if (pos + l + 1 >= cap) break;
+        memcpy(names + pos, nm[k].data(), l);
+        names[pos + l] = '\n';
+        pos += l + 1;
+        ms_sum[w] = ms[k];
+        launches[w] = cnt[k];
+    }
+    if (pos < cap) names[pos] = 0;
+    return w;
+}
+
+}  // extern "C"

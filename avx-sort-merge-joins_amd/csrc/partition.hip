@@ -1,0 +1,424 @@
+// partition.hip -- stable radix partitioning on MI355X (gfx950).
+//
+// Device form of partition_relation / partition_relation_optimized
+// (reference src/partition/partition.c:93-219, 301-354).  The reference does
+// a histogram pass, then a single-threaded scatter through 64-byte software
+// write-combining buffers flushed with non-temporal stores.  Here:
+//
+//   k_hist    : one pass over the input; every workgroup counts its chunk in an
+//               LDS histogram and writes counts[digit][wg] (digit-major).
+//   k_scanrow : per digit, exclusive scan over workgroups (stable order).
+//   k_scandig : one workgroup; partition starts = exclusive scan over digits of
+//               the (optionally 64-byte padded, ALIGN_NUMTUPLES) totals.
+//   k_scatter : every workgroup re-reads its chunk tile by tile.  Each wave
+//               ranks its 64-item steps with ballot matching (__ballot over the
+//               digit bits -> peers mask -> popcount of lower lanes), which
+//               keeps input order inside a digit (stable == radix_cluster).
+//               The tile is then staged in LDS sorted by digit and written out
+//               so that consecutive lanes write consecutive addresses of one
+//               partition: LDS plays the role of the reference's cache-line
+//               write-combining buffers.
+//
+// Digits wider than 12 bits are done as two stable LSD passes plus a
+// padding copy (host side, smj_partition in this file).
+#include "smj_common.hpp"
+#include "smj_internal.hpp"
+
+namespace smj {
+
+constexpr int PT_THREADS = 256;
+constexpr int PT_ITEMS = 8;  // items per thread per tile
+constexpr int PT_TILE = PT_THREADS * PT_ITEMS;
+constexpr int PT_WAVES = PT_THREADS / 64;
+
+// ---------------------------------------------------------------------------
+template <class Digit>
+__global__ void __launch_bounds__(PT_THREADS)
+k_hist(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig,
+       uint32_t nbins, uint32_t* __restrict__ counts, uint32_t nwg) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_hist[];
+    for (uint32_t d = threadIdx.x; d < nbins; d += PT_THREADS) lds_hist[d] = 0;
+    __syncthreads();
+    const uint64_t beg = (uint64_t)blockIdx.x * chunk;
+    uint64_t end = beg + chunk;
+    if (end > n) end = n;
+    for (uint64_t base = beg; base < end; base += PT_TILE) {
+        Tup v[PT_ITEMS];
+#pragma unroll
+        for (int j = 0; j < PT_ITEMS; j++) {
+            uint64_t i = base + (uint64_t)j * PT_THREADS + threadIdx.x;
+            if (i < end) v[j] = in[i];
+        }
+#pragma unroll
+        for (int j = 0; j < PT_ITEMS; j++) {
+            uint64_t i = base + (uint64_t)j * PT_THREADS + threadIdx.x;
+            if (i < end) atomicAdd(&lds_hist[dig(v[j])], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < nbins; d += PT_THREADS)
+        counts[(uint64_t)d * nwg + blockIdx.x] = lds_hist[d];
+}
+
+// per digit: exclusive scan of counts[d][0..nwg) in place, total -> totals[d]
+__global__ void __launch_bounds__(256)
+k_scanrow(uint32_t* __restrict__ counts, uint32_t nwg,
+          uint64_t* __restrict__ totals) {
+    __shared__ uint32_t scratch[8];
+    uint32_t* row = counts + (uint64_t)blockIdx.x * nwg;
+    const uint32_t per = (nwg + 255) / 256;
+    const uint32_t b = threadIdx.x * per;
+    uint32_t loc = 0;
+    for (uint32_t k = 0; k < per; k++)
+        if (b + k < nwg) loc += row[b + k];
+    uint32_t tot;
+    uint32_t ex = block_exclusive_scan(loc, scratch, &tot);
+    for (uint32_t k = 0; k < per; k++) {
+        if (b + k < nwg) {
+            uint32_t c = row[b + k];
+            row[b + k] = ex;
+            ex += c;
+        }
+    }
+    if (threadIdx.x == 0) totals[blockIdx.x] = tot;
+}
+
+// one workgroup: starts[d] = sum_{d'<d} (padded ? align(tot) : tot)
+__global__ void __launch_bounds__(256)
+k_scandig(const uint64_t* __restrict__ totals, uint32_t nbins, int padded,
+          uint64_t* __restrict__ starts, int64_t* __restrict__ hist_out,
+          int64_t* __restrict__ off_out) {
+    __shared__ uint64_t sh[256];
+    const uint32_t per = (nbins + 255) / 256;
+    const uint32_t b = threadIdx.x * per;
+    uint64_t loc = 0;
+    for (uint32_t k = 0; k < per; k++) {
+        if (b + k < nbins) {
+            uint64_t t = totals[b + k];
+            loc += padded ? align_tuples(t) : t;
+        }
+    }
+    sh[threadIdx.x] = loc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t run = 0;
+        for (int t = 0; t < 256; t++) {
+            uint64_t x = sh[t];
+            sh[t] = run;
+            run += x;
+        }
+    }
+    __syncthreads();
+    uint64_t ex = sh[threadIdx.x];
+    for (uint32_t k = 0; k < per; k++) {
+        uint32_t d = b + k;
+        if (d < nbins) {
+            uint64_t t = totals[d];
+            starts[d] = ex;
+            if (hist_out) hist_out[d] = (int64_t)t;
+            if (off_out) off_out[d] = (int64_t)ex;
+            ex += padded ? align_tuples(t) : t;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// stable scatter.  Dynamic LDS layout (16-byte aligned pieces):
+//   stage  : PT_TILE Tups
+//   run    : nbins uint64  (this workgroup's next output slot per digit)
+//   wcnt   : PT_WAVES * nbins uint32 (per-wave counts -> per-wave offsets)
+//   tstart : nbins uint32  (tile-exclusive start of every digit)
+//   scr    : 16 uint32
+template <class Digit>
+__global__ void __launch_bounds__(PT_THREADS)
+k_scatter(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig,
+          uint32_t nbins, uint32_t dbits, const uint32_t* __restrict__ counts,
+          uint32_t nwg, const uint64_t* __restrict__ starts,
+          Tup* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    Tup* stage = reinterpret_cast<Tup*>(lds_raw);
+    uint64_t* run = reinterpret_cast<uint64_t*>(lds_raw + PT_TILE * sizeof(Tup));
+    uint32_t* wcnt = reinterpret_cast<uint32_t*>(run + nbins);
+    uint32_t* tstart = wcnt + PT_WAVES * nbins;
+    uint32_t* scr = tstart + nbins;
+
+    const int lane = lane_id();
+    const int wid = threadIdx.x >> 6;
+    const uint64_t lt = lanemask_lt();
+
+    for (uint32_t d = threadIdx.x; d < nbins; d += PT_THREADS) {
+        run[d] = starts[d] + counts[(uint64_t)d * nwg + blockIdx.x];
+#pragma unroll
+        for (int w = 0; w < PT_WAVES; w++) wcnt[w * nbins + d] = 0;
+    }
+    __syncthreads();
+
+    const uint64_t beg = (uint64_t)blockIdx.x * chunk;
+    uint64_t end = beg + chunk;
+    if (end > n) end = n;
+    // digits handled by this thread in the per-tile scans (contiguous range)
+    const uint32_t dper = (nbins + PT_THREADS - 1) / PT_THREADS;
+    const uint32_t d0 = threadIdx.x * dper;
+
+    for (uint64_t base = beg; base < end; base += PT_TILE) {
+        const uint32_t tcount =
+            (uint32_t)((end - base) < (uint64_t)PT_TILE ? (end - base) : PT_TILE);
+        // wave `wid` owns items [wid*64*ITEMS, (wid+1)*64*ITEMS) of the tile
+        Tup v[PT_ITEMS];
+        uint32_t dg[PT_ITEMS];
+        uint32_t rk[PT_ITEMS];
+        const uint32_t wbase = wid * 64 * PT_ITEMS;
+#pragma unroll
+        for (int j = 0; j < PT_ITEMS; j++) {
+            uint32_t li = wbase + j * 64 + lane;
+            if (li < tcount) {
+                v[j] = in[base + li];
+                dg[j] = dig(v[j]);
+            } else {
+                dg[j] = 0xffffffffu;
+            }
+        }
+        uint32_t* mycnt = wcnt + wid * nbins;
+#pragma unroll
+        for (int j = 0; j < PT_ITEMS; j++) {
+            const bool valid = dg[j] != 0xffffffffu;
+            uint64_t peers = __ballot(valid);
+            const uint32_t d = valid ? dg[j] : 0;
+            for (uint32_t b = 0; b < dbits; b++) {
+                const bool bit = (d >> b) & 1u;
+                const uint64_t bal = __ballot(bit);
+                peers &= bit ? bal : ~bal;
+            }
+            uint32_t before = 0;
+            if (valid) before = mycnt[d];
+            const uint32_t r = (uint32_t)__popcll(peers & lt);
+            const uint32_t c = (uint32_t)__popcll(peers);
+            // lowest lane of the peer group publishes the new count
+            if (valid && r == 0) mycnt[d] = before + c;
+            rk[j] = before + r;
+        }
+        __syncthreads();
+        // per digit: total over waves, tile exclusive scan, per-wave offsets
+        uint32_t loc = 0;
+        for (uint32_t k = 0; k < dper; k++) {
+            uint32_t d = d0 + k;
+            if (d < nbins) {
+#pragma unroll
+                for (int w = 0; w < PT_WAVES; w++) loc += wcnt[w * nbins + d];
+            }
+        }
+        uint32_t tot;
+        uint32_t ex = block_exclusive_scan(loc, scr, &tot);
+        for (uint32_t k = 0; k < dper; k++) {
+            uint32_t d = d0 + k;
+            if (d < nbins) {
+                tstart[d] = ex;
+#pragma unroll
+                for (int w = 0; w < PT_WAVES; w++) {
+                    uint32_t c = wcnt[w * nbins + d];
+                    wcnt[w * nbins + d] = ex;
+                    ex += c;
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < PT_ITEMS; j++) {
+            if (dg[j] != 0xffffffffu) stage[mycnt[dg[j]] + rk[j]] = v[j];
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < tcount; i += PT_THREADS) {
+            Tup t = stage[i];
+            uint32_t d = dig(t);
+            out[run[d] + (i - tstart[d])] = t;
+        }
+        __syncthreads();
+        for (uint32_t k = 0; k < dper; k++) {
+            uint32_t d = d0 + k;
+            if (d < nbins) {
+                uint32_t nxt = (d + 1 < nbins) ? tstart[d + 1] : tcount;
+                run[d] += nxt - tstart[d];
+#pragma unroll
+                for (int w = 0; w < PT_WAVES; w++) wcnt[w * nbins + d] = 0;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// pad copy for wide digits: item at unpadded position i of digit d moves to
+// padded_start[d] + (i - unpadded_start[d])
+template <class Digit>
+__global__ void k_padcopy(const Tup* __restrict__ in, uint64_t n, Digit dig,
+                          const uint64_t* __restrict__ ustart,
+                          const uint64_t* __restrict__ pstart,
+                          Tup* __restrict__ out) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (; i < n; i += stride) {
+        Tup t = in[i];
+        uint32_t d = dig(t);
+        out[pstart[d] + (i - ustart[d])] = t;
+    }
+}
+
+// global-atomic histogram (wide digits only: test-sized inputs)
+template <class Digit>
+__global__ void k_hist_global(const Tup* __restrict__ in, uint64_t n, Digit dig,
+                              unsigned long long* __restrict__ hist) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (; i < n; i += stride) atomicAdd(&hist[dig(in[i])], 1ull);
+}
+
+__global__ void k_u64_to_i64(const unsigned long long* a, int64_t* b,
+                             uint32_t m) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) b[i] = (int64_t)a[i];
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+static size_t scatter_lds_bytes(uint32_t nbins) {
+    size_t b = (size_t)PT_TILE * sizeof(Tup);
+    b += (size_t)nbins * sizeof(uint64_t);
+    b += (size_t)PT_WAVES * nbins * sizeof(uint32_t);
+    b += (size_t)nbins * sizeof(uint32_t);
+    b += 16 * sizeof(uint32_t);
+    return b;
+}
+
+struct LowBits {
+    Digit32 inner;
+    uint32_t lowbits;
+    __device__ __forceinline__ uint32_t operator()(const Tup& t) const {
+        return inner(t) & ((1u << lowbits) - 1u);
+    }
+};
+struct HighBits {
+    Digit32 inner;
+    uint32_t lowbits;
+    __device__ __forceinline__ uint32_t operator()(const Tup& t) const {
+        return inner(t) >> lowbits;
+    }
+};
+
+template <class Digit>
+static void stable_partition_narrow(Workspace* ws, const Tup* in, uint64_t n,
+                                    Tup* out, const Digit& dig, uint32_t dbits,
+                                    int padded, uint64_t* starts_dev,
+                                    int64_t* hist_out, int64_t* off_out,
+                                    hipStream_t st) {
+    const uint32_t nbins = 1u << dbits;
+    uint64_t ntiles = (n + PT_TILE - 1) / PT_TILE;
+    if (ntiles == 0) ntiles = 1;
+    uint32_t nwg = (uint32_t)(ntiles < 2048 ? ntiles : 2048);
+    const uint64_t tiles_per_wg = (ntiles + nwg - 1) / nwg;
+    const uint64_t chunk = tiles_per_wg * PT_TILE;
+    nwg = (uint32_t)((ntiles + tiles_per_wg - 1) / tiles_per_wg);
+
+    uint32_t* counts = (uint32_t*)ws->scratch("pt_counts",
+                                              (size_t)nbins * nwg * 4);
+    uint64_t* totals = (uint64_t*)ws->scratch("pt_totals", (size_t)nbins * 8);
+    {
+        TraceScope ts(ws, "k_hist", st);
+        hipLaunchKernelGGL(k_hist<Digit>, dim3(nwg), dim3(PT_THREADS),
+                           nbins * sizeof(uint32_t), st, in, n, chunk, dig, nbins,
+                           counts, nwg);
+    }
+    {
+        TraceScope ts(ws, "k_scan", st);
+        hipLaunchKernelGGL(k_scanrow, dim3(nbins), dim3(256), 0, st, counts, nwg,
+                           totals);
+        hipLaunchKernelGGL(k_scandig, dim3(1), dim3(256), 0, st, totals, nbins,
+                           padded, starts_dev, hist_out, off_out);
+    }
+    if (n == 0) return;
+    const size_t lds = scatter_lds_bytes(nbins);
+    static bool attr_set = false;
+    if (!attr_set) {
+        SMJ_CHECK(hipFuncSetAttribute(
+            (const void*)k_scatter<Digit>,
+            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr_set = true;
+    }
+    {
+        TraceScope ts(ws, "k_scatter", st);
+        hipLaunchKernelGGL(k_scatter<Digit>, dim3(nwg), dim3(PT_THREADS), lds, st,
+                           in, n, chunk, dig, nbins, dbits, counts, nwg,
+                           starts_dev, out);
+    }
+    SMJ_CHECK(hipGetLastError());
+}
+
+void stable_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
+                      const Digit32& dig, uint32_t dbits, int padded,
+                      int64_t* hist_out, int64_t* off_out, hipStream_t st) {
+    const uint32_t nbins = 1u << dbits;
+    if (dbits <= kNarrowDigitBits) {
+        uint64_t* starts = (uint64_t*)ws->scratch("pt_starts", (size_t)nbins * 8);
+        stable_partition_narrow(ws, in, n, out, dig, dbits, padded, starts,
+                                hist_out, off_out, st);
+        return;
+    }
+    // wide digits: stable LSD (low part, then high part), then pad copy
+    const uint32_t lowb = dbits / 2, highb = dbits - lowb;
+    Tup* t1 = (Tup*)ws->scratch("pt_wide1", (n ? n : 1) * sizeof(Tup));
+    Tup* t2 = (Tup*)ws->scratch("pt_wide2", (n ? n : 1) * sizeof(Tup));
+    uint64_t* st1 = (uint64_t*)ws->scratch("pt_wst1", (1u << lowb) * 8);
+    uint64_t* st2 = (uint64_t*)ws->scratch("pt_wst2", (1u << highb) * 8);
+    LowBits lo{dig, lowb};
+    HighBits hi{dig, lowb};
+    stable_partition_narrow(ws, in, n, t1, lo, lowb, 0, st1, nullptr, nullptr, st);
+    stable_partition_narrow(ws, t1, n, t2, hi, highb, 0, st2, nullptr, nullptr, st);
+    unsigned long long* h = (unsigned long long*)ws->scratch("pt_whist", (size_t)nbins * 8);
+    SMJ_CHECK(hipMemsetAsync(h, 0, (size_t)nbins * 8, st));
+    if (n) hipLaunchKernelGGL(k_hist_global<Digit32>, dim3(1024), dim3(256), 0,
+                              st, in, n, dig, h);
+    uint64_t* ust = (uint64_t*)ws->scratch("pt_wust", (size_t)nbins * 8);
+    uint64_t* pst = (uint64_t*)ws->scratch("pt_wpst", (size_t)nbins * 8);
+    hipLaunchKernelGGL(k_scandig, dim3(1), dim3(256), 0, st,
+                       (const uint64_t*)h, nbins, 0, ust, nullptr, nullptr);
+    hipLaunchKernelGGL(k_scandig, dim3(1), dim3(256), 0, st,
+                       (const uint64_t*)h, nbins, padded, pst, hist_out, off_out);
+    if (n) hipLaunchKernelGGL(k_padcopy<Digit32>, dim3(2048), dim3(256), 0, st,
+                              t2, n, dig, ust, pst, out);
+    SMJ_CHECK(hipGetLastError());
+}
+
+// level-1 partition of the join: range-plan digit, unpadded, stable
+void plan_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
+                    const RangePlan* plan_dev, uint32_t dbits,
+                    uint64_t* starts_dev, int64_t* hist_out, hipStream_t st) {
+    PlanDigit1 dig{plan_dev};
+    stable_partition_narrow(ws, in, n, out, dig, dbits, 0, starts_dev, hist_out,
+                            nullptr, st);
+}
+
+// histogram-only pass + plain copy (histogram_memcpy_bench)
+void hist_memcpy(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
+                 uint32_t dbits, hipStream_t st) {
+    const uint32_t nbins = 1u << dbits;
+    uint64_t ntiles = (n + PT_TILE - 1) / PT_TILE;
+    if (ntiles == 0) ntiles = 1;
+    uint32_t nwg = (uint32_t)(ntiles < 2048 ? ntiles : 2048);
+    const uint64_t tiles_per_wg = (ntiles + nwg - 1) / nwg;
+    const uint64_t chunk = tiles_per_wg * PT_TILE;
+    nwg = (uint32_t)((ntiles + tiles_per_wg - 1) / tiles_per_wg);
+    uint32_t* counts = (uint32_t*)ws->scratch("pt_counts", (size_t)nbins * nwg * 4);
+    Digit32 dig{nbins - 1u, 0u};
+    if (dbits > kNarrowDigitBits) {
+        unsigned long long* h = (unsigned long long*)ws->scratch("pt_whist", (size_t)nbins * 8);
+        SMJ_CHECK(hipMemsetAsync(h, 0, (size_t)nbins * 8, st));
+        if (n) hipLaunchKernelGGL(k_hist_global<Digit32>, dim3(1024), dim3(256), 0, st, in, n, dig, h);
+    } else {
+        hipLaunchKernelGGL(k_hist<Digit32>, dim3(nwg), dim3(PT_THREADS),
+                           nbins * sizeof(uint32_t), st, in, n, chunk, dig, nbins,
+                           counts, nwg);
+    }
+    if (n) SMJ_CHECK(hipMemcpyAsync(out, in, n * sizeof(Tup),
+                                    hipMemcpyDeviceToDevice, st));
+}
+
+}  // namespace smj

@@ -1,0 +1,224 @@
+// smj_common.hpp -- shared device/host definitions for the MI355X sort-merge
+// join kernels (gfx950, wave64).
+//
+// Tuple width is fixed per build (KEY_8B -> 16-byte tuples), mirroring the
+// reference's compile-time switch (src/types.h:23-29).  On the device a tuple
+// is handled as one machine word:
+//   8-byte  tuple -> uint64_t  (payload in bits 0..31, key in bits 32..63)
+//   16-byte tuple -> Tup16     {int64 payload; int64 key}
+// Sort order (the parity contract):
+//   8-byte : signed int64 order of the packed word  (what avxsort produces,
+//            src/avxsort/avxcommon.h:79-190, inside the generators' domain)
+//   16-byte: (key, payload) lexicographic, both signed
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#define SMJ_CHECK(call)                                                        \
+    do {                                                                       \
+        hipError_t e_ = (call);                                                \
+        if (e_ != hipSuccess) {                                                \
+            fprintf(stderr, "[ERROR] smj: %s failed at %s:%d: %s\n", #call,    \
+                    __FILE__, __LINE__, hipGetErrorString(e_));                \
+            abort();                                                           \
+        }                                                                      \
+    } while (0)
+
+namespace smj {
+
+#ifdef KEY_8B
+struct __attribute__((aligned(16))) Tup {
+    int64_t payload;
+    int64_t key;
+};
+#else
+typedef uint64_t Tup;
+#endif
+
+constexpr int kTupBytes = sizeof(Tup);
+
+__host__ __device__ __forceinline__ int64_t tup_key(const Tup& t) {
+#ifdef KEY_8B
+    return t.key;
+#else
+    return (int64_t)(int32_t)(uint32_t)(t >> 32);
+#endif
+}
+
+// strict weak order == total order on the tuple's bytes (see header)
+__host__ __device__ __forceinline__ bool tup_less(const Tup& a, const Tup& b) {
+#ifdef KEY_8B
+    return (a.key < b.key) || (a.key == b.key && a.payload < b.payload);
+#else
+    return (int64_t)a < (int64_t)b;
+#endif
+}
+
+__host__ __device__ __forceinline__ bool tup_eq(const Tup& a, const Tup& b) {
+#ifdef KEY_8B
+    return a.key == b.key && a.payload == b.payload;
+#else
+    return a == b;
+#endif
+}
+
+__host__ __device__ __forceinline__ Tup tup_max_sentinel() {
+#ifdef KEY_8B
+    Tup t;
+    t.payload = INT64_MAX;
+    t.key = INT64_MAX;
+    return t;
+#else
+    return (uint64_t)INT64_MAX;
+#endif
+}
+
+// order-preserving map of a signed key to unsigned
+__host__ __device__ __forceinline__ uint64_t key_u(int64_t k) {
+    return (uint64_t)k ^ 0x8000000000000000ull;
+}
+
+// ---------------------------------------------------------------------------
+// Partition digit of the reference API (src/partition/partition.c:29):
+//   ((key - 1) & (((1<<D)-1) << R)) >> R    with a 32-bit mask
+// ---------------------------------------------------------------------------
+struct RefDigit {
+    uint32_t mask;
+    uint32_t shift;
+    __device__ __forceinline__ uint32_t operator()(const Tup& t) const {
+        uint64_t km1 = (uint64_t)(tup_key(t) - 1);
+        return (uint32_t)((km1 & (uint64_t)mask) >> shift);
+    }
+};
+
+// ---------------------------------------------------------------------------
+// Range plan: monotone (order preserving) multi-level MSD digits over the key
+// range [base, base + 2^L).  Keys outside the range clamp to the first/last
+// digit, so every level stays monotone in the key whatever the estimate.
+//   rel(k) = clamp(key_u(k) - key_u(base), 0, 2^L - 1)
+//   level-1 digit  d1 = rel >> s1                       (fanout 2^D1)
+//   level-2 digit  d2 = (rel >> s2) - (d1 << D2)        (2^D2 per bucket)
+//   level-3 digit  d3 = (rel >> s3) - ((d1<<D2|d2) << D3)
+// ---------------------------------------------------------------------------
+struct RangePlan {
+    int64_t base;     // smallest key of the range
+    uint64_t span;    // 2^L - 1 (all-ones of width L), L <= 64
+    uint32_t D1, D2, D3;
+    uint32_t s1, s2, s3;
+};
+
+__host__ __device__ __forceinline__ uint64_t plan_rel(const RangePlan& p,
+                                                      int64_t k) {
+    uint64_t ku = key_u(k), bu = key_u(p.base);
+    if (ku < bu) return 0;
+    uint64_t r = ku - bu;
+    return r > p.span ? p.span : r;
+}
+
+__host__ __device__ __forceinline__ uint32_t plan_d1(const RangePlan& p,
+                                                     uint64_t rel) {
+    uint64_t d = rel >> p.s1;
+    uint64_t lim = (1ull << p.D1) - 1;
+    return (uint32_t)(d > lim ? lim : d);
+}
+
+// level-2 digit of `rel` inside bucket d1
+__host__ __device__ __forceinline__ uint32_t plan_d2(const RangePlan& p,
+                                                     uint64_t rel,
+                                                     uint32_t d1) {
+    uint64_t v = rel >> p.s2;
+    uint64_t lo = (uint64_t)d1 << p.D2;
+    uint64_t lim = (1ull << p.D2) - 1;
+    if (v < lo) return 0;
+    v -= lo;
+    return (uint32_t)(v > lim ? lim : v);
+}
+
+__host__ __device__ __forceinline__ uint32_t plan_d3(const RangePlan& p,
+                                                     uint64_t rel,
+                                                     uint32_t d12) {
+    uint64_t v = rel >> p.s3;
+    uint64_t lo = (uint64_t)d12 << p.D3;
+    uint64_t lim = (1ull << p.D3) - 1;
+    if (v < lo) return 0;
+    v -= lo;
+    return (uint32_t)(v > lim ? lim : v);
+}
+
+// Host helper: build a plan for key range [kmin, kmax] and level widths.
+__host__ __device__ inline RangePlan make_plan(int64_t kmin, int64_t kmax,
+                                               uint32_t D1, uint32_t D2,
+                                               uint32_t D3max) {
+    RangePlan p;
+    p.base = kmin;
+    uint64_t width = (kmax >= kmin) ? (key_u(kmax) - key_u(kmin)) : 0;
+    uint32_t L = 0;
+    while (L < 64 && (width >> L) != 0) L++;
+    p.span = (L >= 64) ? ~0ull : ((1ull << L) - 1);
+    p.D1 = D1;
+    p.s1 = L > D1 ? L - D1 : 0;
+    p.D2 = D2 < p.s1 ? D2 : p.s1;  // never more level-2 bits than remain
+    p.s2 = p.s1 - p.D2;
+    uint32_t d3 = p.s2 < D3max ? p.s2 : D3max;
+    p.D3 = d3;
+    p.s3 = p.s2 - d3;
+    return p;
+}
+
+// ---------------------------------------------------------------------------
+// Wave / block helpers (wave64)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+__device__ __forceinline__ uint64_t lanemask_lt() {
+    int l = lane_id();
+    return l == 0 ? 0ull : (~0ull >> (64 - l));
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// block-wide exclusive scan of one uint32 per thread (blockDim.x threads,
+// multiple of 64). `scratch` >= blockDim.x/64 + 1 words of LDS.
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v,
+                                                         uint32_t* scratch,
+                                                         uint32_t* total) {
+    const int lane = lane_id();
+    const int wid = threadIdx.x >> 6;
+    const int nw = blockDim.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) scratch[wid] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (int w = 0; w < nw; w++) {
+            uint32_t t = scratch[w];
+            scratch[w] = run;
+            run += t;
+        }
+        scratch[nw] = run;
+    }
+    __syncthreads();
+    uint32_t res = scratch[wid] + x - v;
+    if (total) *total = scratch[nw];
+    __syncthreads();
+    return res;
+}
+
+__host__ __device__ __forceinline__ uint64_t align_tuples(uint64_t n) {
+    const uint64_t tpl = 64 / sizeof(Tup);
+    return (n + tpl - 1) & ~(tpl - 1);
+}
+
+}  // namespace smj

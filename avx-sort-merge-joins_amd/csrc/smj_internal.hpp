@@ -1,0 +1,171 @@
+// smj_internal.hpp -- host-side internal interfaces between the .hip units.
+#pragma once
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "smj_common.hpp"
+
+namespace smj {
+
+constexpr uint32_t kNarrowDigitBits = 12;  // widest digit of a single pass
+
+// reference partition digit (runtime mask/shift), see smj_common.hpp
+typedef RefDigit Digit32;
+
+// level-1 digit of a device-resident range plan
+struct PlanDigit1 {
+    const RangePlan* plan;
+    __device__ __forceinline__ uint32_t operator()(const Tup& t) const {
+        const RangePlan& p = *plan;
+        return plan_d1(p, plan_rel(p, tup_key(t)));
+    }
+};
+
+// Grow-only named device scratch.  Reallocation frees the old buffer with
+// hipFree (which synchronises), so it only happens on warm-up calls.
+struct Workspace {
+    std::map<std::string, std::pair<void*, size_t>> bufs;
+    std::map<std::string, std::pair<void*, size_t>> pinned;
+    hipEvent_t ev[8] = {};
+    bool ev_init = false;
+    float phase_ms[5] = {0, 0, 0, 0, 0};
+
+    void* scratch(const char* name, size_t bytes) {
+        if (bytes == 0) bytes = 16;
+        auto it = bufs.find(name);
+        if (it != bufs.end() && it->second.second >= bytes)
+            return it->second.first;
+        if (it != bufs.end()) SMJ_CHECK(hipFree(it->second.first));
+        void* p = nullptr;
+        size_t cap = bytes + bytes / 8;
+        SMJ_CHECK(hipMalloc(&p, cap));
+        bufs[name] = {p, cap};
+        return p;
+    }
+    void* host_pinned(const char* name, size_t bytes) {
+        if (bytes == 0) bytes = 16;
+        auto it = pinned.find(name);
+        if (it != pinned.end() && it->second.second >= bytes)
+            return it->second.first;
+        if (it != pinned.end()) SMJ_CHECK(hipHostFree(it->second.first));
+        void* p = nullptr;
+        SMJ_CHECK(hipHostMalloc(&p, bytes, hipHostMallocDefault));
+        pinned[name] = {p, bytes};
+        return p;
+    }
+    void events() {
+        if (!ev_init) {
+            for (auto& e : ev) SMJ_CHECK(hipEventCreate(&e));
+            ev_init = true;
+        }
+    }
+
+    // per-kernel event trace (bench.py's roofline needs each kernel's own
+    // duration over the timed region); off unless smj_trace_enable()
+    struct TraceRec {
+        const char* name;
+        hipEvent_t a, b;
+    };
+    bool trace_on = false;
+    std::vector<TraceRec> trace;
+    size_t trace_n = 0;
+    int trace_begin(const char* name, hipStream_t st) {
+        if (!trace_on) return -1;
+        if (trace_n == trace.size()) {
+            TraceRec r;
+            SMJ_CHECK(hipEventCreate(&r.a));
+            SMJ_CHECK(hipEventCreate(&r.b));
+            trace.push_back(r);
+        }
+        trace[trace_n].name = name;
+        SMJ_CHECK(hipEventRecord(trace[trace_n].a, st));
+        return (int)trace_n++;
+    }
+    void trace_end(int idx, hipStream_t st) {
+        if (idx >= 0) SMJ_CHECK(hipEventRecord(trace[idx].b, st));
+    }
+
+    ~Workspace() {
+        for (auto& r : trace) {
+            (void)hipEventDestroy(r.a);
+            (void)hipEventDestroy(r.b);
+        }
+        for (auto& kv : bufs) (void)hipFree(kv.second.first);
+        for (auto& kv : pinned) (void)hipHostFree(kv.second.first);
+        if (ev_init)
+            for (auto& e : ev) (void)hipEventDestroy(e);
+    }
+};
+
+struct TraceScope {
+    Workspace* ws;
+    hipStream_t st;
+    int idx;
+    TraceScope(Workspace* w, const char* name, hipStream_t s)
+        : ws(w), st(s), idx(w ? w->trace_begin(name, s) : -1) {}
+    ~TraceScope() {
+        if (ws) ws->trace_end(idx, st);
+    }
+};
+
+// ---- partition.hip
+void stable_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
+                      const Digit32& dig, uint32_t dbits, int padded,
+                      int64_t* hist_out, int64_t* off_out, hipStream_t st);
+void plan_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
+                    const RangePlan* plan_dev, uint32_t dbits,
+                    uint64_t* starts_dev, int64_t* hist_out, hipStream_t st);
+void hist_memcpy(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
+                 uint32_t dbits, hipStream_t st);
+
+// ---- bucketsort.hip : MSD bucket sort (+ fused merge-join count)
+struct BucketSortArgs {
+    // level-1 partitioned relation(s): bucket b occupies
+    // [bstart[b], bstart[b] + bcount[b]) of `part`.
+    const Tup* part[2];
+    const uint64_t* bstart[2];  // device, nbuckets
+    const int64_t* bcount[2];   // device, nbuckets
+    Tup* tmp[2];                // same size as part (tile-local pass output)
+    Tup* out[2];                // sorted output, bucket b at ostart[b]
+    uint64_t n[2];
+    int nrel;                   // 1 = sort only, 2 = R and S + join count
+    uint32_t nbuckets;          // 1 << D1
+    const RangePlan* plan_dev;
+    unsigned long long* count_dev;  // join count (nrel == 2), accumulated
+    hipEvent_t ev_tile = nullptr;   // optional phase markers
+    hipEvent_t ev_bucket = nullptr;
+    hipEvent_t ev_ovf = nullptr;
+};
+// Runs the tile pass and the bucket pass; handles overflowing sub-buckets
+// (skew) with the merge-sort fallback.  May synchronise `st` once.
+void bucket_sort(Workspace* ws, const BucketSortArgs& a, uint32_t D2,
+                 hipStream_t st);
+
+// plan selection from a device sample (writes plan_dev)
+void plan_from_sample(Workspace* ws, const Tup* const* rels,
+                      const uint64_t* ns, int nrel, uint32_t D1, uint32_t D2,
+                      int64_t hint_min, int64_t hint_max, RangePlan* plan_dev,
+                      hipStream_t st);
+
+// ---- mergesort.hip : general segmented merge sort + merge path kernels
+void segmented_sort(Workspace* ws, Tup* data, const uint64_t* seg_off_host,
+                    const uint64_t* seg_len_host, uint32_t nseg, hipStream_t st);
+void merge2(const Tup* a, uint64_t na, const Tup* b, uint64_t nb, Tup* out,
+            hipStream_t st);
+void merge_join_count(const Tup* r, uint64_t nr, const Tup* s, uint64_t ns,
+                      unsigned long long* count_dev, hipStream_t st);
+void multiway_merge(Workspace* ws, const Tup* const* runs_host,
+                    const uint64_t* lens_host, uint32_t k, Tup* out,
+                    hipStream_t st);
+
+// ---- datagen.hip
+void gen_pk(Tup* out, uint64_t n, uint64_t first, uint64_t total,
+            uint64_t seed, hipStream_t st);
+void gen_fk(Tup* out, uint64_t n, uint64_t first, uint64_t total,
+            uint64_t maxid, uint64_t seed, hipStream_t st);
+void gen_zipf(Workspace* ws, Tup* out, uint64_t n, uint64_t first,
+              uint64_t maxid, double theta, uint64_t seed, hipStream_t st);
+
+}  // namespace smj

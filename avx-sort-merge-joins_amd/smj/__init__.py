@@ -1,0 +1,331 @@
+"""Python binding of the MI355X sort-merge-join C ABI (include/smj.h).
+
+This is plumbing over ctypes, not a second implementation: every call lands in
+libsmj_hip.so (8-byte tuples) or libsmj_hip_k8.so (16-byte tuples) and runs on
+the GPU.  Loading fails loudly when the library is missing, and the library
+itself aborts when no HIP device is present (there is no CPU fallback).
+
+Two views of the same library:
+
+* ``Library.<reference name>`` -- the reference's functions on host numpy
+  arrays (structured dtype payload-then-key, like ``tuple_t``), used by the
+  parity tests: partition_relation[_optimized], avxsort_tuples,
+  avx_merge_tuples, avx_multiway_merge, merge_join, sortmergejoin_multiway.
+* ``Library.dev_*`` -- the device-resident asynchronous API on torch tensors
+  (shape (n, 2): column 0 payload, column 1 key; int32 or int64), used by
+  bench.py and the multi-GPU path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+try:  # torch must own the HIP runtime before our library binds to it
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is part of the image
+    torch = None
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+LIBDIR = os.path.join(ROOT, "lib")
+TUPLE8 = np.dtype([("payload", "<i4"), ("key", "<i4")])
+TUPLE16 = np.dtype([("payload", "<i8"), ("key", "<i8")])
+
+# Every entry point the C ABI exports (include/smj.h).  The CPU test suite
+# checks that both libraries export all of them.
+REFERENCE_SYMBOLS = [
+    "partition_relation", "partition_relation_optimized",
+    "partition_relation_optimized_V2", "histogram_memcpy_bench",
+    "avxsort_tuples", "avxsort_int64", "avxsort_int32",
+    "avxsortmultiway_tuples", "avxsortmultiway_int64",
+    "scalarsort_tuples", "scalarsort_int64", "scalarsort_int32",
+    "avx_merge_tuples", "avx_merge_int64", "scalar_merge_tuples",
+    "scalar_merge_int64", "avx_multiway_merge", "scalar_multiway_merge",
+    "scalar_multiway_merge_modulo", "scalar_multiway_merge_bitand",
+    "merge_join", "sortmergejoin_multiway", "sortmergejoin_mpsm",
+]
+DEVICE_SYMBOLS = [
+    "smj_tuple_bytes", "smj_device_name", "smj_workspace_create",
+    "smj_workspace_destroy", "smj_dev_partition", "smj_dev_sort",
+    "smj_dev_merge2", "smj_dev_multiway_merge_host", "smj_dev_merge_join_count",
+    "smj_dev_join", "smj_join_phase_ms", "smj_dev_gen_pk", "smj_dev_gen_fk",
+    "smj_dev_gen_zipf", "smj_dev_synchronize", "smj_dev_partition_range",
+    "smj_trace_enable", "smj_trace_reset", "smj_trace_read",
+]
+
+
+def lib_path(width: int) -> str:
+    return os.path.join(LIBDIR, "libsmj_hip.so" if width == 8 else "libsmj_hip_k8.so")
+
+
+def build(jobs: int = 8) -> None:
+    """Compile both libraries for gfx950 (hipcc; cross-compiles without a GPU)."""
+    import subprocess
+    subprocess.check_call(["make", "-C", ROOT, f"-j{jobs}"])
+
+
+class Relation(C.Structure):
+    _fields_ = [("tuples", C.c_void_p), ("num_tuples", C.c_uint64)]
+
+
+class JoinConfig(C.Structure):
+    _fields_ = [("NTHREADS", C.c_int), ("PARTFANOUT", C.c_int),
+                ("SCALARSORT", C.c_int), ("SCALARMERGE", C.c_int),
+                ("MWAYMERGEBUFFERSIZE", C.c_int), ("NUMASTRATEGY", C.c_int)]
+
+
+class ThreadResult(C.Structure):
+    _fields_ = [("nresults", C.c_int64), ("results", C.c_void_p),
+                ("threadid", C.c_uint32)]
+
+
+class Result(C.Structure):
+    _fields_ = [("totalresults", C.c_int64),
+                ("resultlist", C.POINTER(ThreadResult)), ("nthreads", C.c_int)]
+
+
+_P = C.c_void_p
+_U64 = C.c_uint64
+_I64 = C.c_int64
+_U32 = C.c_uint32
+
+
+def _ptr(a):
+    return a.ctypes.data
+
+
+class Library:
+    def __init__(self, width: int = 16, path: str | None = None):
+        assert width in (8, 16)
+        self.width = width
+        self.dtype = TUPLE8 if width == 8 else TUPLE16
+        self.path = path or lib_path(width)
+        if not os.path.exists(self.path):
+            raise FileNotFoundError(
+                f"{self.path} missing: build it with `make -C {ROOT}` "
+                "(there is no CPU fallback)")
+        self.lib = C.CDLL(self.path)
+        L = self.lib
+        sig = {
+            "partition_relation": (None, [_P, _P, _P, C.c_int, C.c_int]),
+            "partition_relation_optimized": (None, [_P, _P, _P, _U32, _U32]),
+            "partition_relation_optimized_V2": (None, [_P, _P, _P, _U32, _U32]),
+            "histogram_memcpy_bench": (None, [_P, _P, _P, _U32]),
+            "avxsort_tuples": (None, [_P, _P, _U64]),
+            "avxsort_int64": (None, [_P, _P, _U64]),
+            "avxsort_int32": (None, [_P, _P, _U64]),
+            "avxsortmultiway_tuples": (None, [_P, _P, _U64]),
+            "avxsortmultiway_int64": (None, [_P, _P, _U64]),
+            "scalarsort_tuples": (None, [_P, _P, _U64]),
+            "scalarsort_int64": (None, [_P, _P, _U64]),
+            "scalarsort_int32": (None, [_P, _P, _U64]),
+            "avx_merge_tuples": (_U64, [_P, _P, _P, _U64, _U64]),
+            "avx_merge_int64": (_U64, [_P, _P, _P, _U64, _U64]),
+            "scalar_merge_tuples": (_U64, [_P, _P, _P, _U64, _U64]),
+            "scalar_merge_int64": (_U64, [_P, _P, _P, _U64, _U64]),
+            "avx_multiway_merge": (_U64, [_P, _P, _U32, _P, _U32]),
+            "scalar_multiway_merge": (_U64, [_P, _P, _U32, _P, _U32]),
+            "merge_join": (_U64, [_P, _P, _U64, _U64, _P]),
+            "sortmergejoin_multiway": (C.POINTER(Result), [_P, _P, _P]),
+            "sortmergejoin_mpsm": (C.POINTER(Result), [_P, _P, _P]),
+            "smj_tuple_bytes": (C.c_int, []),
+            "smj_device_name": (C.c_char_p, []),
+            "smj_workspace_create": (_P, []),
+            "smj_workspace_destroy": (None, [_P]),
+            "smj_dev_partition": (None, [_P, _P, _U64, _P, _U32, _U32, C.c_int, _P, _P, _P]),
+            "smj_dev_sort": (None, [_P, _P, _U64, _P, _P]),
+            "smj_dev_merge2": (None, [_P, _U64, _P, _U64, _P, _P]),
+            "smj_dev_multiway_merge_host": (None, [_P, _P, _P, _U32, _P, _P]),
+            "smj_dev_merge_join_count": (None, [_P, _U64, _P, _U64, _P, _P]),
+            "smj_dev_join": (None, [_P, _P, _U64, _P, _U64, _P, _P, _U32, _I64, _I64, _P, _P]),
+            "smj_join_phase_ms": (None, [_P, _P]),
+            "smj_dev_gen_pk": (None, [_P, _U64, _U64, _U64, _U64, C.c_int, _P]),
+            "smj_dev_gen_fk": (None, [_P, _U64, _U64, _U64, _U64, _U64, _P]),
+            "smj_dev_gen_zipf": (None, [_P, _P, _U64, _U64, _U64, C.c_double, _U64, _P]),
+            "smj_dev_synchronize": (None, [_P]),
+            "smj_dev_partition_range": (None, [_P, _P, _U64, _P, _U32, _I64, _I64, _P, _P]),
+            "smj_trace_enable": (None, [_P, C.c_int]),
+            "smj_trace_reset": (None, [_P]),
+            "smj_trace_read": (C.c_int, [_P, C.c_char_p, C.c_int, _P, _P, C.c_int]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        got = L.smj_tuple_bytes()
+        assert got == width, f"{self.path} built for {got}-byte tuples"
+        self._ws = None
+
+    # ------------------------------------------------------------------ host
+    def _rel(self, a: np.ndarray) -> Relation:
+        return Relation(a.ctypes.data, len(a))
+
+    def _parts(self, fan: int):
+        rels = (Relation * fan)()
+        ptrs = (C.POINTER(Relation) * fan)(*[C.pointer(rels[i]) for i in range(fan)])
+        return rels, ptrs
+
+    def partition(self, t: np.ndarray, nbits: int, shift: int, variant: int = 1):
+        """variant 0 = partition_relation, 1 = _optimized, 2 = _optimized_V2.
+        Returns (output buffer, counts, offsets in tuples)."""
+        fan = 1 << nbits
+        t = np.ascontiguousarray(t, dtype=self.dtype)
+        out = np.zeros(len(t) + fan * 64 // self.width, self.dtype)
+        rin, rout = self._rel(t), self._rel(out)
+        rout.num_tuples = len(t)
+        rels, ptrs = self._parts(fan)
+        fn = [self.lib.partition_relation, self.lib.partition_relation_optimized,
+              self.lib.partition_relation_optimized_V2][variant]
+        fn(C.cast(ptrs, _P), C.byref(rin), C.byref(rout), nbits, shift)
+        base = out.ctypes.data
+        cnt = np.array([rels[i].num_tuples for i in range(fan)], np.int64)
+        off = np.array([(rels[i].tuples - base) // self.width for i in range(fan)], np.int64)
+        return out, cnt, off
+
+    def avxsort_tuples(self, t: np.ndarray, fn: str = "avxsort_tuples") -> np.ndarray:
+        a = np.ascontiguousarray(t, dtype=self.dtype).copy()
+        b = np.zeros_like(a)
+        pa, pb = C.c_void_p(a.ctypes.data), C.c_void_p(b.ctypes.data)
+        getattr(self.lib, fn)(C.byref(pa), C.byref(pb), len(a))
+        res = b if pb.value == b.ctypes.data else a
+        return res.copy()
+
+    def sort_int(self, v: np.ndarray, fn: str = "avxsort_int64") -> np.ndarray:
+        dt = np.int32 if fn.endswith("int32") else np.int64
+        a = np.ascontiguousarray(v, dtype=dt).copy()
+        b = np.zeros_like(a)
+        pa, pb = C.c_void_p(a.ctypes.data), C.c_void_p(b.ctypes.data)
+        getattr(self.lib, fn)(C.byref(pa), C.byref(pb), len(a))
+        return (b if pb.value == b.ctypes.data else a).copy()
+
+    def avx_merge_tuples(self, a, b, fn="avx_merge_tuples") -> np.ndarray:
+        a = np.ascontiguousarray(a, dtype=self.dtype)
+        b = np.ascontiguousarray(b, dtype=self.dtype)
+        out = np.zeros(len(a) + len(b), self.dtype)
+        n = getattr(self.lib, fn)(_ptr(a), _ptr(b), _ptr(out), len(a), len(b))
+        assert n == len(out)
+        return out
+
+    def avx_multiway_merge(self, runs, fn="avx_multiway_merge"):
+        runs = [np.ascontiguousarray(r, dtype=self.dtype) for r in runs]
+        k = len(runs)
+        total = sum(len(r) for r in runs)
+        out = np.zeros(total, self.dtype)
+        rels = (Relation * k)(*[Relation(r.ctypes.data, len(r)) for r in runs])
+        ptrs = (C.POINTER(Relation) * k)(*[C.pointer(rels[i]) for i in range(k)])
+        fifo = np.zeros(1 << 16, self.dtype)
+        n = getattr(self.lib, fn)(_ptr(out), C.cast(ptrs, _P), k, _ptr(fifo), len(fifo))
+        consumed = all(rels[i].num_tuples == 0 and
+                       rels[i].tuples == runs[i].ctypes.data + len(runs[i]) * self.width
+                       for i in range(k))
+        return out, int(n), consumed
+
+    def merge_join(self, r, s) -> int:
+        r = np.ascontiguousarray(r, dtype=self.dtype)
+        s = np.ascontiguousarray(s, dtype=self.dtype)
+        return int(self.lib.merge_join(_ptr(r), _ptr(s), len(r), len(s), None))
+
+    def sortmergejoin_multiway(self, R, S, nthreads=1, fanout=128, mpsm=False):
+        R = np.ascontiguousarray(R, dtype=self.dtype)
+        S = np.ascontiguousarray(S, dtype=self.dtype)
+        cfg = JoinConfig(nthreads, fanout, int(self.width == 16), int(self.width == 16),
+                         20 << 20, 2)
+        rr, rs = self._rel(R), self._rel(S)
+        fn = self.lib.sortmergejoin_mpsm if mpsm else self.lib.sortmergejoin_multiway
+        res = fn(C.byref(rr), C.byref(rs), C.byref(cfg))
+        if not res:
+            return None
+        return int(res.contents.totalresults)
+
+    # ---------------------------------------------------------------- device
+    @property
+    def ws(self):
+        if self._ws is None:
+            self._ws = self.lib.smj_workspace_create()
+        return self._ws
+
+    @staticmethod
+    def stream_ptr():
+        return torch.cuda.current_stream().cuda_stream
+
+    def empty(self, n: int, device="cuda"):
+        dt = torch.int32 if self.width == 8 else torch.int64
+        return torch.empty((max(n, 1), 2), dtype=dt, device=device)[:n]
+
+    def to_device(self, a: np.ndarray):
+        v = np.ascontiguousarray(a, dtype=self.dtype).view(
+            np.int32 if self.width == 8 else np.int64).reshape(-1, 2)
+        return torch.from_numpy(v.copy()).cuda()
+
+    def to_host(self, t) -> np.ndarray:
+        return t.cpu().numpy().reshape(-1).view(self.dtype).copy()
+
+    def dev_gen_pk(self, out, first, total, seed, with_payload=True):
+        self.lib.smj_dev_gen_pk(out.data_ptr(), out.shape[0], first, total, seed,
+                                int(with_payload), self.stream_ptr())
+
+    def dev_gen_fk(self, out, first, total, maxid, seed):
+        self.lib.smj_dev_gen_fk(out.data_ptr(), out.shape[0], first, total, maxid,
+                                seed, self.stream_ptr())
+
+    def dev_gen_zipf(self, out, first, maxid, theta, seed):
+        self.lib.smj_dev_gen_zipf(self.ws, out.data_ptr(), out.shape[0], first, maxid,
+                                  theta, seed, self.stream_ptr())
+
+    def dev_sort(self, inp, out):
+        self.lib.smj_dev_sort(self.ws, inp.data_ptr(), inp.shape[0], out.data_ptr(),
+                              self.stream_ptr())
+
+    def dev_partition(self, inp, out, nbits, shift, padded, hist, off):
+        self.lib.smj_dev_partition(self.ws, inp.data_ptr(), inp.shape[0], out.data_ptr(),
+                                   nbits, shift, int(padded), hist.data_ptr(),
+                                   off.data_ptr(), self.stream_ptr())
+
+    def dev_merge2(self, a, b, out):
+        self.lib.smj_dev_merge2(a.data_ptr(), a.shape[0], b.data_ptr(), b.shape[0],
+                                out.data_ptr(), self.stream_ptr())
+
+    def dev_merge_join_count(self, r, s, count):
+        self.lib.smj_dev_merge_join_count(r.data_ptr(), r.shape[0], s.data_ptr(),
+                                          s.shape[0], count.data_ptr(), self.stream_ptr())
+
+    def dev_join(self, R, S, sortedR, sortedS, count, fanout_bits=10,
+                 key_min=1, key_max=0):
+        self.lib.smj_dev_join(self.ws, R.data_ptr(), R.shape[0], S.data_ptr(),
+                              S.shape[0], sortedR.data_ptr(), sortedS.data_ptr(),
+                              fanout_bits, key_min, key_max, count.data_ptr(),
+                              self.stream_ptr())
+
+    def dev_partition_range(self, inp, out, nbits, key_min, key_max, hist):
+        self.lib.smj_dev_partition_range(self.ws, inp.data_ptr(), inp.shape[0],
+                                         out.data_ptr(), nbits, key_min, key_max,
+                                         hist.data_ptr(), self.stream_ptr())
+
+    def trace(self, on: bool):
+        self.lib.smj_trace_enable(self.ws, int(on))
+        self.lib.smj_trace_reset(self.ws)
+
+    def trace_read(self):
+        """{kernel name: (total ms, launches)} since the last trace(True)."""
+        buf = C.create_string_buffer(4096)
+        ms = (C.c_float * 64)()
+        cnt = (C.c_int * 64)()
+        k = self.lib.smj_trace_read(self.ws, buf, 4096, ms, cnt, 64)
+        names = buf.value.decode().split("\n")
+        return {names[i]: (ms[i], cnt[i]) for i in range(k)}
+
+    def join_phase_ms(self):
+        a = (C.c_float * 5)()
+        self.lib.smj_join_phase_ms(self.ws, a)
+        return list(a)
+
+
+_LIBS: dict[int, Library] = {}
+
+
+def load(width: int = 16) -> Library:
+    if width not in _LIBS:
+        _LIBS[width] = Library(width)
+    return _LIBS[width]

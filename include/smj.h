@@ -1,0 +1,337 @@
+/*
+ * smj.h -- C ABI of the MI355X sort-merge-join library (libsmj_hip*.so).
+ *
+ * This header is the drop-in boundary for the m-way sort-merge-join hot path of
+ * sdecoder/AVX-sort-merge-joins.  Every entry point below keeps the name,
+ * argument meaning, pointer-swap conventions and data layout of the reference
+ * function it replaces (cited as reference-path:line), so the reference's own
+ * drivers (bench_sort, bench_partitioning, bench_multiwaymerge, tputbench,
+ * sortmergejoins) and check_* tests compile against include/compat/ and link
+ * against this library instead of the AVX objects.
+ *
+ * Tuple width is a compile-time choice, exactly like the reference
+ * (configure --enable-key8B -> -DKEY_8B, src/types.h:23-29):
+ *   default : 8-byte tuples  {int32 payload; int32 key}  -> libsmj_hip.so
+ *   KEY_8B  : 16-byte tuples {int64 payload; int64 key}  -> libsmj_hip_k8.so
+ *
+ * Pointers handed to the reference-named functions may be host memory (the
+ * library stages them through HBM and writes results back to the same host
+ * addresses/layout) or device memory from hipMalloc (work stays in HBM, no
+ * copies).  The smj_dev_* functions are the asynchronous device-resident form
+ * used by bench.py: device pointers only, explicit HIP stream, no host sync.
+ *
+ * Order of the sorted output (the parity contract):
+ *   8-byte tuples : ascending signed-int64 order of the packed word
+ *                   (key << 32 | (uint32)payload) == what the AVX path yields
+ *                   for keys in the generators' domain (src/avxsort/avxcommon.h).
+ *   16-byte tuples: ascending (key, payload), both signed int64 == the
+ *                   reference scalar path (key-only std::sort,
+ *                   src/scalarsort/scalarsort.c:41-50) with equal-key runs
+ *                   canonicalised by payload.
+ *
+ * Errors: like the reference (no error codes), a HIP failure prints a message
+ * and aborts; the library never falls back to a CPU implementation.
+ */
+#ifndef SMJ_H
+#define SMJ_H
+
+#include <stdint.h>
+#include <stddef.h>
+#include <inttypes.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------------ */
+/* Data ABI (reference src/types.h:51-98). Layout is byte-identical.        */
+/* ------------------------------------------------------------------------ */
+#ifdef KEY_8B
+typedef int64_t intkey_t;   /* 16-byte tuples */
+typedef int64_t value_t;
+#else
+typedef int32_t intkey_t;   /* 8-byte tuples (reference default) */
+typedef int32_t value_t;
+#endif
+
+typedef struct tuple_t        tuple_t;
+typedef struct relation_t     relation_t;
+typedef struct result_t       result_t;
+typedef struct threadresult_t threadresult_t;
+typedef struct joinconfig_t   joinconfig_t;
+
+/* payload first, then key: the reference packs an 8-byte tuple into one
+ * little-endian word whose high half is the key (src/types.h:51-54). */
+struct tuple_t {
+    value_t  payload;
+    intkey_t key;
+};
+
+struct relation_t {
+    tuple_t * tuples;
+    uint64_t  num_tuples;
+};
+
+struct threadresult_t {
+    int64_t  nresults;
+    void *   results;
+    uint32_t threadid;
+};
+
+struct result_t {
+    int64_t          totalresults;
+    threadresult_t * resultlist;
+    int              nthreads;
+};
+
+enum numa_strategy_t { RANDOM, RING, NEXT };
+
+struct joinconfig_t {
+    int NTHREADS;
+    int PARTFANOUT;
+    int SCALARSORT;
+    int SCALARMERGE;
+    int MWAYMERGEBUFFERSIZE;
+    enum numa_strategy_t NUMASTRATEGY;
+};
+
+/* ------------------------------------------------------------------------ */
+/* Compile-time parameters (reference src/params.h:17-72).                  */
+/* ------------------------------------------------------------------------ */
+#ifndef NRADIXBITS_DEFAULT
+#define NRADIXBITS_DEFAULT 7
+#endif
+#ifndef PARTFANOUT_DEFAULT
+#define PARTFANOUT_DEFAULT (1 << NRADIXBITS_DEFAULT)
+#endif
+#ifndef CACHE_LINE_SIZE
+#define CACHE_LINE_SIZE 64
+#endif
+#ifndef L2_CACHE_SIZE
+#define L2_CACHE_SIZE (256 * 1024)
+#endif
+#ifndef L3_CACHE_SIZE
+#define L3_CACHE_SIZE (20 * 1024 * 1024)
+#endif
+#ifndef MWAY_MERGE_BUFFER_SIZE_DEFAULT
+#define MWAY_MERGE_BUFFER_SIZE_DEFAULT L3_CACHE_SIZE
+#endif
+/* one cache line of padding per partition (params.h:47) */
+#ifndef CACHELINEPADDING
+#define CACHELINEPADDING(FANOUT) ((FANOUT) * CACHE_LINE_SIZE / sizeof(tuple_t))
+#endif
+/* tail padding callers allocate behind R, S and temporaries (params.h:56) */
+#ifndef RELATION_PADDING
+#define RELATION_PADDING(NTHR, FANOUT) \
+    ((NTHR) * CACHELINEPADDING(FANOUT) * sizeof(tuple_t))
+#endif
+#define TUPLESPERCACHELINE (CACHE_LINE_SIZE / sizeof(tuple_t))
+#define ALIGN_NUMTUPLES(N) \
+    (((N) + TUPLESPERCACHELINE - 1) & ~(TUPLESPERCACHELINE - 1))
+
+/* ------------------------------------------------------------------------ */
+/* Radix partitioning (reference src/partition/partition.h:57-120).          */
+/* Partition index of a tuple: ((key - 1) & (((1<<nbits)-1) << shift))      */
+/*   >> shift (partition.c:29). Output is a stable scatter.                  */
+/* ------------------------------------------------------------------------ */
+
+/* partition.c:301-327 -- naive stable layout, partitions back to back. */
+void partition_relation(relation_t ** partitions, relation_t * input,
+                        relation_t * output, int radixbits, int shiftbits);
+
+/* partition.c:329-354 -- stable scatter, every partition starts on a 64-byte
+ * boundary (offsets advance by ALIGN_NUMTUPLES(count)). */
+void partition_relation_optimized(relation_t ** partitions, relation_t * input,
+                                  relation_t * output, uint32_t nbits,
+                                  uint32_t shiftbits);
+
+/* partition.c:356-385 -- same output as the optimized variant. */
+void partition_relation_optimized_V2(relation_t ** partitions,
+                                     relation_t * input, relation_t * output,
+                                     uint32_t nbits, uint32_t shiftbits);
+
+/* partition.c:422-436 -- histogram pass + plain copy (bandwidth probe). */
+void histogram_memcpy_bench(relation_t ** partitions, relation_t * input,
+                            relation_t * output, uint32_t nbits);
+
+/* ------------------------------------------------------------------------ */
+/* Sorting (reference src/avxsort/avxsort.h:35-57,                           */
+/* src/avxsort/avxsort_multiway.h:35-55, src/scalarsort/scalarsort.h).       */
+/* Result convention (avxsort.c:117-118,224-225): on return *outputptr       */
+/* points at the sorted items, *inputptr at the other buffer; both buffers   */
+/* may be clobbered.                                                         */
+/* ------------------------------------------------------------------------ */
+void avxsort_tuples(tuple_t ** inputptr, tuple_t ** outputptr, uint64_t nitems);
+void avxsort_int64(int64_t ** inputptr, int64_t ** outputptr, uint64_t nitems);
+/* avxsort.c:247-250 is an empty stub in the reference; here it sorts. */
+void avxsort_int32(int32_t ** inputptr, int32_t ** outputptr, uint64_t nitems);
+void avxsortmultiway_tuples(tuple_t ** inputptr, tuple_t ** outputptr,
+                            uint64_t nitems);
+void avxsortmultiway_int64(int64_t ** inputptr, int64_t ** outputptr,
+                           uint64_t nitems);
+/* scalarsort.c:41-50 sorts in place and swaps the pointers. */
+void scalarsort_tuples(tuple_t ** inputptr, tuple_t ** outputptr,
+                       uint64_t nitems);
+void scalarsort_int64(int64_t ** inputptr, int64_t ** outputptr,
+                      uint64_t nitems);
+void scalarsort_int32(int32_t ** inputptr, int32_t ** outputptr,
+                      uint64_t nitems);
+
+/* ------------------------------------------------------------------------ */
+/* Merging (reference src/merge/merge.h:35-97, avx_multiwaymerge.h:33-38,    */
+/* scalar_multiwaymerge.h:31-78). Return value = tuples written.             */
+/* ------------------------------------------------------------------------ */
+uint64_t avx_merge_tuples(tuple_t * const inA, tuple_t * const inB,
+                          tuple_t * const outp, const uint64_t lenA,
+                          const uint64_t lenB);
+uint64_t avx_merge_int64(int64_t * const inA, int64_t * const inB,
+                         int64_t * const outp, const uint64_t lenA,
+                         const uint64_t lenB);
+uint64_t scalar_merge_tuples(tuple_t * const inA, tuple_t * const inB,
+                             tuple_t * const outp, const uint64_t lenA,
+                             const uint64_t lenB);
+uint64_t scalar_merge_int64(int64_t * const inA, int64_t * const inB,
+                            int64_t * const outp, const uint64_t lenA,
+                            const uint64_t lenB);
+
+/* avx_multiwaymerge.c:199-338. `fifobuffer`/`bufntuples` are accepted for
+ * ABI compatibility; the GPU merge stages run heads in LDS instead of an
+ * L3-resident FIFO tree. On return every parts[i] has been consumed:
+ * parts[i]->tuples advanced by its count and parts[i]->num_tuples == 0,
+ * as the reference leaves them (avx_multiwaymerge.c:268-272). */
+uint64_t avx_multiway_merge(tuple_t * output, relation_t ** parts,
+                            uint32_t nparts, tuple_t * fifobuffer,
+                            uint32_t bufntuples);
+uint64_t scalar_multiway_merge(tuple_t * output, relation_t ** parts,
+                               uint32_t nparts, tuple_t * fifobuffer,
+                               uint32_t bufntuples);
+uint64_t scalar_multiway_merge_modulo(tuple_t * output, relation_t ** parts,
+                                      uint32_t nparts, tuple_t * fifobuffer,
+                                      uint32_t bufntuples);
+uint64_t scalar_multiway_merge_bitand(tuple_t * output, relation_t ** parts,
+                                      uint32_t nparts, tuple_t * fifobuffer,
+                                      uint32_t bufntuples);
+
+/* ------------------------------------------------------------------------ */
+/* Joins (reference src/joins/joincommon.h:78-80,                            */
+/* src/joins/sortmergejoin_multiway.h:37-38, sortmergejoin_mpsm.h).          */
+/* ------------------------------------------------------------------------ */
+
+/* joincommon.c:239-312: number of (r, s) pairs with equal key between two
+ * sorted runs, duplicates on both sides included. `output` must be NULL
+ * (materialisation does not build in the reference either). */
+uint64_t merge_join(tuple_t * rtuples, tuple_t * stuples, const uint64_t numR,
+                    const uint64_t numS, void * output);
+
+/* sortmergejoin_multiway.c:50-61: m-way sort-merge join. Returns a malloc'd
+ * result_t (caller frees resultlist and the struct, main.c:629-632) whose
+ * totalresults is the match count; NULL for a non-power-of-2 NTHREADS as the
+ * reference does. NTHREADS only selects the reference-visible partition
+ * fan-out checks: the whole join runs on the current HIP device. */
+result_t * sortmergejoin_multiway(relation_t * relR, relation_t * relS,
+                                  joinconfig_t * joincfg);
+
+/* sortmergejoin_mpsm.c is a stub that exits in the reference; here it is the
+ * same device pipeline (one process drives one GPU; multi-GPU runs shard
+ * with smj_dev_* + an RCCL all-to-all). */
+result_t * sortmergejoin_mpsm(relation_t * relR, relation_t * relS,
+                              joinconfig_t * joincfg);
+
+/* ------------------------------------------------------------------------ */
+/* Device-resident asynchronous API (no reference counterpart: this is the   */
+/* form a GPU-aware caller binds).  All pointers are device pointers,        */
+/* `stream` is a hipStream_t (NULL = default stream).                        */
+/* ------------------------------------------------------------------------ */
+typedef void * smj_stream_t;
+
+/* Tuple width this library was built for (8 or 16). */
+int smj_tuple_bytes(void);
+/* Name of the device the library initialised, for logs. */
+const char * smj_device_name(void);
+
+/* Opaque reusable scratch (device memory).  One per stream/thread. */
+typedef struct smj_workspace smj_workspace;
+smj_workspace * smj_workspace_create(void);
+void smj_workspace_destroy(smj_workspace * ws);
+
+/* Stable radix partition, the device form of partition_relation*.
+ * padded != 0 -> partition_relation_optimized layout.
+ * hist_out / off_out (device, int64[1<<nbits]) receive per-partition counts
+ * and start offsets in tuples. */
+void smj_dev_partition(smj_workspace * ws, const tuple_t * in, uint64_t n,
+                       tuple_t * out, uint32_t nbits, uint32_t shiftbits,
+                       int padded, int64_t * hist_out, int64_t * off_out,
+                       smj_stream_t stream);
+
+/* Full sort of n tuples into `out` (may equal `in`). */
+void smj_dev_sort(smj_workspace * ws, const tuple_t * in, uint64_t n,
+                  tuple_t * out, smj_stream_t stream);
+
+/* Merge two sorted runs. */
+void smj_dev_merge2(const tuple_t * a, uint64_t na, const tuple_t * b,
+                    uint64_t nb, tuple_t * out, smj_stream_t stream);
+
+/* k-way merge of sorted device runs whose pointers/lengths are host arrays. */
+void smj_dev_multiway_merge_host(smj_workspace * ws,
+                                 const tuple_t * const * runs,
+                                 const uint64_t * lens, uint32_t k,
+                                 tuple_t * out, smj_stream_t stream);
+
+/* Merge-join count of two sorted runs; result is ADDED to *count_dev. */
+void smj_dev_merge_join_count(const tuple_t * r, uint64_t nr,
+                              const tuple_t * s, uint64_t ns,
+                              unsigned long long * count_dev,
+                              smj_stream_t stream);
+
+/* The m-way join on one device.  R and S are left untouched; sortedR/sortedS
+ * (n tuples each) receive the fully sorted relations; the match count is
+ * written to *count_dev.  key_min <= key_max is an optional hint of the key
+ * range (pass key_min > key_max to sample it on the device).  Asynchronous
+ * except for one stream synchronisation that checks for skewed sub-buckets. */
+void smj_dev_join(smj_workspace * ws, const tuple_t * R, uint64_t nR,
+                  const tuple_t * S, uint64_t nS, tuple_t * sortedR,
+                  tuple_t * sortedS, uint32_t fanout_bits, int64_t key_min,
+                  int64_t key_max, unsigned long long * count_dev,
+                  smj_stream_t stream);
+
+/* Phase timings (ms) of the last smj_dev_join on this workspace, from HIP
+ * events: [0]=partition [1]=tile pass [2]=bucket sort+join [3]=skew path
+ * [4]=total. */
+void smj_join_phase_ms(smj_workspace * ws, float * ms5);
+
+/* Deterministic synthetic relations generated in HBM.
+ * pk  : keys 1..total, each once (keyed bijection of the global index),
+ *       payload 5 + global index (or 0 when with_payload == 0, as
+ *       create_relation_pk leaves it);
+ * fk  : keys perm(i) % maxid + 1 (uniform, |S| == maxid -> a permutation);
+ * zipf: keys Zipf(theta) over 1..maxid, hot ranks spread by a bijection,
+ *       payload 0.  `first` = global index of this shard's first tuple. */
+void smj_dev_gen_pk(tuple_t * out, uint64_t n, uint64_t first, uint64_t total,
+                    uint64_t seed, int with_payload, smj_stream_t stream);
+void smj_dev_gen_fk(tuple_t * out, uint64_t n, uint64_t first, uint64_t total,
+                    uint64_t maxid, uint64_t seed, smj_stream_t stream);
+void smj_dev_gen_zipf(smj_workspace * ws, tuple_t * out, uint64_t n,
+                      uint64_t first, uint64_t maxid, double theta,
+                      uint64_t seed, smj_stream_t stream);
+
+void smj_dev_synchronize(smj_stream_t stream);
+
+/* Multi-GPU building block: stable partition of a device relation into
+ * 2^nbits key ranges of [key_min, key_max] (monotone digits, unpadded), so a
+ * caller can hand contiguous partition ranges to their owner GPU with one
+ * all-to-all (bench.py does this over RCCL).  hist_out: device int64[2^nbits]. */
+void smj_dev_partition_range(smj_workspace * ws, const tuple_t * in, uint64_t n,
+                             tuple_t * out, uint32_t nbits, int64_t key_min,
+                             int64_t key_max, int64_t * hist_out,
+                             smj_stream_t stream);
+
+/* Per-kernel HIP-event trace of the join pipeline (bench.py roofline). */
+void smj_trace_enable(smj_workspace * ws, int on);
+void smj_trace_reset(smj_workspace * ws);
+int smj_trace_read(smj_workspace * ws, char * names, int cap, float * ms_sum,
+                   int * launches, int max);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SMJ_H */

@@ -1,0 +1,291 @@
+/*
+ * smj_oracle.c -- CPU restatement of the reference's m-way sort-merge-join
+ * path, used ONLY as test infrastructure (tests/, __graft_entry__.smoke(),
+ * bench.py's cpu_baseline leg).  The product (libsmj_hip*.so) never links,
+ * loads or calls this file.
+ *
+ * Every function cites the reference function it restates
+ * (paths relative to sdecoder/AVX-sort-merge-joins).  Parity is pinned by the
+ * golden vectors in tests/golden/ that tests/golden/make_golden.py produced
+ * from the reference itself (compiled by oracle/build_ref.sh), see
+ * tests/test_oracle.py.
+ *
+ * Compiled twice: default (8-byte tuples) and -DKEY_8B (16-byte tuples),
+ * into oracle/liboracle8.so and oracle/liboracle16.so.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#ifdef KEY_8B
+typedef int64_t intkey_t;
+typedef int64_t value_t;
+#else
+typedef int32_t intkey_t;
+typedef int32_t value_t;
+#endif
+
+typedef struct {
+    value_t payload;
+    intkey_t key;
+} tuple_t;
+
+#define TPL ((int64_t)(64 / sizeof(tuple_t)))
+#define ALIGN_N(n) (((n) + TPL - 1) & ~(TPL - 1))
+
+int orc_tuple_bytes(void) { return (int)sizeof(tuple_t); }
+
+/* ---------------------------------------------------------------------- */
+/* generators: src/datagen/generator.c, src/datagen/genzipf.c              */
+/* ---------------------------------------------------------------------- */
+
+/* generator.c:29-35 seed_generator */
+void orc_seed(unsigned int seed) { srand(seed); }
+
+/* generator.c:22 RAND_RANGE(N) */
+static double rand_range(double n) {
+    return (double)rand() / ((double)RAND_MAX + 1) * n;
+}
+
+/* generator.c:54-64 knuth_shuffle: swaps keys only */
+static void knuth_shuffle(tuple_t *t, int64_t n) {
+    for (int i = (int)n - 1; i > 0; i--) {
+        int64_t j = (int64_t)rand_range(i);
+        intkey_t tmp = t[i].key;
+        t[i].key = t[j].key;
+        t[j].key = tmp;
+    }
+}
+
+/* generator.c:233-252 create_relation_pk -> random_unique_gen (:83-93):
+ * keys 1..n then Knuth shuffle; the payload is not written. */
+void orc_create_relation_pk(tuple_t *t, int64_t n) {
+    for (int64_t i = 0; i < n; i++) t[i].key = (intkey_t)(i + 1);
+    knuth_shuffle(t, n);
+}
+
+/* generator.c:125-178 random_unique_gen_thread with one thread, but with the
+ * glibc rand() Knuth shuffle of create_relation_pk instead of the time-seeded
+ * nrand48 one (the only non-deterministic part): keys firstkey.. wrapping at
+ * maxid, payload 5 + i. */
+void orc_create_relation_mway(tuple_t *t, int64_t n, int64_t maxid) {
+    int64_t firstkey = 1 % maxid;
+    for (int64_t i = 0; i < n; i++) {
+        t[i].key = (intkey_t)firstkey;
+        t[i].payload = (value_t)(5 + i);
+        if (firstkey == maxid) firstkey = 0;
+        firstkey++;
+    }
+    knuth_shuffle(t, n);
+}
+
+/* generator.c:112-120 avoid_NaN on the first 8 bytes of the tuple */
+static void avoid_nan(void *p) {
+    int64_t v;
+    memcpy(&v, p, 8);
+    const int64_t expmask = (int64_t)0x7FF << 52;
+    if ((v & expmask) == expmask) {
+        v &= ~((int64_t)1 << 52);
+        memcpy(p, &v, 8);
+    }
+}
+
+/* generator.c:220-231 random_gen (create_relation_nonunique :490-505) */
+void orc_create_relation_nonunique(tuple_t *t, int64_t n, int64_t maxid) {
+    for (int64_t i = 0; i < n; i++) {
+        t[i].key = (intkey_t)rand_range((double)maxid);
+        t[i].payload = (value_t)(n - i);
+        avoid_nan(&t[i]);
+    }
+}
+
+/* generator.c:408-444 create_relation_fk */
+void orc_create_relation_fk(tuple_t *t, int64_t n, int64_t maxid) {
+    int32_t iters = (int32_t)(n / maxid);
+    for (int32_t i = 0; i < iters; i++)
+        orc_create_relation_pk(t + maxid * i, maxid);
+    int64_t rem = n % maxid;
+    if (rem > 0) orc_create_relation_pk(t + maxid * iters, rem);
+}
+
+/* genzipf.c:28-53 gen_alphabet */
+static uint32_t *gen_alphabet(unsigned int size) {
+    uint32_t *a = (uint32_t *)malloc(size * sizeof(uint32_t));
+    for (unsigned int i = 0; i < size; i++) a[i] = i + 1;
+    for (unsigned int i = size - 1; i > 0; i--) {
+        unsigned int k = (unsigned long)i * rand() / RAND_MAX;
+        uint32_t tmp = a[i];
+        a[i] = a[k];
+        a[k] = tmp;
+    }
+    return a;
+}
+
+/* genzipf.c:60-92 gen_zipf_lut */
+static double *gen_zipf_lut(double theta, unsigned int size) {
+    double *lut = (double *)malloc(size * sizeof(double));
+    double scale = 0.0, sum = 0.0;
+    for (unsigned int i = 1; i <= size; i++) scale += 1.0 / pow(i, theta);
+    for (unsigned int i = 1; i <= size; i++) {
+        sum += 1.0 / pow(i, theta);
+        lut[i - 1] = sum / scale;
+    }
+    return lut;
+}
+
+/* genzipf.c:97-159 gen_zipf (create_relation_zipf generator.c:517-534);
+ * only the key is written, the payload is left as the caller had it. */
+void orc_create_relation_zipf(tuple_t *t, int64_t n, int64_t maxid,
+                              double theta) {
+    uint32_t *alpha = gen_alphabet((unsigned int)maxid);
+    double *lut = gen_zipf_lut(theta, (unsigned int)maxid);
+    for (unsigned int i = 0; i < (unsigned int)n; i++) {
+        double r = ((double)rand()) / RAND_MAX;
+        unsigned int left = 0, right = (unsigned int)maxid - 1, m, pos;
+        if (lut[0] >= r) {
+            pos = 0;
+        } else {
+            while (right - left > 1) {
+                m = (left + right) / 2;
+                if (lut[m] < r) left = m; else right = m;
+            }
+            pos = right;
+        }
+        t[i].key = (intkey_t)alpha[pos];
+    }
+    free(lut);
+    free(alpha);
+}
+
+/* ---------------------------------------------------------------------- */
+/* partitioning: src/partition/partition.c                                 */
+/* ---------------------------------------------------------------------- */
+
+/* partition.c:29 HASH_BIT_MODULO */
+static uint32_t part_idx(intkey_t k, uint32_t mask, uint32_t shift) {
+    return (uint32_t)(((uint64_t)((int64_t)k - 1) & (uint64_t)mask) >> shift);
+}
+
+/* partition.c:93-149 radix_cluster (stable), with the offsets either packed
+ * (partition_relation, :301-327) or advanced by ALIGN_NUMTUPLES
+ * (radix_cluster_optimized :152-219 / partition_relation_optimized :329-354,
+ * whose write-combining scatter is stable too).  Writes counts/offsets (in
+ * tuples) of every partition. */
+void orc_partition(const tuple_t *in, int64_t n, tuple_t *out, int nbits,
+                   int shift, int padded, int64_t *cnt, int64_t *off) {
+    const uint32_t fan = 1u << nbits;
+    const uint32_t mask = (uint32_t)((((uint64_t)1 << nbits) - 1) << shift);
+    int64_t *dst = (int64_t *)malloc(fan * sizeof(int64_t));
+    for (uint32_t i = 0; i < fan; i++) cnt[i] = 0;
+    for (int64_t i = 0; i < n; i++) cnt[part_idx(in[i].key, mask, shift)]++;
+    int64_t o = 0;
+    for (uint32_t i = 0; i < fan; i++) {
+        off[i] = o;
+        dst[i] = o;
+        o += padded ? ALIGN_N(cnt[i]) : cnt[i];
+    }
+    for (int64_t i = 0; i < n; i++)
+        out[dst[part_idx(in[i].key, mask, shift)]++] = in[i];
+    free(dst);
+}
+
+/* ---------------------------------------------------------------------- */
+/* sorting / merging order                                                 */
+/* 8-byte tuples: the AVX path sorts the packed word as a 64-bit item      */
+/* (src/avxsort/avxsort.c:212-226; FP64 min/max of in-domain bit patterns  */
+/* == signed int64 order).  16-byte tuples: scalarsort's   */
+/* key-only std::sort (src/scalarsort/scalarsort.c:34-50) with equal keys  */
+/* ordered by payload (canonical tie order).                 */
+/* ---------------------------------------------------------------------- */
+static int tup_cmp(const void *a, const void *b) {
+#ifdef KEY_8B
+    const tuple_t *x = (const tuple_t *)a, *y = (const tuple_t *)b;
+    if (x->key != y->key) return x->key < y->key ? -1 : 1;
+    if (x->payload != y->payload) return x->payload < y->payload ? -1 : 1;
+    return 0;
+#else
+    int64_t x, y;
+    memcpy(&x, a, 8);
+    memcpy(&y, b, 8);
+    return x < y ? -1 : (x > y);
+#endif
+}
+
+static int tup_le(const tuple_t *a, const tuple_t *b) { return tup_cmp(a, b) <= 0; }
+
+void orc_sort_tuples(tuple_t *t, int64_t n) { qsort(t, (size_t)n, sizeof(tuple_t), tup_cmp); }
+
+static int i64_cmp(const void *a, const void *b) {
+    int64_t x = *(const int64_t *)a, y = *(const int64_t *)b;
+    return x < y ? -1 : (x > y);
+}
+void orc_sort_int64(int64_t *a, int64_t n) { qsort(a, (size_t)n, 8, i64_cmp); }
+
+/* src/merge/merge.c:67-103 scalar_merge_tuples (2-way merge) */
+uint64_t orc_merge_tuples(const tuple_t *A, const tuple_t *B, tuple_t *out,
+                          uint64_t la, uint64_t lb) {
+    uint64_t i = 0, j = 0, k = 0;
+    while (i < la && j < lb) out[k++] = tup_le(&A[i], &B[j]) ? A[i++] : B[j++];
+    while (i < la) out[k++] = A[i++];
+    while (j < lb) out[k++] = B[j++];
+    return k;
+}
+
+/* src/merge/avx_multiwaymerge.c:199-338 / scalar_multiwaymerge.c:131-260:
+ * the merge tree's output is the sorted union of the runs. */
+uint64_t orc_multiway_merge(tuple_t *out, const tuple_t *const *runs,
+                            const uint64_t *lens, uint32_t k) {
+    uint64_t *pos = (uint64_t *)calloc(k, sizeof(uint64_t));
+    uint64_t total = 0;
+    for (uint32_t r = 0; r < k; r++) total += lens[r];
+    for (uint64_t o = 0; o < total; o++) {
+        int best = -1;
+        for (uint32_t r = 0; r < k; r++) {
+            if (pos[r] >= lens[r]) continue;
+            if (best < 0 || tup_cmp(&runs[r][pos[r]], &runs[best][pos[best]]) < 0)
+                best = (int)r;
+        }
+        out[o] = runs[best][pos[best]++];
+    }
+    free(pos);
+    return total;
+}
+
+/* src/joins/joincommon.c:239-312 merge_join (count, dup x dup included) */
+uint64_t orc_merge_join(const tuple_t *R, const tuple_t *S, uint64_t nR,
+                        uint64_t nS) {
+    uint64_t i = 0, j = 0, matches = 0;
+    while (i < nR && j < nS) {
+        if (R[i].key < S[j].key) {
+            i++;
+        } else if (R[i].key > S[j].key) {
+            j++;
+        } else {
+            uint64_t jj;
+            do {
+                jj = j;
+                do {
+                    matches++;
+                    jj++;
+                } while (jj < nS && R[i].key == S[jj].key);
+                i++;
+            } while (i < nR && R[i].key == S[j].key);
+            j = jj;
+        }
+    }
+    return matches;
+}
+
+/* src/joins/sortmergejoin_multiway.c:129-328 with one thread: partition,
+ * sort every partition, join partition pairs.  Because the count does not
+ * depend on the partitioning, this sorts the whole relations (the sorted
+ * outputs are returned for parity of the sorted relations). */
+uint64_t orc_sortmergejoin(const tuple_t *R, const tuple_t *S, uint64_t nR,
+                           uint64_t nS, tuple_t *sortedR, tuple_t *sortedS) {
+    memcpy(sortedR, R, nR * sizeof(tuple_t));
+    memcpy(sortedS, S, nS * sizeof(tuple_t));
+    orc_sort_tuples(sortedR, (int64_t)nR);
+    orc_sort_tuples(sortedS, (int64_t)nS);
+    return orc_merge_join(sortedR, sortedS, nR, nS);
+}

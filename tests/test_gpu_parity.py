@@ -1,0 +1,236 @@
+"""GPU parity of the HIP path against the CPU oracle (bit-exact).
+
+Mirrors the reference's own Check suites (tests/check_partitioning.c,
+check_avxsort.c, check_merge.c, check_scalarsort.c) but with exact
+comparisons instead of sortedness-only asserts, on seeded inputs from the
+reference generators (restated in oracle/smj_oracle.c and pinned by
+tests/golden/), plus the edge cases those suites never hit: empty and tiny
+inputs, ragged sizes, negative/full-range keys, heavy duplicates (Zipf), wide
+digits.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def rand_tuples(width, n, seed, lo=None, hi=None):
+    rng = np.random.default_rng(seed)
+    dt = np.dtype([("payload", "<i4"), ("key", "<i4")]) if width == 8 else \
+        np.dtype([("payload", "<i8"), ("key", "<i8")])
+    t = np.zeros(n, dt)
+    if width == 8:
+        lo = -(1 << 31) if lo is None else lo
+        hi = (1 << 31) - 1 if hi is None else hi
+        t["key"] = rng.integers(lo, hi, n, dtype=np.int64)
+        t["payload"] = rng.integers(-(1 << 31), (1 << 31) - 1, n, dtype=np.int64)
+    else:
+        lo = -(1 << 62) if lo is None else lo
+        hi = (1 << 62) if hi is None else hi
+        t["key"] = rng.integers(lo, hi, n, dtype=np.int64)
+        t["payload"] = rng.integers(-(1 << 62), 1 << 62, n, dtype=np.int64)
+    return t
+
+
+# ------------------------------------------------------------- partitioning
+PART_CASES = [(0, 4, 0), (1, 4, 0), (7, 2, 0), (1000, 4, 0), (20000, 10, 0),
+              (100003, 7, 3), (300001, 10, 17), (65536, 12, 0),
+              (200000, 13, 0), (70000, 16, 0)]
+
+
+@pytest.mark.parametrize("n,nbits,shift", PART_CASES)
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_partition_matches_oracle(libs, oracles, width, n, nbits, shift, variant):
+    orc, lib = oracles[width], libs[width]
+    orc.seed(12345 + n)
+    t = orc.create_relation_pk(n)
+    t["payload"] = np.arange(n) + 5
+    out, cnt, off = lib.partition(t, nbits, shift, variant)
+    eout, ecnt, eoff = orc.partition(t, nbits, shift, padded=variant != 0)
+    np.testing.assert_array_equal(cnt, ecnt)
+    np.testing.assert_array_equal(off, eoff)
+    if variant:
+        assert np.all((off * width) % 64 == 0)  # check_partitioning.c:72-76
+    for i in range(1 << nbits):
+        a = out[off[i]:off[i] + cnt[i]]
+        b = eout[eoff[i]:eoff[i] + ecnt[i]]
+        assert np.array_equal(a, b), f"partition {i} differs"
+
+
+def test_partition_random_keys(libs, oracles, width):
+    orc, lib = oracles[width], libs[width]
+    t = rand_tuples(width, 123457, 7)
+    out, cnt, off = lib.partition(t, 10, 5, 1)
+    eout, ecnt, eoff = orc.partition(t, 10, 5, padded=True)
+    np.testing.assert_array_equal(cnt, ecnt)
+    for i in range(1024):
+        assert np.array_equal(out[off[i]:off[i] + cnt[i]], eout[eoff[i]:eoff[i] + ecnt[i]])
+
+
+# ------------------------------------------------------------------ sorting
+SORT_SIZES = [0, 1, 2, 15, 16, 255, 4096, 16384, 49229, 3 * 16384 + 77, 1 << 20,
+              1000003]
+
+
+@pytest.mark.parametrize("n", SORT_SIZES)
+def test_sort_pk(libs, oracles, width, n):
+    orc, lib = oracles[width], libs[width]
+    orc.seed(12345)
+    t = orc.create_relation_pk(n)  # payload left 0 like bench_sort
+    got = lib.avxsort_tuples(t)
+    assert np.array_equal(got, orc.sort(t))
+
+
+@pytest.mark.parametrize("n", [100, 5000, 262145, 1 << 21])
+@pytest.mark.parametrize("kind", ["nonunique", "random", "narrow"])
+def test_sort_other_inputs(libs, oracles, width, n, kind):
+    orc, lib = oracles[width], libs[width]
+    if kind == "nonunique":
+        orc.seed(54321)
+        t = orc.create_relation_nonunique(n, max(1, n // 3))
+    elif kind == "random":
+        t = rand_tuples(width, n, n)
+    else:  # tiny key range, many payload ties to break
+        t = rand_tuples(width, n, n + 1, 0, 40)
+    for fn in ("avxsort_tuples", "avxsortmultiway_tuples", "scalarsort_tuples"):
+        got = lib.avxsort_tuples(t, fn)
+        assert np.array_equal(got, orc.sort(t)), fn
+
+
+def test_sort_zipf_skew(libs, oracles, width):
+    orc, lib = oracles[width], libs[width]
+    orc.seed(54321)
+    t = orc.create_relation_zipf(400000, 5000, 0.75)
+    t["payload"] = np.random.default_rng(3).integers(0, 1000, len(t))
+    got = lib.avxsort_tuples(t)
+    assert np.array_equal(got, orc.sort(t))
+
+
+def test_sort_int64_int32(libs, oracles, width):
+    orc, lib = oracles[width], libs[width]
+    rng = np.random.default_rng(11)
+    v = rng.integers(-(1 << 62), 1 << 62, 300001, dtype=np.int64)
+    for fn in ("avxsort_int64", "avxsortmultiway_int64", "scalarsort_int64"):
+        assert np.array_equal(lib.sort_int(v, fn), np.sort(v)), fn
+    w = rng.integers(-(1 << 31), (1 << 31) - 1, 100003, dtype=np.int64).astype(np.int32)
+    for fn in ("avxsort_int32", "scalarsort_int32"):
+        assert np.array_equal(lib.sort_int(w, fn), np.sort(w)), fn
+
+
+# ------------------------------------------------------------------ merging
+@pytest.mark.parametrize("la,lb", [(0, 0), (0, 5), (7, 0), (1, 1), (1000, 1),
+                                   (4096, 4096), (100000, 3333), (77777, 200001)])
+def test_merge2(libs, oracles, width, la, lb):
+    orc, lib = oracles[width], libs[width]
+    a = orc.sort(rand_tuples(width, la, la, 0, 5000))
+    b = orc.sort(rand_tuples(width, lb, lb + 1, 0, 5000))
+    exp = orc.merge(a, b)
+    for fn in ("avx_merge_tuples", "scalar_merge_tuples"):
+        assert np.array_equal(lib.avx_merge_tuples(a, b, fn), exp)
+
+
+@pytest.mark.parametrize("k", [1, 2, 4, 5, 64, 128])
+def test_multiway_merge(libs, oracles, width, k):
+    orc, lib = oracles[width], libs[width]
+    rng = np.random.default_rng(k)
+    runs = [orc.sort(rand_tuples(width, int(rng.integers(0, 3000)), 100 * k + i, 0, 10000))
+            for i in range(k)]
+    exp = orc.multiway_merge(runs)
+    for fn in ("avx_multiway_merge", "scalar_multiway_merge"):
+        out, n, consumed = lib.avx_multiway_merge(runs, fn)
+        assert n == len(exp)
+        assert consumed  # parts[] advanced like avx_multiwaymerge.c:268-272
+        assert np.array_equal(out, exp)
+
+
+# -------------------------------------------------------------------- joins
+def test_merge_join_dups(libs, oracles, width):
+    orc, lib = oracles[width], libs[width]
+    for seed, n in [(1, 0), (2, 1), (3, 1000), (4, 200000)]:
+        r = orc.sort(rand_tuples(width, n, seed, 0, max(1, n // 4)))
+        s = orc.sort(rand_tuples(width, n + 3, seed + 9, 0, max(1, n // 4)))
+        assert lib.merge_join(r, s) == orc.merge_join(r, s)
+
+
+JOIN_CASES = [("pk_fk", 0, 0), ("pk_fk", 1, 1), ("pk_fk", 1000, 1000),
+              ("pk_fk", 1 << 20, 1 << 20), ("pk_fk", 300000, 1200000),
+              ("nonunique", 250000, 250000), ("zipf", 200000, 400000),
+              ("random", 100000, 100000)]
+
+
+def make_join_inputs(orc, width, kind, nr, ns):
+    if kind == "pk_fk":
+        orc.seed(12345)
+        R = orc.create_relation_mway(nr, max(nr, 1))
+        orc.seed(54321)
+        S = orc.create_relation_mway(ns, max(nr, 1))
+    elif kind == "nonunique":
+        orc.seed(12345)
+        R = orc.create_relation_nonunique(nr, nr)
+        orc.seed(54321)
+        S = orc.create_relation_nonunique(ns, nr)
+    elif kind == "zipf":
+        orc.seed(12345)
+        R = orc.create_relation_mway(nr, nr)
+        orc.seed(54321)
+        S = orc.create_relation_zipf(ns, nr, 0.75)
+    else:
+        R = rand_tuples(width, nr, 5, -50000, 50000)
+        S = rand_tuples(width, ns, 6, -50000, 50000)
+    return R, S
+
+
+@pytest.mark.parametrize("kind,nr,ns", JOIN_CASES)
+def test_sortmergejoin_count(libs, oracles, width, kind, nr, ns):
+    orc, lib = oracles[width], libs[width]
+    R, S = make_join_inputs(orc, width, kind, nr, ns)
+    exp, _, _ = orc.sortmergejoin(R, S)
+    for nthr in (1, 8):
+        assert lib.sortmergejoin_multiway(R, S, nthreads=nthr) == exp
+    assert lib.sortmergejoin_multiway(R, S, nthreads=3) is None  # pow-2 check
+    assert lib.sortmergejoin_multiway(R, S, nthreads=2, mpsm=True) == exp
+
+
+@pytest.mark.parametrize("kind,nr,ns", JOIN_CASES[2:])
+def test_device_join_sorted_outputs(libs, oracles, width, kind, nr, ns):
+    import torch
+    orc, lib = oracles[width], libs[width]
+    R, S = make_join_inputs(orc, width, kind, nr, ns)
+    exp, eR, eS = orc.sortmergejoin(R, S)
+    dR, dS = lib.to_device(R), lib.to_device(S)
+    sR, sS = lib.empty(nr), lib.empty(ns)
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    lib.dev_join(dR, dS, sR, sS, cnt)
+    torch.cuda.synchronize()
+    assert int(cnt.item()) == exp
+    assert np.array_equal(lib.to_host(sR), eR)
+    assert np.array_equal(lib.to_host(sS), eS)
+    # inputs untouched
+    assert np.array_equal(lib.to_host(dR), R)
+
+
+# --------------------------------------------------------------- generators
+def test_device_generators(libs, width):
+    import torch
+    lib = libs[width]
+    n = 1 << 20
+    t = lib.empty(n)
+    lib.dev_gen_pk(t, 0, n, 12345)
+    h = lib.to_host(t)
+    assert np.array_equal(np.sort(h["key"]), np.arange(1, n + 1))
+    assert np.array_equal(h["payload"], np.arange(n) + 5)
+    # shards of one relation compose to the same relation
+    a, b = lib.empty(n // 2), lib.empty(n - n // 2)
+    lib.dev_gen_pk(a, 0, n, 12345)
+    lib.dev_gen_pk(b, n // 2, n, 12345)
+    assert np.array_equal(np.concatenate([lib.to_host(a), lib.to_host(b)]), h)
+    z = lib.empty(n)
+    lib.dev_gen_zipf(z, 0, 100000, 0.75, 54321)
+    torch.cuda.synchronize()
+    zk = lib.to_host(z)["key"]
+    assert zk.min() >= 1 and zk.max() <= 100000
+    counts = np.bincount(zk)
+    top = np.sort(counts)[::-1]
+    # Zipf(0.75): rank-1 share = 1/H(100000, 0.75)
+    H = np.sum(1.0 / np.arange(1, 100001) ** 0.75)
+    assert abs(top[0] / n - 1 / H) < 0.15 / H
