@@ -6,25 +6,25 @@
 // After the level-1 radix partition (partition.hip) every bucket b holds the
 // tuples whose key falls in one contiguous key range of the RangePlan.
 //
-//   k_tilepass   : every bucket is cut into tiles of TILE2 tuples.  A tile is
-//                  loaded into registers, counted by its level-2 digit d2 in an
-//                  LDS histogram, staged in LDS grouped by d2 and written back
-//                  linearly (fully coalesced), together with the tile's
-//                  exclusive d2 prefix (uint16 per digit).  Traffic: 2w.
-//   k_bucketpass : one workgroup per sub-bucket (b, d2).  It gathers the
-//                  sub-bucket's piece from every tile of bucket b (pieces are
-//                  contiguous runs, read with 64 consecutive lanes), counting-
-//                  sorts the pieces in LDS by the level-3 digit, fixes the few
-//                  equal-digit runs with an in-LDS insertion sort on the full
-//                  (key,payload) order, writes the sorted sub-bucket to its
-//                  final position (coalesced), and -- for a join -- counts the
-//                  matching (r, s) pairs of the R and S sub-buckets that are
-//                  both resident in LDS.  Traffic: 2w, the join reads nothing.
+//   k_tilepass : every bucket is cut into tiles of TILE2 tuples.  A tile is
+//                loaded into registers, counted by its level-2 digit d2 in an
+//                LDS histogram, staged in LDS grouped by d2 and written back in
+//                place, linearly (fully coalesced), together with the tile's
+//                exclusive d2 prefix (uint16 per digit).  Traffic: 2w.
+//   k_subwave  : ONE WAVE per sub-bucket (b, d2) at a time -- no workgroup
+//                barriers on the critical path, eight independent sub-buckets
+//                in flight per workgroup.  The wave gathers the sub-bucket's
+//                piece from every tile of bucket b (contiguous runs, read by
+//                consecutive lanes), counting-sorts them in its private LDS
+//                slice by the level-3 digit, fixes equal-digit runs with an
+//                insertion sort on the full (key, payload) order, writes the
+//                sorted sub-bucket to its final position, and -- for a join --
+//                counts the matching pairs of the R and S sub-buckets that are
+//                both resident in LDS.  Traffic: 2w; the join reads nothing.
 //
-// Sub-buckets that do not fit the LDS capacity or hold long runs of equal
-// digits (heavy skew, e.g. Zipf hot keys) are queued and sorted by the
-// segmented merge sort (mergesort.hip); their join count uses the merge-path
-// join-count kernel.
+// Sub-buckets that do not fit the per-wave LDS capacity, or that hold long
+// runs of equal digits (skew, e.g. Zipf hot keys), are queued and finished by
+// the segmented merge sort (mergesort.hip) and the merge-join count kernel.
 #include "smj_common.hpp"
 #include "smj_internal.hpp"
 
@@ -34,23 +34,25 @@ constexpr int TP_THREADS = 256;
 constexpr int TP_ITEMS = 16;
 constexpr int TILE2 = TP_THREADS * TP_ITEMS;  // 4096 tuples per tile
 
-constexpr int BP_THREADS = 256;
+constexpr int SW_WAVES = 8;  // waves per workgroup, one sub-bucket each
+constexpr int SW_THREADS = SW_WAVES * 64;
 #ifdef KEY_8B
-constexpr int BP_CAP = 1024;  // tuples per relation per sub-bucket in LDS
+constexpr int SW_CAP = 512;  // tuples per relation per sub-bucket
 #else
-constexpr int BP_CAP = 2048;
+constexpr int SW_CAP = 1024;
 #endif
-constexpr int BP_ITEMS = BP_CAP / BP_THREADS;
-constexpr int BP_D3MAX = 10;
-constexpr int BP_PMAX = 512;   // max tiles (pieces) per bucket in the LDS path
-constexpr int BP_RUNMAX = 48;  // longest equal-digit run fixed in LDS
+constexpr int SW_ITEMS = SW_CAP / 64;
+constexpr int SW_D3MAX = 8;  // level-3 bins per wave (256)
+constexpr int SW_NB3 = 1 << SW_D3MAX;
+constexpr int SW_PMAX = 64;    // tiles per bucket handled by the wave path
+constexpr int SW_RUNMAX = 32;  // longest equal-digit run fixed in LDS
 
 struct TileTable {
     uint64_t* off;     // tile start in `part`
     uint32_t* len;     // tile length
     uint32_t* bucket;  // owning bucket
     uint32_t* btile0;  // first tile of every bucket (nbuckets + 1)
-    uint16_t* pref;    // [tile][1<<D2] exclusive prefix
+    uint16_t* pref;    // [tile][nb2] exclusive prefix
     uint32_t* ntiles;  // device scalar
 };
 
@@ -166,13 +168,7 @@ k_tilepass(const Tup* __restrict__ part, Tup* __restrict__ tmp, TileTable tt,
 }
 
 // ---------------------------------------------------------------------------
-struct Piece {
-    uint64_t src;
-    uint32_t len;
-    uint32_t dst;
-};
-
-struct BucketPassArgs {
+struct SubWaveArgs {
     const Tup* tmp[2];
     Tup* out[2];
     const uint64_t* bstart[2];
@@ -180,34 +176,63 @@ struct BucketPassArgs {
     int nrel;
     const RangePlan* plan_dev;
     unsigned long long* count_dev;
-    uint32_t nb2;  // level-2 table stride (>= 1 << plan.D2)
+    uint32_t nb2;   // level-2 table stride (>= 1 << plan.D2)
+    uint32_t nsub;  // nbuckets * nb2
+    uint32_t spw;   // sub-buckets per wave
     OvfEntry* ovf;
     uint32_t* novf;
     uint32_t ovf_cap;
 };
 
-// LDS layout (bytes):
-//   B[2]    : 2 * BP_CAP Tups
-//   h[2]    : 2 * 2^D3MAX uint32  (bin starts after scan)
-//   fill    : 2^D3MAX uint32
-//   pieces  : BP_PMAX Piece
-//   misc    : 32 uint32
-constexpr size_t BP_LDS = 2 * BP_CAP * sizeof(Tup) +
-                          3 * (1u << BP_D3MAX) * sizeof(uint32_t) +
-                          BP_PMAX * sizeof(Piece) + 32 * sizeof(uint32_t);
+// per-wave LDS slice (< 20 KiB: eight waves fill one CU's 160 KiB)
+struct WaveLDS {
+    Tup B[2][SW_CAP];
+    uint32_t h[2][SW_NB3];  // bin starts after the scan
+    uint32_t fill[SW_NB3];
+    uint32_t psrc[SW_PMAX];  // piece start, relative to the bucket start
+    uint32_t pdst[SW_PMAX];  // piece position inside the sub-bucket
+};
+static_assert(sizeof(WaveLDS) * SW_WAVES <= 160 * 1024, "LDS budget");
 
-__device__ __forceinline__ uint32_t piece_of(const Piece* pc, uint32_t np,
-                                             uint32_t i) {
-    // last piece with dst <= i (pieces with len 0 share dst; pick any)
-    uint32_t lo = 0, hi = np;  // invariant: pc[lo].dst <= i
+// order this wave's LDS accesses (LDS executes one wave's instructions in
+// order; the fences stop the compiler from moving accesses across)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    return x;
+}
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        uint32_t y = __shfl_xor(x, o, 64);
+        x = y > x ? y : x;
+    }
+    return x;
+}
+
+// last piece with pdst <= i: with non-decreasing pdst this is the piece that
+// holds position i (empty pieces after it start beyond i)
+__device__ __forceinline__ uint32_t wave_piece_of(const uint32_t* pdst,
+                                                  uint32_t np, uint32_t i) {
+    uint32_t lo = 0, hi = np;
     while (hi - lo > 1) {
         uint32_t m = (lo + hi) >> 1;
-        if (pc[m].dst <= i) lo = m; else hi = m;
+        if (pdst[m] <= i) lo = m; else hi = m;
     }
     return lo;
 }
 
-// insertion sort of a short run in LDS
 __device__ __forceinline__ void lds_insertion_sort(Tup* a, uint32_t n) {
     for (uint32_t i = 1; i < n; i++) {
         Tup x = a[i];
@@ -220,234 +245,212 @@ __device__ __forceinline__ void lds_insertion_sort(Tup* a, uint32_t n) {
     }
 }
 
-__global__ void __launch_bounds__(BP_THREADS)
-k_bucketpass(BucketPassArgs A) {
+__global__ void __launch_bounds__(SW_THREADS)
+k_subwave(SubWaveArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    WaveLDS& L = reinterpret_cast<WaveLDS*>(lds_raw)[threadIdx.x >> 6];
     const RangePlan P = *A.plan_dev;
     const uint32_t nb2 = A.nb2;
     const uint32_t nb3 = 1u << P.D3;
-    Tup* B[2];
-    B[0] = reinterpret_cast<Tup*>(lds_raw);
-    B[1] = B[0] + BP_CAP;
-    uint32_t* h[2];
-    h[0] = reinterpret_cast<uint32_t*>(B[1] + BP_CAP);
-    h[1] = h[0] + (1u << BP_D3MAX);
-    uint32_t* fill = h[1] + (1u << BP_D3MAX);
-    Piece* pc = reinterpret_cast<Piece*>(fill + (1u << BP_D3MAX));
-    uint32_t* misc = reinterpret_cast<uint32_t*>(pc + BP_PMAX);
-    // misc[0..7] scan scratch, misc[16..] flags
+    const uint32_t d2lim = 1u << P.D2;
+    const int lane = lane_id();
+    const uint64_t bu = key_u(P.base);
+    const bool exact = (P.s3 == 0);
 
-    const uint32_t b = blockIdx.x / nb2;
-    const uint32_t d2 = blockIdx.x % nb2;
-    const int nrel = A.nrel;
+    const uint32_t wave = blockIdx.x * SW_WAVES + (threadIdx.x >> 6);
+    const uint32_t s_begin = wave * A.spw;
+    uint32_t s_end = s_begin + A.spw;
+    if (s_end > A.nsub) s_end = A.nsub;
+    unsigned long long matches = 0;
 
-    // ---- phase 1: sizes and offsets of the sub-bucket in every relation
-    uint32_t nsub[2] = {0, 0};
-    uint64_t offsub[2] = {0, 0};
-    bool ovf = false;
-    for (int r = 0; r < nrel; r++) {
-        const TileTable& tt = A.tt[r];
-        const uint32_t t0 = tt.btile0[b], t1 = tt.btile0[b + 1];
-        const uint32_t nt = t1 - t0;
-        if (nt > BP_PMAX) ovf = true;
-        uint32_t mylen = 0;
-        uint64_t mylo = 0;
-        for (uint32_t t = t0 + threadIdx.x; t < t1; t += BP_THREADS) {
-            const uint16_t* pf = tt.pref + (uint64_t)t * nb2;
-            uint32_t lo = pf[d2];
-            uint32_t hi = (d2 + 1 < nb2) ? pf[d2 + 1] : tt.len[t];
-            mylen += hi - lo;
-            mylo += lo;
-        }
-        mylen = wave_sum(mylen);
-        mylo = wave_sum(mylo);
-        if (lane_id() == 0) {
-            misc[(threadIdx.x >> 6)] = mylen;
-            reinterpret_cast<uint64_t*>(misc + 8)[threadIdx.x >> 6] = mylo;
-        }
-        __syncthreads();
-        uint32_t n = 0;
-        uint64_t o = 0;
-        for (int w = 0; w < BP_THREADS / 64; w++) {
-            n += misc[w];
-            o += reinterpret_cast<uint64_t*>(misc + 8)[w];
-        }
-        __syncthreads();
-        nsub[r] = n;
-        offsub[r] = o;
-        if (n > BP_CAP) ovf = true;
-    }
+    for (uint32_t s = s_begin; s < s_end; s++) {
+        const uint32_t b = s / nb2;
+        const uint32_t d2 = s % nb2;
+        if (d2 >= d2lim) continue;  // a table column no digit maps to
+        uint32_t nsub[2] = {0, 0};
+        uint64_t offsub[2] = {0, 0};
+        uint64_t bst[2] = {0, 0};
+        bool clamp[2] = {false, false};
+        bool ovf = false;
 
-    // ---- phase 2: gather + counting sort by d3 into B[r]
-    int maxrun = 0;
-    if (threadIdx.x == 0) misc[28] = 0;  // any key clamped by the plan?
-    __syncthreads();
-    if (!ovf) {
-        for (int r = 0; r < nrel; r++) {
+        for (int r = 0; r < A.nrel && !ovf; r++) {
+            // ---- piece table of relation r (one global round trip)
             const TileTable& tt = A.tt[r];
-            const uint32_t t0 = tt.btile0[b], t1 = tt.btile0[b + 1];
-            const uint32_t nt = t1 - t0;
-            // piece table
-            uint32_t len = 0;
+            const uint32_t t0 = tt.btile0[b];
+            const uint32_t nt = tt.btile0[b + 1] - t0;
+            bst[r] = A.bstart[r][b];
+            if (nt > SW_PMAX) {
+                ovf = true;
+                break;
+            }
+            uint32_t cnt = 0, lo = 0;
             uint64_t src = 0;
-            for (uint32_t base = 0; base < nt; base += BP_THREADS) {
-                uint32_t t = t0 + base + threadIdx.x;
-                len = 0;
-                if (base + threadIdx.x < nt) {
-                    const uint16_t* pf = tt.pref + (uint64_t)t * nb2;
-                    uint32_t lo = pf[d2];
-                    uint32_t hi = (d2 + 1 < nb2) ? pf[d2 + 1] : tt.len[t];
-                    len = hi - lo;
-                    src = tt.off[t] + lo;
-                }
-                uint32_t tot;
-                uint32_t ex = block_exclusive_scan(len, misc, &tot);
-                uint32_t prev = base == 0 ? 0 : misc[20];
-                if (base + threadIdx.x < nt) {
-                    pc[base + threadIdx.x].src = src;
-                    pc[base + threadIdx.x].len = len;
-                    pc[base + threadIdx.x].dst = prev + ex;
-                }
-                __syncthreads();
-                if (threadIdx.x == 0) misc[20] = prev + tot;
-                __syncthreads();
+            if ((uint32_t)lane < nt) {
+                const uint32_t t = t0 + lane;
+                const uint16_t* pf = tt.pref + (uint64_t)t * nb2;
+                lo = pf[d2];
+                const uint32_t hi = (d2 + 1 < nb2) ? pf[d2 + 1] : tt.len[t];
+                cnt = hi - lo;
+                src = tt.off[t] - bst[r] + lo;
             }
-            for (uint32_t d = threadIdx.x; d < nb3; d += BP_THREADS) h[r][d] = 0;
-            __syncthreads();
-            const uint32_t n = nsub[r];
-            const uint32_t np = nt;
-            Tup v[BP_ITEMS];
-            uint32_t dg[BP_ITEMS];
+            const uint32_t incl = wave_incl_scan(cnt);
+            const uint32_t n = __shfl(incl, 63, 64);
+            nsub[r] = n;
+            offsub[r] = wave_sum((unsigned long long)lo);
+            if (n > SW_CAP) {
+                ovf = true;
+                break;
+            }
+            if ((uint32_t)lane < nt) {
+                L.psrc[lane] = (uint32_t)src;
+                L.pdst[lane] = incl - cnt;
+            }
+            for (uint32_t d = lane; d < SW_NB3; d += 64) L.h[r][d] = 0;
+            wave_lds_sync();
+
+            // ---- gather into registers, count level-3 digits
+            const Tup* tp = A.tmp[r] + bst[r];
             const uint32_t d12 = (b << P.D2) | d2;
+            Tup v[SW_ITEMS];
+            uint32_t dg[SW_ITEMS];
+            bool cl = false;
 #pragma unroll
-            for (int j = 0; j < BP_ITEMS; j++) {
-                uint32_t i = j * BP_THREADS + threadIdx.x;
+            for (int k = 0; k < SW_ITEMS; k++) {
+                const uint32_t i = k * 64 + lane;
                 if (i < n) {
-                    uint32_t p = piece_of(pc, np, i);
-                    v[j] = A.tmp[r][pc[p].src + (i - pc[p].dst)];
+                    const uint32_t p = wave_piece_of(L.pdst, nt, i);
+                    v[k] = tp[L.psrc[p] + (i - L.pdst[p])];
                 }
             }
 #pragma unroll
-            for (int j = 0; j < BP_ITEMS; j++) {
-                uint32_t i = j * BP_THREADS + threadIdx.x;
+            for (int k = 0; k < SW_ITEMS; k++) {
+                const uint32_t i = k * 64 + lane;
                 if (i < n) {
-                    const int64_t k = tup_key(v[j]);
-                    const uint64_t ku = key_u(k), bu = key_u(P.base);
-                    if (ku < bu || ku - bu > P.span) misc[28] = 1;
-                    dg[j] = plan_d3(P, plan_rel(P, k), d12);
-                    atomicAdd(&h[r][dg[j]], 1u);
+                    const int64_t key = tup_key(v[k]);
+                    const uint64_t ku = key_u(key);
+                    cl |= (ku < bu) || (ku - bu > P.span);
+                    dg[k] = plan_d3(P, plan_rel(P, key), d12);
+                    atomicAdd(&L.h[r][dg[k]], 1u);
                 }
             }
-            __syncthreads();
-            // exclusive scan of bins, record max run
-            const uint32_t per = (nb3 + BP_THREADS - 1) / BP_THREADS;
-            const uint32_t q0 = threadIdx.x * per;
+            clamp[r] = __any(cl);
+            wave_lds_sync();
+
+            // ---- exclusive scan of the bins: lane owns 4 consecutive bins
+            uint32_t c[SW_NB3 / 64];
             uint32_t loc = 0, mx = 0;
-            for (uint32_t k = 0; k < per; k++) {
-                if (q0 + k < nb3) {
-                    uint32_t c = h[r][q0 + k];
-                    loc += c;
-                    mx = c > mx ? c : mx;
-                }
-            }
-            uint32_t tot;
-            uint32_t ex = block_exclusive_scan(loc, misc, &tot);
-            for (uint32_t k = 0; k < per; k++) {
-                uint32_t d = q0 + k;
-                if (d < nb3) {
-                    uint32_t c = h[r][d];
-                    h[r][d] = ex;
-                    fill[d] = ex;
-                    ex += c;
-                }
-            }
-            // max over block
 #pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                uint32_t y = __shfl_xor(mx, o, 64);
-                mx = y > mx ? y : mx;
+            for (int q = 0; q < SW_NB3 / 64; q++) {
+                c[q] = L.h[r][lane * (SW_NB3 / 64) + q];
+                loc += c[q];
+                mx = c[q] > mx ? c[q] : mx;
             }
-            if (lane_id() == 0) misc[24 + (threadIdx.x >> 6)] = mx;
-            __syncthreads();
-            for (int w = 0; w < BP_THREADS / 64; w++)
-                maxrun = (int)misc[24 + w] > maxrun ? (int)misc[24 + w] : maxrun;
+            uint32_t ex = wave_incl_scan(loc) - loc;
 #pragma unroll
-            for (int j = 0; j < BP_ITEMS; j++) {
-                uint32_t i = j * BP_THREADS + threadIdx.x;
+            for (int q = 0; q < SW_NB3 / 64; q++) {
+                const uint32_t d = lane * (SW_NB3 / 64) + q;
+                L.h[r][d] = ex;
+                L.fill[d] = ex;
+                ex += c[q];
+            }
+            if (wave_max(mx) > SW_RUNMAX) {
+                ovf = true;
+                break;
+            }
+            wave_lds_sync();
+            // ---- place
+#pragma unroll
+            for (int k = 0; k < SW_ITEMS; k++) {
+                const uint32_t i = k * 64 + lane;
                 if (i < n) {
-                    uint32_t pos = atomicAdd(&fill[dg[j]], 1u);
-                    B[r][pos] = v[j];
+                    const uint32_t pos = atomicAdd(&L.fill[dg[k]], 1u);
+                    L.B[r][pos] = v[k];
                 }
             }
-            __syncthreads();
+            wave_lds_sync();
         }
-        if (maxrun > BP_RUNMAX) ovf = true;
-    }
 
-    if (ovf) {
-        if (threadIdx.x == 0) {
-            uint32_t k = atomicAdd(A.novf, 1u);
-            if (k < A.ovf_cap) {
-                OvfEntry e;
-                e.bucket = b;
-                e.d2 = d2;
-                e.nr[0] = nsub[0];
-                e.nr[1] = nsub[1];
-                e.off[0] = offsub[0];
-                e.off[1] = offsub[1];
-                A.ovf[k] = e;
-            }
-        }
-        return;
-    }
-
-    // ---- phase 3: fix equal-digit runs, write out
-    for (int r = 0; r < nrel; r++) {
-        const uint32_t n = nsub[r];
-        for (uint32_t d = threadIdx.x; d < nb3; d += BP_THREADS) {
-            uint32_t s = h[r][d];
-            uint32_t e = (d + 1 < nb3) ? h[r][d + 1] : n;
-            if (e - s > 1) lds_insertion_sort(B[r] + s, e - s);
-        }
-        __syncthreads();
-        Tup* dst = A.out[r] + A.bstart[r][b] + offsub[r];
-        for (uint32_t i = threadIdx.x; i < n; i += BP_THREADS) dst[i] = B[r][i];
-    }
-
-    // ---- phase 4: merge-join count of the two resident sub-buckets
-    if (nrel == 2) {
-        unsigned long long cnt = 0;
-        const uint32_t nR = nsub[0], nS = nsub[1];
-        if (P.s3 == 0 && misc[28] == 0) {
-            // level-3 digit is the exact key: count = sum_k |R_k| * |S_k|
-            for (uint32_t d = threadIdx.x; d < nb3; d += BP_THREADS) {
-                uint32_t cr = ((d + 1 < nb3) ? h[0][d + 1] : nR) - h[0][d];
-                uint32_t cs = ((d + 1 < nb3) ? h[1][d + 1] : nS) - h[1][d];
-                cnt += (unsigned long long)cr * cs;
-            }
-        } else {
-            // generic: for each S run of one key, |R_k| by binary search
-            for (uint32_t i = threadIdx.x; i < nS; i += BP_THREADS) {
-                int64_t k = tup_key(B[1][i]);
-                if (i > 0 && tup_key(B[1][i - 1]) == k) continue;
-                uint32_t e = i + 1;
-                while (e < nS && tup_key(B[1][e]) == k) e++;
-                uint32_t lo = 0, hi = nR;
-                while (lo < hi) {
-                    uint32_t m = (lo + hi) >> 1;
-                    if (tup_key(B[0][m]) < k) lo = m + 1; else hi = m;
+        if (ovf) {
+            if (lane == 0) {
+                // the fallback needs the size of the sub-bucket in every
+                // relation, whatever made this one overflow
+                uint32_t n2[2] = {0, 0};
+                uint64_t o2[2] = {0, 0};
+                for (int r = 0; r < A.nrel; r++) {
+                    const TileTable& tt = A.tt[r];
+                    for (uint32_t t = tt.btile0[b]; t < tt.btile0[b + 1]; t++) {
+                        const uint16_t* pf = tt.pref + (uint64_t)t * nb2;
+                        const uint32_t lo = pf[d2];
+                        const uint32_t hi = (d2 + 1 < nb2) ? pf[d2 + 1] : tt.len[t];
+                        n2[r] += hi - lo;
+                        o2[r] += lo;
+                    }
                 }
-                uint32_t lb = lo;
-                hi = nR;
-                while (lo < hi) {
-                    uint32_t m = (lo + hi) >> 1;
-                    if (tup_key(B[0][m]) <= k) lo = m + 1; else hi = m;
+                const uint32_t k = atomicAdd(A.novf, 1u);
+                if (k < A.ovf_cap) {
+                    OvfEntry e;
+                    e.bucket = b;
+                    e.d2 = d2;
+                    e.nr[0] = n2[0];
+                    e.nr[1] = n2[1];
+                    e.off[0] = o2[0];
+                    e.off[1] = o2[1];
+                    A.ovf[k] = e;
                 }
-                cnt += (unsigned long long)(lo - lb) * (e - i);
+            }
+            wave_lds_sync();
+            continue;
+        }
+
+        // ---- fix equal-digit runs, write the sorted sub-bucket
+        for (int r = 0; r < A.nrel; r++) {
+            const uint32_t n = nsub[r];
+            for (uint32_t d = lane; d < nb3; d += 64) {
+                const uint32_t s0 = L.h[r][d];
+                const uint32_t e0 = (d + 1 < nb3) ? L.h[r][d + 1] : n;
+                if (e0 - s0 > 1) lds_insertion_sort(L.B[r] + s0, e0 - s0);
+            }
+            wave_lds_sync();
+            Tup* dst = A.out[r] + bst[r] + offsub[r];
+            for (uint32_t i = lane; i < n; i += 64) dst[i] = L.B[r][i];
+        }
+
+        // ---- merge-join count of the two resident sub-buckets
+        if (A.nrel == 2) {
+            const uint32_t nR = nsub[0], nS = nsub[1];
+            if (exact && !clamp[0] && !clamp[1]) {
+                // the level-3 digit is the exact key: sum_k |R_k| * |S_k|
+                for (uint32_t d = lane; d < nb3; d += 64) {
+                    const uint32_t cr = ((d + 1 < nb3) ? L.h[0][d + 1] : nR) - L.h[0][d];
+                    const uint32_t cs = ((d + 1 < nb3) ? L.h[1][d + 1] : nS) - L.h[1][d];
+                    matches += (unsigned long long)cr * cs;
+                }
+            } else {
+                for (uint32_t i = lane; i < nS; i += 64) {
+                    const int64_t k = tup_key(L.B[1][i]);
+                    if (i > 0 && tup_key(L.B[1][i - 1]) == k) continue;
+                    uint32_t e = i + 1;
+                    while (e < nS && tup_key(L.B[1][e]) == k) e++;
+                    uint32_t lo = 0, hi = nR;
+                    while (lo < hi) {
+                        const uint32_t m = (lo + hi) >> 1;
+                        if (tup_key(L.B[0][m]) < k) lo = m + 1; else hi = m;
+                    }
+                    const uint32_t lb = lo;
+                    hi = nR;
+                    while (lo < hi) {
+                        const uint32_t m = (lo + hi) >> 1;
+                        if (tup_key(L.B[0][m]) <= k) lo = m + 1; else hi = m;
+                    }
+                    matches += (unsigned long long)(lo - lb) * (e - i);
+                }
             }
         }
-        cnt = wave_sum(cnt);
-        if (lane_id() == 0 && cnt) atomicAdd(A.count_dev, cnt);
+        wave_lds_sync();
+    }
+    if (A.nrel == 2) {
+        matches = wave_sum(matches);
+        if (lane == 0 && matches) atomicAdd(A.count_dev, matches);
     }
 }
 
@@ -505,12 +508,10 @@ k_plan(const Tup* r0, uint64_t n0, const Tup* r1, uint64_t n1, uint32_t D1,
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        for (int w = 1; w < 4; w++) {
+        for (int w = 0; w < 4; w++) {
             mn = smin[w] < mn ? smin[w] : mn;
             mx = smax[w] > mx ? smax[w] : mx;
         }
-        mn = smin[0] < mn ? smin[0] : mn;
-        mx = smax[0] > mx ? smax[0] : mx;
         int64_t lo, hi;
         if (hmin <= hmax) {
             lo = hmin;
@@ -527,7 +528,7 @@ k_plan(const Tup* r0, uint64_t n0, const Tup* r1, uint64_t n1, uint32_t D1,
             lo = (int64_t)(lu ^ 0x8000000000000000ull);
             hi = (int64_t)(hu ^ 0x8000000000000000ull);
         }
-        *plan = make_plan(lo, hi, D1, D2, BP_D3MAX);
+        *plan = make_plan(lo, hi, D1, D2, SW_D3MAX);
     }
 }
 
@@ -569,7 +570,7 @@ void bucket_sort(Workspace* ws, const BucketSortArgs& a, uint32_t D2,
         SMJ_CHECK(hipFuncSetAttribute((const void*)k_tilepass,
                                       hipFuncAttributeMaxDynamicSharedMemorySize,
                                       160 * 1024));
-        SMJ_CHECK(hipFuncSetAttribute((const void*)k_bucketpass,
+        SMJ_CHECK(hipFuncSetAttribute((const void*)k_subwave,
                                       hipFuncAttributeMaxDynamicSharedMemorySize,
                                       160 * 1024));
         attr = true;
@@ -587,7 +588,7 @@ void bucket_sort(Workspace* ws, const BucketSortArgs& a, uint32_t D2,
     OvfEntry* ovf = (OvfEntry*)ws->scratch("bs_ovf", (size_t)ovf_cap * sizeof(OvfEntry));
     uint32_t* novf = (uint32_t*)ws->scratch("bs_novf", 4);
     SMJ_CHECK(hipMemsetAsync(novf, 0, 4, st));
-    BucketPassArgs B;
+    SubWaveArgs B;
     for (int r = 0; r < 2; r++) {
         int rr = r < a.nrel ? r : 0;
         B.tmp[r] = a.tmp[rr];
@@ -599,12 +600,20 @@ void bucket_sort(Workspace* ws, const BucketSortArgs& a, uint32_t D2,
     B.plan_dev = a.plan_dev;
     B.count_dev = a.count_dev;
     B.nb2 = nb2;
+    B.nsub = nsub;
+    // enough waves to fill every SIMD several times over
+    const uint32_t target_waves = 256 * SW_WAVES * 4;
+    B.spw = (nsub + target_waves - 1) / target_waves;
+    if (B.spw == 0) B.spw = 1;
+    const uint32_t nwaves = (nsub + B.spw - 1) / B.spw;
+    const uint32_t nwg = (nwaves + SW_WAVES - 1) / SW_WAVES;
     B.ovf = ovf;
     B.novf = novf;
     B.ovf_cap = ovf_cap;
     {
-        TraceScope ts(ws, "k_bucketpass", st);
-        hipLaunchKernelGGL(k_bucketpass, dim3(nsub), dim3(BP_THREADS), BP_LDS, st, B);
+        TraceScope ts(ws, "k_subwave", st);
+        hipLaunchKernelGGL(k_subwave, dim3(nwg), dim3(SW_THREADS),
+                           sizeof(WaveLDS) * SW_WAVES, st, B);
     }
     SMJ_CHECK(hipGetLastError());
     if (a.ev_ovf) SMJ_CHECK(hipEventRecord(a.ev_ovf, st));
