@@ -12,15 +12,18 @@
 //                place, linearly (fully coalesced), together with the tile's
 //                exclusive d2 prefix (uint16 per digit).  Traffic: 2w.
 //   k_subwave  : ONE WAVE per sub-bucket (b, d2) at a time -- no workgroup
-//                barriers on the critical path, eight independent sub-buckets
-//                in flight per workgroup.  The wave gathers the sub-bucket's
-//                piece from every tile of bucket b (contiguous runs, read by
-//                consecutive lanes), counting-sorts them in its private LDS
-//                slice by the level-3 digit, fixes equal-digit runs with an
-//                insertion sort on the full (key, payload) order, writes the
-//                sorted sub-bucket to its final position, and -- for a join --
-//                counts the matching pairs of the R and S sub-buckets that are
-//                both resident in LDS.  Traffic: 2w; the join reads nothing.
+//                barriers, eight independent waves per workgroup, and a
+//                software pipeline inside every wave: while sub-bucket s is
+//                sorted in LDS, the tuples of s+1 and the tile prefixes of s+2
+//                are already in flight.  A wave gathers the sub-bucket's piece
+//                from every tile of bucket b for R and S in one round trip
+//                (contiguous runs, read by consecutive lanes), counting-sorts
+//                them in its private LDS slice by the level-3 digit, fixes
+//                equal-digit runs with an insertion sort on the full
+//                (key, payload) order, writes the sorted sub-bucket to its
+//                final position, and -- for a join -- counts the matching pairs
+//                of the two resident sub-buckets.  Traffic: 2w; the join reads
+//                nothing more.
 //
 // Sub-buckets that do not fit the per-wave LDS capacity, or that hold long
 // runs of equal digits (skew, e.g. Zipf hot keys), are queued and finished by
@@ -37,9 +40,9 @@ constexpr int TILE2 = TP_THREADS * TP_ITEMS;  // 4096 tuples per tile
 constexpr int SW_WAVES = 8;  // waves per workgroup, one sub-bucket each
 constexpr int SW_THREADS = SW_WAVES * 64;
 #ifdef KEY_8B
-constexpr int SW_CAP = 512;  // tuples per relation per sub-bucket
+constexpr int SW_CAP = 448;  // tuples per relation per sub-bucket
 #else
-constexpr int SW_CAP = 1024;
+constexpr int SW_CAP = 896;
 #endif
 constexpr int SW_ITEMS = SW_CAP / 64;
 constexpr int SW_D3MAX = 8;  // level-3 bins per wave (256)
@@ -63,7 +66,8 @@ struct OvfEntry {
 };
 
 // ---------------------------------------------------------------------------
-// tile table: one workgroup scans the per-bucket tile counts
+// tile table: one workgroup scans the per-bucket tile counts.  The tiles of a
+// bucket are consecutive TILE2-sized chunks of it.
 __global__ void __launch_bounds__(256)
 k_tiles(const uint64_t* __restrict__ bstart, const int64_t* __restrict__ bcount,
         uint32_t nb, TileTable tt) {
@@ -184,13 +188,13 @@ struct SubWaveArgs {
     uint32_t ovf_cap;
 };
 
-// per-wave LDS slice (< 20 KiB: eight waves fill one CU's 160 KiB)
+// per-wave LDS slice (<= 20 KiB: eight waves share one CU's 160 KiB)
 struct WaveLDS {
     Tup B[2][SW_CAP];
     uint32_t h[2][SW_NB3];  // bin starts after the scan
     uint32_t fill[SW_NB3];
-    uint32_t psrc[SW_PMAX];  // piece start, relative to the bucket start
-    uint32_t pdst[SW_PMAX];  // piece position inside the sub-bucket
+    uint32_t psrc[2][2][SW_PMAX];  // [pipeline buffer][relation][piece]
+    uint32_t pdst[2][2][SW_PMAX];
 };
 static_assert(sizeof(WaveLDS) * SW_WAVES <= 160 * 1024, "LDS budget");
 
@@ -245,208 +249,306 @@ __device__ __forceinline__ void lds_insertion_sort(Tup* a, uint32_t n) {
     }
 }
 
+// wave-uniform description of one sub-bucket
+struct SubHead {
+    uint32_t b, d2;
+    bool live;  // a sub-bucket of this wave whose digit exists
+    uint32_t t0[2], nt[2];
+    uint64_t bst[2];
+};
+// per-lane tile prefixes of one sub-bucket (lane = tile index in the bucket)
+struct SubPref {
+    uint32_t lo[2], cnt[2];
+};
+// wave-uniform piece summary
+struct SubPieces {
+    uint32_t n[2];
+    uint64_t off[2];
+    bool ovf;
+};
+
+__device__ __forceinline__ SubHead sub_head(const SubWaveArgs& A, uint32_t s,
+                                            uint32_t s_end, uint32_t d2lim) {
+    SubHead H;
+    H.b = s / A.nb2;
+    H.d2 = s % A.nb2;
+    H.live = s < s_end && H.d2 < d2lim;
+    for (int r = 0; r < 2; r++) {
+        H.t0[r] = 0;
+        H.nt[r] = 0;
+        H.bst[r] = 0;
+    }
+    if (H.live) {
+        _Pragma("unroll") for (int r = 0; r < 2; r++) { if (r >= A.nrel) break;
+            H.t0[r] = A.tt[r].btile0[H.b];
+            H.nt[r] = A.tt[r].btile0[H.b + 1] - H.t0[r];
+            H.bst[r] = A.bstart[r][H.b];
+        }
+    }
+    return H;
+}
+
+__device__ __forceinline__ SubPref sub_pref(const SubWaveArgs& A,
+                                            const SubHead& H, int lane) {
+    SubPref P;
+    for (int r = 0; r < 2; r++) {
+        P.lo[r] = 0;
+        P.cnt[r] = 0;
+        if (r < A.nrel && H.live && (uint32_t)lane < H.nt[r] && H.nt[r] <= SW_PMAX) {
+            const uint32_t t = H.t0[r] + lane;
+            const uint16_t* pf = A.tt[r].pref + (uint64_t)t * A.nb2;
+            const uint32_t lo = pf[H.d2];
+            const uint32_t hi = (H.d2 + 1 < A.nb2) ? pf[H.d2 + 1] : A.tt[r].len[t];
+            P.lo[r] = lo;
+            P.cnt[r] = hi - lo;
+        }
+    }
+    return P;
+}
+
+// piece table of one sub-bucket into pipeline buffer `buf`
+__device__ __forceinline__ SubPieces sub_pieces(const SubWaveArgs& A,
+                                                const SubHead& H,
+                                                const SubPref& P, WaveLDS& L,
+                                                int buf, int lane) {
+    SubPieces X;
+    X.ovf = false;
+    for (int r = 0; r < 2; r++) {
+        X.n[r] = 0;
+        X.off[r] = 0;
+    }
+    if (!H.live) return X;
+    _Pragma("unroll") for (int r = 0; r < 2; r++) { if (r >= A.nrel) break;
+        if (H.nt[r] > SW_PMAX) {
+            X.ovf = true;
+            continue;
+        }
+        const uint32_t incl = wave_incl_scan(P.cnt[r]);
+        X.n[r] = __shfl(incl, 63, 64);
+        X.off[r] = wave_sum((unsigned long long)P.lo[r]);
+        if ((uint32_t)lane < H.nt[r]) {
+            L.psrc[buf][r][lane] = lane * (uint32_t)TILE2 + P.lo[r];
+            L.pdst[buf][r][lane] = incl - P.cnt[r];
+        }
+        if (X.n[r] > SW_CAP) X.ovf = true;
+    }
+    return X;
+}
+
+__device__ __forceinline__ void sub_load(const SubWaveArgs& A, const SubHead& H,
+                                         const SubPieces& X, const WaveLDS& L,
+                                         int buf, int lane,
+                                         Tup (&v)[2][SW_ITEMS]) {
+    if (!H.live || X.ovf) return;
+    _Pragma("unroll") for (int r = 0; r < 2; r++) { if (r >= A.nrel) break;
+        const Tup* tp = A.tmp[r] + H.bst[r];
+#pragma unroll
+        for (int k = 0; k < SW_ITEMS; k++) {
+            const uint32_t i = k * 64 + lane;
+            if (i < X.n[r]) {
+                const uint32_t p = wave_piece_of(L.pdst[buf][r], H.nt[r], i);
+                v[r][k] = tp[L.psrc[buf][r][p] + (i - L.pdst[buf][r][p])];
+            }
+        }
+    }
+}
+
+__device__ void sub_overflow(const SubWaveArgs& A, const SubHead& H, int lane) {
+    if (lane != 0) return;
+    // the fallback needs the size of the sub-bucket in every relation
+    uint32_t n2[2] = {0, 0};
+    uint64_t o2[2] = {0, 0};
+    _Pragma("unroll") for (int r = 0; r < 2; r++) { if (r >= A.nrel) break;
+        const TileTable& tt = A.tt[r];
+        for (uint32_t t = tt.btile0[H.b]; t < tt.btile0[H.b + 1]; t++) {
+            const uint16_t* pf = tt.pref + (uint64_t)t * A.nb2;
+            const uint32_t lo = pf[H.d2];
+            const uint32_t hi = (H.d2 + 1 < A.nb2) ? pf[H.d2 + 1] : tt.len[t];
+            n2[r] += hi - lo;
+            o2[r] += lo;
+        }
+    }
+    const uint32_t k = atomicAdd(A.novf, 1u);
+    if (k < A.ovf_cap) {
+        OvfEntry e;
+        e.bucket = H.b;
+        e.d2 = H.d2;
+        e.nr[0] = n2[0];
+        e.nr[1] = n2[1];
+        e.off[0] = o2[0];
+        e.off[1] = o2[1];
+        A.ovf[k] = e;
+    }
+}
+
+// sort the resident sub-bucket in LDS, write it out, count join matches
+__device__ __forceinline__ void sub_process(const SubWaveArgs& A,
+                                            const RangePlan& P,
+                                            const SubHead& H,
+                                            const SubPieces& X, WaveLDS& L,
+                                            int lane, Tup (&v)[2][SW_ITEMS],
+                                            unsigned long long& matches) {
+    if (!H.live) return;
+    if (X.ovf) {
+        sub_overflow(A, H, lane);
+        return;
+    }
+    const uint32_t nb3 = 1u << P.D3;
+    const uint64_t bu = key_u(P.base);
+    const uint32_t d12 = (H.b << P.D2) | H.d2;
+    bool clamp = false;
+    uint32_t mx = 0;
+    // ---- level-3 histograms of both relations
+    _Pragma("unroll") for (int r = 0; r < 2; r++) { if (r >= A.nrel) break;
+#pragma unroll
+        for (int q = 0; q < SW_NB3 / 64; q++) L.h[r][lane * (SW_NB3 / 64) + q] = 0;
+    }
+    wave_lds_sync();
+    _Pragma("unroll") for (int r = 0; r < 2; r++) { if (r >= A.nrel) break;
+#pragma unroll
+        for (int k = 0; k < SW_ITEMS; k++) {
+            const uint32_t i = k * 64 + lane;
+            if (i < X.n[r]) {
+                const int64_t key = tup_key(v[r][k]);
+                const uint64_t ku = key_u(key);
+                clamp |= (ku < bu) || (ku - bu > P.span);
+                atomicAdd(&L.h[r][plan_d3(P, plan_rel(P, key), d12)], 1u);
+            }
+        }
+    }
+    wave_lds_sync();
+    // ---- exclusive scans: lane owns 4 consecutive bins
+    uint32_t c[2][SW_NB3 / 64];
+    _Pragma("unroll") for (int r = 0; r < 2; r++) { if (r >= A.nrel) break;
+        uint32_t loc = 0;
+#pragma unroll
+        for (int q = 0; q < SW_NB3 / 64; q++) {
+            c[r][q] = L.h[r][lane * (SW_NB3 / 64) + q];
+            loc += c[r][q];
+            mx = c[r][q] > mx ? c[r][q] : mx;
+        }
+        uint32_t ex = wave_incl_scan(loc) - loc;
+#pragma unroll
+        for (int q = 0; q < SW_NB3 / 64; q++) {
+            L.h[r][lane * (SW_NB3 / 64) + q] = ex;
+            ex += c[r][q];
+        }
+    }
+    if (wave_max(mx) > SW_RUNMAX) {
+        wave_lds_sync();
+        sub_overflow(A, H, lane);
+        return;
+    }
+    const bool any_clamp = __any(clamp);
+    // ---- place, fix runs, write
+    _Pragma("unroll") for (int r = 0; r < 2; r++) { if (r >= A.nrel) break;
+        const uint32_t n = X.n[r];
+#pragma unroll
+        for (int q = 0; q < SW_NB3 / 64; q++)
+            L.fill[lane * (SW_NB3 / 64) + q] = L.h[r][lane * (SW_NB3 / 64) + q];
+        wave_lds_sync();
+#pragma unroll
+        for (int k = 0; k < SW_ITEMS; k++) {
+            const uint32_t i = k * 64 + lane;
+            if (i < n) {
+                const uint32_t d = plan_d3(P, plan_rel(P, tup_key(v[r][k])), d12);
+                const uint32_t pos = atomicAdd(&L.fill[d], 1u);
+                L.B[r][pos] = v[r][k];
+            }
+        }
+        wave_lds_sync();
+        for (uint32_t d = lane; d < nb3; d += 64) {
+            const uint32_t s0 = L.h[r][d];
+            const uint32_t e0 = (d + 1 < nb3) ? L.h[r][d + 1] : n;
+            if (e0 - s0 > 1) lds_insertion_sort(L.B[r] + s0, e0 - s0);
+        }
+        wave_lds_sync();
+        Tup* dst = A.out[r] + H.bst[r] + X.off[r];
+        for (uint32_t i = lane; i < n; i += 64) dst[i] = L.B[r][i];
+    }
+    // ---- merge-join count of the two resident sub-buckets
+    if (A.nrel == 2) {
+        const uint32_t nR = X.n[0], nS = X.n[1];
+        if (P.s3 == 0 && !any_clamp) {
+            // the level-3 digit is the exact key: sum_k |R_k| * |S_k|
+            for (uint32_t d = lane; d < nb3; d += 64) {
+                const uint32_t cr = ((d + 1 < nb3) ? L.h[0][d + 1] : nR) - L.h[0][d];
+                const uint32_t cs = ((d + 1 < nb3) ? L.h[1][d + 1] : nS) - L.h[1][d];
+                matches += (unsigned long long)cr * cs;
+            }
+        } else {
+            for (uint32_t i = lane; i < nS; i += 64) {
+                const int64_t k = tup_key(L.B[1][i]);
+                if (i > 0 && tup_key(L.B[1][i - 1]) == k) continue;
+                uint32_t e = i + 1;
+                while (e < nS && tup_key(L.B[1][e]) == k) e++;
+                uint32_t lo = 0, hi = nR;
+                while (lo < hi) {
+                    const uint32_t m = (lo + hi) >> 1;
+                    if (tup_key(L.B[0][m]) < k) lo = m + 1; else hi = m;
+                }
+                const uint32_t lb = lo;
+                hi = nR;
+                while (lo < hi) {
+                    const uint32_t m = (lo + hi) >> 1;
+                    if (tup_key(L.B[0][m]) <= k) lo = m + 1; else hi = m;
+                }
+                matches += (unsigned long long)(lo - lb) * (e - i);
+            }
+        }
+    }
+    wave_lds_sync();
+}
+
 __global__ void __launch_bounds__(SW_THREADS)
 k_subwave(SubWaveArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     WaveLDS& L = reinterpret_cast<WaveLDS*>(lds_raw)[threadIdx.x >> 6];
     const RangePlan P = *A.plan_dev;
-    const uint32_t nb2 = A.nb2;
-    const uint32_t nb3 = 1u << P.D3;
     const uint32_t d2lim = 1u << P.D2;
     const int lane = lane_id();
-    const uint64_t bu = key_u(P.base);
-    const bool exact = (P.s3 == 0);
 
-    const uint32_t wave = blockIdx.x * SW_WAVES + (threadIdx.x >> 6);
-    const uint32_t s_begin = wave * A.spw;
-    uint32_t s_end = s_begin + A.spw;
+    // The workgroup owns sub-buckets [g0, g1); its eight waves take them
+    // interleaved (wave w: g0+w, g0+w+8, ...) so that neighbouring
+    // sub-buckets -- which share the cache lines at their piece boundaries
+    // and the 128-byte lines of the tile prefix table -- are read by the
+    // same CU at the same time (L1/L2 hits instead of refetches).
+    const uint32_t g0 = blockIdx.x * SW_WAVES * A.spw;
+    uint32_t s_end = g0 + SW_WAVES * A.spw;
     if (s_end > A.nsub) s_end = A.nsub;
+    const uint32_t s_begin = g0 + (threadIdx.x >> 6);
+    constexpr uint32_t SS = SW_WAVES;  // sub-bucket stride of a wave
     unsigned long long matches = 0;
 
-    for (uint32_t s = s_begin; s < s_end; s++) {
-        const uint32_t b = s / nb2;
-        const uint32_t d2 = s % nb2;
-        if (d2 >= d2lim) continue;  // a table column no digit maps to
-        uint32_t nsub[2] = {0, 0};
-        uint64_t offsub[2] = {0, 0};
-        uint64_t bst[2] = {0, 0};
-        bool clamp[2] = {false, false};
-        bool ovf = false;
-
-        for (int r = 0; r < A.nrel && !ovf; r++) {
-            // ---- piece table of relation r (one global round trip)
-            const TileTable& tt = A.tt[r];
-            const uint32_t t0 = tt.btile0[b];
-            const uint32_t nt = tt.btile0[b + 1] - t0;
-            bst[r] = A.bstart[r][b];
-            if (nt > SW_PMAX) {
-                ovf = true;
-                break;
-            }
-            uint32_t cnt = 0, lo = 0;
-            uint64_t src = 0;
-            if ((uint32_t)lane < nt) {
-                const uint32_t t = t0 + lane;
-                const uint16_t* pf = tt.pref + (uint64_t)t * nb2;
-                lo = pf[d2];
-                const uint32_t hi = (d2 + 1 < nb2) ? pf[d2 + 1] : tt.len[t];
-                cnt = hi - lo;
-                src = tt.off[t] - bst[r] + lo;
-            }
-            const uint32_t incl = wave_incl_scan(cnt);
-            const uint32_t n = __shfl(incl, 63, 64);
-            nsub[r] = n;
-            offsub[r] = wave_sum((unsigned long long)lo);
-            if (n > SW_CAP) {
-                ovf = true;
-                break;
-            }
-            if ((uint32_t)lane < nt) {
-                L.psrc[lane] = (uint32_t)src;
-                L.pdst[lane] = incl - cnt;
-            }
-            for (uint32_t d = lane; d < SW_NB3; d += 64) L.h[r][d] = 0;
-            wave_lds_sync();
-
-            // ---- gather into registers, count level-3 digits
-            const Tup* tp = A.tmp[r] + bst[r];
-            const uint32_t d12 = (b << P.D2) | d2;
-            Tup v[SW_ITEMS];
-            uint32_t dg[SW_ITEMS];
-            bool cl = false;
-#pragma unroll
-            for (int k = 0; k < SW_ITEMS; k++) {
-                const uint32_t i = k * 64 + lane;
-                if (i < n) {
-                    const uint32_t p = wave_piece_of(L.pdst, nt, i);
-                    v[k] = tp[L.psrc[p] + (i - L.pdst[p])];
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < SW_ITEMS; k++) {
-                const uint32_t i = k * 64 + lane;
-                if (i < n) {
-                    const int64_t key = tup_key(v[k]);
-                    const uint64_t ku = key_u(key);
-                    cl |= (ku < bu) || (ku - bu > P.span);
-                    dg[k] = plan_d3(P, plan_rel(P, key), d12);
-                    atomicAdd(&L.h[r][dg[k]], 1u);
-                }
-            }
-            clamp[r] = __any(cl);
-            wave_lds_sync();
-
-            // ---- exclusive scan of the bins: lane owns 4 consecutive bins
-            uint32_t c[SW_NB3 / 64];
-            uint32_t loc = 0, mx = 0;
-#pragma unroll
-            for (int q = 0; q < SW_NB3 / 64; q++) {
-                c[q] = L.h[r][lane * (SW_NB3 / 64) + q];
-                loc += c[q];
-                mx = c[q] > mx ? c[q] : mx;
-            }
-            uint32_t ex = wave_incl_scan(loc) - loc;
-#pragma unroll
-            for (int q = 0; q < SW_NB3 / 64; q++) {
-                const uint32_t d = lane * (SW_NB3 / 64) + q;
-                L.h[r][d] = ex;
-                L.fill[d] = ex;
-                ex += c[q];
-            }
-            if (wave_max(mx) > SW_RUNMAX) {
-                ovf = true;
-                break;
-            }
-            wave_lds_sync();
-            // ---- place
-#pragma unroll
-            for (int k = 0; k < SW_ITEMS; k++) {
-                const uint32_t i = k * 64 + lane;
-                if (i < n) {
-                    const uint32_t pos = atomicAdd(&L.fill[dg[k]], 1u);
-                    L.B[r][pos] = v[k];
-                }
-            }
-            wave_lds_sync();
-        }
-
-        if (ovf) {
-            if (lane == 0) {
-                // the fallback needs the size of the sub-bucket in every
-                // relation, whatever made this one overflow
-                uint32_t n2[2] = {0, 0};
-                uint64_t o2[2] = {0, 0};
-                for (int r = 0; r < A.nrel; r++) {
-                    const TileTable& tt = A.tt[r];
-                    for (uint32_t t = tt.btile0[b]; t < tt.btile0[b + 1]; t++) {
-                        const uint16_t* pf = tt.pref + (uint64_t)t * nb2;
-                        const uint32_t lo = pf[d2];
-                        const uint32_t hi = (d2 + 1 < nb2) ? pf[d2 + 1] : tt.len[t];
-                        n2[r] += hi - lo;
-                        o2[r] += lo;
-                    }
-                }
-                const uint32_t k = atomicAdd(A.novf, 1u);
-                if (k < A.ovf_cap) {
-                    OvfEntry e;
-                    e.bucket = b;
-                    e.d2 = d2;
-                    e.nr[0] = n2[0];
-                    e.nr[1] = n2[1];
-                    e.off[0] = o2[0];
-                    e.off[1] = o2[1];
-                    A.ovf[k] = e;
-                }
-            }
-            wave_lds_sync();
-            continue;
-        }
-
-        // ---- fix equal-digit runs, write the sorted sub-bucket
-        for (int r = 0; r < A.nrel; r++) {
-            const uint32_t n = nsub[r];
-            for (uint32_t d = lane; d < nb3; d += 64) {
-                const uint32_t s0 = L.h[r][d];
-                const uint32_t e0 = (d + 1 < nb3) ? L.h[r][d + 1] : n;
-                if (e0 - s0 > 1) lds_insertion_sort(L.B[r] + s0, e0 - s0);
-            }
-            wave_lds_sync();
-            Tup* dst = A.out[r] + bst[r] + offsub[r];
-            for (uint32_t i = lane; i < n; i += 64) dst[i] = L.B[r][i];
-        }
-
-        // ---- merge-join count of the two resident sub-buckets
-        if (A.nrel == 2) {
-            const uint32_t nR = nsub[0], nS = nsub[1];
-            if (exact && !clamp[0] && !clamp[1]) {
-                // the level-3 digit is the exact key: sum_k |R_k| * |S_k|
-                for (uint32_t d = lane; d < nb3; d += 64) {
-                    const uint32_t cr = ((d + 1 < nb3) ? L.h[0][d + 1] : nR) - L.h[0][d];
-                    const uint32_t cs = ((d + 1 < nb3) ? L.h[1][d + 1] : nS) - L.h[1][d];
-                    matches += (unsigned long long)cr * cs;
-                }
-            } else {
-                for (uint32_t i = lane; i < nS; i += 64) {
-                    const int64_t k = tup_key(L.B[1][i]);
-                    if (i > 0 && tup_key(L.B[1][i - 1]) == k) continue;
-                    uint32_t e = i + 1;
-                    while (e < nS && tup_key(L.B[1][e]) == k) e++;
-                    uint32_t lo = 0, hi = nR;
-                    while (lo < hi) {
-                        const uint32_t m = (lo + hi) >> 1;
-                        if (tup_key(L.B[0][m]) < k) lo = m + 1; else hi = m;
-                    }
-                    const uint32_t lb = lo;
-                    hi = nR;
-                    while (lo < hi) {
-                        const uint32_t m = (lo + hi) >> 1;
-                        if (tup_key(L.B[0][m]) <= k) lo = m + 1; else hi = m;
-                    }
-                    matches += (unsigned long long)(lo - lb) * (e - i);
-                }
-            }
-        }
+    // software pipeline: cur = loaded tuples in flight, nxt = prefixes in flight
+    int buf = 0;
+    SubHead Hc = sub_head(A, s_begin, s_end, d2lim);
+    SubPref Pc = sub_pref(A, Hc, lane);
+    SubHead Hn = sub_head(A, s_begin + SS, s_end, d2lim);
+    SubPref Pn = sub_pref(A, Hn, lane);
+    SubPieces Xc = sub_pieces(A, Hc, Pc, L, buf, lane);
+    wave_lds_sync();
+    Tup vc[2][SW_ITEMS];
+    Tup vn[2][SW_ITEMS];
+    sub_load(A, Hc, Xc, L, buf, lane, vc);
+    for (uint32_t s = s_begin; s < s_end; s += SS) {
+        // pieces + tuple loads of the next sub-bucket, prefixes of the one after
+        SubPieces Xn = sub_pieces(A, Hn, Pn, L, buf ^ 1, lane);
         wave_lds_sync();
+        sub_load(A, Hn, Xn, L, buf ^ 1, lane, vn);
+        SubHead Hnn = sub_head(A, s + 2 * SS, s_end, d2lim);
+        SubPref Pnn = sub_pref(A, Hnn, lane);
+        // sort / write / join s
+        sub_process(A, P, Hc, Xc, L, lane, vc, matches);
+#pragma unroll
+        for (int r = 0; r < 2; r++)
+#pragma unroll
+            for (int k = 0; k < SW_ITEMS; k++) vc[r][k] = vn[r][k];
+        Hc = Hn;
+        Xc = Xn;
+        Hn = Hnn;
+        Pn = Pnn;
+        buf ^= 1;
     }
     if (A.nrel == 2) {
         matches = wave_sum(matches);
@@ -601,8 +703,8 @@ void bucket_sort(Workspace* ws, const BucketSortArgs& a, uint32_t D2,
     B.count_dev = a.count_dev;
     B.nb2 = nb2;
     B.nsub = nsub;
-    // enough waves to fill every SIMD several times over
-    const uint32_t target_waves = 256 * SW_WAVES * 4;
+    // one resident wave per SIMD slot (8 waves/CU), several sub-buckets each
+    const uint32_t target_waves = 256 * SW_WAVES;
     B.spw = (nsub + target_waves - 1) / target_waves;
     if (B.spw == 0) B.spw = 1;
     const uint32_t nwaves = (nsub + B.spw - 1) / B.spw;

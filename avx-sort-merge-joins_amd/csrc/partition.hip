@@ -16,47 +16,46 @@
 //               keeps input order inside a digit (stable == radix_cluster).
 //               The tile is then staged in LDS sorted by digit and written out
 //               so that consecutive lanes write consecutive addresses of one
-//               partition: LDS plays the role of the reference's cache-line
-//               write-combining buffers.
+//               partition: the LDS tile plays the role of the reference's
+//               cache-line write-combining buffers, and the bigger the tile
+//               the longer each partition's contiguous run per store.
 //
 // Digits wider than 12 bits are done as two stable LSD passes plus a
-// padding copy (host side, smj_partition in this file).
+// padding copy (stable_partition below).
+#include <stdlib.h>
+
 #include "smj_common.hpp"
 #include "smj_internal.hpp"
 
 namespace smj {
 
-constexpr int PT_THREADS = 256;
-constexpr int PT_ITEMS = 8;  // items per thread per tile
-constexpr int PT_TILE = PT_THREADS * PT_ITEMS;
-constexpr int PT_WAVES = PT_THREADS / 64;
-
 // ---------------------------------------------------------------------------
-template <class Digit>
-__global__ void __launch_bounds__(PT_THREADS)
+template <int THREADS, int ITEMS, class Digit>
+__global__ void __launch_bounds__(THREADS)
 k_hist(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig,
        uint32_t nbins, uint32_t* __restrict__ counts, uint32_t nwg) {
+    constexpr int TILE = THREADS * ITEMS;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_hist[];
-    for (uint32_t d = threadIdx.x; d < nbins; d += PT_THREADS) lds_hist[d] = 0;
+    for (uint32_t d = threadIdx.x; d < nbins; d += THREADS) lds_hist[d] = 0;
     __syncthreads();
     const uint64_t beg = (uint64_t)blockIdx.x * chunk;
     uint64_t end = beg + chunk;
     if (end > n) end = n;
-    for (uint64_t base = beg; base < end; base += PT_TILE) {
-        Tup v[PT_ITEMS];
+    for (uint64_t base = beg; base < end; base += TILE) {
+        Tup v[ITEMS];
 #pragma unroll
-        for (int j = 0; j < PT_ITEMS; j++) {
-            uint64_t i = base + (uint64_t)j * PT_THREADS + threadIdx.x;
+        for (int j = 0; j < ITEMS; j++) {
+            uint64_t i = base + (uint64_t)j * THREADS + threadIdx.x;
             if (i < end) v[j] = in[i];
         }
 #pragma unroll
-        for (int j = 0; j < PT_ITEMS; j++) {
-            uint64_t i = base + (uint64_t)j * PT_THREADS + threadIdx.x;
+        for (int j = 0; j < ITEMS; j++) {
+            uint64_t i = base + (uint64_t)j * THREADS + threadIdx.x;
             if (i < end) atomicAdd(&lds_hist[dig(v[j])], 1u);
         }
     }
     __syncthreads();
-    for (uint32_t d = threadIdx.x; d < nbins; d += PT_THREADS)
+    for (uint32_t d = threadIdx.x; d < nbins; d += THREADS)
         counts[(uint64_t)d * nwg + blockIdx.x] = lds_hist[d];
 }
 
@@ -124,32 +123,41 @@ k_scandig(const uint64_t* __restrict__ totals, uint32_t nbins, int padded,
 
 // ---------------------------------------------------------------------------
 // stable scatter.  Dynamic LDS layout (16-byte aligned pieces):
-//   stage  : PT_TILE Tups
+//   stage  : TILE Tups
 //   run    : nbins uint64  (this workgroup's next output slot per digit)
-//   wcnt   : PT_WAVES * nbins uint32 (per-wave counts -> per-wave offsets)
 //   tstart : nbins uint32  (tile-exclusive start of every digit)
+//   wcnt   : WAVES * nbins uint16 (per-wave counts -> per-wave offsets)
 //   scr    : 16 uint32
-template <class Digit>
-__global__ void __launch_bounds__(PT_THREADS)
+template <int THREADS, int ITEMS>
+constexpr size_t scatter_lds(uint32_t nbins) {
+    return (size_t)THREADS * ITEMS * sizeof(Tup) + (size_t)nbins * 8 +
+           (size_t)nbins * 4 + (size_t)(THREADS / 64) * nbins * 2 + 64;
+}
+
+template <int THREADS, int ITEMS, class Digit>
+__global__ void __launch_bounds__(THREADS)
 k_scatter(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig,
           uint32_t nbins, uint32_t dbits, const uint32_t* __restrict__ counts,
           uint32_t nwg, const uint64_t* __restrict__ starts,
-          Tup* __restrict__ out) {
+          Tup* __restrict__ out, int mode) {
+    constexpr int TILE = THREADS * ITEMS;
+    constexpr int WAVES = THREADS / 64;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     Tup* stage = reinterpret_cast<Tup*>(lds_raw);
-    uint64_t* run = reinterpret_cast<uint64_t*>(lds_raw + PT_TILE * sizeof(Tup));
-    uint32_t* wcnt = reinterpret_cast<uint32_t*>(run + nbins);
-    uint32_t* tstart = wcnt + PT_WAVES * nbins;
-    uint32_t* scr = tstart + nbins;
+    uint64_t* run = reinterpret_cast<uint64_t*>(lds_raw + TILE * sizeof(Tup));
+    uint32_t* tstart = reinterpret_cast<uint32_t*>(run + nbins);
+    uint16_t* wcnt = reinterpret_cast<uint16_t*>(tstart + nbins);
+    uint32_t* scr = reinterpret_cast<uint32_t*>(
+        (reinterpret_cast<uintptr_t>(wcnt + WAVES * nbins) + 15) & ~uintptr_t(15));
 
     const int lane = lane_id();
     const int wid = threadIdx.x >> 6;
     const uint64_t lt = lanemask_lt();
 
-    for (uint32_t d = threadIdx.x; d < nbins; d += PT_THREADS) {
+    for (uint32_t d = threadIdx.x; d < nbins; d += THREADS) {
         run[d] = starts[d] + counts[(uint64_t)d * nwg + blockIdx.x];
 #pragma unroll
-        for (int w = 0; w < PT_WAVES; w++) wcnt[w * nbins + d] = 0;
+        for (int w = 0; w < WAVES; w++) wcnt[w * nbins + d] = 0;
     }
     __syncthreads();
 
@@ -157,30 +165,30 @@ k_scatter(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig,
     uint64_t end = beg + chunk;
     if (end > n) end = n;
     // digits handled by this thread in the per-tile scans (contiguous range)
-    const uint32_t dper = (nbins + PT_THREADS - 1) / PT_THREADS;
+    const uint32_t dper = (nbins + THREADS - 1) / THREADS;
     const uint32_t d0 = threadIdx.x * dper;
 
-    for (uint64_t base = beg; base < end; base += PT_TILE) {
+    for (uint64_t base = beg; base < end; base += TILE) {
         const uint32_t tcount =
-            (uint32_t)((end - base) < (uint64_t)PT_TILE ? (end - base) : PT_TILE);
+            (uint32_t)((end - base) < (uint64_t)TILE ? (end - base) : TILE);
         // wave `wid` owns items [wid*64*ITEMS, (wid+1)*64*ITEMS) of the tile
-        Tup v[PT_ITEMS];
-        uint32_t dg[PT_ITEMS];
-        uint32_t rk[PT_ITEMS];
-        const uint32_t wbase = wid * 64 * PT_ITEMS;
+        Tup v[ITEMS];
+        uint32_t dg[ITEMS];
+        uint32_t rk[ITEMS];
+        const uint32_t wbase = wid * 64 * ITEMS;
 #pragma unroll
-        for (int j = 0; j < PT_ITEMS; j++) {
+        for (int j = 0; j < ITEMS; j++) {
             uint32_t li = wbase + j * 64 + lane;
-            if (li < tcount) {
-                v[j] = in[base + li];
-                dg[j] = dig(v[j]);
-            } else {
-                dg[j] = 0xffffffffu;
-            }
+            if (li < tcount) v[j] = in[base + li];
         }
-        uint32_t* mycnt = wcnt + wid * nbins;
 #pragma unroll
-        for (int j = 0; j < PT_ITEMS; j++) {
+        for (int j = 0; j < ITEMS; j++) {
+            uint32_t li = wbase + j * 64 + lane;
+            dg[j] = li < tcount ? dig(v[j]) : 0xffffffffu;
+        }
+        uint16_t* mycnt = wcnt + wid * nbins;
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
             const bool valid = dg[j] != 0xffffffffu;
             uint64_t peers = __ballot(valid);
             const uint32_t d = valid ? dg[j] : 0;
@@ -194,7 +202,7 @@ k_scatter(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig,
             const uint32_t r = (uint32_t)__popcll(peers & lt);
             const uint32_t c = (uint32_t)__popcll(peers);
             // lowest lane of the peer group publishes the new count
-            if (valid && r == 0) mycnt[d] = before + c;
+            if (valid && r == 0) mycnt[d] = (uint16_t)(before + c);
             rk[j] = before + r;
         }
         __syncthreads();
@@ -204,7 +212,7 @@ k_scatter(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig,
             uint32_t d = d0 + k;
             if (d < nbins) {
 #pragma unroll
-                for (int w = 0; w < PT_WAVES; w++) loc += wcnt[w * nbins + d];
+                for (int w = 0; w < WAVES; w++) loc += wcnt[w * nbins + d];
             }
         }
         uint32_t tot;
@@ -214,23 +222,26 @@ k_scatter(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig,
             if (d < nbins) {
                 tstart[d] = ex;
 #pragma unroll
-                for (int w = 0; w < PT_WAVES; w++) {
+                for (int w = 0; w < WAVES; w++) {
                     uint32_t c = wcnt[w * nbins + d];
-                    wcnt[w * nbins + d] = ex;
+                    wcnt[w * nbins + d] = (uint16_t)ex;
                     ex += c;
                 }
             }
         }
         __syncthreads();
 #pragma unroll
-        for (int j = 0; j < PT_ITEMS; j++) {
+        for (int j = 0; j < ITEMS; j++) {
             if (dg[j] != 0xffffffffu) stage[mycnt[dg[j]] + rk[j]] = v[j];
         }
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i < tcount; i += PT_THREADS) {
+#pragma unroll 4
+        for (uint32_t i = threadIdx.x; i < tcount; i += THREADS) {
             Tup t = stage[i];
             uint32_t d = dig(t);
-            out[run[d] + (i - tstart[d])] = t;
+            if (mode == 0) out[run[d] + (i - tstart[d])] = t;
+            else if (mode == 1) out[base + i] = t;  // ablation: linear write
+            else if (tup_key(t) == -12345) out[0] = t;  // ablation: no write
         }
         __syncthreads();
         for (uint32_t k = 0; k < dper; k++) {
@@ -239,9 +250,108 @@ k_scatter(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig,
                 uint32_t nxt = (d + 1 < nbins) ? tstart[d + 1] : tcount;
                 run[d] += nxt - tstart[d];
 #pragma unroll
-                for (int w = 0; w < PT_WAVES; w++) wcnt[w * nbins + d] = 0;
+                for (int w = 0; w < WAVES; w++) wcnt[w * nbins + d] = 0;
             }
         }
+        __syncthreads();
+    }
+}
+
+// Unstable scatter for the join's level-1 partition (the join re-sorts every
+// bucket completely, so the order inside a partition is free).  Ranks come
+// from LDS atomics on tile-level digit counters -- two ds_add per tuple instead
+// of a ballot per digit bit -- and the next tile's tuples are loaded while the
+// current tile is ranked, staged and written.
+// LDS: stage TILE Tups | run nbins u64 | tstart nbins u32 | tfill nbins u32
+template <int THREADS, int ITEMS>
+constexpr size_t scatter_u_lds(uint32_t nbins) {
+    return (size_t)THREADS * ITEMS * sizeof(Tup) + (size_t)nbins * 16 + 64;
+}
+
+template <int THREADS, int ITEMS, class Digit>
+__global__ void __launch_bounds__(THREADS)
+k_scatter_u(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig,
+            uint32_t nbins, const uint32_t* __restrict__ counts, uint32_t nwg,
+            const uint64_t* __restrict__ starts, Tup* __restrict__ out) {
+    constexpr int TILE = THREADS * ITEMS;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    Tup* stage = reinterpret_cast<Tup*>(lds_raw);
+    uint64_t* run = reinterpret_cast<uint64_t*>(lds_raw + TILE * sizeof(Tup));
+    uint32_t* tstart = reinterpret_cast<uint32_t*>(run + nbins);
+    uint32_t* tfill = tstart + nbins;
+    uint32_t* scr = tfill + nbins;
+
+    for (uint32_t d = threadIdx.x; d < nbins; d += THREADS) {
+        run[d] = starts[d] + counts[(uint64_t)d * nwg + blockIdx.x];
+        tfill[d] = 0;
+    }
+    const uint64_t beg = (uint64_t)blockIdx.x * chunk;
+    uint64_t end = beg + chunk;
+    if (end > n) end = n;
+    const uint32_t dper = (nbins + THREADS - 1) / THREADS;
+    const uint32_t d0 = threadIdx.x * dper;
+
+    Tup v[ITEMS], nv[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; j++) {
+        const uint64_t i = beg + (uint64_t)j * THREADS + threadIdx.x;
+        if (i < end) v[j] = in[i];
+    }
+    __syncthreads();
+    for (uint64_t base = beg; base < end; base += TILE) {
+        const uint32_t tcount =
+            (uint32_t)((end - base) < (uint64_t)TILE ? (end - base) : TILE);
+        // prefetch the next tile
+        const uint64_t nb = base + TILE;
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint64_t i = nb + (uint64_t)j * THREADS + threadIdx.x;
+            if (i < end) nv[j] = in[i];
+        }
+        uint32_t dg[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint32_t li = j * THREADS + threadIdx.x;
+            dg[j] = li < tcount ? dig(v[j]) : 0xffffffffu;
+            if (dg[j] != 0xffffffffu) atomicAdd(&tfill[dg[j]], 1u);
+        }
+        __syncthreads();
+        uint32_t loc = 0;
+        for (uint32_t k = 0; k < dper; k++)
+            if (d0 + k < nbins) loc += tfill[d0 + k];
+        uint32_t tot;
+        uint32_t ex = block_exclusive_scan(loc, scr, &tot);
+        for (uint32_t k = 0; k < dper; k++) {
+            const uint32_t d = d0 + k;
+            if (d < nbins) {
+                const uint32_t c = tfill[d];
+                tstart[d] = ex;
+                tfill[d] = ex;
+                ex += c;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            if (dg[j] != 0xffffffffu) stage[atomicAdd(&tfill[dg[j]], 1u)] = v[j];
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (uint32_t i = threadIdx.x; i < tcount; i += THREADS) {
+            const Tup t = stage[i];
+            const uint32_t d = dig(t);
+            out[run[d] + (i - tstart[d])] = t;
+        }
+        __syncthreads();
+        for (uint32_t k = 0; k < dper; k++) {
+            const uint32_t d = d0 + k;
+            if (d < nbins) {
+                run[d] += tfill[d] - tstart[d];
+                tfill[d] = 0;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) v[j] = nv[j];
         __syncthreads();
     }
 }
@@ -271,24 +381,9 @@ __global__ void k_hist_global(const Tup* __restrict__ in, uint64_t n, Digit dig,
     for (; i < n; i += stride) atomicAdd(&hist[dig(in[i])], 1ull);
 }
 
-__global__ void k_u64_to_i64(const unsigned long long* a, int64_t* b,
-                             uint32_t m) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < m) b[i] = (int64_t)a[i];
-}
-
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-static size_t scatter_lds_bytes(uint32_t nbins) {
-    size_t b = (size_t)PT_TILE * sizeof(Tup);
-    b += (size_t)nbins * sizeof(uint64_t);
-    b += (size_t)PT_WAVES * nbins * sizeof(uint32_t);
-    b += (size_t)nbins * sizeof(uint32_t);
-    b += 16 * sizeof(uint32_t);
-    return b;
-}
-
 struct LowBits {
     Digit32 inner;
     uint32_t lowbits;
@@ -304,26 +399,50 @@ struct HighBits {
     }
 };
 
-template <class Digit>
-static void stable_partition_narrow(Workspace* ws, const Tup* in, uint64_t n,
-                                    Tup* out, const Digit& dig, uint32_t dbits,
-                                    int padded, uint64_t* starts_dev,
-                                    int64_t* hist_out, int64_t* off_out,
-                                    hipStream_t st) {
+// Scatter geometry (threads x items per thread = LDS tile).  Selected by
+// SMJ_PT_VARIANT for experiments; the default is the measured best.
+// ablation switch for measurements only (SMJ_SCATTER_MODE=1 linear write,
+// 2 no write); the default 0 is the real scatter
+static int scatter_mode() {
+    static int m = -1;
+    if (m < 0) {
+        const char* e = getenv("SMJ_SCATTER_MODE");
+        m = e ? atoi(e) : 0;
+    }
+    return m;
+}
+
+static int pt_variant() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("SMJ_PT_VARIANT");
+        v = e ? atoi(e) : 2;
+        if (v < 0 || v > 2) v = 2;
+    }
+    return v;
+}
+
+template <int THREADS, int ITEMS, bool STABLE, class Digit>
+static void stable_partition_t(Workspace* ws, const Tup* in, uint64_t n,
+                               Tup* out, const Digit& dig, uint32_t dbits,
+                               int padded, uint64_t* starts_dev,
+                               int64_t* hist_out, int64_t* off_out,
+                               hipStream_t st) {
+    constexpr int TILE = THREADS * ITEMS;
     const uint32_t nbins = 1u << dbits;
-    uint64_t ntiles = (n + PT_TILE - 1) / PT_TILE;
+    uint64_t ntiles = (n + TILE - 1) / TILE;
     if (ntiles == 0) ntiles = 1;
-    uint32_t nwg = (uint32_t)(ntiles < 2048 ? ntiles : 2048);
+    const uint32_t maxwg = 256 * 8;
+    uint32_t nwg = (uint32_t)(ntiles < maxwg ? ntiles : maxwg);
     const uint64_t tiles_per_wg = (ntiles + nwg - 1) / nwg;
-    const uint64_t chunk = tiles_per_wg * PT_TILE;
+    const uint64_t chunk = tiles_per_wg * TILE;
     nwg = (uint32_t)((ntiles + tiles_per_wg - 1) / tiles_per_wg);
 
-    uint32_t* counts = (uint32_t*)ws->scratch("pt_counts",
-                                              (size_t)nbins * nwg * 4);
+    uint32_t* counts = (uint32_t*)ws->scratch("pt_counts", (size_t)nbins * nwg * 4);
     uint64_t* totals = (uint64_t*)ws->scratch("pt_totals", (size_t)nbins * 8);
     {
         TraceScope ts(ws, "k_hist", st);
-        hipLaunchKernelGGL(k_hist<Digit>, dim3(nwg), dim3(PT_THREADS),
+        hipLaunchKernelGGL((k_hist<THREADS, ITEMS, Digit>), dim3(nwg), dim3(THREADS),
                            nbins * sizeof(uint32_t), st, in, n, chunk, dig, nbins,
                            counts, nwg);
     }
@@ -335,21 +454,92 @@ static void stable_partition_narrow(Workspace* ws, const Tup* in, uint64_t n,
                            padded, starts_dev, hist_out, off_out);
     }
     if (n == 0) return;
-    const size_t lds = scatter_lds_bytes(nbins);
+    if (!STABLE) {
+        const size_t ldsu = scatter_u_lds<THREADS, ITEMS>(nbins);
+        static bool attr_u = false;
+        if (!attr_u) {
+            SMJ_CHECK(hipFuncSetAttribute(
+                (const void*)k_scatter_u<THREADS, ITEMS, Digit>,
+                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+            attr_u = true;
+        }
+        if (ldsu > 160 * 1024) {
+            fprintf(stderr, "[ERROR] smj: scatter LDS %zu > 160 KiB\n", ldsu);
+            abort();
+        }
+        TraceScope ts(ws, "k_scatter", st);
+        hipLaunchKernelGGL((k_scatter_u<THREADS, ITEMS, Digit>), dim3(nwg),
+                           dim3(THREADS), ldsu, st, in, n, chunk, dig, nbins,
+                           counts, nwg, starts_dev, out);
+        SMJ_CHECK(hipGetLastError());
+        return;
+    }
+    const size_t lds = scatter_lds<THREADS, ITEMS>(nbins);
     static bool attr_set = false;
     if (!attr_set) {
         SMJ_CHECK(hipFuncSetAttribute(
-            (const void*)k_scatter<Digit>,
+            (const void*)k_scatter<THREADS, ITEMS, Digit>,
             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr_set = true;
     }
+    if (lds > 160 * 1024) {
+        fprintf(stderr, "[ERROR] smj: scatter LDS %zu > 160 KiB\n", lds);
+        abort();
+    }
     {
         TraceScope ts(ws, "k_scatter", st);
-        hipLaunchKernelGGL(k_scatter<Digit>, dim3(nwg), dim3(PT_THREADS), lds, st,
-                           in, n, chunk, dig, nbins, dbits, counts, nwg,
-                           starts_dev, out);
+        hipLaunchKernelGGL((k_scatter<THREADS, ITEMS, Digit>), dim3(nwg),
+                           dim3(THREADS), lds, st, in, n, chunk, dig, nbins, dbits,
+                           counts, nwg, starts_dev, out, scatter_mode());
     }
     SMJ_CHECK(hipGetLastError());
+}
+
+template <class Digit>
+static void stable_partition_narrow(Workspace* ws, const Tup* in, uint64_t n,
+                                    Tup* out, const Digit& dig, uint32_t dbits,
+                                    int padded, uint64_t* starts_dev,
+                                    int64_t* hist_out, int64_t* off_out,
+                                    hipStream_t st) {
+    // the big tiles need the 16-bit per-wave counters and <= 160 KiB LDS
+    const int v = dbits > 10 ? 0 : pt_variant();
+    if (v == 2)
+        stable_partition_t<512, 16, true>(ws, in, n, out, dig, dbits, padded,
+                                          starts_dev, hist_out, off_out, st);
+    else if (v == 1)
+        stable_partition_t<256, 16, true>(ws, in, n, out, dig, dbits, padded,
+                                          starts_dev, hist_out, off_out, st);
+    else
+        stable_partition_t<256, 8, true>(ws, in, n, out, dig, dbits, padded,
+                                         starts_dev, hist_out, off_out, st);
+}
+
+// unstable variant (join level 1); SMJ_PTU_VARIANT picks the tile geometry
+static int ptu_variant() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("SMJ_PTU_VARIANT");
+        v = e ? atoi(e) : 2;  // measured: 512x16 tiles are fastest
+        if (v < 0 || v > 2) v = 2;
+    }
+    return v;
+}
+
+template <class Digit>
+static void unstable_partition(Workspace* ws, const Tup* in, uint64_t n,
+                               Tup* out, const Digit& dig, uint32_t dbits,
+                               uint64_t* starts_dev, int64_t* hist_out,
+                               hipStream_t st) {
+    const int v = dbits > 10 ? 0 : ptu_variant();
+    if (v == 2)
+        stable_partition_t<512, 16, false>(ws, in, n, out, dig, dbits, 0, starts_dev,
+                                           hist_out, nullptr, st);
+    else if (v == 1)
+        stable_partition_t<256, 16, false>(ws, in, n, out, dig, dbits, 0, starts_dev,
+                                           hist_out, nullptr, st);
+    else
+        stable_partition_t<256, 8, false>(ws, in, n, out, dig, dbits, 0, starts_dev,
+                                          hist_out, nullptr, st);
 }
 
 void stable_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
@@ -387,24 +577,25 @@ void stable_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
     SMJ_CHECK(hipGetLastError());
 }
 
-// level-1 partition of the join: range-plan digit, unpadded, stable
+// level-1 partition of the join/sort: range-plan digit, unpadded; the order
+// inside a partition is free (every bucket is fully sorted afterwards)
 void plan_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
                     const RangePlan* plan_dev, uint32_t dbits,
                     uint64_t* starts_dev, int64_t* hist_out, hipStream_t st) {
     PlanDigit1 dig{plan_dev};
-    stable_partition_narrow(ws, in, n, out, dig, dbits, 0, starts_dev, hist_out,
-                            nullptr, st);
+    unstable_partition(ws, in, n, out, dig, dbits, starts_dev, hist_out, st);
 }
 
 // histogram-only pass + plain copy (histogram_memcpy_bench)
 void hist_memcpy(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
                  uint32_t dbits, hipStream_t st) {
+    constexpr int THREADS = 256, ITEMS = 8, TILE = THREADS * ITEMS;
     const uint32_t nbins = 1u << dbits;
-    uint64_t ntiles = (n + PT_TILE - 1) / PT_TILE;
+    uint64_t ntiles = (n + TILE - 1) / TILE;
     if (ntiles == 0) ntiles = 1;
     uint32_t nwg = (uint32_t)(ntiles < 2048 ? ntiles : 2048);
     const uint64_t tiles_per_wg = (ntiles + nwg - 1) / nwg;
-    const uint64_t chunk = tiles_per_wg * PT_TILE;
+    const uint64_t chunk = tiles_per_wg * TILE;
     nwg = (uint32_t)((ntiles + tiles_per_wg - 1) / tiles_per_wg);
     uint32_t* counts = (uint32_t*)ws->scratch("pt_counts", (size_t)nbins * nwg * 4);
     Digit32 dig{nbins - 1u, 0u};
@@ -413,7 +604,7 @@ void hist_memcpy(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
         SMJ_CHECK(hipMemsetAsync(h, 0, (size_t)nbins * 8, st));
         if (n) hipLaunchKernelGGL(k_hist_global<Digit32>, dim3(1024), dim3(256), 0, st, in, n, dig, h);
     } else {
-        hipLaunchKernelGGL(k_hist<Digit32>, dim3(nwg), dim3(PT_THREADS),
+        hipLaunchKernelGGL((k_hist<THREADS, ITEMS, Digit32>), dim3(nwg), dim3(THREADS),
                            nbins * sizeof(uint32_t), st, in, n, chunk, dig, nbins,
                            counts, nwg);
     }
