@@ -10,20 +10,24 @@
 //                loaded into registers, counted by its level-2 digit d2 in an
 //                LDS histogram, staged in LDS grouped by d2 and written back in
 //                place, linearly (fully coalesced), together with the tile's
-//                exclusive d2 prefix (uint16 per digit).  Traffic: 2w.
-//   k_subwave  : ONE WAVE per sub-bucket (b, d2) at a time -- no workgroup
-//                barriers, eight independent waves per workgroup, and a
-//                software pipeline inside every wave: while sub-bucket s is
-//                sorted in LDS, the tuples of s+1 and the tile prefixes of s+2
-//                are already in flight.  A wave gathers the sub-bucket's piece
-//                from every tile of bucket b for R and S in one round trip
-//                (contiguous runs, read by consecutive lanes), counting-sorts
-//                them in its private LDS slice by the level-3 digit, fixes
-//                equal-digit runs with an insertion sort on the full
-//                (key, payload) order, writes the sorted sub-bucket to its
-//                final position, and -- for a join -- counts the matching pairs
-//                of the two resident sub-buckets.  Traffic: 2w; the join reads
-//                nothing more.
+//                exclusive d2 prefix (uint16 per digit + a sentinel = length).
+//                Traffic: 2w.
+//   k_subwave  : ONE WAVE per sub-bucket (b, d2) at a time, twelve independent
+//                waves per CU, no workgroup barriers.  The wave gathers the
+//                sub-bucket's piece from every tile of bucket b (contiguous
+//                runs read by consecutive lanes; the piece of a lane is found
+//                with one ballot over a piece-start map instead of a search),
+//                counting-sorts it in its private LDS slice by the level-3
+//                digit, fixes equal-digit runs with an insertion sort on the
+//                full (key, payload) order and writes the sorted sub-bucket to
+//                its final position -- R first, then S in the same LDS slice --
+//                and, for a join, counts the matching pairs of the two
+//                sub-buckets from their level-3 histograms (exact digits) or
+//                by binary search in R's sorted keys.  Traffic: 2w; the join
+//                reads nothing more.  The eight-to-twelve waves of a workgroup
+//                take neighbouring sub-buckets at the same time, so the cache
+//                lines shared at piece boundaries and the 128-byte lines of the
+//                prefix table are served from L1/L2, not refetched.
 //
 // Sub-buckets that do not fit the per-wave LDS capacity, or that hold long
 // runs of equal digits (skew, e.g. Zipf hot keys), are queued and finished by
@@ -37,12 +41,12 @@ constexpr int TP_THREADS = 256;
 constexpr int TP_ITEMS = 16;
 constexpr int TILE2 = TP_THREADS * TP_ITEMS;  // 4096 tuples per tile
 
-constexpr int SW_WAVES = 8;  // waves per workgroup, one sub-bucket each
-constexpr int SW_THREADS = SW_WAVES * 64;
 #ifdef KEY_8B
-constexpr int SW_CAP = 448;  // tuples per relation per sub-bucket
+constexpr int SW_CAP = 384;  // tuples per sub-bucket per relation in LDS
+typedef int64_t KeyT;
 #else
-constexpr int SW_CAP = 896;
+constexpr int SW_CAP = 768;
+typedef int32_t KeyT;
 #endif
 constexpr int SW_ITEMS = SW_CAP / 64;
 constexpr int SW_D3MAX = 8;  // level-3 bins per wave (256)
@@ -55,7 +59,7 @@ struct TileTable {
     uint32_t* len;     // tile length
     uint32_t* bucket;  // owning bucket
     uint32_t* btile0;  // first tile of every bucket (nbuckets + 1)
-    uint16_t* pref;    // [tile][nb2] exclusive prefix
+    uint16_t* pref;    // [tile][nb2 + 1] exclusive prefix, sentinel = length
     uint32_t* ntiles;  // device scalar
 };
 
@@ -144,7 +148,9 @@ k_tilepass(const Tup* __restrict__ part, Tup* __restrict__ tmp, TileTable tt,
         if (d0 + k < nb2) loc += hist[d0 + k];
     uint32_t tot;
     uint32_t ex = block_exclusive_scan(loc, scr, &tot);
-    uint16_t* pref = tt.pref + (uint64_t)t * nb2;
+    // row of nb2 + 1 entries: the sentinel pref[nb2] = tile length lets the
+    // bucket pass read [pref[d2], pref[d2+1]) without a select
+    uint16_t* pref = tt.pref + (uint64_t)t * (nb2 + 1);
     for (uint32_t k = 0; k < per; k++) {
         uint32_t d = d0 + k;
         if (d < nb2) {
@@ -154,6 +160,7 @@ k_tilepass(const Tup* __restrict__ part, Tup* __restrict__ tmp, TileTable tt,
             ex += c;
         }
     }
+    if (threadIdx.x == 0) pref[nb2] = (uint16_t)len;
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < TP_ITEMS; j++) {
@@ -188,15 +195,20 @@ struct SubWaveArgs {
     uint32_t ovf_cap;
 };
 
-// per-wave LDS slice (<= 20 KiB: eight waves share one CU's 160 KiB)
+// per-wave LDS slice; R and S pass through B one after the other
 struct WaveLDS {
-    Tup B[2][SW_CAP];
-    uint32_t h[2][SW_NB3];  // bin starts after the scan
+    Tup B[SW_CAP];
+    KeyT rkey[SW_CAP];       // R's sorted keys (generic join)
+    uint32_t h[2][SW_NB3];   // level-3 bin starts of R and S
     uint32_t fill[SW_NB3];
-    uint32_t psrc[2][2][SW_PMAX];  // [pipeline buffer][relation][piece]
-    uint32_t pdst[2][2][SW_PMAX];
+    uint32_t psrc[SW_PMAX];  // piece start, relative to the bucket start
+    uint32_t pdst[SW_PMAX];  // piece position inside the sub-bucket
+    uint8_t pat[SW_CAP];     // piece starting at a position, 0xff = none
 };
-static_assert(sizeof(WaveLDS) * SW_WAVES <= 160 * 1024, "LDS budget");
+constexpr int SW_WAVES_RAW = (160 * 1024) / (int)sizeof(WaveLDS);
+constexpr int SW_WAVES = SW_WAVES_RAW > 16 ? 16 : SW_WAVES_RAW;
+constexpr int SW_THREADS = SW_WAVES * 64;
+static_assert(SW_WAVES >= 8, "LDS slice too large");
 
 // order this wave's LDS accesses (LDS executes one wave's instructions in
 // order; the fences stop the compiler from moving accesses across)
@@ -225,18 +237,6 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
     return x;
 }
 
-// last piece with pdst <= i: with non-decreasing pdst this is the piece that
-// holds position i (empty pieces after it start beyond i)
-__device__ __forceinline__ uint32_t wave_piece_of(const uint32_t* pdst,
-                                                  uint32_t np, uint32_t i) {
-    uint32_t lo = 0, hi = np;
-    while (hi - lo > 1) {
-        uint32_t m = (lo + hi) >> 1;
-        if (pdst[m] <= i) lo = m; else hi = m;
-    }
-    return lo;
-}
-
 __device__ __forceinline__ void lds_insertion_sort(Tup* a, uint32_t n) {
     for (uint32_t i = 1; i < n; i++) {
         Tup x = a[i];
@@ -249,130 +249,30 @@ __device__ __forceinline__ void lds_insertion_sort(Tup* a, uint32_t n) {
     }
 }
 
-// wave-uniform description of one sub-bucket
-struct SubHead {
-    uint32_t b, d2;
-    bool live;  // a sub-bucket of this wave whose digit exists
-    uint32_t t0[2], nt[2];
-    uint64_t bst[2];
-};
-// per-lane tile prefixes of one sub-bucket (lane = tile index in the bucket)
-struct SubPref {
-    uint32_t lo[2], cnt[2];
-};
-// wave-uniform piece summary
-struct SubPieces {
-    uint32_t n[2];
-    uint64_t off[2];
-    bool ovf;
-};
-
-__device__ __forceinline__ SubHead sub_head(const SubWaveArgs& A, uint32_t s,
-                                            uint32_t s_end, uint32_t d2lim) {
-    SubHead H;
-    H.b = s / A.nb2;
-    H.d2 = s % A.nb2;
-    H.live = s < s_end && H.d2 < d2lim;
-    for (int r = 0; r < 2; r++) {
-        H.t0[r] = 0;
-        H.nt[r] = 0;
-        H.bst[r] = 0;
-    }
-    if (H.live) {
-        _Pragma("unroll") for (int r = 0; r < 2; r++) { if (r >= A.nrel) break;
-            H.t0[r] = A.tt[r].btile0[H.b];
-            H.nt[r] = A.tt[r].btile0[H.b + 1] - H.t0[r];
-            H.bst[r] = A.bstart[r][H.b];
-        }
-    }
-    return H;
-}
-
-__device__ __forceinline__ SubPref sub_pref(const SubWaveArgs& A,
-                                            const SubHead& H, int lane) {
-    SubPref P;
-    for (int r = 0; r < 2; r++) {
-        P.lo[r] = 0;
-        P.cnt[r] = 0;
-        if (r < A.nrel && H.live && (uint32_t)lane < H.nt[r] && H.nt[r] <= SW_PMAX) {
-            const uint32_t t = H.t0[r] + lane;
-            const uint16_t* pf = A.tt[r].pref + (uint64_t)t * A.nb2;
-            const uint32_t lo = pf[H.d2];
-            const uint32_t hi = (H.d2 + 1 < A.nb2) ? pf[H.d2 + 1] : A.tt[r].len[t];
-            P.lo[r] = lo;
-            P.cnt[r] = hi - lo;
-        }
-    }
-    return P;
-}
-
-// piece table of one sub-bucket into pipeline buffer `buf`
-__device__ __forceinline__ SubPieces sub_pieces(const SubWaveArgs& A,
-                                                const SubHead& H,
-                                                const SubPref& P, WaveLDS& L,
-                                                int buf, int lane) {
-    SubPieces X;
-    X.ovf = false;
-    for (int r = 0; r < 2; r++) {
-        X.n[r] = 0;
-        X.off[r] = 0;
-    }
-    if (!H.live) return X;
-    _Pragma("unroll") for (int r = 0; r < 2; r++) { if (r >= A.nrel) break;
-        if (H.nt[r] > SW_PMAX) {
-            X.ovf = true;
-            continue;
-        }
-        const uint32_t incl = wave_incl_scan(P.cnt[r]);
-        X.n[r] = __shfl(incl, 63, 64);
-        X.off[r] = wave_sum((unsigned long long)P.lo[r]);
-        if ((uint32_t)lane < H.nt[r]) {
-            L.psrc[buf][r][lane] = lane * (uint32_t)TILE2 + P.lo[r];
-            L.pdst[buf][r][lane] = incl - P.cnt[r];
-        }
-        if (X.n[r] > SW_CAP) X.ovf = true;
-    }
-    return X;
-}
-
-__device__ __forceinline__ void sub_load(const SubWaveArgs& A, const SubHead& H,
-                                         const SubPieces& X, const WaveLDS& L,
-                                         int buf, int lane,
-                                         Tup (&v)[2][SW_ITEMS]) {
-    if (!H.live || X.ovf) return;
-    _Pragma("unroll") for (int r = 0; r < 2; r++) { if (r >= A.nrel) break;
-        const Tup* tp = A.tmp[r] + H.bst[r];
-#pragma unroll
-        for (int k = 0; k < SW_ITEMS; k++) {
-            const uint32_t i = k * 64 + lane;
-            if (i < X.n[r]) {
-                const uint32_t p = wave_piece_of(L.pdst[buf][r], H.nt[r], i);
-                v[r][k] = tp[L.psrc[buf][r][p] + (i - L.pdst[buf][r][p])];
-            }
-        }
-    }
-}
-
-__device__ void sub_overflow(const SubWaveArgs& A, const SubHead& H, int lane) {
+__device__ void sub_overflow(const SubWaveArgs& A, uint32_t b, uint32_t d2,
+                             const uint32_t* n, const uint64_t* off,
+                             bool sizes_known, int lane) {
     if (lane != 0) return;
-    // the fallback needs the size of the sub-bucket in every relation
     uint32_t n2[2] = {0, 0};
     uint64_t o2[2] = {0, 0};
-    _Pragma("unroll") for (int r = 0; r < 2; r++) { if (r >= A.nrel) break;
+    for (int r = 0; r < A.nrel; r++) {
+        if (sizes_known) {
+            n2[r] = n[r];
+            o2[r] = off[r];
+            continue;
+        }
         const TileTable& tt = A.tt[r];
-        for (uint32_t t = tt.btile0[H.b]; t < tt.btile0[H.b + 1]; t++) {
-            const uint16_t* pf = tt.pref + (uint64_t)t * A.nb2;
-            const uint32_t lo = pf[H.d2];
-            const uint32_t hi = (H.d2 + 1 < A.nb2) ? pf[H.d2 + 1] : tt.len[t];
-            n2[r] += hi - lo;
-            o2[r] += lo;
+        for (uint32_t t = tt.btile0[b]; t < tt.btile0[b + 1]; t++) {
+            const uint16_t* pf = tt.pref + (uint64_t)t * (A.nb2 + 1);
+            n2[r] += (uint32_t)pf[d2 + 1] - pf[d2];
+            o2[r] += pf[d2];
         }
     }
     const uint32_t k = atomicAdd(A.novf, 1u);
     if (k < A.ovf_cap) {
         OvfEntry e;
-        e.bucket = H.b;
-        e.d2 = H.d2;
+        e.bucket = b;
+        e.d2 = d2;
         e.nr[0] = n2[0];
         e.nr[1] = n2[1];
         e.off[0] = o2[0];
@@ -381,174 +281,206 @@ __device__ void sub_overflow(const SubWaveArgs& A, const SubHead& H, int lane) {
     }
 }
 
-// sort the resident sub-bucket in LDS, write it out, count join matches
-__device__ __forceinline__ void sub_process(const SubWaveArgs& A,
-                                            const RangePlan& P,
-                                            const SubHead& H,
-                                            const SubPieces& X, WaveLDS& L,
-                                            int lane, Tup (&v)[2][SW_ITEMS],
-                                            unsigned long long& matches) {
-    if (!H.live) return;
-    if (X.ovf) {
-        sub_overflow(A, H, lane);
-        return;
-    }
-    const uint32_t nb3 = 1u << P.D3;
-    const uint64_t bu = key_u(P.base);
-    const uint32_t d12 = (H.b << P.D2) | H.d2;
-    bool clamp = false;
-    uint32_t mx = 0;
-    // ---- level-3 histograms of both relations
-    _Pragma("unroll") for (int r = 0; r < 2; r++) { if (r >= A.nrel) break;
-#pragma unroll
-        for (int q = 0; q < SW_NB3 / 64; q++) L.h[r][lane * (SW_NB3 / 64) + q] = 0;
-    }
-    wave_lds_sync();
-    _Pragma("unroll") for (int r = 0; r < 2; r++) { if (r >= A.nrel) break;
-#pragma unroll
-        for (int k = 0; k < SW_ITEMS; k++) {
-            const uint32_t i = k * 64 + lane;
-            if (i < X.n[r]) {
-                const int64_t key = tup_key(v[r][k]);
-                const uint64_t ku = key_u(key);
-                clamp |= (ku < bu) || (ku - bu > P.span);
-                atomicAdd(&L.h[r][plan_d3(P, plan_rel(P, key), d12)], 1u);
-            }
-        }
-    }
-    wave_lds_sync();
-    // ---- exclusive scans: lane owns 4 consecutive bins
-    uint32_t c[2][SW_NB3 / 64];
-    _Pragma("unroll") for (int r = 0; r < 2; r++) { if (r >= A.nrel) break;
-        uint32_t loc = 0;
-#pragma unroll
-        for (int q = 0; q < SW_NB3 / 64; q++) {
-            c[r][q] = L.h[r][lane * (SW_NB3 / 64) + q];
-            loc += c[r][q];
-            mx = c[r][q] > mx ? c[r][q] : mx;
-        }
-        uint32_t ex = wave_incl_scan(loc) - loc;
-#pragma unroll
-        for (int q = 0; q < SW_NB3 / 64; q++) {
-            L.h[r][lane * (SW_NB3 / 64) + q] = ex;
-            ex += c[r][q];
-        }
-    }
-    if (wave_max(mx) > SW_RUNMAX) {
-        wave_lds_sync();
-        sub_overflow(A, H, lane);
-        return;
-    }
-    const bool any_clamp = __any(clamp);
-    // ---- place, fix runs, write
-    _Pragma("unroll") for (int r = 0; r < 2; r++) { if (r >= A.nrel) break;
-        const uint32_t n = X.n[r];
-#pragma unroll
-        for (int q = 0; q < SW_NB3 / 64; q++)
-            L.fill[lane * (SW_NB3 / 64) + q] = L.h[r][lane * (SW_NB3 / 64) + q];
-        wave_lds_sync();
-#pragma unroll
-        for (int k = 0; k < SW_ITEMS; k++) {
-            const uint32_t i = k * 64 + lane;
-            if (i < n) {
-                const uint32_t d = plan_d3(P, plan_rel(P, tup_key(v[r][k])), d12);
-                const uint32_t pos = atomicAdd(&L.fill[d], 1u);
-                L.B[r][pos] = v[r][k];
-            }
-        }
-        wave_lds_sync();
-        for (uint32_t d = lane; d < nb3; d += 64) {
-            const uint32_t s0 = L.h[r][d];
-            const uint32_t e0 = (d + 1 < nb3) ? L.h[r][d + 1] : n;
-            if (e0 - s0 > 1) lds_insertion_sort(L.B[r] + s0, e0 - s0);
-        }
-        wave_lds_sync();
-        Tup* dst = A.out[r] + H.bst[r] + X.off[r];
-        for (uint32_t i = lane; i < n; i += 64) dst[i] = L.B[r][i];
-    }
-    // ---- merge-join count of the two resident sub-buckets
-    if (A.nrel == 2) {
-        const uint32_t nR = X.n[0], nS = X.n[1];
-        if (P.s3 == 0 && !any_clamp) {
-            // the level-3 digit is the exact key: sum_k |R_k| * |S_k|
-            for (uint32_t d = lane; d < nb3; d += 64) {
-                const uint32_t cr = ((d + 1 < nb3) ? L.h[0][d + 1] : nR) - L.h[0][d];
-                const uint32_t cs = ((d + 1 < nb3) ? L.h[1][d + 1] : nS) - L.h[1][d];
-                matches += (unsigned long long)cr * cs;
-            }
-        } else {
-            for (uint32_t i = lane; i < nS; i += 64) {
-                const int64_t k = tup_key(L.B[1][i]);
-                if (i > 0 && tup_key(L.B[1][i - 1]) == k) continue;
-                uint32_t e = i + 1;
-                while (e < nS && tup_key(L.B[1][e]) == k) e++;
-                uint32_t lo = 0, hi = nR;
-                while (lo < hi) {
-                    const uint32_t m = (lo + hi) >> 1;
-                    if (tup_key(L.B[0][m]) < k) lo = m + 1; else hi = m;
-                }
-                const uint32_t lb = lo;
-                hi = nR;
-                while (lo < hi) {
-                    const uint32_t m = (lo + hi) >> 1;
-                    if (tup_key(L.B[0][m]) <= k) lo = m + 1; else hi = m;
-                }
-                matches += (unsigned long long)(lo - lb) * (e - i);
-            }
-        }
-    }
-    wave_lds_sync();
-}
-
 __global__ void __launch_bounds__(SW_THREADS)
 k_subwave(SubWaveArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     WaveLDS& L = reinterpret_cast<WaveLDS*>(lds_raw)[threadIdx.x >> 6];
     const RangePlan P = *A.plan_dev;
+    const uint32_t nb2 = A.nb2;
+    const uint32_t nb3 = 1u << P.D3;
     const uint32_t d2lim = 1u << P.D2;
     const int lane = lane_id();
+    const uint64_t lmask_le = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+    const uint64_t bu = key_u(P.base);
 
-    // The workgroup owns sub-buckets [g0, g1); its eight waves take them
-    // interleaved (wave w: g0+w, g0+w+8, ...) so that neighbouring
-    // sub-buckets -- which share the cache lines at their piece boundaries
-    // and the 128-byte lines of the tile prefix table -- are read by the
-    // same CU at the same time (L1/L2 hits instead of refetches).
+    // the workgroup owns [g0, s_end); its waves take them interleaved
     const uint32_t g0 = blockIdx.x * SW_WAVES * A.spw;
     uint32_t s_end = g0 + SW_WAVES * A.spw;
     if (s_end > A.nsub) s_end = A.nsub;
-    const uint32_t s_begin = g0 + (threadIdx.x >> 6);
-    constexpr uint32_t SS = SW_WAVES;  // sub-bucket stride of a wave
     unsigned long long matches = 0;
+    uint32_t cur_b = 0xffffffffu;
+    uint32_t t0[2] = {0, 0}, nt[2] = {0, 0};
+    uint64_t bst[2] = {0, 0};
 
-    // software pipeline: cur = loaded tuples in flight, nxt = prefixes in flight
-    int buf = 0;
-    SubHead Hc = sub_head(A, s_begin, s_end, d2lim);
-    SubPref Pc = sub_pref(A, Hc, lane);
-    SubHead Hn = sub_head(A, s_begin + SS, s_end, d2lim);
-    SubPref Pn = sub_pref(A, Hn, lane);
-    SubPieces Xc = sub_pieces(A, Hc, Pc, L, buf, lane);
-    wave_lds_sync();
-    Tup vc[2][SW_ITEMS];
-    Tup vn[2][SW_ITEMS];
-    sub_load(A, Hc, Xc, L, buf, lane, vc);
-    for (uint32_t s = s_begin; s < s_end; s += SS) {
-        // pieces + tuple loads of the next sub-bucket, prefixes of the one after
-        SubPieces Xn = sub_pieces(A, Hn, Pn, L, buf ^ 1, lane);
-        wave_lds_sync();
-        sub_load(A, Hn, Xn, L, buf ^ 1, lane, vn);
-        SubHead Hnn = sub_head(A, s + 2 * SS, s_end, d2lim);
-        SubPref Pnn = sub_pref(A, Hnn, lane);
-        // sort / write / join s
-        sub_process(A, P, Hc, Xc, L, lane, vc, matches);
+    for (uint32_t s = g0 + (threadIdx.x >> 6); s < s_end; s += SW_WAVES) {
+        const uint32_t b = s / nb2;
+        const uint32_t d2 = s % nb2;
+        if (d2 >= d2lim) continue;  // a table column no digit maps to
+        if (b != cur_b) {
+            cur_b = b;
 #pragma unroll
-        for (int r = 0; r < 2; r++)
+            for (int r = 0; r < 2; r++) {
+                if (r < A.nrel) {
+                    t0[r] = A.tt[r].btile0[b];
+                    nt[r] = A.tt[r].btile0[b + 1] - t0[r];
+                    bst[r] = A.bstart[r][b];
+                }
+            }
+        }
+        // ---- sizes of the sub-bucket in both relations (one round trip)
+        uint32_t n[2] = {0, 0}, plo[2] = {0, 0}, pcnt[2] = {0, 0}, pincl[2] = {0, 0};
+        uint64_t off[2] = {0, 0};
+        bool ovf = false, known = true;
 #pragma unroll
-            for (int k = 0; k < SW_ITEMS; k++) vc[r][k] = vn[r][k];
-        Hc = Hn;
-        Xc = Xn;
-        Hn = Hnn;
-        Pn = Pnn;
-        buf ^= 1;
+        for (int r = 0; r < 2; r++) {
+            if (r >= A.nrel) break;
+            if (nt[r] > SW_PMAX) {
+                ovf = true;
+                known = false;
+                continue;
+            }
+            if ((uint32_t)lane < nt[r]) {
+                const uint16_t* pf =
+                    A.tt[r].pref + (uint64_t)(t0[r] + lane) * (nb2 + 1) + d2;
+                plo[r] = pf[0];
+                pcnt[r] = (uint32_t)pf[1] - plo[r];
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+            if (r >= A.nrel || nt[r] > SW_PMAX) continue;
+            pincl[r] = wave_incl_scan(pcnt[r]);
+            n[r] = __shfl(pincl[r], 63, 64);
+            off[r] = wave_sum((unsigned long long)plo[r]);
+            if (n[r] > SW_CAP) ovf = true;
+        }
+        if (ovf) {
+            sub_overflow(A, b, d2, n, off, known, lane);
+            continue;
+        }
+
+        const uint32_t d12 = (b << P.D2) | d2;
+        bool clamped = false;
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+            if (r >= A.nrel) break;
+            const uint32_t nr = n[r];
+            // ---- piece tables and the piece-start map
+            if ((uint32_t)lane < nt[r]) {
+                L.psrc[lane] = lane * (uint32_t)TILE2 + plo[r];
+                L.pdst[lane] = pincl[r] - pcnt[r];
+            }
+            for (uint32_t j = lane; j < SW_CAP / 4; j += 64)
+                reinterpret_cast<uint32_t*>(L.pat)[j] = 0xffffffffu;
+#pragma unroll
+            for (int q = 0; q < SW_NB3 / 64; q++) L.h[r][lane * (SW_NB3 / 64) + q] = 0;
+            wave_lds_sync();
+            if ((uint32_t)lane < nt[r] && pcnt[r] > 0)
+                L.pat[pincl[r] - pcnt[r]] = (uint8_t)lane;
+            wave_lds_sync();
+
+            // ---- gather: the piece of position i is the last piece start <= i
+            Tup v[SW_ITEMS];
+            uint32_t dg[SW_ITEMS];
+            const Tup* tp = A.tmp[r] + bst[r];
+            uint32_t carry = 0;
+#pragma unroll
+            for (int k = 0; k < SW_ITEMS; k++) {
+                const uint32_t i = k * 64 + lane;
+                const bool valid = i < nr;
+                const uint32_t m = valid ? L.pat[i] : 0xffu;
+                const uint64_t starts = __ballot(m != 0xffu) & lmask_le;
+                const uint32_t src_lane = starts ? 63 - __clzll(starts) : 0;
+                const uint32_t pm = __shfl(m, src_lane, 64);
+                const uint32_t p = starts ? pm : carry;
+                carry = __shfl(p, 63, 64);
+                if (valid) v[k] = tp[L.psrc[p] + (i - L.pdst[p])];
+            }
+            // ---- level-3 digits, histogram
+#pragma unroll
+            for (int k = 0; k < SW_ITEMS; k++) {
+                const uint32_t i = k * 64 + lane;
+                if (i < nr) {
+                    const int64_t key = tup_key(v[k]);
+                    const uint64_t ku = key_u(key);
+                    clamped |= (ku < bu) || (ku - bu > P.span);
+                    dg[k] = plan_d3(P, plan_rel(P, key), d12);
+                    atomicAdd(&L.h[r][dg[k]], 1u);
+                }
+            }
+            wave_lds_sync();
+            // ---- exclusive scan of the bins: lane owns 4 consecutive bins
+            uint32_t c[SW_NB3 / 64];
+            uint32_t loc = 0, mx = 0;
+#pragma unroll
+            for (int q = 0; q < SW_NB3 / 64; q++) {
+                c[q] = L.h[r][lane * (SW_NB3 / 64) + q];
+                loc += c[q];
+                mx = c[q] > mx ? c[q] : mx;
+            }
+            uint32_t ex = wave_incl_scan(loc) - loc;
+#pragma unroll
+            for (int q = 0; q < SW_NB3 / 64; q++) {
+                L.h[r][lane * (SW_NB3 / 64) + q] = ex;
+                L.fill[lane * (SW_NB3 / 64) + q] = ex;
+                ex += c[q];
+            }
+            if (wave_max(mx) > SW_RUNMAX) {
+                ovf = true;
+                break;
+            }
+            wave_lds_sync();
+            // ---- place, fix equal-digit runs, write
+#pragma unroll
+            for (int k = 0; k < SW_ITEMS; k++) {
+                const uint32_t i = k * 64 + lane;
+                if (i < nr) L.B[atomicAdd(&L.fill[dg[k]], 1u)] = v[k];
+            }
+            wave_lds_sync();
+            for (uint32_t d = lane; d < nb3; d += 64) {
+                const uint32_t s0 = L.h[r][d];
+                const uint32_t e0 = (d + 1 < nb3) ? L.h[r][d + 1] : nr;
+                if (e0 - s0 > 1) lds_insertion_sort(L.B + s0, e0 - s0);
+            }
+            wave_lds_sync();
+            Tup* dst = A.out[r] + bst[r] + off[r];
+            for (uint32_t i = lane; i < nr; i += 64) {
+                const Tup t = L.B[i];
+                dst[i] = t;
+                if (r == 0) L.rkey[i] = (KeyT)tup_key(t);
+            }
+            wave_lds_sync();
+        }
+        if (ovf) {
+            // a long equal-digit run: the fallback re-sorts the sub-bucket of
+            // both relations (an R already written here is simply rewritten)
+            sub_overflow(A, b, d2, n, off, true, lane);
+            continue;
+        }
+
+        // ---- merge-join count of the two sub-buckets
+        if (A.nrel == 2) {
+            const uint32_t nR = n[0], nS = n[1];
+            if (P.s3 == 0 && !__any(clamped)) {
+                // the level-3 digit is the exact key: sum_k |R_k| * |S_k|
+                for (uint32_t d = lane; d < nb3; d += 64) {
+                    const uint32_t cr = ((d + 1 < nb3) ? L.h[0][d + 1] : nR) - L.h[0][d];
+                    const uint32_t cs = ((d + 1 < nb3) ? L.h[1][d + 1] : nS) - L.h[1][d];
+                    matches += (unsigned long long)cr * cs;
+                }
+            } else {
+                // S is still in B, R's sorted keys in rkey
+                for (uint32_t i = lane; i < nS; i += 64) {
+                    const int64_t k = tup_key(L.B[i]);
+                    if (i > 0 && tup_key(L.B[i - 1]) == k) continue;
+                    uint32_t e = i + 1;
+                    while (e < nS && tup_key(L.B[e]) == k) e++;
+                    uint32_t lo = 0, hi = nR;
+                    while (lo < hi) {
+                        const uint32_t m = (lo + hi) >> 1;
+                        if ((int64_t)L.rkey[m] < k) lo = m + 1; else hi = m;
+                    }
+                    const uint32_t lb = lo;
+                    hi = nR;
+                    while (lo < hi) {
+                        const uint32_t m = (lo + hi) >> 1;
+                        if ((int64_t)L.rkey[m] <= k) lo = m + 1; else hi = m;
+                    }
+                    matches += (unsigned long long)(lo - lb) * (e - i);
+                }
+            }
+            wave_lds_sync();
+        }
     }
     if (A.nrel == 2) {
         matches = wave_sum(matches);
@@ -567,9 +499,9 @@ k_gather_sub(const Tup* __restrict__ tmp, Tup* __restrict__ out,
     Tup* dst = out + bstart[b] + e.off[r];
     uint32_t pos = 0;
     for (uint32_t t = tt.btile0[b]; t < tt.btile0[b + 1]; t++) {
-        const uint16_t* pf = tt.pref + (uint64_t)t * nb2;
+        const uint16_t* pf = tt.pref + (uint64_t)t * (nb2 + 1);
         uint32_t lo = pf[d2];
-        uint32_t hi = (d2 + 1 < nb2) ? pf[d2 + 1] : tt.len[t];
+        uint32_t hi = pf[d2 + 1];
         const Tup* src = tmp + tt.off[t] + lo;
         for (uint32_t i = threadIdx.x; i < hi - lo; i += 256) dst[pos + i] = src[i];
         pos += hi - lo;
@@ -661,7 +593,7 @@ void bucket_sort(Workspace* ws, const BucketSortArgs& a, uint32_t D2,
         tt[r].len = (uint32_t*)ws->scratch(names[r][1], maxt[r] * 4);
         tt[r].bucket = (uint32_t*)ws->scratch(names[r][2], maxt[r] * 4);
         tt[r].btile0 = (uint32_t*)ws->scratch(names[r][3], (nb + 1) * 4);
-        tt[r].pref = (uint16_t*)ws->scratch(names[r][4], maxt[r] * nb2 * 2);
+        tt[r].pref = (uint16_t*)ws->scratch(names[r][4], maxt[r] * (nb2 + 1) * 2);
         tt[r].ntiles = (uint32_t*)ws->scratch(names[r][5], 4);
         hipLaunchKernelGGL(k_tiles, dim3(1), dim3(256), 0, st, a.bstart[r],
                            a.bcount[r], nb, tt[r]);
@@ -703,12 +635,11 @@ void bucket_sort(Workspace* ws, const BucketSortArgs& a, uint32_t D2,
     B.count_dev = a.count_dev;
     B.nb2 = nb2;
     B.nsub = nsub;
-    // one resident wave per SIMD slot (8 waves/CU), several sub-buckets each
+    // one workgroup of SW_WAVES waves per CU, several sub-buckets per wave
     const uint32_t target_waves = 256 * SW_WAVES;
     B.spw = (nsub + target_waves - 1) / target_waves;
     if (B.spw == 0) B.spw = 1;
-    const uint32_t nwaves = (nsub + B.spw - 1) / B.spw;
-    const uint32_t nwg = (nwaves + SW_WAVES - 1) / SW_WAVES;
+    const uint32_t nwg = (nsub + SW_WAVES * B.spw - 1) / (SW_WAVES * B.spw);
     B.ovf = ovf;
     B.novf = novf;
     B.ovf_cap = ovf_cap;

@@ -110,7 +110,8 @@ static uint32_t ceil_log2(uint64_t x) {
 // expected sub-bucket is a few hundred tuples (fits the in-LDS bucket pass)
 static void choose_levels(uint64_t n, uint32_t want_d1, uint32_t* D1,
                           uint32_t* D2) {
-    const uint64_t target = (sizeof(Tup) == 16) ? 320 : 640;
+    // mean sub-bucket <= 2/3 of the per-wave LDS capacity (384 / 768 tuples)
+    const uint64_t target = (sizeof(Tup) == 16) ? 256 : 512;
     uint32_t B = n > target ? ceil_log2((n + target - 1) / target) : 0;
     uint32_t d1 = want_d1 ? want_d1 : 10;
     if (d1 > B) d1 = B;
