@@ -57,7 +57,7 @@ def alg_bytes_per_launch(name, n_rel, nR, nS, w):
         "k_hist": n_rel * w,
         "k_scatter": 2 * n_rel * w,
         "k_tilepass": 2 * n_rel * w,
-        "k_bucketpass": 2 * (nR + nS) * w,
+        "k_subwave": 2 * (nR + nS) * w,
     }.get(name)
 
 
@@ -160,42 +160,11 @@ def main():
         def step():
             lib.dev_join(R, S, sR, sS, count, a.fanout_bits, 1, total)
     else:
-        D1 = a.fanout_bits
-        F = 1 << D1
-        assert F % N == 0
-        partR, partS = lib.empty(n), lib.empty(n)
-        hR = torch.zeros(F, dtype=torch.int64, device="cuda")
-        hS = torch.zeros(F, dtype=torch.int64, device="cuda")
-        per = F // N
-        lo_key = 1 + (rank * per) * ((total + F - 1) // F)
-        # receive buffers sized on the first step (inputs are fixed)
-        state = {}
-
-        def exchange(part, hist, key):
-            send = hist.view(N, per).sum(1)
-            recv = torch.empty_like(send)
-            dist.all_to_all_single(recv, send)
-            sl, rl = send.tolist(), recv.tolist()
-            cap = state.get(key)
-            if cap is None or cap.shape[0] < sum(rl):
-                cap = lib.empty(max(sum(rl), 1))
-                state[key] = cap
-            out = cap[: sum(rl)]
-            dist.all_to_all_single(out, part, rl, sl)
-            return out
+        from smj.dist import DeviceOps, DistributedJoin
+        dj = DistributedJoin(DeviceOps(lib), a.fanout_bits, 1, total)
 
         def step():
-            lib.dev_partition_range(R, partR, D1, 1, total, hR)
-            lib.dev_partition_range(S, partS, D1, 1, total, hS)
-            rR = exchange(partR, hR, "R")
-            rS = exchange(partS, hS, "S")
-            if "sR" not in state or state["sR"].shape[0] < rR.shape[0]:
-                state["sR"] = lib.empty(rR.shape[0])
-            if "sS" not in state or state["sS"].shape[0] < rS.shape[0]:
-                state["sS"] = lib.empty(rS.shape[0])
-            lib.dev_join(rR, rS, state["sR"][: rR.shape[0]], state["sS"][: rS.shape[0]],
-                         count, D1, 1, total)
-            dist.all_reduce(count)
+            dj.step(R, S, count)
 
     for _ in range(a.warmup):
         step()

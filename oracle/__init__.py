@@ -177,8 +177,11 @@ class Reference(_Lib):
 
     def partition(self, t, nbits, shift, variant):
         fan = 1 << nbits
-        inp = np.ascontiguousarray(t).copy()
-        out = np.zeros(len(t) + fan * 64 // self.width + 64, self.dtype)
+        inp = self._aligned(len(t))
+        inp[:] = t
+        # 64-byte aligned: the optimized variants flush 64-byte lines with
+        # _mm256_stream_si256 (src/partition/partition.c:59-91)
+        out = self._aligned(len(t) + fan * 64 // self.width + 64)
         cnt = np.zeros(fan, np.int64)
         off = np.zeros(fan, np.int64)
         self.fn("partition", None, _P, _I64, _P, C.c_int, C.c_int, C.c_int, _P, _P)(

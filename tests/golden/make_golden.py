@@ -1,0 +1,159 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/*.npz from the REFERENCE implementation.
+
+Runs in the container that has /root/reference: oracle/build_ref.sh compiles
+the reference sources into oracle/_ref/libref{8,16}.so, and this script calls
+them through oracle.Reference (ctypes).  The fixtures are plain arrays (inputs
+and the reference's outputs), loaded with numpy.load(allow_pickle=False) by
+tests/test_oracle.py, which pins oracle/smj_oracle.c (the CPU restatement) to
+them.  Nothing here runs on the GPU box.
+
+    python tests/golden/make_golden.py
+"""
+import os
+import re
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+import oracle  # noqa: E402
+
+PART_N = 5000
+PART_CASES = [(4, 0), (10, 0), (7, 3), (4, 20)]
+SORT_NS = [16, 255, 16384, 2 * 16384 + 77]
+MW_FANIN = [4, 64]
+JOIN_CASES = [("pk", 200000, 200000), ("pk", 300000, 100000),
+              ("nonunique", 100000, 150000), ("zipf", 100000, 200000)]
+
+
+def join_inputs(gen, kind, nr, ns):
+    """R and S of a join case; gen is oracle.Reference or oracle.Oracle."""
+    gen.seed(12345)
+    R = gen.create_relation_nonunique(nr, nr) if kind == "nonunique" else gen.create_relation_pk(nr)
+    gen.seed(54321)
+    if kind == "pk":
+        S = gen.create_relation_pk(ns)
+    elif kind == "nonunique":
+        S = gen.create_relation_nonunique(ns, nr)
+    else:
+        S = gen.create_relation_zipf(ns, nr, 0.75)
+    return R, S
+
+
+def join_case(w, ki, T):
+    ref = oracle.Reference(w)
+    kind, nr, ns = JOIN_CASES[ki]
+    R, S = join_inputs(ref, kind, nr, ns)
+    print("\nCOUNT", ref.sortmergejoin_multiway(R, S, nthreads=T, fanout=128), flush=True)
+
+
+def sorted_runs(rng, k, maxlen, dtype, keymax=100000):
+    runs = []
+    for _ in range(k):
+        n = int(rng.integers(1, maxlen))
+        t = np.zeros(n, dtype)
+        t["key"] = np.sort(rng.integers(1, keymax, n))
+        t["payload"] = rng.integers(0, 1 << 20, n)
+        # canonical order (key, payload) so 8- and 16-byte semantics agree
+        t = np.sort(t, order=["key", "payload"])
+        runs.append(t)
+    return runs
+
+
+def main():
+    for w in (8, 16):
+        ref = oracle.Reference(w)
+        out = {}
+        # ---- generators (src/datagen/generator.c, genzipf.c)
+        ref.seed(12345)
+        out["gen_pk"] = ref.create_relation_pk(1000)
+        ref.seed(54321)
+        out["gen_nonunique"] = ref.create_relation_nonunique(1000, 300)
+        ref.seed(777)
+        out["gen_zipf"] = ref.create_relation_zipf(2000, 500, 0.75)
+        ref.seed(99)
+        out["gen_fk"] = ref.create_relation_fk(1500, 400)
+
+        # ---- partitioning (src/partition/partition.c)
+        ref.seed(12345)
+        pin = ref.create_relation_pk(PART_N)
+        pin["payload"] = np.arange(PART_N) + 5
+        out["part_in"] = pin
+        for nbits, shift in PART_CASES:
+            for variant in (0, 1, 2):
+                o, cnt, off = ref.partition(pin, nbits, shift, variant)
+                dense = np.concatenate([o[off[i]:off[i] + cnt[i]] for i in range(1 << nbits)])
+                tag = f"part_b{nbits}_s{shift}_v{variant}"
+                out[tag + "_cnt"] = cnt
+                out[tag + "_off"] = off
+                out[tag + "_dense"] = dense
+
+        # ---- sorting: AVX path for 8-byte tuples, scalar for 16-byte
+        for n in SORT_NS:
+            ref.seed(1000 + n)
+            t = ref.create_relation_nonunique(n, max(2, n // 2))
+            out[f"sort_in_{n}"] = t
+            if w == 8:
+                out[f"sort_out_{n}"] = ref.sort(t, "avxsort_tuples")
+            else:
+                out[f"sort_out_{n}"] = ref.sort(t, "scalarsort_tuples")
+
+        # ---- 2-way merge (src/merge/merge.c)
+        rng = np.random.default_rng(5)
+        a, b = sorted_runs(rng, 2, 1200, ref.dtype)
+        out["merge_a"], out["merge_b"] = a, b
+        out["merge_out"] = ref.merge(a, b, "avx_merge_tuples" if w == 8 else "scalar_merge_tuples")
+
+        # ---- multiway merge (src/merge/avx_multiwaymerge.c, scalar_multiwaymerge.c)
+        for k in MW_FANIN:
+            runs = sorted_runs(np.random.default_rng(k), k, 900, ref.dtype)
+            mo, mn = ref.multiway_merge(runs, 4 << 20, scalar=(w == 16))
+            out[f"mw{k}_runs"] = np.concatenate(runs)
+            out[f"mw{k}_lens"] = np.array([len(r) for r in runs], np.int64)
+            out[f"mw{k}_out"] = mo
+            out[f"mw{k}_n"] = np.array([mn], np.int64)
+
+        # ---- merge_join on dup x dup sorted runs (src/joins/joincommon.c)
+        mj = []
+        for seed, n in [(1, 10), (2, 1000), (3, 20000)]:
+            r = np.random.default_rng(seed)
+            R = np.zeros(n, ref.dtype)
+            S = np.zeros(n + 7, ref.dtype)
+            R["key"] = np.sort(r.integers(0, max(2, n // 4), n))
+            S["key"] = np.sort(r.integers(0, max(2, n // 4), n + 7))
+            out[f"mj{seed}_R"], out[f"mj{seed}_S"] = R, S
+            mj.append(ref.merge_join(R, S))
+        out["mj_counts"] = np.array(mj, np.int64)
+
+        # ---- sortmergejoin_multiway counts (src/joins/sortmergejoin_multiway.c)
+        # inputs are regenerated by the oracle from the seeds (pinned above).
+        # Each case runs in a child process: the reference's 8-byte AVX path
+        # segfaults deterministically on (nonunique, NTHREADS=8) here; such a
+        # case is recorded with count -1 and skipped by the tests.
+        cases = []
+        for ki, (kind, nr, ns) in enumerate(JOIN_CASES):
+            for T in (1, 2, 4, 8):
+                r = subprocess.run([sys.executable, __file__, "--join-case",
+                                    str(w), str(ki), str(T)],
+                                   capture_output=True, text=True, timeout=600)
+                c = -1
+                m = re.search(r"COUNT (-?\d+)", r.stdout)
+                if r.returncode == 0 and m:
+                    c = int(m.group(1))
+                cases.append((["pk", "nonunique", "zipf"].index(kind), nr, ns, T, c))
+        out["join_cases"] = np.array(cases, np.int64)
+
+        path = os.path.join(HERE, f"golden_w{w}.npz")
+        np.savez_compressed(path, **out)
+        print(f"wrote {path} ({os.path.getsize(path) / 1e6:.2f} MB, {len(out)} arrays)")
+
+
+if __name__ == "__main__":
+    if len(sys.argv) == 5 and sys.argv[1] == "--join-case":
+        join_case(*map(int, sys.argv[2:]))
+    else:
+        main()

@@ -1,0 +1,68 @@
+"""The C ABI (include/smj.h) on CPU: both libraries load, report their tuple
+width, and export every function the header declares.  No compute call is made
+here -- the library aborts without a HIP device (no CPU fallback)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import PKG, ROOT
+
+HEADER = os.path.join(ROOT, "include", "smj.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    src = re.sub(r"//[^\n]*", "", src)
+    src = re.sub(r"#[^\n]*", "", src)
+    # a declaration: <type> name(args);  -- skip typedef'd function pointers
+    names = set(re.findall(r"\b([A-Za-z_]\w*)\s*\([^;{}()]*(?:\([^()]*\)[^;{}()]*)*\)\s*;", src))
+    return {n for n in names if n not in ("sizeof",)}
+
+
+@pytest.fixture(scope="module")
+def smj_mod():
+    import smj
+    for w in (8, 16):
+        if not os.path.exists(smj.lib_path(w)):
+            smj.build()
+            break
+    return smj
+
+
+def test_header_lists_match_binding(smj_mod):
+    decl = declared_functions()
+    listed = set(smj_mod.REFERENCE_SYMBOLS) | set(smj_mod.DEVICE_SYMBOLS)
+    assert decl == listed, (sorted(decl - listed), sorted(listed - decl))
+
+
+@pytest.mark.parametrize("width", [8, 16])
+def test_library_exports(smj_mod, width):
+    path = smj_mod.lib_path(width)
+    lib = ctypes.CDLL(path)
+    missing = [s for s in declared_functions() if not hasattr(lib, s)]
+    assert not missing, missing
+    lib.smj_tuple_bytes.restype = ctypes.c_int
+    assert lib.smj_tuple_bytes() == width
+
+
+@pytest.mark.parametrize("width", [8, 16])
+def test_binding_loads(smj_mod, width):
+    L = smj_mod.Library(width)  # binds every signature; no device call
+    assert L.dtype.itemsize == width
+
+
+def test_binding_fails_loudly_without_library(smj_mod, tmp_path):
+    with pytest.raises(FileNotFoundError):
+        smj_mod.Library(16, path=str(tmp_path / "nope.so"))
+
+
+def test_product_does_not_reference_oracle():
+    """The shipped path never imports or links the oracle."""
+    for root, _, files in os.walk(PKG):
+        for f in files:
+            if f.endswith((".py", ".hip", ".hpp", ".h", ".cpp")) or f == "Makefile":
+                text = open(os.path.join(root, f), errors="ignore").read()
+                assert "oracle" not in text.replace("no oracle", ""), os.path.join(root, f)

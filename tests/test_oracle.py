@@ -1,0 +1,158 @@
+"""Pin the CPU oracle (oracle/smj_oracle.c) to the reference's golden vectors.
+
+tests/golden/golden_w{8,16}.npz were produced by tests/golden/make_golden.py
+from the reference itself (compiled from /root/reference by
+oracle/build_ref.sh).  These tests run on CPU only; the GPU parity tests then
+compare the HIP library with the oracle pinned here (and with the fixtures
+directly, tests/test_gpu_parity.py::test_golden_*).
+
+Ordering contract: 8-byte tuples sort as the packed 64-bit word
+(key, payload), a total order, so outputs compare exactly.  The reference's
+16-byte path sorts by key only and leaves equal keys in an implementation
+order; those outputs compare keys exactly and the (key, payload) multiset.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+GOLD = os.path.join(ROOT, "tests", "golden")
+PART_CASES = [(4, 0), (10, 0), (7, 3), (4, 20)]
+SORT_NS = [16, 255, 16384, 2 * 16384 + 77]
+KINDS = ["pk", "nonunique", "zipf"]
+
+
+@pytest.fixture(scope="module", params=[8, 16], ids=["w8", "w16"])
+def case(request, oracles):
+    w = request.param
+    with np.load(os.path.join(GOLD, f"golden_w{w}.npz"), allow_pickle=False) as d:
+        gold = {k: d[k] for k in d.files}
+    return w, oracles[w], gold
+
+
+def canon(t):
+    return np.sort(t, order=["key", "payload"])
+
+
+def same_order(w, got, want):
+    """Exact for 8-byte tuples; keys exact + canonical multiset for 16-byte."""
+    assert len(got) == len(want)
+    if w == 8:
+        np.testing.assert_array_equal(got, want)
+    else:
+        np.testing.assert_array_equal(got["key"], want["key"])
+        np.testing.assert_array_equal(canon(got), canon(want))
+
+
+def test_generators(case):
+    w, orc, g = case
+    orc.seed(12345)
+    np.testing.assert_array_equal(orc.create_relation_pk(1000), g["gen_pk"])
+    orc.seed(54321)
+    np.testing.assert_array_equal(orc.create_relation_nonunique(1000, 300), g["gen_nonunique"])
+    orc.seed(777)
+    np.testing.assert_array_equal(orc.create_relation_zipf(2000, 500, 0.75), g["gen_zipf"])
+    orc.seed(99)
+    np.testing.assert_array_equal(orc.create_relation_fk(1500, 400), g["gen_fk"])
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("nbits,shift", PART_CASES)
+def test_partition(case, nbits, shift, variant):
+    w, orc, g = case
+    tag = f"part_b{nbits}_s{shift}_v{variant}"
+    out, cnt, off = orc.partition(g["part_in"], nbits, shift, padded=variant > 0)
+    np.testing.assert_array_equal(cnt, g[tag + "_cnt"])
+    np.testing.assert_array_equal(off, g[tag + "_off"])
+    dense = np.concatenate([out[off[i]:off[i] + cnt[i]] for i in range(1 << nbits)])
+    # every variant of the reference partitioner is stable: exact order
+    np.testing.assert_array_equal(dense, g[tag + "_dense"])
+
+
+@pytest.mark.parametrize("n", SORT_NS)
+def test_sort(case, n):
+    w, orc, g = case
+    same_order(w, orc.sort(g[f"sort_in_{n}"]), g[f"sort_out_{n}"])
+
+
+def test_merge(case):
+    w, orc, g = case
+    same_order(w, orc.merge(g["merge_a"], g["merge_b"]), g["merge_out"])
+
+
+@pytest.mark.parametrize("k", [4, 64])
+def test_multiway_merge(case, k):
+    w, orc, g = case
+    runs = np.split(g[f"mw{k}_runs"], np.cumsum(g[f"mw{k}_lens"])[:-1])
+    assert len(runs) == k
+    out = orc.multiway_merge(runs)
+    assert int(g[f"mw{k}_n"][0]) == len(out)
+    same_order(w, out, g[f"mw{k}_out"])
+
+
+def test_merge_join(case):
+    w, orc, g = case
+    got = [orc.merge_join(g[f"mj{s}_R"], g[f"mj{s}_S"]) for s in (1, 2, 3)]
+    np.testing.assert_array_equal(got, g["mj_counts"])
+
+
+def join_inputs(gen, kind, nr, ns):
+    """Same inputs as tests/golden/make_golden.py:join_inputs."""
+    gen.seed(12345)
+    R = gen.create_relation_nonunique(nr, nr) if kind == "nonunique" else gen.create_relation_pk(nr)
+    gen.seed(54321)
+    if kind == "pk":
+        S = gen.create_relation_pk(ns)
+    elif kind == "nonunique":
+        S = gen.create_relation_nonunique(ns, nr)
+    else:
+        S = gen.create_relation_zipf(ns, nr, 0.75)
+    return R, S
+
+
+def test_sortmergejoin_counts(case):
+    w, orc, g = case
+    rows = g["join_cases"]
+    seen = set()
+    for kind_i, nr, ns, T, count in rows.tolist():
+        if count < 0:  # the reference crashed on this case (make_golden.py)
+            continue
+        key = (kind_i, nr, ns)
+        R, S = join_inputs(orc, KINDS[kind_i], nr, ns)
+        c, sR, sS = orc.sortmergejoin(R, S)
+        assert c == count, (KINDS[kind_i], nr, ns, T)
+        if key not in seen:
+            seen.add(key)
+            assert np.all(np.diff(sR["key"]) >= 0) and np.all(np.diff(sS["key"]) >= 0)
+            np.testing.assert_array_equal(canon(sR), canon(R))
+    assert len(seen) == 4
+
+
+# -- live cross-check against the compiled reference (this container only) ----
+def _reference(w):
+    import oracle
+    if not oracle.reference_available(w):
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    return oracle.Reference(w)
+
+
+@pytest.mark.parametrize("w", [8, 16])
+def test_live_reference_partition_sort(w, oracles):
+    ref, orc = _reference(w), oracles[w]
+    rng = np.random.default_rng(7 + w)
+    t = np.zeros(20000, orc.dtype)
+    # the reference's AVX sort compares tuples as doubles
+    # (src/avxsort/avxsort_core.h:2259-2266), so its domain is non-negative
+    # keys below the NaN range; the device library sorts all signed keys
+    t["key"] = rng.integers(0, 1 << 20, len(t))
+    t["payload"] = np.arange(len(t))
+    for nbits, shift in [(6, 0), (5, 9)]:
+        o1, c1, f1 = ref.partition(t, nbits, shift, 1)
+        o2, c2, f2 = orc.partition(t, nbits, shift, padded=True)
+        np.testing.assert_array_equal(c1, c2)
+        np.testing.assert_array_equal(f1, f2)
+        np.testing.assert_array_equal(o1[: f1[-1] + c1[-1]], o2[: f2[-1] + c2[-1]])
+    fn = "avxsort_tuples" if w == 8 else "scalarsort_tuples"
+    same_order(w, orc.sort(t), ref.sort(t, fn))
