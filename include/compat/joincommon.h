@@ -1,0 +1,11 @@
+/*
+ * joincommon.h -- drop-in for the hot-path part of the reference header
+ * src/joins/joincommon.h:78-80 (sdecoder/AVX-sort-merge-joins): merge_join.
+ * The reference's pthread scaffolding (arg_t, sortmergejoin_initrun,
+ * print_timing) drives CPU threads and has no counterpart here: the joins in
+ * ../smj.h own their device work.
+ */
+#ifndef JOINCOMMON_H_
+#define JOINCOMMON_H_
+#include "../smj.h"
+#endif /* JOINCOMMON_H_ */

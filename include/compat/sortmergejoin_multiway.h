@@ -1,0 +1,11 @@
+/*
+ * sortmergejoin_multiway.h -- drop-in for the reference header src/joins/sortmergejoin_multiway.h:37-38
+ * (sdecoder/AVX-sort-merge-joins).  Same file name and include guard, so a
+ * reference driver that includes "sortmergejoin_multiway.h" compiles unchanged against
+ * libsmj_hip.so (8-byte tuples) or libsmj_hip_k8.so (-DKEY_8B, 16-byte tuples).
+ * Provides: sortmergejoin_multiway.  The declarations live in ../smj.h.
+ */
+#ifndef SORTMERGEJOIN_MULTIWAY_H_
+#define SORTMERGEJOIN_MULTIWAY_H_
+#include "../smj.h"
+#endif /* SORTMERGEJOIN_MULTIWAY_H_ */

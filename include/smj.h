@@ -44,8 +44,12 @@ extern "C" {
 #endif
 
 /* ------------------------------------------------------------------------ */
-/* Data ABI (reference src/types.h:51-98). Layout is byte-identical.        */
+/* Data ABI (reference src/types.h:22-98). Layout is byte-identical, and the */
+/* include guard is the reference's own (TYPES_H), so this header and the    */
+/* reference's types.h can both be included in one translation unit.        */
 /* ------------------------------------------------------------------------ */
+#ifndef TYPES_H
+#define TYPES_H
 #ifdef KEY_8B
 typedef int64_t intkey_t;   /* 16-byte tuples */
 typedef int64_t value_t;
@@ -94,10 +98,13 @@ struct joinconfig_t {
     int MWAYMERGEBUFFERSIZE;
     enum numa_strategy_t NUMASTRATEGY;
 };
+#endif /* TYPES_H */
 
 /* ------------------------------------------------------------------------ */
-/* Compile-time parameters (reference src/params.h:17-72).                  */
+/* Compile-time parameters (reference src/params.h:17-72, guard PARAMS_H_).  */
 /* ------------------------------------------------------------------------ */
+#ifndef PARAMS_H_
+#define PARAMS_H_
 #ifndef NRADIXBITS_DEFAULT
 #define NRADIXBITS_DEFAULT 7
 #endif
@@ -113,9 +120,6 @@ struct joinconfig_t {
 #ifndef L3_CACHE_SIZE
 #define L3_CACHE_SIZE (20 * 1024 * 1024)
 #endif
-#ifndef MWAY_MERGE_BUFFER_SIZE_DEFAULT
-#define MWAY_MERGE_BUFFER_SIZE_DEFAULT L3_CACHE_SIZE
-#endif
 /* one cache line of padding per partition (params.h:47) */
 #ifndef CACHELINEPADDING
 #define CACHELINEPADDING(FANOUT) ((FANOUT) * CACHE_LINE_SIZE / sizeof(tuple_t))
@@ -125,9 +129,13 @@ struct joinconfig_t {
 #define RELATION_PADDING(NTHR, FANOUT) \
     ((NTHR) * CACHELINEPADDING(FANOUT) * sizeof(tuple_t))
 #endif
+#ifndef MWAY_MERGE_BUFFER_SIZE_DEFAULT
+#define MWAY_MERGE_BUFFER_SIZE_DEFAULT L3_CACHE_SIZE
+#endif
 #define TUPLESPERCACHELINE (CACHE_LINE_SIZE / sizeof(tuple_t))
 #define ALIGN_NUMTUPLES(N) \
     (((N) + TUPLESPERCACHELINE - 1) & ~(TUPLESPERCACHELINE - 1))
+#endif /* PARAMS_H_ */
 
 /* ------------------------------------------------------------------------ */
 /* Radix partitioning (reference src/partition/partition.h:57-120).          */
