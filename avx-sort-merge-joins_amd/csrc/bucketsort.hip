@@ -6,53 +6,66 @@
 // After the level-1 radix partition (partition.hip) every bucket b holds the
 // tuples whose key falls in one contiguous key range of the RangePlan.
 //
-//   k_tilepass : every bucket is cut into tiles of TILE2 tuples.  A tile is
-//                loaded into registers, counted by its level-2 digit d2 in an
-//                LDS histogram, staged in LDS grouped by d2 and written back in
-//                place, linearly (fully coalesced), together with the tile's
-//                exclusive d2 prefix (uint16 per digit + a sentinel = length).
-//                Traffic: 2w.
-//   k_subwave  : ONE WAVE per sub-bucket (b, d2) at a time, twelve independent
-//                waves per CU, no workgroup barriers.  The wave gathers the
-//                sub-bucket's piece from every tile of bucket b (contiguous
-//                runs read by consecutive lanes; the piece of a lane is found
-//                with one ballot over a piece-start map instead of a search),
-//                counting-sorts it in its private LDS slice by the level-3
-//                digit, fixes equal-digit runs with an insertion sort on the
-//                full (key, payload) order and writes the sorted sub-bucket to
-//                its final position -- R first, then S in the same LDS slice --
-//                and, for a join, counts the matching pairs of the two
-//                sub-buckets from their level-3 histograms (exact digits) or
-//                by binary search in R's sorted keys.  Traffic: 2w; the join
-//                reads nothing more.  The eight-to-twelve waves of a workgroup
-//                take neighbouring sub-buckets at the same time, so the cache
-//                lines shared at piece boundaries and the 128-byte lines of the
-//                prefix table are served from L1/L2, not refetched.
+//   k_tilepass  : every bucket is cut into tiles of TILE2 tuples.  A tile is
+//                 loaded into registers, counted by its level-2 digit d2 (the
+//                 "group") in an LDS histogram, staged in LDS grouped by d2 and
+//                 written back linearly (fully coalesced), together with the
+//                 tile's exclusive d2 prefix (uint16 per digit + a sentinel =
+//                 tile length).  Traffic: 2w.
+//   k_groupsort : one workgroup per group (b, d2), two workgroups per CU.  The
+//                 group's piece in each tile of bucket b is one contiguous run
+//                 (about 1 KiB at the default plan), so the workgroup gathers
+//                 R's and S's runs with fully used 128-byte lines, all loads in
+//                 flight at once (the run of an element is found with a
+//                 run-start bitmap in LDS, no search).  It then counting-sorts
+//                 each relation in LDS by the level-3 digit d3, fixes the
+//                 (rare) equal-digit runs on the full (key, payload) order,
+//                 writes the group to its final place in one contiguous
+//                 stream, and counts the matching pairs from the two d3
+//                 histograms (the plan makes d3 the exact key when it can) or
+//                 by binary search.  Traffic: 2w; the join reads nothing more.
 //
-// Sub-buckets that do not fit the per-wave LDS capacity, or that hold long
-// runs of equal digits (skew, e.g. Zipf hot keys), are queued and finished by
-// the segmented merge sort (mergesort.hip) and the merge-join count kernel.
+// Groups that do not fit in LDS, or whose long equal-key runs are not already
+// in payload order (skew), are copied unsorted to their final place and
+// finished by the segmented merge sort (mergesort.hip) and the merge-join
+// count kernel.
+#include <algorithm>
+#include <vector>
+
 #include "smj_common.hpp"
 #include "smj_internal.hpp"
 
 namespace smj {
 
-constexpr int TP_THREADS = 256;
+#ifndef SMJ_TP_THREADS
+#define SMJ_TP_THREADS 512
+#endif
+constexpr int TP_THREADS = SMJ_TP_THREADS;
 constexpr int TP_ITEMS = 16;
-constexpr int TILE2 = TP_THREADS * TP_ITEMS;  // 4096 tuples per tile
+constexpr int TILE2 = TP_THREADS * TP_ITEMS;  // tuples per tile
+const uint32_t kTileTuples = TILE2;
+
+#ifndef SMJ_GS_THREADS
+#define SMJ_GS_THREADS 128
+#endif
+constexpr int GS_THREADS = SMJ_GS_THREADS;      // one workgroup per group
+constexpr int GS_WG_PER_CU = 512 / GS_THREADS;  // resident workgroups per CU
+constexpr int GS_D3MAX = GS_THREADS >= 256 ? 11 : 10;  // level-3 bits sorted in LDS
+constexpr int GS_ITEMS = 10;                    // tuples per thread per relation
+constexpr int GS_CAP = GS_THREADS * GS_ITEMS;   // tuples per group per relation
+constexpr int GS_BPT = (1 << GS_D3MAX) / GS_THREADS;  // d3 bins per thread
+constexpr int GS_NB3 = 1 << GS_D3MAX;
+constexpr int GS_TMAX = 128;    // tiles per bucket on the fast path (two per lane of one wave)
+constexpr int GS_WIN = GS_CAP / 64;
+constexpr int GS_RUNMAX = 32;   // longest equal-digit run fixed serially
+constexpr int GS_LONGMAX = 64;  // long runs checked per group
+static_assert(GS_CAP % 64 == 0 && GS_CAP % GS_THREADS == 0, "group capacity");
 
 #ifdef KEY_8B
-constexpr int SW_CAP = 384;  // tuples per sub-bucket per relation in LDS
 typedef int64_t KeyT;
 #else
-constexpr int SW_CAP = 768;
 typedef int32_t KeyT;
 #endif
-constexpr int SW_ITEMS = SW_CAP / 64;
-constexpr int SW_D3MAX = 8;  // level-3 bins per wave (256)
-constexpr int SW_NB3 = 1 << SW_D3MAX;
-constexpr int SW_PMAX = 64;    // tiles per bucket handled by the wave path
-constexpr int SW_RUNMAX = 32;  // longest equal-digit run fixed in LDS
 
 struct TileTable {
     uint64_t* off;     // tile start in `part`
@@ -60,64 +73,60 @@ struct TileTable {
     uint32_t* bucket;  // owning bucket
     uint32_t* btile0;  // first tile of every bucket (nbuckets + 1)
     uint16_t* pref;    // [tile][nb2 + 1] exclusive prefix, sentinel = length
-    uint32_t* ntiles;  // device scalar
 };
 
 struct OvfEntry {
     uint32_t bucket, d2;
     uint32_t nr[2];
-    uint64_t off[2];  // offset of the sub-bucket inside its bucket
+    uint64_t off[2];  // offset of the group inside its bucket
 };
 
 // ---------------------------------------------------------------------------
-// tile table: one workgroup scans the per-bucket tile counts.  The tiles of a
-// bucket are consecutive TILE2-sized chunks of it.
-__global__ void __launch_bounds__(256)
+// tile table: block b writes the tiles of bucket b (consecutive TILE2 chunks),
+// numbered from btile0[b] (uploaded by the host).
+__global__ void __launch_bounds__(64)
 k_tiles(const uint64_t* __restrict__ bstart, const int64_t* __restrict__ bcount,
-        uint32_t nb, TileTable tt) {
-    __shared__ uint32_t scr[8];
-    __shared__ uint32_t base_sh;
-    if (threadIdx.x == 0) base_sh = 0;
-    __syncthreads();
-    for (uint32_t b0 = 0; b0 < nb; b0 += 256) {
-        uint32_t b = b0 + threadIdx.x;
-        uint32_t nt = 0;
-        if (b < nb) nt = (uint32_t)((bcount[b] + TILE2 - 1) / TILE2);
-        uint32_t tot;
-        uint32_t ex = block_exclusive_scan(nt, scr, &tot);
-        uint32_t t0 = base_sh + ex;
-        if (b < nb) {
-            tt.btile0[b] = t0;
-            for (uint32_t i = 0; i < nt; i++) {
-                uint64_t o = (uint64_t)i * TILE2;
-                int64_t rem = bcount[b] - (int64_t)o;
-                tt.off[t0 + i] = bstart[b] + o;
-                tt.len[t0 + i] = (uint32_t)(rem < TILE2 ? rem : TILE2);
-                tt.bucket[t0 + i] = b;
-            }
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) base_sh += tot;
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        tt.btile0[nb] = base_sh;
-        *tt.ntiles = base_sh;
+        TileTable tt) {
+    const uint32_t b = blockIdx.x;
+    const uint32_t t0 = tt.btile0[b], nt = tt.btile0[b + 1] - t0;
+    for (uint32_t i = threadIdx.x; i < nt; i += 64) {
+        const uint64_t o = (uint64_t)i * TILE2;
+        const int64_t rem = bcount[b] - (int64_t)o;
+        tt.off[t0 + i] = bstart[b] + o;
+        tt.len[t0 + i] = (uint32_t)(rem < TILE2 ? rem : TILE2);
+        tt.bucket[t0 + i] = b;
     }
 }
 
 // ---------------------------------------------------------------------------
+// One launch covers the tiles [t0[r], t0[r] + nt[r]) of both relations
+// (blocks [0, nt[0]) are R's, the rest S's).  A tile at part offset `off` is
+// written to tmp[r][off]: `tmp` is either the partition buffer itself (in
+// place) or a ring buffer shifted by the batch's first offset (bucket_sort).
+struct TilePassArgs {
+    const Tup* part[2];
+    Tup* tmp[2];
+    TileTable tt[2];
+    uint32_t t0[2];
+    uint32_t nt[2];
+    RangePlan plan;  // by value: kernel arguments live in SGPRs
+    uint32_t nb2;
+};
+
 __global__ void __launch_bounds__(TP_THREADS)
-k_tilepass(const Tup* __restrict__ part, Tup* __restrict__ tmp, TileTable tt,
-           const RangePlan* __restrict__ plan_dev, uint32_t nb2) {
+k_tilepass(TilePassArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
-    const RangePlan P = *plan_dev;
+    const RangePlan& P = A.plan;
+    const uint32_t nb2 = A.nb2;
     Tup* stage = reinterpret_cast<Tup*>(lds_raw);
     uint32_t* hist = reinterpret_cast<uint32_t*>(lds_raw + TILE2 * sizeof(Tup));
     uint32_t* scr = hist + nb2;
 
-    const uint32_t t = blockIdx.x;
-    if (t >= *tt.ntiles) return;
+    const int r = blockIdx.x < A.nt[0] ? 0 : 1;
+    const uint32_t t = A.t0[r] + (r ? blockIdx.x - A.nt[0] : blockIdx.x);
+    const TileTable& tt = A.tt[r];
+    const Tup* __restrict__ part = A.part[r];
+    Tup* __restrict__ tmp = A.tmp[r];
     const uint64_t off = tt.off[t];
     const uint32_t len = tt.len[t];
     const uint32_t b = tt.bucket[t];
@@ -179,65 +188,146 @@ k_tilepass(const Tup* __restrict__ part, Tup* __restrict__ tmp, TileTable tt,
 }
 
 // ---------------------------------------------------------------------------
-struct SubWaveArgs {
+struct GroupArgs {
     const Tup* tmp[2];
     Tup* out[2];
     const uint64_t* bstart[2];
     TileTable tt[2];
     int nrel;
-    const RangePlan* plan_dev;
+    RangePlan plan;  // by value: kernel arguments live in SGPRs
     unsigned long long* count_dev;
-    uint32_t nb2;   // level-2 table stride (>= 1 << plan.D2)
-    uint32_t nsub;  // nbuckets * nb2
-    uint32_t spw;   // sub-buckets per wave
+    uint32_t nb2;             // groups per bucket (= 1 << plan.D2 = pref stride - 1)
+    uint32_t g_begin, g_end;  // groups b * nb2 + d2 of this launch
+    uint32_t per;             // consecutive groups per workgroup
     OvfEntry* ovf;
     uint32_t* novf;
     uint32_t ovf_cap;
 };
 
-// per-wave LDS slice; R and S pass through B one after the other
-struct WaveLDS {
-    Tup B[SW_CAP];
-    KeyT rkey[SW_CAP];       // R's sorted keys (generic join)
-    uint32_t h[2][SW_NB3];   // level-3 bin starts of R and S
-    uint32_t fill[SW_NB3];
-    uint32_t psrc[SW_PMAX];  // piece start, relative to the bucket start
-    uint32_t pdst[SW_PMAX];  // piece position inside the sub-bucket
-    uint8_t pat[SW_CAP];     // piece starting at a position, 0xff = none
-};
-constexpr int SW_WAVES_RAW = (160 * 1024) / (int)sizeof(WaveLDS);
-constexpr int SW_WAVES = SW_WAVES_RAW > 16 ? 16 : SW_WAVES_RAW;
-constexpr int SW_THREADS = SW_WAVES * 64;
-static_assert(SW_WAVES >= 8, "LDS slice too large");
+// threadIdx.x behind an empty asm: per-thread LDS addresses are recomputed
+// where they are used instead of being hoisted out of the group loop (which
+// ran the persistent kernel out of VGPRs)
+__device__ __forceinline__ uint32_t otid() {
+    uint32_t t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
 
-// order this wave's LDS accesses (LDS executes one wave's instructions in
-// order; the fences stop the compiler from moving accesses across)
+struct GroupLDS {
+    Tup B[GS_CAP + 1];                    // one relation's group (+ a dump slot)
+    uint32_t cnt[2][GS_NB3 / 2];          // d3 histograms of R and S (2 x u16)
+    uint32_t cur[GS_NB3 / 2];             // placement cursors (2 x u16)
+    uint32_t runoff[2][GS_TMAX + 1];      // run t starts at position runoff[t]
+    uint32_t runsrc[2][GS_TMAX];          // run t's offset in its bucket
+    unsigned long long smap[2][GS_WIN];   // bit j: a run starts at position j
+    uint8_t stile[2][GS_CAP];             // tile of the run starting at j
+    uint8_t wtile[2][GS_WIN];             // tile holding position 64 * w
+    uint32_t wtot[GS_THREADS / 64];
+    unsigned long long scan64[GS_THREADS / 64 + 1];
+    uint32_t lrun[GS_LONGMAX][2];         // long equal-digit runs [s, e)
+    uint32_t nlong;
+    uint32_t n[2];
+    uint32_t off[2];
+};
+
+// A group and, for the calling thread, its tile run: wave r < nrel owns
+// relation r, lane t its tile t (lo = run start in the tile, len = length).
+struct GroupMeta {
+    uint32_t b, g;
+    uint32_t t0[2], nt[2];  // first tile and tile count of the bucket
+    uint64_t bst[2];        // bucket start
+    uint32_t lo[2], len[2];  // tiles lane and lane + 64
+};
+
+__device__ __forceinline__ void load_meta(const GroupArgs& A, uint32_t gi,
+                                          GroupMeta& M, bool same_bucket) {
+    const uint32_t b = gi / A.nb2;
+    M.g = gi % A.nb2;
+    if (!same_bucket || b != M.b) {
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+            M.t0[r] = M.nt[r] = 0;
+            M.bst[r] = 0;
+            if (r < A.nrel) {
+                // uniform: keep them in SGPRs
+                M.t0[r] = __builtin_amdgcn_readfirstlane(A.tt[r].btile0[b]);
+                M.nt[r] = __builtin_amdgcn_readfirstlane(A.tt[r].btile0[b + 1]) - M.t0[r];
+                const uint64_t bs = A.bstart[r][b];
+                M.bst[r] = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(bs >> 32)) << 32) |
+                           __builtin_amdgcn_readfirstlane((uint32_t)bs);
+            }
+        }
+    }
+    M.b = b;
+    const uint32_t wid = otid() >> 6, lane = otid() & 63;
+    M.lo[0] = M.len[0] = M.lo[1] = M.len[1] = 0;
+    if (wid < (uint32_t)A.nrel) {
+        const uint32_t nt = wid ? M.nt[1] : M.nt[0];
+        const uint32_t t0 = wid ? M.t0[1] : M.t0[0];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const uint32_t t = lane + 64 * h;
+            if (nt <= GS_TMAX && t < nt) {
+                const uint16_t* pf =
+                    A.tt[wid].pref + (uint64_t)(t0 + t) * (A.nb2 + 1) + M.g;
+                M.lo[h] = pf[0];
+                M.len[h] = (uint32_t)(pf[1] - pf[0]);
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t x) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    return x;
+}
+
+__device__ __forceinline__ unsigned long long wave_incl_scan64(unsigned long long x) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    return x;
+}
+
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
-    const int lane = lane_id();
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
+// block-wide exclusive scan of one uint64 per thread
+__device__ __forceinline__ unsigned long long block_scan64(unsigned long long v,
+                                                           unsigned long long* scr,
+                                                           unsigned long long* total) {
+    const int lane = lane_id(), wid = otid() >> 6, nw = blockDim.x >> 6;
+    const unsigned long long x = wave_incl_scan64(v);
+    if (lane == 63) scr[wid] = x;
+    __syncthreads();
+    if (otid() == 0) {
+        unsigned long long run = 0;
+        for (int w = 0; w < nw; w++) {
+            const unsigned long long t = scr[w];
+            scr[w] = run;
+            run += t;
+        }
+        scr[nw] = run;
     }
-    return x;
+    __syncthreads();
+    const unsigned long long r = scr[wid] + x - v;
+    *total = scr[nw];
+    __syncthreads();
+    return r;
 }
 
-__device__ __forceinline__ uint32_t wave_max(uint32_t x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        uint32_t y = __shfl_xor(x, o, 64);
-        x = y > x ? y : x;
-    }
-    return x;
-}
-
-__device__ __forceinline__ void lds_insertion_sort(Tup* a, uint32_t n) {
+__device__ __forceinline__ void insertion_sort(Tup* a, uint32_t n) {
     for (uint32_t i = 1; i < n; i++) {
         Tup x = a[i];
         uint32_t j = i;
@@ -249,218 +339,305 @@ __device__ __forceinline__ void lds_insertion_sort(Tup* a, uint32_t n) {
     }
 }
 
-__device__ void sub_overflow(const SubWaveArgs& A, uint32_t b, uint32_t d2,
-                             const uint32_t* n, const uint64_t* off,
-                             bool sizes_known, int lane) {
-    if (lane != 0) return;
-    uint32_t n2[2] = {0, 0};
-    uint64_t o2[2] = {0, 0};
-    for (int r = 0; r < A.nrel; r++) {
-        if (sizes_known) {
-            n2[r] = n[r];
-            o2[r] = off[r];
-            continue;
+// Group tables in LDS: wave r builds relation r's run table, run-start bitmap
+// and window tiles (no block barrier inside; one at the end), every thread
+// clears the d3 histograms.
+__device__ __forceinline__ void build_tables(const GroupArgs& A, GroupLDS& L,
+                                             const GroupMeta& M) {
+    const uint32_t wid = otid() >> 6, lane = otid() & 63;
+    if (wid < (uint32_t)A.nrel) {
+        const int r = wid;
+        const uint32_t nt = r ? M.nt[1] : M.nt[0];
+        if (lane < GS_WIN) L.smap[r][lane] = 0ull;
+        // tiles lane and lane + 64: scan of (start in tile << 32 | length)
+        const unsigned long long p0 = ((unsigned long long)M.lo[0] << 32) | M.len[0];
+        const unsigned long long p1 = ((unsigned long long)M.lo[1] << 32) | M.len[1];
+        const unsigned long long i0 = wave_incl_scan64(p0);
+        const unsigned long long tot0 = __shfl(i0, 63, 64);
+        const unsigned long long i1 = wave_incl_scan64(p1) + tot0;
+        const unsigned long long tot = __shfl(i1, 63, 64);
+        const uint32_t sA = (uint32_t)(i0 - p0), sB = (uint32_t)(i1 - p1);
+        if (lane < nt) {
+            L.runoff[r][lane] = sA;
+            L.runsrc[r][lane] = lane * (uint32_t)TILE2 + M.lo[0];
         }
-        const TileTable& tt = A.tt[r];
-        for (uint32_t t = tt.btile0[b]; t < tt.btile0[b + 1]; t++) {
-            const uint16_t* pf = tt.pref + (uint64_t)t * (A.nb2 + 1);
-            n2[r] += (uint32_t)pf[d2 + 1] - pf[d2];
-            o2[r] += pf[d2];
+        if (lane + 64 < nt) {
+            L.runoff[r][lane + 64] = sB;
+            L.runsrc[r][lane + 64] = (lane + 64) * (uint32_t)TILE2 + M.lo[1];
+        }
+        if (lane == 0) {
+            L.runoff[r][nt <= GS_TMAX ? nt : 0] = (uint32_t)tot;
+            L.n[r] = nt <= GS_TMAX ? (uint32_t)tot : 0xffffffffu;
+            L.off[r] = (uint32_t)(tot >> 32);
+        }
+        wave_lds_sync();
+        if (lane < nt && M.len[0] > 0) {
+            atomicOr(&L.smap[r][sA >> 6], 1ull << (sA & 63));
+            L.stile[r][sA] = (uint8_t)lane;
+        }
+        if (lane + 64 < nt && M.len[1] > 0) {
+            atomicOr(&L.smap[r][sB >> 6], 1ull << (sB & 63));
+            L.stile[r][sB] = (uint8_t)(lane + 64);
+        }
+        if (lane < GS_WIN && nt > 0 && nt <= GS_TMAX) {
+            const uint32_t pos = lane * 64;
+            uint32_t t = 0;
+#pragma unroll
+            for (uint32_t step = GS_TMAX / 2; step; step >>= 1)
+                if (t + step < nt && L.runoff[r][t + step] <= pos) t += step;
+            L.wtile[r][lane] = (uint8_t)t;
         }
     }
-    const uint32_t k = atomicAdd(A.novf, 1u);
-    if (k < A.ovf_cap) {
-        OvfEntry e;
-        e.bucket = b;
-        e.d2 = d2;
-        e.nr[0] = n2[0];
-        e.nr[1] = n2[1];
-        e.off[0] = o2[0];
-        e.off[1] = o2[1];
-        A.ovf[k] = e;
+    for (uint32_t i = otid(); i < GS_NB3; i += GS_THREADS) (&L.cnt[0][0])[i] = 0u;
+    if (otid() == 0) L.nlong = 0;
+    __syncthreads();
+}
+
+// The group goes to the skew path: its runs are copied, unsorted, to the
+// group's final place in `out` and the group is queued.  Called by the whole
+// workgroup (uniform control flow).
+__device__ __forceinline__ void group_overflow(const GroupArgs& A, GroupLDS& L,
+                                               const GroupMeta& M) {
+    uint32_t nn[2] = {0, 0};
+    uint64_t oo[2] = {0, 0};
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        if (r >= A.nrel) break;
+        const uint16_t* pref = A.tt[r].pref;
+        const uint32_t t0 = M.t0[r], nt = M.nt[r];
+        unsigned long long acc = 0;
+        for (uint32_t t = otid(); t < nt; t += GS_THREADS) {
+            const uint16_t* pf = pref + (uint64_t)(t0 + t) * (A.nb2 + 1) + M.g;
+            acc += ((unsigned long long)pf[0] << 32) | (uint32_t)(pf[1] - pf[0]);
+        }
+        unsigned long long tot;
+        (void)block_scan64(acc, L.scan64, &tot);
+        nn[r] = (uint32_t)tot;
+        oo[r] = tot >> 32;
+        Tup* dst = A.out[r] + M.bst[r] + oo[r];
+        const Tup* tp = A.tmp[r] + M.bst[r];
+        uint32_t pos = 0;
+        for (uint32_t t = 0; t < nt; t++) {
+            const uint16_t* pf = pref + (uint64_t)(t0 + t) * (A.nb2 + 1) + M.g;
+            const uint32_t lo = pf[0], len = (uint32_t)(pf[1] - pf[0]);
+            const Tup* src = tp + (uint64_t)t * TILE2 + lo;
+            for (uint32_t i = otid(); i < len; i += GS_THREADS) dst[pos + i] = src[i];
+            pos += len;
+        }
+    }
+    if (otid() == 0) {
+        const uint32_t k = atomicAdd(A.novf, 1u);
+        if (k < A.ovf_cap) {
+            OvfEntry e;
+            e.bucket = M.b;
+            e.d2 = M.g;
+            e.nr[0] = nn[0];
+            e.nr[1] = nn[1];
+            e.off[0] = oo[0];
+            e.off[1] = oo[1];
+            A.ovf[k] = e;
+        }
     }
 }
 
-__global__ void __launch_bounds__(SW_THREADS)
-k_subwave(SubWaveArgs A) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
-    WaveLDS& L = reinterpret_cast<WaveLDS*>(lds_raw)[threadIdx.x >> 6];
-    const RangePlan P = *A.plan_dev;
-    const uint32_t nb2 = A.nb2;
-    const uint32_t nb3 = 1u << P.D3;
-    const uint32_t d2lim = 1u << P.D2;
-    const int lane = lane_id();
-    const uint64_t lmask_le = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+// gather relation r's group into registers (loads only: every load in
+// flight at once); lanes past the end re-read the last element
+__device__ __forceinline__ void gather_group(const GroupArgs& A, GroupLDS& L,
+                                             const GroupMeta& C, int r, uint32_t n,
+                                             Tup (&v)[GS_ITEMS]) {
+    if (n == 0) return;
+    const Tup* tp = A.tmp[r] + C.bst[r];
+    const uint32_t last = n - 1;
+#pragma unroll
+    for (int k = 0; k < GS_ITEMS; k++) {
+        const uint32_t j = min(k * GS_THREADS + otid(), last);
+        const uint32_t w = j >> 6;
+        const unsigned long long bits = L.smap[r][w] & (~0ull >> (63 - (j & 63)));
+        const uint32_t t = bits ? L.stile[r][(w << 6) + 63 - __clzll(bits)]
+                                : L.wtile[r][w];
+        v[k] = tp[L.runsrc[r][t] + (j - L.runoff[r][t])];
+    }
+}
+
+// Sort relation r's group (in registers) by the level-3 digit in LDS and
+// write it to its final place.  With GATHER_NEXT, S's gather is issued
+// right after R's elements are placed (R's registers are free then).
+// Returns false when the group must take the skew path.
+template <bool GATHER_NEXT>
+__device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS& L,
+                                           const GroupMeta& C, const RangePlan& P,
+                                           int r, uint32_t nr, Tup (&v)[GS_ITEMS],
+                                           bool& clamped, Tup (&vnext)[GS_ITEMS],
+                                           uint32_t nnext) {
+    const uint32_t tid = otid(), wid = tid >> 6, lane = tid & 63;
+    const uint32_t d12 = (C.b << P.D2) | C.g;
     const uint64_t bu = key_u(P.base);
+    // ---- level-3 digits, histogram (two u16 counters per word)
+    uint32_t dg[GS_ITEMS];
+#pragma unroll
+    for (int k = 0; k < GS_ITEMS; k++) {
+        const bool valid = k * GS_THREADS + tid < nr;
+        const int64_t key = tup_key(v[k]);
+        const uint64_t ku = key_u(key);
+        clamped |= valid && ((ku < bu) || (ku - bu > P.span));
+        dg[k] = plan_d3(P, plan_rel(P, key), d12);
+        if (valid) atomicAdd(&L.cnt[r][dg[k] >> 1], 1u << ((dg[k] & 1) * 16));
+    }
+    __syncthreads();
+    // ---- exclusive scan of the bins: thread owns GS_BPT consecutive bins;
+    // wave totals meet in LDS (two barriers, one carries the "any equal-digit
+    // run" vote)
+    uint32_t c[GS_BPT];
+    uint32_t loc = 0, mx = 0;
+#pragma unroll
+    for (int q = 0; q < GS_BPT / 2; q++) {
+        const uint32_t wv = L.cnt[r][tid * (GS_BPT / 2) + q];
+        c[2 * q] = wv & 0xffffu;
+        c[2 * q + 1] = wv >> 16;
+        loc += c[2 * q] + c[2 * q + 1];
+        mx = max(mx, max(c[2 * q], c[2 * q + 1]));
+    }
+    const uint32_t incl = wave_incl_scan32(loc);
+    if (lane == 63) L.wtot[wid] = incl;
+    const bool dup = __syncthreads_or(mx > 1);
+    uint32_t ex = incl - loc;
+#pragma unroll
+    for (uint32_t w = 0; w < GS_THREADS / 64; w++)
+        if (w < wid) ex += L.wtot[w];
+    const uint32_t first = ex;
+#pragma unroll
+    for (int q = 0; q < GS_BPT / 2; q++) {
+        const uint32_t lo16 = ex;
+        ex += c[2 * q];
+        L.cur[tid * (GS_BPT / 2) + q] = lo16 | (ex << 16);
+        ex += c[2 * q + 1];
+    }
+    __syncthreads();
+    // ---- place (lanes past the end drop their element in the dump slot)
+#pragma unroll
+    for (int k = 0; k < GS_ITEMS; k++) {
+        const bool valid = k * GS_THREADS + tid < nr;
+        const uint32_t sh = (dg[k] & 1) * 16;
+        const uint32_t old = atomicAdd(&L.cur[dg[k] >> 1], valid ? 1u << sh : 0u);
+        L.B[valid ? (old >> sh) & 0xffffu : GS_CAP] = v[k];
+    }
+    if (GATHER_NEXT) gather_group(A, L, C, 1, nnext, vnext);
+    __syncthreads();
+    if (dup) {
+        // ---- equal-digit runs: short ones sorted here, long ones listed
+        uint32_t e = first;
+#pragma unroll
+        for (int q = 0; q < GS_BPT; q++) {
+            const uint32_t b0 = e;
+            e += c[q];
+            if (c[q] > 1) {
+                if (c[q] <= GS_RUNMAX) {
+                    insertion_sort(L.B + b0, c[q]);
+                } else {
+                    const uint32_t li = atomicAdd(&L.nlong, 1u);
+                    if (li < GS_LONGMAX) {
+                        L.lrun[li][0] = b0;
+                        L.lrun[li][1] = e;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        // long runs are accepted only when already in order (e.g. equal
+        // tuples of a hot key); otherwise the skew path
+        const uint32_t nl = L.nlong;
+        bool bad = nl > GS_LONGMAX;
+        for (uint32_t li = 0; li < nl && li < GS_LONGMAX && !bad; li++) {
+            const uint32_t s0 = L.lrun[li][0], e0 = L.lrun[li][1];
+            bool ok = true;
+            for (uint32_t i = s0 + 1 + tid; i < e0; i += GS_THREADS)
+                ok &= !tup_less(L.B[i], L.B[i - 1]);
+            bad = __syncthreads_or(!ok);
+        }
+        if (bad) return false;
+        if (tid == 0) L.nlong = 0;
+    }
+    // ---- write the sorted group: one contiguous stream
+    Tup* dst = A.out[r] + C.bst[r] + L.off[r];
+#pragma unroll
+    for (int k = 0; k < GS_ITEMS; k++) {
+        const uint32_t j = k * GS_THREADS + tid;
+        if (j < nr) dst[j] = L.B[j];
+    }
+    return true;
+}
 
-    // the workgroup owns [g0, s_end); its waves take them interleaved
-    const uint32_t g0 = blockIdx.x * SW_WAVES * A.spw;
-    uint32_t s_end = g0 + SW_WAVES * A.spw;
-    if (s_end > A.nsub) s_end = A.nsub;
+// When S's group is gathered: 0 = with R's (both in flight at once),
+// 1 = once R's elements sit in LDS, 2 = after R's group is written.  The
+// later, the fewer VGPRs (16-byte tuples need it to stay under 256).
+#ifdef KEY_8B
+constexpr int kGatherS = 2;
+#else
+constexpr int kGatherS = 0;
+#endif
+
+// Persistent: workgroup w sorts groups [g_begin + w * per, ... + per) in
+// order; the next group's tile runs are loaded while the current one is
+// gathered and sorted.
+__global__ void __launch_bounds__(GS_THREADS, GS_WG_PER_CU * GS_THREADS / 256)
+k_groupsort(GroupArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    GroupLDS& L = *reinterpret_cast<GroupLDS*>(lds_raw);
+    const RangePlan& P = A.plan;
+    const uint32_t tid = otid(), lane = tid & 63;
+    const int nrel = A.nrel;
+    const uint32_t gbeg = A.g_begin + blockIdx.x * A.per;
+    const uint32_t gend = min(gbeg + A.per, A.g_end);
     unsigned long long matches = 0;
-    uint32_t cur_b = 0xffffffffu;
-    uint32_t t0[2] = {0, 0}, nt[2] = {0, 0};
-    uint64_t bst[2] = {0, 0};
+    if (gbeg >= gend) return;
 
-    for (uint32_t s = g0 + (threadIdx.x >> 6); s < s_end; s += SW_WAVES) {
-        const uint32_t b = s / nb2;
-        const uint32_t d2 = s % nb2;
-        if (d2 >= d2lim) continue;  // a table column no digit maps to
-        if (b != cur_b) {
-            cur_b = b;
-#pragma unroll
-            for (int r = 0; r < 2; r++) {
-                if (r < A.nrel) {
-                    t0[r] = A.tt[r].btile0[b];
-                    nt[r] = A.tt[r].btile0[b + 1] - t0[r];
-                    bst[r] = A.bstart[r][b];
-                }
-            }
-        }
-        // ---- sizes of the sub-bucket in both relations (one round trip)
-        uint32_t n[2] = {0, 0}, plo[2] = {0, 0}, pcnt[2] = {0, 0}, pincl[2] = {0, 0};
-        uint64_t off[2] = {0, 0};
-        bool ovf = false, known = true;
-#pragma unroll
-        for (int r = 0; r < 2; r++) {
-            if (r >= A.nrel) break;
-            if (nt[r] > SW_PMAX) {
-                ovf = true;
-                known = false;
-                continue;
-            }
-            if ((uint32_t)lane < nt[r]) {
-                const uint16_t* pf =
-                    A.tt[r].pref + (uint64_t)(t0[r] + lane) * (nb2 + 1) + d2;
-                plo[r] = pf[0];
-                pcnt[r] = (uint32_t)pf[1] - plo[r];
-            }
-        }
-#pragma unroll
-        for (int r = 0; r < 2; r++) {
-            if (r >= A.nrel || nt[r] > SW_PMAX) continue;
-            pincl[r] = wave_incl_scan(pcnt[r]);
-            n[r] = __shfl(pincl[r], 63, 64);
-            off[r] = wave_sum((unsigned long long)plo[r]);
-            if (n[r] > SW_CAP) ovf = true;
-        }
-        if (ovf) {
-            sub_overflow(A, b, d2, n, off, known, lane);
+    GroupMeta M;
+    load_meta(A, gbeg, M, false);
+    for (uint32_t gi = gbeg; gi < gend; gi++) {
+        build_tables(A, L, M);
+        const GroupMeta C = M;
+        if (gi + 1 < gend) load_meta(A, gi + 1, M, true);  // prefetch
+        const uint32_t n0 = __builtin_amdgcn_readfirstlane(L.n[0]);
+        const uint32_t n1 = nrel > 1 ? __builtin_amdgcn_readfirstlane(L.n[1]) : 0;
+        if (n0 > GS_CAP || n1 > GS_CAP) {
+            group_overflow(A, L, C);
+            __syncthreads();
             continue;
         }
-
-        const uint32_t d12 = (b << P.D2) | d2;
+        Tup vr[GS_ITEMS], vs[GS_ITEMS];
+        gather_group(A, L, C, 0, n0, vr);
+        if (kGatherS == 0 && nrel > 1) gather_group(A, L, C, 1, n1, vs);
         bool clamped = false;
-#pragma unroll
-        for (int r = 0; r < 2; r++) {
-            if (r >= A.nrel) break;
-            const uint32_t nr = n[r];
-            // ---- piece tables and the piece-start map
-            if ((uint32_t)lane < nt[r]) {
-                L.psrc[lane] = lane * (uint32_t)TILE2 + plo[r];
-                L.pdst[lane] = pincl[r] - pcnt[r];
-            }
-            for (uint32_t j = lane; j < SW_CAP / 4; j += 64)
-                reinterpret_cast<uint32_t*>(L.pat)[j] = 0xffffffffu;
-#pragma unroll
-            for (int q = 0; q < SW_NB3 / 64; q++) L.h[r][lane * (SW_NB3 / 64) + q] = 0;
-            wave_lds_sync();
-            if ((uint32_t)lane < nt[r] && pcnt[r] > 0)
-                L.pat[pincl[r] - pcnt[r]] = (uint8_t)lane;
-            wave_lds_sync();
-
-            // ---- gather: the piece of position i is the last piece start <= i
-            Tup v[SW_ITEMS];
-            uint32_t dg[SW_ITEMS];
-            const Tup* tp = A.tmp[r] + bst[r];
-            uint32_t carry = 0;
-#pragma unroll
-            for (int k = 0; k < SW_ITEMS; k++) {
-                const uint32_t i = k * 64 + lane;
-                const bool valid = i < nr;
-                const uint32_t m = valid ? L.pat[i] : 0xffu;
-                const uint64_t starts = __ballot(m != 0xffu) & lmask_le;
-                const uint32_t src_lane = starts ? 63 - __clzll(starts) : 0;
-                const uint32_t pm = __shfl(m, src_lane, 64);
-                const uint32_t p = starts ? pm : carry;
-                carry = __shfl(p, 63, 64);
-                if (valid) v[k] = tp[L.psrc[p] + (i - L.pdst[p])];
-            }
-            // ---- level-3 digits, histogram
-#pragma unroll
-            for (int k = 0; k < SW_ITEMS; k++) {
-                const uint32_t i = k * 64 + lane;
-                if (i < nr) {
-                    const int64_t key = tup_key(v[k]);
-                    const uint64_t ku = key_u(key);
-                    clamped |= (ku < bu) || (ku - bu > P.span);
-                    dg[k] = plan_d3(P, plan_rel(P, key), d12);
-                    atomicAdd(&L.h[r][dg[k]], 1u);
-                }
-            }
-            wave_lds_sync();
-            // ---- exclusive scan of the bins: lane owns 4 consecutive bins
-            uint32_t c[SW_NB3 / 64];
-            uint32_t loc = 0, mx = 0;
-#pragma unroll
-            for (int q = 0; q < SW_NB3 / 64; q++) {
-                c[q] = L.h[r][lane * (SW_NB3 / 64) + q];
-                loc += c[q];
-                mx = c[q] > mx ? c[q] : mx;
-            }
-            uint32_t ex = wave_incl_scan(loc) - loc;
-#pragma unroll
-            for (int q = 0; q < SW_NB3 / 64; q++) {
-                L.h[r][lane * (SW_NB3 / 64) + q] = ex;
-                L.fill[lane * (SW_NB3 / 64) + q] = ex;
-                ex += c[q];
-            }
-            if (wave_max(mx) > SW_RUNMAX) {
-                ovf = true;
-                break;
-            }
-            wave_lds_sync();
-            // ---- place, fix equal-digit runs, write
-#pragma unroll
-            for (int k = 0; k < SW_ITEMS; k++) {
-                const uint32_t i = k * 64 + lane;
-                if (i < nr) L.B[atomicAdd(&L.fill[dg[k]], 1u)] = v[k];
-            }
-            wave_lds_sync();
-            for (uint32_t d = lane; d < nb3; d += 64) {
-                const uint32_t s0 = L.h[r][d];
-                const uint32_t e0 = (d + 1 < nb3) ? L.h[r][d + 1] : nr;
-                if (e0 - s0 > 1) lds_insertion_sort(L.B + s0, e0 - s0);
-            }
-            wave_lds_sync();
-            Tup* dst = A.out[r] + bst[r] + off[r];
-            for (uint32_t i = lane; i < nr; i += 64) {
-                const Tup t = L.B[i];
-                dst[i] = t;
-                if (r == 0) L.rkey[i] = (KeyT)tup_key(t);
-            }
-            wave_lds_sync();
-        }
-        if (ovf) {
-            // a long equal-digit run: the fallback re-sorts the sub-bucket of
-            // both relations (an R already written here is simply rewritten)
-            sub_overflow(A, b, d2, n, off, true, lane);
+        bool ok = sort_group<kGatherS == 1>(A, L, C, P, 0, n0, vr, clamped, vs,
+                                            nrel > 1 ? n1 : 0);
+        if (kGatherS == 2 && nrel > 1) gather_group(A, L, C, 1, n1, vs);
+        if (ok && nrel > 1)
+            ok = sort_group<false>(A, L, C, P, 1, n1, vs, clamped, vs, 0);
+        if (!ok) {
+            __syncthreads();
+            group_overflow(A, L, C);
+            __syncthreads();
             continue;
         }
 
-        // ---- merge-join count of the two sub-buckets
-        if (A.nrel == 2) {
-            const uint32_t nR = n[0], nS = n[1];
-            if (P.s3 == 0 && !__any(clamped)) {
+        // ---- merge-join count of the two groups
+        if (nrel == 2) {
+            const bool exact = P.s3 == 0 && !__syncthreads_or(clamped);
+            if (exact) {
                 // the level-3 digit is the exact key: sum_k |R_k| * |S_k|
-                for (uint32_t d = lane; d < nb3; d += 64) {
-                    const uint32_t cr = ((d + 1 < nb3) ? L.h[0][d + 1] : nR) - L.h[0][d];
-                    const uint32_t cs = ((d + 1 < nb3) ? L.h[1][d + 1] : nS) - L.h[1][d];
-                    matches += (unsigned long long)cr * cs;
+#pragma unroll
+                for (int q = 0; q < GS_BPT / 2; q++) {
+                    const uint32_t a0 = L.cnt[0][tid * (GS_BPT / 2) + q];
+                    const uint32_t a1 = L.cnt[1][tid * (GS_BPT / 2) + q];
+                    matches += (unsigned long long)(a0 & 0xffffu) * (a1 & 0xffffu) +
+                               (unsigned long long)(a0 >> 16) * (a1 >> 16);
                 }
             } else {
-                // S is still in B, R's sorted keys in rkey
-                for (uint32_t i = lane; i < nS; i += 64) {
+                // S is still in B; R's sorted group is in out (written above
+                // by this workgroup: visible after the barrier)
+                const Tup* Rs = A.out[0] + C.bst[0] + L.off[0];
+                const uint32_t nR = n0, nS = n1;
+                for (uint32_t i = tid; i < nS; i += GS_THREADS) {
                     const int64_t k = tup_key(L.B[i]);
                     if (i > 0 && tup_key(L.B[i - 1]) == k) continue;
                     uint32_t e = i + 1;
@@ -468,43 +645,23 @@ k_subwave(SubWaveArgs A) {
                     uint32_t lo = 0, hi = nR;
                     while (lo < hi) {
                         const uint32_t m = (lo + hi) >> 1;
-                        if ((int64_t)L.rkey[m] < k) lo = m + 1; else hi = m;
+                        if (tup_key(Rs[m]) < k) lo = m + 1; else hi = m;
                     }
                     const uint32_t lb = lo;
                     hi = nR;
                     while (lo < hi) {
                         const uint32_t m = (lo + hi) >> 1;
-                        if ((int64_t)L.rkey[m] <= k) lo = m + 1; else hi = m;
+                        if (tup_key(Rs[m]) <= k) lo = m + 1; else hi = m;
                     }
                     matches += (unsigned long long)(lo - lb) * (e - i);
                 }
             }
-            wave_lds_sync();
         }
+        __syncthreads();  // tables, histograms and B are rebuilt next
     }
-    if (A.nrel == 2) {
+    if (nrel == 2) {
         matches = wave_sum(matches);
         if (lane == 0 && matches) atomicAdd(A.count_dev, matches);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// overflow: copy the pieces of a sub-bucket, unsorted, into its output slot
-__global__ void __launch_bounds__(256)
-k_gather_sub(const Tup* __restrict__ tmp, Tup* __restrict__ out,
-             const uint64_t* __restrict__ bstart, TileTable tt,
-             const OvfEntry* __restrict__ ovf, int r, uint32_t nb2) {
-    const OvfEntry e = ovf[blockIdx.x];
-    const uint32_t b = e.bucket, d2 = e.d2;
-    Tup* dst = out + bstart[b] + e.off[r];
-    uint32_t pos = 0;
-    for (uint32_t t = tt.btile0[b]; t < tt.btile0[b + 1]; t++) {
-        const uint16_t* pf = tt.pref + (uint64_t)t * (nb2 + 1);
-        uint32_t lo = pf[d2];
-        uint32_t hi = pf[d2 + 1];
-        const Tup* src = tmp + tt.off[t] + lo;
-        for (uint32_t i = threadIdx.x; i < hi - lo; i += 256) dst[pos + i] = src[i];
-        pos += hi - lo;
     }
 }
 
@@ -512,7 +669,7 @@ k_gather_sub(const Tup* __restrict__ tmp, Tup* __restrict__ out,
 // range plan from a strided sample of the relations (or from hints)
 __global__ void __launch_bounds__(256)
 k_plan(const Tup* r0, uint64_t n0, const Tup* r1, uint64_t n1, uint32_t D1,
-       uint32_t D2, int64_t hmin, int64_t hmax, RangePlan* plan) {
+       uint32_t D2, uint32_t D2cap, int64_t hmin, int64_t hmax, RangePlan* plan) {
     __shared__ int64_t smin[4], smax[4];
     int64_t mn = INT64_MAX, mx = INT64_MIN;
     const int S = 4096;
@@ -562,91 +719,197 @@ k_plan(const Tup* r0, uint64_t n0, const Tup* r1, uint64_t n1, uint32_t D1,
             lo = (int64_t)(lu ^ 0x8000000000000000ull);
             hi = (int64_t)(hu ^ 0x8000000000000000ull);
         }
-        *plan = make_plan(lo, hi, D1, D2, SW_D3MAX);
+        *plan = make_plan(lo, hi, D1, D2, D2cap, GS_D3MAX);
     }
 }
 
 void plan_from_sample(Workspace* ws, const Tup* const* rels, const uint64_t* ns,
-                      int nrel, uint32_t D1, uint32_t D2, int64_t hint_min,
-                      int64_t hint_max, RangePlan* plan_dev, hipStream_t st) {
+                      int nrel, uint32_t D1, uint32_t D2, uint32_t D2cap,
+                      int64_t hint_min, int64_t hint_max, RangePlan* plan_dev,
+                      hipStream_t st) {
     (void)ws;
     hipLaunchKernelGGL(k_plan, dim3(1), dim3(256), 0, st, rels[0], ns[0],
                        nrel > 1 ? rels[1] : (const Tup*)nullptr,
-                       nrel > 1 ? ns[1] : 0, D1, D2, hint_min, hint_max,
+                       nrel > 1 ? ns[1] : 0, D1, D2, D2cap, hint_min, hint_max,
                        plan_dev);
     SMJ_CHECK(hipGetLastError());
 }
 
+// expected group size the plan aims for (capi.hip choose_levels)
+const uint32_t kGroupTarget = GS_CAP * 4 / 5 >= 2048 ? 2048 : (GS_CAP * 4 / 5 >= 1024 ? 1024 : 512);
+
 // ---------------------------------------------------------------------------
-void bucket_sort(Workspace* ws, const BucketSortArgs& a, uint32_t D2,
-                 hipStream_t st) {
-    const uint32_t nb = a.nbuckets;
-    const uint32_t nb2 = 1u << D2;
-    TileTable tt[2];
-    static const char* names[2][6] = {
-        {"bs_off0", "bs_len0", "bs_bkt0", "bs_bt00", "bs_pref0", "bs_nt0"},
-        {"bs_off1", "bs_len1", "bs_bkt1", "bs_bt01", "bs_pref1", "bs_nt1"}};
-    uint64_t maxt[2] = {0, 0};
-    for (int r = 0; r < a.nrel; r++) {
-        maxt[r] = (a.n[r] + TILE2 - 1) / TILE2 + nb + 1;
-        tt[r].off = (uint64_t*)ws->scratch(names[r][0], maxt[r] * 8);
-        tt[r].len = (uint32_t*)ws->scratch(names[r][1], maxt[r] * 4);
-        tt[r].bucket = (uint32_t*)ws->scratch(names[r][2], maxt[r] * 4);
-        tt[r].btile0 = (uint32_t*)ws->scratch(names[r][3], (nb + 1) * 4);
-        tt[r].pref = (uint16_t*)ws->scratch(names[r][4], maxt[r] * (nb2 + 1) * 2);
-        tt[r].ntiles = (uint32_t*)ws->scratch(names[r][5], 4);
-        hipLaunchKernelGGL(k_tiles, dim3(1), dim3(256), 0, st, a.bstart[r],
-                           a.bcount[r], nb, tt[r]);
+// Ring size per relation in tuples (0 = the tile pass works in place in the
+// partition buffer).  With a ring, buckets are processed in batches whose
+// tile-pass output fits the ring, so the group pass re-reads it from the
+// Infinity Cache instead of HBM.  SMJ_RING_MB overrides the default.
+static uint64_t ring_tuples() {
+    static int64_t mb = -1;
+    if (mb < 0) {
+        const char* e = getenv("SMJ_RING_MB");
+        mb = e ? atoll(e) : 0;
+        if (mb < 0) mb = 0;
     }
-    if (a.ev_tile) SMJ_CHECK(hipEventRecord(a.ev_tile, st));
+    return (uint64_t)mb * (1ull << 20) / sizeof(Tup);
+}
+
+void bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
+    const uint32_t nb = a.nbuckets;
+    const int nrel = a.nrel;
     static bool attr = false;
     if (!attr) {
         SMJ_CHECK(hipFuncSetAttribute((const void*)k_tilepass,
                                       hipFuncAttributeMaxDynamicSharedMemorySize,
                                       160 * 1024));
-        SMJ_CHECK(hipFuncSetAttribute((const void*)k_subwave,
+        // two workgroups per CU (launch bounds): ask for exactly what one needs
+        SMJ_CHECK(hipFuncSetAttribute((const void*)k_groupsort,
                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      160 * 1024));
+                                      (int)sizeof(GroupLDS)));
         attr = true;
     }
-    const size_t tp_lds = TILE2 * sizeof(Tup) + nb2 * 4 + 64;
-    for (int r = 0; r < a.nrel; r++) {
-        TraceScope ts(ws, "k_tilepass", st);
-        hipLaunchKernelGGL(k_tilepass, dim3((uint32_t)maxt[r]), dim3(TP_THREADS),
-                           tp_lds, st, a.part[r], a.tmp[r], tt[r], a.plan_dev, nb2);
-    }
-    if (a.ev_bucket) SMJ_CHECK(hipEventRecord(a.ev_bucket, st));
 
-    const uint32_t nsub = nb * nb2;
-    const uint32_t ovf_cap = nsub;
+    // ---- host view of the plan and the bucket counts (one synchronisation):
+    // launch sizes, tile numbering and batches are derived from them
+    uint64_t* hcnt = (uint64_t*)ws->host_pinned("bs_hcnt", (size_t)2 * nb * 8);
+    uint64_t* hst = (uint64_t*)ws->host_pinned("bs_hst", (size_t)2 * nb * 8);
+    RangePlan* hplan = (RangePlan*)ws->host_pinned("bs_hplan", sizeof(RangePlan));
+    for (int r = 0; r < nrel; r++) {
+        SMJ_CHECK(hipMemcpyAsync(hcnt + r * nb, a.bcount[r], nb * 8,
+                                 hipMemcpyDeviceToHost, st));
+        SMJ_CHECK(hipMemcpyAsync(hst + r * nb, a.bstart[r], nb * 8,
+                                 hipMemcpyDeviceToHost, st));
+    }
+    SMJ_CHECK(hipMemcpyAsync(hplan, a.plan_dev, sizeof(RangePlan),
+                             hipMemcpyDeviceToHost, st));
+    SMJ_CHECK(hipStreamSynchronize(st));
+    const uint32_t nb2 = 1u << hplan->D2;  // groups per bucket
+
+    TileTable tt[2];
+    static const char* names[2][5] = {
+        {"bs_off0", "bs_len0", "bs_bkt0", "bs_bt00", "bs_pref0"},
+        {"bs_off1", "bs_len1", "bs_bkt1", "bs_bt01", "bs_pref1"}};
+    uint32_t* hbt = (uint32_t*)ws->host_pinned("bs_hbt", (size_t)2 * (nb + 1) * 4);
+    uint64_t maxb[2] = {0, 0};
+    for (int r = 0; r < nrel; r++) {
+        uint32_t* bt0 = hbt + r * (nb + 1);
+        uint32_t acc = 0;
+        for (uint32_t b = 0; b < nb; b++) {
+            bt0[b] = acc;
+            acc += (uint32_t)((hcnt[r * nb + b] + TILE2 - 1) / TILE2);
+            maxb[r] = std::max<uint64_t>(maxb[r], hcnt[r * nb + b]);
+        }
+        bt0[nb] = acc;
+        const uint64_t ntl = acc ? acc : 1;
+        tt[r].off = (uint64_t*)ws->scratch(names[r][0], ntl * 8);
+        tt[r].len = (uint32_t*)ws->scratch(names[r][1], ntl * 4);
+        tt[r].bucket = (uint32_t*)ws->scratch(names[r][2], ntl * 4);
+        tt[r].btile0 = (uint32_t*)ws->scratch(names[r][3], (nb + 1) * 4);
+        tt[r].pref = (uint16_t*)ws->scratch(names[r][4], ntl * (nb2 + 1) * 2);
+        SMJ_CHECK(hipMemcpyAsync(tt[r].btile0, bt0, (nb + 1) * 4,
+                                 hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(k_tiles, dim3(nb), dim3(64), 0, st, a.bstart[r],
+                           a.bcount[r], tt[r]);
+    }
+    if (nrel == 1) tt[1] = tt[0];
+    if (a.ev_tile) SMJ_CHECK(hipEventRecord(a.ev_tile, st));
+
+    const uint64_t ring = ring_tuples();
+    Tup* ringbuf[2] = {nullptr, nullptr};
+    uint64_t ringcap[2] = {0, 0};
+    if (ring) {
+        for (int r = 0; r < nrel; r++) {
+            ringcap[r] = std::max<uint64_t>(ring, maxb[r]);
+            ringbuf[r] = (Tup*)ws->scratch(r ? "bs_ring1" : "bs_ring0",
+                                           ringcap[r] * sizeof(Tup));
+        }
+    }
+    // batches [b0, b1): every relation's tuples of the batch fit its ring
+    std::vector<std::pair<uint32_t, uint32_t>> batches;
+    if (!ring) {
+        batches.push_back({0u, nb});
+    } else {
+        uint32_t b0 = 0;
+        while (b0 < nb) {
+            uint32_t b1 = b0;
+            uint64_t fill[2] = {0, 0};
+            while (b1 < nb) {
+                bool fits = true;
+                for (int r = 0; r < nrel; r++)
+                    if (fill[r] + hcnt[r * nb + b1] > ringcap[r]) fits = false;
+                if (!fits && b1 > b0) break;
+                for (int r = 0; r < nrel; r++) fill[r] += hcnt[r * nb + b1];
+                b1++;
+            }
+            batches.push_back({b0, b1});
+            b0 = b1;
+        }
+    }
+
+    const uint32_t ngroups = nb * nb2;
+    const uint32_t ovf_cap = ngroups;
     OvfEntry* ovf = (OvfEntry*)ws->scratch("bs_ovf", (size_t)ovf_cap * sizeof(OvfEntry));
     uint32_t* novf = (uint32_t*)ws->scratch("bs_novf", 4);
     SMJ_CHECK(hipMemsetAsync(novf, 0, 4, st));
-    SubWaveArgs B;
+    const size_t tp_lds = TILE2 * sizeof(Tup) + nb2 * 4 + 64;
+
+    TilePassArgs T;
+    GroupArgs G;
     for (int r = 0; r < 2; r++) {
-        int rr = r < a.nrel ? r : 0;
-        B.tmp[r] = a.tmp[rr];
-        B.out[r] = a.out[rr];
-        B.bstart[r] = a.bstart[rr];
-        B.tt[r] = tt[rr];
+        const int rr = r < nrel ? r : 0;
+        T.part[r] = a.part[rr];
+        T.tt[r] = tt[rr];
+        T.t0[r] = 0;
+        T.nt[r] = 0;
+        G.out[r] = a.out[rr];
+        G.bstart[r] = a.bstart[rr];
+        G.tt[r] = tt[rr];
     }
-    B.nrel = a.nrel;
-    B.plan_dev = a.plan_dev;
-    B.count_dev = a.count_dev;
-    B.nb2 = nb2;
-    B.nsub = nsub;
-    // one workgroup of SW_WAVES waves per CU, several sub-buckets per wave
-    const uint32_t target_waves = 256 * SW_WAVES;
-    B.spw = (nsub + target_waves - 1) / target_waves;
-    if (B.spw == 0) B.spw = 1;
-    const uint32_t nwg = (nsub + SW_WAVES * B.spw - 1) / (SW_WAVES * B.spw);
-    B.ovf = ovf;
-    B.novf = novf;
-    B.ovf_cap = ovf_cap;
-    {
-        TraceScope ts(ws, "k_subwave", st);
-        hipLaunchKernelGGL(k_subwave, dim3(nwg), dim3(SW_THREADS),
-                           sizeof(WaveLDS) * SW_WAVES, st, B);
+    T.plan = *hplan;
+    T.nb2 = nb2;
+    G.nrel = nrel;
+    G.plan = *hplan;
+    G.count_dev = a.count_dev;
+    G.nb2 = nb2;
+    G.ovf = ovf;
+    G.novf = novf;
+    G.ovf_cap = ovf_cap;
+    bool ev_bucket_done = false;
+    for (const auto& bt : batches) {
+        const uint32_t b0 = bt.first, b1 = bt.second;
+        uint32_t ntiles = 0;
+        for (int r = 0; r < 2; r++) {
+            const int rr = r < nrel ? r : 0;
+            Tup* tmp = a.tmp[rr];
+            // ring: tile offsets of the batch start at hst[b0] -> ring[0]
+            if (ring) tmp = ringbuf[rr] - (ptrdiff_t)hst[rr * nb + b0];
+            T.tmp[r] = tmp;
+            G.tmp[r] = tmp;
+            if (r < nrel) {
+                const uint32_t* bt0 = hbt + r * (nb + 1);
+                T.t0[r] = bt0[b0];
+                T.nt[r] = bt0[b1] - bt0[b0];
+                ntiles += T.nt[r];
+            }
+        }
+        if (ntiles) {
+            TraceScope ts(ws, "k_tilepass", st);
+            hipLaunchKernelGGL(k_tilepass, dim3(ntiles), dim3(TP_THREADS), tp_lds,
+                               st, T);
+        }
+        if (a.ev_bucket && !ev_bucket_done) {
+            SMJ_CHECK(hipEventRecord(a.ev_bucket, st));
+            ev_bucket_done = true;
+        }
+        G.g_begin = b0 * nb2;
+        G.g_end = b1 * nb2;
+        const uint32_t ng = G.g_end - G.g_begin;
+        // persistent: two workgroups per CU, consecutive groups per workgroup
+        const uint32_t maxwg = GS_WG_PER_CU * 256;
+        G.per = (ng + maxwg - 1) / maxwg;
+        const uint32_t nwg = (ng + G.per - 1) / G.per;
+        TraceScope ts(ws, "k_groupsort", st);
+        hipLaunchKernelGGL(k_groupsort, dim3(nwg), dim3(GS_THREADS),
+                           sizeof(GroupLDS), st, G);
     }
     SMJ_CHECK(hipGetLastError());
     if (a.ev_ovf) SMJ_CHECK(hipEventRecord(a.ev_ovf, st));
@@ -664,27 +927,19 @@ void bucket_sort(Workspace* ws, const BucketSortArgs& a, uint32_t D2,
     std::vector<OvfEntry> he(no);
     SMJ_CHECK(hipMemcpyAsync(he.data(), ovf, no * sizeof(OvfEntry),
                              hipMemcpyDeviceToHost, st));
-    std::vector<uint64_t> hbstart[2];
-    for (int r = 0; r < a.nrel; r++) {
-        hbstart[r].resize(nb);
-        SMJ_CHECK(hipMemcpyAsync(hbstart[r].data(), a.bstart[r], nb * 8,
-                                 hipMemcpyDeviceToHost, st));
-    }
     SMJ_CHECK(hipStreamSynchronize(st));
-    for (int r = 0; r < a.nrel; r++) {
-        hipLaunchKernelGGL(k_gather_sub, dim3(no), dim3(256), 0, st, a.tmp[r],
-                           a.out[r], a.bstart[r], tt[r], ovf, r, nb2);
+    for (int r = 0; r < nrel; r++) {
         std::vector<uint64_t> so(no), sl(no);
         for (uint32_t i = 0; i < no; i++) {
-            so[i] = hbstart[r][he[i].bucket] + he[i].off[r];
+            so[i] = hst[r * nb + he[i].bucket] + he[i].off[r];
             sl[i] = he[i].nr[r];
         }
         segmented_sort(ws, a.out[r], so.data(), sl.data(), no, st);
     }
-    if (a.nrel == 2) {
+    if (nrel == 2) {
         for (uint32_t i = 0; i < no; i++) {
-            const Tup* rp = a.out[0] + hbstart[0][he[i].bucket] + he[i].off[0];
-            const Tup* sp = a.out[1] + hbstart[1][he[i].bucket] + he[i].off[1];
+            const Tup* rp = a.out[0] + hst[he[i].bucket] + he[i].off[0];
+            const Tup* sp = a.out[1] + hst[nb + he[i].bucket] + he[i].off[1];
             if (he[i].nr[0] && he[i].nr[1])
                 merge_join_count(rp, he[i].nr[0], sp, he[i].nr[1], a.count_dev, st);
         }

@@ -106,31 +106,38 @@ static uint32_t ceil_log2(uint64_t x) {
     return b;
 }
 
-// level widths: D1 (partition fan-out) and D2 (tile-pass fan-out) so that the
-// expected sub-bucket is a few hundred tuples (fits the in-LDS bucket pass)
+// level widths: D1 (partition fan-out) and D2 (tile-pass fan-out = groups per
+// bucket) so that the expected group is kGroupTarget tuples (3/4 of what the
+// group pass holds in LDS); the plan may widen D2 up to D2cap to make the last
+// digit the exact key
 static void choose_levels(uint64_t n, uint32_t want_d1, uint32_t* D1,
-                          uint32_t* D2) {
-    // mean sub-bucket <= 2/3 of the per-wave LDS capacity (384 / 768 tuples)
-    const uint64_t target = (sizeof(Tup) == 16) ? 256 : 512;
+                          uint32_t* D2, uint32_t* D2cap) {
+    const uint64_t target = kGroupTarget;
     uint32_t B = n > target ? ceil_log2((n + target - 1) / target) : 0;
-    uint32_t d1 = want_d1 ? want_d1 : 10;
+    // level 1: 512 partitions by default (the scatter's write streams stay
+    // long enough), more when a bucket would exceed ~96 tiles of the tile pass
+    uint32_t d1 = want_d1 ? want_d1 : 9;
+    const uint64_t bucket_cap = 96ull * kTileTuples;
+    while (d1 < kNarrowDigitBits && (n >> d1) > bucket_cap) d1++;
     if (d1 > B) d1 = B;
     if (d1 > kNarrowDigitBits) d1 = kNarrowDigitBits;
     uint32_t d2 = B > d1 ? B - d1 : 0;
     if (d2 > 9) d2 = 9;
     *D1 = d1;
     *D2 = d2;
+    // the plan may add up to two level-2 bits to make the last digit exact
+    *D2cap = d2 + 2 > 9 ? (d2 > 9 ? d2 : 9) : d2 + 2;
 }
 
 static void device_sort(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
                         hipStream_t st) {
     if (n == 0) return;
-    uint32_t D1, D2;
-    choose_levels(n, 0, &D1, &D2);
+    uint32_t D1, D2, D2cap;
+    choose_levels(n, 0, &D1, &D2, &D2cap);
     RangePlan* plan = (RangePlan*)ws->scratch("plan", sizeof(RangePlan));
     const Tup* rels[1] = {in};
     uint64_t ns[1] = {n};
-    plan_from_sample(ws, rels, ns, 1, D1, D2, 1, 0, plan, st);
+    plan_from_sample(ws, rels, ns, 1, D1, D2, D2cap, 1, 0, plan, st);
     const uint32_t nb = 1u << D1;
     Tup* part = (Tup*)ws->scratch("sort_part", n * sizeof(Tup));
     uint64_t* starts = (uint64_t*)ws->scratch("sort_starts", nb * 8);
@@ -153,7 +160,7 @@ static void device_sort(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
     a.nbuckets = nb;
     a.plan_dev = plan;
     a.count_dev = nullptr;
-    bucket_sort(ws, a, D2, st);
+    bucket_sort(ws, a, st);
 }
 
 static void device_join(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
@@ -164,12 +171,12 @@ static void device_join(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
     ws->events();
     SMJ_CHECK(hipEventRecord(ws->ev[0], st));
     SMJ_CHECK(hipMemsetAsync(count_dev, 0, sizeof(unsigned long long), st));
-    uint32_t D1, D2;
-    choose_levels(nR > nS ? nR : nS, fanout_bits, &D1, &D2);
+    uint32_t D1, D2, D2cap;
+    choose_levels(nR > nS ? nR : nS, fanout_bits, &D1, &D2, &D2cap);
     RangePlan* plan = (RangePlan*)ws->scratch("plan", sizeof(RangePlan));
     const Tup* rels[2] = {R, S};
     uint64_t ns[2] = {nR, nS};
-    plan_from_sample(ws, rels, ns, 2, D1, D2, hint_min, hint_max, plan, st);
+    plan_from_sample(ws, rels, ns, 2, D1, D2, D2cap, hint_min, hint_max, plan, st);
     const uint32_t nb = 1u << D1;
     Tup* partR = (Tup*)ws->scratch("join_partR", (nR ? nR : 1) * sizeof(Tup));
     Tup* partS = (Tup*)ws->scratch("join_partS", (nS ? nS : 1) * sizeof(Tup));
@@ -200,7 +207,7 @@ static void device_join(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
     a.ev_tile = nullptr;
     a.ev_bucket = ws->ev[2];
     a.ev_ovf = ws->ev[3];
-    bucket_sort(ws, a, D2, st);
+    bucket_sort(ws, a, st);
     SMJ_CHECK(hipEventRecord(ws->ev[4], st));
 }
 
@@ -608,8 +615,8 @@ static result_t* join_api(relation_t* relR, relation_t* relS,
     uint32_t fb = 0;
     if (joincfg->PARTFANOUT > 0) fb = ceil_log2((uint64_t)joincfg->PARTFANOUT);
     // the reference fan-out (128 by default) only sizes the level-1 pass here;
-    // at least 10 bits keep the sub-buckets LDS sized
-    if (fb < 10) fb = 10;
+    // choose_levels raises it as the relation size needs
+    if (fb < 9) fb = 9;
     device_join(&c.ws, r.d, nR, s.d, nS, sR, sS, fb, 1, 0, cnt, c.st);
     unsigned long long h = 0;
     SMJ_CHECK(hipMemcpyAsync(&h, cnt, 8, hipMemcpyDeviceToHost, c.st));
@@ -769,7 +776,7 @@ void smj_dev_partition_range(smj_workspace* wsp, const tuple_t* in, uint64_t n,
     Workspace* ws = (Workspace*)wsp;
     hipStream_t st = (hipStream_t)stream;
     RangePlan* plan = (RangePlan*)ws->scratch("range_plan", sizeof(RangePlan));
-    RangePlan h = make_plan(key_min, key_max, nbits, 0, 0);
+    RangePlan h = make_plan(key_min, key_max, nbits, 0, 0, 0);
     hipLaunchKernelGGL(k_setplan, dim3(1), dim3(1), 0, st, plan, h);
     uint64_t* starts = (uint64_t*)ws->scratch("range_starts", (1u << nbits) * 8);
     plan_partition(ws, (const Tup*)in, n, (Tup*)out, plan, nbits, starts,

@@ -32,8 +32,9 @@ namespace smj {
 // ---------------------------------------------------------------------------
 template <int THREADS, int ITEMS, class Digit>
 __global__ void __launch_bounds__(THREADS)
-k_hist(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig,
+k_hist(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_arg,
        uint32_t nbins, uint32_t* __restrict__ counts, uint32_t nwg) {
+    const auto dig = dig_arg.load();
     constexpr int TILE = THREADS * ITEMS;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_hist[];
     for (uint32_t d = threadIdx.x; d < nbins; d += THREADS) lds_hist[d] = 0;
@@ -136,10 +137,11 @@ constexpr size_t scatter_lds(uint32_t nbins) {
 
 template <int THREADS, int ITEMS, class Digit>
 __global__ void __launch_bounds__(THREADS)
-k_scatter(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig,
+k_scatter(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_arg,
           uint32_t nbins, uint32_t dbits, const uint32_t* __restrict__ counts,
           uint32_t nwg, const uint64_t* __restrict__ starts,
           Tup* __restrict__ out, int mode) {
+    const auto dig = dig_arg.load();
     constexpr int TILE = THREADS * ITEMS;
     constexpr int WAVES = THREADS / 64;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
@@ -270,9 +272,10 @@ constexpr size_t scatter_u_lds(uint32_t nbins) {
 
 template <int THREADS, int ITEMS, class Digit>
 __global__ void __launch_bounds__(THREADS)
-k_scatter_u(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig,
+k_scatter_u(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_arg,
             uint32_t nbins, const uint32_t* __restrict__ counts, uint32_t nwg,
-            const uint64_t* __restrict__ starts, Tup* __restrict__ out) {
+            const uint64_t* __restrict__ starts, Tup* __restrict__ out, int mode) {
+    const auto dig = dig_arg.load();
     constexpr int TILE = THREADS * ITEMS;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     Tup* stage = reinterpret_cast<Tup*>(lds_raw);
@@ -340,7 +343,9 @@ k_scatter_u(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig,
         for (uint32_t i = threadIdx.x; i < tcount; i += THREADS) {
             const Tup t = stage[i];
             const uint32_t d = dig(t);
-            out[run[d] + (i - tstart[d])] = t;
+            if (mode == 0) out[run[d] + (i - tstart[d])] = t;
+            else if (mode == 1) out[base + i] = t;  // ablation: linear write
+            else if (tup_key(t) == -12345) out[0] = t;  // ablation: no write
         }
         __syncthreads();
         for (uint32_t k = 0; k < dper; k++) {
@@ -356,13 +361,168 @@ k_scatter_u(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig,
     }
 }
 
+// Write-combining scatter for the join's level-1 partition (order inside a
+// partition is free).  The reference flushes 64-byte software write-combining
+// buffers per partition (src/partition/partition.c:38-46, 191-206); here each
+// workgroup keeps, per partition, the tail of its output that does not yet
+// fill a 64-byte segment in an LDS carry buffer and prepends it to the next
+// tile's run, so apart from the first and last segment of a workgroup's
+// region every store completes a whole aligned segment.  Ranks come from LDS
+// atomics; the next tile is loaded while the current one is ranked, staged
+// and written.
+// LDS: stage TILE | carry nbins*SEG Tups | pos nbins u64 | tstart, tfill, kc
+//      nbins u32 each | scan scratch
+template <int THREADS, int ITEMS>
+constexpr size_t scatter_wc_lds(uint32_t nbins) {
+    return (size_t)THREADS * ITEMS * sizeof(Tup) + (size_t)nbins * 64 +
+           (size_t)nbins * (8 + 4 + 4 + 4) + 64;
+}
+
+template <int THREADS, int ITEMS, class Digit>
+__global__ void __launch_bounds__(THREADS)
+k_scatter_wc(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_arg,
+             uint32_t nbins, const uint32_t* __restrict__ counts, uint32_t nwg,
+             const uint64_t* __restrict__ starts, Tup* __restrict__ out) {
+    const auto dig = dig_arg.load();
+    constexpr int TILE = THREADS * ITEMS;
+    constexpr uint32_t SEG = 64 / sizeof(Tup);  // tuples per 64-byte segment
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    Tup* stage = reinterpret_cast<Tup*>(lds_raw);
+    Tup* carry = stage + TILE;
+    uint64_t* pos = reinterpret_cast<uint64_t*>(carry + (size_t)nbins * SEG);
+    uint32_t* tstart = reinterpret_cast<uint32_t*>(pos + nbins);
+    uint32_t* tfill = tstart + nbins;
+    uint32_t* kc = tfill + nbins;
+    uint32_t* scr = kc + nbins;
+
+    for (uint32_t d = threadIdx.x; d < nbins; d += THREADS) {
+        pos[d] = starts[d] + counts[(uint64_t)d * nwg + blockIdx.x];
+        tfill[d] = 0;
+        kc[d] = 0;
+    }
+    const uint64_t beg = (uint64_t)blockIdx.x * chunk;
+    uint64_t end = beg + chunk;
+    if (end > n) end = n;
+    const uint32_t dper = (nbins + THREADS - 1) / THREADS;
+    const uint32_t d0 = threadIdx.x * dper;
+
+    Tup v[ITEMS], nv[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; j++) {
+        const uint64_t i = beg + (uint64_t)j * THREADS + threadIdx.x;
+        if (i < end) v[j] = in[i];
+    }
+    __syncthreads();
+    for (uint64_t base = beg; base < end; base += TILE) {
+        const uint32_t tcount =
+            (uint32_t)((end - base) < (uint64_t)TILE ? (end - base) : TILE);
+        // prefetch the next tile
+        const uint64_t nb = base + TILE;
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint64_t i = nb + (uint64_t)j * THREADS + threadIdx.x;
+            if (i < end) nv[j] = in[i];
+        }
+        // ---- rank: tile counts per partition
+        uint32_t dg[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint32_t li = j * THREADS + threadIdx.x;
+            dg[j] = li < tcount ? dig(v[j]) : 0xffffffffu;
+            if (dg[j] != 0xffffffffu) atomicAdd(&tfill[dg[j]], 1u);
+        }
+        __syncthreads();
+        uint32_t loc = 0;
+        for (uint32_t k = 0; k < dper; k++)
+            if (d0 + k < nbins) loc += tfill[d0 + k];
+        uint32_t tot;
+        uint32_t ex = block_exclusive_scan(loc, scr, &tot);
+        for (uint32_t k = 0; k < dper; k++) {
+            const uint32_t d = d0 + k;
+            if (d < nbins) {
+                const uint32_t c = tfill[d];
+                tstart[d] = ex;
+                tfill[d] = ex;
+                ex += c;
+            }
+        }
+        __syncthreads();
+        // ---- stage the tile grouped by partition
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++)
+            if (dg[j] != 0xffffffffu) stage[atomicAdd(&tfill[dg[j]], 1u)] = v[j];
+        __syncthreads();
+        // ---- per partition: emit E of the T = carry + tile elements so that
+        // the region cursor lands on a segment boundary (tfill := E)
+        for (uint32_t k = 0; k < dper; k++) {
+            const uint32_t d = d0 + k;
+            if (d < nbins) {
+                const uint32_t T = kc[d] + (tfill[d] - tstart[d]);
+                const uint32_t m = (uint32_t)((pos[d] + T) % SEG);
+                tfill[d] = m <= T ? T - m : 0u;
+            }
+        }
+        __syncthreads();
+        // ---- emit: old carry first (a carry never moves: it is either
+        // emitted whole or kept when nothing is emitted), then the tile
+        for (uint32_t q = threadIdx.x; q < nbins * SEG; q += THREADS) {
+            const uint32_t d = q / SEG, j = q % SEG;
+            if (j < kc[d] && j < tfill[d]) out[pos[d] + j] = carry[q];
+        }
+        Tup keep[ITEMS];
+        uint32_t kslot[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint32_t i = j * THREADS + threadIdx.x;
+            kslot[j] = 0xffffffffu;
+            if (i < tcount) {
+                const Tup t = stage[i];
+                const uint32_t d = dig(t);
+                const uint32_t vv = kc[d] + (i - tstart[d]);
+                const uint32_t E = tfill[d];
+                if (vv < E) {
+                    out[pos[d] + vv] = t;
+                } else {
+                    keep[j] = t;
+                    kslot[j] = d * SEG + (vv - E);
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++)
+            if (kslot[j] != 0xffffffffu) carry[kslot[j]] = keep[j];
+        __syncthreads();
+        for (uint32_t k = 0; k < dper; k++) {
+            const uint32_t d = d0 + k;
+            if (d < nbins) {
+                const uint32_t cnt = ((d + 1 < nbins) ? tstart[d + 1] : tcount) - tstart[d];
+                const uint32_t E = tfill[d];
+                const uint32_t T = kc[d] + cnt;
+                pos[d] += E;
+                kc[d] = T - E;
+                tfill[d] = 0;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) v[j] = nv[j];
+        __syncthreads();
+    }
+    // ---- flush the carries (partial last segments of this region)
+    for (uint32_t q = threadIdx.x; q < nbins * SEG; q += THREADS) {
+        const uint32_t d = q / SEG, j = q % SEG;
+        if (j < kc[d]) out[pos[d] + j] = carry[q];
+    }
+}
+
 // pad copy for wide digits: item at unpadded position i of digit d moves to
 // padded_start[d] + (i - unpadded_start[d])
 template <class Digit>
-__global__ void k_padcopy(const Tup* __restrict__ in, uint64_t n, Digit dig,
+__global__ void k_padcopy(const Tup* __restrict__ in, uint64_t n, Digit dig_arg,
                           const uint64_t* __restrict__ ustart,
                           const uint64_t* __restrict__ pstart,
                           Tup* __restrict__ out) {
+    const auto dig = dig_arg.load();
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (; i < n; i += stride) {
@@ -374,8 +534,9 @@ __global__ void k_padcopy(const Tup* __restrict__ in, uint64_t n, Digit dig,
 
 // global-atomic histogram (wide digits only: test-sized inputs)
 template <class Digit>
-__global__ void k_hist_global(const Tup* __restrict__ in, uint64_t n, Digit dig,
+__global__ void k_hist_global(const Tup* __restrict__ in, uint64_t n, Digit dig_arg,
                               unsigned long long* __restrict__ hist) {
+    const auto dig = dig_arg.load();
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (; i < n; i += stride) atomicAdd(&hist[dig(in[i])], 1ull);
@@ -387,6 +548,7 @@ __global__ void k_hist_global(const Tup* __restrict__ in, uint64_t n, Digit dig,
 struct LowBits {
     Digit32 inner;
     uint32_t lowbits;
+    __device__ __forceinline__ LowBits load() const { return *this; }
     __device__ __forceinline__ uint32_t operator()(const Tup& t) const {
         return inner(t) & ((1u << lowbits) - 1u);
     }
@@ -394,6 +556,7 @@ struct LowBits {
 struct HighBits {
     Digit32 inner;
     uint32_t lowbits;
+    __device__ __forceinline__ HighBits load() const { return *this; }
     __device__ __forceinline__ uint32_t operator()(const Tup& t) const {
         return inner(t) >> lowbits;
     }
@@ -470,7 +633,7 @@ static void stable_partition_t(Workspace* ws, const Tup* in, uint64_t n,
         TraceScope ts(ws, "k_scatter", st);
         hipLaunchKernelGGL((k_scatter_u<THREADS, ITEMS, Digit>), dim3(nwg),
                            dim3(THREADS), ldsu, st, in, n, chunk, dig, nbins,
-                           counts, nwg, starts_dev, out);
+                           counts, nwg, starts_dev, out, scatter_mode());
         SMJ_CHECK(hipGetLastError());
         return;
     }
@@ -578,12 +741,69 @@ void stable_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
 }
 
 // level-1 partition of the join/sort: range-plan digit, unpadded; the order
-// inside a partition is free (every bucket is fully sorted afterwards)
+// inside a partition is free (every bucket is fully sorted afterwards).
+// Histogram + write-combining scatter, one workgroup per CU and a long chunk
+// per workgroup (the carries pay off over many tiles).
+// measured: write combining pays for 16-byte tuples (4-tuple segments), not
+// for 8-byte ones; SMJ_SCATTER_WC overrides
+static int wc_enabled() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("SMJ_SCATTER_WC");
+        v = e ? atoi(e) : (sizeof(Tup) == 16 ? 1 : 0);
+    }
+    return v;
+}
+
 void plan_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
                     const RangePlan* plan_dev, uint32_t dbits,
                     uint64_t* starts_dev, int64_t* hist_out, hipStream_t st) {
     PlanDigit1 dig{plan_dev};
-    unstable_partition(ws, in, n, out, dig, dbits, starts_dev, hist_out, st);
+    const uint32_t nbins = 1u << dbits;
+    constexpr int THREADS = 512;
+    constexpr int ITEMS = sizeof(Tup) == 16 ? 8 : 16;
+    constexpr int TILE = THREADS * ITEMS;
+    const size_t lds = scatter_wc_lds<THREADS, ITEMS>(nbins);
+    if (!wc_enabled() || dbits > 10 || lds > 160 * 1024 || scatter_mode() != 0) {
+        unstable_partition(ws, in, n, out, dig, dbits, starts_dev, hist_out, st);
+        return;
+    }
+    uint64_t ntiles = (n + TILE - 1) / TILE;
+    if (ntiles == 0) ntiles = 1;
+    const uint32_t maxwg = 256;  // one per CU
+    uint32_t nwg = (uint32_t)(ntiles < maxwg ? ntiles : maxwg);
+    const uint64_t tiles_per_wg = (ntiles + nwg - 1) / nwg;
+    const uint64_t chunk = tiles_per_wg * TILE;
+    nwg = (uint32_t)((ntiles + tiles_per_wg - 1) / tiles_per_wg);
+    uint32_t* counts = (uint32_t*)ws->scratch("pt_counts", (size_t)nbins * nwg * 4);
+    uint64_t* totals = (uint64_t*)ws->scratch("pt_totals", (size_t)nbins * 8);
+    {
+        // one workgroup per scatter chunk: 16 waves keep enough loads in flight
+        TraceScope ts(ws, "k_hist", st);
+        hipLaunchKernelGGL((k_hist<1024, 8, PlanDigit1>), dim3(nwg), dim3(1024),
+                           nbins * sizeof(uint32_t), st, in, n, chunk, dig, nbins,
+                           counts, nwg);
+    }
+    {
+        TraceScope ts(ws, "k_scan", st);
+        hipLaunchKernelGGL(k_scanrow, dim3(nbins), dim3(256), 0, st, counts, nwg,
+                           totals);
+        hipLaunchKernelGGL(k_scandig, dim3(1), dim3(256), 0, st, totals, nbins, 0,
+                           starts_dev, hist_out, (int64_t*)nullptr);
+    }
+    if (n == 0) return;
+    static bool attr = false;
+    if (!attr) {
+        SMJ_CHECK(hipFuncSetAttribute(
+            (const void*)k_scatter_wc<THREADS, ITEMS, PlanDigit1>,
+            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr = true;
+    }
+    TraceScope ts(ws, "k_scatter", st);
+    hipLaunchKernelGGL((k_scatter_wc<THREADS, ITEMS, PlanDigit1>), dim3(nwg),
+                       dim3(THREADS), lds, st, in, n, chunk, dig, nbins, counts,
+                       nwg, starts_dev, out);
+    SMJ_CHECK(hipGetLastError());
 }
 
 // histogram-only pass + plain copy (histogram_memcpy_bench)

@@ -87,6 +87,7 @@ __host__ __device__ __forceinline__ uint64_t key_u(int64_t k) {
 struct RefDigit {
     uint32_t mask;
     uint32_t shift;
+    __host__ __device__ __forceinline__ RefDigit load() const { return *this; }
     __device__ __forceinline__ uint32_t operator()(const Tup& t) const {
         uint64_t km1 = (uint64_t)(tup_key(t) - 1);
         return (uint32_t)((km1 & (uint64_t)mask) >> shift);
@@ -147,10 +148,12 @@ __host__ __device__ __forceinline__ uint32_t plan_d3(const RangePlan& p,
     return (uint32_t)(v > lim ? lim : v);
 }
 
-// Host helper: build a plan for key range [kmin, kmax] and level widths.
+// Build a plan for key range [kmin, kmax]: D1 level-1 bits, D2 level-2 bits
+// preferred by size, widened up to D2cap when that makes the last digit exact
+// (s3 == 0 with D3 <= D3max).
 __host__ __device__ inline RangePlan make_plan(int64_t kmin, int64_t kmax,
                                                uint32_t D1, uint32_t D2,
-                                               uint32_t D3max) {
+                                               uint32_t D2cap, uint32_t D3max) {
     RangePlan p;
     p.base = kmin;
     uint64_t width = (kmax >= kmin) ? (key_u(kmax) - key_u(kmin)) : 0;
@@ -160,10 +163,16 @@ __host__ __device__ inline RangePlan make_plan(int64_t kmin, int64_t kmax,
     p.D1 = D1;
     p.s1 = L > D1 ? L - D1 : 0;
     p.D2 = D2 < p.s1 ? D2 : p.s1;  // never more level-2 bits than remain
-    p.s2 = p.s1 - p.D2;
-    uint32_t d3 = p.s2 < D3max ? p.s2 : D3max;
-    p.D3 = d3;
-    p.s3 = p.s2 - d3;
+    uint32_t s2 = p.s1 - p.D2;
+    if (s2 > D3max && p.D2 < D2cap) {
+        uint32_t extra = s2 - D3max;
+        if (extra > D2cap - p.D2) extra = D2cap - p.D2;
+        p.D2 += extra;
+        s2 -= extra;
+    }
+    p.s2 = s2;
+    p.D3 = s2 < D3max ? s2 : D3max;
+    p.s3 = s2 - p.D3;
     return p;
 }
 

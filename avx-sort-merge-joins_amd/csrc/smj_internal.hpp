@@ -14,12 +14,40 @@ constexpr uint32_t kNarrowDigitBits = 12;  // widest digit of a single pass
 // reference partition digit (runtime mask/shift), see smj_common.hpp
 typedef RefDigit Digit32;
 
-// level-1 digit of a device-resident range plan
+// wave-uniform 32/64-bit values into SGPRs
+__device__ __forceinline__ uint32_t uniform32(uint32_t x) {
+    return __builtin_amdgcn_readfirstlane(x);
+}
+__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
+    return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
+           __builtin_amdgcn_readfirstlane((uint32_t)x);
+}
+
+// level-1 digit of a range plan held by value (in SGPRs)
+struct PlanDigitV {
+    RangePlan p;
+    __device__ __forceinline__ uint32_t operator()(const Tup& t) const {
+        return plan_d1(p, plan_rel(p, tup_key(t)));
+    }
+};
+
+// level-1 digit of a device-resident range plan.  Kernels call load() once:
+// the plan is read a single time instead of at every digit (the output
+// stores may alias it, so the compiler would reload it).
 struct PlanDigit1 {
     const RangePlan* plan;
-    __device__ __forceinline__ uint32_t operator()(const Tup& t) const {
-        const RangePlan& p = *plan;
-        return plan_d1(p, plan_rel(p, tup_key(t)));
+    __device__ __forceinline__ PlanDigitV load() const {
+        RangePlan q = *plan;
+        PlanDigitV v;
+        v.p.base = (int64_t)uniform64((uint64_t)q.base);
+        v.p.span = uniform64(q.span);
+        v.p.D1 = uniform32(q.D1);
+        v.p.D2 = uniform32(q.D2);
+        v.p.D3 = uniform32(q.D3);
+        v.p.s1 = uniform32(q.s1);
+        v.p.s2 = uniform32(q.s2);
+        v.p.s3 = uniform32(q.s3);
+        return v;
     }
 };
 
@@ -121,6 +149,8 @@ void hist_memcpy(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
                  uint32_t dbits, hipStream_t st);
 
 // ---- bucketsort.hip : MSD bucket sort (+ fused merge-join count)
+extern const uint32_t kGroupTarget;  // expected tuples per group of the plan
+extern const uint32_t kTileTuples;   // tile of the tile pass
 struct BucketSortArgs {
     // level-1 partitioned relation(s): bucket b occupies
     // [bstart[b], bstart[b] + bcount[b]) of `part`.
@@ -138,16 +168,18 @@ struct BucketSortArgs {
     hipEvent_t ev_bucket = nullptr;
     hipEvent_t ev_ovf = nullptr;
 };
-// Runs the tile pass and the bucket pass; handles overflowing sub-buckets
-// (skew) with the merge-sort fallback.  May synchronise `st` once.
-void bucket_sort(Workspace* ws, const BucketSortArgs& a, uint32_t D2,
-                 hipStream_t st);
+// Runs the tile pass and the group pass; handles overflowing groups (skew)
+// with the merge-sort fallback.  Synchronises `st` twice: once for the bucket
+// counts (launch sizes) and once for the overflow count.
+void bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st);
 
 // plan selection from a device sample (writes plan_dev)
+// (D2 is the size-preferred level-2 width, D2cap the widest the plan may use
+// to make the last digit exact)
 void plan_from_sample(Workspace* ws, const Tup* const* rels,
                       const uint64_t* ns, int nrel, uint32_t D1, uint32_t D2,
-                      int64_t hint_min, int64_t hint_max, RangePlan* plan_dev,
-                      hipStream_t st);
+                      uint32_t D2cap, int64_t hint_min, int64_t hint_max,
+                      RangePlan* plan_dev, hipStream_t st);
 
 // ---- mergesort.hip : general segmented merge sort + merge path kernels
 void segmented_sort(Workspace* ws, Tup* data, const uint64_t* seg_off_host,

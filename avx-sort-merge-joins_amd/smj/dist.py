@@ -55,7 +55,7 @@ class DeviceOps:
     def join(self, R, S, sR, sS, count):
         # the local key range is a 1/world slice of the global one: let the
         # library sample it (key_max = 0) rather than plan for the global span
-        self.lib.dev_join(R, S, sR, sS, count, 10, 1, 0)
+        self.lib.dev_join(R, S, sR, sS, count, 9, 1, 0)
 
 
 class DistributedJoin:

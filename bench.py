@@ -40,7 +40,7 @@ def parse():
     p.add_argument("--width", type=int, default=16, choices=(8, 16))
     p.add_argument("--dist", default="uniform", choices=("uniform", "zipf"))
     p.add_argument("--theta", type=float, default=0.75)
-    p.add_argument("--fanout-bits", type=int, default=10)
+    p.add_argument("--fanout-bits", type=int, default=9)
     p.add_argument("--cpu-n", type=int, default=64_000_000,
                    help="tuples per relation of the bounded CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -57,7 +57,7 @@ def alg_bytes_per_launch(name, n_rel, nR, nS, w):
         "k_hist": n_rel * w,
         "k_scatter": 2 * n_rel * w,
         "k_tilepass": 2 * n_rel * w,
-        "k_subwave": 2 * (nR + nS) * w,
+        "k_groupsort": 2 * (nR + nS) * w,
     }.get(name)
 
 

@@ -20,10 +20,10 @@ import smj  # noqa: E402
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("what", choices=["partition", "sort", "join", "merge"])
+    p.add_argument("what", choices=["partition", "sort", "join", "merge", "copy"])
     p.add_argument("--n", type=int, default=1 << 27)
     p.add_argument("--width", type=int, default=16)
-    p.add_argument("--bits", type=int, default=10)
+    p.add_argument("--bits", type=int, default=9)
     p.add_argument("--shift", type=int, default=0)
     p.add_argument("--reps", type=int, default=5)
     p.add_argument("--dist", default="uniform")
@@ -34,7 +34,12 @@ def main():
     lib.dev_gen_pk(R, 0, n, 12345, with_payload=a.what != "sort")
     res = {"what": a.what, "n": n, "width": a.width,
            "variant": os.environ.get("SMJ_PT_VARIANT", "default")}
-    if a.what == "partition":
+    if a.what == "copy":
+        # achievable-bandwidth reference: device-to-device copy of one relation
+        out = lib.empty(n)
+        f = lambda: out.copy_(R)
+        alg = 2 * n * a.width
+    elif a.what == "partition":
         out = lib.empty(n + (1 << a.bits) * 64 // a.width)
         h = torch.zeros(1 << a.bits, dtype=torch.int64, device="cuda")
         o = torch.zeros_like(h)
@@ -60,7 +65,7 @@ def main():
             lib.dev_gen_zipf(S, 0, n, 0.75, 54321)
         sR, sS = lib.empty(n), lib.empty(n)
         cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
-        f = lambda: lib.dev_join(R, S, sR, sS, cnt, 10, 1, n)
+        f = lambda: lib.dev_join(R, S, sR, sS, cnt, a.bits, 1, n)
         alg = 5 * 2 * n * a.width
     f()
     torch.cuda.synchronize()
