@@ -82,19 +82,27 @@ struct OvfEntry {
 };
 
 // ---------------------------------------------------------------------------
-// tile table: block b writes the tiles of bucket b (consecutive TILE2 chunks),
-// numbered from btile0[b] (uploaded by the host).
+// tile table: block b writes the tiles of bucket b, numbered from btile0[b]
+// (uploaded by the host): consecutive TILE2 chunks of each of its segments
+// (one segment = the whole bucket, or kShards of a sampled partition).
 __global__ void __launch_bounds__(64)
 k_tiles(const uint64_t* __restrict__ bstart, const int64_t* __restrict__ bcount,
-        TileTable tt) {
+        const uint64_t* __restrict__ seg_start, const int64_t* __restrict__ seg_cnt,
+        uint32_t nseg, TileTable tt) {
     const uint32_t b = blockIdx.x;
-    const uint32_t t0 = tt.btile0[b], nt = tt.btile0[b + 1] - t0;
-    for (uint32_t i = threadIdx.x; i < nt; i += 64) {
-        const uint64_t o = (uint64_t)i * TILE2;
-        const int64_t rem = bcount[b] - (int64_t)o;
-        tt.off[t0 + i] = bstart[b] + o;
-        tt.len[t0 + i] = (uint32_t)(rem < TILE2 ? rem : TILE2);
-        tt.bucket[t0 + i] = b;
+    uint32_t t0 = tt.btile0[b];
+    for (uint32_t q = 0; q < nseg; q++) {
+        const uint64_t s0 = seg_start ? seg_start[(size_t)b * nseg + q] : bstart[b];
+        const int64_t cnt = seg_cnt ? seg_cnt[(size_t)b * nseg + q] : bcount[b];
+        const uint32_t nt = (uint32_t)((cnt + TILE2 - 1) / TILE2);
+        for (uint32_t i = threadIdx.x; i < nt; i += 64) {
+            const uint64_t o = (uint64_t)i * TILE2;
+            const int64_t rem = cnt - (int64_t)o;
+            tt.off[t0 + i] = s0 + o;
+            tt.len[t0 + i] = (uint32_t)(rem < TILE2 ? rem : TILE2);
+            tt.bucket[t0 + i] = b;
+        }
+        t0 += nt;
     }
 }
 
@@ -191,7 +199,8 @@ k_tilepass(TilePassArgs A) {
 struct GroupArgs {
     const Tup* tmp[2];
     Tup* out[2];
-    const uint64_t* bstart[2];
+    const uint64_t* bstart[2];  // bucket start in the partition / tmp buffer
+    const uint64_t* ostart[2];  // bucket start in the (dense) output
     TileTable tt[2];
     int nrel;
     RangePlan plan;  // by value: kernel arguments live in SGPRs
@@ -235,8 +244,10 @@ struct GroupLDS {
 struct GroupMeta {
     uint32_t b, g;
     uint32_t t0[2], nt[2];  // first tile and tile count of the bucket
-    uint64_t bst[2];        // bucket start
+    uint64_t bst[2];        // bucket start (partition buffer)
+    uint64_t ost[2];        // bucket start (output)
     uint32_t lo[2], len[2];  // tiles lane and lane + 64
+    uint32_t toff[2];        // their offsets from the bucket start
 };
 
 __device__ __forceinline__ void load_meta(const GroupArgs& A, uint32_t gi,
@@ -247,7 +258,7 @@ __device__ __forceinline__ void load_meta(const GroupArgs& A, uint32_t gi,
 #pragma unroll
         for (int r = 0; r < 2; r++) {
             M.t0[r] = M.nt[r] = 0;
-            M.bst[r] = 0;
+            M.bst[r] = M.ost[r] = 0;
             if (r < A.nrel) {
                 // uniform: keep them in SGPRs
                 M.t0[r] = __builtin_amdgcn_readfirstlane(A.tt[r].btile0[b]);
@@ -255,12 +266,16 @@ __device__ __forceinline__ void load_meta(const GroupArgs& A, uint32_t gi,
                 const uint64_t bs = A.bstart[r][b];
                 M.bst[r] = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(bs >> 32)) << 32) |
                            __builtin_amdgcn_readfirstlane((uint32_t)bs);
+                const uint64_t os = A.ostart[r][b];
+                M.ost[r] = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(os >> 32)) << 32) |
+                           __builtin_amdgcn_readfirstlane((uint32_t)os);
             }
         }
     }
     M.b = b;
     const uint32_t wid = otid() >> 6, lane = otid() & 63;
     M.lo[0] = M.len[0] = M.lo[1] = M.len[1] = 0;
+    M.toff[0] = M.toff[1] = 0;
     if (wid < (uint32_t)A.nrel) {
         const uint32_t nt = wid ? M.nt[1] : M.nt[0];
         const uint32_t t0 = wid ? M.t0[1] : M.t0[0];
@@ -272,6 +287,7 @@ __device__ __forceinline__ void load_meta(const GroupArgs& A, uint32_t gi,
                     A.tt[wid].pref + (uint64_t)(t0 + t) * (A.nb2 + 1) + M.g;
                 M.lo[h] = pf[0];
                 M.len[h] = (uint32_t)(pf[1] - pf[0]);
+                M.toff[h] = (uint32_t)(A.tt[wid].off[t0 + t] - (wid ? M.bst[1] : M.bst[0]));
             }
         }
     }
@@ -359,11 +375,11 @@ __device__ __forceinline__ void build_tables(const GroupArgs& A, GroupLDS& L,
         const uint32_t sA = (uint32_t)(i0 - p0), sB = (uint32_t)(i1 - p1);
         if (lane < nt) {
             L.runoff[r][lane] = sA;
-            L.runsrc[r][lane] = lane * (uint32_t)TILE2 + M.lo[0];
+            L.runsrc[r][lane] = M.toff[0] + M.lo[0];
         }
         if (lane + 64 < nt) {
             L.runoff[r][lane + 64] = sB;
-            L.runsrc[r][lane + 64] = (lane + 64) * (uint32_t)TILE2 + M.lo[1];
+            L.runsrc[r][lane + 64] = M.toff[1] + M.lo[1];
         }
         if (lane == 0) {
             L.runoff[r][nt <= GS_TMAX ? nt : 0] = (uint32_t)tot;
@@ -371,11 +387,13 @@ __device__ __forceinline__ void build_tables(const GroupArgs& A, GroupLDS& L,
             L.off[r] = (uint32_t)(tot >> 32);
         }
         wave_lds_sync();
-        if (lane < nt && M.len[0] > 0) {
+        // run starts at or past GS_CAP only occur in groups that overflow
+        // (they never reach the gather): keep them out of the LDS tables
+        if (lane < nt && M.len[0] > 0 && sA < GS_CAP) {
             atomicOr(&L.smap[r][sA >> 6], 1ull << (sA & 63));
             L.stile[r][sA] = (uint8_t)lane;
         }
-        if (lane + 64 < nt && M.len[1] > 0) {
+        if (lane + 64 < nt && M.len[1] > 0 && sB < GS_CAP) {
             atomicOr(&L.smap[r][sB >> 6], 1ull << (sB & 63));
             L.stile[r][sB] = (uint8_t)(lane + 64);
         }
@@ -414,13 +432,13 @@ __device__ __forceinline__ void group_overflow(const GroupArgs& A, GroupLDS& L,
         (void)block_scan64(acc, L.scan64, &tot);
         nn[r] = (uint32_t)tot;
         oo[r] = tot >> 32;
-        Tup* dst = A.out[r] + M.bst[r] + oo[r];
+        Tup* dst = A.out[r] + M.ost[r] + oo[r];
         const Tup* tp = A.tmp[r] + M.bst[r];
         uint32_t pos = 0;
         for (uint32_t t = 0; t < nt; t++) {
             const uint16_t* pf = pref + (uint64_t)(t0 + t) * (A.nb2 + 1) + M.g;
             const uint32_t lo = pf[0], len = (uint32_t)(pf[1] - pf[0]);
-            const Tup* src = tp + (uint64_t)t * TILE2 + lo;
+            const Tup* src = A.tmp[r] + A.tt[r].off[t0 + t] + lo;
             for (uint32_t i = otid(); i < len; i += GS_THREADS) dst[pos + i] = src[i];
             pos += len;
         }
@@ -558,7 +576,7 @@ __device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS& L,
         if (tid == 0) L.nlong = 0;
     }
     // ---- write the sorted group: one contiguous stream
-    Tup* dst = A.out[r] + C.bst[r] + L.off[r];
+    Tup* dst = A.out[r] + C.ost[r] + L.off[r];
 #pragma unroll
     for (int k = 0; k < GS_ITEMS; k++) {
         const uint32_t j = k * GS_THREADS + tid;
@@ -635,7 +653,7 @@ k_groupsort(GroupArgs A) {
             } else {
                 // S is still in B; R's sorted group is in out (written above
                 // by this workgroup: visible after the barrier)
-                const Tup* Rs = A.out[0] + C.bst[0] + L.off[0];
+                const Tup* Rs = A.out[0] + C.ost[0] + L.off[0];
                 const uint32_t nR = n0, nS = n1;
                 for (uint32_t i = tid; i < nS; i += GS_THREADS) {
                     const int64_t k = tup_key(L.B[i]);
@@ -753,7 +771,7 @@ static uint64_t ring_tuples() {
     return (uint64_t)mb * (1ull << 20) / sizeof(Tup);
 }
 
-void bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
+bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
     const uint32_t nb = a.nbuckets;
     const int nrel = a.nrel;
     static bool attr = false;
@@ -773,15 +791,26 @@ void bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
     uint64_t* hcnt = (uint64_t*)ws->host_pinned("bs_hcnt", (size_t)2 * nb * 8);
     uint64_t* hst = (uint64_t*)ws->host_pinned("bs_hst", (size_t)2 * nb * 8);
     RangePlan* hplan = (RangePlan*)ws->host_pinned("bs_hplan", sizeof(RangePlan));
+    const bool segs = a.seg_start[0] != nullptr;
+    const uint32_t nseg = segs ? kShards : 1;
+    int64_t* hseg = (int64_t*)ws->host_pinned("bs_hseg", (size_t)2 * nb * kShards * 8);
     for (int r = 0; r < nrel; r++) {
         SMJ_CHECK(hipMemcpyAsync(hcnt + r * nb, a.bcount[r], nb * 8,
                                  hipMemcpyDeviceToHost, st));
         SMJ_CHECK(hipMemcpyAsync(hst + r * nb, a.bstart[r], nb * 8,
                                  hipMemcpyDeviceToHost, st));
+        if (segs)
+            SMJ_CHECK(hipMemcpyAsync(hseg + (size_t)r * nb * kShards, a.seg_cnt[r],
+                                     (size_t)nb * kShards * 8, hipMemcpyDeviceToHost, st));
     }
     SMJ_CHECK(hipMemcpyAsync(hplan, a.plan_dev, sizeof(RangePlan),
                              hipMemcpyDeviceToHost, st));
+    unsigned int* hflag = (unsigned int*)ws->host_pinned("bs_hflag", 4);
+    *hflag = 0;
+    if (a.part_flag)
+        SMJ_CHECK(hipMemcpyAsync(hflag, a.part_flag, 4, hipMemcpyDeviceToHost, st));
     SMJ_CHECK(hipStreamSynchronize(st));
+    if (*hflag) return false;
     const uint32_t nb2 = 1u << hplan->D2;  // groups per bucket
 
     TileTable tt[2];
@@ -789,13 +818,24 @@ void bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
         {"bs_off0", "bs_len0", "bs_bkt0", "bs_bt00", "bs_pref0"},
         {"bs_off1", "bs_len1", "bs_bkt1", "bs_bt01", "bs_pref1"}};
     uint32_t* hbt = (uint32_t*)ws->host_pinned("bs_hbt", (size_t)2 * (nb + 1) * 4);
+    // dense output start of every bucket (partition regions may have slack)
+    uint64_t* hdst = (uint64_t*)ws->host_pinned("bs_hdst", (size_t)2 * nb * 8);
+    uint64_t* ostart[2] = {nullptr, nullptr};
     uint64_t maxb[2] = {0, 0};
     for (int r = 0; r < nrel; r++) {
         uint32_t* bt0 = hbt + r * (nb + 1);
         uint32_t acc = 0;
+        uint64_t dacc = 0;
         for (uint32_t b = 0; b < nb; b++) {
+            hdst[r * nb + b] = dacc;
+            dacc += hcnt[r * nb + b];
             bt0[b] = acc;
-            acc += (uint32_t)((hcnt[r * nb + b] + TILE2 - 1) / TILE2);
+            if (segs) {
+                for (uint32_t q = 0; q < kShards; q++)
+                    acc += (uint32_t)((hseg[((size_t)r * nb + b) * kShards + q] + TILE2 - 1) / TILE2);
+            } else {
+                acc += (uint32_t)((hcnt[r * nb + b] + TILE2 - 1) / TILE2);
+            }
             maxb[r] = std::max<uint64_t>(maxb[r], hcnt[r * nb + b]);
         }
         bt0[nb] = acc;
@@ -807,18 +847,22 @@ void bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
         tt[r].pref = (uint16_t*)ws->scratch(names[r][4], ntl * (nb2 + 1) * 2);
         SMJ_CHECK(hipMemcpyAsync(tt[r].btile0, bt0, (nb + 1) * 4,
                                  hipMemcpyHostToDevice, st));
+        ostart[r] = (uint64_t*)ws->scratch(r ? "bs_ost1" : "bs_ost0", (size_t)nb * 8);
+        SMJ_CHECK(hipMemcpyAsync(ostart[r], hdst + r * nb, (size_t)nb * 8,
+                                 hipMemcpyHostToDevice, st));
         hipLaunchKernelGGL(k_tiles, dim3(nb), dim3(64), 0, st, a.bstart[r],
-                           a.bcount[r], tt[r]);
+                           a.bcount[r], a.seg_start[r], a.seg_cnt[r], nseg, tt[r]);
     }
     if (nrel == 1) tt[1] = tt[0];
     if (a.ev_tile) SMJ_CHECK(hipEventRecord(a.ev_tile, st));
 
-    const uint64_t ring = ring_tuples();
+    // (the ring needs buckets contiguous in the partition buffer)
+    const uint64_t ring = segs ? 0 : ring_tuples();
     Tup* ringbuf[2] = {nullptr, nullptr};
     uint64_t ringcap[2] = {0, 0};
     if (ring) {
         for (int r = 0; r < nrel; r++) {
-            ringcap[r] = std::max<uint64_t>(ring, maxb[r]);
+            ringcap[r] = std::max<uint64_t>(ring, maxb[r] + 2 * kTileTuples);
             ringbuf[r] = (Tup*)ws->scratch(r ? "bs_ring1" : "bs_ring0",
                                            ringcap[r] * sizeof(Tup));
         }
@@ -831,13 +875,13 @@ void bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
         uint32_t b0 = 0;
         while (b0 < nb) {
             uint32_t b1 = b0;
-            uint64_t fill[2] = {0, 0};
             while (b1 < nb) {
+                // span of buckets b0..b1 in the partition buffer (with slack)
                 bool fits = true;
                 for (int r = 0; r < nrel; r++)
-                    if (fill[r] + hcnt[r * nb + b1] > ringcap[r]) fits = false;
+                    if (hst[r * nb + b1] + hcnt[r * nb + b1] - hst[r * nb + b0] > ringcap[r])
+                        fits = false;
                 if (!fits && b1 > b0) break;
-                for (int r = 0; r < nrel; r++) fill[r] += hcnt[r * nb + b1];
                 b1++;
             }
             batches.push_back({b0, b1});
@@ -862,6 +906,7 @@ void bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
         T.nt[r] = 0;
         G.out[r] = a.out[rr];
         G.bstart[r] = a.bstart[rr];
+        G.ostart[r] = ostart[rr];
         G.tt[r] = tt[rr];
     }
     T.plan = *hplan;
@@ -919,7 +964,7 @@ void bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
     SMJ_CHECK(hipMemcpyAsync(h_novf, novf, 4, hipMemcpyDeviceToHost, st));
     SMJ_CHECK(hipStreamSynchronize(st));
     const uint32_t no = *h_novf;
-    if (no == 0) return;
+    if (no == 0) return true;
     if (no > ovf_cap) {
         fprintf(stderr, "[ERROR] smj: overflow table too small\n");
         abort();
@@ -928,23 +973,32 @@ void bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
     SMJ_CHECK(hipMemcpyAsync(he.data(), ovf, no * sizeof(OvfEntry),
                              hipMemcpyDeviceToHost, st));
     SMJ_CHECK(hipStreamSynchronize(st));
+    if (getenv("SMJ_DEBUG_OVF")) {
+        fprintf(stderr, "[smj] %u overflow groups (nb %u, nb2 %u)\n", no, nb, nb2);
+        for (uint32_t i = 0; i < no && i < 64; i++)
+            fprintf(stderr, "[smj]   b %u g %u nR %u nS %u outR %llu outS %llu\n",
+                    he[i].bucket, he[i].d2, he[i].nr[0], he[i].nr[1],
+                    (unsigned long long)(hdst[he[i].bucket] + he[i].off[0]),
+                    (unsigned long long)(hdst[nb + he[i].bucket] + he[i].off[1]));
+    }
     for (int r = 0; r < nrel; r++) {
         std::vector<uint64_t> so(no), sl(no);
         for (uint32_t i = 0; i < no; i++) {
-            so[i] = hst[r * nb + he[i].bucket] + he[i].off[r];
+            so[i] = hdst[r * nb + he[i].bucket] + he[i].off[r];
             sl[i] = he[i].nr[r];
         }
         segmented_sort(ws, a.out[r], so.data(), sl.data(), no, st);
     }
     if (nrel == 2) {
         for (uint32_t i = 0; i < no; i++) {
-            const Tup* rp = a.out[0] + hst[he[i].bucket] + he[i].off[0];
-            const Tup* sp = a.out[1] + hst[nb + he[i].bucket] + he[i].off[1];
+            const Tup* rp = a.out[0] + hdst[he[i].bucket] + he[i].off[0];
+            const Tup* sp = a.out[1] + hdst[nb + he[i].bucket] + he[i].off[1];
             if (he[i].nr[0] && he[i].nr[1])
                 merge_join_count(rp, he[i].nr[0], sp, he[i].nr[1], a.count_dev, st);
         }
     }
     SMJ_CHECK(hipGetLastError());
+    return true;
 }
 
 }  // namespace smj

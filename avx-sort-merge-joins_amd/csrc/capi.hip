@@ -129,6 +129,17 @@ static void choose_levels(uint64_t n, uint32_t want_d1, uint32_t* D1,
     *D2cap = d2 + 2 > 9 ? (d2 > 9 ? d2 : 9) : d2 + 2;
 }
 
+// level-1 partition of sorts and joins: sampled regions (no histogram pass)
+// unless SMJ_SAMPLED=0
+static bool use_sampled() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("SMJ_SAMPLED");
+        v = e ? atoi(e) : 1;
+    }
+    return v != 0;
+}
+
 static void device_sort(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
                         hipStream_t st) {
     if (n == 0) return;
@@ -139,10 +150,20 @@ static void device_sort(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
     uint64_t ns[1] = {n};
     plan_from_sample(ws, rels, ns, 1, D1, D2, D2cap, 1, 0, plan, st);
     const uint32_t nb = 1u << D1;
-    Tup* part = (Tup*)ws->scratch("sort_part", n * sizeof(Tup));
+    const bool sampled = use_sampled() && D1 <= 10;  // LDS carries up to 1024
+    Tup* part = (Tup*)ws->scratch(
+        "sort_part", (sampled ? sampled_capacity(n, D1) : n) * sizeof(Tup));
     uint64_t* starts = (uint64_t*)ws->scratch("sort_starts", nb * 8);
     int64_t* hist = (int64_t*)ws->scratch("sort_hist", nb * 8);
-    plan_partition(ws, in, n, part, plan, D1, starts, hist, st);
+    unsigned int* flag = (unsigned int*)ws->scratch("part_flag", 4);
+    uint64_t* sgs = (uint64_t*)ws->scratch("sort_sgs", (size_t)nb * kShards * 8);
+    int64_t* sgc = (int64_t*)ws->scratch("sort_sgc", (size_t)nb * kShards * 8);
+    if (sampled) {
+        SMJ_CHECK(hipMemsetAsync(flag, 0, 4, st));
+        sampled_partition(ws, in, n, part, plan, D1, starts, hist, sgs, sgc, flag, st);
+    } else {
+        plan_partition(ws, in, n, part, plan, D1, starts, hist, st);
+    }
     BucketSortArgs a;
     a.part[0] = part;
     a.bstart[0] = starts;
@@ -160,7 +181,19 @@ static void device_sort(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
     a.nbuckets = nb;
     a.plan_dev = plan;
     a.count_dev = nullptr;
-    bucket_sort(ws, a, st);
+    a.part_flag = sampled ? flag : nullptr;
+    if (sampled) {
+        a.seg_start[0] = sgs;
+        a.seg_cnt[0] = sgc;
+    }
+    if (!bucket_sort(ws, a, st)) {
+        // a sampled region overflowed (very skewed keys): exact partition
+        plan_partition(ws, in, n, part, plan, D1, starts, hist, st);
+        a.part_flag = nullptr;
+        a.seg_start[0] = nullptr;
+        a.seg_cnt[0] = nullptr;
+        bucket_sort(ws, a, st);
+    }
 }
 
 static void device_join(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
@@ -178,14 +211,28 @@ static void device_join(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
     uint64_t ns[2] = {nR, nS};
     plan_from_sample(ws, rels, ns, 2, D1, D2, D2cap, hint_min, hint_max, plan, st);
     const uint32_t nb = 1u << D1;
-    Tup* partR = (Tup*)ws->scratch("join_partR", (nR ? nR : 1) * sizeof(Tup));
-    Tup* partS = (Tup*)ws->scratch("join_partS", (nS ? nS : 1) * sizeof(Tup));
+    const bool sampled = use_sampled() && D1 <= 10;  // LDS carries up to 1024
+    Tup* partR = (Tup*)ws->scratch(
+        "join_partR", (sampled ? sampled_capacity(nR, D1) : (nR ? nR : 1)) * sizeof(Tup));
+    Tup* partS = (Tup*)ws->scratch(
+        "join_partS", (sampled ? sampled_capacity(nS, D1) : (nS ? nS : 1)) * sizeof(Tup));
     uint64_t* stR = (uint64_t*)ws->scratch("join_stR", nb * 8);
     uint64_t* stS = (uint64_t*)ws->scratch("join_stS", nb * 8);
     int64_t* hR = (int64_t*)ws->scratch("join_hR", nb * 8);
     int64_t* hS = (int64_t*)ws->scratch("join_hS", nb * 8);
-    plan_partition(ws, R, nR, partR, plan, D1, stR, hR, st);
-    plan_partition(ws, S, nS, partS, plan, D1, stS, hS, st);
+    unsigned int* flag = (unsigned int*)ws->scratch("part_flag", 4);
+    uint64_t* sgsR = (uint64_t*)ws->scratch("join_sgsR", (size_t)nb * kShards * 8);
+    int64_t* sgcR = (int64_t*)ws->scratch("join_sgcR", (size_t)nb * kShards * 8);
+    uint64_t* sgsS = (uint64_t*)ws->scratch("join_sgsS", (size_t)nb * kShards * 8);
+    int64_t* sgcS = (int64_t*)ws->scratch("join_sgcS", (size_t)nb * kShards * 8);
+    if (sampled) {
+        SMJ_CHECK(hipMemsetAsync(flag, 0, 4, st));
+        sampled_partition(ws, R, nR, partR, plan, D1, stR, hR, sgsR, sgcR, flag, st);
+        sampled_partition(ws, S, nS, partS, plan, D1, stS, hS, sgsS, sgcS, flag, st);
+    } else {
+        plan_partition(ws, R, nR, partR, plan, D1, stR, hR, st);
+        plan_partition(ws, S, nS, partS, plan, D1, stS, hS, st);
+    }
     SMJ_CHECK(hipEventRecord(ws->ev[1], st));
     BucketSortArgs a;
     a.part[0] = partR;
@@ -207,7 +254,22 @@ static void device_join(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
     a.ev_tile = nullptr;
     a.ev_bucket = ws->ev[2];
     a.ev_ovf = ws->ev[3];
-    bucket_sort(ws, a, st);
+    a.part_flag = sampled ? flag : nullptr;
+    if (sampled) {
+        a.seg_start[0] = sgsR;
+        a.seg_cnt[0] = sgcR;
+        a.seg_start[1] = sgsS;
+        a.seg_cnt[1] = sgcS;
+    }
+    if (!bucket_sort(ws, a, st)) {
+        // a sampled region overflowed (very skewed keys): exact partitions
+        plan_partition(ws, R, nR, partR, plan, D1, stR, hR, st);
+        plan_partition(ws, S, nS, partS, plan, D1, stS, hS, st);
+        a.part_flag = nullptr;
+        a.seg_start[0] = a.seg_start[1] = nullptr;
+        a.seg_cnt[0] = a.seg_cnt[1] = nullptr;
+        bucket_sort(ws, a, st);
+    }
     SMJ_CHECK(hipEventRecord(ws->ev[4], st));
 }
 

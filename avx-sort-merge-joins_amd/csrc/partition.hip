@@ -515,6 +515,256 @@ k_scatter_wc(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_a
     }
 }
 
+// ---------------------------------------------------------------------------
+// Sampled partitioning (join level 1): no histogram pass.  A strided 1/stride
+// sample estimates every partition's size; each partition gets a region of
+// 9/8 of the estimate plus slack, and workgroups reserve whole 64-byte
+// segments in it with one atomic per (tile, partition) while write-combining
+// exactly like k_scatter_wc.  Partitions come out contiguous from their
+// region start (unstable order), followed by unused slack.  A region that
+// would overflow raises a flag and the caller repeats the exact
+// (histogram) partition.
+template <class Digit>
+__global__ void __launch_bounds__(256)
+k_sample_hist(const Tup* __restrict__ in, uint64_t n, uint32_t stride,
+              Digit dig_arg, uint32_t nbins, unsigned int* __restrict__ hist) {
+    const auto dig = dig_arg.load();
+    extern __shared__ unsigned int sh_hist[];
+    for (uint32_t d = threadIdx.x; d < nbins; d += 256) sh_hist[d] = 0;
+    __syncthreads();
+    const uint64_t step = (uint64_t)gridDim.x * 256 * stride;
+    for (uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * stride; i < n; i += step)
+        atomicAdd(&sh_hist[dig(in[i])], 1u);
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < nbins; d += 256)
+        if (sh_hist[d]) atomicAdd(&hist[d], sh_hist[d]);
+}
+
+// one workgroup: region capacities from the sample, their starts, cursors.
+// Every partition's region is cut into kShards shards (one per group of
+// workgroups, blockIdx % kShards), so that the reservation atomics of a
+// partition are spread over kShards cursors (kShards: smj_internal.hpp).
+
+__global__ void __launch_bounds__(256)
+k_regions(const unsigned int* __restrict__ sample, uint32_t nbins,
+          uint32_t stride, uint64_t slack, uint64_t* __restrict__ base,
+          uint64_t* __restrict__ seg_start, unsigned long long* __restrict__ cursor,
+          uint64_t* __restrict__ cap_end) {
+    __shared__ uint64_t sh[256];
+    constexpr uint64_t SEG = 64 / sizeof(Tup);
+    const uint32_t per = (nbins + 255) / 256;
+    const uint32_t b = threadIdx.x * per;
+    // capacity of one shard of partition d
+    auto cap = [&](uint32_t d) {
+        const uint64_t est = (uint64_t)sample[d] * stride / kShards;
+        return (est + est / 8 + slack + SEG - 1) / SEG * SEG;
+    };
+    uint64_t loc = 0;
+    for (uint32_t k = 0; k < per; k++)
+        if (b + k < nbins) loc += kShards * cap(b + k);
+    sh[threadIdx.x] = loc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t run = 0;
+        for (int t = 0; t < 256; t++) {
+            const uint64_t x = sh[t];
+            sh[t] = run;
+            run += x;
+        }
+    }
+    __syncthreads();
+    uint64_t ex = sh[threadIdx.x];
+    for (uint32_t k = 0; k < per; k++) {
+        const uint32_t d = b + k;
+        if (d < nbins) {
+            base[d] = ex;
+            const uint64_t c = cap(d);
+            for (uint32_t q = 0; q < kShards; q++) {
+                seg_start[d * kShards + q] = ex;
+                cursor[d * kShards + q] = ex;
+                ex += c;
+                cap_end[d * kShards + q] = ex;
+            }
+        }
+    }
+}
+
+// partition and shard sizes from the cursors; flag = 1 when a shard overflowed
+__global__ void __launch_bounds__(256)
+k_regions_done(const uint64_t* __restrict__ seg_start,
+               const unsigned long long* __restrict__ cursor,
+               const uint64_t* __restrict__ cap_end, uint32_t nbins,
+               int64_t* __restrict__ hist_out, int64_t* __restrict__ seg_cnt,
+               unsigned int* __restrict__ flag) {
+    for (uint32_t d = threadIdx.x; d < nbins; d += 256) {
+        int64_t tot = 0;
+        for (uint32_t q = 0; q < kShards; q++) {
+            const uint32_t i = d * kShards + q;
+            const int64_t c = (int64_t)(cursor[i] - seg_start[i]);
+            seg_cnt[i] = c;
+            tot += c;
+            if (cursor[i] > cap_end[i]) atomicOr(flag, 1u);
+        }
+        hist_out[d] = tot;
+    }
+}
+
+template <int THREADS, int ITEMS, class Digit>
+__global__ void __launch_bounds__(THREADS)
+k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_arg,
+              uint32_t nbins, unsigned long long* __restrict__ cursor_all,
+              const uint64_t* __restrict__ cap_end_all, Tup* __restrict__ out) {
+    const auto dig = dig_arg.load();
+    // this workgroup's shard of every partition: cursor[d * kShards + shard]
+    const uint32_t shard = blockIdx.x % kShards;
+    unsigned long long* cursor = cursor_all + shard;
+    const uint64_t* cap_end = cap_end_all + shard;
+    constexpr int TILE = THREADS * ITEMS;
+    constexpr uint32_t SEG = 64 / sizeof(Tup);  // tuples per 64-byte segment
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    Tup* stage = reinterpret_cast<Tup*>(lds_raw);
+    Tup* carry = stage + TILE;
+    uint64_t* pos = reinterpret_cast<uint64_t*>(carry + (size_t)nbins * SEG);
+    uint32_t* tstart = reinterpret_cast<uint32_t*>(pos + nbins);
+    uint32_t* tfill = tstart + nbins;
+    uint32_t* kc = tfill + nbins;
+    uint32_t* scr = kc + nbins;
+
+    for (uint32_t d = threadIdx.x; d < nbins; d += THREADS) {
+        tfill[d] = 0;
+        kc[d] = 0;
+    }
+    const uint64_t beg = (uint64_t)blockIdx.x * chunk;
+    uint64_t end = beg + chunk;
+    if (end > n) end = n;
+    const uint32_t dper = (nbins + THREADS - 1) / THREADS;
+    const uint32_t d0 = threadIdx.x * dper;
+
+    Tup v[ITEMS], nv[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; j++) {
+        const uint64_t i = beg + (uint64_t)j * THREADS + threadIdx.x;
+        if (i < end) v[j] = in[i];
+    }
+    __syncthreads();
+    for (uint64_t base = beg; base < end; base += TILE) {
+        const uint32_t tcount =
+            (uint32_t)((end - base) < (uint64_t)TILE ? (end - base) : TILE);
+        const uint64_t nb = base + TILE;
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint64_t i = nb + (uint64_t)j * THREADS + threadIdx.x;
+            if (i < end) nv[j] = in[i];
+        }
+        // ---- rank: tile counts per partition
+        uint32_t dg[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint32_t li = j * THREADS + threadIdx.x;
+            dg[j] = li < tcount ? dig(v[j]) : 0xffffffffu;
+            if (dg[j] != 0xffffffffu) atomicAdd(&tfill[dg[j]], 1u);
+        }
+        __syncthreads();
+        uint32_t loc = 0;
+        for (uint32_t k = 0; k < dper; k++)
+            if (d0 + k < nbins) loc += tfill[d0 + k];
+        uint32_t tot;
+        uint32_t ex = block_exclusive_scan(loc, scr, &tot);
+        // ---- per partition: reserve the whole segments of carry + tile (E,
+        // a multiple of SEG) in the region; the reservation's latency
+        // overlaps the staging below
+        uint32_t Eown[4];
+        for (uint32_t k = 0; k < dper && k < 4; k++) {
+            const uint32_t d = d0 + k;
+            Eown[k] = 0;
+            if (d < nbins) {
+                const uint32_t c = tfill[d];
+                tstart[d] = ex;
+                tfill[d] = ex;
+                ex += c;
+                const uint32_t T = kc[d] + c;
+                const uint32_t E = T / SEG * SEG;
+                Eown[k] = E;
+                if (E) pos[d] = atomicAdd(&cursor[(size_t)d * kShards], (unsigned long long)E);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++)
+            if (dg[j] != 0xffffffffu) stage[atomicAdd(&tfill[dg[j]], 1u)] = v[j];
+        __syncthreads();
+        for (uint32_t k = 0; k < dper && k < 4; k++) {
+            const uint32_t d = d0 + k;
+            if (d < nbins) {
+                uint32_t E = Eown[k];
+                // an overflowing region writes nothing (the caller repeats
+                // the exact partition)
+                if (E && pos[d] + E > cap_end[(size_t)d * kShards]) E = 0;
+                tfill[d] = E;
+            }
+        }
+        __syncthreads();
+        for (uint32_t q = threadIdx.x; q < nbins * SEG; q += THREADS) {
+            const uint32_t d = q / SEG, j = q % SEG;
+            if (j < kc[d] && j < tfill[d]) out[pos[d] + j] = carry[q];
+        }
+        Tup keep[ITEMS];
+        uint32_t kslot[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint32_t i = j * THREADS + threadIdx.x;
+            kslot[j] = 0xffffffffu;
+            if (i < tcount) {
+                const Tup t = stage[i];
+                const uint32_t d = dig(t);
+                const uint32_t vv = kc[d] + (i - tstart[d]);
+                const uint32_t E = tfill[d];
+                if (vv < E) {
+                    out[pos[d] + vv] = t;
+                } else if (vv - E < SEG) {  // always, unless the region overflowed
+                    keep[j] = t;
+                    kslot[j] = d * SEG + (vv - E);
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++)
+            if (kslot[j] != 0xffffffffu) carry[kslot[j]] = keep[j];
+        for (uint32_t k = 0; k < dper; k++) {
+            const uint32_t d = d0 + k;
+            if (d < nbins) {
+                const uint32_t cnt = ((d + 1 < nbins) ? tstart[d + 1] : tcount) - tstart[d];
+                const uint32_t T = kc[d] + cnt;
+                const uint32_t E = tfill[d];
+                // E == 0 after an overflow: keep at most SEG - 1 (the rest is
+                // lost; the partition is repeated anyway)
+                kc[d] = T - E < SEG ? T - E : SEG - 1;
+                tfill[d] = 0;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) v[j] = nv[j];
+        __syncthreads();
+    }
+    // ---- flush the carries: reserve exactly what is left
+    for (uint32_t k = 0; k < dper; k++) {
+        const uint32_t d = d0 + k;
+        if (d < nbins) {
+            pos[d] = 0;
+            if (kc[d]) {
+                const uint64_t p = atomicAdd(&cursor[(size_t)d * kShards], (unsigned long long)kc[d]);
+                pos[d] = p + kc[d] <= cap_end[(size_t)d * kShards] ? p : ~0ull;
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < nbins * SEG; q += THREADS) {
+        const uint32_t d = q / SEG, j = q % SEG;
+        if (j < kc[d] && pos[d] != ~0ull) out[pos[d] + j] = carry[q];
+    }
+}
+
 // pad copy for wide digits: item at unpadded position i of digit d moves to
 // padded_start[d] + (i - unpadded_start[d])
 template <class Digit>
@@ -803,6 +1053,77 @@ void plan_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
     hipLaunchKernelGGL((k_scatter_wc<THREADS, ITEMS, PlanDigit1>), dim3(nwg),
                        dim3(THREADS), lds, st, in, n, chunk, dig, nbins, counts,
                        nwg, starts_dev, out);
+    SMJ_CHECK(hipGetLastError());
+}
+
+// Sampled level-1 partition (see k_scatter_res): `out` must hold
+// sampled_capacity(n, dbits) tuples.  starts_dev/hist_out receive each
+// partition's region start and size; *flag_dev is OR-ed with 1 when a region
+// overflowed (then the output is incomplete and the exact partition must be
+// used).  Nothing is read back to the host.
+static constexpr uint32_t kSampleStride = 128;
+static constexpr uint64_t kRegionSlack = 1024;  // per shard
+
+uint64_t sampled_capacity(uint64_t n, uint32_t dbits) {
+    const uint64_t SEG = 64 / sizeof(Tup);
+    return n + n / 8 + 2 * kSampleStride +
+           ((uint64_t)1 << dbits) * kShards * (kRegionSlack + 2 * SEG);
+}
+
+void sampled_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
+                       const RangePlan* plan_dev, uint32_t dbits,
+                       uint64_t* starts_dev, int64_t* hist_out,
+                       uint64_t* seg_start, int64_t* seg_cnt,
+                       unsigned int* flag_dev, hipStream_t st) {
+    PlanDigit1 dig{plan_dev};
+    const uint32_t nbins = 1u << dbits;
+    constexpr int THREADS = 512;
+    constexpr int ITEMS = sizeof(Tup) == 16 ? 8 : 16;
+    constexpr int TILE = THREADS * ITEMS;
+    unsigned int* sample = (unsigned int*)ws->scratch("sp_sample", (size_t)nbins * 4);
+    unsigned long long* cursor =
+        (unsigned long long*)ws->scratch("sp_cursor", (size_t)nbins * kShards * 8);
+    uint64_t* cap_end = (uint64_t*)ws->scratch("sp_capend", (size_t)nbins * kShards * 8);
+    SMJ_CHECK(hipMemsetAsync(sample, 0, (size_t)nbins * 4, st));
+    {
+        TraceScope ts(ws, "k_sample", st);
+        const uint64_t ns = (n + kSampleStride - 1) / kSampleStride;
+        uint32_t g = (uint32_t)((ns + 255) / 256);
+        if (g > 1024) g = 1024;
+        if (g == 0) g = 1;
+        hipLaunchKernelGGL((k_sample_hist<PlanDigit1>), dim3(g), dim3(256),
+                           nbins * sizeof(unsigned int), st, in, n, kSampleStride,
+                           dig, nbins, sample);
+        hipLaunchKernelGGL(k_regions, dim3(1), dim3(256), 0, st, sample, nbins,
+                           kSampleStride, kRegionSlack, starts_dev, seg_start, cursor,
+                           cap_end);
+    }
+    if (n) {
+        uint64_t ntiles = (n + TILE - 1) / TILE;
+        const uint32_t maxwg = 256;  // one per CU
+        uint32_t nwg = (uint32_t)(ntiles < maxwg ? ntiles : maxwg);
+        const uint64_t tiles_per_wg = (ntiles + nwg - 1) / nwg;
+        const uint64_t chunk = tiles_per_wg * TILE;
+        nwg = (uint32_t)((ntiles + tiles_per_wg - 1) / tiles_per_wg);
+        const size_t lds = scatter_wc_lds<THREADS, ITEMS>(nbins);
+        static bool attr = false;
+        if (!attr) {
+            SMJ_CHECK(hipFuncSetAttribute(
+                (const void*)k_scatter_res<THREADS, ITEMS, PlanDigit1>,
+                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+            attr = true;
+        }
+        if (lds > 160 * 1024) {
+            fprintf(stderr, "[ERROR] smj: scatter LDS %zu > 160 KiB\n", lds);
+            abort();
+        }
+        TraceScope ts(ws, "k_scatter", st);
+        hipLaunchKernelGGL((k_scatter_res<THREADS, ITEMS, PlanDigit1>), dim3(nwg),
+                           dim3(THREADS), lds, st, in, n, chunk, dig, nbins, cursor,
+                           cap_end, out);
+    }
+    hipLaunchKernelGGL(k_regions_done, dim3(1), dim3(256), 0, st, seg_start, cursor,
+                       cap_end, nbins, hist_out, seg_cnt, flag_dev);
     SMJ_CHECK(hipGetLastError());
 }
 

@@ -145,6 +145,15 @@ void stable_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
 void plan_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
                     const RangePlan* plan_dev, uint32_t dbits,
                     uint64_t* starts_dev, int64_t* hist_out, hipStream_t st);
+// sampled level-1 partition (join): regions with slack, no histogram pass
+uint64_t sampled_capacity(uint64_t n, uint32_t dbits);
+// every partition is kShards segments: seg_start/seg_cnt[d * kShards + q]
+constexpr uint32_t kShards = 8;
+void sampled_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
+                       const RangePlan* plan_dev, uint32_t dbits,
+                       uint64_t* starts_dev, int64_t* hist_out,
+                       uint64_t* seg_start, int64_t* seg_cnt,
+                       unsigned int* flag_dev, hipStream_t st);
 void hist_memcpy(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
                  uint32_t dbits, hipStream_t st);
 
@@ -157,6 +166,10 @@ struct BucketSortArgs {
     const Tup* part[2];
     const uint64_t* bstart[2];  // device, nbuckets
     const int64_t* bcount[2];   // device, nbuckets
+    // optional (sampled partition): bucket b = kShards segments
+    // [seg_start[b*kShards+q], + seg_cnt[...]) inside its region
+    const uint64_t* seg_start[2] = {nullptr, nullptr};
+    const int64_t* seg_cnt[2] = {nullptr, nullptr};
     Tup* tmp[2];                // same size as part (tile-local pass output)
     Tup* out[2];                // sorted output, bucket b at ostart[b]
     uint64_t n[2];
@@ -164,6 +177,7 @@ struct BucketSortArgs {
     uint32_t nbuckets;          // 1 << D1
     const RangePlan* plan_dev;
     unsigned long long* count_dev;  // join count (nrel == 2), accumulated
+    const unsigned int* part_flag = nullptr;  // sampled partition overflowed?
     hipEvent_t ev_tile = nullptr;   // optional phase markers
     hipEvent_t ev_bucket = nullptr;
     hipEvent_t ev_ovf = nullptr;
@@ -171,7 +185,9 @@ struct BucketSortArgs {
 // Runs the tile pass and the group pass; handles overflowing groups (skew)
 // with the merge-sort fallback.  Synchronises `st` twice: once for the bucket
 // counts (launch sizes) and once for the overflow count.
-void bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st);
+// Returns false (and does nothing) when a->part_flag reports an overflowed
+// sampled partition: the caller repeats the exact partition.
+bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st);
 
 // plan selection from a device sample (writes plan_dev)
 // (D2 is the size-preferred level-2 width, D2cap the widest the plan may use

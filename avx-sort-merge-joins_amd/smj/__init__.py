@@ -29,7 +29,9 @@ except Exception:  # pragma: no cover - torch is part of the image
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
-LIBDIR = os.path.join(ROOT, "lib")
+# SMJ_LIB_DIR selects an alternative build of the same libraries (kernel
+# geometry experiments, tools/); the default is the in-tree lib/.
+LIBDIR = os.environ.get("SMJ_LIB_DIR") or os.path.join(ROOT, "lib")
 TUPLE8 = np.dtype([("payload", "<i4"), ("key", "<i4")])
 TUPLE16 = np.dtype([("payload", "<i8"), ("key", "<i8")])
 

@@ -130,3 +130,26 @@ def test_full_size_join_properties(libs, width, dist_):
         assert _checksum(torch, src) == _checksum(torch, out)
     del R, S, sR, sS
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("fanout_bits", [9, 10])
+def test_zipf_join_repeatable(libs, width, fanout_bits):
+    """Skewed S (Zipf 0.75, 16M): many groups take the skew path; the join
+    must give the same, exact result on every run (a race in the group
+    tables once dropped groups non-deterministically)."""
+    import torch
+    lib = libs[width]
+    n = 16_000_000
+    R, S = lib.empty(n), lib.empty(n)
+    lib.dev_gen_pk(R, 0, n, 12345)
+    lib.dev_gen_zipf(S, 0, n, 0.75, 54321)
+    ref = torch.sort(S[:, 1].to(torch.int64)).values
+    sR, sS = lib.empty(n), lib.empty(n)
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    for _ in range(3):
+        lib.dev_join(R, S, sR, sS, cnt, fanout_bits, 1, n)
+        torch.cuda.synchronize()
+        assert int(cnt.item()) == n
+        assert torch.equal(sS[:, 1].to(torch.int64), ref)
+    del R, S, sR, sS, ref
+    torch.cuda.empty_cache()
