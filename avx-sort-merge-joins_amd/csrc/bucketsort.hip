@@ -116,7 +116,8 @@ struct TilePassArgs {
     Tup* tmp[2];
     TileTable tt[2];
     uint32_t t0[2];
-    uint32_t nt[2];
+    uint32_t nt[2];               // blocks of relation r (an upper bound when...)
+    const uint32_t* ntiles[2];    // ...the tile count is only known on the device
     RangePlan plan;  // by value: kernel arguments live in SGPRs
     uint32_t nb2;
 };
@@ -132,6 +133,7 @@ k_tilepass(TilePassArgs A) {
 
     const int r = blockIdx.x < A.nt[0] ? 0 : 1;
     const uint32_t t = A.t0[r] + (r ? blockIdx.x - A.nt[0] : blockIdx.x);
+    if (A.ntiles[r] && t >= *A.ntiles[r]) return;
     const TileTable& tt = A.tt[r];
     const Tup* __restrict__ part = A.part[r];
     Tup* __restrict__ tmp = A.tmp[r];
@@ -753,6 +755,7 @@ void plan_from_sample(Workspace* ws, const Tup* const* rels, const uint64_t* ns,
     SMJ_CHECK(hipGetLastError());
 }
 
+const uint32_t kGroupD3Max = GS_D3MAX;
 // expected group size the plan aims for (capi.hip choose_levels)
 const uint32_t kGroupTarget = GS_CAP * 4 / 5 >= 2048 ? 2048 : (GS_CAP * 4 / 5 >= 1024 ? 1024 : 512);
 
@@ -771,6 +774,168 @@ static uint64_t ring_tuples() {
     return (uint64_t)mb * (1ull << 20) / sizeof(Tup);
 }
 
+// device-side tile numbering of a segmented (sampled) partition: per bucket
+// the tiles of its segments, their exclusive scan (btile0, total in
+// btile0[nb] and *ntiles) and the dense output start of every bucket
+__global__ void __launch_bounds__(256)
+k_seg_scan(const int64_t* __restrict__ seg_cnt, const int64_t* __restrict__ bcount,
+           uint32_t nb, uint32_t nseg, uint32_t* __restrict__ btile0,
+           uint32_t* __restrict__ ntiles, uint64_t* __restrict__ ostart) {
+    __shared__ unsigned long long scr[5];
+    __shared__ unsigned long long base;
+    if (threadIdx.x == 0) base = 0;
+    __syncthreads();
+    for (uint32_t b0 = 0; b0 < nb; b0 += 256) {
+        const uint32_t b = b0 + threadIdx.x;
+        uint32_t nt = 0;
+        uint64_t cnt = 0;
+        if (b < nb) {
+            for (uint32_t q = 0; q < nseg; q++)
+                nt += (uint32_t)((seg_cnt[(size_t)b * nseg + q] + TILE2 - 1) / TILE2);
+            cnt = (uint64_t)bcount[b];
+        }
+        // (tiles << 40 | count): both exclusive scans in one
+        unsigned long long tot;
+        const unsigned long long ex =
+            block_scan64(((unsigned long long)nt << 40) | cnt, scr, &tot);
+        const unsigned long long run = base;
+        if (b < nb) {
+            btile0[b] = (uint32_t)((run >> 40) + (ex >> 40));
+            ostart[b] = (run & ((1ull << 40) - 1)) + (ex & ((1ull << 40) - 1));
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) base = run + tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        btile0[nb] = (uint32_t)(base >> 40);
+        *ntiles = (uint32_t)(base >> 40);
+    }
+}
+
+// Bucket pass without a host synchronisation before the kernels (sampled
+// partition + host-known plan): launch sizes are upper bounds, the tile
+// numbering is computed on the device.  One synchronisation at the end (skew
+// queue and the partition's overflow flag).
+static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
+    const uint32_t nb = a.nbuckets;
+    const int nrel = a.nrel;
+    const uint32_t nb2 = 1u << a.host_plan->D2;
+    TileTable tt[2];
+    static const char* names[2][7] = {
+        {"bs_off0", "bs_len0", "bs_bkt0", "bs_bt00", "bs_pref0", "bs_ost0", "bs_nt0"},
+        {"bs_off1", "bs_len1", "bs_bkt1", "bs_bt01", "bs_pref1", "bs_ost1", "bs_nt1"}};
+    uint64_t* ostart[2] = {nullptr, nullptr};
+    uint32_t* ntiles[2] = {nullptr, nullptr};
+    uint32_t ub[2] = {0, 0};
+    for (int r = 0; r < nrel; r++) {
+        ub[r] = (uint32_t)((a.n[r] + TILE2 - 1) / TILE2 + (uint64_t)nb * kShards);
+        tt[r].off = (uint64_t*)ws->scratch(names[r][0], (size_t)ub[r] * 8);
+        tt[r].len = (uint32_t*)ws->scratch(names[r][1], (size_t)ub[r] * 4);
+        tt[r].bucket = (uint32_t*)ws->scratch(names[r][2], (size_t)ub[r] * 4);
+        tt[r].btile0 = (uint32_t*)ws->scratch(names[r][3], (nb + 1) * 4);
+        tt[r].pref = (uint16_t*)ws->scratch(names[r][4], (size_t)ub[r] * (nb2 + 1) * 2);
+        ostart[r] = (uint64_t*)ws->scratch(names[r][5], (size_t)nb * 8);
+        ntiles[r] = (uint32_t*)ws->scratch(names[r][6], 4);
+        hipLaunchKernelGGL(k_seg_scan, dim3(1), dim3(256), 0, st, a.seg_cnt[r],
+                           a.bcount[r], nb, kShards, tt[r].btile0, ntiles[r], ostart[r]);
+        hipLaunchKernelGGL(k_tiles, dim3(nb), dim3(64), 0, st, a.bstart[r],
+                           a.bcount[r], a.seg_start[r], a.seg_cnt[r], kShards, tt[r]);
+    }
+    if (nrel == 1) tt[1] = tt[0];
+    if (a.ev_tile) SMJ_CHECK(hipEventRecord(a.ev_tile, st));
+
+    const uint32_t ngroups = nb * nb2;
+    const uint32_t ovf_cap = ngroups;
+    OvfEntry* ovf = (OvfEntry*)ws->scratch("bs_ovf", (size_t)ovf_cap * sizeof(OvfEntry));
+    uint32_t* novf = (uint32_t*)ws->scratch("bs_novf", 4);
+    SMJ_CHECK(hipMemsetAsync(novf, 0, 4, st));
+    TilePassArgs T;
+    GroupArgs G;
+    for (int r = 0; r < 2; r++) {
+        const int rr = r < nrel ? r : 0;
+        T.part[r] = a.part[rr];
+        T.tmp[r] = a.tmp[rr];
+        T.tt[r] = tt[rr];
+        T.t0[r] = 0;
+        T.nt[r] = r < nrel ? ub[r] : 0;
+        T.ntiles[r] = ntiles[rr];
+        G.tmp[r] = a.tmp[rr];
+        G.out[r] = a.out[rr];
+        G.bstart[r] = a.bstart[rr];
+        G.ostart[r] = ostart[rr];
+        G.tt[r] = tt[rr];
+    }
+    T.plan = *a.host_plan;
+    T.nb2 = nb2;
+    {
+        TraceScope ts(ws, "k_tilepass", st);
+        const size_t tp_lds = TILE2 * sizeof(Tup) + nb2 * 4 + 64;
+        hipLaunchKernelGGL(k_tilepass, dim3(T.nt[0] + T.nt[1]), dim3(TP_THREADS),
+                           tp_lds, st, T);
+    }
+    if (a.ev_bucket) SMJ_CHECK(hipEventRecord(a.ev_bucket, st));
+    G.nrel = nrel;
+    G.plan = *a.host_plan;
+    G.count_dev = a.count_dev;
+    G.nb2 = nb2;
+    G.ovf = ovf;
+    G.novf = novf;
+    G.ovf_cap = ovf_cap;
+    G.g_begin = 0;
+    G.g_end = ngroups;
+    const uint32_t maxwg = GS_WG_PER_CU * 256;
+    G.per = (ngroups + maxwg - 1) / maxwg;
+    {
+        const uint32_t nwg = (ngroups + G.per - 1) / G.per;
+        TraceScope ts(ws, "k_groupsort", st);
+        hipLaunchKernelGGL(k_groupsort, dim3(nwg), dim3(GS_THREADS),
+                           sizeof(GroupLDS), st, G);
+    }
+    SMJ_CHECK(hipGetLastError());
+    if (a.ev_ovf) SMJ_CHECK(hipEventRecord(a.ev_ovf, st));
+
+    // ---- the one synchronisation: partition overflow flag + skew queue
+    uint32_t* h = (uint32_t*)ws->host_pinned("bs_h_flagovf", 8);
+    h[0] = h[1] = 0;
+    SMJ_CHECK(hipMemcpyAsync(h, a.part_flag, 4, hipMemcpyDeviceToHost, st));
+    SMJ_CHECK(hipMemcpyAsync(h + 1, novf, 4, hipMemcpyDeviceToHost, st));
+    SMJ_CHECK(hipStreamSynchronize(st));
+    if (h[0]) return false;  // the caller repeats with exact partitions
+    const uint32_t no = h[1];
+    if (no == 0) return true;
+    if (no > ovf_cap) {
+        fprintf(stderr, "[ERROR] smj: overflow table too small\n");
+        abort();
+    }
+    std::vector<OvfEntry> he(no);
+    std::vector<uint64_t> hdst((size_t)2 * nb);
+    SMJ_CHECK(hipMemcpyAsync(he.data(), ovf, no * sizeof(OvfEntry),
+                             hipMemcpyDeviceToHost, st));
+    for (int r = 0; r < nrel; r++)
+        SMJ_CHECK(hipMemcpyAsync(hdst.data() + (size_t)r * nb, ostart[r], (size_t)nb * 8,
+                                 hipMemcpyDeviceToHost, st));
+    SMJ_CHECK(hipStreamSynchronize(st));
+    for (int r = 0; r < nrel; r++) {
+        std::vector<uint64_t> so(no), sl(no);
+        for (uint32_t i = 0; i < no; i++) {
+            so[i] = hdst[(size_t)r * nb + he[i].bucket] + he[i].off[r];
+            sl[i] = he[i].nr[r];
+        }
+        segmented_sort(ws, a.out[r], so.data(), sl.data(), no, st);
+    }
+    if (nrel == 2) {
+        for (uint32_t i = 0; i < no; i++) {
+            const Tup* rp = a.out[0] + hdst[he[i].bucket] + he[i].off[0];
+            const Tup* sp = a.out[1] + hdst[nb + he[i].bucket] + he[i].off[1];
+            if (he[i].nr[0] && he[i].nr[1])
+                merge_join_count(rp, he[i].nr[0], sp, he[i].nr[1], a.count_dev, st);
+        }
+    }
+    SMJ_CHECK(hipGetLastError());
+    return true;
+}
+
 bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
     const uint32_t nb = a.nbuckets;
     const int nrel = a.nrel;
@@ -779,12 +944,14 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
         SMJ_CHECK(hipFuncSetAttribute((const void*)k_tilepass,
                                       hipFuncAttributeMaxDynamicSharedMemorySize,
                                       160 * 1024));
-        // two workgroups per CU (launch bounds): ask for exactly what one needs
+        // several workgroups per CU (launch bounds): ask for what one needs
         SMJ_CHECK(hipFuncSetAttribute((const void*)k_groupsort,
                                       hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)sizeof(GroupLDS)));
         attr = true;
     }
+    if (a.host_plan && a.seg_start[0] && a.part_flag && ring_tuples() == 0)
+        return bucket_sort_nosync(ws, a, st);
 
     // ---- host view of the plan and the bucket counts (one synchronisation):
     // launch sizes, tile numbering and batches are derived from them
@@ -904,6 +1071,7 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
         T.tt[r] = tt[rr];
         T.t0[r] = 0;
         T.nt[r] = 0;
+        T.ntiles[r] = nullptr;
         G.out[r] = a.out[rr];
         G.bstart[r] = a.bstart[rr];
         G.ostart[r] = ostart[rr];

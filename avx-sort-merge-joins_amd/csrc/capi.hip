@@ -16,6 +16,8 @@
 #include "smj_common.hpp"
 #include "smj_internal.hpp"
 
+__global__ void k_setplan(smj::RangePlan* p, smj::RangePlan v) { *p = v; }
+
 namespace smj {
 void gen_pk_nopayload(Tup* out, uint64_t n, uint64_t first, uint64_t total,
                       uint64_t seed, hipStream_t st);
@@ -52,7 +54,6 @@ static Ctx& ctx() {
     return *c;
 }
 
-__global__ void k_setplan(RangePlan* p, RangePlan v) { *p = v; }
 
 static bool is_device_ptr(const void* p) {
     if (!p) return false;
@@ -209,7 +210,13 @@ static void device_join(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
     RangePlan* plan = (RangePlan*)ws->scratch("plan", sizeof(RangePlan));
     const Tup* rels[2] = {R, S};
     uint64_t ns[2] = {nR, nS};
-    plan_from_sample(ws, rels, ns, 2, D1, D2, D2cap, hint_min, hint_max, plan, st);
+    // with a key-range hint the plan is known here (same make_plan as k_plan)
+    RangePlan hplan = make_plan(hint_min, hint_max, D1, D2, D2cap, kGroupD3Max);
+    const bool plan_on_host = hint_min <= hint_max;
+    if (plan_on_host)
+        hipLaunchKernelGGL(k_setplan, dim3(1), dim3(1), 0, st, plan, hplan);
+    else
+        plan_from_sample(ws, rels, ns, 2, D1, D2, D2cap, hint_min, hint_max, plan, st);
     const uint32_t nb = 1u << D1;
     const bool sampled = use_sampled() && D1 <= 10;  // LDS carries up to 1024
     Tup* partR = (Tup*)ws->scratch(
@@ -255,6 +262,7 @@ static void device_join(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
     a.ev_bucket = ws->ev[2];
     a.ev_ovf = ws->ev[3];
     a.part_flag = sampled ? flag : nullptr;
+    a.host_plan = plan_on_host ? &hplan : nullptr;
     if (sampled) {
         a.seg_start[0] = sgsR;
         a.seg_cnt[0] = sgcR;

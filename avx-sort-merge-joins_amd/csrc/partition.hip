@@ -532,9 +532,19 @@ k_sample_hist(const Tup* __restrict__ in, uint64_t n, uint32_t stride,
     extern __shared__ unsigned int sh_hist[];
     for (uint32_t d = threadIdx.x; d < nbins; d += 256) sh_hist[d] = 0;
     __syncthreads();
-    const uint64_t step = (uint64_t)gridDim.x * 256 * stride;
-    for (uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * stride; i < n; i += step)
-        atomicAdd(&sh_hist[dig(in[i])], 1u);
+    // sample points every 4 * stride tuples, 4 consecutive tuples each (one
+    // 64-byte read for 16-byte tuples): 1/stride of the input
+    const uint64_t pstride = 4ull * stride;
+    const uint64_t step = (uint64_t)gridDim.x * 256 * pstride;
+    for (uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * pstride; i < n; i += step) {
+        Tup t[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (i + k < n) t[k] = in[i + k];
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (i + k < n) atomicAdd(&sh_hist[dig(t[k])], 1u);
+    }
     __syncthreads();
     for (uint32_t d = threadIdx.x; d < nbins; d += 256)
         if (sh_hist[d]) atomicAdd(&hist[d], sh_hist[d]);
@@ -600,7 +610,10 @@ k_regions_done(const uint64_t* __restrict__ seg_start,
         int64_t tot = 0;
         for (uint32_t q = 0; q < kShards; q++) {
             const uint32_t i = d * kShards + q;
-            const int64_t c = (int64_t)(cursor[i] - seg_start[i]);
+            // clamped: after an overflow the (discarded) result must still
+            // describe memory inside the region
+            const uint64_t e = cursor[i] < cap_end[i] ? cursor[i] : cap_end[i];
+            const int64_t c = (int64_t)(e - seg_start[i]);
             seg_cnt[i] = c;
             tot += c;
             if (cursor[i] > cap_end[i]) atomicOr(flag, 1u);
@@ -1087,7 +1100,7 @@ void sampled_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
     SMJ_CHECK(hipMemsetAsync(sample, 0, (size_t)nbins * 4, st));
     {
         TraceScope ts(ws, "k_sample", st);
-        const uint64_t ns = (n + kSampleStride - 1) / kSampleStride;
+        const uint64_t ns = (n + 4 * kSampleStride - 1) / (4 * kSampleStride);
         uint32_t g = (uint32_t)((ns + 255) / 256);
         if (g > 1024) g = 1024;
         if (g == 0) g = 1;

@@ -160,6 +160,7 @@ void hist_memcpy(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
 // ---- bucketsort.hip : MSD bucket sort (+ fused merge-join count)
 extern const uint32_t kGroupTarget;  // expected tuples per group of the plan
 extern const uint32_t kTileTuples;   // tile of the tile pass
+extern const uint32_t kGroupD3Max;   // widest level-3 digit of the group pass
 struct BucketSortArgs {
     // level-1 partitioned relation(s): bucket b occupies
     // [bstart[b], bstart[b] + bcount[b]) of `part`.
@@ -178,6 +179,9 @@ struct BucketSortArgs {
     const RangePlan* plan_dev;
     unsigned long long* count_dev;  // join count (nrel == 2), accumulated
     const unsigned int* part_flag = nullptr;  // sampled partition overflowed?
+    // the plan, when the host computed it (key-range hints): with a sampled
+    // partition the bucket pass then runs without a mid-pipeline host sync
+    const RangePlan* host_plan = nullptr;
     hipEvent_t ev_tile = nullptr;   // optional phase markers
     hipEvent_t ev_bucket = nullptr;
     hipEvent_t ev_ovf = nullptr;
