@@ -54,10 +54,10 @@ def alg_bytes_per_launch(name, n_rel, nR, nS, w):
     """Algorithmic HBM bytes of one launch: a materialising
     pass reads and writes every tuple once (2w), a histogram reads once (w)."""
     return {
-        "k_hist": n_rel * w,
-        "k_scatter": 2 * n_rel * w,
-        "k_tilepass": 2 * n_rel * w,
-        "k_groupsort": 2 * (nR + nS) * w,
+        "k_hist": n_rel * w,                 # one relation per launch
+        "k_scatter": 2 * n_rel * w,          # one relation per launch
+        "k_tilepass": 2 * (nR + nS) * w,     # R and S in one launch
+        "k_groupsort": 2 * (nR + nS) * w,    # R and S in one launch
     }.get(name)
 
 
@@ -113,12 +113,15 @@ def cpu_baseline(width, n):
 
 
 def load_traffic(kernel, cfg_key):
+    """HBM bytes per launch of `kernel` (FETCH_SIZE*2 + WRITE_SIZE, separate
+    rocprofv3 --pmc passes of this same bench command; tools/make_traffic.py
+    wrote profiles/pmc_traffic.json).  None when not profiled."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
         e = d.get(cfg_key, {}).get(kernel)
-        return e
+        return int(e["bytes"]) if e else None
     except Exception:
         return None
 
