@@ -78,7 +78,9 @@ struct TileTable {
 struct OvfEntry {
     uint32_t bucket, d2;
     uint32_t nr[2];
-    uint64_t off[2];  // offset of the group inside its bucket
+    uint64_t off[2];   // offset of the group inside its bucket
+    uint32_t counted;  // 1: its matches were already added (exact digits)
+    uint32_t pad;
 };
 
 // ---------------------------------------------------------------------------
@@ -420,6 +422,17 @@ __device__ __forceinline__ void group_overflow(const GroupArgs& A, GroupLDS& L,
                                                const GroupMeta& M) {
     uint32_t nn[2] = {0, 0};
     uint64_t oo[2] = {0, 0};
+    const RangePlan& P = A.plan;
+    const uint32_t d12 = (M.b << P.D2) | M.g;
+    const uint64_t bu = key_u(P.base);
+    // the group's level-3 histograms (u32: skewed groups exceed 16 bits), in
+    // the LDS of the sort buffer: when the last digit is the exact key they
+    // give the group's match count without sorting it
+    uint32_t* hc = reinterpret_cast<uint32_t*>(L.B);
+    static_assert(sizeof(L.B) >= 2 * GS_NB3 * sizeof(uint32_t), "histogram space");
+    for (uint32_t i = otid(); i < 2 * GS_NB3; i += GS_THREADS) hc[i] = 0;
+    __syncthreads();
+    bool clamped = false;
 #pragma unroll
     for (int r = 0; r < 2; r++) {
         if (r >= A.nrel) break;
@@ -435,15 +448,29 @@ __device__ __forceinline__ void group_overflow(const GroupArgs& A, GroupLDS& L,
         nn[r] = (uint32_t)tot;
         oo[r] = tot >> 32;
         Tup* dst = A.out[r] + M.ost[r] + oo[r];
-        const Tup* tp = A.tmp[r] + M.bst[r];
         uint32_t pos = 0;
         for (uint32_t t = 0; t < nt; t++) {
             const uint16_t* pf = pref + (uint64_t)(t0 + t) * (A.nb2 + 1) + M.g;
             const uint32_t lo = pf[0], len = (uint32_t)(pf[1] - pf[0]);
             const Tup* src = A.tmp[r] + A.tt[r].off[t0 + t] + lo;
-            for (uint32_t i = otid(); i < len; i += GS_THREADS) dst[pos + i] = src[i];
+            for (uint32_t i = otid(); i < len; i += GS_THREADS) {
+                const Tup x = src[i];
+                dst[pos + i] = x;
+                const int64_t key = tup_key(x);
+                const uint64_t ku = key_u(key);
+                clamped |= (ku < bu) || (ku - bu > P.span);
+                atomicAdd(&hc[r * GS_NB3 + plan_d3(P, plan_rel(P, key), d12)], 1u);
+            }
             pos += len;
         }
+    }
+    const bool exact = A.nrel == 2 && P.s3 == 0 && !__syncthreads_or(clamped);
+    if (exact) {
+        unsigned long long m = 0;
+        for (uint32_t d = otid(); d < GS_NB3; d += GS_THREADS)
+            m += (unsigned long long)hc[d] * hc[GS_NB3 + d];
+        m = wave_sum(m);
+        if ((otid() & 63) == 0 && m) atomicAdd(A.count_dev, m);
     }
     if (otid() == 0) {
         const uint32_t k = atomicAdd(A.novf, 1u);
@@ -455,9 +482,12 @@ __device__ __forceinline__ void group_overflow(const GroupArgs& A, GroupLDS& L,
             e.nr[1] = nn[1];
             e.off[0] = oo[0];
             e.off[1] = oo[1];
+            e.counted = exact ? 1u : 0u;
+            e.pad = 0;
             A.ovf[k] = e;
         }
     }
+    __syncthreads();  // the histograms lived in the sort buffer
 }
 
 // gather relation r's group into registers (loads only: every load in
@@ -925,12 +955,17 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
         segmented_sort(ws, a.out[r], so.data(), sl.data(), no, st);
     }
     if (nrel == 2) {
+        std::vector<const Tup*> rp, sp;
+        std::vector<uint64_t> nr, ns;
         for (uint32_t i = 0; i < no; i++) {
-            const Tup* rp = a.out[0] + hdst[he[i].bucket] + he[i].off[0];
-            const Tup* sp = a.out[1] + hdst[nb + he[i].bucket] + he[i].off[1];
-            if (he[i].nr[0] && he[i].nr[1])
-                merge_join_count(rp, he[i].nr[0], sp, he[i].nr[1], a.count_dev, st);
+            if (he[i].counted || !he[i].nr[0] || !he[i].nr[1]) continue;
+            rp.push_back(a.out[0] + hdst[he[i].bucket] + he[i].off[0]);
+            sp.push_back(a.out[1] + hdst[nb + he[i].bucket] + he[i].off[1]);
+            nr.push_back(he[i].nr[0]);
+            ns.push_back(he[i].nr[1]);
         }
+        merge_join_count_batch(ws, rp.data(), nr.data(), sp.data(), ns.data(),
+                               (uint32_t)rp.size(), a.count_dev, st);
     }
     SMJ_CHECK(hipGetLastError());
     return true;
@@ -1158,12 +1193,17 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
         segmented_sort(ws, a.out[r], so.data(), sl.data(), no, st);
     }
     if (nrel == 2) {
+        std::vector<const Tup*> rp, sp;
+        std::vector<uint64_t> nr, ns;
         for (uint32_t i = 0; i < no; i++) {
-            const Tup* rp = a.out[0] + hdst[he[i].bucket] + he[i].off[0];
-            const Tup* sp = a.out[1] + hdst[nb + he[i].bucket] + he[i].off[1];
-            if (he[i].nr[0] && he[i].nr[1])
-                merge_join_count(rp, he[i].nr[0], sp, he[i].nr[1], a.count_dev, st);
+            if (he[i].counted || !he[i].nr[0] || !he[i].nr[1]) continue;
+            rp.push_back(a.out[0] + hdst[he[i].bucket] + he[i].off[0]);
+            sp.push_back(a.out[1] + hdst[nb + he[i].bucket] + he[i].off[1]);
+            nr.push_back(he[i].nr[0]);
+            ns.push_back(he[i].nr[1]);
         }
+        merge_join_count_batch(ws, rp.data(), nr.data(), sp.data(), ns.data(),
+                               (uint32_t)rp.size(), a.count_dev, st);
     }
     SMJ_CHECK(hipGetLastError());
     return true;

@@ -170,6 +170,44 @@ k_mjcount(const Tup* __restrict__ R, uint64_t nr, const Tup* __restrict__ S,
     if (lane_id() == 0 && c) atomicAdd(count, c);
 }
 
+// one block per pair of sorted runs: k_mjcount's counting, grid-batched
+struct JoinPair {
+    const Tup* r;
+    const Tup* s;
+    uint64_t nr, ns;
+};
+
+__global__ void __launch_bounds__(256)
+k_mjcount_batch(const JoinPair* __restrict__ pairs, unsigned long long* __restrict__ count) {
+    const JoinPair P = pairs[blockIdx.x];
+    unsigned long long c = 0;
+    for (uint64_t i = threadIdx.x; i < P.ns; i += 256) {
+        const int64_t k = tup_key(P.s[i]);
+        if (i > 0 && tup_key(P.s[i - 1]) == k) continue;
+        uint64_t lo = i + 1, hi = P.ns;
+        while (lo < hi) {
+            const uint64_t m = (lo + hi) >> 1;
+            if (tup_key(P.s[m]) <= k) lo = m + 1; else hi = m;
+        }
+        const uint64_t sc = lo - i;
+        lo = 0;
+        hi = P.nr;
+        while (lo < hi) {
+            const uint64_t m = (lo + hi) >> 1;
+            if (tup_key(P.r[m]) < k) lo = m + 1; else hi = m;
+        }
+        const uint64_t rl = lo;
+        hi = P.nr;
+        while (lo < hi) {
+            const uint64_t m = (lo + hi) >> 1;
+            if (tup_key(P.r[m]) <= k) lo = m + 1; else hi = m;
+        }
+        c += (unsigned long long)(lo - rl) * sc;
+    }
+    c = wave_sum(c);
+    if (lane_id() == 0 && c) atomicAdd(count, c);
+}
+
 __global__ void k_copy(const Tup* __restrict__ a, Tup* __restrict__ b,
                        uint64_t n) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -231,6 +269,20 @@ void merge_join_count(const Tup* r, uint64_t nr, const Tup* s, uint64_t ns,
     SMJ_CHECK(hipGetLastError());
 }
 
+void merge_join_count_batch(Workspace* ws, const Tup* const* r, const uint64_t* nr,
+                            const Tup* const* s, const uint64_t* ns, uint32_t k,
+                            unsigned long long* count_dev, hipStream_t st) {
+    if (k == 0) return;
+    const size_t bytes = (size_t)k * sizeof(JoinPair);
+    JoinPair* dev = (JoinPair*)ws->scratch("mj_pairs", bytes);
+    JoinPair* h = (JoinPair*)ws->host_pinned("mj_pairs_h", bytes);
+    SMJ_CHECK(hipStreamSynchronize(st));  // the pinned table is reused
+    for (uint32_t i = 0; i < k; i++) h[i] = JoinPair{r[i], s[i], nr[i], ns[i]};
+    SMJ_CHECK(hipMemcpyAsync(dev, h, bytes, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_mjcount_batch, dim3(k), dim3(256), 0, st, dev, count_dev);
+    SMJ_CHECK(hipGetLastError());
+}
+
 // Sort every segment [off, off+len) of `data` in place.
 void segmented_sort(Workspace* ws, Tup* data, const uint64_t* seg_off,
                     const uint64_t* seg_len, uint32_t nseg, hipStream_t st) {
@@ -287,12 +339,12 @@ void segmented_sort(Workspace* ws, Tup* data, const uint64_t* seg_off,
         in_data = !in_data;
     }
     if (!in_data) {
-        for (uint32_t s = 0; s < nseg; s++) {
-            if (seg_len[s] == 0) continue;
-            hipLaunchKernelGGL(k_copy, dim3(256), dim3(256), 0, st,
-                               tmp + tmp_off[s], data + seg_off[s], seg_len[s]);
-        }
-        SMJ_CHECK(hipGetLastError());
+        // copy every segment back in one launch (a merge with an empty run)
+        std::vector<MergeTile> tiles;
+        for (uint32_t s = 0; s < nseg; s++)
+            if (seg_len[s]) add_pair_tiles(tiles, tmp + tmp_off[s], seg_len[s],
+                                           tmp + tmp_off[s], 0, data + seg_off[s]);
+        launch_tiles(ws, tiles, st);
     }
 }
 

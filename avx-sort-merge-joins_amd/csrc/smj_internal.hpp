@@ -208,6 +208,10 @@ void merge2(const Tup* a, uint64_t na, const Tup* b, uint64_t nb, Tup* out,
             hipStream_t st);
 void merge_join_count(const Tup* r, uint64_t nr, const Tup* s, uint64_t ns,
                       unsigned long long* count_dev, hipStream_t st);
+// k independent merge-join counts (host arrays), one launch
+void merge_join_count_batch(Workspace* ws, const Tup* const* r, const uint64_t* nr,
+                            const Tup* const* s, const uint64_t* ns, uint32_t k,
+                            unsigned long long* count_dev, hipStream_t st);
 void multiway_merge(Workspace* ws, const Tup* const* runs_host,
                     const uint64_t* lens_host, uint32_t k, Tup* out,
                     hipStream_t st);
