@@ -46,7 +46,8 @@ REFERENCE_SYMBOLS = [
     "avx_merge_tuples", "avx_merge_int64", "scalar_merge_tuples",
     "scalar_merge_int64", "avx_multiway_merge", "scalar_multiway_merge",
     "scalar_multiway_merge_modulo", "scalar_multiway_merge_bitand",
-    "merge_join", "sortmergejoin_multiway", "sortmergejoin_mpsm",
+    "merge_join", "print_timing", "sortmergejoin_multiway", "sortmergejoin_multipass",
+    "sortmergejoin_mpsm",
 ]
 DEVICE_SYMBOLS = [
     "smj_tuple_bytes", "smj_device_name", "smj_workspace_create",
@@ -131,6 +132,7 @@ class Library:
             "scalar_multiway_merge": (_U64, [_P, _P, _U32, _P, _U32]),
             "merge_join": (_U64, [_P, _P, _U64, _U64, _P]),
             "sortmergejoin_multiway": (C.POINTER(Result), [_P, _P, _P]),
+            "sortmergejoin_multipass": (C.POINTER(Result), [_P, _P, _P]),
             "sortmergejoin_mpsm": (C.POINTER(Result), [_P, _P, _P]),
             "smj_tuple_bytes": (C.c_int, []),
             "smj_device_name": (C.c_char_p, []),
@@ -229,17 +231,29 @@ class Library:
         s = np.ascontiguousarray(s, dtype=self.dtype)
         return int(self.lib.merge_join(_ptr(r), _ptr(s), len(r), len(s), None))
 
-    def sortmergejoin_multiway(self, R, S, nthreads=1, fanout=128, mpsm=False):
+    def sortmergejoin_multiway(self, R, S, nthreads=1, fanout=128, mpsm=False,
+                               algo=None):
+        """algo: "m-way" (default), "m-pass" or "mpsm" -- the reference's
+        sortmergejoins -a choices (src/main.c:455-466)."""
         R = np.ascontiguousarray(R, dtype=self.dtype)
         S = np.ascontiguousarray(S, dtype=self.dtype)
         cfg = JoinConfig(nthreads, fanout, int(self.width == 16), int(self.width == 16),
                          20 << 20, 2)
         rr, rs = self._rel(R), self._rel(S)
-        fn = self.lib.sortmergejoin_mpsm if mpsm else self.lib.sortmergejoin_multiway
+        algo = algo or ("mpsm" if mpsm else "m-way")
+        fn = {"m-way": self.lib.sortmergejoin_multiway,
+              "m-pass": self.lib.sortmergejoin_multipass,
+              "mpsm": self.lib.sortmergejoin_mpsm}[algo]
         res = fn(C.byref(rr), C.byref(rs), C.byref(cfg))
         if not res:
             return None
-        return int(res.contents.totalresults)
+        total = int(res.contents.totalresults)
+        # the caller frees the result (src/main.c:629-632)
+        libc = C.CDLL(None)
+        libc.free.argtypes = [C.c_void_p]
+        libc.free(res.contents.resultlist)
+        libc.free(C.cast(res, C.c_void_p))
+        return total
 
     # ---------------------------------------------------------------- device
     @property

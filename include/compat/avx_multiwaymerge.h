@@ -7,5 +7,8 @@
  */
 #ifndef AVXMULTIWAYMERGE_H
 #define AVXMULTIWAYMERGE_H
+#ifndef SMJ_H
+#define SMJ_COMPAT_HIDE_PRINT_TIMING
+#endif
 #include "../smj.h"
 #endif /* AVXMULTIWAYMERGE_H */

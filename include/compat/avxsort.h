@@ -7,5 +7,8 @@
  */
 #ifndef AVXSORT_H
 #define AVXSORT_H
+#ifndef SMJ_H
+#define SMJ_COMPAT_HIDE_PRINT_TIMING
+#endif
 #include "../smj.h"
 #endif /* AVXSORT_H */

@@ -7,5 +7,8 @@
  */
 #ifndef AVXSORT_MULTIWAYMERGE_H_
 #define AVXSORT_MULTIWAYMERGE_H_
+#ifndef SMJ_H
+#define SMJ_COMPAT_HIDE_PRINT_TIMING
+#endif
 #include "../smj.h"
 #endif /* AVXSORT_MULTIWAYMERGE_H_ */

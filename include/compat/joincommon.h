@@ -8,4 +8,9 @@
 #ifndef JOINCOMMON_H_
 #define JOINCOMMON_H_
 #include "../smj.h"
+#ifdef SMJ_COMPAT_HIDE_PRINT_TIMING
+/* joincommon.h:64-66 (smj.h was included first by another compat header) */
+void print_timing(uint64_t numtuples, struct timeval * start,
+                  struct timeval * end, FILE * out);
+#endif
 #endif /* JOINCOMMON_H_ */

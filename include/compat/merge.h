@@ -7,5 +7,8 @@
  */
 #ifndef MERGE_H
 #define MERGE_H
+#ifndef SMJ_H
+#define SMJ_COMPAT_HIDE_PRINT_TIMING
+#endif
 #include "../smj.h"
 #endif /* MERGE_H */

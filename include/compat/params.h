@@ -5,4 +5,7 @@
  * params.h are interchangeable in one translation unit.
  * Provides: NRADIXBITS_DEFAULT, CACHELINEPADDING, RELATION_PADDING, ALIGN_NUMTUPLES, ....
  */
+#ifndef SMJ_H
+#define SMJ_COMPAT_HIDE_PRINT_TIMING
+#endif
 #include "../smj.h"

@@ -7,5 +7,8 @@
  */
 #ifndef PARTITION_H
 #define PARTITION_H
+#ifndef SMJ_H
+#define SMJ_COMPAT_HIDE_PRINT_TIMING
+#endif
 #include "../smj.h"
 #endif /* PARTITION_H */

@@ -7,5 +7,8 @@
  */
 #ifndef SCALARMULTIWAYMERGE_H
 #define SCALARMULTIWAYMERGE_H
+#ifndef SMJ_H
+#define SMJ_COMPAT_HIDE_PRINT_TIMING
+#endif
 #include "../smj.h"
 #endif /* SCALARMULTIWAYMERGE_H */

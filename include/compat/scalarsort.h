@@ -7,5 +7,8 @@
  */
 #ifndef SCALARSORT_H
 #define SCALARSORT_H
+#ifndef SMJ_H
+#define SMJ_COMPAT_HIDE_PRINT_TIMING
+#endif
 #include "../smj.h"
 #endif /* SCALARSORT_H */

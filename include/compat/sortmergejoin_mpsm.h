@@ -7,5 +7,8 @@
  */
 #ifndef SORTMERGEJOIN_MPSM_H
 #define SORTMERGEJOIN_MPSM_H
+#ifndef SMJ_H
+#define SMJ_COMPAT_HIDE_PRINT_TIMING
+#endif
 #include "../smj.h"
 #endif /* SORTMERGEJOIN_MPSM_H */

@@ -7,5 +7,8 @@
  */
 #ifndef SORTMERGEJOIN_MULTIWAY_H_
 #define SORTMERGEJOIN_MULTIWAY_H_
+#ifndef SMJ_H
+#define SMJ_COMPAT_HIDE_PRINT_TIMING
+#endif
 #include "../smj.h"
 #endif /* SORTMERGEJOIN_MULTIWAY_H_ */

@@ -5,4 +5,7 @@
  * types.h are interchangeable in one translation unit.
  * Provides: tuple_t, relation_t, result_t, threadresult_t, joinconfig_t (KEY_8B selects 16-byte tuples).
  */
+#ifndef SMJ_H
+#define SMJ_COMPAT_HIDE_PRINT_TIMING
+#endif
 #include "../smj.h"

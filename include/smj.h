@@ -37,7 +37,9 @@
 
 #include <stdint.h>
 #include <stddef.h>
+#include <stdio.h>
 #include <inttypes.h>
+#include <sys/time.h>
 
 #ifdef __cplusplus
 extern "C" {
@@ -231,6 +233,15 @@ uint64_t scalar_multiway_merge_bitand(tuple_t * output, relation_t ** parts,
 uint64_t merge_join(tuple_t * rtuples, tuple_t * stuples, const uint64_t numR,
                     const uint64_t numS, void * output);
 
+/* joincommon.c:214-227: the drivers' timing line ("NUM-TUPLES = ...
+ * TOTAL-TIME-USECS = ... TUPLES-PER-SECOND = ..."), host-side.  Declared in
+ * the reference only by joincommon.h (some drivers define their own
+ * print_timing), so the compat headers other than joincommon.h hide it. */
+#ifndef SMJ_COMPAT_HIDE_PRINT_TIMING
+void print_timing(uint64_t numtuples, struct timeval * start,
+                  struct timeval * end, FILE * out);
+#endif
+
 /* sortmergejoin_multiway.c:50-61: m-way sort-merge join. Returns a malloc'd
  * result_t (caller frees resultlist and the struct, main.c:629-632) whose
  * totalresults is the match count; NULL for a non-power-of-2 NTHREADS as the
@@ -238,6 +249,11 @@ uint64_t merge_join(tuple_t * rtuples, tuple_t * stuples, const uint64_t numR,
  * fan-out checks: the whole join runs on the current HIP device. */
 result_t * sortmergejoin_multiway(relation_t * relR, relation_t * relS,
                                   joinconfig_t * joincfg);
+
+/* sortmergejoin_multipass.c:51-736 (m-pass): sort R and S completely, then
+ * one merge-join scan; same result contract as sortmergejoin_multiway. */
+result_t * sortmergejoin_multipass(relation_t * relR, relation_t * relS,
+                                   joinconfig_t * joincfg);
 
 /* sortmergejoin_mpsm.c is a stub that exits in the reference; here it is the
  * same device pipeline (one process drives one GPU; multi-GPU runs shard

@@ -47,5 +47,12 @@ for w in 8 16; do
     $CXX -shared -Wl,-Bsymbolic $objs "$objdir/ref_shim.o" -o "$HERE/_ref/libref$w.so" -lpthread -lm
     $CXX -O2 $def $INC -c "$HERE/cpu_baseline.cpp" -o "$objdir/cpu_baseline.o" -w
     $CXX $objs "$objdir/cpu_baseline.o" -o "$HERE/_ref/cpu_baseline$w" -lpthread -lm
+    # the reference's own driver (src/main.c) on the reference objects: the
+    # A side of tests/test_dropin.py's A/B run against oracle/_ref/dropin/
+    for f in $S/joins/sortmergejoin_multipass.c $S/joins/sortmergejoin_mpsm.c $S/main.c; do
+        $CXX $FLAGS $def $INC -c "$f" -o "$objdir/$(basename "$f" .c).o"
+    done
+    $CXX $objs "$objdir/sortmergejoin_multipass.o" "$objdir/sortmergejoin_mpsm.o" \
+        "$objdir/main.o" -o "$HERE/_ref/sortmergejoins_ref$w" -lpthread -lm
 done
 echo "[build_ref] built oracle/_ref from $REF"

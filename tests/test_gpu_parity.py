@@ -189,6 +189,9 @@ def test_sortmergejoin_count(libs, oracles, width, kind, nr, ns):
         assert lib.sortmergejoin_multiway(R, S, nthreads=nthr) == exp
     assert lib.sortmergejoin_multiway(R, S, nthreads=3) is None  # pow-2 check
     assert lib.sortmergejoin_multiway(R, S, nthreads=2, mpsm=True) == exp
+    # m-pass (src/joins/sortmergejoin_multipass.c): sort both, then one scan
+    assert lib.sortmergejoin_multiway(R, S, nthreads=4, algo="m-pass") == exp
+    assert lib.sortmergejoin_multiway(R, S, nthreads=3, algo="m-pass") is None
 
 
 @pytest.mark.parametrize("kind,nr,ns", JOIN_CASES[2:])
