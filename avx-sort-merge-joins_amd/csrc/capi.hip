@@ -381,28 +381,44 @@ void scalarsort_tuples(tuple_t** inputptr, tuple_t** outputptr,
 }  // extern "C"
 
 // ---- int64 / int32 item sorts: items viewed as tuples with key = value
+// The AVX int64 entry points order their items as IEEE doubles (the
+// networks' _mm256_min_pd/_max_pd, reference src/avxsort/avxcommon.h:79-190):
+// sign-magnitude order for every non-NaN pattern, which this fork's (key, ptr)
+// carriers rely on (SetKeyInt, avxcommon.h:205-213).  fp64_ord maps a pattern
+// to a signed int64 of that order and is its own inverse; the scalar twins
+// keep plain int64 order (std::sort, src/scalarsort/scalarsort.c:23-30).
+__device__ __forceinline__ int64_t fp64_ord(int64_t x) {
+    return x ^ ((x >> 63) & INT64_MAX);
+}
+__global__ void k_fp64_ord(const int64_t* __restrict__ a, int64_t* __restrict__ b,
+                           uint64_t n) {
+    const uint64_t s = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += s)
+        b[i] = fp64_ord(a[i]);
+}
+
 __global__ void k_expand_i64(const int64_t* __restrict__ a, Tup* __restrict__ t,
-                             uint64_t n) {
+                             uint64_t n, bool fp64) {
     const uint64_t s = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += s) {
 #ifdef KEY_8B
         Tup x;
-        x.key = a[i];
+        x.key = fp64 ? fp64_ord(a[i]) : a[i];
         x.payload = 0;
         t[i] = x;
 #else
-        t[i] = (uint64_t)a[i];
+        t[i] = (uint64_t)(fp64 ? fp64_ord(a[i]) : a[i]);
 #endif
     }
 }
 __global__ void k_compact_i64(const Tup* __restrict__ t, int64_t* __restrict__ a,
-                              uint64_t n) {
+                              uint64_t n, bool fp64) {
     const uint64_t s = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += s) {
 #ifdef KEY_8B
-        a[i] = t[i].key;
+        a[i] = fp64 ? fp64_ord(t[i].key) : t[i].key;
 #else
-        a[i] = (int64_t)t[i];
+        a[i] = fp64 ? fp64_ord((int64_t)t[i]) : (int64_t)t[i];
 #endif
     }
 }
@@ -432,13 +448,30 @@ static uint32_t grid_n(uint64_t n) {
     return (uint32_t)(b < 4096 ? (b ? b : 1) : 4096);
 }
 
-static void sort_int64_into(const int64_t* inp, int64_t* outp, uint64_t n) {
+static void sort_int64_into(const int64_t* inp, int64_t* outp, uint64_t n, bool fp64) {
     if (n == 0) return;
-#ifndef KEY_8B
-    sort_tuples_into(inp, outp, n);  // an 8-byte tuple is an int64 word
-#else
     Ctx& c = ctx();
     const bool din = is_device_ptr(inp), dout = is_device_ptr(outp);
+#ifndef KEY_8B
+    if (!fp64) {
+        sort_tuples_into(inp, outp, n);  // an 8-byte tuple is an int64 word
+        return;
+    }
+    // map to int64 order, sort the words as tuples, map back
+    int64_t* t = (int64_t*)c.ws.scratch("api_i64_t", n * 8);
+    int64_t* u = (int64_t*)c.ws.scratch("api_i64_u", n * 8);
+    const int64_t* src = inp;
+    if (!din) {
+        SMJ_CHECK(hipMemcpyAsync(t, inp, n * 8, hipMemcpyHostToDevice, c.st));
+        src = t;
+    }
+    hipLaunchKernelGGL(k_fp64_ord, dim3(grid_n(n)), dim3(256), 0, c.st, src, t, n);
+    device_sort(&c.ws, (const Tup*)t, n, (Tup*)u, c.st);
+    int64_t* dst = dout ? outp : t;
+    hipLaunchKernelGGL(k_fp64_ord, dim3(grid_n(n)), dim3(256), 0, c.st, u, dst, n);
+    if (!dout) SMJ_CHECK(hipMemcpyAsync(outp, t, n * 8, hipMemcpyDeviceToHost, c.st));
+    sync();
+#else
     int64_t* di = (int64_t*)inp;
     int64_t* dout_p = outp;
     if (!din) {
@@ -448,9 +481,9 @@ static void sort_int64_into(const int64_t* inp, int64_t* outp, uint64_t n) {
     if (!dout) dout_p = (int64_t*)c.ws.scratch("api_i64_out", n * 8);
     Tup* t = (Tup*)c.ws.scratch("api_i64_t", n * sizeof(Tup));
     Tup* u = (Tup*)c.ws.scratch("api_i64_u", n * sizeof(Tup));
-    hipLaunchKernelGGL(k_expand_i64, dim3(grid_n(n)), dim3(256), 0, c.st, di, t, n);
+    hipLaunchKernelGGL(k_expand_i64, dim3(grid_n(n)), dim3(256), 0, c.st, di, t, n, fp64);
     device_sort(&c.ws, t, n, u, c.st);
-    hipLaunchKernelGGL(k_compact_i64, dim3(grid_n(n)), dim3(256), 0, c.st, u, dout_p, n);
+    hipLaunchKernelGGL(k_compact_i64, dim3(grid_n(n)), dim3(256), 0, c.st, u, dout_p, n, fp64);
     if (!dout)
         SMJ_CHECK(hipMemcpyAsync(outp, dout_p, n * 8, hipMemcpyDeviceToHost, c.st));
     sync();
@@ -481,11 +514,11 @@ static void sort_int32_into(const int32_t* inp, int32_t* outp, uint64_t n) {
 extern "C" {
 
 void avxsort_int64(int64_t** inputptr, int64_t** outputptr, uint64_t nitems) {
-    sort_int64_into(*inputptr, *outputptr, nitems);
+    sort_int64_into(*inputptr, *outputptr, nitems, true);
 }
 void avxsortmultiway_int64(int64_t** inputptr, int64_t** outputptr,
                            uint64_t nitems) {
-    sort_int64_into(*inputptr, *outputptr, nitems);
+    sort_int64_into(*inputptr, *outputptr, nitems, true);
 }
 void avxsort_int32(int32_t** inputptr, int32_t** outputptr, uint64_t nitems) {
     sort_int32_into(*inputptr, *outputptr, nitems);
@@ -493,7 +526,7 @@ void avxsort_int32(int32_t** inputptr, int32_t** outputptr, uint64_t nitems) {
 void scalarsort_int64(int64_t** inputptr, int64_t** outputptr, uint64_t nitems) {
     int64_t* in = *inputptr;
     int64_t* out = *outputptr;
-    sort_int64_into(in, in, nitems);
+    sort_int64_into(in, in, nitems, false);
     *inputptr = out;
     *outputptr = in;
 }
@@ -533,11 +566,11 @@ uint64_t scalar_merge_tuples(tuple_t* const inA, tuple_t* const inB,
 }
 
 static uint64_t merge_int64_common(const int64_t* A, const int64_t* B, int64_t* O,
-                                   uint64_t la, uint64_t lb) {
+                                   uint64_t la, uint64_t lb, bool fp64) {
 #ifndef KEY_8B
-    return merge_tuples_common(A, B, O, la, lb);
-#else
-    // 16-byte build: widen, merge, narrow
+    if (!fp64) return merge_tuples_common(A, B, O, la, lb);
+#endif
+    // stage, map to int64 order (or widen to 16-byte tuples), merge, map back
     Ctx& c = ctx();
     const uint64_t n = la + lb;
     if (n == 0) return 0;
@@ -546,28 +579,34 @@ static uint64_t merge_int64_common(const int64_t* A, const int64_t* B, int64_t* 
     int64_t* dn = (int64_t*)c.ws.scratch("api_mi_o", n * 8);
     if (la) SMJ_CHECK(hipMemcpyAsync(da, A, la * 8, hipMemcpyDefault, c.st));
     if (lb) SMJ_CHECK(hipMemcpyAsync(db, B, lb * 8, hipMemcpyDefault, c.st));
+#ifndef KEY_8B
+    if (la) hipLaunchKernelGGL(k_fp64_ord, dim3(grid_n(la)), dim3(256), 0, c.st, da, da, la);
+    if (lb) hipLaunchKernelGGL(k_fp64_ord, dim3(grid_n(lb)), dim3(256), 0, c.st, db, db, lb);
+    merge2((const Tup*)da, la, (const Tup*)db, lb, (Tup*)dn, c.st);
+    hipLaunchKernelGGL(k_fp64_ord, dim3(grid_n(n)), dim3(256), 0, c.st, dn, dn, n);
+#else
     Tup* ta = (Tup*)c.ws.scratch("api_mi_ta", (la ? la : 1) * sizeof(Tup));
     Tup* tb = (Tup*)c.ws.scratch("api_mi_tb", (lb ? lb : 1) * sizeof(Tup));
     Tup* to = (Tup*)c.ws.scratch("api_mi_to", n * sizeof(Tup));
-    if (la) hipLaunchKernelGGL(k_expand_i64, dim3(grid_n(la)), dim3(256), 0, c.st, da, ta, la);
-    if (lb) hipLaunchKernelGGL(k_expand_i64, dim3(grid_n(lb)), dim3(256), 0, c.st, db, tb, lb);
+    if (la) hipLaunchKernelGGL(k_expand_i64, dim3(grid_n(la)), dim3(256), 0, c.st, da, ta, la, fp64);
+    if (lb) hipLaunchKernelGGL(k_expand_i64, dim3(grid_n(lb)), dim3(256), 0, c.st, db, tb, lb, fp64);
     merge2(ta, la, tb, lb, to, c.st);
-    hipLaunchKernelGGL(k_compact_i64, dim3(grid_n(n)), dim3(256), 0, c.st, to, dn, n);
+    hipLaunchKernelGGL(k_compact_i64, dim3(grid_n(n)), dim3(256), 0, c.st, to, dn, n, fp64);
+#endif
     SMJ_CHECK(hipMemcpyAsync(O, dn, n * 8, hipMemcpyDefault, c.st));
     sync();
     return n;
-#endif
 }
 
 uint64_t avx_merge_int64(int64_t* const inA, int64_t* const inB,
                          int64_t* const outp, const uint64_t lenA,
                          const uint64_t lenB) {
-    return merge_int64_common(inA, inB, outp, lenA, lenB);
+    return merge_int64_common(inA, inB, outp, lenA, lenB, true);
 }
 uint64_t scalar_merge_int64(int64_t* const inA, int64_t* const inB,
                             int64_t* const outp, const uint64_t lenA,
                             const uint64_t lenB) {
-    return merge_int64_common(inA, inB, outp, lenA, lenB);
+    return merge_int64_common(inA, inB, outp, lenA, lenB, false);
 }
 
 static uint64_t multiway_common(tuple_t* output, relation_t** parts,
@@ -663,6 +702,137 @@ uint64_t merge_join(tuple_t* rtuples, tuple_t* stuples, const uint64_t numR,
     SMJ_CHECK(hipMemcpyAsync(&h, cnt, 8, hipMemcpyDeviceToHost, c.st));
     sync();
     return h;
+}
+
+uint64_t merge_join_interpolation(tuple_t* rtuples, tuple_t* stuples,
+                                  const uint64_t numR, const uint64_t numS,
+                                  void* output) {
+    // the interpolation search only picks the CPU scan's start; the device
+    // merge-path count needs none
+    return merge_join(rtuples, stuples, numR, numS, output);
+}
+
+// joincommon.c:29-212.  The orchestration of the reference's T join threads,
+// kept for drivers that bring their own join thread (tputbench.c:124-144).
+// Differences: threads are not pinned (their work is device work; the
+// reference's cpu_mapping.c belongs to the driver), and the chunk sizes are
+// computed in 64 bits before they land in the int32 fields of arg_t.
+static void* host_alloc64(size_t bytes) {
+    void* p = nullptr;
+    if (posix_memalign(&p, CACHE_LINE_SIZE, bytes ? bytes : CACHE_LINE_SIZE)) {
+        perror("[ERROR] smj: posix_memalign");
+        exit(EXIT_FAILURE);
+    }
+    return p;
+}
+
+result_t* sortmergejoin_initrun(relation_t* relR, relation_t* relS,
+                                joinconfig_t* joincfg,
+                                void* (*jointhread)(void*)) {
+    const int T = joincfg->NTHREADS;
+    const int F = joincfg->PARTFANOUT;
+    if (T <= 0) {
+        fprintf(stdout, "[ERROR] NTHREADS must be positive.\n");
+        return 0;
+    }
+    const uint64_t nR = relR->num_tuples, nS = relS->num_tuples;
+    const size_t pad = RELATION_PADDING(T, F);
+    tuple_t* tmpPR = (tuple_t*)host_alloc64(nR * sizeof(tuple_t) + pad);
+    tuple_t* tmpPS = (tuple_t*)host_alloc64(nS * sizeof(tuple_t) + pad);
+    tuple_t* tmpSR = (tuple_t*)host_alloc64(nR * sizeof(tuple_t) + pad);
+    tuple_t* tmpSS = (tuple_t*)host_alloc64(nS * sizeof(tuple_t) + pad);
+    relationpair_t** chunks = (relationpair_t**)calloc(T, sizeof(relationpair_t*));
+    uint32_t** histR = (uint32_t**)calloc(T, sizeof(uint32_t*));
+    // indexed by the driver's NUMA region id (< T, or 0 without libnuma)
+    tuple_t** shared = (tuple_t**)calloc(T < 64 ? 64 : T, sizeof(tuple_t*));
+    arg_t* args = (arg_t*)host_alloc64(sizeof(arg_t) * T);
+    memset(args, 0, sizeof(arg_t) * T);
+    std::vector<pthread_t> tid(T);
+    pthread_barrier_t barrier;
+    if (pthread_barrier_init(&barrier, NULL, T) != 0) {
+        printf("[ERROR] Couldn't create the barrier\n");
+        exit(EXIT_FAILURE);
+    }
+    pthread_attr_t attr;
+    pthread_attr_init(&attr);
+    size_t stack = 0;
+    pthread_attr_getstacksize(&attr, &stack);
+    const size_t kStack = 32u << 20;  // joincommon.c:26 REQUIRED_STACK_SIZE
+    if (stack < kStack && pthread_attr_setstacksize(&attr, kStack)) {
+        perror("[ERROR] pthread stack size could not be set!");
+        exit(0);
+    }
+    const uint64_t perR = nR / T, perS = nS / T;
+    const uint64_t cpad = CACHELINEPADDING(F);
+    result_t* res = (result_t*)malloc(sizeof(result_t));
+    res->resultlist = (threadresult_t*)calloc(T, sizeof(threadresult_t));
+    for (int i = 0; i < T; i++) {
+        arg_t& a = args[i];
+        a.relR = relR->tuples + i * perR;
+        a.relS = relS->tuples + i * perS;
+        a.tmp_partR = tmpPR + i * (perR + cpad);
+        a.tmp_partS = tmpPS + i * (perS + cpad);
+        a.tmp_sortR = tmpSR + i * perR;
+        a.tmp_sortS = tmpSS + i * perS;
+        a.numR = (int32_t)(i == T - 1 ? nR - i * perR : perR);
+        a.numS = (int32_t)(i == T - 1 ? nS - i * perS : perS);
+        a.my_tid = i;
+        a.nthreads = T;
+        a.joincfg = joincfg;
+        a.barrier = &barrier;
+        a.threadrelchunks = chunks;
+        a.sharedmergebuffer = shared;
+        a.histR = histR;
+        a.tmpRglobal = tmpPR;
+        a.totalR = nR;
+#ifdef JOIN_MATERIALIZE
+        a.threadresult = &res->resultlist[i];
+#endif
+        const int rv = pthread_create(&tid[i], &attr, jointhread, (void*)&a);
+        if (rv) {
+            printf("[ERROR] return code from pthread_create() is %d\n", rv);
+            exit(-1);
+        }
+    }
+    int64_t total = 0;
+    for (int i = 0; i < T; i++) {
+        pthread_join(tid[i], NULL);
+        total += args[i].result;
+        res->resultlist[i].nresults = args[i].result;
+    }
+    res->totalresults = total;
+    res->nthreads = T;
+    // joincommon.c:176-199, the same lines from args[0]'s timers
+    const arg_t& a0 = args[0];
+    fprintf(stdout, "Total, Partitioning, Sort, First-Merge, Merge, Join\n");
+    fprintf(stdout, "%llu, %llu, %llu, %llu, %llu, %llu\n",
+            (unsigned long long)a0.join, (unsigned long long)a0.part,
+            (unsigned long long)a0.sort, (unsigned long long)a0.mergedelta,
+            (unsigned long long)a0.merge, (unsigned long long)a0.join);
+    fprintf(stdout, "Perstage: ");
+    fflush(stdout);
+    fprintf(stderr, "%llu, %llu, %llu, %llu, %llu, ", (unsigned long long)a0.part,
+            (unsigned long long)(a0.sort - a0.part),
+            (unsigned long long)(a0.mergedelta - a0.sort),
+            (unsigned long long)(a0.merge - a0.mergedelta),
+            (unsigned long long)(a0.join - a0.merge));
+    fflush(stderr);
+    fprintf(stdout, "\n");
+    print_timing(nS, &args[0].start, &args[0].end, stderr);
+    const bool owned = args[0].tmp_partR != 0;
+    free(chunks);
+    free(shared);
+    free(histR);
+    free(args);
+    if (owned) {
+        free(tmpPR);
+        free(tmpPS);
+        free(tmpSR);
+        free(tmpSS);
+    }
+    pthread_attr_destroy(&attr);
+    pthread_barrier_destroy(&barrier);
+    return res;
 }
 
 static result_t* join_api(relation_t* relR, relation_t* relS,

@@ -204,6 +204,14 @@ class Library:
         getattr(self.lib, fn)(C.byref(pa), C.byref(pb), len(a))
         return (b if pb.value == b.ctypes.data else a).copy()
 
+    def merge_int64(self, a, b, fn="avx_merge_int64") -> np.ndarray:
+        a = np.ascontiguousarray(a, dtype=np.int64)
+        b = np.ascontiguousarray(b, dtype=np.int64)
+        out = np.zeros(len(a) + len(b), np.int64)
+        n = getattr(self.lib, fn)(_ptr(a), _ptr(b), _ptr(out), len(a), len(b))
+        assert n == len(out)
+        return out
+
     def avx_merge_tuples(self, a, b, fn="avx_merge_tuples") -> np.ndarray:
         a = np.ascontiguousarray(a, dtype=self.dtype)
         b = np.ascontiguousarray(b, dtype=self.dtype)

@@ -40,6 +40,7 @@
 #include <stdio.h>
 #include <inttypes.h>
 #include <sys/time.h>
+#include <pthread.h>
 
 #ifdef __cplusplus
 extern "C" {
@@ -241,6 +242,61 @@ uint64_t merge_join(tuple_t * rtuples, tuple_t * stuples, const uint64_t numR,
 void print_timing(uint64_t numtuples, struct timeval * start,
                   struct timeval * end, FILE * out);
 #endif
+
+/* joincommon.c (not in joincommon.h's prose): merge_join with an
+ * interpolation search for the start; same count as merge_join. */
+uint64_t merge_join_interpolation(tuple_t * rtuples, tuple_t * stuples,
+                                  const uint64_t numR, const uint64_t numS,
+                                  void * output);
+
+/* The thread scaffolding of the reference joins (joincommon.h:40-44,
+ * 105-155), layout-identical so that drivers with their own join thread
+ * (tputbench.c:124-144) run unchanged on sortmergejoin_initrun below. */
+#ifndef SMJ_ARG_T
+#define SMJ_ARG_T
+typedef struct arg_t arg_t;
+typedef struct relationpair_t relationpair_t;
+struct arg_t {
+    tuple_t *  relR;
+    tuple_t *  relS;
+    tuple_t *  tmp_partR;   /* partitioning output, per thread */
+    tuple_t *  tmp_partS;
+    tuple_t *  tmp_sortR;   /* sorting output, per thread */
+    tuple_t *  tmp_sortS;
+    int32_t numR;
+    int32_t numS;
+    int32_t my_tid;
+    int     nthreads;
+    joinconfig_t * joincfg;
+    pthread_barrier_t * barrier;
+    int64_t result;
+    relationpair_t ** threadrelchunks;
+    tuple_t ** sharedmergebuffer;
+    uint32_t ** histR;      /* mpsm-specific */
+    tuple_t * tmpRglobal;
+    uint64_t totalR;
+#ifdef JOIN_MATERIALIZE
+    threadresult_t * threadresult;
+#endif
+    struct timeval start, end;
+    uint64_t part, sort, mergedelta, merge, join;
+} __attribute__((aligned(CACHE_LINE_SIZE)));
+struct relationpair_t {
+    relation_t R;
+    relation_t S;
+};
+#endif /* SMJ_ARG_T */
+
+/* joincommon.c:29-212: allocates the per-thread temporaries (partition and
+ * sort outputs, RELATION_PADDING behind each), slices R and S into T
+ * contiguous chunks, runs `jointhread` on T pthreads sharing one barrier,
+ * sums args[i].result into a malloc'd result_t and prints the stats lines
+ * from args[0]'s timers.  The join thread's own calls (partition, sort,
+ * merge, merge_join) are this library's device entry points.  Host-side
+ * orchestration only: no tuple is touched here. */
+result_t * sortmergejoin_initrun(relation_t * relR, relation_t * relS,
+                                 joinconfig_t * joincfg,
+                                 void * (*jointhread)(void *));
 
 /* sortmergejoin_multiway.c:50-61: m-way sort-merge join. Returns a malloc'd
  * result_t (caller frees resultlist and the struct, main.c:629-632) whose

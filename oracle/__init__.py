@@ -119,6 +119,20 @@ class Oracle(_Lib):
         self.fn("sort_int64", None, _P, _I64)(_ptr(b), len(b))
         return b
 
+    def sort_int64_fp64(self, a: np.ndarray) -> np.ndarray:
+        """avxsort_int64's order: the items compared as IEEE doubles."""
+        b = np.ascontiguousarray(a, dtype=np.int64).copy()
+        self.fn("sort_int64_fp64", None, _P, _I64)(_ptr(b), len(b))
+        return b
+
+    def merge_int64_fp64(self, a: np.ndarray, b: np.ndarray) -> np.ndarray:
+        a = np.ascontiguousarray(a, dtype=np.int64)
+        b = np.ascontiguousarray(b, dtype=np.int64)
+        out = np.zeros(len(a) + len(b), np.int64)
+        self.fn("merge_int64_fp64", _U64, _P, _P, _P, _U64, _U64)(
+            _ptr(a), _ptr(b), _ptr(out), len(a), len(b))
+        return out
+
     def merge(self, a: np.ndarray, b: np.ndarray) -> np.ndarray:
         out = np.zeros(len(a) + len(b), self.dtype)
         self.fn("merge_tuples", _U64, _P, _P, _P, _U64, _U64)(
@@ -209,6 +223,16 @@ class Reference(_Lib):
         res = np.zeros(len(v), np.int64)
         self.fn("avxsort_int64", None, _P, _P, _U64, _P)(_ptr(a), _ptr(b), len(v), _ptr(res))
         return res
+
+    def merge_int64(self, a, b):
+        A = np.zeros(len(a) + 16, np.int64)[: len(a)]
+        A[:] = a
+        B = np.zeros(len(b) + 16, np.int64)[: len(b)]
+        B[:] = b
+        out = np.zeros(len(a) + len(b) + 16, np.int64)[: len(a) + len(b)]
+        self.fn("avx_merge_int64", _U64, _P, _P, _P, _U64, _U64)(
+            _ptr(A), _ptr(B), _ptr(out), len(a), len(b))
+        return np.array(out)
 
     def merge(self, a, b, fn="avx_merge_tuples"):
         A = self._aligned(len(a))

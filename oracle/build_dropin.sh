@@ -19,6 +19,7 @@ OUT="$HERE/_ref/dropin"
 LIB="$ROOT/avx-sort-merge-joins_amd/lib"
 mkdir -p "$OUT"
 CC="${CC:-gcc}"
+CXX="${CXX:-g++}"
 INC="-I$ROOT/include/compat -I$ROOT/tests/compat_check -I$REF -I$S -I$S/util -I$S/datagen -I$T"
 FLAGS="-O2 -std=gnu99 -D_GNU_SOURCE -w"
 RPATH='-Wl,-rpath,$ORIGIN/../../../avx-sort-merge-joins_amd/lib'
@@ -29,13 +30,23 @@ build() {  # name width sources...
     if [ "$w" = 16 ]; then def="-DKEY_8B"; lib="-lsmj_hip_k8"; fi
     $CC $FLAGS $def $INC "$@" -L"$LIB" $lib $RPATH -lpthread -lm -o "$OUT/$name$w"
 }
+buildxx() {  # C++ drivers (sortbench.c includes <algorithm>)
+    local name=$1 w=$2; shift 2
+    local def="" lib="-lsmj_hip"
+    if [ "$w" = 16 ]; then def="-DKEY_8B"; lib="-lsmj_hip_k8"; fi
+    $CXX -x c++ -O2 -D_GNU_SOURCE -w $def $INC "$@" -x none -L"$LIB" $lib $RPATH \
+        -lpthread -lm -o "$OUT/$name$w"
+}
 for w in 8 16; do
     build check_partitioning $w "$T/check_partitioning.c" "$T/testutil.c" $GEN
     build check_scalarsort $w "$T/check_scalarsort.c" "$T/testutil.c"
     build bench_partitioning $w "$S/bench/partitioningbench.c" $GEN "$S/util/memalloc.c"
     build bench_multiwaymerge $w "$S/bench/multiwaymergebench.c" "$T/testutil.c"
     build sortmergejoins $w "$S/main.c" $GEN "$S/util/memalloc.c" "$S/util/numa_shuffle.c"
+    build tputbench $w "$S/bench/tputbench.c" $GEN "$S/util/memalloc.c" "$S/util/numa_shuffle.c"
 done
+# sortbench.c sorts 8-byte items with avxsort_int64/avxsortmultiway_int64
+buildxx bench_sort 8 "$S/bench/sortbench.c" "$T/testutil.c" $GEN
 # avxsort only exists for 8-byte tuples (the reference forces scalar for 16 B)
 build check_avxsort 8 "$T/check_avxsort.c" "$T/testutil.c"
 echo "[build_dropin] built $(ls "$OUT" | wc -l) binaries in oracle/_ref/dropin"

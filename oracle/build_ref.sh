@@ -54,5 +54,7 @@ for w in 8 16; do
     done
     $CXX $objs "$objdir/sortmergejoin_multipass.o" "$objdir/sortmergejoin_mpsm.o" \
         "$objdir/main.o" -o "$HERE/_ref/sortmergejoins_ref$w" -lpthread -lm
+    $CXX $FLAGS $def $INC -c "$S/bench/tputbench.c" -o "$objdir/tputbench.o"
+    $CXX $objs "$objdir/tputbench.o" -o "$HERE/_ref/tputbench_ref$w" -lpthread -lm
 done
 echo "[build_ref] built oracle/_ref from $REF"

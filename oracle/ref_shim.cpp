@@ -118,6 +118,11 @@ uint64_t ref_avx_merge_tuples(tuple_t* A, tuple_t* B, tuple_t* out,
     return avx_merge_tuples(A, B, out, la, lb);
 }
 
+uint64_t ref_avx_merge_int64(int64_t* A, int64_t* B, int64_t* out,
+                             uint64_t la, uint64_t lb) {
+    return avx_merge_int64(A, B, out, la, lb);
+}
+
 uint64_t ref_scalar_merge_tuples(tuple_t* A, tuple_t* B, tuple_t* out,
                                  uint64_t la, uint64_t lb) {
     return scalar_merge_tuples(A, B, out, la, lb);

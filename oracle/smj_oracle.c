@@ -222,6 +222,30 @@ static int i64_cmp(const void *a, const void *b) {
 }
 void orc_sort_int64(int64_t *a, int64_t n) { qsort(a, (size_t)n, 8, i64_cmp); }
 
+/* The AVX int64 entry points (avxsort_int64, src/avxsort/avxsort.c:229-245;
+ * avx_merge_int64, src/merge/merge.c:27-65) compare the items as IEEE doubles
+ * (_mm256_min_pd/_max_pd, src/avxsort/avxcommon.h:79-190; the scalar merge
+ * step IFELSECONDMOVE, :186-193).  For every non-NaN bit pattern that is
+ * sign-magnitude order, which this fork's (key, ptr) carriers rely on
+ * (SetKeyInt, avxcommon.h:205-213: sign | |key| << 20 | ptr).  fp64_ord maps
+ * a pattern to a signed int64 with that order (-0 sorts before +0; the
+ * networks treat them as equal). */
+static int64_t fp64_ord(int64_t x) { return x < 0 ? x ^ INT64_MAX : x; }
+static int i64_fp_cmp(const void *a, const void *b) {
+    int64_t x = fp64_ord(*(const int64_t *)a), y = fp64_ord(*(const int64_t *)b);
+    return x < y ? -1 : (x > y);
+}
+void orc_sort_int64_fp64(int64_t *a, int64_t n) { qsort(a, (size_t)n, 8, i64_fp_cmp); }
+uint64_t orc_merge_int64_fp64(const int64_t *A, const int64_t *B, int64_t *out,
+                              uint64_t la, uint64_t lb) {
+    uint64_t i = 0, j = 0, k = 0;
+    while (i < la && j < lb)
+        out[k++] = fp64_ord(A[i]) <= fp64_ord(B[j]) ? A[i++] : B[j++];
+    while (i < la) out[k++] = A[i++];
+    while (j < lb) out[k++] = B[j++];
+    return k;
+}
+
 /* src/merge/merge.c:67-103 scalar_merge_tuples (2-way merge) */
 uint64_t orc_merge_tuples(const tuple_t *A, const tuple_t *B, tuple_t *out,
                           uint64_t la, uint64_t lb) {

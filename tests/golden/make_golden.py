@@ -8,7 +8,8 @@ and the reference's outputs), loaded with numpy.load(allow_pickle=False) by
 tests/test_oracle.py, which pins oracle/smj_oracle.c (the CPU restatement) to
 them.  Nothing here runs on the GPU box.
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py           # golden_w8/w16.npz
+    python tests/golden/make_golden.py --int64   # golden_int64.npz
 """
 import os
 import re
@@ -152,8 +153,57 @@ def main():
         print(f"wrote {path} ({os.path.getsize(path) / 1e6:.2f} MB, {len(out)} arrays)")
 
 
+def carriers(rng, n):
+    """This fork's (key, ptr) int64 carriers with signed keys, built as
+    src/bench/sortbench.c:267-298 does (gen_random_int, SetPtr, SetKeyInt):
+    sign bit | |key| << 20 | (i & 0xFFFFF)."""
+    key = rng.integers(-(2 ** 31 - 1), 2 ** 31 - 1, n)
+    w = (np.abs(key).astype(np.int64) << 20) | (np.arange(n, dtype=np.int64) & 0xFFFFF)
+    return np.where(key < 0, w | np.int64(-2 ** 63), w).astype(np.int64)
+
+
+def non_nan_words(rng, n):
+    """Random int64 patterns that are no NaN and not -0 as doubles."""
+    v = rng.integers(-(1 << 63), (1 << 63) - 1, 2 * n, dtype=np.int64)
+    v = v[(((v >> 52) & 0x7FF) != 0x7FF) & (v != np.int64(-2 ** 63))]
+    return v[:n]
+
+
+def int64_fixtures():
+    """avxsort_int64 / avx_merge_int64 on signed items: the AVX networks order
+    int64 items as IEEE doubles (sign-magnitude), not as integers."""
+    ref = oracle.Reference(8)
+    rng = np.random.default_rng(2012)
+    out = {}
+
+    def perm(inp, res):
+        # the reference's output as indices into the input (distinct items)
+        order = {int(x): i for i, x in enumerate(inp)}
+        assert len(order) == len(inp)
+        return np.array([order[int(x)] for x in res], np.uint32)
+
+    for n in (100, 16384 + 255, 2 * 16384 + 77):
+        v = carriers(rng, n)
+        out[f"carrier_in_{n}"] = v
+        out[f"carrier_perm_{n}"] = perm(v, ref.sort_int64(v))
+    v = non_nan_words(rng, 5000)
+    out["words_in"] = v
+    out["words_perm"] = perm(v, ref.sort_int64(v))
+    a = ref.sort_int64(carriers(rng, 1500))
+    b = ref.sort_int64(carriers(rng, 2001))
+    b = b[~np.isin(b, a)]
+    out["merge_a"], out["merge_b"] = a, b
+    ab = np.concatenate([a, b])
+    out["merge_perm"] = perm(ab, ref.merge_int64(a, b))
+    path = os.path.join(HERE, "golden_int64.npz")
+    np.savez_compressed(path, **out)
+    print(f"wrote {path} ({os.path.getsize(path) / 1e6:.2f} MB, {len(out)} arrays)")
+
+
 if __name__ == "__main__":
     if len(sys.argv) == 5 and sys.argv[1] == "--join-case":
         join_case(*map(int, sys.argv[2:]))
+    elif len(sys.argv) == 2 and sys.argv[1] == "--int64":
+        int64_fixtures()
     else:
         main()

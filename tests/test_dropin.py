@@ -102,3 +102,29 @@ def test_reference_multiwaymerge_bench(w):
     assert r.returncode == 0, r.stderr[-2000:]
     assert "Output relation is now sorted" in r.stderr, r.stderr[-2000:]
     assert "not sorted" not in r.stderr
+
+
+@pytest.mark.gpu
+def test_reference_sortbench_posneg():
+    """src/bench/sortbench.c unchanged: this fork's signed (key, ptr)
+    carriers through avxsort_int64, checked by the bench itself."""
+    r = run([binary("bench_sort8"), "1", "0", "1"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "[dbg] PASS" in r.stdout, r.stdout[-3000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w", [8, 16])
+@pytest.mark.parametrize("nthreads", [1, 2, 4])
+def test_tputbench_ab_against_reference(w, nthreads):
+    """src/bench/tputbench.c unchanged: its own join thread (partition, sort,
+    multiway merge, merge_join per thread) on sortmergejoin_initrun.  A/B
+    against the same driver on the reference's objects; T threads call the
+    library concurrently."""
+    ref = os.path.join(ROOT, "oracle", "_ref", f"tputbench_ref{w}")
+    if not os.path.exists(ref):
+        pytest.skip("reference tputbench not built")
+    exe = binary(f"tputbench{w}")
+    args = ["-a", "tputbench", "-n", str(nthreads), "-r", "1000000", "-s", "1000000",
+            "--non-unique"] + SCALAR[w]
+    assert results(run([exe] + args)) == results(run([ref] + args))

@@ -106,15 +106,60 @@ def test_sort_zipf_skew(libs, oracles, width):
     assert np.array_equal(got, orc.sort(t))
 
 
+def non_nan_words(rng, n):
+    """int64 patterns that are neither NaN nor -0 as IEEE doubles."""
+    v = rng.integers(-(1 << 63), (1 << 63) - 1, 2 * n, dtype=np.int64)
+    v = v[(((v >> 52) & 0x7FF) != 0x7FF) & (v != np.int64(-2 ** 63))]
+    return v[:n]
+
+
 def test_sort_int64_int32(libs, oracles, width):
+    """avx* int64 entry points: IEEE-double order, like the reference's AVX
+    networks (oracle pinned in test_oracle.py); scalar ones: integer order."""
     orc, lib = oracles[width], libs[width]
     rng = np.random.default_rng(11)
-    v = rng.integers(-(1 << 62), 1 << 62, 300001, dtype=np.int64)
-    for fn in ("avxsort_int64", "avxsortmultiway_int64", "scalarsort_int64"):
-        assert np.array_equal(lib.sort_int(v, fn), np.sort(v)), fn
+    v = non_nan_words(rng, 300001)
+    for fn in ("avxsort_int64", "avxsortmultiway_int64"):
+        assert np.array_equal(lib.sort_int(v, fn), orc.sort_int64_fp64(v)), fn
+    assert np.array_equal(lib.sort_int(v, "scalarsort_int64"), np.sort(v))
     w = rng.integers(-(1 << 31), (1 << 31) - 1, 100003, dtype=np.int64).astype(np.int32)
     for fn in ("avxsort_int32", "scalarsort_int32"):
         assert np.array_equal(lib.sort_int(w, fn), np.sort(w)), fn
+
+
+def test_int64_fp64_golden(libs, width):
+    """This fork's signed (key, ptr) carriers (src/bench/sortbench.c:267-298)
+    through avxsort_int64 / avx_merge_int64: the reference's own outputs."""
+    import os
+    from conftest import ROOT
+    lib = libs[width]
+    with np.load(os.path.join(ROOT, "tests", "golden", "golden_int64.npz"),
+                 allow_pickle=False) as d:
+        g = {k: d[k] for k in d.files}
+    for k in g:
+        if k.startswith("carrier_in_"):
+            n = k.rsplit("_", 1)[1]
+            v = g[k]
+            want = v[g[f"carrier_perm_{n}"]]
+            for fn in ("avxsort_int64", "avxsortmultiway_int64"):
+                assert np.array_equal(lib.sort_int(v, fn), want), (fn, n)
+    v = g["words_in"]
+    assert np.array_equal(lib.sort_int(v), v[g["words_perm"]])
+    a, b = g["merge_a"], g["merge_b"]
+    assert np.array_equal(lib.merge_int64(a, b),
+                          np.concatenate([a, b])[g["merge_perm"]])
+
+
+@pytest.mark.parametrize("la,lb", [(0, 0), (0, 9), (5, 0), (70000, 33333)])
+def test_merge_int64(libs, oracles, width, la, lb):
+    orc, lib = oracles[width], libs[width]
+    rng = np.random.default_rng(la + 7 * lb)
+    a = orc.sort_int64_fp64(non_nan_words(rng, la))
+    b = orc.sort_int64_fp64(non_nan_words(rng, lb))
+    assert np.array_equal(lib.merge_int64(a, b), orc.merge_int64_fp64(a, b))
+    a, b = np.sort(a), np.sort(b)
+    assert np.array_equal(lib.merge_int64(a, b, "scalar_merge_int64"),
+                          np.sort(np.concatenate([a, b])))
 
 
 # ------------------------------------------------------------------ merging

@@ -156,3 +156,39 @@ def test_live_reference_partition_sort(w, oracles):
         np.testing.assert_array_equal(o1[: f1[-1] + c1[-1]], o2[: f2[-1] + c2[-1]])
     fn = "avxsort_tuples" if w == 8 else "scalarsort_tuples"
     same_order(w, orc.sort(t), ref.sort(t, fn))
+
+
+# ------------------------------------------- int64 items in the AVX (FP64) order
+def int64_gold():
+    with np.load(os.path.join(GOLD, "golden_int64.npz"), allow_pickle=False) as d:
+        return {k: d[k] for k in d.files}
+
+
+def test_int64_fp64_order_golden(oracles):
+    """avxsort_int64 / avx_merge_int64 order items as IEEE doubles
+    (src/avxsort/avxcommon.h:79-190): this fork's signed (key, ptr) carriers
+    (src/bench/sortbench.c:267-298) come out key-ascending, negative keys
+    included.  Pins orc_sort_int64_fp64 / orc_merge_int64_fp64."""
+    g = int64_gold()
+    orc = oracles[8]
+    ns = [int(k.rsplit("_", 1)[1]) for k in g if k.startswith("carrier_in_")]
+    assert ns
+    for n in ns:
+        v = g[f"carrier_in_{n}"]
+        want = v[g[f"carrier_perm_{n}"]]
+        np.testing.assert_array_equal(orc.sort_int64_fp64(v), want)
+        assert not np.array_equal(np.sort(v), want)  # not the integer order
+    v = g["words_in"]
+    np.testing.assert_array_equal(orc.sort_int64_fp64(v), v[g["words_perm"]])
+    a, b = g["merge_a"], g["merge_b"]
+    np.testing.assert_array_equal(orc.merge_int64_fp64(a, b),
+                                  np.concatenate([a, b])[g["merge_perm"]])
+
+
+def test_int64_fp64_order_live_reference(oracles):
+    ref = _reference(8)
+    rng = np.random.default_rng(77)
+    key = rng.integers(-(2 ** 31 - 1), 2 ** 31 - 1, 40000)
+    w = (np.abs(key).astype(np.int64) << 20) | (np.arange(40000) & 0xFFFFF)
+    v = np.where(key < 0, w | np.int64(-2 ** 63), w).astype(np.int64)
+    np.testing.assert_array_equal(oracles[8].sort_int64_fp64(v), ref.sort_int64(v))
