@@ -304,8 +304,22 @@ static void partition_common(relation_t** parts, relation_t* input,
     SMJ_CHECK(hipMemcpyAsync(ho.data(), off, fan * 8, hipMemcpyDeviceToHost, c.st));
     sync();
     const uint64_t extent = fan ? (uint64_t)(ho[fan - 1] + hh[fan - 1]) : 0;
+    // the reference never writes the padding between padded partitions
+    // (partition.c:183-206): keep the caller's bytes there when staging back
+    std::vector<tuple_t> gaps;
+    if (out.staged && padded) {
+        for (uint32_t i = 0; i + 1 < fan; i++)
+            for (int64_t j = ho[i] + hh[i]; j < ho[i + 1]; j++)
+                gaps.push_back(output->tuples[j]);
+    }
     dev_out(out, extent);
     sync();
+    if (!gaps.empty()) {
+        size_t k = 0;
+        for (uint32_t i = 0; i + 1 < fan; i++)
+            for (int64_t j = ho[i] + hh[i]; j < ho[i + 1]; j++)
+                output->tuples[j] = gaps[k++];
+    }
     for (uint32_t i = 0; i < fan; i++) {
         parts[i]->tuples = output->tuples + ho[i];
         parts[i]->num_tuples = (uint64_t)hh[i];
@@ -714,9 +728,13 @@ uint64_t merge_join_interpolation(tuple_t* rtuples, tuple_t* stuples,
 
 // joincommon.c:29-212.  The orchestration of the reference's T join threads,
 // kept for drivers that bring their own join thread (tputbench.c:124-144).
-// Differences: threads are not pinned (their work is device work; the
-// reference's cpu_mapping.c belongs to the driver), and the chunk sizes are
-// computed in 64 bits before they land in the int32 fields of arg_t.
+// The CPU mapping (src/util/cpu_mapping.c) is the driver's: when the driver
+// links it, thread i is pinned to get_cpu_id(i) and marked active in its NUMA
+// region as joincommon.c:118-126 does (the driver's threads look themselves
+// up there); the weak references resolve to nothing otherwise.  The chunk
+// sizes are computed in 64 bits before they land in arg_t's int32 fields.
+extern "C" int get_cpu_id(int thread_id) __attribute__((weak));
+extern "C" void numa_thread_mark_active(int phytid) __attribute__((weak));
 static void* host_alloc64(size_t bytes) {
     void* p = nullptr;
     if (posix_memalign(&p, CACHE_LINE_SIZE, bytes ? bytes : CACHE_LINE_SIZE)) {
@@ -785,6 +803,14 @@ result_t* sortmergejoin_initrun(relation_t* relR, relation_t* relS,
         a.histR = histR;
         a.tmpRglobal = tmpPR;
         a.totalR = nR;
+        if (get_cpu_id) {
+            const int cpu = get_cpu_id(i);
+            if (numa_thread_mark_active) numa_thread_mark_active(cpu);
+            cpu_set_t set;
+            CPU_ZERO(&set);
+            CPU_SET(cpu, &set);
+            pthread_attr_setaffinity_np(&attr, sizeof(cpu_set_t), &set);
+        }
 #ifdef JOIN_MATERIALIZE
         a.threadresult = &res->resultlist[i];
 #endif

@@ -115,12 +115,19 @@ def test_reference_sortbench_posneg():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("w", [8, 16])
-@pytest.mark.parametrize("nthreads", [1, 2, 4])
+@pytest.mark.parametrize("nthreads", [2, 4, 8])
 def test_tputbench_ab_against_reference(w, nthreads):
     """src/bench/tputbench.c unchanged: its own join thread (partition, sort,
     multiway merge, merge_join per thread) on sortmergejoin_initrun.  A/B
     against the same driver on the reference's objects; T threads call the
-    library concurrently."""
+    library concurrently.
+
+    T = 1 is not compared: that path joins R with itself
+    (tputbench.c:485, ``partsS[i]->tuples = rels->R.tuples``) and reads |S_i|
+    tuples from R_i's place, past its end into padding and the next
+    partition, so merge_join gets unsorted input and the count depends on
+    the scan's behaviour outside its contract (the reference itself prints
+    1993423 there for 999597 true matches)."""
     ref = os.path.join(ROOT, "oracle", "_ref", f"tputbench_ref{w}")
     if not os.path.exists(ref):
         pytest.skip("reference tputbench not built")
