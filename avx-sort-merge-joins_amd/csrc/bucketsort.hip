@@ -46,13 +46,19 @@ constexpr int TILE2 = TP_THREADS * TP_ITEMS;  // tuples per tile
 const uint32_t kTileTuples = TILE2;
 
 #ifndef SMJ_GS_THREADS
-#define SMJ_GS_THREADS 128
+#define SMJ_GS_THREADS 256
 #endif
 constexpr int GS_THREADS = SMJ_GS_THREADS;      // one workgroup per group
-constexpr int GS_WG_PER_CU = 512 / GS_THREADS;  // resident workgroups per CU
-constexpr int GS_D3MAX = GS_THREADS >= 256 ? 11 : 10;  // level-3 bits sorted in LDS
-constexpr int GS_ITEMS = 10;                    // tuples per thread per relation
+#ifndef SMJ_GS_WG_PER_CU
+#define SMJ_GS_WG_PER_CU 4
+#endif
+constexpr int GS_WG_PER_CU = SMJ_GS_WG_PER_CU;  // resident workgroups per CU
+#ifndef SMJ_GS_ITEMS
+#define SMJ_GS_ITEMS (1280 / SMJ_GS_THREADS)
+#endif
+constexpr int GS_ITEMS = SMJ_GS_ITEMS;          // tuples per thread per relation
 constexpr int GS_CAP = GS_THREADS * GS_ITEMS;   // tuples per group per relation
+constexpr int GS_D3MAX = GS_CAP >= 2048 ? 11 : 10;  // level-3 bits sorted in LDS
 constexpr int GS_BPT = (1 << GS_D3MAX) / GS_THREADS;  // d3 bins per thread
 constexpr int GS_NB3 = 1 << GS_D3MAX;
 constexpr int GS_TMAX = 128;    // tiles per bucket on the fast path (two per lane of one wave)
@@ -360,8 +366,7 @@ __device__ __forceinline__ void insertion_sort(Tup* a, uint32_t n) {
 }
 
 // Group tables in LDS: wave r builds relation r's run table, run-start bitmap
-// and window tiles (no block barrier inside; one at the end), every thread
-// clears the d3 histograms.
+// and window tiles (no block barrier inside; one at the end).
 __device__ __forceinline__ void build_tables(const GroupArgs& A, GroupLDS& L,
                                              const GroupMeta& M) {
     const uint32_t wid = otid() >> 6, lane = otid() & 63;
@@ -410,7 +415,6 @@ __device__ __forceinline__ void build_tables(const GroupArgs& A, GroupLDS& L,
             L.wtile[r][lane] = (uint8_t)t;
         }
     }
-    for (uint32_t i = otid(); i < GS_NB3; i += GS_THREADS) (&L.cnt[0][0])[i] = 0u;
     if (otid() == 0) L.nlong = 0;
     __syncthreads();
 }
@@ -510,15 +514,16 @@ __device__ __forceinline__ void gather_group(const GroupArgs& A, GroupLDS& L,
 }
 
 // Sort relation r's group (in registers) by the level-3 digit in LDS and
-// write it to its final place.  With GATHER_NEXT, S's gather is issued
-// right after R's elements are placed (R's registers are free then).
-// Returns false when the group must take the skew path.
-template <bool GATHER_NEXT>
+// write it to out at offset `off` of its bucket.  `after_place` runs as soon
+// as the elements sit in LDS (the registers are free): the persistent loop
+// issues the next group's gather there.  Returns false when the group must
+// take the skew path.
+template <typename Hook>
 __device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS& L,
                                            const GroupMeta& C, const RangePlan& P,
-                                           int r, uint32_t nr, Tup (&v)[GS_ITEMS],
-                                           bool& clamped, Tup (&vnext)[GS_ITEMS],
-                                           uint32_t nnext) {
+                                           int r, uint32_t nr, uint32_t off,
+                                           Tup (&v)[GS_ITEMS], bool& clamped,
+                                           Hook&& after_place) {
     const uint32_t tid = otid(), wid = tid >> 6, lane = tid & 63;
     const uint32_t d12 = (C.b << P.D2) | C.g;
     const uint64_t bu = key_u(P.base);
@@ -571,7 +576,7 @@ __device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS& L,
         const uint32_t old = atomicAdd(&L.cur[dg[k] >> 1], valid ? 1u << sh : 0u);
         L.B[valid ? (old >> sh) & 0xffffu : GS_CAP] = v[k];
     }
-    if (GATHER_NEXT) gather_group(A, L, C, 1, nnext, vnext);
+    after_place();
     __syncthreads();
     if (dup) {
         // ---- equal-digit runs: short ones sorted here, long ones listed
@@ -608,7 +613,7 @@ __device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS& L,
         if (tid == 0) L.nlong = 0;
     }
     // ---- write the sorted group: one contiguous stream
-    Tup* dst = A.out[r] + C.ost[r] + L.off[r];
+    Tup* dst = A.out[r] + C.ost[r] + off;
 #pragma unroll
     for (int k = 0; k < GS_ITEMS; k++) {
         const uint32_t j = k * GS_THREADS + tid;
@@ -617,18 +622,11 @@ __device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS& L,
     return true;
 }
 
-// When S's group is gathered: 0 = with R's (both in flight at once),
-// 1 = once R's elements sit in LDS, 2 = after R's group is written.  The
-// later, the fewer VGPRs (16-byte tuples need it to stay under 256).
-#ifdef KEY_8B
-constexpr int kGatherS = 2;
-#else
-constexpr int kGatherS = 0;
-#endif
-
 // Persistent: workgroup w sorts groups [g_begin + w * per, ... + per) in
-// order; the next group's tile runs are loaded while the current one is
-// gathered and sorted.
+// order, software-pipelined across groups: group g+1's tables are built while
+// g's data is in registers, g+1's R is gathered as soon as g's R sits in LDS
+// and g+1's S as soon as g's S does, so both gathers fly under g's sort,
+// write-out and count; g+2's tile runs are loaded one group further ahead.
 __global__ void __launch_bounds__(GS_THREADS, GS_WG_PER_CU * GS_THREADS / 256)
 k_groupsort(GroupArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
@@ -641,73 +639,109 @@ k_groupsort(GroupArgs A) {
     unsigned long long matches = 0;
     if (gbeg >= gend) return;
 
+    for (uint32_t i = tid; i < GS_NB3; i += GS_THREADS) (&L.cnt[0][0])[i] = 0u;
     GroupMeta M;
     load_meta(A, gbeg, M, false);
-    for (uint32_t gi = gbeg; gi < gend; gi++) {
-        build_tables(A, L, M);
-        const GroupMeta C = M;
-        if (gi + 1 < gend) load_meta(A, gi + 1, M, true);  // prefetch
-        const uint32_t n0 = __builtin_amdgcn_readfirstlane(L.n[0]);
-        const uint32_t n1 = nrel > 1 ? __builtin_amdgcn_readfirstlane(L.n[1]) : 0;
-        if (n0 > GS_CAP || n1 > GS_CAP) {
-            group_overflow(A, L, C);
-            __syncthreads();
-            continue;
-        }
-        Tup vr[GS_ITEMS], vs[GS_ITEMS];
-        gather_group(A, L, C, 0, n0, vr);
-        if (kGatherS == 0 && nrel > 1) gather_group(A, L, C, 1, n1, vs);
-        bool clamped = false;
-        bool ok = sort_group<kGatherS == 1>(A, L, C, P, 0, n0, vr, clamped, vs,
-                                            nrel > 1 ? n1 : 0);
-        if (kGatherS == 2 && nrel > 1) gather_group(A, L, C, 1, n1, vs);
-        if (ok && nrel > 1)
-            ok = sort_group<false>(A, L, C, P, 1, n1, vs, clamped, vs, 0);
-        if (!ok) {
-            __syncthreads();
-            group_overflow(A, L, C);
-            __syncthreads();
-            continue;
-        }
-
-        // ---- merge-join count of the two groups
-        if (nrel == 2) {
-            const bool exact = P.s3 == 0 && !__syncthreads_or(clamped);
-            if (exact) {
-                // the level-3 digit is the exact key: sum_k |R_k| * |S_k|
+    build_tables(A, L, M);
+    GroupMeta C = M;
+    uint32_t cn[2], co[2];
 #pragma unroll
-                for (int q = 0; q < GS_BPT / 2; q++) {
-                    const uint32_t a0 = L.cnt[0][tid * (GS_BPT / 2) + q];
-                    const uint32_t a1 = L.cnt[1][tid * (GS_BPT / 2) + q];
-                    matches += (unsigned long long)(a0 & 0xffffu) * (a1 & 0xffffu) +
-                               (unsigned long long)(a0 >> 16) * (a1 >> 16);
-                }
-            } else {
-                // S is still in B; R's sorted group is in out (written above
-                // by this workgroup: visible after the barrier)
-                const Tup* Rs = A.out[0] + C.ost[0] + L.off[0];
-                const uint32_t nR = n0, nS = n1;
-                for (uint32_t i = tid; i < nS; i += GS_THREADS) {
-                    const int64_t k = tup_key(L.B[i]);
-                    if (i > 0 && tup_key(L.B[i - 1]) == k) continue;
-                    uint32_t e = i + 1;
-                    while (e < nS && tup_key(L.B[e]) == k) e++;
-                    uint32_t lo = 0, hi = nR;
-                    while (lo < hi) {
-                        const uint32_t m = (lo + hi) >> 1;
-                        if (tup_key(Rs[m]) < k) lo = m + 1; else hi = m;
+    for (int r = 0; r < 2; r++) {
+        cn[r] = r < nrel ? __builtin_amdgcn_readfirstlane(L.n[r]) : 0;
+        co[r] = r < nrel ? __builtin_amdgcn_readfirstlane(L.off[r]) : 0;
+    }
+    bool cur_fits = cn[0] <= GS_CAP && cn[1] <= GS_CAP;
+    Tup vr[GS_ITEMS], vs[GS_ITEMS];
+    if (cur_fits) {
+        gather_group(A, L, C, 0, cn[0], vr);
+        if (nrel > 1) gather_group(A, L, C, 1, cn[1], vs);
+    }
+    if (gbeg + 1 < gend) load_meta(A, gbeg + 1, M, true);
+
+    for (uint32_t gi = gbeg; gi < gend; gi++) {
+        const bool has_next = gi + 1 < gend;
+        // every lane's gather of group gi has read the tables: rebuild them
+        __syncthreads();
+        const GroupMeta N = M;
+        uint32_t nn[2] = {0, 0}, no[2] = {0, 0};
+        if (has_next) {
+            build_tables(A, L, N);
+#pragma unroll
+            for (int r = 0; r < 2; r++) {
+                nn[r] = r < nrel ? __builtin_amdgcn_readfirstlane(L.n[r]) : 0;
+                no[r] = r < nrel ? __builtin_amdgcn_readfirstlane(L.off[r]) : 0;
+            }
+        }
+        if (gi + 2 < gend) load_meta(A, gi + 2, M, true);
+        const bool next_fits = has_next && nn[0] <= GS_CAP && nn[1] <= GS_CAP;
+        auto gather_next_r = [&]() {
+            if (next_fits) gather_group(A, L, N, 0, nn[0], vr);
+        };
+        auto gather_next_s = [&]() {
+            if (next_fits && nrel > 1) gather_group(A, L, N, 1, nn[1], vs);
+        };
+        if (!cur_fits) {
+            group_overflow(A, L, C);
+            gather_next_r();
+            gather_next_s();
+        } else {
+            bool clamped = false;
+            bool ok = sort_group(A, L, C, P, 0, cn[0], co[0], vr, clamped, gather_next_r);
+            bool s_issued = false;
+            if (ok && nrel > 1) {
+                ok = sort_group(A, L, C, P, 1, cn[1], co[1], vs, clamped, gather_next_s);
+                s_issued = true;
+            }
+            if (!ok) {
+                __syncthreads();
+                group_overflow(A, L, C);
+                if (!s_issued) gather_next_s();
+            } else if (nrel == 2) {
+                // ---- merge-join count of the two groups
+                const bool exact = P.s3 == 0 && !__syncthreads_or(clamped);
+                if (exact) {
+                    // the level-3 digit is the exact key: sum_k |R_k| * |S_k|
+#pragma unroll
+                    for (int q = 0; q < GS_BPT / 2; q++) {
+                        const uint32_t a0 = L.cnt[0][tid * (GS_BPT / 2) + q];
+                        const uint32_t a1 = L.cnt[1][tid * (GS_BPT / 2) + q];
+                        matches += (unsigned long long)(a0 & 0xffffu) * (a1 & 0xffffu) +
+                                   (unsigned long long)(a0 >> 16) * (a1 >> 16);
                     }
-                    const uint32_t lb = lo;
-                    hi = nR;
-                    while (lo < hi) {
-                        const uint32_t m = (lo + hi) >> 1;
-                        if (tup_key(Rs[m]) <= k) lo = m + 1; else hi = m;
+                } else {
+                    // S is still in B; R's sorted group is in out (written above
+                    // by this workgroup: visible after the barrier)
+                    const Tup* Rs = A.out[0] + C.ost[0] + co[0];
+                    const uint32_t nR = cn[0], nS = cn[1];
+                    for (uint32_t i = tid; i < nS; i += GS_THREADS) {
+                        const int64_t k = tup_key(L.B[i]);
+                        if (i > 0 && tup_key(L.B[i - 1]) == k) continue;
+                        uint32_t e = i + 1;
+                        while (e < nS && tup_key(L.B[e]) == k) e++;
+                        uint32_t lo = 0, hi = nR;
+                        while (lo < hi) {
+                            const uint32_t m = (lo + hi) >> 1;
+                            if (tup_key(Rs[m]) < k) lo = m + 1; else hi = m;
+                        }
+                        const uint32_t lb = lo;
+                        hi = nR;
+                        while (lo < hi) {
+                            const uint32_t m = (lo + hi) >> 1;
+                            if (tup_key(Rs[m]) <= k) lo = m + 1; else hi = m;
+                        }
+                        matches += (unsigned long long)(lo - lb) * (e - i);
                     }
-                    matches += (unsigned long long)(lo - lb) * (e - i);
                 }
             }
         }
-        __syncthreads();  // tables, histograms and B are rebuilt next
+        __syncthreads();  // histograms and B are reused by the next group
+        for (uint32_t i = tid; i < GS_NB3; i += GS_THREADS) (&L.cnt[0][0])[i] = 0u;
+        C = N;
+        cn[0] = nn[0];
+        cn[1] = nn[1];
+        co[0] = no[0];
+        co[1] = no[1];
+        cur_fits = next_fits;
     }
     if (nrel == 2) {
         matches = wave_sum(matches);
