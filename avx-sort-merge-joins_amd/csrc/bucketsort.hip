@@ -155,7 +155,7 @@ k_tilepass(TilePassArgs A) {
 #pragma unroll
     for (int j = 0; j < TP_ITEMS; j++) {
         uint32_t i = j * TP_THREADS + threadIdx.x;
-        if (i < len) v[j] = part[off + i];
+        if (i < len) v[j] = ld_stream(part + off + i);
     }
     __syncthreads();
 #pragma unroll
@@ -201,7 +201,7 @@ k_tilepass(TilePassArgs A) {
 #pragma unroll
     for (int j = 0; j < TP_ITEMS; j++) {
         uint32_t i = j * TP_THREADS + threadIdx.x;
-        if (i < len) tmp[off + i] = stage[i];
+        if (i < len) st_stream(tmp + off + i, stage[i]);
     }
 }
 
@@ -509,7 +509,7 @@ __device__ __forceinline__ void gather_group(const GroupArgs& A, GroupLDS& L,
         const unsigned long long bits = L.smap[r][w] & (~0ull >> (63 - (j & 63)));
         const uint32_t t = bits ? L.stile[r][(w << 6) + 63 - __clzll(bits)]
                                 : L.wtile[r][w];
-        v[k] = tp[L.runsrc[r][t] + (j - L.runoff[r][t])];
+        v[k] = ld_stream(tp + L.runsrc[r][t] + (j - L.runoff[r][t]));
     }
 }
 
@@ -617,7 +617,7 @@ __device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS& L,
 #pragma unroll
     for (int k = 0; k < GS_ITEMS; k++) {
         const uint32_t j = k * GS_THREADS + tid;
-        if (j < nr) dst[j] = L.B[j];
+        if (j < nr) st_stream(dst + j, L.B[j]);
     }
     return true;
 }

@@ -555,13 +555,20 @@ k_sample_hist(const Tup* __restrict__ in, uint64_t n, uint32_t stride,
 // workgroups, blockIdx % kShards), so that the reservation atomics of a
 // partition are spread over kShards cursors (kShards: smj_internal.hpp).
 
+// Write unit of the sampled scatter: every store writes whole segments of
+// this many bytes (128 = one L2 line: no partially written lines).
+#ifndef SMJ_SC_SEG
+#define SMJ_SC_SEG 64
+#endif
+constexpr uint32_t kSegBytes = SMJ_SC_SEG;
+
 __global__ void __launch_bounds__(256)
 k_regions(const unsigned int* __restrict__ sample, uint32_t nbins,
           uint32_t stride, uint64_t slack, uint64_t* __restrict__ base,
           uint64_t* __restrict__ seg_start, unsigned long long* __restrict__ cursor,
           uint64_t* __restrict__ cap_end) {
     __shared__ uint64_t sh[256];
-    constexpr uint64_t SEG = 64 / sizeof(Tup);
+    constexpr uint64_t SEG = kSegBytes / sizeof(Tup);
     const uint32_t per = (nbins + 255) / 256;
     const uint32_t b = threadIdx.x * per;
     // capacity of one shard of partition d
@@ -633,7 +640,7 @@ k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
     unsigned long long* cursor = cursor_all + shard;
     const uint64_t* cap_end = cap_end_all + shard;
     constexpr int TILE = THREADS * ITEMS;
-    constexpr uint32_t SEG = 64 / sizeof(Tup);  // tuples per 64-byte segment
+    constexpr uint32_t SEG = kSegBytes / sizeof(Tup);  // tuples per segment
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     Tup* stage = reinterpret_cast<Tup*>(lds_raw);
     Tup* carry = stage + TILE;
@@ -657,7 +664,7 @@ k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
 #pragma unroll
     for (int j = 0; j < ITEMS; j++) {
         const uint64_t i = beg + (uint64_t)j * THREADS + threadIdx.x;
-        if (i < end) v[j] = in[i];
+        if (i < end) v[j] = ld_stream(in + i);
     }
     __syncthreads();
     for (uint64_t base = beg; base < end; base += TILE) {
@@ -667,7 +674,7 @@ k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
 #pragma unroll
         for (int j = 0; j < ITEMS; j++) {
             const uint64_t i = nb + (uint64_t)j * THREADS + threadIdx.x;
-            if (i < end) nv[j] = in[i];
+            if (i < end) nv[j] = ld_stream(in + i);
         }
         // ---- rank: tile counts per partition
         uint32_t dg[ITEMS];
@@ -733,7 +740,7 @@ k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
                 const uint32_t vv = kc[d] + (i - tstart[d]);
                 const uint32_t E = tfill[d];
                 if (vv < E) {
-                    out[pos[d] + vv] = t;
+                    out[pos[d] + vv] = t;  // plain stores: the L2 merges partial lines
                 } else if (vv - E < SEG) {  // always, unless the region overflowed
                     keep[j] = t;
                     kslot[j] = d * SEG + (vv - E);
@@ -1074,11 +1081,23 @@ void plan_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
 // partition's region start and size; *flag_dev is OR-ed with 1 when a region
 // overflowed (then the output is incomplete and the exact partition must be
 // used).  Nothing is read back to the host.
+#ifndef SMJ_SC_THREADS
+#define SMJ_SC_THREADS 1024
+#endif
+#ifndef SMJ_SC_ITEMS16
+#define SMJ_SC_ITEMS16 4
+#endif
+#ifndef SMJ_SC_ITEMS8
+#define SMJ_SC_ITEMS8 8
+#endif
+#ifndef SMJ_SC_WG_PER_CU
+#define SMJ_SC_WG_PER_CU 1
+#endif
 static constexpr uint32_t kSampleStride = 128;
 static constexpr uint64_t kRegionSlack = 1024;  // per shard
 
 uint64_t sampled_capacity(uint64_t n, uint32_t dbits) {
-    const uint64_t SEG = 64 / sizeof(Tup);
+    const uint64_t SEG = kSegBytes / sizeof(Tup);
     return n + n / 8 + 2 * kSampleStride +
            ((uint64_t)1 << dbits) * kShards * (kRegionSlack + 2 * SEG);
 }
@@ -1090,8 +1109,8 @@ void sampled_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
                        unsigned int* flag_dev, hipStream_t st) {
     PlanDigit1 dig{plan_dev};
     const uint32_t nbins = 1u << dbits;
-    constexpr int THREADS = 512;
-    constexpr int ITEMS = sizeof(Tup) == 16 ? 8 : 16;
+    constexpr int THREADS = SMJ_SC_THREADS;
+    constexpr int ITEMS = sizeof(Tup) == 16 ? SMJ_SC_ITEMS16 : SMJ_SC_ITEMS8;
     constexpr int TILE = THREADS * ITEMS;
     unsigned int* sample = (unsigned int*)ws->scratch("sp_sample", (size_t)nbins * 4);
     unsigned long long* cursor =
@@ -1113,12 +1132,14 @@ void sampled_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
     }
     if (n) {
         uint64_t ntiles = (n + TILE - 1) / TILE;
-        const uint32_t maxwg = 256;  // one per CU
+        const uint32_t maxwg = 256 * SMJ_SC_WG_PER_CU;
         uint32_t nwg = (uint32_t)(ntiles < maxwg ? ntiles : maxwg);
         const uint64_t tiles_per_wg = (ntiles + nwg - 1) / nwg;
         const uint64_t chunk = tiles_per_wg * TILE;
         nwg = (uint32_t)((ntiles + tiles_per_wg - 1) / tiles_per_wg);
-        const size_t lds = scatter_wc_lds<THREADS, ITEMS>(nbins);
+        // stage TILE | carry nbins segments | pos u64, tstart, tfill, kc u32
+        const size_t lds = (size_t)TILE * sizeof(Tup) + (size_t)nbins * kSegBytes +
+                           (size_t)nbins * (8 + 4 + 4 + 4) + 64;
         static bool attr = false;
         if (!attr) {
             SMJ_CHECK(hipFuncSetAttribute(

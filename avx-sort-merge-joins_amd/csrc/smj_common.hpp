@@ -39,6 +39,45 @@ typedef uint64_t Tup;
 
 constexpr int kTupBytes = sizeof(Tup);
 
+// Streaming accesses of the tuple passes (each byte read once, written once):
+// optionally with the non-temporal cache policy.
+#ifndef SMJ_NT_STORES
+#define SMJ_NT_STORES 1
+#endif
+#ifndef SMJ_NT_LOADS
+#define SMJ_NT_LOADS 0
+#endif
+#ifdef KEY_8B
+typedef long long TupVec __attribute__((ext_vector_type(2)));
+#endif
+__device__ __forceinline__ void st_stream(Tup* p, const Tup& v) {
+#if SMJ_NT_STORES
+#ifdef KEY_8B
+    TupVec x = {v.payload, v.key};
+    __builtin_nontemporal_store(x, reinterpret_cast<TupVec*>(p));
+#else
+    __builtin_nontemporal_store(v, p);
+#endif
+#else
+    *p = v;
+#endif
+}
+__device__ __forceinline__ Tup ld_stream(const Tup* p) {
+#if SMJ_NT_LOADS
+#ifdef KEY_8B
+    const TupVec x = __builtin_nontemporal_load(reinterpret_cast<const TupVec*>(p));
+    Tup t;
+    t.payload = x.x;
+    t.key = x.y;
+    return t;
+#else
+    return __builtin_nontemporal_load(p);
+#endif
+#else
+    return *p;
+#endif
+}
+
 __host__ __device__ __forceinline__ int64_t tup_key(const Tup& t) {
 #ifdef KEY_8B
     return t.key;
