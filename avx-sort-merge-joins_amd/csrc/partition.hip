@@ -560,6 +560,9 @@ k_sample_hist(const Tup* __restrict__ in, uint64_t n, uint32_t stride,
 #ifndef SMJ_SC_SEG
 #define SMJ_SC_SEG 64
 #endif
+#ifndef SMJ_SC_ABL
+#define SMJ_SC_ABL 0
+#endif
 constexpr uint32_t kSegBytes = SMJ_SC_SEG;
 
 __global__ void __launch_bounds__(256)
@@ -657,8 +660,11 @@ k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
     const uint64_t beg = (uint64_t)blockIdx.x * chunk;
     uint64_t end = beg + chunk;
     if (end > n) end = n;
-    const uint32_t dper = (nbins + THREADS - 1) / THREADS;
-    const uint32_t d0 = threadIdx.x * dper;
+    // one partition per thread (the host launches nbins <= THREADS): the
+    // per-partition state lives in registers, no dynamic indexing
+    const uint32_t d0 = threadIdx.x;
+    const bool own = d0 < nbins;
+    const uint64_t my_cap = own ? cap_end[(size_t)d0 * kShards] : 0;
 
     Tup v[ITEMS], nv[ITEMS];
 #pragma unroll
@@ -671,11 +677,10 @@ k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
         const uint32_t tcount =
             (uint32_t)((end - base) < (uint64_t)TILE ? (end - base) : TILE);
         const uint64_t nb = base + TILE;
-#pragma unroll
-        for (int j = 0; j < ITEMS; j++) {
-            const uint64_t i = nb + (uint64_t)j * THREADS + threadIdx.x;
-            if (i < end) nv[j] = ld_stream(in + i);
-        }
+        // this tile's loads (the previous prefetch) have landed: an explicit
+        // vmcnt(0) on every path, so the compiler's own bookkeeping does not
+        // re-wait (for the next prefetch) at each conditional use below
+        __builtin_amdgcn_s_waitcnt(0x0f70);
         // ---- rank: tile counts per partition
         uint32_t dg[ITEMS];
 #pragma unroll
@@ -685,44 +690,45 @@ k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
             if (dg[j] != 0xffffffffu) atomicAdd(&tfill[dg[j]], 1u);
         }
         __syncthreads();
-        uint32_t loc = 0;
-        for (uint32_t k = 0; k < dper; k++)
-            if (d0 + k < nbins) loc += tfill[d0 + k];
+        const uint32_t loc = own ? tfill[d0] : 0;
         uint32_t tot;
         uint32_t ex = block_exclusive_scan(loc, scr, &tot);
         // ---- per partition: reserve the whole segments of carry + tile (E,
-        // a multiple of SEG) in the region; the reservation's latency
-        // overlaps the staging below
-        uint32_t Eown[4];
-        for (uint32_t k = 0; k < dper && k < 4; k++) {
-            const uint32_t d = d0 + k;
-            Eown[k] = 0;
-            if (d < nbins) {
-                const uint32_t c = tfill[d];
-                tstart[d] = ex;
-                tfill[d] = ex;
-                ex += c;
-                const uint32_t T = kc[d] + c;
-                const uint32_t E = T / SEG * SEG;
-                Eown[k] = E;
-                if (E) pos[d] = atomicAdd(&cursor[(size_t)d * kShards], (unsigned long long)E);
-            }
+        // a multiple of SEG) in the region.  The reservations are issued
+        // before the next tile's loads, so waiting for them (after the
+        // staging below) does not wait for that prefetch.
+        uint32_t Eown = 0;
+        unsigned long long Pown = 0;
+        if (own) {
+            const uint32_t d = d0;
+            const uint32_t c = loc;
+            tstart[d] = ex;
+            tfill[d] = ex;
+            const uint32_t T = kc[d] + c;
+            Eown = T / SEG * SEG;
+            if (Eown) Pown = atomicAdd(&cursor[(size_t)d * kShards], (unsigned long long)Eown);
+        }
+        // unconditional (clamped) loads: a fixed count in flight lets the
+        // reservation results be waited for with vmcnt(ITEMS)
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint64_t i = nb + (uint64_t)j * THREADS + threadIdx.x;
+            nv[j] = ld_stream(in + (i < end ? i : end - 1));
         }
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < ITEMS; j++)
             if (dg[j] != 0xffffffffu) stage[atomicAdd(&tfill[dg[j]], 1u)] = v[j];
-        __syncthreads();
-        for (uint32_t k = 0; k < dper && k < 4; k++) {
-            const uint32_t d = d0 + k;
-            if (d < nbins) {
-                uint32_t E = Eown[k];
-                // an overflowing region writes nothing (the caller repeats
-                // the exact partition)
-                if (E && pos[d] + E > cap_end[(size_t)d * kShards]) E = 0;
-                tfill[d] = E;
-            }
+        if (own) {
+            // an overflowing region writes nothing (the caller repeats the
+            // exact partition)
+            uint32_t E = Eown;
+            if (E && Pown + E > my_cap) E = 0;
+            pos[d0] = Pown;
+            Eown = E;
         }
+        __syncthreads();
+        if (own) tfill[d0] = Eown;
         __syncthreads();
         for (uint32_t q = threadIdx.x; q < nbins * SEG; q += THREADS) {
             const uint32_t d = q / SEG, j = q % SEG;
@@ -740,7 +746,13 @@ k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
                 const uint32_t vv = kc[d] + (i - tstart[d]);
                 const uint32_t E = tfill[d];
                 if (vv < E) {
+#if SMJ_SC_ABL == 1
+                    out[base + i] = t;  // ablation: linear writes
+#elif SMJ_SC_ABL == 2
+                    if (tup_key(t) == -12345) out[pos[d] + vv] = t;  // ablation: no writes
+#else
                     out[pos[d] + vv] = t;  // plain stores: the L2 merges partial lines
+#endif
                 } else if (vv - E < SEG) {  // always, unless the region overflowed
                     keep[j] = t;
                     kslot[j] = d * SEG + (vv - E);
@@ -751,31 +763,24 @@ k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
 #pragma unroll
         for (int j = 0; j < ITEMS; j++)
             if (kslot[j] != 0xffffffffu) carry[kslot[j]] = keep[j];
-        for (uint32_t k = 0; k < dper; k++) {
-            const uint32_t d = d0 + k;
-            if (d < nbins) {
-                const uint32_t cnt = ((d + 1 < nbins) ? tstart[d + 1] : tcount) - tstart[d];
-                const uint32_t T = kc[d] + cnt;
-                const uint32_t E = tfill[d];
-                // E == 0 after an overflow: keep at most SEG - 1 (the rest is
-                // lost; the partition is repeated anyway)
-                kc[d] = T - E < SEG ? T - E : SEG - 1;
-                tfill[d] = 0;
-            }
+        if (own) {
+            const uint32_t T = kc[d0] + loc;
+            // E == 0 after an overflow: keep at most SEG - 1 (the rest is
+            // lost; the partition is repeated anyway)
+            kc[d0] = T - Eown < SEG ? T - Eown : SEG - 1;
+            tfill[d0] = 0;
         }
 #pragma unroll
         for (int j = 0; j < ITEMS; j++) v[j] = nv[j];
         __syncthreads();
     }
     // ---- flush the carries: reserve exactly what is left
-    for (uint32_t k = 0; k < dper; k++) {
-        const uint32_t d = d0 + k;
-        if (d < nbins) {
-            pos[d] = 0;
-            if (kc[d]) {
-                const uint64_t p = atomicAdd(&cursor[(size_t)d * kShards], (unsigned long long)kc[d]);
-                pos[d] = p + kc[d] <= cap_end[(size_t)d * kShards] ? p : ~0ull;
-            }
+    if (own) {
+        const uint32_t d = d0;
+        pos[d] = 0;
+        if (kc[d]) {
+            const uint64_t p = atomicAdd(&cursor[(size_t)d * kShards], (unsigned long long)kc[d]);
+            pos[d] = p + kc[d] <= my_cap ? p : ~0ull;
         }
     }
     __syncthreads();
@@ -1149,6 +1154,10 @@ void sampled_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
         }
         if (lds > 160 * 1024) {
             fprintf(stderr, "[ERROR] smj: scatter LDS %zu > 160 KiB\n", lds);
+            abort();
+        }
+        if (nbins > (uint32_t)THREADS) {
+            fprintf(stderr, "[ERROR] smj: sampled scatter needs <= %d partitions\n", THREADS);
             abort();
         }
         TraceScope ts(ws, "k_scatter", st);
