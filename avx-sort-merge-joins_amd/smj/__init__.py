@@ -46,8 +46,8 @@ REFERENCE_SYMBOLS = [
     "avx_merge_tuples", "avx_merge_int64", "scalar_merge_tuples",
     "scalar_merge_int64", "avx_multiway_merge", "scalar_multiway_merge",
     "scalar_multiway_merge_modulo", "scalar_multiway_merge_bitand",
-    "merge_join", "print_timing", "sortmergejoin_multiway", "sortmergejoin_multipass",
-    "sortmergejoin_mpsm",
+    "merge_join", "merge_join_interpolation", "print_timing", "sortmergejoin_multiway",
+    "sortmergejoin_multipass", "sortmergejoin_mpsm", "sortmergejoin_initrun",
 ]
 DEVICE_SYMBOLS = [
     "smj_tuple_bytes", "smj_device_name", "smj_workspace_create",
