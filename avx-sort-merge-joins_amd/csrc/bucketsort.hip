@@ -41,6 +41,13 @@ namespace smj {
 #define SMJ_TP_THREADS 512
 #endif
 constexpr int TP_THREADS = SMJ_TP_THREADS;
+// group pass: digit-major prefix table (k_preft) and non-temporal gathers
+#ifndef SMJ_PREFT
+#define SMJ_PREFT 1
+#endif
+#ifndef SMJ_GATHER_NT
+#define SMJ_GATHER_NT 0
+#endif
 constexpr int TP_ITEMS = 16;
 constexpr int TILE2 = TP_THREADS * TP_ITEMS;  // tuples per tile
 const uint32_t kTileTuples = TILE2;
@@ -79,6 +86,8 @@ struct TileTable {
     uint32_t* bucket;  // owning bucket
     uint32_t* btile0;  // first tile of every bucket (nbuckets + 1)
     uint16_t* pref;    // [tile][nb2 + 1] exclusive prefix, sentinel = length
+    uint16_t* prefT;   // the same, digit-major: [d2][tstride] (k_preft)
+    uint32_t tstride;  // tiles per prefT row (>= the tile count)
 };
 
 struct OvfEntry {
@@ -206,6 +215,35 @@ k_tilepass(TilePassArgs A) {
 }
 
 // ---------------------------------------------------------------------------
+// prefix rows -> digit-major (prefT[d][t]): a group reads one entry per tile
+// of its bucket, and the bucket's tiles are consecutive, so the group pass
+// loads its run table with one or two lines per relation instead of one
+// line per tile.  One block per 64 tiles of one relation (upper-bound grid
+// when the tile count is only known on the device).
+constexpr int PT_TILES = 64;
+__global__ void __launch_bounds__(256)
+k_preft(TileTable tt0, TileTable tt1, uint32_t nb0, const uint32_t* __restrict__ ntiles0,
+        const uint32_t* __restrict__ ntiles1, uint32_t nt0_host, uint32_t nt1_host,
+        uint32_t nb2) {
+    extern __shared__ uint16_t sp[];  // [PT_TILES][nb2 + 1]
+    const int r = blockIdx.x < nb0 ? 0 : 1;
+    const TileTable& tt = r ? tt1 : tt0;
+    const uint32_t ntl = (r ? ntiles1 : ntiles0) ? *(r ? ntiles1 : ntiles0)
+                                                 : (r ? nt1_host : nt0_host);
+    const uint32_t tb = (r ? blockIdx.x - nb0 : blockIdx.x) * PT_TILES;
+    if (tb >= ntl) return;
+    const uint32_t nt = min((uint32_t)PT_TILES, ntl - tb);
+    const uint32_t row = nb2 + 1;
+    const uint16_t* src = tt.pref + (uint64_t)tb * row;
+    for (uint32_t i = threadIdx.x; i < nt * row; i += 256) sp[i] = src[i];
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < row * PT_TILES; i += 256) {
+        const uint32_t d = i / PT_TILES, t = i % PT_TILES;
+        if (t < nt) tt.prefT[(uint64_t)d * tt.tstride + tb + t] = sp[t * row + d];
+    }
+}
+
+// ---------------------------------------------------------------------------
 struct GroupArgs {
     const Tup* tmp[2];
     Tup* out[2];
@@ -264,7 +302,8 @@ __device__ __forceinline__ void load_meta(const GroupArgs& A, uint32_t gi,
                                           GroupMeta& M, bool same_bucket) {
     const uint32_t b = gi / A.nb2;
     M.g = gi % A.nb2;
-    if (!same_bucket || b != M.b) {
+    const bool newb = !same_bucket || b != M.b;
+    if (newb) {
 #pragma unroll
         for (int r = 0; r < 2; r++) {
             M.t0[r] = M.nt[r] = 0;
@@ -283,20 +322,28 @@ __device__ __forceinline__ void load_meta(const GroupArgs& A, uint32_t gi,
         }
     }
     M.b = b;
-    const uint32_t wid = otid() >> 6, lane = otid() & 63;
+    // the wave index is uniform: table pointers stay scalar
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(otid() >> 6), lane = otid() & 63;
     M.lo[0] = M.len[0] = M.lo[1] = M.len[1] = 0;
     M.toff[0] = M.toff[1] = 0;
     if (wid < (uint32_t)A.nrel) {
         const uint32_t nt = wid ? M.nt[1] : M.nt[0];
         const uint32_t t0 = wid ? M.t0[1] : M.t0[0];
+        const uint32_t ts = A.tt[wid].tstride;
 #pragma unroll
         for (int h = 0; h < 2; h++) {
             const uint32_t t = lane + 64 * h;
             if (nt <= GS_TMAX && t < nt) {
-                const uint16_t* pf =
-                    A.tt[wid].pref + (uint64_t)(t0 + t) * (A.nb2 + 1) + M.g;
+#if SMJ_PREFT
+                // digit-major prefix: lanes read consecutive entries
+                const uint16_t* pf = A.tt[wid].prefT + (uint64_t)M.g * ts + t0 + t;
+                M.lo[h] = pf[0];
+                M.len[h] = (uint32_t)(pf[ts] - pf[0]);
+#else
+                const uint16_t* pf = A.tt[wid].pref + (uint64_t)(t0 + t) * (A.nb2 + 1) + M.g;
                 M.lo[h] = pf[0];
                 M.len[h] = (uint32_t)(pf[1] - pf[0]);
+#endif
                 M.toff[h] = (uint32_t)(A.tt[wid].off[t0 + t] - (wid ? M.bst[1] : M.bst[0]));
             }
         }
@@ -440,12 +487,13 @@ __device__ __forceinline__ void group_overflow(const GroupArgs& A, GroupLDS& L,
 #pragma unroll
     for (int r = 0; r < 2; r++) {
         if (r >= A.nrel) break;
-        const uint16_t* pref = A.tt[r].pref;
+        const uint16_t* pref = A.tt[r].prefT;
+        const uint32_t ts = A.tt[r].tstride;
         const uint32_t t0 = M.t0[r], nt = M.nt[r];
         unsigned long long acc = 0;
         for (uint32_t t = otid(); t < nt; t += GS_THREADS) {
-            const uint16_t* pf = pref + (uint64_t)(t0 + t) * (A.nb2 + 1) + M.g;
-            acc += ((unsigned long long)pf[0] << 32) | (uint32_t)(pf[1] - pf[0]);
+            const uint16_t* pf = pref + (uint64_t)M.g * ts + t0 + t;
+            acc += ((unsigned long long)pf[0] << 32) | (uint32_t)(pf[ts] - pf[0]);
         }
         unsigned long long tot;
         (void)block_scan64(acc, L.scan64, &tot);
@@ -454,8 +502,8 @@ __device__ __forceinline__ void group_overflow(const GroupArgs& A, GroupLDS& L,
         Tup* dst = A.out[r] + M.ost[r] + oo[r];
         uint32_t pos = 0;
         for (uint32_t t = 0; t < nt; t++) {
-            const uint16_t* pf = pref + (uint64_t)(t0 + t) * (A.nb2 + 1) + M.g;
-            const uint32_t lo = pf[0], len = (uint32_t)(pf[1] - pf[0]);
+            const uint16_t* pf = pref + (uint64_t)M.g * ts + t0 + t;
+            const uint32_t lo = pf[0], len = (uint32_t)(pf[ts] - pf[0]);
             const Tup* src = A.tmp[r] + A.tt[r].off[t0 + t] + lo;
             for (uint32_t i = otid(); i < len; i += GS_THREADS) {
                 const Tup x = src[i];
@@ -509,7 +557,11 @@ __device__ __forceinline__ void gather_group(const GroupArgs& A, GroupLDS& L,
         const unsigned long long bits = L.smap[r][w] & (~0ull >> (63 - (j & 63)));
         const uint32_t t = bits ? L.stile[r][(w << 6) + 63 - __clzll(bits)]
                                 : L.wtile[r][w];
+#if SMJ_GATHER_NT
+        v[k] = ld_nt(tp + L.runsrc[r][t] + (j - L.runoff[r][t]));
+#else
         v[k] = ld_stream(tp + L.runsrc[r][t] + (j - L.runoff[r][t]));
+#endif
     }
 }
 
@@ -877,6 +929,37 @@ k_seg_scan(const int64_t* __restrict__ seg_cnt, const int64_t* __restrict__ bcou
     }
 }
 
+// digit-major prefix tables of both relations (k_preft); `ub` bounds the
+// tile count, `ntiles` holds it on the device (nullptr: ub is exact)
+static void launch_preft(const TileTable* tt, int nrel, const uint32_t* ub,
+                         uint32_t* const* ntiles, uint32_t nb2, hipStream_t st) {
+    const uint32_t nb0 = (ub[0] + PT_TILES - 1) / PT_TILES;
+    const uint32_t nb1 = nrel > 1 ? (ub[1] + PT_TILES - 1) / PT_TILES : 0;
+    if (nb0 + nb1 == 0) return;
+    const size_t lds = (size_t)PT_TILES * (nb2 + 1) * 2;
+    hipLaunchKernelGGL(k_preft, dim3(nb0 + nb1), dim3(256), lds, st, tt[0],
+                       tt[nrel > 1 ? 1 : 0], nb0, ntiles[0], nrel > 1 ? ntiles[1] : nullptr,
+                       ub[0], nrel > 1 ? ub[1] : 0u, nb2);
+}
+
+// the tiles [t0, t0 + nt) of one tile-pass batch: shift the tables so the
+// batch's first tile is tile 0 of the launch
+static void launch_preft_range(const TilePassArgs& T, int nrel, uint32_t nb2,
+                               hipStream_t st) {
+    TileTable tt[2];
+    uint32_t ub[2] = {0, 0};
+    uint32_t* nt[2] = {nullptr, nullptr};
+    for (int r = 0; r < 2; r++) {
+        tt[r] = T.tt[r];
+        if (r < nrel) {
+            tt[r].pref += (uint64_t)T.t0[r] * (nb2 + 1);
+            tt[r].prefT += T.t0[r];
+            ub[r] = T.nt[r];
+        }
+    }
+    launch_preft(tt, nrel, ub, nt, nb2, st);
+}
+
 // Bucket pass without a host synchronisation before the kernels (sampled
 // partition + host-known plan): launch sizes are upper bounds, the tile
 // numbering is computed on the device.  One synchronisation at the end (skew
@@ -886,9 +969,9 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
     const int nrel = a.nrel;
     const uint32_t nb2 = 1u << a.host_plan->D2;
     TileTable tt[2];
-    static const char* names[2][7] = {
-        {"bs_off0", "bs_len0", "bs_bkt0", "bs_bt00", "bs_pref0", "bs_ost0", "bs_nt0"},
-        {"bs_off1", "bs_len1", "bs_bkt1", "bs_bt01", "bs_pref1", "bs_ost1", "bs_nt1"}};
+    static const char* names[2][8] = {
+        {"bs_off0", "bs_len0", "bs_bkt0", "bs_bt00", "bs_pref0", "bs_ost0", "bs_nt0", "bs_preft0"},
+        {"bs_off1", "bs_len1", "bs_bkt1", "bs_bt01", "bs_pref1", "bs_ost1", "bs_nt1", "bs_preft1"}};
     uint64_t* ostart[2] = {nullptr, nullptr};
     uint32_t* ntiles[2] = {nullptr, nullptr};
     uint32_t ub[2] = {0, 0};
@@ -899,6 +982,8 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
         tt[r].bucket = (uint32_t*)ws->scratch(names[r][2], (size_t)ub[r] * 4);
         tt[r].btile0 = (uint32_t*)ws->scratch(names[r][3], (nb + 1) * 4);
         tt[r].pref = (uint16_t*)ws->scratch(names[r][4], (size_t)ub[r] * (nb2 + 1) * 2);
+        tt[r].prefT = (uint16_t*)ws->scratch(names[r][7], (size_t)ub[r] * (nb2 + 1) * 2);
+        tt[r].tstride = ub[r];
         ostart[r] = (uint64_t*)ws->scratch(names[r][5], (size_t)nb * 8);
         ntiles[r] = (uint32_t*)ws->scratch(names[r][6], 4);
         hipLaunchKernelGGL(k_seg_scan, dim3(1), dim3(256), 0, st, a.seg_cnt[r],
@@ -938,6 +1023,7 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
         hipLaunchKernelGGL(k_tilepass, dim3(T.nt[0] + T.nt[1]), dim3(TP_THREADS),
                            tp_lds, st, T);
     }
+    launch_preft(tt, nrel, ub, ntiles, nb2, st);
     if (a.ev_bucket) SMJ_CHECK(hipEventRecord(a.ev_bucket, st));
     G.nrel = nrel;
     G.plan = *a.host_plan;
@@ -1017,6 +1103,9 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
         SMJ_CHECK(hipFuncSetAttribute((const void*)k_groupsort,
                                       hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)sizeof(GroupLDS)));
+        SMJ_CHECK(hipFuncSetAttribute((const void*)k_preft,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      PT_TILES * ((1 << 9) + 1) * 2));
         attr = true;
     }
     if (a.host_plan && a.seg_start[0] && a.part_flag && ring_tuples() == 0)
@@ -1050,9 +1139,9 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
     const uint32_t nb2 = 1u << hplan->D2;  // groups per bucket
 
     TileTable tt[2];
-    static const char* names[2][5] = {
-        {"bs_off0", "bs_len0", "bs_bkt0", "bs_bt00", "bs_pref0"},
-        {"bs_off1", "bs_len1", "bs_bkt1", "bs_bt01", "bs_pref1"}};
+    static const char* names[2][6] = {
+        {"bs_off0", "bs_len0", "bs_bkt0", "bs_bt00", "bs_pref0", "bs_preft0"},
+        {"bs_off1", "bs_len1", "bs_bkt1", "bs_bt01", "bs_pref1", "bs_preft1"}};
     uint32_t* hbt = (uint32_t*)ws->host_pinned("bs_hbt", (size_t)2 * (nb + 1) * 4);
     // dense output start of every bucket (partition regions may have slack)
     uint64_t* hdst = (uint64_t*)ws->host_pinned("bs_hdst", (size_t)2 * nb * 8);
@@ -1081,6 +1170,8 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
         tt[r].bucket = (uint32_t*)ws->scratch(names[r][2], ntl * 4);
         tt[r].btile0 = (uint32_t*)ws->scratch(names[r][3], (nb + 1) * 4);
         tt[r].pref = (uint16_t*)ws->scratch(names[r][4], ntl * (nb2 + 1) * 2);
+        tt[r].prefT = (uint16_t*)ws->scratch(names[r][5], ntl * (nb2 + 1) * 2);
+        tt[r].tstride = (uint32_t)ntl;
         SMJ_CHECK(hipMemcpyAsync(tt[r].btile0, bt0, (nb + 1) * 4,
                                  hipMemcpyHostToDevice, st));
         ostart[r] = (uint64_t*)ws->scratch(r ? "bs_ost1" : "bs_ost0", (size_t)nb * 8);
@@ -1174,9 +1265,13 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
             }
         }
         if (ntiles) {
-            TraceScope ts(ws, "k_tilepass", st);
-            hipLaunchKernelGGL(k_tilepass, dim3(ntiles), dim3(TP_THREADS), tp_lds,
-                               st, T);
+            {
+                TraceScope ts(ws, "k_tilepass", st);
+                hipLaunchKernelGGL(k_tilepass, dim3(ntiles), dim3(TP_THREADS), tp_lds,
+                                   st, T);
+            }
+            // the batch's rows only (a ring batch rewrites its tiles' rows)
+            launch_preft_range(T, nrel, nb2, st);
         }
         if (a.ev_bucket && !ev_bucket_done) {
             SMJ_CHECK(hipEventRecord(a.ev_bucket, st));

@@ -78,6 +78,20 @@ __device__ __forceinline__ Tup ld_stream(const Tup* p) {
 #endif
 }
 
+// non-temporal load regardless of SMJ_NT_LOADS: gathers of once-read tuples
+// that must not push the small per-group tables out of L2
+__device__ __forceinline__ Tup ld_nt(const Tup* p) {
+#ifdef KEY_8B
+    const TupVec x = __builtin_nontemporal_load(reinterpret_cast<const TupVec*>(p));
+    Tup t;
+    t.payload = x.x;
+    t.key = x.y;
+    return t;
+#else
+    return __builtin_nontemporal_load(p);
+#endif
+}
+
 __host__ __device__ __forceinline__ int64_t tup_key(const Tup& t) {
 #ifdef KEY_8B
     return t.key;
