@@ -127,7 +127,7 @@ k_tiles(const uint64_t* __restrict__ bstart, const int64_t* __restrict__ bcount,
 // One launch covers the tiles [t0[r], t0[r] + nt[r]) of both relations
 // (blocks [0, nt[0]) are R's, the rest S's).  A tile at part offset `off` is
 // written to tmp[r][off]: `tmp` is either the partition buffer itself (in
-// place) or a ring buffer shifted by the batch's first offset (bucket_sort).
+// place) or any buffer of the same layout.
 struct TilePassArgs {
     const Tup* part[2];
     Tup* tmp[2];
@@ -466,24 +466,15 @@ __device__ __forceinline__ void build_tables(const GroupArgs& A, GroupLDS& L,
     __syncthreads();
 }
 
-// The group goes to the skew path: its runs are copied, unsorted, to the
-// group's final place in `out` and the group is queued.  Called by the whole
-// workgroup (uniform control flow).
+// A group too large for LDS (or with long equal-digit runs out of order) is
+// queued: its size and offset in each relation come from the prefix table,
+// its tuples are sorted and counted afterwards by the skew kernels below, over
+// many workgroups.  Called by the whole workgroup (uniform control flow).
 __device__ __forceinline__ void group_overflow(const GroupArgs& A, GroupLDS& L,
                                                const GroupMeta& M) {
     uint32_t nn[2] = {0, 0};
     uint64_t oo[2] = {0, 0};
-    const RangePlan& P = A.plan;
-    const uint32_t d12 = (M.b << P.D2) | M.g;
-    const uint64_t bu = key_u(P.base);
-    // the group's level-3 histograms (u32: skewed groups exceed 16 bits), in
-    // the LDS of the sort buffer: when the last digit is the exact key they
-    // give the group's match count without sorting it
-    uint32_t* hc = reinterpret_cast<uint32_t*>(L.B);
-    static_assert(sizeof(L.B) >= 2 * GS_NB3 * sizeof(uint32_t), "histogram space");
-    for (uint32_t i = otid(); i < 2 * GS_NB3; i += GS_THREADS) hc[i] = 0;
-    __syncthreads();
-    bool clamped = false;
+    const uint32_t tid = otid();
 #pragma unroll
     for (int r = 0; r < 2; r++) {
         if (r >= A.nrel) break;
@@ -491,7 +482,7 @@ __device__ __forceinline__ void group_overflow(const GroupArgs& A, GroupLDS& L,
         const uint32_t ts = A.tt[r].tstride;
         const uint32_t t0 = M.t0[r], nt = M.nt[r];
         unsigned long long acc = 0;
-        for (uint32_t t = otid(); t < nt; t += GS_THREADS) {
+        for (uint32_t t = tid; t < nt; t += GS_THREADS) {
             const uint16_t* pf = pref + (uint64_t)M.g * ts + t0 + t;
             acc += ((unsigned long long)pf[0] << 32) | (uint32_t)(pf[ts] - pf[0]);
         }
@@ -499,32 +490,8 @@ __device__ __forceinline__ void group_overflow(const GroupArgs& A, GroupLDS& L,
         (void)block_scan64(acc, L.scan64, &tot);
         nn[r] = (uint32_t)tot;
         oo[r] = tot >> 32;
-        Tup* dst = A.out[r] + M.ost[r] + oo[r];
-        uint32_t pos = 0;
-        for (uint32_t t = 0; t < nt; t++) {
-            const uint16_t* pf = pref + (uint64_t)M.g * ts + t0 + t;
-            const uint32_t lo = pf[0], len = (uint32_t)(pf[ts] - pf[0]);
-            const Tup* src = A.tmp[r] + A.tt[r].off[t0 + t] + lo;
-            for (uint32_t i = otid(); i < len; i += GS_THREADS) {
-                const Tup x = src[i];
-                dst[pos + i] = x;
-                const int64_t key = tup_key(x);
-                const uint64_t ku = key_u(key);
-                clamped |= (ku < bu) || (ku - bu > P.span);
-                atomicAdd(&hc[r * GS_NB3 + plan_d3(P, plan_rel(P, key), d12)], 1u);
-            }
-            pos += len;
-        }
     }
-    const bool exact = A.nrel == 2 && P.s3 == 0 && !__syncthreads_or(clamped);
-    if (exact) {
-        unsigned long long m = 0;
-        for (uint32_t d = otid(); d < GS_NB3; d += GS_THREADS)
-            m += (unsigned long long)hc[d] * hc[GS_NB3 + d];
-        m = wave_sum(m);
-        if ((otid() & 63) == 0 && m) atomicAdd(A.count_dev, m);
-    }
-    if (otid() == 0) {
+    if (tid == 0) {
         const uint32_t k = atomicAdd(A.novf, 1u);
         if (k < A.ovf_cap) {
             OvfEntry e;
@@ -534,12 +501,12 @@ __device__ __forceinline__ void group_overflow(const GroupArgs& A, GroupLDS& L,
             e.nr[1] = nn[1];
             e.off[0] = oo[0];
             e.off[1] = oo[1];
-            e.counted = exact ? 1u : 0u;
+            e.counted = 0;
             e.pad = 0;
             A.ovf[k] = e;
         }
     }
-    __syncthreads();  // the histograms lived in the sort buffer
+    __syncthreads();
 }
 
 // gather relation r's group into registers (loads only: every load in
@@ -802,6 +769,496 @@ k_groupsort(GroupArgs A) {
 }
 
 // ---------------------------------------------------------------------------
+// Skew path on the device: the queued groups (too large for LDS, e.g. the
+// groups of hot Zipf keys) are counting-sorted by the last digit through HBM.
+// The host sorts the queue by size once it has read it:
+//   k_skew_small : one workgroup per group of up to kSkewSmall tuples per
+//                  relation: d3 histograms in LDS (exact digits give the
+//                  match count sum_k |R_k|*|S_k|), cursors, placement in
+//                  `out`, then a check that equal-key runs came out in
+//                  (key, payload) order
+//   larger groups are split over many workgroups, one work item = one
+//   relation of one group and every ts-th tile run of it:
+//   k_skew_hist  : d3 histogram of the item's runs -> the group's global
+//                  histogram; flags keys outside the plan (digit not exact)
+//   k_skew_scan  : per group: match count, histograms -> cursors
+//   k_skew_place : every run chunk reserves its digits' ranges at the group's
+//                  cursors and places its tuples (inexact groups: the run is
+//                  copied unsorted to its place in the group)
+//   k_skew_check : per group: equal-key runs in (key, payload) order?
+// What is left (inexact digits, equal-key runs out of payload order) goes to
+// the host-driven merge sort and merge-join count.
+constexpr int SK_THREADS = 256;
+constexpr int SK_ITEMS = 8;
+constexpr int SK_CHUNK = SK_THREADS * SK_ITEMS;
+constexpr uint32_t kSkewSmall = 16384;  // tuples per relation, one workgroup
+constexpr int SK_TM = 256;              // tile runs in LDS tables (small groups)
+
+struct SkewArgs {
+    GroupArgs G;
+    OvfEntry* q;            // every queued group
+    const uint32_t* list;   // k_skew_small / _scan / _check: group indices
+    const uint4* items;     // large groups: {group, slot, r << 16 | s, ts}
+    uint32_t n;             // list or item count
+    uint32_t* ghist;        // [slot][2][GS_NB3]: histograms, then cursors
+    const uint32_t* slot;   // k_skew_scan / _check: slot of list[i]
+    uint32_t* gflag;        // [group] bit 0: key outside the plan, bit 1: run out of order
+};
+
+// tile t of group (b, g) in relation r: run [src, src + len)
+__device__ __forceinline__ const Tup* skew_run(const GroupArgs& G, int r, uint32_t g,
+                                               uint32_t t0, uint32_t t, uint32_t& len) {
+    const TileTable& tt = G.tt[r];
+    const uint16_t* pf = tt.prefT + (uint64_t)g * tt.tstride + t0 + t;
+    const uint32_t lo = pf[0];
+    len = (uint32_t)(pf[tt.tstride] - lo);
+    return G.tmp[r] + tt.off[t0 + t] + lo;
+}
+
+struct SkewSmallLDS {
+    uint32_t h[2][GS_NB3];
+    uint32_t runoff[2][SK_TM + 1];
+    uint64_t runsrc[2][SK_TM];
+    unsigned long long scr[SK_THREADS / 64 + 1];
+};
+
+// element j of relation r's group (run tables in LDS) -> its source tuple
+__device__ __forceinline__ const Tup* skew_elem(const SkewSmallLDS& L, int r, const Tup* tmp,
+                                                uint32_t nt, uint32_t j) {
+    uint32_t lo = 0, hi = nt;  // last run with runoff <= j
+    while (hi - lo > 1) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (L.runoff[r][m] <= j) lo = m; else hi = m;
+    }
+    return tmp + L.runsrc[r][lo] + (j - L.runoff[r][lo]);
+}
+
+// apply f(x) to every tuple of relation r's group, SK_ITEMS loads in flight
+// per thread (groups of more than SK_TM runs: run by run)
+template <class F>
+__device__ __forceinline__ void skew_for_each(const GroupArgs& G, const SkewSmallLDS& L, int r,
+                                              uint32_t g, uint32_t t0, uint32_t nt, uint32_t n,
+                                              F&& f) {
+    if (nt <= SK_TM) {
+        for (uint32_t c = 0; c < n; c += SK_CHUNK) {
+            Tup v[SK_ITEMS];
+#pragma unroll
+            for (int k = 0; k < SK_ITEMS; k++) {
+                const uint32_t j = c + k * SK_THREADS + threadIdx.x;
+                if (j < n) v[k] = ld_stream(skew_elem(L, r, G.tmp[r], nt, j));
+            }
+#pragma unroll
+            for (int k = 0; k < SK_ITEMS; k++)
+                if (c + k * SK_THREADS + threadIdx.x < n) f(v[k]);
+        }
+    } else {
+        for (uint32_t t = 0; t < nt; t++) {
+            uint32_t len;
+            const Tup* src = skew_run(G, r, g, t0, t, len);
+            for (uint32_t i = threadIdx.x; i < len; i += SK_THREADS) f(src[i]);
+        }
+    }
+}
+
+// any i in [lo, hi) with out[i] < out[i - 1]  (lo >= 1)
+__device__ __forceinline__ bool skew_inversion(const Tup* dst, uint32_t lo, uint32_t hi) {
+    bool inv = false;
+    for (uint32_t c = lo; c < hi; c += SK_CHUNK) {
+        Tup a[SK_ITEMS], b[SK_ITEMS];
+#pragma unroll
+        for (int k = 0; k < SK_ITEMS; k++) {
+            const uint32_t i = c + k * SK_THREADS + threadIdx.x;
+            if (i < hi) {
+                a[k] = dst[i - 1];
+                b[k] = dst[i];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < SK_ITEMS; k++)
+            if (c + k * SK_THREADS + threadIdx.x < hi) inv |= tup_less(b[k], a[k]);
+    }
+    return inv;
+}
+
+__global__ void __launch_bounds__(SK_THREADS)
+k_skew_small(SkewArgs K) {
+    __shared__ SkewSmallLDS L;
+    const GroupArgs& G = K.G;
+    const RangePlan& P = G.plan;
+    const uint32_t qi = K.list[blockIdx.x];
+    const OvfEntry e = K.q[qi];
+    const uint32_t d12 = (e.bucket << P.D2) | e.d2;
+    const uint64_t bu = key_u(P.base);
+    const uint32_t tid = threadIdx.x;
+    uint32_t t0[2] = {0, 0}, nt[2] = {0, 0};
+    for (uint32_t i = tid; i < 2 * GS_NB3; i += SK_THREADS) (&L.h[0][0])[i] = 0;
+    // ---- run tables
+    for (int r = 0; r < G.nrel; r++) {
+        t0[r] = G.tt[r].btile0[e.bucket];
+        nt[r] = G.tt[r].btile0[e.bucket + 1] - t0[r];
+        if (nt[r] > SK_TM) continue;
+        unsigned long long acc = 0;
+        uint64_t src = 0;
+        if (tid < nt[r]) {
+            const TileTable& tt = G.tt[r];
+            const uint16_t* pf = tt.prefT + (uint64_t)e.d2 * tt.tstride + t0[r] + tid;
+            acc = (uint32_t)(pf[tt.tstride] - pf[0]);
+            src = tt.off[t0[r] + tid] + pf[0];
+        }
+        unsigned long long tot;
+        const unsigned long long ex = block_scan64(acc, L.scr, &tot);
+        if (tid < nt[r]) {
+            L.runoff[r][tid] = (uint32_t)ex;
+            L.runsrc[r][tid] = src;
+        }
+        if (tid == 0) L.runoff[r][nt[r]] = (uint32_t)tot;
+    }
+    __syncthreads();
+    // ---- pass 1: d3 histograms
+    bool clamped = false;
+    for (int r = 0; r < G.nrel; r++)
+        skew_for_each(G, L, r, e.d2, t0[r], nt[r], e.nr[r], [&](const Tup& x) {
+            const int64_t key = tup_key(x);
+            const uint64_t ku = key_u(key);
+            clamped |= (ku < bu) || (ku - bu > P.span);
+            atomicAdd(&L.h[r][plan_d3(P, plan_rel(P, key), d12)], 1u);
+        });
+    const bool exact = P.s3 == 0 && !__syncthreads_or(clamped);
+    if (!exact) {
+        // inexact digits: copy the runs unsorted to the group's place
+        for (int r = 0; r < G.nrel; r++) {
+            Tup* dst = G.out[r] + G.ostart[r][e.bucket] + e.off[r];
+            uint32_t pos = 0;
+            for (uint32_t t = 0; t < nt[r]; t++) {
+                uint32_t len;
+                const Tup* src = skew_run(G, r, e.d2, t0[r], t, len);
+                for (uint32_t i = tid; i < len; i += SK_THREADS) dst[pos + i] = src[i];
+                pos += len;
+            }
+        }
+        if (tid == 0) K.gflag[qi] |= 1u;
+        return;
+    }
+    if (G.nrel == 2) {
+        unsigned long long m = 0;
+        for (uint32_t d = tid; d < GS_NB3; d += SK_THREADS)
+            m += (unsigned long long)L.h[0][d] * L.h[1][d];
+        m = wave_sum(m);
+        if ((tid & 63) == 0 && m) atomicAdd(G.count_dev, m);
+        if (tid == 0) K.q[qi].counted = 1;
+    }
+    bool inv = false;
+    for (int r = 0; r < G.nrel; r++) {
+        Tup* dst = G.out[r] + G.ostart[r][e.bucket] + e.off[r];
+        // ---- cursors: exclusive scan of the bins (thread owns a range)
+        constexpr int BPT = GS_NB3 / SK_THREADS;
+        uint32_t c[BPT];
+        unsigned long long loc = 0;
+#pragma unroll
+        for (int k = 0; k < BPT; k++) {
+            c[k] = L.h[r][tid * BPT + k];
+            loc += c[k];
+        }
+        unsigned long long tot;
+        unsigned long long ex = block_scan64(loc, L.scr, &tot);
+#pragma unroll
+        for (int k = 0; k < BPT; k++) {
+            L.h[r][tid * BPT + k] = (uint32_t)ex;
+            ex += c[k];
+        }
+        __syncthreads();
+        // ---- pass 2: place
+        skew_for_each(G, L, r, e.d2, t0[r], nt[r], e.nr[r], [&](const Tup& x) {
+            const uint32_t d = plan_d3(P, plan_rel(P, tup_key(x)), d12);
+            dst[atomicAdd(&L.h[r][d], 1u)] = x;
+        });
+        __threadfence_block();
+        __syncthreads();
+        // ---- pass 3: ordered by key; an inversion sits inside an equal-key run
+        inv |= skew_inversion(dst, 1, e.nr[r]);
+    }
+    if (__syncthreads_or(inv) && tid == 0) K.gflag[qi] |= 2u;
+}
+
+__global__ void __launch_bounds__(SK_THREADS)
+k_skew_hist(SkewArgs K) {
+    __shared__ uint32_t h[GS_NB3];
+    const GroupArgs& G = K.G;
+    const RangePlan& P = G.plan;
+    const uint64_t bu = key_u(P.base);
+    const uint4 it = K.items[blockIdx.x];
+    const uint32_t qi = it.x, sl = it.y, r = it.z >> 16, s = it.z & 0xffffu, ts = it.w;
+    const OvfEntry& e = K.q[qi];
+    const uint32_t t0 = G.tt[r].btile0[e.bucket];
+    const uint32_t nt = G.tt[r].btile0[e.bucket + 1] - t0;
+    if (s >= nt) return;
+    for (uint32_t d = threadIdx.x; d < GS_NB3; d += SK_THREADS) h[d] = 0;
+    __syncthreads();
+    const uint32_t d12 = (e.bucket << P.D2) | e.d2;
+    bool clamped = false;
+    for (uint32_t t = s; t < nt; t += ts) {
+        uint32_t len;
+        const Tup* src = skew_run(G, (int)r, e.d2, t0, t, len);
+        for (uint32_t c = 0; c < len; c += SK_CHUNK) {
+            Tup v[SK_ITEMS];
+#pragma unroll
+            for (int k = 0; k < SK_ITEMS; k++) {
+                const uint32_t i = c + k * SK_THREADS + threadIdx.x;
+                if (i < len) v[k] = ld_stream(src + i);
+            }
+#pragma unroll
+            for (int k = 0; k < SK_ITEMS; k++) {
+                const uint32_t i = c + k * SK_THREADS + threadIdx.x;
+                if (i < len) {
+                    const int64_t key = tup_key(v[k]);
+                    const uint64_t ku = key_u(key);
+                    clamped |= (ku < bu) || (ku - bu > P.span);
+                    atomicAdd(&h[plan_d3(P, plan_rel(P, key), d12)], 1u);
+                }
+            }
+        }
+    }
+    const bool any = __syncthreads_or(clamped);
+    uint32_t* gh = K.ghist + ((size_t)sl * 2 + r) * GS_NB3;
+    for (uint32_t d = threadIdx.x; d < GS_NB3; d += SK_THREADS)
+        if (h[d]) atomicAdd(&gh[d], h[d]);
+    if (any && threadIdx.x == 0) atomicOr(&K.gflag[qi], 1u);
+}
+
+__global__ void __launch_bounds__(SK_THREADS)
+k_skew_scan(SkewArgs K) {
+    __shared__ unsigned long long scr[SK_THREADS / 64 + 1];
+    const uint32_t qi = K.list[blockIdx.x], sl = K.slot[blockIdx.x];
+    const RangePlan& P = K.G.plan;
+    const bool exact = P.s3 == 0 && !(K.gflag[qi] & 1u);
+    if (!exact) return;
+    uint32_t* gh = K.ghist + (size_t)sl * 2 * GS_NB3;
+    if (K.G.nrel == 2) {
+        unsigned long long m = 0;
+        for (uint32_t d = threadIdx.x; d < GS_NB3; d += SK_THREADS)
+            m += (unsigned long long)gh[d] * gh[GS_NB3 + d];
+        m = wave_sum(m);
+        if ((threadIdx.x & 63) == 0 && m) atomicAdd(K.G.count_dev, m);
+        if (threadIdx.x == 0) K.q[qi].counted = 1;
+    }
+    constexpr int BPT = GS_NB3 / SK_THREADS;
+    for (int r = 0; r < K.G.nrel; r++) {
+        uint32_t* h = gh + r * GS_NB3;
+        uint32_t c[BPT];
+        unsigned long long loc = 0;
+#pragma unroll
+        for (int k = 0; k < BPT; k++) {
+            c[k] = h[threadIdx.x * BPT + k];
+            loc += c[k];
+        }
+        unsigned long long tot;
+        unsigned long long ex = block_scan64(loc, scr, &tot);
+#pragma unroll
+        for (int k = 0; k < BPT; k++) {
+            h[threadIdx.x * BPT + k] = (uint32_t)ex;
+            ex += c[k];
+        }
+    }
+}
+
+__global__ void __launch_bounds__(SK_THREADS)
+k_skew_place(SkewArgs K) {
+    __shared__ uint32_t h[GS_NB3];
+    __shared__ unsigned long long scr[SK_THREADS / 64 + 1];
+    const GroupArgs& G = K.G;
+    const RangePlan& P = G.plan;
+    const uint4 it = K.items[blockIdx.x];
+    const uint32_t qi = it.x, sl = it.y, r = it.z >> 16, s = it.z & 0xffffu, ts = it.w;
+    const OvfEntry& e = K.q[qi];
+    const uint32_t t0 = G.tt[r].btile0[e.bucket];
+    const uint32_t nt = G.tt[r].btile0[e.bucket + 1] - t0;
+    if (s >= nt) return;
+    Tup* dst = G.out[r] + G.ostart[r][e.bucket] + e.off[r];
+    const bool exact = P.s3 == 0 && !(K.gflag[qi] & 1u);
+    if (!exact) {
+        // copy the runs unsorted: run t starts after the runs before it
+        for (uint32_t t = s; t < nt; t += ts) {
+            unsigned long long acc = 0;
+            for (uint32_t u = threadIdx.x; u < t; u += SK_THREADS) {
+                uint32_t l;
+                (void)skew_run(G, (int)r, e.d2, t0, u, l);
+                acc += l;
+            }
+            unsigned long long pos;
+            (void)block_scan64(acc, scr, &pos);
+            uint32_t len;
+            const Tup* src = skew_run(G, (int)r, e.d2, t0, t, len);
+            for (uint32_t i = threadIdx.x; i < len; i += SK_THREADS) dst[pos + i] = src[i];
+        }
+        return;
+    }
+    const uint32_t d12 = (e.bucket << P.D2) | e.d2;
+    uint32_t* gcur = K.ghist + ((size_t)sl * 2 + r) * GS_NB3;
+    for (uint32_t t = s; t < nt; t += ts) {
+        uint32_t len;
+        const Tup* src = skew_run(G, (int)r, e.d2, t0, t, len);
+        for (uint32_t c = 0; c < len; c += SK_CHUNK) {
+            for (uint32_t d = threadIdx.x; d < GS_NB3; d += SK_THREADS) h[d] = 0;
+            Tup v[SK_ITEMS];
+            uint32_t dg[SK_ITEMS];
+#pragma unroll
+            for (int k = 0; k < SK_ITEMS; k++) {
+                const uint32_t i = c + k * SK_THREADS + threadIdx.x;
+                if (i < len) v[k] = ld_stream(src + i);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < SK_ITEMS; k++) {
+                const uint32_t i = c + k * SK_THREADS + threadIdx.x;
+                dg[k] = 0xffffffffu;
+                if (i < len) {
+                    dg[k] = plan_d3(P, plan_rel(P, tup_key(v[k])), d12);
+                    atomicAdd(&h[dg[k]], 1u);
+                }
+            }
+            __syncthreads();
+            // reserve this chunk's share of every digit at the cursors
+            for (uint32_t d = threadIdx.x; d < GS_NB3; d += SK_THREADS) {
+                const uint32_t n = h[d];
+                if (n) h[d] = atomicAdd(&gcur[d], n);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < SK_ITEMS; k++)
+                if (dg[k] != 0xffffffffu) dst[atomicAdd(&h[dg[k]], 1u)] = v[k];
+            __syncthreads();
+        }
+    }
+}
+
+__global__ void __launch_bounds__(SK_THREADS)
+k_skew_check(SkewArgs K) {
+    const uint4 it = K.items[blockIdx.x];
+    const uint32_t qi = it.x, r = it.z >> 16, s = it.z & 0xffffu, ts = it.w;
+    const RangePlan& P = K.G.plan;
+    if (!(P.s3 == 0 && !(K.gflag[qi] & 1u))) return;
+    const OvfEntry& e = K.q[qi];
+    const Tup* dst = K.G.out[r] + K.G.ostart[r][e.bucket] + e.off[r];
+    const uint32_t n = e.nr[r];
+    const uint32_t lo = max(1u, (uint32_t)((uint64_t)n * s / ts));
+    const uint32_t hi = (uint32_t)((uint64_t)n * (s + 1) / ts);
+    if (__syncthreads_or(skew_inversion(dst, lo, hi)) && threadIdx.x == 0)
+        atomicOr(&K.gflag[qi], 2u);
+}
+
+// The queued groups [0, no): device skew kernels, then whatever they could
+// not finish (inexact digits, equal-key runs out of payload order) through
+// the segmented merge sort and the merge-join count.  hdst[r * nb + b] is
+// bucket b's output start.
+static void skew_path(Workspace* ws, const GroupArgs& G, OvfEntry* ovf, uint32_t no,
+                      const uint64_t* hdst, uint32_t nb, hipStream_t st) {
+    const int nrel = G.nrel;
+    std::vector<OvfEntry> he(no);
+    SMJ_CHECK(hipMemcpyAsync(he.data(), ovf, no * sizeof(OvfEntry),
+                             hipMemcpyDeviceToHost, st));
+    SMJ_CHECK(hipStreamSynchronize(st));
+    // small groups: one workgroup each; large ones: work items over their runs
+    std::vector<uint32_t> small, large, lslot;
+    std::vector<uint4> items;
+    for (uint32_t i = 0; i < no; i++) {
+        const uint32_t m = std::max(he[i].nr[0], nrel > 1 ? he[i].nr[1] : 0u);
+        if (m <= kSkewSmall) {
+            small.push_back(i);
+            continue;
+        }
+        const uint32_t sl = (uint32_t)large.size();
+        large.push_back(i);
+        lslot.push_back(sl);
+        for (int r = 0; r < nrel; r++) {
+            // about 8K tuples per item (runs are strided over the items)
+            const uint32_t ts = std::min<uint32_t>(std::max<uint32_t>(he[i].nr[r] / 8192, 1), 256);
+            for (uint32_t s = 0; s < ts; s++)
+                items.push_back(make_uint4(i, sl, ((uint32_t)r << 16) | s, ts));
+        }
+    }
+    const size_t nl = large.size();
+    const size_t lbytes = (small.size() + 2 * nl) * 4;
+    const size_t ibytes = items.size() * sizeof(uint4);
+    unsigned char* hbuf = (unsigned char*)ws->host_pinned("sk_h", lbytes + ibytes + 16);
+    unsigned char* dbuf = (unsigned char*)ws->scratch("sk_d", lbytes + ibytes + 16);
+    uint32_t* hl = (uint32_t*)hbuf;
+    std::copy(small.begin(), small.end(), hl);
+    std::copy(large.begin(), large.end(), hl + small.size());
+    std::copy(lslot.begin(), lslot.end(), hl + small.size() + nl);
+    const size_t ioff = (lbytes + 15) / 16 * 16;
+    std::copy(items.begin(), items.end(), (uint4*)(hbuf + ioff));
+    SMJ_CHECK(hipMemcpyAsync(dbuf, hbuf, ioff + ibytes, hipMemcpyHostToDevice, st));
+    uint32_t* gflag = (uint32_t*)ws->scratch("sk_flag", (size_t)no * 4);
+    SMJ_CHECK(hipMemsetAsync(gflag, 0, (size_t)no * 4, st));
+    SkewArgs K;
+    K.G = G;
+    K.q = ovf;
+    K.gflag = gflag;
+    K.ghist = nullptr;
+    K.slot = nullptr;
+    K.items = nullptr;
+    if (!small.empty()) {
+        K.list = (const uint32_t*)dbuf;
+        K.n = (uint32_t)small.size();
+        TraceScope ts(ws, "k_skew_small", st);
+        hipLaunchKernelGGL(k_skew_small, dim3(K.n), dim3(SK_THREADS), 0, st, K);
+    }
+    if (nl) {
+        K.ghist = (uint32_t*)ws->scratch("sk_hist", nl * 2 * GS_NB3 * 4);
+        SMJ_CHECK(hipMemsetAsync(K.ghist, 0, nl * 2 * GS_NB3 * 4, st));
+        K.list = (const uint32_t*)dbuf + small.size();
+        K.slot = K.list + nl;
+        K.items = (const uint4*)(dbuf + ioff);
+        const uint32_t ni = (uint32_t)items.size();
+        {
+            TraceScope ts(ws, "k_skew_hist", st);
+            hipLaunchKernelGGL(k_skew_hist, dim3(ni), dim3(SK_THREADS), 0, st, K);
+        }
+        hipLaunchKernelGGL(k_skew_scan, dim3((uint32_t)nl), dim3(SK_THREADS), 0, st, K);
+        {
+            TraceScope ts(ws, "k_skew_place", st);
+            hipLaunchKernelGGL(k_skew_place, dim3(ni), dim3(SK_THREADS), 0, st, K);
+        }
+        hipLaunchKernelGGL(k_skew_check, dim3(ni), dim3(SK_THREADS), 0, st, K);
+    }
+    SMJ_CHECK(hipGetLastError());
+    std::vector<uint32_t> flags(no, 0);
+    SMJ_CHECK(hipMemcpyAsync(flags.data(), gflag, (size_t)no * 4, hipMemcpyDeviceToHost, st));
+    SMJ_CHECK(hipMemcpyAsync(he.data(), ovf, no * sizeof(OvfEntry),
+                             hipMemcpyDeviceToHost, st));
+    SMJ_CHECK(hipStreamSynchronize(st));
+    // what the device could not finish
+    std::vector<uint32_t> rest;
+    for (uint32_t i = 0; i < no; i++)
+        if (flags[i] != 0 || G.plan.s3 != 0) rest.push_back(i);
+    if (getenv("SMJ_DEBUG_OVF"))
+        fprintf(stderr, "[smj] skew: %u queued groups (%zu small, %zu large, %zu items), "
+                "%zu left to the merge sort\n", no, small.size(), nl, items.size(), rest.size());
+    if (rest.empty()) return;
+    for (int r = 0; r < nrel; r++) {
+        std::vector<uint64_t> so, sl;
+        for (uint32_t i : rest) {
+            so.push_back(hdst[(size_t)r * nb + he[i].bucket] + he[i].off[r]);
+            sl.push_back(he[i].nr[r]);
+        }
+        segmented_sort(ws, G.out[r], so.data(), sl.data(), (uint32_t)rest.size(), st);
+    }
+    if (nrel == 2) {
+        std::vector<const Tup*> rp, sp;
+        std::vector<uint64_t> nr, ns;
+        for (uint32_t i : rest) {
+            if (he[i].counted || !he[i].nr[0] || !he[i].nr[1]) continue;
+            rp.push_back(G.out[0] + hdst[he[i].bucket] + he[i].off[0]);
+            sp.push_back(G.out[1] + hdst[nb + he[i].bucket] + he[i].off[1]);
+            nr.push_back(he[i].nr[0]);
+            ns.push_back(he[i].nr[1]);
+        }
+        merge_join_count_batch(ws, rp.data(), nr.data(), sp.data(), ns.data(),
+                               (uint32_t)rp.size(), G.count_dev, st);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // range plan from a strided sample of the relations (or from hints)
 __global__ void __launch_bounds__(256)
 k_plan(const Tup* r0, uint64_t n0, const Tup* r1, uint64_t n1, uint32_t D1,
@@ -876,20 +1333,6 @@ const uint32_t kGroupD3Max = GS_D3MAX;
 const uint32_t kGroupTarget = GS_CAP * 4 / 5 >= 2048 ? 2048 : (GS_CAP * 4 / 5 >= 1024 ? 1024 : 512);
 
 // ---------------------------------------------------------------------------
-// Ring size per relation in tuples (0 = the tile pass works in place in the
-// partition buffer).  With a ring, buckets are processed in batches whose
-// tile-pass output fits the ring, so the group pass re-reads it from the
-// Infinity Cache instead of HBM.  SMJ_RING_MB overrides the default.
-static uint64_t ring_tuples() {
-    static int64_t mb = -1;
-    if (mb < 0) {
-        const char* e = getenv("SMJ_RING_MB");
-        mb = e ? atoll(e) : 0;
-        if (mb < 0) mb = 0;
-    }
-    return (uint64_t)mb * (1ull << 20) / sizeof(Tup);
-}
-
 // device-side tile numbering of a segmented (sampled) partition: per bucket
 // the tiles of its segments, their exclusive scan (btile0, total in
 // btile0[nb] and *ntiles) and the dense output start of every bucket
@@ -1058,35 +1501,11 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
         fprintf(stderr, "[ERROR] smj: overflow table too small\n");
         abort();
     }
-    std::vector<OvfEntry> he(no);
     std::vector<uint64_t> hdst((size_t)2 * nb);
-    SMJ_CHECK(hipMemcpyAsync(he.data(), ovf, no * sizeof(OvfEntry),
-                             hipMemcpyDeviceToHost, st));
     for (int r = 0; r < nrel; r++)
         SMJ_CHECK(hipMemcpyAsync(hdst.data() + (size_t)r * nb, ostart[r], (size_t)nb * 8,
                                  hipMemcpyDeviceToHost, st));
-    SMJ_CHECK(hipStreamSynchronize(st));
-    for (int r = 0; r < nrel; r++) {
-        std::vector<uint64_t> so(no), sl(no);
-        for (uint32_t i = 0; i < no; i++) {
-            so[i] = hdst[(size_t)r * nb + he[i].bucket] + he[i].off[r];
-            sl[i] = he[i].nr[r];
-        }
-        segmented_sort(ws, a.out[r], so.data(), sl.data(), no, st);
-    }
-    if (nrel == 2) {
-        std::vector<const Tup*> rp, sp;
-        std::vector<uint64_t> nr, ns;
-        for (uint32_t i = 0; i < no; i++) {
-            if (he[i].counted || !he[i].nr[0] || !he[i].nr[1]) continue;
-            rp.push_back(a.out[0] + hdst[he[i].bucket] + he[i].off[0]);
-            sp.push_back(a.out[1] + hdst[nb + he[i].bucket] + he[i].off[1]);
-            nr.push_back(he[i].nr[0]);
-            ns.push_back(he[i].nr[1]);
-        }
-        merge_join_count_batch(ws, rp.data(), nr.data(), sp.data(), ns.data(),
-                               (uint32_t)rp.size(), a.count_dev, st);
-    }
+    skew_path(ws, G, ovf, no, hdst.data(), nb, st);
     SMJ_CHECK(hipGetLastError());
     return true;
 }
@@ -1108,21 +1527,18 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
                                       PT_TILES * ((1 << 9) + 1) * 2));
         attr = true;
     }
-    if (a.host_plan && a.seg_start[0] && a.part_flag && ring_tuples() == 0)
+    if (a.host_plan && a.seg_start[0] && a.part_flag)
         return bucket_sort_nosync(ws, a, st);
 
     // ---- host view of the plan and the bucket counts (one synchronisation):
-    // launch sizes, tile numbering and batches are derived from them
+    // launch sizes and the tile numbering are derived from them
     uint64_t* hcnt = (uint64_t*)ws->host_pinned("bs_hcnt", (size_t)2 * nb * 8);
-    uint64_t* hst = (uint64_t*)ws->host_pinned("bs_hst", (size_t)2 * nb * 8);
     RangePlan* hplan = (RangePlan*)ws->host_pinned("bs_hplan", sizeof(RangePlan));
     const bool segs = a.seg_start[0] != nullptr;
     const uint32_t nseg = segs ? kShards : 1;
     int64_t* hseg = (int64_t*)ws->host_pinned("bs_hseg", (size_t)2 * nb * kShards * 8);
     for (int r = 0; r < nrel; r++) {
         SMJ_CHECK(hipMemcpyAsync(hcnt + r * nb, a.bcount[r], nb * 8,
-                                 hipMemcpyDeviceToHost, st));
-        SMJ_CHECK(hipMemcpyAsync(hst + r * nb, a.bstart[r], nb * 8,
                                  hipMemcpyDeviceToHost, st));
         if (segs)
             SMJ_CHECK(hipMemcpyAsync(hseg + (size_t)r * nb * kShards, a.seg_cnt[r],
@@ -1146,7 +1562,6 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
     // dense output start of every bucket (partition regions may have slack)
     uint64_t* hdst = (uint64_t*)ws->host_pinned("bs_hdst", (size_t)2 * nb * 8);
     uint64_t* ostart[2] = {nullptr, nullptr};
-    uint64_t maxb[2] = {0, 0};
     for (int r = 0; r < nrel; r++) {
         uint32_t* bt0 = hbt + r * (nb + 1);
         uint32_t acc = 0;
@@ -1161,7 +1576,6 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
             } else {
                 acc += (uint32_t)((hcnt[r * nb + b] + TILE2 - 1) / TILE2);
             }
-            maxb[r] = std::max<uint64_t>(maxb[r], hcnt[r * nb + b]);
         }
         bt0[nb] = acc;
         const uint64_t ntl = acc ? acc : 1;
@@ -1182,39 +1596,6 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
     }
     if (nrel == 1) tt[1] = tt[0];
     if (a.ev_tile) SMJ_CHECK(hipEventRecord(a.ev_tile, st));
-
-    // (the ring needs buckets contiguous in the partition buffer)
-    const uint64_t ring = segs ? 0 : ring_tuples();
-    Tup* ringbuf[2] = {nullptr, nullptr};
-    uint64_t ringcap[2] = {0, 0};
-    if (ring) {
-        for (int r = 0; r < nrel; r++) {
-            ringcap[r] = std::max<uint64_t>(ring, maxb[r] + 2 * kTileTuples);
-            ringbuf[r] = (Tup*)ws->scratch(r ? "bs_ring1" : "bs_ring0",
-                                           ringcap[r] * sizeof(Tup));
-        }
-    }
-    // batches [b0, b1): every relation's tuples of the batch fit its ring
-    std::vector<std::pair<uint32_t, uint32_t>> batches;
-    if (!ring) {
-        batches.push_back({0u, nb});
-    } else {
-        uint32_t b0 = 0;
-        while (b0 < nb) {
-            uint32_t b1 = b0;
-            while (b1 < nb) {
-                // span of buckets b0..b1 in the partition buffer (with slack)
-                bool fits = true;
-                for (int r = 0; r < nrel; r++)
-                    if (hst[r * nb + b1] + hcnt[r * nb + b1] - hst[r * nb + b0] > ringcap[r])
-                        fits = false;
-                if (!fits && b1 > b0) break;
-                b1++;
-            }
-            batches.push_back({b0, b1});
-            b0 = b1;
-        }
-    }
 
     const uint32_t ngroups = nb * nb2;
     const uint32_t ovf_cap = ngroups;
@@ -1246,41 +1627,30 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
     G.ovf = ovf;
     G.novf = novf;
     G.ovf_cap = ovf_cap;
-    bool ev_bucket_done = false;
-    for (const auto& bt : batches) {
-        const uint32_t b0 = bt.first, b1 = bt.second;
-        uint32_t ntiles = 0;
-        for (int r = 0; r < 2; r++) {
-            const int rr = r < nrel ? r : 0;
-            Tup* tmp = a.tmp[rr];
-            // ring: tile offsets of the batch start at hst[b0] -> ring[0]
-            if (ring) tmp = ringbuf[rr] - (ptrdiff_t)hst[rr * nb + b0];
-            T.tmp[r] = tmp;
-            G.tmp[r] = tmp;
-            if (r < nrel) {
-                const uint32_t* bt0 = hbt + r * (nb + 1);
-                T.t0[r] = bt0[b0];
-                T.nt[r] = bt0[b1] - bt0[b0];
-                ntiles += T.nt[r];
-            }
+    uint32_t ntiles = 0;
+    for (int r = 0; r < 2; r++) {
+        const int rr = r < nrel ? r : 0;
+        T.tmp[r] = a.tmp[rr];
+        G.tmp[r] = a.tmp[rr];
+        if (r < nrel) {
+            T.t0[r] = 0;
+            T.nt[r] = hbt[r * (nb + 1) + nb];
+            ntiles += T.nt[r];
         }
-        if (ntiles) {
-            {
-                TraceScope ts(ws, "k_tilepass", st);
-                hipLaunchKernelGGL(k_tilepass, dim3(ntiles), dim3(TP_THREADS), tp_lds,
-                                   st, T);
-            }
-            // the batch's rows only (a ring batch rewrites its tiles' rows)
-            launch_preft_range(T, nrel, nb2, st);
+    }
+    if (ntiles) {
+        {
+            TraceScope ts(ws, "k_tilepass", st);
+            hipLaunchKernelGGL(k_tilepass, dim3(ntiles), dim3(TP_THREADS), tp_lds, st, T);
         }
-        if (a.ev_bucket && !ev_bucket_done) {
-            SMJ_CHECK(hipEventRecord(a.ev_bucket, st));
-            ev_bucket_done = true;
-        }
-        G.g_begin = b0 * nb2;
-        G.g_end = b1 * nb2;
+        launch_preft_range(T, nrel, nb2, st);
+    }
+    if (a.ev_bucket) SMJ_CHECK(hipEventRecord(a.ev_bucket, st));
+    G.g_begin = 0;
+    G.g_end = nb * nb2;
+    {
+        // persistent: GS_WG_PER_CU workgroups per CU, consecutive groups each
         const uint32_t ng = G.g_end - G.g_begin;
-        // persistent: two workgroups per CU, consecutive groups per workgroup
         const uint32_t maxwg = GS_WG_PER_CU * 256;
         G.per = (ng + maxwg - 1) / maxwg;
         const uint32_t nwg = (ng + G.per - 1) / G.per;
@@ -1301,39 +1671,7 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
         fprintf(stderr, "[ERROR] smj: overflow table too small\n");
         abort();
     }
-    std::vector<OvfEntry> he(no);
-    SMJ_CHECK(hipMemcpyAsync(he.data(), ovf, no * sizeof(OvfEntry),
-                             hipMemcpyDeviceToHost, st));
-    SMJ_CHECK(hipStreamSynchronize(st));
-    if (getenv("SMJ_DEBUG_OVF")) {
-        fprintf(stderr, "[smj] %u overflow groups (nb %u, nb2 %u)\n", no, nb, nb2);
-        for (uint32_t i = 0; i < no && i < 64; i++)
-            fprintf(stderr, "[smj]   b %u g %u nR %u nS %u outR %llu outS %llu\n",
-                    he[i].bucket, he[i].d2, he[i].nr[0], he[i].nr[1],
-                    (unsigned long long)(hdst[he[i].bucket] + he[i].off[0]),
-                    (unsigned long long)(hdst[nb + he[i].bucket] + he[i].off[1]));
-    }
-    for (int r = 0; r < nrel; r++) {
-        std::vector<uint64_t> so(no), sl(no);
-        for (uint32_t i = 0; i < no; i++) {
-            so[i] = hdst[r * nb + he[i].bucket] + he[i].off[r];
-            sl[i] = he[i].nr[r];
-        }
-        segmented_sort(ws, a.out[r], so.data(), sl.data(), no, st);
-    }
-    if (nrel == 2) {
-        std::vector<const Tup*> rp, sp;
-        std::vector<uint64_t> nr, ns;
-        for (uint32_t i = 0; i < no; i++) {
-            if (he[i].counted || !he[i].nr[0] || !he[i].nr[1]) continue;
-            rp.push_back(a.out[0] + hdst[he[i].bucket] + he[i].off[0]);
-            sp.push_back(a.out[1] + hdst[nb + he[i].bucket] + he[i].off[1]);
-            nr.push_back(he[i].nr[0]);
-            ns.push_back(he[i].nr[1]);
-        }
-        merge_join_count_batch(ws, rp.data(), nr.data(), sp.data(), ns.data(),
-                               (uint32_t)rp.size(), a.count_dev, st);
-    }
+    skew_path(ws, G, ovf, no, hdst, nb, st);
     SMJ_CHECK(hipGetLastError());
     return true;
 }

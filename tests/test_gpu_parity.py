@@ -282,3 +282,64 @@ def test_device_generators(libs, width):
     # Zipf(0.75): rank-1 share = 1/H(100000, 0.75)
     H = np.sum(1.0 / np.arange(1, 100001) ** 0.75)
     assert abs(top[0] / n - 1 / H) < 0.15 / H
+
+
+# ------------------------------------------------------------ skew path
+def _hot_inputs(orc, width, n, payload):
+    """R = PK 1..n; half of S is key 7 (one group far beyond LDS: the split
+    skew kernels), a tenth is key 1000 (a small skew group), the rest FK."""
+    orc.seed(12345)
+    R = orc.create_relation_mway(n, n)
+    orc.seed(54321)
+    S = orc.create_relation_mway(n, n)
+    S["key"][: n // 2] = 7
+    S["key"][n // 2: n // 2 + n // 10] = 1000
+    if payload == "equal":
+        S["payload"] = 0
+    else:  # descending payloads: equal-key runs come out of order
+        S["payload"] = np.arange(n, 0, -1)
+    return R, S
+
+
+@pytest.mark.parametrize("payload", ["equal", "descending"])
+@pytest.mark.parametrize("hint", [True, False])
+def test_device_join_hot_keys(libs, oracles, width, payload, hint):
+    """Groups too large for LDS: counting-sorted on the device (exact last
+    digit); equal-key runs out of payload order fall back to the segmented
+    merge sort.  With the key-range hint the host-planned path runs, without
+    it the sampled plan."""
+    import torch
+    orc, lib = oracles[width], libs[width]
+    n = 1 << 20
+    R, S = _hot_inputs(orc, width, n, payload)
+    exp, eR, eS = orc.sortmergejoin(R, S)
+    dR, dS = lib.to_device(R), lib.to_device(S)
+    sR, sS = lib.empty(n), lib.empty(n)
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    if hint:
+        lib.dev_join(dR, dS, sR, sS, cnt, 9, 1, n)
+    else:
+        lib.dev_join(dR, dS, sR, sS, cnt)
+    torch.cuda.synchronize()
+    assert int(cnt.item()) == exp
+    assert np.array_equal(lib.to_host(sR), eR)
+    assert np.array_equal(lib.to_host(sS), eS)
+
+
+def test_device_join_keys_outside_hint(libs, oracles, width):
+    """A key-range hint narrower than the data: keys outside clamp to the end
+    digits (order kept), the last digit is then not exact and the clamped
+    groups take the merge-sort and merge-join fallback."""
+    import torch
+    orc, lib = oracles[width], libs[width]
+    n = 300000
+    R, S = make_join_inputs(orc, width, "pk_fk", n, n)
+    exp, eR, eS = orc.sortmergejoin(R, S)
+    dR, dS = lib.to_device(R), lib.to_device(S)
+    sR, sS = lib.empty(n), lib.empty(n)
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    lib.dev_join(dR, dS, sR, sS, cnt, 9, n // 4, n // 2)
+    torch.cuda.synchronize()
+    assert int(cnt.item()) == exp
+    assert np.array_equal(lib.to_host(sR), eR)
+    assert np.array_equal(lib.to_host(sS), eS)
