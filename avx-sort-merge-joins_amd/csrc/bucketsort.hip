@@ -1419,7 +1419,7 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
     uint32_t* ntiles[2] = {nullptr, nullptr};
     uint32_t ub[2] = {0, 0};
     for (int r = 0; r < nrel; r++) {
-        ub[r] = (uint32_t)((a.n[r] + TILE2 - 1) / TILE2 + (uint64_t)nb * kShards);
+        ub[r] = (uint32_t)((a.n[r] + TILE2 - 1) / TILE2 + (uint64_t)nb * a.nseg);
         tt[r].off = (uint64_t*)ws->scratch(names[r][0], (size_t)ub[r] * 8);
         tt[r].len = (uint32_t*)ws->scratch(names[r][1], (size_t)ub[r] * 4);
         tt[r].bucket = (uint32_t*)ws->scratch(names[r][2], (size_t)ub[r] * 4);
@@ -1430,9 +1430,9 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
         ostart[r] = (uint64_t*)ws->scratch(names[r][5], (size_t)nb * 8);
         ntiles[r] = (uint32_t*)ws->scratch(names[r][6], 4);
         hipLaunchKernelGGL(k_seg_scan, dim3(1), dim3(256), 0, st, a.seg_cnt[r],
-                           a.bcount[r], nb, kShards, tt[r].btile0, ntiles[r], ostart[r]);
+                           a.bcount[r], nb, a.nseg, tt[r].btile0, ntiles[r], ostart[r]);
         hipLaunchKernelGGL(k_tiles, dim3(nb), dim3(64), 0, st, a.bstart[r],
-                           a.bcount[r], a.seg_start[r], a.seg_cnt[r], kShards, tt[r]);
+                           a.bcount[r], a.seg_start[r], a.seg_cnt[r], a.nseg, tt[r]);
     }
     if (nrel == 1) tt[1] = tt[0];
     if (a.ev_tile) SMJ_CHECK(hipEventRecord(a.ev_tile, st));
@@ -1535,14 +1535,14 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
     uint64_t* hcnt = (uint64_t*)ws->host_pinned("bs_hcnt", (size_t)2 * nb * 8);
     RangePlan* hplan = (RangePlan*)ws->host_pinned("bs_hplan", sizeof(RangePlan));
     const bool segs = a.seg_start[0] != nullptr;
-    const uint32_t nseg = segs ? kShards : 1;
-    int64_t* hseg = (int64_t*)ws->host_pinned("bs_hseg", (size_t)2 * nb * kShards * 8);
+    const uint32_t nseg = segs ? a.nseg : 1;
+    int64_t* hseg = (int64_t*)ws->host_pinned("bs_hseg", (size_t)2 * nb * nseg * 8);
     for (int r = 0; r < nrel; r++) {
         SMJ_CHECK(hipMemcpyAsync(hcnt + r * nb, a.bcount[r], nb * 8,
                                  hipMemcpyDeviceToHost, st));
         if (segs)
-            SMJ_CHECK(hipMemcpyAsync(hseg + (size_t)r * nb * kShards, a.seg_cnt[r],
-                                     (size_t)nb * kShards * 8, hipMemcpyDeviceToHost, st));
+            SMJ_CHECK(hipMemcpyAsync(hseg + (size_t)r * nb * nseg, a.seg_cnt[r],
+                                     (size_t)nb * nseg * 8, hipMemcpyDeviceToHost, st));
     }
     SMJ_CHECK(hipMemcpyAsync(hplan, a.plan_dev, sizeof(RangePlan),
                              hipMemcpyDeviceToHost, st));
@@ -1571,8 +1571,8 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
             dacc += hcnt[r * nb + b];
             bt0[b] = acc;
             if (segs) {
-                for (uint32_t q = 0; q < kShards; q++)
-                    acc += (uint32_t)((hseg[((size_t)r * nb + b) * kShards + q] + TILE2 - 1) / TILE2);
+                for (uint32_t q = 0; q < nseg; q++)
+                    acc += (uint32_t)((hseg[((size_t)r * nb + b) * nseg + q] + TILE2 - 1) / TILE2);
             } else {
                 acc += (uint32_t)((hcnt[r * nb + b] + TILE2 - 1) / TILE2);
             }

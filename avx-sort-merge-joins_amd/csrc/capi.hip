@@ -1051,6 +1051,105 @@ void smj_dev_join(smj_workspace* ws, const tuple_t* R, uint64_t nR,
                 count_dev, (hipStream_t)stream);
 }
 
+// Segment tables of an exchanged relation: the receive buffer holds, for
+// every source s in order, that source's partitions 0..nb-1 back to back
+// (cnt[s * nb + b] tuples each).  Bucket b = the nseg segments
+// seg_start/seg_cnt[b * nseg + s]; bucket starts are 0 (offsets absolute).
+__global__ void __launch_bounds__(256)
+k_seg_tables(const int64_t* __restrict__ cnt, uint32_t nseg, uint32_t nb,
+             uint64_t* __restrict__ seg_start, int64_t* __restrict__ seg_cnt,
+             int64_t* __restrict__ bcount, uint64_t* __restrict__ bstart) {
+    __shared__ uint32_t scr[5];
+    __shared__ unsigned long long base;
+    if (threadIdx.x == 0) base = 0;
+    for (uint32_t b = threadIdx.x; b < nb; b += 256) {
+        bcount[b] = 0;
+        bstart[b] = 0;
+    }
+    __syncthreads();
+    for (uint32_t s = 0; s < nseg; s++) {
+        for (uint32_t b0 = 0; b0 < nb; b0 += 256) {
+            const uint32_t b = b0 + threadIdx.x;
+            const int64_t c = b < nb ? cnt[(size_t)s * nb + b] : 0;
+            uint32_t tot;  // a source sends < 2^32 tuples (checked by the host)
+            const uint32_t ex = block_exclusive_scan((uint32_t)c, scr, &tot);
+            if (b < nb) {
+                seg_start[(size_t)b * nseg + s] = base + ex;
+                seg_cnt[(size_t)b * nseg + s] = c;
+                bcount[b] += c;
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) base += tot;
+            __syncthreads();
+        }
+    }
+}
+
+void smj_dev_join_segmented(smj_workspace* wsp, tuple_t* R, uint64_t nR,
+                            const int64_t* segR, tuple_t* S, uint64_t nS,
+                            const int64_t* segS, uint32_t nseg, uint32_t bucket_bits,
+                            int64_t key_lo, int64_t key_hi, tuple_t* sortedR,
+                            tuple_t* sortedS, unsigned long long* count_dev,
+                            smj_stream_t stream) {
+    Workspace* ws = (Workspace*)wsp;
+    hipStream_t st = (hipStream_t)stream;
+    if (nseg == 0 || bucket_bits > 10 || nR >= (1ull << 32) || nS >= (1ull << 32)) {
+        fprintf(stderr, "[ERROR] smj_dev_join_segmented: nseg %u, bucket_bits %u "
+                "(<= 10), nR %llu, nS %llu (< 2^32)\n", nseg, bucket_bits,
+                (unsigned long long)nR, (unsigned long long)nS);
+        abort();
+    }
+    SMJ_CHECK(hipMemsetAsync(count_dev, 0, sizeof(unsigned long long), st));
+    uint32_t D1, D2, D2cap;
+    choose_levels(nR > nS ? nR : nS, bucket_bits, &D1, &D2, &D2cap);
+    // the buckets are the exchanged partitions: level 1 is fixed
+    const uint32_t tot_bits = D1 + D2;
+    D1 = bucket_bits;
+    D2 = tot_bits > D1 ? tot_bits - D1 : 0;
+    if (D2 > 9) D2 = 9;
+    D2cap = D2 + 2 > 9 ? (D2 > 9 ? D2 : 9) : D2 + 2;
+    RangePlan hplan = make_plan(key_lo, key_hi, D1, D2, D2cap, kGroupD3Max);
+    RangePlan* plan = (RangePlan*)ws->scratch("plan", sizeof(RangePlan));
+    hipLaunchKernelGGL(k_setplan, dim3(1), dim3(1), 0, st, plan, hplan);
+    const uint32_t nb = 1u << D1;
+    Tup* rel[2] = {(Tup*)R, (Tup*)S};
+    const int64_t* seg[2] = {segR, segS};
+    static const char* nm[2][4] = {{"xs_startR", "xs_cntR", "xs_bcR", "xs_bsR"},
+                                   {"xs_startS", "xs_cntS", "xs_bcS", "xs_bsS"}};
+    BucketSortArgs a;
+    for (int r = 0; r < 2; r++) {
+        uint64_t* ss = (uint64_t*)ws->scratch(nm[r][0], (size_t)nb * nseg * 8);
+        int64_t* sc = (int64_t*)ws->scratch(nm[r][1], (size_t)nb * nseg * 8);
+        int64_t* bc = (int64_t*)ws->scratch(nm[r][2], (size_t)nb * 8);
+        uint64_t* bs = (uint64_t*)ws->scratch(nm[r][3], (size_t)nb * 8);
+        hipLaunchKernelGGL(k_seg_tables, dim3(1), dim3(256), 0, st, seg[r], nseg, nb,
+                           ss, sc, bc, bs);
+        a.part[r] = rel[r];
+        a.tmp[r] = rel[r];  // the tile pass works in place in the receive buffer
+        a.bstart[r] = bs;
+        a.bcount[r] = bc;
+        a.seg_start[r] = ss;
+        a.seg_cnt[r] = sc;
+    }
+    a.nseg = nseg;
+    a.out[0] = (Tup*)sortedR;
+    a.out[1] = (Tup*)sortedS;
+    a.n[0] = nR;
+    a.n[1] = nS;
+    a.nrel = 2;
+    a.nbuckets = nb;
+    a.plan_dev = plan;
+    a.count_dev = count_dev;
+    unsigned int* flag = (unsigned int*)ws->scratch("xs_flag", 4);
+    SMJ_CHECK(hipMemsetAsync(flag, 0, 4, st));
+    a.part_flag = flag;  // never set: the buckets are exact
+    a.host_plan = &hplan;
+    if (!bucket_sort(ws, a, st)) {
+        fprintf(stderr, "[ERROR] smj_dev_join_segmented: unexpected partition flag\n");
+        abort();
+    }
+}
+
 void smj_join_phase_ms(smj_workspace* wsp, float* ms5) {
     Workspace* ws = (Workspace*)wsp;
     for (int i = 0; i < 5; i++) ms5[i] = 0.f;

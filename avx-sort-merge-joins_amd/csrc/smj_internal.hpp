@@ -171,6 +171,7 @@ struct BucketSortArgs {
     // [seg_start[b*kShards+q], + seg_cnt[...]) inside its region
     const uint64_t* seg_start[2] = {nullptr, nullptr};
     const int64_t* seg_cnt[2] = {nullptr, nullptr};
+    uint32_t nseg = kShards;    // segments per bucket (the exchange: one per source GPU)
     Tup* tmp[2];                // same size as part (tile-local pass output)
     Tup* out[2];                // sorted output, bucket b at ostart[b]
     uint64_t n[2];

@@ -7,30 +7,79 @@ its own ranges, and the per-thread counts are summed
 (src/joins/sortmergejoin_multiway.c:195-330, threads joined in
 src/joins/joincommon.c:140-260).  Here a rank plays the part of a thread:
 
-1. range-partition the local slices of R and S on the device
-   (``smj_dev_partition_range``: monotone digit of the key over the global key
-   range, so partition p holds a contiguous key interval);
+1. range-partition the local slices of R and S on the device into
+   F = 2^pbits partitions (``smj_dev_partition_range``: the library's range
+   plan over the GLOBAL key range, so partition p holds one contiguous key
+   interval of width 2^s1);
 2. partition p is owned by rank ``p * world // F`` -- contiguous, balanced
    ownership, so every key lands on exactly one rank;
-3. one ``all_to_all_single`` of the per-owner counts, then one of the rows
-   (RCCL over xGMI on the GPU, gloo in the CPU tests): each rank receives its
-   whole key ranges of R and S;
-4. the local join (``smj_dev_join``), then an ``all_reduce`` of the count.
+3. per relation one ``all_to_all_single`` of the owned partition sizes and
+   one of the rows (RCCL over xGMI on the GPU, gloo in the CPU tests).  The
+   row exchange of R is asynchronous: it runs on the communication stream
+   while S is partitioned;
+4. the received partitions ARE the level-1 buckets of the local sort
+   (``smj_dev_join_segmented``: source s's partitions back to back, one
+   segment per source), so the local join starts at its tile pass -- no
+   second partition pass -- then an ``all_reduce`` of the count.
 
 The class is written against a small ``ops`` interface (``empty``,
-``partition_range``, ``join``) so that the orchestration the GPU bench runs is
-the same code the CPU multi-process tests run (with host stand-ins for the
-device ops that live in tests/).
+``partition_range``, ``join_segmented``) so that the orchestration the GPU
+bench runs is the same code the CPU multi-process tests run (with host
+stand-ins for the device ops that live in tests/).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
+
+MAX_PARTITION_BITS = 12  # widest single-pass partition digit of the library
+# Largest single message of the row exchange.  RCCL 2.26 (torch 2.10 ROCm)
+# corrupts all_to_all_single messages of 1.6 GB and more (tools/debug_a2a.py);
+# larger exchanges go as chunked point-to-point sends in one group.
+CHUNK_BYTES = int(os.environ.get("SMJ_A2A_CHUNK_MB", "512")) << 20
+
+
+class _Works:
+    """wait() on several collective works (or none)."""
+
+    def __init__(self, works):
+        self.works = [w for w in works if w is not None]
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
 
 
 def owners(fanout: int, world: int) -> torch.Tensor:
     """Owner rank of each of the `fanout` range partitions (contiguous)."""
     return torch.arange(fanout, dtype=torch.int64) * world // fanout
+
+
+def owned(fanout: int, world: int, rank: int) -> tuple[int, int]:
+    """[first, last) partition owned by `rank` (the inverse of owners)."""
+    lo = -(-rank * fanout // world)
+    hi = -(-(rank + 1) * fanout // world)
+    return lo, hi
+
+
+def plan_shift(key_min: int, key_max: int, bits: int) -> int:
+    """s1 of the library's range plan (smj_common.hpp make_plan): partition
+    p covers keys [key_min + p * 2^s1, key_min + (p + 1) * 2^s1)."""
+    width = max(key_max - key_min, 0)
+    return max(width.bit_length() - bits, 0)
+
+
+def range_digit(keys: torch.Tensor, key_min: int, key_max: int, bits: int) -> torch.Tensor:
+    """The level-1 digit of the range plan (plan_rel + d1), for host stand-ins."""
+    L = max(key_max - key_min, 0).bit_length()
+    rel = (keys.to(torch.int64) - key_min).clamp(0, (1 << L) - 1)
+    return rel >> plan_shift(key_min, key_max, bits)
+
+
+def ceil_log2(x: int) -> int:
+    return max(x - 1, 0).bit_length()
 
 
 def send_counts(hist: torch.Tensor, world: int) -> torch.Tensor:
@@ -52,29 +101,37 @@ class DeviceOps:
     def partition_range(self, inp, out, nbits, key_min, key_max, hist):
         self.lib.dev_partition_range(inp, out, nbits, key_min, key_max, hist)
 
-    def join(self, R, S, sR, sS, count):
-        # the local key range is a 1/world slice of the global one: let the
-        # library sample it (key_max = 0) rather than plan for the global span
-        self.lib.dev_join(R, S, sR, sS, count, 9, 1, 0)
+    def join_segmented(self, R, segR, S, segS, bucket_bits, key_lo, key_hi, sR, sS, count):
+        self.lib.dev_join_segmented(R, segR, S, segS, bucket_bits, key_lo, key_hi,
+                                    sR, sS, count)
 
 
 class DistributedJoin:
     """One process per device; `step` joins the local slices of R and S
     against the slices on all other ranks and leaves the GLOBAL match count in
-    `count` on every rank."""
+    `count` on every rank.  `bucket_bits`: level-1 buckets per rank (2^9 =
+    512, what the 1-GPU join uses)."""
 
-    def __init__(self, ops, fanout_bits: int, key_min: int, key_max: int,
+    def __init__(self, ops, bucket_bits: int, key_min: int, key_max: int,
                  group=None):
         self.ops = ops
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
-        self.bits = fanout_bits
-        self.fanout = 1 << fanout_bits
+        self.pbits = min(bucket_bits + ceil_log2(self.world), MAX_PARTITION_BITS)
+        self.fanout = 1 << self.pbits
         if self.fanout < self.world:
-            raise ValueError(f"fanout 2^{fanout_bits} < world size {self.world}")
+            raise ValueError(f"fanout 2^{self.pbits} < world size {self.world}")
         self.key_min = key_min
         self.key_max = key_max
+        F, G = self.fanout, self.world
+        self.per_rank = [owned(F, G, g)[1] - owned(F, G, g)[0] for g in range(G)]
+        self.p_lo, self.p_hi = owned(F, G, self.rank)
+        # the local plan: this rank's partitions are its level-1 buckets
+        self.lbits = ceil_log2(max(self.p_hi - self.p_lo, 1))
+        s1 = plan_shift(key_min, key_max, self.pbits)
+        self.key_lo = key_min + (self.p_lo << s1)
+        self.key_hi = self.key_lo + (1 << (s1 + self.lbits)) - 1
         self.buf = {}
         self.last_recv = {}
 
@@ -85,29 +142,66 @@ class DistributedJoin:
             self.buf[key] = b
         return b[:n]
 
-    def exchange(self, part, hist, key):
-        """All-to-all of the range partitions; returns this rank's rows."""
-        send = send_counts(hist, self.world)
-        recv = torch.empty_like(send)
-        dist.all_to_all_single(recv, send, group=self.group)
-        sl, rl = send.tolist(), recv.tolist()
+    def _exchange(self, rel, key):
+        """Partition `rel`, swap partition sizes, start the row all-to-all.
+        Returns (receive buffer, per-source sizes of the owned partitions
+        (world, 2^lbits) padded with empty buckets, async work)."""
+        G, F = self.world, self.fanout
+        dev = rel.device
+        part = self._grow("part" + key, rel.shape[0])
+        hist = torch.zeros(F, dtype=torch.int64, device=dev)
+        self.ops.partition_range(rel, part, self.pbits, self.key_min, self.key_max, hist)
+        mine = self.p_hi - self.p_lo
+        seg = torch.empty(G * mine, dtype=torch.int64, device=dev)
+        dist.all_to_all_single(seg, hist, [mine] * G, self.per_rank, group=self.group)
+        seg = seg.view(G, mine)
+        sizes = torch.cat([send_counts(hist, G), seg.sum(1)]).tolist()  # one sync
+        sl, rl = sizes[:G], sizes[G:]
         out = self._grow("recv" + key, sum(rl))
-        dist.all_to_all_single(out, part, rl, sl, group=self.group)
+        work = self._rows(out, part, rl, sl)
         self.last_recv[key] = (sl, rl)
-        return out
+        pad = torch.zeros(G, 1 << self.lbits, dtype=torch.int64, device=dev)
+        pad[:, :mine] = seg
+        return out, pad, work
+
+    def _rows(self, out, inp, rl, sl):
+        """Asynchronous row all-to-all: `inp` holds sl[g] rows for rank g in
+        rank order, `out` receives rl[g] rows from rank g.  One
+        all_to_all_single, or chunked isend/irecv pairs (one batch) when a
+        message would exceed CHUNK_BYTES; this rank's own rows are a copy."""
+        row = inp.element_size() * (inp[0].numel() if inp.dim() > 1 and inp.shape[0] else 1)
+        if max(rl + sl) * row <= CHUNK_BYTES:
+            return dist.all_to_all_single(out, inp, rl, sl, group=self.group, async_op=True)
+        so = [sum(sl[:g]) for g in range(self.world)]
+        ro = [sum(rl[:g]) for g in range(self.world)]
+        me = self.rank
+        out[ro[me]:ro[me] + rl[me]].copy_(inp[so[me]:so[me] + sl[me]])
+        step = max(CHUNK_BYTES // row, 1)
+        peers = [self._global(g) for g in range(self.world)]
+        ops = []
+        for g in range(self.world):
+            if g == me:
+                continue
+            for k in range(0, sl[g], step):
+                ops.append(dist.P2POp(dist.isend, inp[so[g] + k:so[g] + min(k + step, sl[g])],
+                                      peers[g], group=self.group))
+            for k in range(0, rl[g], step):
+                ops.append(dist.P2POp(dist.irecv, out[ro[g] + k:ro[g] + min(k + step, rl[g])],
+                                      peers[g], group=self.group))
+        return _Works(dist.batch_isend_irecv(ops) if ops else [])
+
+    def _global(self, g):
+        return g if self.group is None else dist.get_global_rank(self.group, g)
 
     def step(self, R, S, count):
-        dev = count.device
-        parts = []
-        for key, rel in (("R", R), ("S", S)):
-            part = self._grow("part" + key, rel.shape[0])
-            hist = torch.zeros(self.fanout, dtype=torch.int64, device=dev)
-            self.ops.partition_range(rel, part, self.bits, self.key_min,
-                                     self.key_max, hist)
-            parts.append(self.exchange(part, hist, key))
-        rR, rS = parts
+        # the row exchange of R overlaps the partition of S
+        rR, segR, wR = self._exchange(R, "R")
+        rS, segS, wS = self._exchange(S, "S")
+        wR.wait()
+        wS.wait()
         sR = self._grow("sortR", rR.shape[0])
         sS = self._grow("sortS", rS.shape[0])
-        self.ops.join(rR, rS, sR, sS, count)
+        self.ops.join_segmented(rR, segR, rS, segS, self.lbits, self.key_lo,
+                                self.key_hi, sR, sS, count)
         dist.all_reduce(count, group=self.group)
-        return rR, rS
+        return sR, sS

@@ -46,6 +46,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--check", action="store_true",
                    help="also verify sortedness/multiset of the sorted outputs")
+    p.add_argument("--exchange-path", action="store_true",
+                   help="run the multi-GPU code path (range partition, all-to-all, "
+                        "segmented local join) even at N=1 (a one-rank RCCL group)")
     return p.parse_args()
 
 
@@ -137,8 +140,13 @@ def main():
         print(f"[bench] --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     torch.cuda.set_device(local)
     dist = None
-    if N > 1:
+    exchange = N > 1 or a.exchange_path
+    if exchange:
         import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29531")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import smj
@@ -157,7 +165,7 @@ def main():
     torch.cuda.synchronize()
 
     count = torch.zeros(1, dtype=torch.int64, device="cuda")
-    if N == 1:
+    if not exchange:
         sR, sS = lib.empty(n), lib.empty(n)
 
         def step():
@@ -172,19 +180,19 @@ def main():
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
-    if N > 1:
+    if dist:
         dist.barrier()
     lib.trace(True)
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
     torch.cuda.synchronize()
-    if N > 1:
+    if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern = lib.trace_read()
     lib.trace(False)
-    if N > 1:
+    if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())

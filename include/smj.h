@@ -405,6 +405,24 @@ void smj_dev_partition_range(smj_workspace * ws, const tuple_t * in, uint64_t n,
                              int64_t key_max, int64_t * hist_out,
                              smj_stream_t stream);
 
+/* Local join of one GPU's share after the exchange (multi-GPU join, no
+ * reference counterpart: it replaces the per-thread multiway merge of the
+ * reference's T>1 path, src/joins/sortmergejoin_multiway.c:463-556).  R and
+ * S are the receive buffers: for every source GPU s in order, its range
+ * partitions 0..2^bucket_bits-1 back to back, seg[s * 2^bucket_bits + b]
+ * tuples each (device int64).  Every partition b covers the keys
+ * [key_lo + b * w, key_lo + (b + 1) * w) with 2^bucket_bits * w =
+ * key_hi - key_lo + 1 (a power of two), so the partitions are the level-1
+ * buckets of the local sort: no local partition pass.  R and S are used as
+ * scratch (overwritten).  sortedR/sortedS receive the sorted relations,
+ * count_dev the number of matching pairs. */
+void smj_dev_join_segmented(smj_workspace * ws, tuple_t * R, uint64_t nR,
+                            const int64_t * segR, tuple_t * S, uint64_t nS,
+                            const int64_t * segS, uint32_t nseg,
+                            uint32_t bucket_bits, int64_t key_lo, int64_t key_hi,
+                            tuple_t * sortedR, tuple_t * sortedS,
+                            unsigned long long * count_dev, smj_stream_t stream);
+
 /* Per-kernel HIP-event trace of the join pipeline (bench.py roofline). */
 void smj_trace_enable(smj_workspace * ws, int on);
 void smj_trace_reset(smj_workspace * ws);

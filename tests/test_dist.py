@@ -28,14 +28,23 @@ class HostOps:
         return torch.empty((n, 2), dtype=torch.int64)
 
     def partition_range(self, inp, out, nbits, key_min, key_max, hist):
-        F = 1 << nbits
-        span = key_max - key_min + 1
-        d = ((inp[:, 1] - key_min).clamp(0, span - 1) * F) // span
+        from smj.dist import range_digit
+        d = range_digit(inp[:, 1], key_min, key_max, nbits)
         order = torch.argsort(d, stable=True)
         out[: inp.shape[0]] = inp[order]
-        hist.copy_(torch.bincount(d, minlength=F))
+        hist.copy_(torch.bincount(d, minlength=1 << nbits))
 
-    def join(self, R, S, sR, sS, count):
+    def join_segmented(self, R, segR, S, segS, bucket_bits, key_lo, key_hi, sR, sS, count):
+        from smj.dist import range_digit
+        # the receive layout the device join relies on: source by source,
+        # local bucket b holds exactly the keys of local digit b
+        for rows, seg in ((R, segR), (S, segS)):
+            assert seg.shape[1] == 1 << bucket_bits
+            assert int(seg.sum()) == rows.shape[0]
+            d = range_digit(rows[:, 1], key_lo, key_hi, bucket_bits)
+            expect = torch.repeat_interleave(
+                torch.arange(seg.shape[1]).repeat(seg.shape[0]), seg.reshape(-1))
+            assert torch.equal(d, expect)
         r = R.numpy().reshape(-1).view(self.orc.dtype)
         s = S.numpy().reshape(-1).view(self.orc.dtype)
         c, a, b = self.orc.sortmergejoin(r, s)
@@ -49,7 +58,7 @@ def _worker(rank, world, port, n, q):
     for p in (ROOT, PKG):
         sys.path.insert(0, p)
     import oracle
-    from smj.dist import DistributedJoin, owners
+    from smj.dist import DistributedJoin, owners, range_digit
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}",
                             rank=rank, world_size=world)
@@ -71,16 +80,17 @@ def _worker(rank, world, port, n, q):
         dj = DistributedJoin(HostOps(orc), 6, 1, total)
         count = torch.zeros(1, dtype=torch.int64)
         for _ in range(2):  # second step reuses the grown buffers
-            rR, rS = dj.step(rows(R), rows(S), count)
+            sR, sS = dj.step(rows(R), rows(S), count)
             assert int(count.item()) == expect
-        # every received key is in this rank's contiguous share of the range
-        F, span = 64, total
-        own = owners(F, world)
-        for got in (rR, rS):
-            d = ((got[:, 1] - 1).clamp(0, span - 1) * F) // span
+        # every key this rank sorted is in its contiguous share of the range
+        own = owners(dj.fanout, world)
+        for got in (sR, sS):
+            d = range_digit(got[:, 1], 1, total, dj.pbits)
             assert bool((own[d] == rank).all())
+            k = got[:, 1]
+            assert bool((k[1:] >= k[:-1]).all())
         # no row lost or duplicated
-        sizes = torch.tensor([rR.shape[0], rS.shape[0]])
+        sizes = torch.tensor([sR.shape[0], sS.shape[0]])
         dist.all_reduce(sizes)
         assert sizes.tolist() == [total, total]
         q.put((rank, "ok"))
@@ -97,8 +107,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_distributed_join_gloo(world, oracles):
+@pytest.mark.parametrize("world,chunk_mb", [(2, None), (3, None), (2, 0), (3, 0)])
+def test_distributed_join_gloo(world, chunk_mb, oracles, monkeypatch):
+    """chunk_mb 0: every row message over the chunk limit, so the exchange
+    takes the chunked isend/irecv path (the one RCCL needs for >1.6 GB)."""
+    if chunk_mb is not None:
+        monkeypatch.setenv("SMJ_A2A_CHUNK_MB", str(chunk_mb))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -117,9 +131,16 @@ def test_distributed_join_gloo(world, oracles):
 def test_owners_and_send_counts():
     import sys
     sys.path.insert(0, PKG)
-    from smj.dist import owners, send_counts
+    from smj.dist import owned, owners, plan_shift, send_counts
     assert owners(8, 2).tolist() == [0, 0, 0, 0, 1, 1, 1, 1]
     assert owners(8, 3).tolist() == [0, 0, 0, 1, 1, 1, 2, 2]
+    for F, G in ((8, 3), (4096, 8), (2048, 3), (64, 5)):
+        own = owners(F, G)
+        for g in range(G):
+            lo, hi = owned(F, G, g)
+            assert own[lo:hi].eq(g).all() and int(own.eq(g).sum()) == hi - lo
+    # 1..2^30 in 4096 partitions of 2^18 keys (make_plan's s1)
+    assert plan_shift(1, 1 << 30, 12) == 18
     h = torch.arange(8)
     assert send_counts(h, 2).tolist() == [6, 22]
     assert send_counts(h, 3).tolist() == [3, 12, 13]

@@ -1,0 +1,120 @@
+"""GPU side of the multi-GPU join (smj/dist.py) on one device.
+
+* The exchange is simulated on one GPU: every "source rank" range-partitions
+  its slice with smj_dev_partition_range, the receive buffer of a rank is the
+  concatenation of the sources' owned partitions, and smj_dev_join_segmented
+  joins it; per-rank counts and sorted outputs are checked against the oracle.
+* DistributedJoin itself runs over a one-rank NCCL (RCCL) group: the same
+  code path bench.py --gpus N runs, with the collectives degenerate.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _inputs(orc, kind, n):
+    orc.seed(12345)
+    R = orc.create_relation_mway(n, n)
+    orc.seed(54321)
+    if kind == "zipf":
+        S = orc.create_relation_zipf(n, n, 0.75)
+    else:
+        S = orc.create_relation_mway(n, n)
+    return R, S
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("kind", ["pk_fk", "zipf"])
+def test_segmented_join_simulated_exchange(libs, oracles, width, world, kind):
+    import torch
+    from smj.dist import DistributedJoin, ceil_log2, owned, plan_shift
+    orc, lib = oracles[width], libs[width]
+    n = 600_000
+    R, S = _inputs(orc, kind, n)
+    total, _, _ = orc.sortmergejoin(R, S)
+    bucket_bits = 6
+    pbits = min(bucket_bits + ceil_log2(world), 12)
+    F = 1 << pbits
+    s1 = plan_shift(1, n, pbits)
+    # every source partitions its slice of R and S
+    parts = {}
+    for key, rel in (("R", R), ("S", S)):
+        for s in range(world):
+            sl = rel[s * n // world:(s + 1) * n // world]
+            d_in = lib.to_device(sl)
+            out = lib.empty(len(sl))
+            hist = torch.zeros(F, dtype=torch.int64, device="cuda")
+            lib.dev_partition_range(d_in, out, pbits, 1, n, hist)
+            torch.cuda.synchronize()
+            parts[key, s] = (out, hist)
+    got_total = 0
+    for g in range(world):
+        p_lo, p_hi = owned(F, world, g)
+        lbits = ceil_log2(max(p_hi - p_lo, 1))
+        key_lo = 1 + (p_lo << s1)
+        key_hi = key_lo + (1 << (s1 + lbits)) - 1
+        recv, segs = {}, {}
+        for key in ("R", "S"):
+            rows, seg = [], torch.zeros(world, 1 << lbits, dtype=torch.int64, device="cuda")
+            for s in range(world):
+                out, hist = parts[key, s]
+                start = int(hist[:p_lo].sum())
+                cnt = int(hist[p_lo:p_hi].sum())
+                rows.append(out[start:start + cnt])
+                seg[s, :p_hi - p_lo] = hist[p_lo:p_hi]
+            recv[key] = torch.cat(rows).contiguous()
+            segs[key] = seg
+        nR, nS = recv["R"].shape[0], recv["S"].shape[0]
+        sR, sS = lib.empty(nR), lib.empty(nS)
+        cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+        lib.dev_join_segmented(recv["R"], segs["R"], recv["S"], segs["S"], lbits,
+                               key_lo, key_hi, sR, sS, cnt)
+        torch.cuda.synchronize()
+        # the oracle on this rank's share of the key range
+        lo_k, hi_k = 1 + (p_lo << s1), 1 + (p_hi << s1)
+        mR = R[(R["key"] >= lo_k) & (R["key"] < hi_k)] if g < world - 1 else R[R["key"] >= lo_k]
+        mS = S[(S["key"] >= lo_k) & (S["key"] < hi_k)] if g < world - 1 else S[S["key"] >= lo_k]
+        exp, eR, eS = orc.sortmergejoin(mR, mS)
+        assert int(cnt.item()) == exp, (g, int(cnt.item()), exp)
+        assert np.array_equal(lib.to_host(sR), eR)
+        assert np.array_equal(lib.to_host(sS), eS)
+        got_total += exp
+    assert got_total == total
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_distributed_join_one_rank_rccl(libs, width):
+    """DistributedJoin over a one-rank RCCL group, device ops, 4M x 4M."""
+    import torch
+    import torch.distributed as dist
+    from smj.dist import DeviceOps, DistributedJoin
+    lib = libs[width]
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        n = 4_000_000
+        R, S = lib.empty(n), lib.empty(n)
+        lib.dev_gen_pk(R, 0, n, 12345)
+        lib.dev_gen_fk(S, 0, n, n, 54321)
+        dj = DistributedJoin(DeviceOps(lib), 9, 1, n)
+        count = torch.zeros(1, dtype=torch.int64, device="cuda")
+        for _ in range(2):
+            sR, sS = dj.step(R, S, count)
+            torch.cuda.synchronize()
+            assert int(count.item()) == n
+        ref = torch.sort(S[:, 1].to(torch.int64)).values
+        assert torch.equal(sS[:, 1].to(torch.int64), ref)
+        assert torch.equal(sR[:, 1].to(torch.int64), torch.arange(1, n + 1, device="cuda"))
+    finally:
+        dist.destroy_process_group()
