@@ -129,49 +129,53 @@ k_tiles(const uint64_t* __restrict__ bstart, const int64_t* __restrict__ bcount,
 // written to tmp[r][off]: `tmp` is either the partition buffer itself (in
 // place) or any buffer of the same layout.
 struct TilePassArgs {
-    const Tup* part[2];
-    Tup* tmp[2];
+    const void* part[2];  // Lay::W elements
+    void* tmp[2];
     TileTable tt[2];
     uint32_t t0[2];
     uint32_t nt[2];               // blocks of relation r (an upper bound when...)
     const uint32_t* ntiles[2];    // ...the tile count is only known on the device
     RangePlan plan;  // by value: kernel arguments live in SGPRs
     uint32_t nb2;
+    const unsigned int* pack_bad;  // set: the packed partition is void, exit
 };
 
+template <class Lay>
 __global__ void __launch_bounds__(TP_THREADS)
 k_tilepass(TilePassArgs A) {
+    typedef typename Lay::W W;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    if (A.pack_bad && *A.pack_bad) return;
     const RangePlan& P = A.plan;
     const uint32_t nb2 = A.nb2;
-    Tup* stage = reinterpret_cast<Tup*>(lds_raw);
-    uint32_t* hist = reinterpret_cast<uint32_t*>(lds_raw + TILE2 * sizeof(Tup));
+    W* stage = reinterpret_cast<W*>(lds_raw);
+    uint32_t* hist = reinterpret_cast<uint32_t*>(lds_raw + TILE2 * sizeof(W));
     uint32_t* scr = hist + nb2;
 
     const int r = blockIdx.x < A.nt[0] ? 0 : 1;
     const uint32_t t = A.t0[r] + (r ? blockIdx.x - A.nt[0] : blockIdx.x);
     if (A.ntiles[r] && t >= *A.ntiles[r]) return;
     const TileTable& tt = A.tt[r];
-    const Tup* __restrict__ part = A.part[r];
-    Tup* __restrict__ tmp = A.tmp[r];
+    const W* __restrict__ part = static_cast<const W*>(A.part[r]);
+    W* __restrict__ tmp = static_cast<W*>(A.tmp[r]);
     const uint64_t off = tt.off[t];
     const uint32_t len = tt.len[t];
     const uint32_t b = tt.bucket[t];
 
     for (uint32_t d = threadIdx.x; d < nb2; d += TP_THREADS) hist[d] = 0;
-    Tup v[TP_ITEMS];
+    W v[TP_ITEMS];
     uint32_t dg[TP_ITEMS];
 #pragma unroll
     for (int j = 0; j < TP_ITEMS; j++) {
         uint32_t i = j * TP_THREADS + threadIdx.x;
-        if (i < len) v[j] = ld_stream(part + off + i);
+        if (i < len) v[j] = part[off + i];
     }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < TP_ITEMS; j++) {
         uint32_t i = j * TP_THREADS + threadIdx.x;
         if (i < len) {
-            dg[j] = plan_d2(P, plan_rel(P, tup_key(v[j])), b);
+            dg[j] = plan_d2(P, Lay::rel(P, v[j], b), b);
             atomicAdd(&hist[dg[j]], 1u);
         }
     }
@@ -210,7 +214,7 @@ k_tilepass(TilePassArgs A) {
 #pragma unroll
     for (int j = 0; j < TP_ITEMS; j++) {
         uint32_t i = j * TP_THREADS + threadIdx.x;
-        if (i < len) st_stream(tmp + off + i, stage[i]);
+        if (i < len) st_w(tmp + off + i, stage[i]);
     }
 }
 
@@ -245,7 +249,7 @@ k_preft(TileTable tt0, TileTable tt1, uint32_t nb0, const uint32_t* __restrict__
 
 // ---------------------------------------------------------------------------
 struct GroupArgs {
-    const Tup* tmp[2];
+    const void* tmp[2];  // Lay::W elements (tile-pass output)
     Tup* out[2];
     const uint64_t* bstart[2];  // bucket start in the partition / tmp buffer
     const uint64_t* ostart[2];  // bucket start in the (dense) output
@@ -259,6 +263,7 @@ struct GroupArgs {
     OvfEntry* ovf;
     uint32_t* novf;
     uint32_t ovf_cap;
+    const unsigned int* pack_bad;  // set: the packed partition is void, exit
 };
 
 // threadIdx.x behind an empty asm: per-thread LDS addresses are recomputed
@@ -270,8 +275,9 @@ __device__ __forceinline__ uint32_t otid() {
     return t;
 }
 
+template <class W>
 struct GroupLDS {
-    Tup B[GS_CAP + 1];                    // one relation's group (+ a dump slot)
+    W B[GS_CAP + 1];                      // one relation's group (+ a dump slot)
     uint32_t cnt[2][GS_NB3 / 2];          // d3 histograms of R and S (2 x u16)
     uint32_t cur[GS_NB3 / 2];             // placement cursors (2 x u16)
     uint32_t runoff[2][GS_TMAX + 1];      // run t starts at position runoff[t]
@@ -400,11 +406,12 @@ __device__ __forceinline__ unsigned long long block_scan64(unsigned long long v,
     return r;
 }
 
-__device__ __forceinline__ void insertion_sort(Tup* a, uint32_t n) {
+template <class Lay>
+__device__ __forceinline__ void insertion_sort(typename Lay::W* a, uint32_t n) {
     for (uint32_t i = 1; i < n; i++) {
-        Tup x = a[i];
+        typename Lay::W x = a[i];
         uint32_t j = i;
-        while (j > 0 && tup_less(x, a[j - 1])) {
+        while (j > 0 && Lay::less(x, a[j - 1])) {
             a[j] = a[j - 1];
             j--;
         }
@@ -414,7 +421,8 @@ __device__ __forceinline__ void insertion_sort(Tup* a, uint32_t n) {
 
 // Group tables in LDS: wave r builds relation r's run table, run-start bitmap
 // and window tiles (no block barrier inside; one at the end).
-__device__ __forceinline__ void build_tables(const GroupArgs& A, GroupLDS& L,
+template <class LDS>
+__device__ __forceinline__ void build_tables(const GroupArgs& A, LDS& L,
                                              const GroupMeta& M) {
     const uint32_t wid = otid() >> 6, lane = otid() & 63;
     if (wid < (uint32_t)A.nrel) {
@@ -470,7 +478,8 @@ __device__ __forceinline__ void build_tables(const GroupArgs& A, GroupLDS& L,
 // queued: its size and offset in each relation come from the prefix table,
 // its tuples are sorted and counted afterwards by the skew kernels below, over
 // many workgroups.  Called by the whole workgroup (uniform control flow).
-__device__ __forceinline__ void group_overflow(const GroupArgs& A, GroupLDS& L,
+template <class LDS>
+__device__ __forceinline__ void group_overflow(const GroupArgs& A, LDS& L,
                                                const GroupMeta& M) {
     uint32_t nn[2] = {0, 0};
     uint64_t oo[2] = {0, 0};
@@ -511,11 +520,12 @@ __device__ __forceinline__ void group_overflow(const GroupArgs& A, GroupLDS& L,
 
 // gather relation r's group into registers (loads only: every load in
 // flight at once); lanes past the end re-read the last element
-__device__ __forceinline__ void gather_group(const GroupArgs& A, GroupLDS& L,
+template <class Lay>
+__device__ __forceinline__ void gather_group(const GroupArgs& A, GroupLDS<typename Lay::W>& L,
                                              const GroupMeta& C, int r, uint32_t n,
-                                             Tup (&v)[GS_ITEMS]) {
+                                             typename Lay::W (&v)[GS_ITEMS]) {
     if (n == 0) return;
-    const Tup* tp = A.tmp[r] + C.bst[r];
+    const typename Lay::W* tp = static_cast<const typename Lay::W*>(A.tmp[r]) + C.bst[r];
     const uint32_t last = n - 1;
 #pragma unroll
     for (int k = 0; k < GS_ITEMS; k++) {
@@ -524,11 +534,7 @@ __device__ __forceinline__ void gather_group(const GroupArgs& A, GroupLDS& L,
         const unsigned long long bits = L.smap[r][w] & (~0ull >> (63 - (j & 63)));
         const uint32_t t = bits ? L.stile[r][(w << 6) + 63 - __clzll(bits)]
                                 : L.wtile[r][w];
-#if SMJ_GATHER_NT
-        v[k] = ld_nt(tp + L.runsrc[r][t] + (j - L.runoff[r][t]));
-#else
-        v[k] = ld_stream(tp + L.runsrc[r][t] + (j - L.runoff[r][t]));
-#endif
+        v[k] = tp[L.runsrc[r][t] + (j - L.runoff[r][t])];
     }
 }
 
@@ -537,24 +543,21 @@ __device__ __forceinline__ void gather_group(const GroupArgs& A, GroupLDS& L,
 // as the elements sit in LDS (the registers are free): the persistent loop
 // issues the next group's gather there.  Returns false when the group must
 // take the skew path.
-template <typename Hook>
-__device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS& L,
+template <class Lay, typename Hook>
+__device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS<typename Lay::W>& L,
                                            const GroupMeta& C, const RangePlan& P,
                                            int r, uint32_t nr, uint32_t off,
-                                           Tup (&v)[GS_ITEMS], bool& clamped,
+                                           typename Lay::W (&v)[GS_ITEMS], bool& clamped,
                                            Hook&& after_place) {
     const uint32_t tid = otid(), wid = tid >> 6, lane = tid & 63;
     const uint32_t d12 = (C.b << P.D2) | C.g;
-    const uint64_t bu = key_u(P.base);
     // ---- level-3 digits, histogram (two u16 counters per word)
     uint32_t dg[GS_ITEMS];
 #pragma unroll
     for (int k = 0; k < GS_ITEMS; k++) {
         const bool valid = k * GS_THREADS + tid < nr;
-        const int64_t key = tup_key(v[k]);
-        const uint64_t ku = key_u(key);
-        clamped |= valid && ((ku < bu) || (ku - bu > P.span));
-        dg[k] = plan_d3(P, plan_rel(P, key), d12);
+        clamped |= valid && Lay::clamped(P, v[k]);
+        dg[k] = plan_d3(P, Lay::rel(P, v[k], C.b), d12);
         if (valid) atomicAdd(&L.cnt[r][dg[k] >> 1], 1u << ((dg[k] & 1) * 16));
     }
     __syncthreads();
@@ -606,7 +609,7 @@ __device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS& L,
             e += c[q];
             if (c[q] > 1) {
                 if (c[q] <= GS_RUNMAX) {
-                    insertion_sort(L.B + b0, c[q]);
+                    insertion_sort<Lay>(L.B + b0, c[q]);
                 } else {
                     const uint32_t li = atomicAdd(&L.nlong, 1u);
                     if (li < GS_LONGMAX) {
@@ -625,7 +628,7 @@ __device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS& L,
             const uint32_t s0 = L.lrun[li][0], e0 = L.lrun[li][1];
             bool ok = true;
             for (uint32_t i = s0 + 1 + tid; i < e0; i += GS_THREADS)
-                ok &= !tup_less(L.B[i], L.B[i - 1]);
+                ok &= !Lay::less(L.B[i], L.B[i - 1]);
             bad = __syncthreads_or(!ok);
         }
         if (bad) return false;
@@ -636,7 +639,7 @@ __device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS& L,
 #pragma unroll
     for (int k = 0; k < GS_ITEMS; k++) {
         const uint32_t j = k * GS_THREADS + tid;
-        if (j < nr) st_stream(dst + j, L.B[j]);
+        if (j < nr) st_stream(dst + j, Lay::unpack(P, L.B[j], C.b));
     }
     return true;
 }
@@ -646,10 +649,13 @@ __device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS& L,
 // g's data is in registers, g+1's R is gathered as soon as g's R sits in LDS
 // and g+1's S as soon as g's S does, so both gathers fly under g's sort,
 // write-out and count; g+2's tile runs are loaded one group further ahead.
+template <class Lay>
 __global__ void __launch_bounds__(GS_THREADS, GS_WG_PER_CU * GS_THREADS / 256)
 k_groupsort(GroupArgs A) {
+    typedef typename Lay::W W;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
-    GroupLDS& L = *reinterpret_cast<GroupLDS*>(lds_raw);
+    if (A.pack_bad && *A.pack_bad) return;
+    GroupLDS<W>& L = *reinterpret_cast<GroupLDS<W>*>(lds_raw);
     const RangePlan& P = A.plan;
     const uint32_t tid = otid(), lane = tid & 63;
     const int nrel = A.nrel;
@@ -670,10 +676,10 @@ k_groupsort(GroupArgs A) {
         co[r] = r < nrel ? __builtin_amdgcn_readfirstlane(L.off[r]) : 0;
     }
     bool cur_fits = cn[0] <= GS_CAP && cn[1] <= GS_CAP;
-    Tup vr[GS_ITEMS], vs[GS_ITEMS];
+    W vr[GS_ITEMS], vs[GS_ITEMS];
     if (cur_fits) {
-        gather_group(A, L, C, 0, cn[0], vr);
-        if (nrel > 1) gather_group(A, L, C, 1, cn[1], vs);
+        gather_group<Lay>(A, L, C, 0, cn[0], vr);
+        if (nrel > 1) gather_group<Lay>(A, L, C, 1, cn[1], vs);
     }
     if (gbeg + 1 < gend) load_meta(A, gbeg + 1, M, true);
 
@@ -694,10 +700,10 @@ k_groupsort(GroupArgs A) {
         if (gi + 2 < gend) load_meta(A, gi + 2, M, true);
         const bool next_fits = has_next && nn[0] <= GS_CAP && nn[1] <= GS_CAP;
         auto gather_next_r = [&]() {
-            if (next_fits) gather_group(A, L, N, 0, nn[0], vr);
+            if (next_fits) gather_group<Lay>(A, L, N, 0, nn[0], vr);
         };
         auto gather_next_s = [&]() {
-            if (next_fits && nrel > 1) gather_group(A, L, N, 1, nn[1], vs);
+            if (next_fits && nrel > 1) gather_group<Lay>(A, L, N, 1, nn[1], vs);
         };
         if (!cur_fits) {
             group_overflow(A, L, C);
@@ -705,10 +711,10 @@ k_groupsort(GroupArgs A) {
             gather_next_s();
         } else {
             bool clamped = false;
-            bool ok = sort_group(A, L, C, P, 0, cn[0], co[0], vr, clamped, gather_next_r);
+            bool ok = sort_group<Lay>(A, L, C, P, 0, cn[0], co[0], vr, clamped, gather_next_r);
             bool s_issued = false;
             if (ok && nrel > 1) {
-                ok = sort_group(A, L, C, P, 1, cn[1], co[1], vs, clamped, gather_next_s);
+                ok = sort_group<Lay>(A, L, C, P, 1, cn[1], co[1], vs, clamped, gather_next_s);
                 s_issued = true;
             }
             if (!ok) {
@@ -733,10 +739,10 @@ k_groupsort(GroupArgs A) {
                     const Tup* Rs = A.out[0] + C.ost[0] + co[0];
                     const uint32_t nR = cn[0], nS = cn[1];
                     for (uint32_t i = tid; i < nS; i += GS_THREADS) {
-                        const int64_t k = tup_key(L.B[i]);
-                        if (i > 0 && tup_key(L.B[i - 1]) == k) continue;
+                        const int64_t k = tup_key(Lay::unpack(P, L.B[i], C.b));
+                        if (i > 0 && tup_key(Lay::unpack(P, L.B[i - 1], C.b)) == k) continue;
                         uint32_t e = i + 1;
-                        while (e < nS && tup_key(L.B[e]) == k) e++;
+                        while (e < nS && tup_key(Lay::unpack(P, L.B[e], C.b)) == k) e++;
                         uint32_t lo = 0, hi = nR;
                         while (lo < hi) {
                             const uint32_t m = (lo + hi) >> 1;
@@ -806,13 +812,14 @@ struct SkewArgs {
 };
 
 // tile t of group (b, g) in relation r: run [src, src + len)
-__device__ __forceinline__ const Tup* skew_run(const GroupArgs& G, int r, uint32_t g,
-                                               uint32_t t0, uint32_t t, uint32_t& len) {
+template <class Lay>
+__device__ __forceinline__ const typename Lay::W* skew_run(const GroupArgs& G, int r, uint32_t g,
+                                                         uint32_t t0, uint32_t t, uint32_t& len) {
     const TileTable& tt = G.tt[r];
     const uint16_t* pf = tt.prefT + (uint64_t)g * tt.tstride + t0 + t;
     const uint32_t lo = pf[0];
     len = (uint32_t)(pf[tt.tstride] - lo);
-    return G.tmp[r] + tt.off[t0 + t] + lo;
+    return static_cast<const typename Lay::W*>(G.tmp[r]) + tt.off[t0 + t] + lo;
 }
 
 struct SkewSmallLDS {
@@ -823,8 +830,9 @@ struct SkewSmallLDS {
 };
 
 // element j of relation r's group (run tables in LDS) -> its source tuple
-__device__ __forceinline__ const Tup* skew_elem(const SkewSmallLDS& L, int r, const Tup* tmp,
-                                                uint32_t nt, uint32_t j) {
+template <class W>
+__device__ __forceinline__ const W* skew_elem(const SkewSmallLDS& L, int r, const W* tmp,
+                                              uint32_t nt, uint32_t j) {
     uint32_t lo = 0, hi = nt;  // last run with runoff <= j
     while (hi - lo > 1) {
         const uint32_t m = (lo + hi) >> 1;
@@ -835,17 +843,18 @@ __device__ __forceinline__ const Tup* skew_elem(const SkewSmallLDS& L, int r, co
 
 // apply f(x) to every tuple of relation r's group, SK_ITEMS loads in flight
 // per thread (groups of more than SK_TM runs: run by run)
-template <class F>
+template <class Lay, class F>
 __device__ __forceinline__ void skew_for_each(const GroupArgs& G, const SkewSmallLDS& L, int r,
                                               uint32_t g, uint32_t t0, uint32_t nt, uint32_t n,
                                               F&& f) {
+    typedef typename Lay::W W;
     if (nt <= SK_TM) {
         for (uint32_t c = 0; c < n; c += SK_CHUNK) {
-            Tup v[SK_ITEMS];
+            W v[SK_ITEMS];
 #pragma unroll
             for (int k = 0; k < SK_ITEMS; k++) {
                 const uint32_t j = c + k * SK_THREADS + threadIdx.x;
-                if (j < n) v[k] = ld_stream(skew_elem(L, r, G.tmp[r], nt, j));
+                if (j < n) v[k] = *skew_elem(L, r, static_cast<const W*>(G.tmp[r]), nt, j);
             }
 #pragma unroll
             for (int k = 0; k < SK_ITEMS; k++)
@@ -854,7 +863,7 @@ __device__ __forceinline__ void skew_for_each(const GroupArgs& G, const SkewSmal
     } else {
         for (uint32_t t = 0; t < nt; t++) {
             uint32_t len;
-            const Tup* src = skew_run(G, r, g, t0, t, len);
+            const W* src = skew_run<Lay>(G, r, g, t0, t, len);
             for (uint32_t i = threadIdx.x; i < len; i += SK_THREADS) f(src[i]);
         }
     }
@@ -880,15 +889,16 @@ __device__ __forceinline__ bool skew_inversion(const Tup* dst, uint32_t lo, uint
     return inv;
 }
 
+template <class Lay>
 __global__ void __launch_bounds__(SK_THREADS)
 k_skew_small(SkewArgs K) {
+    typedef typename Lay::W W;
     __shared__ SkewSmallLDS L;
     const GroupArgs& G = K.G;
     const RangePlan& P = G.plan;
     const uint32_t qi = K.list[blockIdx.x];
     const OvfEntry e = K.q[qi];
     const uint32_t d12 = (e.bucket << P.D2) | e.d2;
-    const uint64_t bu = key_u(P.base);
     const uint32_t tid = threadIdx.x;
     uint32_t t0[2] = {0, 0}, nt[2] = {0, 0};
     for (uint32_t i = tid; i < 2 * GS_NB3; i += SK_THREADS) (&L.h[0][0])[i] = 0;
@@ -917,11 +927,9 @@ k_skew_small(SkewArgs K) {
     // ---- pass 1: d3 histograms
     bool clamped = false;
     for (int r = 0; r < G.nrel; r++)
-        skew_for_each(G, L, r, e.d2, t0[r], nt[r], e.nr[r], [&](const Tup& x) {
-            const int64_t key = tup_key(x);
-            const uint64_t ku = key_u(key);
-            clamped |= (ku < bu) || (ku - bu > P.span);
-            atomicAdd(&L.h[r][plan_d3(P, plan_rel(P, key), d12)], 1u);
+        skew_for_each<Lay>(G, L, r, e.d2, t0[r], nt[r], e.nr[r], [&](const W& x) {
+            clamped |= Lay::clamped(P, x);
+            atomicAdd(&L.h[r][plan_d3(P, Lay::rel(P, x, e.bucket), d12)], 1u);
         });
     const bool exact = P.s3 == 0 && !__syncthreads_or(clamped);
     if (!exact) {
@@ -931,8 +939,9 @@ k_skew_small(SkewArgs K) {
             uint32_t pos = 0;
             for (uint32_t t = 0; t < nt[r]; t++) {
                 uint32_t len;
-                const Tup* src = skew_run(G, r, e.d2, t0[r], t, len);
-                for (uint32_t i = tid; i < len; i += SK_THREADS) dst[pos + i] = src[i];
+                const W* src = skew_run<Lay>(G, r, e.d2, t0[r], t, len);
+                for (uint32_t i = tid; i < len; i += SK_THREADS)
+                    dst[pos + i] = Lay::unpack(P, src[i], e.bucket);
                 pos += len;
             }
         }
@@ -968,9 +977,9 @@ k_skew_small(SkewArgs K) {
         }
         __syncthreads();
         // ---- pass 2: place
-        skew_for_each(G, L, r, e.d2, t0[r], nt[r], e.nr[r], [&](const Tup& x) {
-            const uint32_t d = plan_d3(P, plan_rel(P, tup_key(x)), d12);
-            dst[atomicAdd(&L.h[r][d], 1u)] = x;
+        skew_for_each<Lay>(G, L, r, e.d2, t0[r], nt[r], e.nr[r], [&](const W& x) {
+            const uint32_t d = plan_d3(P, Lay::rel(P, x, e.bucket), d12);
+            dst[atomicAdd(&L.h[r][d], 1u)] = Lay::unpack(P, x, e.bucket);
         });
         __threadfence_block();
         __syncthreads();
@@ -980,12 +989,13 @@ k_skew_small(SkewArgs K) {
     if (__syncthreads_or(inv) && tid == 0) K.gflag[qi] |= 2u;
 }
 
+template <class Lay>
 __global__ void __launch_bounds__(SK_THREADS)
 k_skew_hist(SkewArgs K) {
+    typedef typename Lay::W W;
     __shared__ uint32_t h[GS_NB3];
     const GroupArgs& G = K.G;
     const RangePlan& P = G.plan;
-    const uint64_t bu = key_u(P.base);
     const uint4 it = K.items[blockIdx.x];
     const uint32_t qi = it.x, sl = it.y, r = it.z >> 16, s = it.z & 0xffffu, ts = it.w;
     const OvfEntry& e = K.q[qi];
@@ -998,22 +1008,20 @@ k_skew_hist(SkewArgs K) {
     bool clamped = false;
     for (uint32_t t = s; t < nt; t += ts) {
         uint32_t len;
-        const Tup* src = skew_run(G, (int)r, e.d2, t0, t, len);
+        const W* src = skew_run<Lay>(G, (int)r, e.d2, t0, t, len);
         for (uint32_t c = 0; c < len; c += SK_CHUNK) {
-            Tup v[SK_ITEMS];
+            W v[SK_ITEMS];
 #pragma unroll
             for (int k = 0; k < SK_ITEMS; k++) {
                 const uint32_t i = c + k * SK_THREADS + threadIdx.x;
-                if (i < len) v[k] = ld_stream(src + i);
+                if (i < len) v[k] = src[i];
             }
 #pragma unroll
             for (int k = 0; k < SK_ITEMS; k++) {
                 const uint32_t i = c + k * SK_THREADS + threadIdx.x;
                 if (i < len) {
-                    const int64_t key = tup_key(v[k]);
-                    const uint64_t ku = key_u(key);
-                    clamped |= (ku < bu) || (ku - bu > P.span);
-                    atomicAdd(&h[plan_d3(P, plan_rel(P, key), d12)], 1u);
+                    clamped |= Lay::clamped(P, v[k]);
+                    atomicAdd(&h[plan_d3(P, Lay::rel(P, v[k], e.bucket), d12)], 1u);
                 }
             }
         }
@@ -1061,8 +1069,10 @@ k_skew_scan(SkewArgs K) {
     }
 }
 
+template <class Lay>
 __global__ void __launch_bounds__(SK_THREADS)
 k_skew_place(SkewArgs K) {
+    typedef typename Lay::W W;
     __shared__ uint32_t h[GS_NB3];
     __shared__ unsigned long long scr[SK_THREADS / 64 + 1];
     const GroupArgs& G = K.G;
@@ -1081,14 +1091,15 @@ k_skew_place(SkewArgs K) {
             unsigned long long acc = 0;
             for (uint32_t u = threadIdx.x; u < t; u += SK_THREADS) {
                 uint32_t l;
-                (void)skew_run(G, (int)r, e.d2, t0, u, l);
+                (void)skew_run<Lay>(G, (int)r, e.d2, t0, u, l);
                 acc += l;
             }
             unsigned long long pos;
             (void)block_scan64(acc, scr, &pos);
             uint32_t len;
-            const Tup* src = skew_run(G, (int)r, e.d2, t0, t, len);
-            for (uint32_t i = threadIdx.x; i < len; i += SK_THREADS) dst[pos + i] = src[i];
+            const W* src = skew_run<Lay>(G, (int)r, e.d2, t0, t, len);
+            for (uint32_t i = threadIdx.x; i < len; i += SK_THREADS)
+                dst[pos + i] = Lay::unpack(P, src[i], e.bucket);
         }
         return;
     }
@@ -1096,15 +1107,15 @@ k_skew_place(SkewArgs K) {
     uint32_t* gcur = K.ghist + ((size_t)sl * 2 + r) * GS_NB3;
     for (uint32_t t = s; t < nt; t += ts) {
         uint32_t len;
-        const Tup* src = skew_run(G, (int)r, e.d2, t0, t, len);
+        const W* src = skew_run<Lay>(G, (int)r, e.d2, t0, t, len);
         for (uint32_t c = 0; c < len; c += SK_CHUNK) {
             for (uint32_t d = threadIdx.x; d < GS_NB3; d += SK_THREADS) h[d] = 0;
-            Tup v[SK_ITEMS];
+            W v[SK_ITEMS];
             uint32_t dg[SK_ITEMS];
 #pragma unroll
             for (int k = 0; k < SK_ITEMS; k++) {
                 const uint32_t i = c + k * SK_THREADS + threadIdx.x;
-                if (i < len) v[k] = ld_stream(src + i);
+                if (i < len) v[k] = src[i];
             }
             __syncthreads();
 #pragma unroll
@@ -1112,7 +1123,7 @@ k_skew_place(SkewArgs K) {
                 const uint32_t i = c + k * SK_THREADS + threadIdx.x;
                 dg[k] = 0xffffffffu;
                 if (i < len) {
-                    dg[k] = plan_d3(P, plan_rel(P, tup_key(v[k])), d12);
+                    dg[k] = plan_d3(P, Lay::rel(P, v[k], e.bucket), d12);
                     atomicAdd(&h[dg[k]], 1u);
                 }
             }
@@ -1125,7 +1136,8 @@ k_skew_place(SkewArgs K) {
             __syncthreads();
 #pragma unroll
             for (int k = 0; k < SK_ITEMS; k++)
-                if (dg[k] != 0xffffffffu) dst[atomicAdd(&h[dg[k]], 1u)] = v[k];
+                if (dg[k] != 0xffffffffu)
+                    dst[atomicAdd(&h[dg[k]], 1u)] = Lay::unpack(P, v[k], e.bucket);
             __syncthreads();
         }
     }
@@ -1150,6 +1162,7 @@ k_skew_check(SkewArgs K) {
 // not finish (inexact digits, equal-key runs out of payload order) through
 // the segmented merge sort and the merge-join count.  hdst[r * nb + b] is
 // bucket b's output start.
+template <class Lay>
 static void skew_path(Workspace* ws, const GroupArgs& G, OvfEntry* ovf, uint32_t no,
                       const uint64_t* hdst, uint32_t nb, hipStream_t st) {
     const int nrel = G.nrel;
@@ -1201,7 +1214,7 @@ static void skew_path(Workspace* ws, const GroupArgs& G, OvfEntry* ovf, uint32_t
         K.list = (const uint32_t*)dbuf;
         K.n = (uint32_t)small.size();
         TraceScope ts(ws, "k_skew_small", st);
-        hipLaunchKernelGGL(k_skew_small, dim3(K.n), dim3(SK_THREADS), 0, st, K);
+        hipLaunchKernelGGL(k_skew_small<Lay>, dim3(K.n), dim3(SK_THREADS), 0, st, K);
     }
     if (nl) {
         K.ghist = (uint32_t*)ws->scratch("sk_hist", nl * 2 * GS_NB3 * 4);
@@ -1212,12 +1225,12 @@ static void skew_path(Workspace* ws, const GroupArgs& G, OvfEntry* ovf, uint32_t
         const uint32_t ni = (uint32_t)items.size();
         {
             TraceScope ts(ws, "k_skew_hist", st);
-            hipLaunchKernelGGL(k_skew_hist, dim3(ni), dim3(SK_THREADS), 0, st, K);
+            hipLaunchKernelGGL(k_skew_hist<Lay>, dim3(ni), dim3(SK_THREADS), 0, st, K);
         }
         hipLaunchKernelGGL(k_skew_scan, dim3((uint32_t)nl), dim3(SK_THREADS), 0, st, K);
         {
             TraceScope ts(ws, "k_skew_place", st);
-            hipLaunchKernelGGL(k_skew_place, dim3(ni), dim3(SK_THREADS), 0, st, K);
+            hipLaunchKernelGGL(k_skew_place<Lay>, dim3(ni), dim3(SK_THREADS), 0, st, K);
         }
         hipLaunchKernelGGL(k_skew_check, dim3(ni), dim3(SK_THREADS), 0, st, K);
     }
@@ -1403,11 +1416,28 @@ static void launch_preft_range(const TilePassArgs& T, int nrel, uint32_t nb2,
     launch_preft(tt, nrel, ub, nt, nb2, st);
 }
 
+// dynamic LDS limits of the tile and group passes (per layout)
+template <class Lay>
+static void set_pass_attrs() {
+    static bool done = false;
+    if (done) return;
+    SMJ_CHECK(hipFuncSetAttribute((const void*)k_tilepass<Lay>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    // several workgroups per CU (launch bounds): ask for what one needs
+    SMJ_CHECK(hipFuncSetAttribute((const void*)k_groupsort<Lay>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)sizeof(GroupLDS<typename Lay::W>)));
+    done = true;
+}
+
 // Bucket pass without a host synchronisation before the kernels (sampled
 // partition + host-known plan): launch sizes are upper bounds, the tile
 // numbering is computed on the device.  One synchronisation at the end (skew
 // queue and the partition's overflow flag).
+template <class Lay>
 static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
+    typedef typename Lay::W W;
+    set_pass_attrs<Lay>();
     const uint32_t nb = a.nbuckets;
     const int nrel = a.nrel;
     const uint32_t nb2 = 1u << a.host_plan->D2;
@@ -1460,10 +1490,12 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
     }
     T.plan = *a.host_plan;
     T.nb2 = nb2;
+    T.pack_bad = a.pack_bad;
+    G.pack_bad = a.pack_bad;
     {
         TraceScope ts(ws, "k_tilepass", st);
-        const size_t tp_lds = TILE2 * sizeof(Tup) + nb2 * 4 + 64;
-        hipLaunchKernelGGL(k_tilepass, dim3(T.nt[0] + T.nt[1]), dim3(TP_THREADS),
+        const size_t tp_lds = TILE2 * sizeof(W) + nb2 * 4 + 64;
+        hipLaunchKernelGGL(k_tilepass<Lay>, dim3(T.nt[0] + T.nt[1]), dim3(TP_THREADS),
                            tp_lds, st, T);
     }
     launch_preft(tt, nrel, ub, ntiles, nb2, st);
@@ -1482,19 +1514,23 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
     {
         const uint32_t nwg = (ngroups + G.per - 1) / G.per;
         TraceScope ts(ws, "k_groupsort", st);
-        hipLaunchKernelGGL(k_groupsort, dim3(nwg), dim3(GS_THREADS),
-                           sizeof(GroupLDS), st, G);
+        hipLaunchKernelGGL(k_groupsort<Lay>, dim3(nwg), dim3(GS_THREADS),
+                           sizeof(GroupLDS<W>), st, G);
     }
     SMJ_CHECK(hipGetLastError());
     if (a.ev_ovf) SMJ_CHECK(hipEventRecord(a.ev_ovf, st));
 
     // ---- the one synchronisation: partition overflow flag + skew queue
-    uint32_t* h = (uint32_t*)ws->host_pinned("bs_h_flagovf", 8);
-    h[0] = h[1] = 0;
+    uint32_t* h = (uint32_t*)ws->host_pinned("bs_h_flagovf", 12);
+    h[0] = h[1] = h[2] = 0;
     SMJ_CHECK(hipMemcpyAsync(h, a.part_flag, 4, hipMemcpyDeviceToHost, st));
     SMJ_CHECK(hipMemcpyAsync(h + 1, novf, 4, hipMemcpyDeviceToHost, st));
+    if (a.pack_bad)
+        SMJ_CHECK(hipMemcpyAsync(h + 2, a.pack_bad, 4, hipMemcpyDeviceToHost, st));
     SMJ_CHECK(hipStreamSynchronize(st));
-    if (h[0]) return false;  // the caller repeats with exact partitions
+    // the caller repeats with exact partitions (region overflow) or on tuples
+    // (not packable); the tile and group passes exited at once on the latter
+    if (h[0] || h[2]) return false;
     const uint32_t no = h[1];
     if (no == 0) return true;
     if (no > ovf_cap) {
@@ -1505,7 +1541,7 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
     for (int r = 0; r < nrel; r++)
         SMJ_CHECK(hipMemcpyAsync(hdst.data() + (size_t)r * nb, ostart[r], (size_t)nb * 8,
                                  hipMemcpyDeviceToHost, st));
-    skew_path(ws, G, ovf, no, hdst.data(), nb, st);
+    skew_path<Lay>(ws, G, ovf, no, hdst.data(), nb, st);
     SMJ_CHECK(hipGetLastError());
     return true;
 }
@@ -1515,20 +1551,22 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
     const int nrel = a.nrel;
     static bool attr = false;
     if (!attr) {
-        SMJ_CHECK(hipFuncSetAttribute((const void*)k_tilepass,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      160 * 1024));
-        // several workgroups per CU (launch bounds): ask for what one needs
-        SMJ_CHECK(hipFuncSetAttribute((const void*)k_groupsort,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)sizeof(GroupLDS)));
         SMJ_CHECK(hipFuncSetAttribute((const void*)k_preft,
                                       hipFuncAttributeMaxDynamicSharedMemorySize,
                                       PT_TILES * ((1 << 9) + 1) * 2));
         attr = true;
     }
-    if (a.host_plan && a.seg_start[0] && a.part_flag)
-        return bucket_sort_nosync(ws, a, st);
+    set_pass_attrs<LayTup>();
+    if (a.host_plan && a.seg_start[0] && a.part_flag) {
+#ifdef KEY_8B
+        if (a.packed) return bucket_sort_nosync<LayPacked>(ws, a, st);
+#endif
+        return bucket_sort_nosync<LayTup>(ws, a, st);
+    }
+    if (a.packed) {
+        fprintf(stderr, "[ERROR] smj: packed bucket sort needs the host plan\n");
+        abort();
+    }
 
     // ---- host view of the plan and the bucket counts (one synchronisation):
     // launch sizes and the tile numbering are derived from them
@@ -1620,6 +1658,8 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
     }
     T.plan = *hplan;
     T.nb2 = nb2;
+    T.pack_bad = nullptr;
+    G.pack_bad = nullptr;
     G.nrel = nrel;
     G.plan = *hplan;
     G.count_dev = a.count_dev;
@@ -1641,7 +1681,7 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
     if (ntiles) {
         {
             TraceScope ts(ws, "k_tilepass", st);
-            hipLaunchKernelGGL(k_tilepass, dim3(ntiles), dim3(TP_THREADS), tp_lds, st, T);
+            hipLaunchKernelGGL(k_tilepass<LayTup>, dim3(ntiles), dim3(TP_THREADS), tp_lds, st, T);
         }
         launch_preft_range(T, nrel, nb2, st);
     }
@@ -1655,8 +1695,8 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
         G.per = (ng + maxwg - 1) / maxwg;
         const uint32_t nwg = (ng + G.per - 1) / G.per;
         TraceScope ts(ws, "k_groupsort", st);
-        hipLaunchKernelGGL(k_groupsort, dim3(nwg), dim3(GS_THREADS),
-                           sizeof(GroupLDS), st, G);
+        hipLaunchKernelGGL(k_groupsort<LayTup>, dim3(nwg), dim3(GS_THREADS),
+                           sizeof(GroupLDS<Tup>), st, G);
     }
     SMJ_CHECK(hipGetLastError());
     if (a.ev_ovf) SMJ_CHECK(hipEventRecord(a.ev_ovf, st));
@@ -1671,7 +1711,7 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
         fprintf(stderr, "[ERROR] smj: overflow table too small\n");
         abort();
     }
-    skew_path(ws, G, ovf, no, hdst, nb, st);
+    skew_path<LayTup>(ws, G, ovf, no, hdst, nb, st);
     SMJ_CHECK(hipGetLastError());
     return true;
 }

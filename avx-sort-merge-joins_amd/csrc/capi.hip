@@ -197,6 +197,17 @@ static void device_sort(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
     }
 }
 
+// 16-byte joins carry packed words through the intermediate passes when the
+// plan allows it (LayPacked); SMJ_PACK=0 keeps tuples
+static bool use_packing() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("SMJ_PACK");
+        v = e ? atoi(e) : 1;
+    }
+    return v != 0;
+}
+
 static void device_join(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
                         uint64_t nS, Tup* sortedR, Tup* sortedS,
                         uint32_t fanout_bits, int64_t hint_min,
@@ -204,7 +215,6 @@ static void device_join(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
                         hipStream_t st) {
     ws->events();
     SMJ_CHECK(hipEventRecord(ws->ev[0], st));
-    SMJ_CHECK(hipMemsetAsync(count_dev, 0, sizeof(unsigned long long), st));
     uint32_t D1, D2, D2cap;
     choose_levels(nR > nS ? nR : nS, fanout_bits, &D1, &D2, &D2cap);
     RangePlan* plan = (RangePlan*)ws->scratch("plan", sizeof(RangePlan));
@@ -219,6 +229,11 @@ static void device_join(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
         plan_from_sample(ws, rels, ns, 2, D1, D2, D2cap, hint_min, hint_max, plan, st);
     const uint32_t nb = 1u << D1;
     const bool sampled = use_sampled() && D1 <= 10;  // LDS carries up to 1024
+#ifdef KEY_8B
+    const bool can_pack = sampled && plan_on_host && use_packing() && LayPacked::usable(hplan);
+#else
+    const bool can_pack = false;
+#endif
     Tup* partR = (Tup*)ws->scratch(
         "join_partR", (sampled ? sampled_capacity(nR, D1) : (nR ? nR : 1)) * sizeof(Tup));
     Tup* partS = (Tup*)ws->scratch(
@@ -227,56 +242,60 @@ static void device_join(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
     uint64_t* stS = (uint64_t*)ws->scratch("join_stS", nb * 8);
     int64_t* hR = (int64_t*)ws->scratch("join_hR", nb * 8);
     int64_t* hS = (int64_t*)ws->scratch("join_hS", nb * 8);
-    unsigned int* flag = (unsigned int*)ws->scratch("part_flag", 4);
+    unsigned int* flag = (unsigned int*)ws->scratch("part_flag", 8);  // [1]: not packable
     uint64_t* sgsR = (uint64_t*)ws->scratch("join_sgsR", (size_t)nb * kShards * 8);
     int64_t* sgcR = (int64_t*)ws->scratch("join_sgcR", (size_t)nb * kShards * 8);
     uint64_t* sgsS = (uint64_t*)ws->scratch("join_sgsS", (size_t)nb * kShards * 8);
     int64_t* sgcS = (int64_t*)ws->scratch("join_sgcS", (size_t)nb * kShards * 8);
-    if (sampled) {
-        SMJ_CHECK(hipMemsetAsync(flag, 0, 4, st));
-        sampled_partition(ws, R, nR, partR, plan, D1, stR, hR, sgsR, sgcR, flag, st);
-        sampled_partition(ws, S, nS, partS, plan, D1, stS, hS, sgsS, sgcS, flag, st);
-    } else {
-        plan_partition(ws, R, nR, partR, plan, D1, stR, hR, st);
-        plan_partition(ws, S, nS, partS, plan, D1, stS, hS, st);
-    }
-    SMJ_CHECK(hipEventRecord(ws->ev[1], st));
-    BucketSortArgs a;
-    a.part[0] = partR;
-    a.part[1] = partS;
-    a.bstart[0] = stR;
-    a.bstart[1] = stS;
-    a.bcount[0] = hR;
-    a.bcount[1] = hS;
-    a.tmp[0] = partR;
-    a.tmp[1] = partS;
-    a.out[0] = sortedR;
-    a.out[1] = sortedS;
-    a.n[0] = nR;
-    a.n[1] = nS;
-    a.nrel = 2;
-    a.nbuckets = nb;
-    a.plan_dev = plan;
-    a.count_dev = count_dev;
-    a.ev_tile = nullptr;
-    a.ev_bucket = ws->ev[2];
-    a.ev_ovf = ws->ev[3];
-    a.part_flag = sampled ? flag : nullptr;
-    a.host_plan = plan_on_host ? &hplan : nullptr;
-    if (sampled) {
-        a.seg_start[0] = sgsR;
-        a.seg_cnt[0] = sgcR;
-        a.seg_start[1] = sgsS;
-        a.seg_cnt[1] = sgcS;
-    }
-    if (!bucket_sort(ws, a, st)) {
-        // a sampled region overflowed (very skewed keys): exact partitions
-        plan_partition(ws, R, nR, partR, plan, D1, stR, hR, st);
-        plan_partition(ws, S, nS, partS, plan, D1, stS, hS, st);
-        a.part_flag = nullptr;
-        a.seg_start[0] = a.seg_start[1] = nullptr;
-        a.seg_cnt[0] = a.seg_cnt[1] = nullptr;
-        bucket_sort(ws, a, st);
+    // attempts: sampled + packed words, sampled tuples, exact tuples; a later
+    // one runs only when the one before reported a region overflow or an
+    // unpackable tuple (its tile and group passes then did nothing or are
+    // discarded: the count restarts from 0)
+    for (int mode = can_pack ? 0 : (sampled ? 1 : 2); mode <= 2; mode++) {
+        const bool packed = mode == 0;
+        SMJ_CHECK(hipMemsetAsync(count_dev, 0, sizeof(unsigned long long), st));
+        if (mode < 2) {
+            SMJ_CHECK(hipMemsetAsync(flag, 0, 8, st));
+            sampled_partition(ws, R, nR, partR, plan, D1, stR, hR, sgsR, sgcR, flag, st,
+                              packed ? &hplan : nullptr, flag + 1);
+            sampled_partition(ws, S, nS, partS, plan, D1, stS, hS, sgsS, sgcS, flag, st,
+                              packed ? &hplan : nullptr, flag + 1);
+        } else {
+            plan_partition(ws, R, nR, partR, plan, D1, stR, hR, st);
+            plan_partition(ws, S, nS, partS, plan, D1, stS, hS, st);
+        }
+        SMJ_CHECK(hipEventRecord(ws->ev[1], st));
+        BucketSortArgs a;
+        a.part[0] = partR;
+        a.part[1] = partS;
+        a.bstart[0] = stR;
+        a.bstart[1] = stS;
+        a.bcount[0] = hR;
+        a.bcount[1] = hS;
+        a.tmp[0] = partR;
+        a.tmp[1] = partS;
+        a.out[0] = sortedR;
+        a.out[1] = sortedS;
+        a.n[0] = nR;
+        a.n[1] = nS;
+        a.nrel = 2;
+        a.nbuckets = nb;
+        a.plan_dev = plan;
+        a.count_dev = count_dev;
+        a.ev_tile = nullptr;
+        a.ev_bucket = ws->ev[2];
+        a.ev_ovf = ws->ev[3];
+        a.host_plan = plan_on_host ? &hplan : nullptr;
+        a.packed = packed;
+        a.pack_bad = packed ? flag + 1 : nullptr;
+        if (mode < 2) {
+            a.part_flag = flag;
+            a.seg_start[0] = sgsR;
+            a.seg_cnt[0] = sgcR;
+            a.seg_start[1] = sgsS;
+            a.seg_cnt[1] = sgcS;
+        }
+        if (bucket_sort(ws, a, st)) break;
     }
     SMJ_CHECK(hipEventRecord(ws->ev[4], st));
 }

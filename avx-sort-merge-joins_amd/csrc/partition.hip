@@ -569,9 +569,9 @@ __global__ void __launch_bounds__(256)
 k_regions(const unsigned int* __restrict__ sample, uint32_t nbins,
           uint32_t stride, uint64_t slack, uint64_t* __restrict__ base,
           uint64_t* __restrict__ seg_start, unsigned long long* __restrict__ cursor,
-          uint64_t* __restrict__ cap_end) {
+          uint64_t* __restrict__ cap_end, uint32_t elem_bytes) {
     __shared__ uint64_t sh[256];
-    constexpr uint64_t SEG = kSegBytes / sizeof(Tup);
+    const uint64_t SEG = kSegBytes / elem_bytes;
     const uint32_t per = (nbins + 255) / 256;
     const uint32_t b = threadIdx.x * per;
     // capacity of one shard of partition d
@@ -632,21 +632,25 @@ k_regions_done(const uint64_t* __restrict__ seg_start,
     }
 }
 
-template <int THREADS, int ITEMS, class Digit>
+template <int THREADS, int ITEMS, class Digit, class Pack>
 __global__ void __launch_bounds__(THREADS)
 k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_arg,
               uint32_t nbins, unsigned long long* __restrict__ cursor_all,
-              const uint64_t* __restrict__ cap_end_all, Tup* __restrict__ out) {
+              const uint64_t* __restrict__ cap_end_all,
+              typename Pack::OutT* __restrict__ out, Pack pk,
+              unsigned int* __restrict__ bad_flag) {
+    typedef typename Pack::OutT OutT;
+    bool bad = false;
     const auto dig = dig_arg.load();
     // this workgroup's shard of every partition: cursor[d * kShards + shard]
     const uint32_t shard = blockIdx.x % kShards;
     unsigned long long* cursor = cursor_all + shard;
     const uint64_t* cap_end = cap_end_all + shard;
     constexpr int TILE = THREADS * ITEMS;
-    constexpr uint32_t SEG = kSegBytes / sizeof(Tup);  // tuples per segment
+    constexpr uint32_t SEG = kSegBytes / sizeof(OutT);  // elements per segment
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     Tup* stage = reinterpret_cast<Tup*>(lds_raw);
-    Tup* carry = stage + TILE;
+    OutT* carry = reinterpret_cast<OutT*>(stage + TILE);
     uint64_t* pos = reinterpret_cast<uint64_t*>(carry + (size_t)nbins * SEG);
     uint32_t* tstart = reinterpret_cast<uint32_t*>(pos + nbins);
     uint32_t* tfill = tstart + nbins;
@@ -734,7 +738,7 @@ k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
             const uint32_t d = q / SEG, j = q % SEG;
             if (j < kc[d] && j < tfill[d]) out[pos[d] + j] = carry[q];
         }
-        Tup keep[ITEMS];
+        OutT keep[ITEMS];
         uint32_t kslot[ITEMS];
 #pragma unroll
         for (int j = 0; j < ITEMS; j++) {
@@ -747,14 +751,14 @@ k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
                 const uint32_t E = tfill[d];
                 if (vv < E) {
 #if SMJ_SC_ABL == 1
-                    out[base + i] = t;  // ablation: linear writes
+                    out[base + i] = pk(t, bad);  // ablation: linear writes
 #elif SMJ_SC_ABL == 2
-                    if (tup_key(t) == -12345) out[pos[d] + vv] = t;  // ablation: no writes
+                    if (tup_key(t) == -12345) out[pos[d] + vv] = pk(t, bad);  // ablation: no writes
 #else
-                    out[pos[d] + vv] = t;  // plain stores: the L2 merges partial lines
+                    out[pos[d] + vv] = pk(t, bad);  // plain stores: the L2 merges partial lines
 #endif
                 } else if (vv - E < SEG) {  // always, unless the region overflowed
-                    keep[j] = t;
+                    keep[j] = pk(t, bad);
                     kslot[j] = d * SEG + (vv - E);
                 }
             }
@@ -788,6 +792,7 @@ k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
         const uint32_t d = q / SEG, j = q % SEG;
         if (j < kc[d] && pos[d] != ~0ull) out[pos[d] + j] = carry[q];
     }
+    if (bad_flag && bad) atomicOr(bad_flag, 1u);
 }
 
 // pad copy for wide digits: item at unpadded position i of digit d moves to
@@ -1102,21 +1107,63 @@ static constexpr uint32_t kSampleStride = 128;
 static constexpr uint64_t kRegionSlack = 1024;  // per shard
 
 uint64_t sampled_capacity(uint64_t n, uint32_t dbits) {
-    const uint64_t SEG = kSegBytes / sizeof(Tup);
+    // in elements of the smallest layout (8-byte words: the most per segment)
+    const uint64_t SEG = kSegBytes / 8;
     return n + n / 8 + 2 * kSampleStride +
            ((uint64_t)1 << dbits) * kShards * (kRegionSlack + 2 * SEG);
 }
 
-void sampled_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
-                       const RangePlan* plan_dev, uint32_t dbits,
-                       uint64_t* starts_dev, int64_t* hist_out,
-                       uint64_t* seg_start, int64_t* seg_cnt,
-                       unsigned int* flag_dev, hipStream_t st) {
-    PlanDigit1 dig{plan_dev};
-    const uint32_t nbins = 1u << dbits;
+template <class Pack>
+static void sampled_scatter(Workspace* ws, const Tup* in, uint64_t n, void* out,
+                            const PlanDigit1& dig, uint32_t nbins,
+                            unsigned long long* cursor, const uint64_t* cap_end,
+                            const Pack& pk, unsigned int* bad_flag, hipStream_t st) {
     constexpr int THREADS = SMJ_SC_THREADS;
     constexpr int ITEMS = sizeof(Tup) == 16 ? SMJ_SC_ITEMS16 : SMJ_SC_ITEMS8;
     constexpr int TILE = THREADS * ITEMS;
+    uint64_t ntiles = (n + TILE - 1) / TILE;
+    const uint32_t maxwg = 256 * SMJ_SC_WG_PER_CU;
+    uint32_t nwg = (uint32_t)(ntiles < maxwg ? ntiles : maxwg);
+    const uint64_t tiles_per_wg = (ntiles + nwg - 1) / nwg;
+    const uint64_t chunk = tiles_per_wg * TILE;
+    nwg = (uint32_t)((ntiles + tiles_per_wg - 1) / tiles_per_wg);
+    // stage TILE | carry nbins segments | pos u64, tstart, tfill, kc u32
+    const size_t lds = (size_t)TILE * sizeof(Tup) + (size_t)nbins * kSegBytes +
+                       (size_t)nbins * (8 + 4 + 4 + 4) + 64;
+    static bool attr = false;
+    if (!attr) {
+        SMJ_CHECK(hipFuncSetAttribute(
+            (const void*)k_scatter_res<THREADS, ITEMS, PlanDigit1, Pack>,
+            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr = true;
+    }
+    if (lds > 160 * 1024) {
+        fprintf(stderr, "[ERROR] smj: scatter LDS %zu > 160 KiB\n", lds);
+        abort();
+    }
+    if (nbins > (uint32_t)THREADS) {
+        fprintf(stderr, "[ERROR] smj: sampled scatter needs <= %d partitions\n", THREADS);
+        abort();
+    }
+    TraceScope ts(ws, "k_scatter", st);
+    hipLaunchKernelGGL((k_scatter_res<THREADS, ITEMS, PlanDigit1, Pack>), dim3(nwg),
+                       dim3(THREADS), lds, st, in, n, chunk, dig, nbins, cursor,
+                       cap_end, (typename Pack::OutT*)out, pk, bad_flag);
+}
+
+void sampled_partition(Workspace* ws, const Tup* in, uint64_t n, void* out,
+                       const RangePlan* plan_dev, uint32_t dbits,
+                       uint64_t* starts_dev, int64_t* hist_out,
+                       uint64_t* seg_start, int64_t* seg_cnt,
+                       unsigned int* flag_dev, hipStream_t st,
+                       const RangePlan* pack_plan, unsigned int* pack_bad) {
+    PlanDigit1 dig{plan_dev};
+    const uint32_t nbins = 1u << dbits;
+#ifdef KEY_8B
+    const bool packed = pack_plan != nullptr;
+#else
+    const bool packed = false;
+#endif
     unsigned int* sample = (unsigned int*)ws->scratch("sp_sample", (size_t)nbins * 4);
     unsigned long long* cursor =
         (unsigned long long*)ws->scratch("sp_cursor", (size_t)nbins * kShards * 8);
@@ -1133,37 +1180,23 @@ void sampled_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
                            dig, nbins, sample);
         hipLaunchKernelGGL(k_regions, dim3(1), dim3(256), 0, st, sample, nbins,
                            kSampleStride, kRegionSlack, starts_dev, seg_start, cursor,
-                           cap_end);
+                           cap_end, packed ? 8u : (uint32_t)sizeof(Tup));
     }
     if (n) {
-        uint64_t ntiles = (n + TILE - 1) / TILE;
-        const uint32_t maxwg = 256 * SMJ_SC_WG_PER_CU;
-        uint32_t nwg = (uint32_t)(ntiles < maxwg ? ntiles : maxwg);
-        const uint64_t tiles_per_wg = (ntiles + nwg - 1) / nwg;
-        const uint64_t chunk = tiles_per_wg * TILE;
-        nwg = (uint32_t)((ntiles + tiles_per_wg - 1) / tiles_per_wg);
-        // stage TILE | carry nbins segments | pos u64, tstart, tfill, kc u32
-        const size_t lds = (size_t)TILE * sizeof(Tup) + (size_t)nbins * kSegBytes +
-                           (size_t)nbins * (8 + 4 + 4 + 4) + 64;
-        static bool attr = false;
-        if (!attr) {
-            SMJ_CHECK(hipFuncSetAttribute(
-                (const void*)k_scatter_res<THREADS, ITEMS, PlanDigit1>,
-                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-            attr = true;
+#ifdef KEY_8B
+        if (packed) {
+            LayPacked::Pack pk;
+            pk.bu = key_u(pack_plan->base);
+            pk.span = pack_plan->span;
+            pk.s1 = pack_plan->s1;
+            sampled_scatter(ws, in, n, out, dig, nbins, cursor, cap_end, pk, pack_bad, st);
+        } else
+#endif
+        {
+            (void)pack_bad;
+            sampled_scatter(ws, in, n, out, dig, nbins, cursor, cap_end, PackNone(),
+                            (unsigned int*)nullptr, st);
         }
-        if (lds > 160 * 1024) {
-            fprintf(stderr, "[ERROR] smj: scatter LDS %zu > 160 KiB\n", lds);
-            abort();
-        }
-        if (nbins > (uint32_t)THREADS) {
-            fprintf(stderr, "[ERROR] smj: sampled scatter needs <= %d partitions\n", THREADS);
-            abort();
-        }
-        TraceScope ts(ws, "k_scatter", st);
-        hipLaunchKernelGGL((k_scatter_res<THREADS, ITEMS, PlanDigit1>), dim3(nwg),
-                           dim3(THREADS), lds, st, in, n, chunk, dig, nbins, cursor,
-                           cap_end, out);
     }
     hipLaunchKernelGGL(k_regions_done, dim3(1), dim3(256), 0, st, seg_start, cursor,
                        cap_end, nbins, hist_out, seg_cnt, flag_dev);

@@ -78,6 +78,18 @@ __device__ __forceinline__ Tup ld_stream(const Tup* p) {
 #endif
 }
 
+// streaming store of an intermediate element (tuple or packed word)
+__device__ __forceinline__ void st_w(uint64_t* p, uint64_t v) {
+#if SMJ_NT_STORES
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+#ifdef KEY_8B
+__device__ __forceinline__ void st_w(Tup* p, const Tup& v) { st_stream(p, v); }
+#endif
+
 // non-temporal load regardless of SMJ_NT_LOADS: gathers of once-read tuples
 // that must not push the small per-group tables out of L2
 __device__ __forceinline__ Tup ld_nt(const Tup* p) {
@@ -179,6 +191,76 @@ __host__ __device__ __forceinline__ uint32_t plan_d1(const RangePlan& p,
 }
 
 // level-2 digit of `rel` inside bucket d1
+// ---------------------------------------------------------------------------
+// Element layouts of the intermediate passes (tile pass, group pass, skew
+// kernels).  LayTup: the tuples themselves.  LayPacked (16-byte tuples): the
+// level-1 partition packs every tuple into ONE 64-bit word
+//     w = (rel mod 2^s1) << pb  |  payload          (pb = 64 - s1)
+// where rel = key_u(key) - key_u(base) is the key's offset in the plan range
+// and the bucket (rel >> s1) is implied by where the word sits.  Within a
+// bucket the unsigned order of w is the (key, payload) order, so the passes
+// sort words; the group pass unpacks when it writes the sorted tuples.  It
+// applies when every key lies in the plan range and every payload in
+// [0, 2^pb) -- the partition flags anything else and the join reruns on
+// tuples.  Halves the bytes of the two intermediate passes.
+// ---------------------------------------------------------------------------
+struct LayTup {
+    typedef Tup W;
+    static constexpr bool packed = false;
+    __device__ static __forceinline__ uint64_t rel(const RangePlan& P, const W& w, uint32_t) {
+        return plan_rel(P, tup_key(w));
+    }
+    __device__ static __forceinline__ bool clamped(const RangePlan& P, const W& w) {
+        const uint64_t ku = key_u(tup_key(w)), bu = key_u(P.base);
+        return ku < bu || ku - bu > P.span;
+    }
+    __device__ static __forceinline__ bool less(const W& a, const W& b) { return tup_less(a, b); }
+    __device__ static __forceinline__ Tup unpack(const RangePlan&, const W& w, uint32_t) {
+        return w;
+    }
+};
+
+#ifdef KEY_8B
+struct LayPacked {
+    typedef uint64_t W;
+    static constexpr bool packed = true;
+    __device__ static __forceinline__ uint64_t rel(const RangePlan& P, const W& w, uint32_t b) {
+        return ((uint64_t)b << P.s1) | (w >> (64 - P.s1));
+    }
+    __device__ static __forceinline__ bool clamped(const RangePlan&, const W&) { return false; }
+    __device__ static __forceinline__ bool less(const W& a, const W& b) { return a < b; }
+    __device__ static __forceinline__ Tup unpack(const RangePlan& P, const W& w, uint32_t b) {
+        Tup t;
+        t.payload = (int64_t)(w & (~0ull >> P.s1));
+        t.key = (int64_t)((key_u(P.base) + rel(P, w, b)) ^ 0x8000000000000000ull);
+        return t;
+    }
+    // the level-1 partition's packing of tuple t into bucket rel >> s1;
+    // `bad` is set when t cannot be packed (key outside the plan, payload
+    // outside [0, 2^pb))
+    struct Pack {
+        typedef uint64_t OutT;
+        uint64_t bu, span;
+        uint32_t s1;
+        __device__ __forceinline__ uint64_t operator()(const Tup& t, bool& bad) const {
+            const uint64_t ku = key_u(t.key);
+            const uint64_t r = ku - bu;
+            const uint32_t pb = 64 - s1;
+            bad |= ku < bu || r > span || ((uint64_t)t.payload >> pb) != 0;
+            return ((r & ((1ull << s1) - 1)) << pb) | (uint64_t)t.payload;
+        }
+    };
+    // packing applies to plans whose level-1 buckets span 2^1 .. 2^32 keys
+    __host__ static bool usable(const RangePlan& P) { return P.s1 >= 1 && P.s1 <= 32; }
+};
+#endif
+
+// identity "packing" of the plain layout
+struct PackNone {
+    typedef Tup OutT;
+    __device__ __forceinline__ Tup operator()(const Tup& t, bool&) const { return t; }
+};
+
 __host__ __device__ __forceinline__ uint32_t plan_d2(const RangePlan& p,
                                                      uint64_t rel,
                                                      uint32_t d1) {

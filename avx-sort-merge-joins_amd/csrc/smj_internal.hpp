@@ -149,11 +149,16 @@ void plan_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
 uint64_t sampled_capacity(uint64_t n, uint32_t dbits);
 // every partition is kShards segments: seg_start/seg_cnt[d * kShards + q]
 constexpr uint32_t kShards = 8;
-void sampled_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
+// `out` holds sampled_capacity() elements: tuples, or (pack_plan != nullptr,
+// 16-byte tuples only) LayPacked words for that plan; *pack_bad is OR-ed with
+// 1 when a tuple cannot be packed (the caller then repeats on tuples).
+void sampled_partition(Workspace* ws, const Tup* in, uint64_t n, void* out,
                        const RangePlan* plan_dev, uint32_t dbits,
                        uint64_t* starts_dev, int64_t* hist_out,
                        uint64_t* seg_start, int64_t* seg_cnt,
-                       unsigned int* flag_dev, hipStream_t st);
+                       unsigned int* flag_dev, hipStream_t st,
+                       const RangePlan* pack_plan = nullptr,
+                       unsigned int* pack_bad = nullptr);
 void hist_memcpy(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
                  uint32_t dbits, hipStream_t st);
 
@@ -164,7 +169,7 @@ extern const uint32_t kGroupD3Max;   // widest level-3 digit of the group pass
 struct BucketSortArgs {
     // level-1 partitioned relation(s): bucket b occupies
     // [bstart[b], bstart[b] + bcount[b]) of `part`.
-    const Tup* part[2];
+    const void* part[2];        // tuples, or LayPacked words when `packed`
     const uint64_t* bstart[2];  // device, nbuckets
     const int64_t* bcount[2];   // device, nbuckets
     // optional (sampled partition): bucket b = kShards segments
@@ -172,7 +177,7 @@ struct BucketSortArgs {
     const uint64_t* seg_start[2] = {nullptr, nullptr};
     const int64_t* seg_cnt[2] = {nullptr, nullptr};
     uint32_t nseg = kShards;    // segments per bucket (the exchange: one per source GPU)
-    Tup* tmp[2];                // same size as part (tile-local pass output)
+    void* tmp[2];               // same size as part (tile-local pass output)
     Tup* out[2];                // sorted output, bucket b at ostart[b]
     uint64_t n[2];
     int nrel;                   // 1 = sort only, 2 = R and S + join count
@@ -183,6 +188,8 @@ struct BucketSortArgs {
     // the plan, when the host computed it (key-range hints): with a sampled
     // partition the bucket pass then runs without a mid-pipeline host sync
     const RangePlan* host_plan = nullptr;
+    bool packed = false;            // part/tmp hold LayPacked words (host_plan's)
+    const unsigned int* pack_bad = nullptr;  // set by the partition: not packable
     hipEvent_t ev_tile = nullptr;   // optional phase markers
     hipEvent_t ev_bucket = nullptr;
     hipEvent_t ev_ovf = nullptr;

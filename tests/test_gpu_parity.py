@@ -343,3 +343,30 @@ def test_device_join_keys_outside_hint(libs, oracles, width):
     assert int(cnt.item()) == exp
     assert np.array_equal(lib.to_host(sR), eR)
     assert np.array_equal(lib.to_host(sS), eS)
+
+
+@pytest.mark.parametrize("payload", ["rowid", "negative", "wide"])
+def test_device_join_packed_words(libs, oracles, width, payload):
+    """With a key-range hint the 16-byte join carries packed words (key offset
+    in the bucket + payload in one 64-bit word) through the intermediate
+    passes.  Payloads that do not fit (negative, or wider than 64 - s1 bits)
+    make the partition flag the attempt and the join rerun on tuples; the
+    result is the same either way."""
+    import torch
+    orc, lib = oracles[width], libs[width]
+    n = 500_000
+    R, S = make_join_inputs(orc, width, "pk_fk", n, n)
+    if payload == "negative":
+        S["payload"][n // 3] = -5
+    elif payload == "wide" and width == 16:
+        R["payload"][7] = np.int64(1) << 60
+    exp, eR, eS = orc.sortmergejoin(R, S)
+    dR, dS = lib.to_device(R), lib.to_device(S)
+    sR, sS = lib.empty(n), lib.empty(n)
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    for _ in range(2):
+        lib.dev_join(dR, dS, sR, sS, cnt, 9, 1, n)
+        torch.cuda.synchronize()
+        assert int(cnt.item()) == exp
+        assert np.array_equal(lib.to_host(sR), eR)
+        assert np.array_equal(lib.to_host(sS), eS)
