@@ -56,10 +56,18 @@ const uint32_t kTileTuples = TILE2;
 #define SMJ_GS_THREADS 256
 #endif
 constexpr int GS_THREADS = SMJ_GS_THREADS;      // one workgroup per group
+// resident group-pass workgroups per CU: 16-byte elements (LDS- and
+// VGPR-bound) and 8-byte ones (tuples or packed words)
 #ifndef SMJ_GS_WG_PER_CU
 #define SMJ_GS_WG_PER_CU 4
 #endif
-constexpr int GS_WG_PER_CU = SMJ_GS_WG_PER_CU;  // resident workgroups per CU
+#ifndef SMJ_GS_WG_PER_CU8
+#define SMJ_GS_WG_PER_CU8 5
+#endif
+template <class W>
+constexpr int gs_wg_per_cu() {
+    return sizeof(W) == 16 ? SMJ_GS_WG_PER_CU : SMJ_GS_WG_PER_CU8;
+}
 #ifndef SMJ_GS_ITEMS
 #define SMJ_GS_ITEMS (1280 / SMJ_GS_THREADS)
 #endif
@@ -650,7 +658,7 @@ __device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS<typename
 // and g+1's S as soon as g's S does, so both gathers fly under g's sort,
 // write-out and count; g+2's tile runs are loaded one group further ahead.
 template <class Lay>
-__global__ void __launch_bounds__(GS_THREADS, GS_WG_PER_CU * GS_THREADS / 256)
+__global__ void __launch_bounds__(GS_THREADS, gs_wg_per_cu<typename Lay::W>() * GS_THREADS / 256)
 k_groupsort(GroupArgs A) {
     typedef typename Lay::W W;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
@@ -1509,7 +1517,7 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
     G.ovf_cap = ovf_cap;
     G.g_begin = 0;
     G.g_end = ngroups;
-    const uint32_t maxwg = GS_WG_PER_CU * 256;
+    const uint32_t maxwg = gs_wg_per_cu<W>() * 256;
     G.per = (ngroups + maxwg - 1) / maxwg;
     {
         const uint32_t nwg = (ngroups + G.per - 1) / G.per;
@@ -1689,9 +1697,9 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
     G.g_begin = 0;
     G.g_end = nb * nb2;
     {
-        // persistent: GS_WG_PER_CU workgroups per CU, consecutive groups each
+        // persistent: gs_wg_per_cu workgroups per CU, consecutive groups each
         const uint32_t ng = G.g_end - G.g_begin;
-        const uint32_t maxwg = GS_WG_PER_CU * 256;
+        const uint32_t maxwg = gs_wg_per_cu<Tup>() * 256;
         G.per = (ng + maxwg - 1) / maxwg;
         const uint32_t nwg = (ng + G.per - 1) / G.per;
         TraceScope ts(ws, "k_groupsort", st);
