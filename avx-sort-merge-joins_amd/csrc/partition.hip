@@ -560,9 +560,6 @@ k_sample_hist(const Tup* __restrict__ in, uint64_t n, uint32_t stride,
 #ifndef SMJ_SC_SEG
 #define SMJ_SC_SEG 64
 #endif
-#ifndef SMJ_SC_ABL
-#define SMJ_SC_ABL 0
-#endif
 constexpr uint32_t kSegBytes = SMJ_SC_SEG;
 
 __global__ void __launch_bounds__(256)
@@ -632,6 +629,24 @@ k_regions_done(const uint64_t* __restrict__ seg_start,
     }
 }
 
+// lanes of the scatter write whole 64-byte segments: the complete segments
+// of a tile are numbered, segown[s] = the partition of segment s
+template <int THREADS, int ITEMS, class OutT>
+struct ScatterGeom {
+    static constexpr uint32_t SEG = kSegBytes / sizeof(OutT);  // elements per segment
+    static constexpr uint32_t TILE = THREADS * ITEMS;
+    static __host__ __device__ constexpr uint32_t max_segs(uint32_t nbins) {
+        return (TILE + nbins * (SEG - 1)) / SEG;
+    }
+    // stage OutT[TILE] | carry OutT[nbins * SEG] | pos u64[nbins] |
+    // tstart, tfill, kc, segpre u32[nbins] | segown u16[max_segs] | scan scratch
+    static __host__ __device__ constexpr size_t lds_bytes(uint32_t nbins) {
+        return (size_t)TILE * sizeof(OutT) + (size_t)nbins * kSegBytes +
+               (size_t)nbins * (8 + 4 * 4) + ((size_t)max_segs(nbins) * 2 + 15) / 16 * 16 +
+               (THREADS / 64 + 1) * 4;
+    }
+};
+
 template <int THREADS, int ITEMS, class Digit, class Pack>
 __global__ void __launch_bounds__(THREADS)
 k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_arg,
@@ -640,22 +655,26 @@ k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
               typename Pack::OutT* __restrict__ out, Pack pk,
               unsigned int* __restrict__ bad_flag) {
     typedef typename Pack::OutT OutT;
+    typedef ScatterGeom<THREADS, ITEMS, OutT> Geo;
+    constexpr uint32_t SEG = Geo::SEG;
+    constexpr int TILE = (int)Geo::TILE;
     bool bad = false;
     const auto dig = dig_arg.load();
     // this workgroup's shard of every partition: cursor[d * kShards + shard]
     const uint32_t shard = blockIdx.x % kShards;
     unsigned long long* cursor = cursor_all + shard;
     const uint64_t* cap_end = cap_end_all + shard;
-    constexpr int TILE = THREADS * ITEMS;
-    constexpr uint32_t SEG = kSegBytes / sizeof(OutT);  // elements per segment
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
-    Tup* stage = reinterpret_cast<Tup*>(lds_raw);
-    OutT* carry = reinterpret_cast<OutT*>(stage + TILE);
+    OutT* stage = reinterpret_cast<OutT*>(lds_raw);
+    OutT* carry = stage + TILE;
     uint64_t* pos = reinterpret_cast<uint64_t*>(carry + (size_t)nbins * SEG);
     uint32_t* tstart = reinterpret_cast<uint32_t*>(pos + nbins);
     uint32_t* tfill = tstart + nbins;
     uint32_t* kc = tfill + nbins;
-    uint32_t* scr = kc + nbins;
+    uint32_t* segpre = kc + nbins;
+    uint16_t* segown = reinterpret_cast<uint16_t*>(segpre + nbins);
+    uint32_t* scr = reinterpret_cast<uint32_t*>(
+        reinterpret_cast<unsigned char*>(segown) + ((size_t)Geo::max_segs(nbins) * 2 + 15) / 16 * 16);
 
     for (uint32_t d = threadIdx.x; d < nbins; d += THREADS) {
         tfill[d] = 0;
@@ -669,6 +688,7 @@ k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
     const uint32_t d0 = threadIdx.x;
     const bool own = d0 < nbins;
     const uint64_t my_cap = own ? cap_end[(size_t)d0 * kShards] : 0;
+    uint32_t my_kc = 0;
 
     Tup v[ITEMS], nv[ITEMS];
 #pragma unroll
@@ -694,23 +714,24 @@ k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
             if (dg[j] != 0xffffffffu) atomicAdd(&tfill[dg[j]], 1u);
         }
         __syncthreads();
-        const uint32_t loc = own ? tfill[d0] : 0;
+        // ---- per partition: the whole segments of carry + tile (E, a
+        // multiple of SEG) are written now; stage offsets and segment numbers
+        // in one scan (c | segments << 16: both stay below 2^16)
+        const uint32_t c = own ? tfill[d0] : 0;
+        const uint32_t T = my_kc + c;
+        uint32_t Eown = T / SEG * SEG;
         uint32_t tot;
-        uint32_t ex = block_exclusive_scan(loc, scr, &tot);
-        // ---- per partition: reserve the whole segments of carry + tile (E,
-        // a multiple of SEG) in the region.  The reservations are issued
-        // before the next tile's loads, so waiting for them (after the
-        // staging below) does not wait for that prefetch.
-        uint32_t Eown = 0;
+        const uint32_t ex = block_exclusive_scan(own ? (c | ((Eown / SEG) << 16)) : 0u, scr, &tot);
+        const uint32_t nseg = tot >> 16;
         unsigned long long Pown = 0;
         if (own) {
-            const uint32_t d = d0;
-            const uint32_t c = loc;
-            tstart[d] = ex;
-            tfill[d] = ex;
-            const uint32_t T = kc[d] + c;
-            Eown = T / SEG * SEG;
-            if (Eown) Pown = atomicAdd(&cursor[(size_t)d * kShards], (unsigned long long)Eown);
+            tstart[d0] = ex & 0xffffu;
+            tfill[d0] = ex & 0xffffu;
+            segpre[d0] = ex >> 16;
+            for (uint32_t k = 0; k < Eown / SEG; k++) segown[(ex >> 16) + k] = (uint16_t)d0;
+            // reservation issued before the next tile's loads, so waiting for
+            // it (after the staging below) does not wait for that prefetch
+            if (Eown) Pown = atomicAdd(&cursor[(size_t)d0 * kShards], (unsigned long long)Eown);
         }
         // unconditional (clamped) loads: a fixed count in flight lets the
         // reservation results be waited for with vmcnt(ITEMS)
@@ -722,56 +743,36 @@ k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < ITEMS; j++)
-            if (dg[j] != 0xffffffffu) stage[atomicAdd(&tfill[dg[j]], 1u)] = v[j];
+            if (dg[j] != 0xffffffffu) stage[atomicAdd(&tfill[dg[j]], 1u)] = pk(v[j], bad);
         if (own) {
             // an overflowing region writes nothing (the caller repeats the
             // exact partition)
-            uint32_t E = Eown;
-            if (E && Pown + E > my_cap) E = 0;
-            pos[d0] = Pown;
-            Eown = E;
+            const bool ovf = Eown && Pown + Eown > my_cap;
+            pos[d0] = ovf ? ~0ull : Pown;
+            if (ovf) Eown = 0;
         }
         __syncthreads();
-        if (own) tfill[d0] = Eown;
-        __syncthreads();
-        for (uint32_t q = threadIdx.x; q < nbins * SEG; q += THREADS) {
-            const uint32_t d = q / SEG, j = q % SEG;
-            if (j < kc[d] && j < tfill[d]) out[pos[d] + j] = carry[q];
-        }
-        OutT keep[ITEMS];
-        uint32_t kslot[ITEMS];
-#pragma unroll
-        for (int j = 0; j < ITEMS; j++) {
-            const uint32_t i = j * THREADS + threadIdx.x;
-            kslot[j] = 0xffffffffu;
-            if (i < tcount) {
-                const Tup t = stage[i];
-                const uint32_t d = dig(t);
-                const uint32_t vv = kc[d] + (i - tstart[d]);
-                const uint32_t E = tfill[d];
-                if (vv < E) {
-#if SMJ_SC_ABL == 1
-                    out[base + i] = pk(t, bad);  // ablation: linear writes
-#elif SMJ_SC_ABL == 2
-                    if (tup_key(t) == -12345) out[pos[d] + vv] = pk(t, bad);  // ablation: no writes
-#else
-                    out[pos[d] + vv] = pk(t, bad);  // plain stores: the L2 merges partial lines
-#endif
-                } else if (vv - E < SEG) {  // always, unless the region overflowed
-                    keep[j] = pk(t, bad);
-                    kslot[j] = d * SEG + (vv - E);
-                }
-            }
+        // ---- whole segments: SEG consecutive lanes per segment, element e of
+        // a partition = carry (e < kc) or its staged tuples
+        for (uint32_t q = threadIdx.x; q < nseg * SEG; q += THREADS) {
+            const uint32_t sg = q / SEG;
+            const uint32_t d = segown[sg];
+            const uint32_t e = (sg - segpre[d]) * SEG + q % SEG;
+            const uint32_t k = kc[d];
+            const uint64_t p = pos[d];
+            const OutT x = e < k ? carry[d * SEG + e] : stage[tstart[d] + e - k];
+            if (p != ~0ull) out[p + e] = x;
         }
         __syncthreads();
-#pragma unroll
-        for (int j = 0; j < ITEMS; j++)
-            if (kslot[j] != 0xffffffffu) carry[kslot[j]] = keep[j];
+        // ---- leftovers (< SEG) become the partition's carry
         if (own) {
-            const uint32_t T = kc[d0] + loc;
-            // E == 0 after an overflow: keep at most SEG - 1 (the rest is
-            // lost; the partition is repeated anyway)
-            kc[d0] = T - Eown < SEG ? T - Eown : SEG - 1;
+            uint32_t left = T - Eown;
+            if (left > SEG - 1) left = SEG - 1;  // only after an overflow (discarded)
+            for (uint32_t e = Eown; e < Eown + left; e++)
+                carry[d0 * SEG + (e - Eown)] =
+                    e < my_kc ? carry[d0 * SEG + e] : stage[tstart[d0] + e - my_kc];
+            my_kc = left;
+            kc[d0] = left;
             tfill[d0] = 0;
         }
 #pragma unroll
@@ -1127,9 +1128,8 @@ static void sampled_scatter(Workspace* ws, const Tup* in, uint64_t n, void* out,
     const uint64_t tiles_per_wg = (ntiles + nwg - 1) / nwg;
     const uint64_t chunk = tiles_per_wg * TILE;
     nwg = (uint32_t)((ntiles + tiles_per_wg - 1) / tiles_per_wg);
-    // stage TILE | carry nbins segments | pos u64, tstart, tfill, kc u32
-    const size_t lds = (size_t)TILE * sizeof(Tup) + (size_t)nbins * kSegBytes +
-                       (size_t)nbins * (8 + 4 + 4 + 4) + 64;
+    const size_t lds =
+        ScatterGeom<THREADS, ITEMS, typename Pack::OutT>::lds_bytes(nbins);
     static bool attr = false;
     if (!attr) {
         SMJ_CHECK(hipFuncSetAttribute(
