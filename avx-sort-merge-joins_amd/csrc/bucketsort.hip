@@ -48,6 +48,9 @@ constexpr int TP_THREADS = SMJ_TP_THREADS;
 #ifndef SMJ_GATHER_NT
 #define SMJ_GATHER_NT 0
 #endif
+#ifndef SMJ_GS_ABL
+#define SMJ_GS_ABL 0  // ablations for measurements only (1: no in-group sort)
+#endif
 constexpr int TP_ITEMS = 16;
 constexpr int TILE2 = TP_THREADS * TP_ITEMS;  // tuples per tile
 const uint32_t kTileTuples = TILE2;
@@ -559,6 +562,19 @@ __device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS<typename
                                            Hook&& after_place) {
     const uint32_t tid = otid(), wid = tid >> 6, lane = tid & 63;
     const uint32_t d12 = (C.b << P.D2) | C.g;
+#if SMJ_GS_ABL == 1
+    {   // ablation (measurements only): no sort, gathered order written out
+        Tup* dst = A.out[r] + C.ost[r] + off;
+#pragma unroll
+        for (int k = 0; k < GS_ITEMS; k++) {
+            const uint32_t j = k * GS_THREADS + tid;
+            if (j < nr) st_stream(dst + j, Lay::unpack(P, v[k], C.b));
+        }
+        after_place();
+        __syncthreads();
+        return true;
+    }
+#endif
     // ---- level-3 digits, histogram (two u16 counters per word)
     uint32_t dg[GS_ITEMS];
 #pragma unroll

@@ -1104,12 +1104,12 @@ k_seg_tables(const int64_t* __restrict__ cnt, uint32_t nseg, uint32_t nb,
     }
 }
 
-void smj_dev_join_segmented(smj_workspace* wsp, tuple_t* R, uint64_t nR,
-                            const int64_t* segR, tuple_t* S, uint64_t nS,
+void smj_dev_join_segmented(smj_workspace* wsp, void* R, uint64_t nR,
+                            const int64_t* segR, void* S, uint64_t nS,
                             const int64_t* segS, uint32_t nseg, uint32_t bucket_bits,
-                            int64_t key_lo, int64_t key_hi, tuple_t* sortedR,
-                            tuple_t* sortedS, unsigned long long* count_dev,
-                            smj_stream_t stream) {
+                            int64_t key_lo, int64_t key_hi, uint32_t flags,
+                            tuple_t* sortedR, tuple_t* sortedS,
+                            unsigned long long* count_dev, smj_stream_t stream) {
     Workspace* ws = (Workspace*)wsp;
     hipStream_t st = (hipStream_t)stream;
     if (nseg == 0 || bucket_bits > 10 || nR >= (1ull << 32) || nS >= (1ull << 32)) {
@@ -1128,10 +1128,24 @@ void smj_dev_join_segmented(smj_workspace* wsp, tuple_t* R, uint64_t nR,
     if (D2 > 9) D2 = 9;
     D2cap = D2 + 2 > 9 ? (D2 > 9 ? D2 : 9) : D2 + 2;
     RangePlan hplan = make_plan(key_lo, key_hi, D1, D2, D2cap, kGroupD3Max);
+    const bool packed = (flags & SMJ_SEG_PACKED) != 0;
+#ifdef KEY_8B
+    if (packed && !LayPacked::usable(hplan)) {
+        fprintf(stderr, "[ERROR] smj_dev_join_segmented: packed words need 1 <= s1 <= 32 "
+                "(s1 = %u)\n", hplan.s1);
+        abort();
+    }
+#else
+    if (packed) {
+        fprintf(stderr, "[ERROR] smj_dev_join_segmented: packed words are a 16-byte-tuple "
+                "layout\n");
+        abort();
+    }
+#endif
     RangePlan* plan = (RangePlan*)ws->scratch("plan", sizeof(RangePlan));
     hipLaunchKernelGGL(k_setplan, dim3(1), dim3(1), 0, st, plan, hplan);
     const uint32_t nb = 1u << D1;
-    Tup* rel[2] = {(Tup*)R, (Tup*)S};
+    void* rel[2] = {R, S};
     const int64_t* seg[2] = {segR, segS};
     static const char* nm[2][4] = {{"xs_startR", "xs_cntR", "xs_bcR", "xs_bsR"},
                                    {"xs_startS", "xs_cntS", "xs_bcS", "xs_bsS"}};
@@ -1163,6 +1177,7 @@ void smj_dev_join_segmented(smj_workspace* wsp, tuple_t* R, uint64_t nR,
     SMJ_CHECK(hipMemsetAsync(flag, 0, 4, st));
     a.part_flag = flag;  // never set: the buckets are exact
     a.host_plan = &hplan;
+    a.packed = packed;  // checked packable before the exchange: no pack_bad here
     if (!bucket_sort(ws, a, st)) {
         fprintf(stderr, "[ERROR] smj_dev_join_segmented: unexpected partition flag\n");
         abort();
@@ -1222,6 +1237,28 @@ void smj_dev_partition_range(smj_workspace* wsp, const tuple_t* in, uint64_t n,
     uint64_t* starts = (uint64_t*)ws->scratch("range_starts", (1u << nbits) * 8);
     plan_partition(ws, (const Tup*)in, n, (Tup*)out, plan, nbits, starts,
                    hist_out, st);
+}
+
+int smj_dev_partition_range_packed(smj_workspace* wsp, const tuple_t* in, uint64_t n,
+                                   uint64_t* out, uint32_t nbits, int64_t key_min,
+                                   int64_t key_max, int64_t* hist_out,
+                                   unsigned int* bad_flag, smj_stream_t stream) {
+#ifdef KEY_8B
+    Workspace* ws = (Workspace*)wsp;
+    hipStream_t st = (hipStream_t)stream;
+    RangePlan h = make_plan(key_min, key_max, nbits, 0, 0, 0);
+    if (!LayPacked::usable(h)) return 0;
+    RangePlan* plan = (RangePlan*)ws->scratch("range_plan", sizeof(RangePlan));
+    hipLaunchKernelGGL(k_setplan, dim3(1), dim3(1), 0, st, plan, h);
+    uint64_t* starts = (uint64_t*)ws->scratch("range_starts", (1u << nbits) * 8);
+    plan_partition_packed(ws, (const Tup*)in, n, out, plan, h, nbits, starts, hist_out,
+                          bad_flag, st);
+    return 1;
+#else
+    (void)wsp; (void)in; (void)n; (void)out; (void)nbits; (void)key_min; (void)key_max;
+    (void)hist_out; (void)bad_flag; (void)stream;
+    return 0;
+#endif
 }
 
 void smj_trace_enable(smj_workspace* wsp, int on) {

@@ -270,12 +270,14 @@ constexpr size_t scatter_u_lds(uint32_t nbins) {
     return (size_t)THREADS * ITEMS * sizeof(Tup) + (size_t)nbins * 16 + 64;
 }
 
-template <int THREADS, int ITEMS, class Digit>
+template <int THREADS, int ITEMS, class Digit, class Pack = PackNone>
 __global__ void __launch_bounds__(THREADS)
 k_scatter_u(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_arg,
             uint32_t nbins, const uint32_t* __restrict__ counts, uint32_t nwg,
-            const uint64_t* __restrict__ starts, Tup* __restrict__ out, int mode) {
+            const uint64_t* __restrict__ starts, typename Pack::OutT* __restrict__ out,
+            int mode, Pack pk = Pack(), unsigned int* __restrict__ bad_flag = nullptr) {
     const auto dig = dig_arg.load();
+    bool bad = false;
     constexpr int TILE = THREADS * ITEMS;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     Tup* stage = reinterpret_cast<Tup*>(lds_raw);
@@ -343,9 +345,9 @@ k_scatter_u(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_ar
         for (uint32_t i = threadIdx.x; i < tcount; i += THREADS) {
             const Tup t = stage[i];
             const uint32_t d = dig(t);
-            if (mode == 0) out[run[d] + (i - tstart[d])] = t;
-            else if (mode == 1) out[base + i] = t;  // ablation: linear write
-            else if (tup_key(t) == -12345) out[0] = t;  // ablation: no write
+            if (mode == 0) out[run[d] + (i - tstart[d])] = pk(t, bad);
+            else if (mode == 1) out[base + i] = pk(t, bad);  // ablation: linear write
+            else if (tup_key(t) == -12345) out[0] = pk(t, bad);  // ablation: no write
         }
         __syncthreads();
         for (uint32_t k = 0; k < dper; k++) {
@@ -359,6 +361,7 @@ k_scatter_u(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_ar
         for (int j = 0; j < ITEMS; j++) v[j] = nv[j];
         __syncthreads();
     }
+    if (bad_flag && bad) atomicOr(bad_flag, 1u);
 }
 
 // Write-combining scatter for the join's level-1 partition (order inside a
@@ -866,12 +869,13 @@ static int pt_variant() {
     return v;
 }
 
-template <int THREADS, int ITEMS, bool STABLE, class Digit>
+template <int THREADS, int ITEMS, bool STABLE, class Digit, class Pack = PackNone>
 static void stable_partition_t(Workspace* ws, const Tup* in, uint64_t n,
-                               Tup* out, const Digit& dig, uint32_t dbits,
+                               typename Pack::OutT* out, const Digit& dig, uint32_t dbits,
                                int padded, uint64_t* starts_dev,
                                int64_t* hist_out, int64_t* off_out,
-                               hipStream_t st) {
+                               hipStream_t st, const Pack& pk = Pack(),
+                               unsigned int* bad_flag = nullptr) {
     constexpr int TILE = THREADS * ITEMS;
     const uint32_t nbins = 1u << dbits;
     uint64_t ntiles = (n + TILE - 1) / TILE;
@@ -898,12 +902,12 @@ static void stable_partition_t(Workspace* ws, const Tup* in, uint64_t n,
                            padded, starts_dev, hist_out, off_out);
     }
     if (n == 0) return;
-    if (!STABLE) {
+    if constexpr (!STABLE) {
         const size_t ldsu = scatter_u_lds<THREADS, ITEMS>(nbins);
         static bool attr_u = false;
         if (!attr_u) {
             SMJ_CHECK(hipFuncSetAttribute(
-                (const void*)k_scatter_u<THREADS, ITEMS, Digit>,
+                (const void*)k_scatter_u<THREADS, ITEMS, Digit, Pack>,
                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
             attr_u = true;
         }
@@ -912,29 +916,30 @@ static void stable_partition_t(Workspace* ws, const Tup* in, uint64_t n,
             abort();
         }
         TraceScope ts(ws, "k_scatter", st);
-        hipLaunchKernelGGL((k_scatter_u<THREADS, ITEMS, Digit>), dim3(nwg),
+        hipLaunchKernelGGL((k_scatter_u<THREADS, ITEMS, Digit, Pack>), dim3(nwg),
                            dim3(THREADS), ldsu, st, in, n, chunk, dig, nbins,
-                           counts, nwg, starts_dev, out, scatter_mode());
+                           counts, nwg, starts_dev, out, scatter_mode(), pk, bad_flag);
         SMJ_CHECK(hipGetLastError());
         return;
-    }
-    const size_t lds = scatter_lds<THREADS, ITEMS>(nbins);
-    static bool attr_set = false;
-    if (!attr_set) {
-        SMJ_CHECK(hipFuncSetAttribute(
-            (const void*)k_scatter<THREADS, ITEMS, Digit>,
-            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        attr_set = true;
-    }
-    if (lds > 160 * 1024) {
-        fprintf(stderr, "[ERROR] smj: scatter LDS %zu > 160 KiB\n", lds);
-        abort();
-    }
-    {
-        TraceScope ts(ws, "k_scatter", st);
-        hipLaunchKernelGGL((k_scatter<THREADS, ITEMS, Digit>), dim3(nwg),
-                           dim3(THREADS), lds, st, in, n, chunk, dig, nbins, dbits,
-                           counts, nwg, starts_dev, out, scatter_mode());
+    } else {
+        const size_t lds = scatter_lds<THREADS, ITEMS>(nbins);
+        static bool attr_set = false;
+        if (!attr_set) {
+            SMJ_CHECK(hipFuncSetAttribute(
+                (const void*)k_scatter<THREADS, ITEMS, Digit>,
+                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+            attr_set = true;
+        }
+        if (lds > 160 * 1024) {
+            fprintf(stderr, "[ERROR] smj: scatter LDS %zu > 160 KiB\n", lds);
+            abort();
+        }
+        {
+            TraceScope ts(ws, "k_scatter", st);
+            hipLaunchKernelGGL((k_scatter<THREADS, ITEMS, Digit>), dim3(nwg),
+                               dim3(THREADS), lds, st, in, n, chunk, dig, nbins, dbits,
+                               counts, nwg, starts_dev, out, scatter_mode());
+        }
     }
     SMJ_CHECK(hipGetLastError());
 }
@@ -1086,6 +1091,29 @@ void plan_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
                        nwg, starts_dev, out);
     SMJ_CHECK(hipGetLastError());
 }
+
+#ifdef KEY_8B
+// plan_partition writing LayPacked words for `pack_plan` (the multi-GPU
+// exchange: half the bytes on the wire); *pack_bad |= 1 when a tuple does
+// not pack.  Histogram + unstable scatter (partitions back to back).
+void plan_partition_packed(Workspace* ws, const Tup* in, uint64_t n, uint64_t* out,
+                           const RangePlan* plan_dev, const RangePlan& pack_plan,
+                           uint32_t dbits, uint64_t* starts_dev, int64_t* hist_out,
+                           unsigned int* pack_bad, hipStream_t st) {
+    PlanDigit1 dig{plan_dev};
+    LayPacked::Pack pk;
+    pk.bu = key_u(pack_plan.base);
+    pk.span = pack_plan.span;
+    pk.s1 = pack_plan.s1;
+    // the 16-byte stage of 512x16 tiles and 2^12 bins would exceed 160 KiB
+    if (dbits > 10)
+        stable_partition_t<256, 8, false, PlanDigit1, LayPacked::Pack>(
+            ws, in, n, out, dig, dbits, 0, starts_dev, hist_out, nullptr, st, pk, pack_bad);
+    else
+        stable_partition_t<512, 16, false, PlanDigit1, LayPacked::Pack>(
+            ws, in, n, out, dig, dbits, 0, starts_dev, hist_out, nullptr, st, pk, pack_bad);
+}
+#endif
 
 // Sampled level-1 partition (see k_scatter_res): `out` must hold
 // sampled_capacity(n, dbits) tuples.  starts_dev/hist_out receive each

@@ -145,6 +145,12 @@ void stable_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
 void plan_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
                     const RangePlan* plan_dev, uint32_t dbits,
                     uint64_t* starts_dev, int64_t* hist_out, hipStream_t st);
+#ifdef KEY_8B
+void plan_partition_packed(Workspace* ws, const Tup* in, uint64_t n, uint64_t* out,
+                           const RangePlan* plan_dev, const RangePlan& pack_plan,
+                           uint32_t dbits, uint64_t* starts_dev, int64_t* hist_out,
+                           unsigned int* pack_bad, hipStream_t st);
+#endif
 // sampled level-1 partition (join): regions with slack, no histogram pass
 uint64_t sampled_capacity(uint64_t n, uint32_t dbits);
 // every partition is kShards segments: seg_start/seg_cnt[d * kShards + q]

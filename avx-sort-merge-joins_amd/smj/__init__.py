@@ -56,6 +56,7 @@ DEVICE_SYMBOLS = [
     "smj_dev_join", "smj_join_phase_ms", "smj_dev_gen_pk", "smj_dev_gen_fk",
     "smj_dev_gen_zipf", "smj_dev_synchronize", "smj_dev_partition_range",
     "smj_trace_enable", "smj_trace_reset", "smj_trace_read", "smj_dev_join_segmented",
+    "smj_dev_partition_range_packed",
 ]
 
 
@@ -151,7 +152,9 @@ class Library:
             "smj_dev_synchronize": (None, [_P]),
             "smj_dev_partition_range": (None, [_P, _P, _U64, _P, _U32, _I64, _I64, _P, _P]),
             "smj_dev_join_segmented": (None, [_P, _P, _U64, _P, _P, _U64, _P, _U32, _U32,
-                                              _I64, _I64, _P, _P, _P, _P]),
+                                              _I64, _I64, _U32, _P, _P, _P, _P]),
+            "smj_dev_partition_range_packed": (C.c_int, [_P, _P, _U64, _P, _U32, _I64, _I64,
+                                                         _P, _P, _P]),
             "smj_trace_enable": (None, [_P, C.c_int]),
             "smj_trace_reset": (None, [_P]),
             "smj_trace_read": (C.c_int, [_P, C.c_char_p, C.c_int, _P, _P, C.c_int]),
@@ -325,16 +328,26 @@ class Library:
                               self.stream_ptr())
 
     def dev_join_segmented(self, R, segR, S, segS, bucket_bits, key_lo, key_hi,
-                           sortedR, sortedS, count):
+                           sortedR, sortedS, count, packed=False):
         """Local join of exchanged range partitions (smj_dev_join_segmented):
         segR/segS are int64 (nseg, 2^bucket_bits) device tensors, row s = the
-        partition sizes received from source s.  R and S are overwritten."""
+        partition sizes received from source s.  R and S (tuples, or with
+        packed=True int64 words of dev_partition_range_packed) are
+        overwritten."""
         assert segR.is_contiguous() and segS.is_contiguous()
         assert segR.shape == segS.shape and segR.shape[1] == 1 << bucket_bits
         self.lib.smj_dev_join_segmented(
             self.ws, R.data_ptr(), R.shape[0], segR.data_ptr(), S.data_ptr(),
             S.shape[0], segS.data_ptr(), segR.shape[0], bucket_bits, key_lo, key_hi,
-            sortedR.data_ptr(), sortedS.data_ptr(), count.data_ptr(), self.stream_ptr())
+            1 if packed else 0, sortedR.data_ptr(), sortedS.data_ptr(), count.data_ptr(),
+            self.stream_ptr())
+
+    def dev_partition_range_packed(self, inp, out_words, nbits, key_min, key_max, hist, bad):
+        """smj_dev_partition_range writing packed int64 words; False (nothing
+        launched) when the layout does not apply."""
+        return bool(self.lib.smj_dev_partition_range_packed(
+            self.ws, inp.data_ptr(), inp.shape[0], out_words.data_ptr(), nbits, key_min,
+            key_max, hist.data_ptr(), bad.data_ptr(), self.stream_ptr()))
 
     def dev_partition_range(self, inp, out, nbits, key_min, key_max, hist):
         self.lib.smj_dev_partition_range(self.ws, inp.data_ptr(), inp.shape[0],

@@ -34,7 +34,11 @@ import os
 import torch
 import torch.distributed as dist
 
-MAX_PARTITION_BITS = 12  # widest single-pass partition digit of the library
+# Widest exchange partition: 2^11 partitions (at 8 GPUs 256 per rank, each
+# ~61 tiles of the local tile pass, within its 128-tile bucket limit).  The
+# exact scatter costs 0.96 / 1.09 / 1.53 / 3.32 ms per 128M 16-byte tuples at
+# 9 / 10 / 11 / 12 bits (tools/bench_xpart.py): 12 bits scatter too thinly.
+MAX_PARTITION_BITS = 11
 # Largest single message of the row exchange.  RCCL 2.26 (torch 2.10 ROCm)
 # corrupts all_to_all_single messages of 1.6 GB and more (tools/debug_a2a.py);
 # larger exchanges go as chunked point-to-point sends in one group.
@@ -90,20 +94,31 @@ def send_counts(hist: torch.Tensor, world: int) -> torch.Tensor:
 
 
 class DeviceOps:
-    """The device implementation of the ops interface (libsmj_hip*.so)."""
+    """The device implementation of the ops interface (libsmj_hip*.so).
+    16-byte tuples travel as packed 64-bit words (smj_dev_partition_range_packed)
+    unless SMJ_PACK=0."""
 
     def __init__(self, lib):
         self.lib = lib
+        self.can_pack = lib.width == 16 and os.environ.get("SMJ_PACK", "1") != "0"
 
     def empty(self, n):
         return self.lib.empty(n)
 
+    def empty_words(self, n):
+        return torch.empty(max(n, 1), dtype=torch.int64, device="cuda")[:n]
+
     def partition_range(self, inp, out, nbits, key_min, key_max, hist):
         self.lib.dev_partition_range(inp, out, nbits, key_min, key_max, hist)
 
-    def join_segmented(self, R, segR, S, segS, bucket_bits, key_lo, key_hi, sR, sS, count):
+    def partition_range_packed(self, inp, out_words, nbits, key_min, key_max, hist, bad):
+        return self.lib.dev_partition_range_packed(inp, out_words, nbits, key_min, key_max,
+                                                   hist, bad)
+
+    def join_segmented(self, R, segR, S, segS, bucket_bits, key_lo, key_hi, sR, sS, count,
+                       packed=False):
         self.lib.dev_join_segmented(R, segR, S, segS, bucket_bits, key_lo, key_hi,
-                                    sR, sS, count)
+                                    sR, sS, count, packed=packed)
 
 
 class DistributedJoin:
@@ -119,6 +134,8 @@ class DistributedJoin:
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.pbits = min(bucket_bits + ceil_log2(self.world), MAX_PARTITION_BITS)
+        if os.environ.get("SMJ_XBITS"):  # rehearse the G-GPU partition width on fewer
+            self.pbits = int(os.environ["SMJ_XBITS"])
         self.fanout = 1 << self.pbits
         if self.fanout < self.world:
             raise ValueError(f"fanout 2^{self.pbits} < world size {self.world}")
@@ -134,35 +151,60 @@ class DistributedJoin:
         self.key_hi = self.key_lo + (1 << (s1 + self.lbits)) - 1
         self.buf = {}
         self.last_recv = {}
+        self.last_packed = False  # the layout of the last step's exchange
 
-    def _grow(self, key, n):
+    def _grow(self, key, n, words=False):
         b = self.buf.get(key)
         if b is None or b.shape[0] < n:
-            b = self.ops.empty(max(n, 1))
+            b = (self.ops.empty_words if words else self.ops.empty)(max(n, 1))
             self.buf[key] = b
         return b[:n]
 
-    def _exchange(self, rel, key):
+    def _partition(self, rel, key, packed):
+        """Range-partition `rel` (packed words or tuples).  Returns (buffer,
+        histogram, whether every rank packed) -- the last is only known after
+        the size exchange, so it is returned as a device flag."""
+        dev = rel.device
+        hist = torch.zeros(self.fanout, dtype=torch.int64, device=dev)
+        if packed:
+            part = self._grow("pw" + key, rel.shape[0], words=True)
+            bad = torch.zeros(1, dtype=torch.int32, device=dev)
+            if self.ops.partition_range_packed(rel, part, self.pbits, self.key_min,
+                                               self.key_max, hist, bad):
+                return part, hist, bad.to(torch.int64)
+        part = self._grow("part" + key, rel.shape[0])
+        self.ops.partition_range(rel, part, self.pbits, self.key_min, self.key_max, hist)
+        return part, hist, torch.full((1,), -1, dtype=torch.int64, device=dev)
+
+    def _exchange(self, rel, key, allow_pack=True):
         """Partition `rel`, swap partition sizes, start the row all-to-all.
         Returns (receive buffer, per-source sizes of the owned partitions
-        (world, 2^lbits) padded with empty buckets, async work)."""
-        G, F = self.world, self.fanout
+        (world, 2^lbits) padded with empty buckets, async work, packed?)."""
+        G = self.world
         dev = rel.device
-        part = self._grow("part" + key, rel.shape[0])
-        hist = torch.zeros(F, dtype=torch.int64, device=dev)
-        self.ops.partition_range(rel, part, self.pbits, self.key_min, self.key_max, hist)
         mine = self.p_hi - self.p_lo
-        seg = torch.empty(G * mine, dtype=torch.int64, device=dev)
-        dist.all_to_all_single(seg, hist, [mine] * G, self.per_rank, group=self.group)
-        seg = seg.view(G, mine)
-        sizes = torch.cat([send_counts(hist, G), seg.sum(1)]).tolist()  # one sync
-        sl, rl = sizes[:G], sizes[G:]
-        out = self._grow("recv" + key, sum(rl))
+        packed = allow_pack and bool(getattr(self.ops, "can_pack", False))
+        while True:
+            part, hist, flag = self._partition(rel, key, packed)
+            # any rank that could not pack (1) or did not try (-1): all ranks
+            # send tuples.  MAX over ranks of (flag != 0).
+            agree = flag.ne(0).to(torch.int64)
+            dist.all_reduce(agree, op=dist.ReduceOp.MAX, group=self.group)
+            seg = torch.empty(G * mine, dtype=torch.int64, device=dev)
+            dist.all_to_all_single(seg, hist, [mine] * G, self.per_rank, group=self.group)
+            seg = seg.view(G, mine)
+            sizes = torch.cat([send_counts(hist, G), seg.sum(1), agree]).tolist()  # one sync
+            if packed and sizes[-1]:
+                packed = False  # repeat on tuples, on every rank
+                continue
+            break
+        sl, rl = sizes[:G], sizes[G:2 * G]
+        out = self._grow(("rw" if packed else "recv") + key, sum(rl), words=packed)
         work = self._rows(out, part, rl, sl)
         self.last_recv[key] = (sl, rl)
         pad = torch.zeros(G, 1 << self.lbits, dtype=torch.int64, device=dev)
         pad[:, :mine] = seg
-        return out, pad, work
+        return out, pad, work, packed
 
     def _rows(self, out, inp, rl, sl):
         """Asynchronous row all-to-all: `inp` holds sl[g] rows for rank g in
@@ -195,13 +237,17 @@ class DistributedJoin:
 
     def step(self, R, S, count):
         # the row exchange of R overlaps the partition of S
-        rR, segR, wR = self._exchange(R, "R")
-        rS, segS, wS = self._exchange(S, "S")
+        rR, segR, wR, pR = self._exchange(R, "R")
+        rS, segS, wS, pS = self._exchange(S, "S")
         wR.wait()
         wS.wait()
+        if pR != pS:  # S could not be packed: R again, as tuples
+            rR, segR, wR, pR = self._exchange(R, "R", allow_pack=False)
+            wR.wait()
+        self.last_packed = pR
         sR = self._grow("sortR", rR.shape[0])
         sS = self._grow("sortS", rS.shape[0])
         self.ops.join_segmented(rR, segR, rS, segS, self.lbits, self.key_lo,
-                                self.key_hi, sR, sS, count)
+                                self.key_hi, sR, sS, count, packed=pR)
         dist.all_reduce(count, group=self.group)
         return sR, sS

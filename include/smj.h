@@ -405,22 +405,39 @@ void smj_dev_partition_range(smj_workspace * ws, const tuple_t * in, uint64_t n,
                              int64_t key_max, int64_t * hist_out,
                              smj_stream_t stream);
 
+/* Range partition of smj_dev_partition_range writing one 64-bit word per
+ * tuple instead of the tuple (16-byte tuples only): word = (key offset inside
+ * its partition, the low s1 bits) << (64 - s1) | payload, where partitions
+ * cover 2^s1 keys.  Halves the bytes of the multi-GPU exchange.  Returns 0
+ * (and launches nothing) when the layout does not apply -- the 8-byte
+ * library, or partitions wider than 2^32 keys; otherwise 1, and *bad_flag is
+ * OR-ed with 1 when some tuple cannot be packed (key outside [key_min,
+ * key_max], payload outside [0, 2^(64 - s1))): the caller then partitions
+ * the tuples instead. */
+int smj_dev_partition_range_packed(smj_workspace * ws, const tuple_t * in, uint64_t n,
+                                   uint64_t * out, uint32_t nbits, int64_t key_min,
+                                   int64_t key_max, int64_t * hist_out,
+                                   unsigned int * bad_flag, smj_stream_t stream);
+
 /* Local join of one GPU's share after the exchange (multi-GPU join, no
  * reference counterpart: it replaces the per-thread multiway merge of the
  * reference's T>1 path, src/joins/sortmergejoin_multiway.c:463-556).  R and
  * S are the receive buffers: for every source GPU s in order, its range
  * partitions 0..2^bucket_bits-1 back to back, seg[s * 2^bucket_bits + b]
- * tuples each (device int64).  Every partition b covers the keys
+ * elements each (device int64).  Every partition b covers the keys
  * [key_lo + b * w, key_lo + (b + 1) * w) with 2^bucket_bits * w =
  * key_hi - key_lo + 1 (a power of two), so the partitions are the level-1
- * buckets of the local sort: no local partition pass.  R and S are used as
- * scratch (overwritten).  sortedR/sortedS receive the sorted relations,
- * count_dev the number of matching pairs. */
-void smj_dev_join_segmented(smj_workspace * ws, tuple_t * R, uint64_t nR,
-                            const int64_t * segR, tuple_t * S, uint64_t nS,
+ * buckets of the local sort: no local partition pass.  The elements are
+ * tuples, or (flags & SMJ_SEG_PACKED) the words of
+ * smj_dev_partition_range_packed for the same w.  R and S are used as
+ * scratch (overwritten).  sortedR/sortedS receive the sorted relations as
+ * tuples, count_dev the number of matching pairs. */
+#define SMJ_SEG_PACKED 1u
+void smj_dev_join_segmented(smj_workspace * ws, void * R, uint64_t nR,
+                            const int64_t * segR, void * S, uint64_t nS,
                             const int64_t * segS, uint32_t nseg,
                             uint32_t bucket_bits, int64_t key_lo, int64_t key_hi,
-                            tuple_t * sortedR, tuple_t * sortedS,
+                            uint32_t flags, tuple_t * sortedR, tuple_t * sortedS,
                             unsigned long long * count_dev, smj_stream_t stream);
 
 /* Per-kernel HIP-event trace of the join pipeline (bench.py roofline). */

@@ -19,13 +19,54 @@ from conftest import PKG, ROOT
 
 
 class HostOps:
-    """Host stand-ins for DeviceOps (16-byte tuples as (n, 2) int64 rows)."""
+    """Host stand-ins for DeviceOps (16-byte tuples as (n, 2) int64 rows; the
+    packed exchange as int64 words, like smj_dev_partition_range_packed)."""
+
+    can_pack = True
 
     def __init__(self, orc):
         self.orc = orc
 
     def empty(self, n):
         return torch.empty((n, 2), dtype=torch.int64)
+
+    def empty_words(self, n):
+        return torch.empty(n, dtype=torch.int64)
+
+    @staticmethod
+    def _s1(key_min, key_max, bits):
+        from smj.dist import plan_shift
+        return plan_shift(key_min, key_max, bits)
+
+    def partition_range_packed(self, inp, out, nbits, key_min, key_max, hist, bad):
+        from smj.dist import range_digit
+        s1 = self._s1(key_min, key_max, nbits)
+        if not 1 <= s1 <= 32:
+            return False
+        L = max(key_max - key_min, 0).bit_length()
+        k = inp[:, 1].numpy().astype(np.int64)
+        p = inp[:, 0].numpy().astype(np.int64)
+        rel = k - key_min
+        if ((k < key_min) | (rel > (1 << L) - 1) | (p < 0) | (p >= (1 << (64 - s1)))).any():
+            bad.fill_(1)
+        d = range_digit(inp[:, 1], key_min, key_max, nbits)
+        w = ((rel.astype(np.uint64) & np.uint64((1 << s1) - 1)) << np.uint64(64 - s1)) | \
+            p.astype(np.uint64)
+        order = torch.argsort(d, stable=True)
+        out[: inp.shape[0]] = torch.from_numpy(w.view(np.int64))[order]
+        hist.copy_(torch.bincount(d, minlength=1 << nbits))
+        return True
+
+    def _unpack(self, words, seg, key_lo, key_hi, bucket_bits):
+        s1 = self._s1(key_lo, key_hi, bucket_bits)
+        b = torch.repeat_interleave(torch.arange(seg.shape[1]).repeat(seg.shape[0]),
+                                    seg.reshape(-1)).numpy().astype(np.uint64)
+        w = words.numpy().view(np.uint64)
+        rel = (b << np.uint64(s1)) | (w >> np.uint64(64 - s1))
+        rows = np.empty((len(w), 2), np.int64)
+        rows[:, 1] = key_lo + rel.astype(np.int64)
+        rows[:, 0] = (w & np.uint64((1 << (64 - s1)) - 1)).astype(np.int64)
+        return torch.from_numpy(rows)
 
     def partition_range(self, inp, out, nbits, key_min, key_max, hist):
         from smj.dist import range_digit
@@ -34,8 +75,12 @@ class HostOps:
         out[: inp.shape[0]] = inp[order]
         hist.copy_(torch.bincount(d, minlength=1 << nbits))
 
-    def join_segmented(self, R, segR, S, segS, bucket_bits, key_lo, key_hi, sR, sS, count):
+    def join_segmented(self, R, segR, S, segS, bucket_bits, key_lo, key_hi, sR, sS, count,
+                       packed=False):
         from smj.dist import range_digit
+        if packed:
+            R = self._unpack(R, segR, key_lo, key_hi, bucket_bits)
+            S = self._unpack(S, segS, key_lo, key_hi, bucket_bits)
         # the receive layout the device join relies on: source by source,
         # local bucket b holds exactly the keys of local digit b
         for rows, seg in ((R, segR), (S, segS)):
@@ -53,7 +98,7 @@ class HostOps:
         count.fill_(c)
 
 
-def _worker(rank, world, port, n, q):
+def _worker(rank, world, port, n, q, s_payload="negative"):
     import sys
     for p in (ROOT, PKG):
         sys.path.insert(0, p)
@@ -71,7 +116,9 @@ def _worker(rank, world, port, n, q):
         R["payload"] = np.arange(total)
         orc.seed(54321)
         S = orc.create_relation_zipf(total, total, 0.5)
-        S["payload"] = -np.arange(total)
+        # negative S payloads cannot be packed: R goes packed first, then both
+        # as tuples; non-negative ones: both relations travel as packed words
+        S["payload"] = -np.arange(total) if s_payload == "negative" else np.arange(total)
         expect = orc.merge_join(np.sort(R, order="key"), np.sort(S, order="key"))
 
         def rows(t):
@@ -82,6 +129,7 @@ def _worker(rank, world, port, n, q):
         for _ in range(2):  # second step reuses the grown buffers
             sR, sS = dj.step(rows(R), rows(S), count)
             assert int(count.item()) == expect
+            assert dj.last_packed == (s_payload == "rowid")
         # every key this rank sorted is in its contiguous share of the range
         own = owners(dj.fanout, world)
         for got in (sR, sS):
@@ -107,16 +155,21 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world,chunk_mb", [(2, None), (3, None), (2, 0), (3, 0)])
-def test_distributed_join_gloo(world, chunk_mb, oracles, monkeypatch):
+@pytest.mark.parametrize("world,chunk_mb,s_payload", [
+    (2, None, "negative"), (3, None, "negative"), (2, 0, "negative"), (3, 0, "rowid"),
+    (2, None, "rowid"), (3, None, "rowid")])
+def test_distributed_join_gloo(world, chunk_mb, s_payload, oracles, monkeypatch):
     """chunk_mb 0: every row message over the chunk limit, so the exchange
-    takes the chunked isend/irecv path (the one RCCL needs for >1.6 GB)."""
+    takes the chunked isend/irecv path (the one RCCL needs for >1.6 GB).
+    s_payload "rowid": both relations exchanged as packed words; "negative":
+    S cannot be packed, every rank falls back to tuples for both."""
     if chunk_mb is not None:
         monkeypatch.setenv("SMJ_A2A_CHUNK_MB", str(chunk_mb))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, 5000, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, 5000, q, s_payload))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

@@ -29,10 +29,13 @@ def _inputs(orc, kind, n):
 
 @pytest.mark.parametrize("world", [2, 3, 8])
 @pytest.mark.parametrize("kind", ["pk_fk", "zipf"])
-def test_segmented_join_simulated_exchange(libs, oracles, width, world, kind):
+@pytest.mark.parametrize("packed", [False, True])
+def test_segmented_join_simulated_exchange(libs, oracles, width, world, kind, packed):
     import torch
     from smj.dist import DistributedJoin, ceil_log2, owned, plan_shift
     orc, lib = oracles[width], libs[width]
+    if packed and width != 16:
+        pytest.skip("packed words are the 16-byte layout")
     n = 600_000
     R, S = _inputs(orc, kind, n)
     total, _, _ = orc.sortmergejoin(R, S)
@@ -46,10 +49,17 @@ def test_segmented_join_simulated_exchange(libs, oracles, width, world, kind):
         for s in range(world):
             sl = rel[s * n // world:(s + 1) * n // world]
             d_in = lib.to_device(sl)
-            out = lib.empty(len(sl))
             hist = torch.zeros(F, dtype=torch.int64, device="cuda")
-            lib.dev_partition_range(d_in, out, pbits, 1, n, hist)
-            torch.cuda.synchronize()
+            if packed:
+                out = torch.empty(len(sl), dtype=torch.int64, device="cuda")
+                bad = torch.zeros(1, dtype=torch.int32, device="cuda")
+                assert lib.dev_partition_range_packed(d_in, out, pbits, 1, n, hist, bad)
+                torch.cuda.synchronize()
+                assert int(bad.item()) == 0
+            else:
+                out = lib.empty(len(sl))
+                lib.dev_partition_range(d_in, out, pbits, 1, n, hist)
+                torch.cuda.synchronize()
             parts[key, s] = (out, hist)
     got_total = 0
     for g in range(world):
@@ -72,7 +82,7 @@ def test_segmented_join_simulated_exchange(libs, oracles, width, world, kind):
         sR, sS = lib.empty(nR), lib.empty(nS)
         cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
         lib.dev_join_segmented(recv["R"], segs["R"], recv["S"], segs["S"], lbits,
-                               key_lo, key_hi, sR, sS, cnt)
+                               key_lo, key_hi, sR, sS, cnt, packed=packed)
         torch.cuda.synchronize()
         # the oracle on this rank's share of the key range
         lo_k, hi_k = 1 + (p_lo << s1), 1 + (p_hi << s1)
@@ -113,6 +123,7 @@ def test_distributed_join_one_rank_rccl(libs, width):
             sR, sS = dj.step(R, S, count)
             torch.cuda.synchronize()
             assert int(count.item()) == n
+            assert dj.last_packed == (width == 16)
         ref = torch.sort(S[:, 1].to(torch.int64)).values
         assert torch.equal(sS[:, 1].to(torch.int64), ref)
         assert torch.equal(sR[:, 1].to(torch.int64), torch.arange(1, n + 1, device="cuda"))
