@@ -152,6 +152,14 @@ class DistributedJoin:
         self.buf = {}
         self.last_recv = {}
         self.last_packed = False  # the layout of the last step's exchange
+        self.stats_reset()
+
+    def stats_reset(self):
+        """Exchange statistics since the last reset: bytes this rank sent to
+        other ranks, steps, and (GPU) the time of S's row exchange -- from
+        its issue to its completion, with nothing else queued behind it."""
+        self.stats = {"steps": 0, "sent_B": 0, "recv_B": 0, "xS_ms": 0.0}
+        self._ev = []
 
     def _grow(self, key, n, words=False):
         b = self.buf.get(key)
@@ -200,10 +208,18 @@ class DistributedJoin:
             break
         sl, rl = sizes[:G], sizes[G:2 * G]
         out = self._grow(("rw" if packed else "recv") + key, sum(rl), words=packed)
+        row = 8 if packed else part.element_size() * (part.shape[1] if part.dim() > 1 else 1)
+        self.stats["sent_B"] += row * (sum(sl) - sl[self.rank])
+        self.stats["recv_B"] += row * (sum(rl) - rl[self.rank])
+        ev = None
+        if key == "S" and out.is_cuda:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
         work = self._rows(out, part, rl, sl)
         self.last_recv[key] = (sl, rl)
         pad = torch.zeros(G, 1 << self.lbits, dtype=torch.int64, device=dev)
         pad[:, :mine] = seg
+        self._ev_issue = ev
         return out, pad, work, packed
 
     def _rows(self, out, inp, rl, sl):
@@ -239,8 +255,14 @@ class DistributedJoin:
         # the row exchange of R overlaps the partition of S
         rR, segR, wR, pR = self._exchange(R, "R")
         rS, segS, wS, pS = self._exchange(S, "S")
+        eS = self._ev_issue
         wR.wait()
         wS.wait()
+        if eS is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            self._ev.append((eS, e1))
+        self.stats["steps"] += 1
         if pR != pS:  # S could not be packed: R again, as tuples
             rR, segR, wR, pR = self._exchange(R, "R", allow_pack=False)
             wR.wait()
@@ -251,3 +273,11 @@ class DistributedJoin:
                                 self.key_hi, sR, sS, count, packed=pR)
         dist.all_reduce(count, group=self.group)
         return sR, sS
+
+    def stats_read(self):
+        """The statistics with S's exchange time summed (synchronises)."""
+        for a, b in self._ev:
+            b.synchronize()
+            self.stats["xS_ms"] += a.elapsed_time(b)
+        self._ev = []
+        return dict(self.stats)

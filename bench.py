@@ -182,6 +182,8 @@ def main():
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
+    if exchange:
+        dj.stats_reset()
     lib.trace(True)
     t0 = time.perf_counter()
     for _ in range(a.steps):
@@ -197,6 +199,19 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    xchg = None
+    if exchange:
+        st = dj.stats_read()
+        k = max(st["steps"], 1)
+        # xGMI bytes per GPU per step and S's row all-to-all rate (SURVEY.md
+        # §8(d): against 7 links x 153 GB/s, not HBM)
+        xchg = {"xgmi_bytes_sent_per_gpu": st["sent_B"] // k,
+                "xgmi_bytes_recv_per_gpu": st["recv_B"] // k,
+                "packed_words": bool(dj.last_packed),
+                "exchange_S_ms": round(st["xS_ms"] / k, 3),
+                "exchange_S_GBps": round(st["sent_B"] / 2 / k / (st["xS_ms"] / k * 1e-3) / 1e9, 1)
+                if st["xS_ms"] > 0 and st["sent_B"] > 0 else None,
+                "xgmi_peak_GBps": 7 * 153}
     got = int(count.item())
     expect = total  # every S key exists once in R (PK/FK and Zipf over 1..|R|)
     ok = got == expect
@@ -263,6 +278,7 @@ def main():
             "pipeline_frac": round(pipeline_gbs / HBM_PEAK_GBS, 4),
             "kernels_ms_per_step": {k: round(v[0] / a.steps, 4) for k, v in kern.items()},
             "device": lib.lib.smj_device_name().decode(),
+            "exchange": xchg,
         },
     }
     print(json.dumps(out))
