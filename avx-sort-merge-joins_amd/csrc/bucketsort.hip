@@ -1494,8 +1494,8 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
     const uint32_t ngroups = nb * nb2;
     const uint32_t ovf_cap = ngroups;
     OvfEntry* ovf = (OvfEntry*)ws->scratch("bs_ovf", (size_t)ovf_cap * sizeof(OvfEntry));
-    uint32_t* novf = (uint32_t*)ws->scratch("bs_novf", 4);
-    SMJ_CHECK(hipMemsetAsync(novf, 0, 4, st));
+    uint32_t* novf = a.status ? a.status + 2 : (uint32_t*)ws->scratch("bs_novf", 4);
+    if (!a.status) SMJ_CHECK(hipMemsetAsync(novf, 0, 4, st));
     TilePassArgs T;
     GroupArgs G;
     for (int r = 0; r < 2; r++) {
@@ -1545,17 +1545,21 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
     if (a.ev_ovf) SMJ_CHECK(hipEventRecord(a.ev_ovf, st));
 
     // ---- the one synchronisation: partition overflow flag + skew queue
-    uint32_t* h = (uint32_t*)ws->host_pinned("bs_h_flagovf", 12);
+    uint32_t* h = (uint32_t*)ws->host_pinned("bs_h_flagovf", 16);
     h[0] = h[1] = h[2] = 0;
-    SMJ_CHECK(hipMemcpyAsync(h, a.part_flag, 4, hipMemcpyDeviceToHost, st));
-    SMJ_CHECK(hipMemcpyAsync(h + 1, novf, 4, hipMemcpyDeviceToHost, st));
-    if (a.pack_bad)
-        SMJ_CHECK(hipMemcpyAsync(h + 2, a.pack_bad, 4, hipMemcpyDeviceToHost, st));
+    if (a.status) {
+        SMJ_CHECK(hipMemcpyAsync(h, a.status, 12, hipMemcpyDeviceToHost, st));
+    } else {
+        SMJ_CHECK(hipMemcpyAsync(h, a.part_flag, 4, hipMemcpyDeviceToHost, st));
+        SMJ_CHECK(hipMemcpyAsync(h + 2, novf, 4, hipMemcpyDeviceToHost, st));
+        if (a.pack_bad)
+            SMJ_CHECK(hipMemcpyAsync(h + 1, a.pack_bad, 4, hipMemcpyDeviceToHost, st));
+    }
     SMJ_CHECK(hipStreamSynchronize(st));
     // the caller repeats with exact partitions (region overflow) or on tuples
     // (not packable); the tile and group passes exited at once on the latter
-    if (h[0] || h[2]) return false;
-    const uint32_t no = h[1];
+    if (h[0] || h[1]) return false;
+    const uint32_t no = h[2];
     if (no == 0) return true;
     if (no > ovf_cap) {
         fprintf(stderr, "[ERROR] smj: overflow table too small\n");

@@ -18,6 +18,17 @@
 
 __global__ void k_setplan(smj::RangePlan* p, smj::RangePlan v) { *p = v; }
 
+// start of a join attempt: the plan (when known on the host), the count and
+// the 4-word status block (BucketSortArgs::status) in one launch
+__global__ void k_join_begin(smj::RangePlan* p, smj::RangePlan v, int set_plan,
+                             unsigned long long* count, unsigned int* status) {
+    if (threadIdx.x == 0) {
+        if (set_plan) *p = v;
+        *count = 0;
+    }
+    if (threadIdx.x < 4) status[threadIdx.x] = 0;
+}
+
 namespace smj {
 void gen_pk_nopayload(Tup* out, uint64_t n, uint64_t first, uint64_t total,
                       uint64_t seed, hipStream_t st);
@@ -223,9 +234,7 @@ static void device_join(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
     // with a key-range hint the plan is known here (same make_plan as k_plan)
     RangePlan hplan = make_plan(hint_min, hint_max, D1, D2, D2cap, kGroupD3Max);
     const bool plan_on_host = hint_min <= hint_max;
-    if (plan_on_host)
-        hipLaunchKernelGGL(k_setplan, dim3(1), dim3(1), 0, st, plan, hplan);
-    else
+    if (!plan_on_host)
         plan_from_sample(ws, rels, ns, 2, D1, D2, D2cap, hint_min, hint_max, plan, st);
     const uint32_t nb = 1u << D1;
     const bool sampled = use_sampled() && D1 <= 10;  // LDS carries up to 1024
@@ -242,7 +251,8 @@ static void device_join(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
     uint64_t* stS = (uint64_t*)ws->scratch("join_stS", nb * 8);
     int64_t* hR = (int64_t*)ws->scratch("join_hR", nb * 8);
     int64_t* hS = (int64_t*)ws->scratch("join_hS", nb * 8);
-    unsigned int* flag = (unsigned int*)ws->scratch("part_flag", 8);  // [1]: not packable
+    // [0] region overflow, [1] not packable, [2] skew queue length
+    unsigned int* status = (unsigned int*)ws->scratch("join_status", 16);
     uint64_t* sgsR = (uint64_t*)ws->scratch("join_sgsR", (size_t)nb * kShards * 8);
     int64_t* sgcR = (int64_t*)ws->scratch("join_sgcR", (size_t)nb * kShards * 8);
     uint64_t* sgsS = (uint64_t*)ws->scratch("join_sgsS", (size_t)nb * kShards * 8);
@@ -253,13 +263,13 @@ static void device_join(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
     // discarded: the count restarts from 0)
     for (int mode = can_pack ? 0 : (sampled ? 1 : 2); mode <= 2; mode++) {
         const bool packed = mode == 0;
-        SMJ_CHECK(hipMemsetAsync(count_dev, 0, sizeof(unsigned long long), st));
+        hipLaunchKernelGGL(k_join_begin, dim3(1), dim3(64), 0, st, plan, hplan,
+                           plan_on_host ? 1 : 0, count_dev, status);
         if (mode < 2) {
-            SMJ_CHECK(hipMemsetAsync(flag, 0, 8, st));
-            sampled_partition(ws, R, nR, partR, plan, D1, stR, hR, sgsR, sgcR, flag, st,
-                              packed ? &hplan : nullptr, flag + 1);
-            sampled_partition(ws, S, nS, partS, plan, D1, stS, hS, sgsS, sgcS, flag, st,
-                              packed ? &hplan : nullptr, flag + 1);
+            sampled_partition(ws, R, nR, partR, plan, D1, stR, hR, sgsR, sgcR, status, st,
+                              packed ? &hplan : nullptr, status + 1);
+            sampled_partition(ws, S, nS, partS, plan, D1, stS, hS, sgsS, sgcS, status, st,
+                              packed ? &hplan : nullptr, status + 1);
         } else {
             plan_partition(ws, R, nR, partR, plan, D1, stR, hR, st);
             plan_partition(ws, S, nS, partS, plan, D1, stS, hS, st);
@@ -287,9 +297,10 @@ static void device_join(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
         a.ev_ovf = ws->ev[3];
         a.host_plan = plan_on_host ? &hplan : nullptr;
         a.packed = packed;
-        a.pack_bad = packed ? flag + 1 : nullptr;
+        a.pack_bad = packed ? status + 1 : nullptr;
+        a.status = status;
         if (mode < 2) {
-            a.part_flag = flag;
+            a.part_flag = status;
             a.seg_start[0] = sgsR;
             a.seg_cnt[0] = sgcR;
             a.seg_start[1] = sgsS;

@@ -195,6 +195,9 @@ struct BucketSortArgs {
     // partition the bucket pass then runs without a mid-pipeline host sync
     const RangePlan* host_plan = nullptr;
     bool packed = false;            // part/tmp hold LayPacked words (host_plan's)
+    // optional 4-word block zeroed by the caller: [0] = part_flag, [1] =
+    // pack_bad, [2] = the skew queue length (read back in one copy)
+    unsigned int* status = nullptr;
     const unsigned int* pack_bad = nullptr;  // set by the partition: not packable
     hipEvent_t ev_tile = nullptr;   // optional phase markers
     hipEvent_t ev_bucket = nullptr;
