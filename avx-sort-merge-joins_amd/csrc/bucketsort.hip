@@ -82,7 +82,6 @@ constexpr int GS_NB3 = 1 << GS_D3MAX;
 constexpr int GS_TMAX = 128;    // tiles per bucket on the fast path (two per lane of one wave)
 constexpr int GS_WIN = GS_CAP / 64;
 constexpr int GS_RUNMAX = 32;   // longest equal-digit run fixed serially
-constexpr int GS_LONGMAX = 64;  // long runs checked per group
 static_assert(GS_CAP % 64 == 0 && GS_CAP % GS_THREADS == 0, "group capacity");
 
 #ifdef KEY_8B
@@ -298,8 +297,6 @@ struct GroupLDS {
     uint8_t wtile[2][GS_WIN];             // tile holding position 64 * w
     uint32_t wtot[GS_THREADS / 64];
     unsigned long long scan64[GS_THREADS / 64 + 1];
-    uint32_t lrun[GS_LONGMAX][2];         // long equal-digit runs [s, e)
-    uint32_t nlong;
     uint32_t n[2];
     uint32_t off[2];
 };
@@ -481,7 +478,6 @@ __device__ __forceinline__ void build_tables(const GroupArgs& A, LDS& L,
             L.wtile[r][lane] = (uint8_t)t;
         }
     }
-    if (otid() == 0) L.nlong = 0;
     __syncthreads();
 }
 
@@ -625,38 +621,35 @@ __device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS<typename
     after_place();
     __syncthreads();
     if (dup) {
-        // ---- equal-digit runs: short ones sorted here, long ones listed
-        uint32_t e = first;
+        // ---- equal-digit runs.  The group is ordered by digit, so an
+        // inversion can only sit inside such a run: one parallel pass finds
+        // out whether any needs sorting (never for equal tuples of a hot key).
+        // If so, short runs are insertion-sorted by their bin's thread; long
+        // ones must already be in order, otherwise the skew path.
+        bool ok = true;
+        for (uint32_t i = tid + 1; i < nr; i += GS_THREADS)
+            ok &= !Lay::less(L.B[i], L.B[i - 1]);
+        if (__syncthreads_or(!ok)) {
+            uint32_t e = first;
+            bool has_long = false;
 #pragma unroll
-        for (int q = 0; q < GS_BPT; q++) {
-            const uint32_t b0 = e;
-            e += c[q];
-            if (c[q] > 1) {
-                if (c[q] <= GS_RUNMAX) {
-                    insertion_sort<Lay>(L.B + b0, c[q]);
-                } else {
-                    const uint32_t li = atomicAdd(&L.nlong, 1u);
-                    if (li < GS_LONGMAX) {
-                        L.lrun[li][0] = b0;
-                        L.lrun[li][1] = e;
-                    }
+            for (int q = 0; q < GS_BPT; q++) {
+                const uint32_t b0 = e;
+                e += c[q];
+                if (c[q] > 1) {
+                    if (c[q] <= GS_RUNMAX)
+                        insertion_sort<Lay>(L.B + b0, c[q]);
+                    else
+                        has_long = true;
                 }
             }
+            if (__syncthreads_or(has_long)) {
+                ok = true;
+                for (uint32_t i = tid + 1; i < nr; i += GS_THREADS)
+                    ok &= !Lay::less(L.B[i], L.B[i - 1]);
+                if (__syncthreads_or(!ok)) return false;
+            }
         }
-        __syncthreads();
-        // long runs are accepted only when already in order (e.g. equal
-        // tuples of a hot key); otherwise the skew path
-        const uint32_t nl = L.nlong;
-        bool bad = nl > GS_LONGMAX;
-        for (uint32_t li = 0; li < nl && li < GS_LONGMAX && !bad; li++) {
-            const uint32_t s0 = L.lrun[li][0], e0 = L.lrun[li][1];
-            bool ok = true;
-            for (uint32_t i = s0 + 1 + tid; i < e0; i += GS_THREADS)
-                ok &= !Lay::less(L.B[i], L.B[i - 1]);
-            bad = __syncthreads_or(!ok);
-        }
-        if (bad) return false;
-        if (tid == 0) L.nlong = 0;
     }
     // ---- write the sorted group: one contiguous stream
     Tup* dst = A.out[r] + C.ost[r] + off;
@@ -848,6 +841,7 @@ __device__ __forceinline__ const typename Lay::W* skew_run(const GroupArgs& G, i
 
 struct SkewSmallLDS {
     uint32_t h[2][GS_NB3];
+    unsigned long long first[GS_NB3];  // pass 2: an element seen per digit
     uint32_t runoff[2][SK_TM + 1];
     uint64_t runsrc[2][SK_TM];
     unsigned long long scr[SK_THREADS / 64 + 1];
@@ -881,14 +875,16 @@ __device__ __forceinline__ void skew_for_each(const GroupArgs& G, const SkewSmal
                 if (j < n) v[k] = *skew_elem(L, r, static_cast<const W*>(G.tmp[r]), nt, j);
             }
 #pragma unroll
-            for (int k = 0; k < SK_ITEMS; k++)
-                if (c + k * SK_THREADS + threadIdx.x < n) f(v[k]);
+            for (int k = 0; k < SK_ITEMS; k++) f(v[k], c + k * SK_THREADS + threadIdx.x < n);
         }
     } else {
         for (uint32_t t = 0; t < nt; t++) {
             uint32_t len;
             const W* src = skew_run<Lay>(G, r, g, t0, t, len);
-            for (uint32_t i = threadIdx.x; i < len; i += SK_THREADS) f(src[i]);
+            for (uint32_t i0 = 0; i0 < len; i0 += SK_THREADS) {
+                const uint32_t i = i0 + threadIdx.x;
+                f(src[i < len ? i : len - 1], i < len);
+            }
         }
     }
 }
@@ -951,9 +947,9 @@ k_skew_small(SkewArgs K) {
     // ---- pass 1: d3 histograms
     bool clamped = false;
     for (int r = 0; r < G.nrel; r++)
-        skew_for_each<Lay>(G, L, r, e.d2, t0[r], nt[r], e.nr[r], [&](const W& x) {
-            clamped |= Lay::clamped(P, x);
-            atomicAdd(&L.h[r][plan_d3(P, Lay::rel(P, x, e.bucket), d12)], 1u);
+        skew_for_each<Lay>(G, L, r, e.d2, t0[r], nt[r], e.nr[r], [&](const W& x, bool ok) {
+            clamped |= ok && Lay::clamped(P, x);
+            if (ok) atomicAdd(&L.h[r][plan_d3(P, Lay::rel(P, x, e.bucket), d12)], 1u);
         });
     const bool exact = P.s3 == 0 && !__syncthreads_or(clamped);
     if (!exact) {
@@ -1000,15 +996,25 @@ k_skew_small(SkewArgs K) {
             ex += c[k];
         }
         __syncthreads();
-        // ---- pass 2: place
-        skew_for_each<Lay>(G, L, r, e.d2, t0[r], nt[r], e.nr[r], [&](const W& x) {
+        for (uint32_t d = tid; d < GS_NB3; d += SK_THREADS) L.first[d] = ~0ull;
+        __syncthreads();
+        // ---- pass 2: place; and note whether some key holds differing
+        // elements (the first element seen per digit is kept: ~0 is the
+        // empty mark, an element equal to it just counts as differing)
+        bool differ = false;
+        skew_for_each<Lay>(G, L, r, e.d2, t0[r], nt[r], e.nr[r], [&](const W& x, bool ok) {
             const uint32_t d = plan_d3(P, Lay::rel(P, x, e.bucket), d12);
-            dst[atomicAdd(&L.h[r][d], 1u)] = Lay::unpack(P, x, e.bucket);
+            if (ok) {
+                dst[atomicAdd(&L.h[r][d], 1u)] = Lay::unpack(P, x, e.bucket);
+                const unsigned long long id = Lay::same_key_id(x);
+                const unsigned long long old = atomicCAS(&L.first[d], ~0ull, id);
+                differ |= id == ~0ull || (old != ~0ull && old != id);
+            }
         });
         __threadfence_block();
-        __syncthreads();
-        // ---- pass 3: ordered by key; an inversion sits inside an equal-key run
-        inv |= skew_inversion(dst, 1, e.nr[r]);
+        // ---- pass 3 (only when a key holds differing elements): ordered by
+        // key, an inversion sits inside an equal-key run
+        if (__syncthreads_or(differ)) inv |= skew_inversion(dst, 1, e.nr[r]);
     }
     if (__syncthreads_or(inv) && tid == 0) K.gflag[qi] |= 2u;
 }
@@ -1043,10 +1049,9 @@ k_skew_hist(SkewArgs K) {
 #pragma unroll
             for (int k = 0; k < SK_ITEMS; k++) {
                 const uint32_t i = c + k * SK_THREADS + threadIdx.x;
-                if (i < len) {
-                    clamped |= Lay::clamped(P, v[k]);
-                    atomicAdd(&h[plan_d3(P, Lay::rel(P, v[k], e.bucket), d12)], 1u);
-                }
+                const bool ok = i < len;
+                clamped |= ok && Lay::clamped(P, v[k]);
+                if (ok) atomicAdd(&h[plan_d3(P, Lay::rel(P, v[k], e.bucket), d12)], 1u);
             }
         }
     }
@@ -1145,11 +1150,8 @@ k_skew_place(SkewArgs K) {
 #pragma unroll
             for (int k = 0; k < SK_ITEMS; k++) {
                 const uint32_t i = c + k * SK_THREADS + threadIdx.x;
-                dg[k] = 0xffffffffu;
-                if (i < len) {
-                    dg[k] = plan_d3(P, Lay::rel(P, v[k], e.bucket), d12);
-                    atomicAdd(&h[dg[k]], 1u);
-                }
+                dg[k] = i < len ? plan_d3(P, Lay::rel(P, v[k], e.bucket), d12) : 0u;
+                if (i < len) atomicAdd(&h[dg[k]], 1u);
             }
             __syncthreads();
             // reserve this chunk's share of every digit at the cursors
@@ -1159,9 +1161,10 @@ k_skew_place(SkewArgs K) {
             }
             __syncthreads();
 #pragma unroll
-            for (int k = 0; k < SK_ITEMS; k++)
-                if (dg[k] != 0xffffffffu)
-                    dst[atomicAdd(&h[dg[k]], 1u)] = Lay::unpack(P, v[k], e.bucket);
+            for (int k = 0; k < SK_ITEMS; k++) {
+                const bool ok = c + k * SK_THREADS + threadIdx.x < len;
+                if (ok) dst[atomicAdd(&h[dg[k]], 1u)] = Lay::unpack(P, v[k], e.bucket);
+            }
             __syncthreads();
         }
     }

@@ -218,6 +218,14 @@ struct LayTup {
     __device__ static __forceinline__ Tup unpack(const RangePlan&, const W& w, uint32_t) {
         return w;
     }
+    // equal keys: the elements are identical iff these values are
+    __device__ static __forceinline__ uint64_t same_key_id(const W& w) {
+#ifdef KEY_8B
+        return (uint64_t)w.payload;
+#else
+        return w;
+#endif
+    }
 };
 
 #ifdef KEY_8B
@@ -229,6 +237,7 @@ struct LayPacked {
     }
     __device__ static __forceinline__ bool clamped(const RangePlan&, const W&) { return false; }
     __device__ static __forceinline__ bool less(const W& a, const W& b) { return a < b; }
+    __device__ static __forceinline__ uint64_t same_key_id(const W& w) { return w; }
     __device__ static __forceinline__ Tup unpack(const RangePlan& P, const W& w, uint32_t b) {
         Tup t;
         t.payload = (int64_t)(w & (~0ull >> P.s1));
