@@ -152,64 +152,63 @@ static bool use_sampled() {
     return v != 0;
 }
 
-static void device_sort(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
-                        hipStream_t st) {
-    if (n == 0) return;
-    uint32_t D1, D2, D2cap;
-    choose_levels(n, 0, &D1, &D2, &D2cap);
-    RangePlan* plan = (RangePlan*)ws->scratch("plan", sizeof(RangePlan));
-    const Tup* rels[1] = {in};
-    uint64_t ns[1] = {n};
-    plan_from_sample(ws, rels, ns, 1, D1, D2, D2cap, 1, 0, plan, st);
-    const uint32_t nb = 1u << D1;
-    const bool sampled = use_sampled() && D1 <= 10;  // LDS carries up to 1024
-    Tup* part = (Tup*)ws->scratch(
-        "sort_part", (sampled ? sampled_capacity(n, D1) : n) * sizeof(Tup));
-    uint64_t* starts = (uint64_t*)ws->scratch("sort_starts", nb * 8);
-    int64_t* hist = (int64_t*)ws->scratch("sort_hist", nb * 8);
-    unsigned int* flag = (unsigned int*)ws->scratch("part_flag", 4);
-    uint64_t* sgs = (uint64_t*)ws->scratch("sort_sgs", (size_t)nb * kShards * 8);
-    int64_t* sgc = (int64_t*)ws->scratch("sort_sgc", (size_t)nb * kShards * 8);
-    if (sampled) {
-        SMJ_CHECK(hipMemsetAsync(flag, 0, 4, st));
-        sampled_partition(ws, in, n, part, plan, D1, starts, hist, sgs, sgc, flag, st);
-    } else {
-        plan_partition(ws, in, n, part, plan, D1, starts, hist, st);
+// exact key range [min, max] of the relations (one read pass); min > max
+// when they are empty
+__global__ void __launch_bounds__(256)
+k_keyrange(const Tup* __restrict__ r0, uint64_t n0, const Tup* __restrict__ r1, uint64_t n1,
+           unsigned long long* __restrict__ mm) {
+    uint64_t lo = ~0ull, hi = 0;  // key_u order
+    const uint64_t stride = (uint64_t)gridDim.x * 256 * 4;
+    for (int rel = 0; rel < 2; rel++) {
+        const Tup* p = rel ? r1 : r0;
+        const uint64_t n = rel ? n1 : n0;
+        if (!p) continue;
+        for (uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += stride) {
+            Tup t[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) t[k] = p[i + k < n ? i + k : n - 1];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint64_t u = key_u(tup_key(t[k]));
+                lo = u < lo ? u : lo;
+                hi = u > hi ? u : hi;
+            }
+        }
     }
-    BucketSortArgs a;
-    a.part[0] = part;
-    a.bstart[0] = starts;
-    a.bcount[0] = hist;
-    a.tmp[0] = part;
-    a.out[0] = out;
-    a.n[0] = n;
-    a.part[1] = nullptr;
-    a.bstart[1] = nullptr;
-    a.bcount[1] = nullptr;
-    a.tmp[1] = nullptr;
-    a.out[1] = nullptr;
-    a.n[1] = 0;
-    a.nrel = 1;
-    a.nbuckets = nb;
-    a.plan_dev = plan;
-    a.count_dev = nullptr;
-    a.part_flag = sampled ? flag : nullptr;
-    if (sampled) {
-        a.seg_start[0] = sgs;
-        a.seg_cnt[0] = sgc;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t a = __shfl_xor(lo, o, 64), c = __shfl_xor(hi, o, 64);
+        lo = a < lo ? a : lo;
+        hi = c > hi ? c : hi;
     }
-    if (!bucket_sort(ws, a, st)) {
-        // a sampled region overflowed (very skewed keys): exact partition
-        plan_partition(ws, in, n, part, plan, D1, starts, hist, st);
-        a.part_flag = nullptr;
-        a.seg_start[0] = nullptr;
-        a.seg_cnt[0] = nullptr;
-        bucket_sort(ws, a, st);
+    if (lane_id() == 0) {
+        atomicMin(&mm[0], (unsigned long long)lo);
+        atomicMax(&mm[1], (unsigned long long)hi);
     }
 }
 
-// 16-byte joins carry packed words through the intermediate passes when the
-// plan allows it (LayPacked); SMJ_PACK=0 keeps tuples
+static bool key_range(Workspace* ws, const Tup* const* rels, const uint64_t* ns, int nrel,
+                      int64_t* lo, int64_t* hi, hipStream_t st) {
+    unsigned long long* mm = (unsigned long long*)ws->scratch("keyrange", 16);
+    unsigned long long* h = (unsigned long long*)ws->host_pinned("keyrange_h", 16);
+    const unsigned long long init[2] = {~0ull, 0ull};
+    SMJ_CHECK(hipMemcpyAsync(mm, init, 16, hipMemcpyHostToDevice, st));
+    const uint64_t n = ns[0] + (nrel > 1 ? ns[1] : 0);
+    uint32_t g = (uint32_t)((n + 1023) / 1024);
+    if (g > 2048) g = 2048;
+    if (g == 0) g = 1;
+    hipLaunchKernelGGL(k_keyrange, dim3(g), dim3(256), 0, st, rels[0], ns[0],
+                       nrel > 1 ? rels[1] : (const Tup*)nullptr, nrel > 1 ? ns[1] : 0, mm);
+    SMJ_CHECK(hipMemcpyAsync(h, mm, 16, hipMemcpyDeviceToHost, st));
+    SMJ_CHECK(hipStreamSynchronize(st));
+    if (h[0] > h[1]) return false;
+    *lo = (int64_t)(h[0] ^ 0x8000000000000000ull);
+    *hi = (int64_t)(h[1] ^ 0x8000000000000000ull);
+    return true;
+}
+
+// 16-byte sorts and joins carry packed words through the intermediate passes
+// when the plan allows it (LayPacked); SMJ_PACK=0 keeps tuples
 static bool use_packing() {
     static int v = -1;
     if (v < 0) {
@@ -219,23 +218,29 @@ static bool use_packing() {
     return v != 0;
 }
 
-static void device_join(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
-                        uint64_t nS, Tup* sortedR, Tup* sortedS,
-                        uint32_t fanout_bits, int64_t hint_min,
-                        int64_t hint_max, unsigned long long* count_dev,
-                        hipStream_t st) {
+// Sort of one relation (nrel 1) or sort + merge-join count of two (nrel 2):
+// range plan -> sampled level-1 partition -> tile pass -> group pass.  The
+// plan comes from the caller's key-range hint, or else from one exact
+// min/max pass (so that it is known on the host: no mid-pipeline
+// synchronisation, and 16-byte tuples travel as packed words).
+static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t* ns,
+                          int nrel, Tup* const* outs, uint32_t fanout_bits,
+                          int64_t hint_min, int64_t hint_max,
+                          unsigned long long* count_dev, hipStream_t st) {
+    static const char* nm[2][6] = {{"bk_part0", "bk_st0", "bk_h0", "bk_sgs0", "bk_sgc0", ""},
+                                   {"bk_part1", "bk_st1", "bk_h1", "bk_sgs1", "bk_sgc1", ""}};
     ws->events();
     SMJ_CHECK(hipEventRecord(ws->ev[0], st));
+    const uint64_t nmax = nrel > 1 && ns[1] > ns[0] ? ns[1] : ns[0];
     uint32_t D1, D2, D2cap;
-    choose_levels(nR > nS ? nR : nS, fanout_bits, &D1, &D2, &D2cap);
+    choose_levels(nmax, fanout_bits, &D1, &D2, &D2cap);
     RangePlan* plan = (RangePlan*)ws->scratch("plan", sizeof(RangePlan));
-    const Tup* rels[2] = {R, S};
-    uint64_t ns[2] = {nR, nS};
-    // with a key-range hint the plan is known here (same make_plan as k_plan)
+    bool plan_on_host = hint_min <= hint_max;
+    if (!plan_on_host && !getenv("SMJ_SAMPLED_PLAN"))
+        plan_on_host = key_range(ws, rels, ns, nrel, &hint_min, &hint_max, st);
     RangePlan hplan = make_plan(hint_min, hint_max, D1, D2, D2cap, kGroupD3Max);
-    const bool plan_on_host = hint_min <= hint_max;
     if (!plan_on_host)
-        plan_from_sample(ws, rels, ns, 2, D1, D2, D2cap, hint_min, hint_max, plan, st);
+        plan_from_sample(ws, rels, ns, nrel, D1, D2, D2cap, hint_min, hint_max, plan, st);
     const uint32_t nb = 1u << D1;
     const bool sampled = use_sampled() && D1 <= 10;  // LDS carries up to 1024
 #ifdef KEY_8B
@@ -243,20 +248,23 @@ static void device_join(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
 #else
     const bool can_pack = false;
 #endif
-    Tup* partR = (Tup*)ws->scratch(
-        "join_partR", (sampled ? sampled_capacity(nR, D1) : (nR ? nR : 1)) * sizeof(Tup));
-    Tup* partS = (Tup*)ws->scratch(
-        "join_partS", (sampled ? sampled_capacity(nS, D1) : (nS ? nS : 1)) * sizeof(Tup));
-    uint64_t* stR = (uint64_t*)ws->scratch("join_stR", nb * 8);
-    uint64_t* stS = (uint64_t*)ws->scratch("join_stS", nb * 8);
-    int64_t* hR = (int64_t*)ws->scratch("join_hR", nb * 8);
-    int64_t* hS = (int64_t*)ws->scratch("join_hS", nb * 8);
+    Tup* part[2] = {nullptr, nullptr};
+    uint64_t* bst[2] = {nullptr, nullptr};
+    int64_t* bh[2] = {nullptr, nullptr};
+    uint64_t* sgs[2] = {nullptr, nullptr};
+    int64_t* sgc[2] = {nullptr, nullptr};
+    for (int r = 0; r < nrel; r++) {
+        const uint64_t cap = sampled ? sampled_capacity(ns[r], D1) : (ns[r] ? ns[r] : 1);
+        part[r] = (Tup*)ws->scratch(nm[r][0], cap * sizeof(Tup));
+        bst[r] = (uint64_t*)ws->scratch(nm[r][1], nb * 8);
+        bh[r] = (int64_t*)ws->scratch(nm[r][2], nb * 8);
+        sgs[r] = (uint64_t*)ws->scratch(nm[r][3], (size_t)nb * kShards * 8);
+        sgc[r] = (int64_t*)ws->scratch(nm[r][4], (size_t)nb * kShards * 8);
+    }
     // [0] region overflow, [1] not packable, [2] skew queue length
     unsigned int* status = (unsigned int*)ws->scratch("join_status", 16);
-    uint64_t* sgsR = (uint64_t*)ws->scratch("join_sgsR", (size_t)nb * kShards * 8);
-    int64_t* sgcR = (int64_t*)ws->scratch("join_sgcR", (size_t)nb * kShards * 8);
-    uint64_t* sgsS = (uint64_t*)ws->scratch("join_sgsS", (size_t)nb * kShards * 8);
-    int64_t* sgcS = (int64_t*)ws->scratch("join_sgcS", (size_t)nb * kShards * 8);
+    unsigned long long* cnt = count_dev
+        ? count_dev : (unsigned long long*)ws->scratch("sort_cnt", 8);
     // attempts: sampled + packed words, sampled tuples, exact tuples; a later
     // one runs only when the one before reported a region overflow or an
     // unpackable tuple (its tile and group passes then did nothing or are
@@ -264,34 +272,33 @@ static void device_join(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
     for (int mode = can_pack ? 0 : (sampled ? 1 : 2); mode <= 2; mode++) {
         const bool packed = mode == 0;
         hipLaunchKernelGGL(k_join_begin, dim3(1), dim3(64), 0, st, plan, hplan,
-                           plan_on_host ? 1 : 0, count_dev, status);
-        if (mode < 2) {
-            sampled_partition(ws, R, nR, partR, plan, D1, stR, hR, sgsR, sgcR, status, st,
-                              packed ? &hplan : nullptr, status + 1);
-            sampled_partition(ws, S, nS, partS, plan, D1, stS, hS, sgsS, sgcS, status, st,
-                              packed ? &hplan : nullptr, status + 1);
-        } else {
-            plan_partition(ws, R, nR, partR, plan, D1, stR, hR, st);
-            plan_partition(ws, S, nS, partS, plan, D1, stS, hS, st);
+                           plan_on_host ? 1 : 0, cnt, status);
+        for (int r = 0; r < nrel; r++) {
+            if (mode < 2)
+                sampled_partition(ws, rels[r], ns[r], part[r], plan, D1, bst[r], bh[r],
+                                  sgs[r], sgc[r], status, st, packed ? &hplan : nullptr,
+                                  status + 1);
+            else
+                plan_partition(ws, rels[r], ns[r], part[r], plan, D1, bst[r], bh[r], st);
         }
         SMJ_CHECK(hipEventRecord(ws->ev[1], st));
         BucketSortArgs a;
-        a.part[0] = partR;
-        a.part[1] = partS;
-        a.bstart[0] = stR;
-        a.bstart[1] = stS;
-        a.bcount[0] = hR;
-        a.bcount[1] = hS;
-        a.tmp[0] = partR;
-        a.tmp[1] = partS;
-        a.out[0] = sortedR;
-        a.out[1] = sortedS;
-        a.n[0] = nR;
-        a.n[1] = nS;
-        a.nrel = 2;
+        for (int r = 0; r < 2; r++) {
+            a.part[r] = part[r];
+            a.bstart[r] = bst[r];
+            a.bcount[r] = bh[r];
+            a.tmp[r] = part[r];
+            a.out[r] = r < nrel ? outs[r] : nullptr;
+            a.n[r] = r < nrel ? ns[r] : 0;
+            if (mode < 2) {
+                a.seg_start[r] = sgs[r];
+                a.seg_cnt[r] = sgc[r];
+            }
+        }
+        a.nrel = nrel;
         a.nbuckets = nb;
         a.plan_dev = plan;
-        a.count_dev = count_dev;
+        a.count_dev = nrel == 2 ? count_dev : nullptr;
         a.ev_tile = nullptr;
         a.ev_bucket = ws->ev[2];
         a.ev_ovf = ws->ev[3];
@@ -299,16 +306,30 @@ static void device_join(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
         a.packed = packed;
         a.pack_bad = packed ? status + 1 : nullptr;
         a.status = status;
-        if (mode < 2) {
-            a.part_flag = status;
-            a.seg_start[0] = sgsR;
-            a.seg_cnt[0] = sgcR;
-            a.seg_start[1] = sgsS;
-            a.seg_cnt[1] = sgcS;
-        }
+        if (mode < 2) a.part_flag = status;
         if (bucket_sort(ws, a, st)) break;
     }
     SMJ_CHECK(hipEventRecord(ws->ev[4], st));
+}
+
+static void device_sort(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
+                        hipStream_t st) {
+    if (n == 0) return;
+    const Tup* rels[1] = {in};
+    uint64_t ns[1] = {n};
+    Tup* outs[1] = {out};
+    device_bucket(ws, rels, ns, 1, outs, 0, 1, 0, nullptr, st);
+}
+
+static void device_join(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
+                        uint64_t nS, Tup* sortedR, Tup* sortedS,
+                        uint32_t fanout_bits, int64_t hint_min,
+                        int64_t hint_max, unsigned long long* count_dev,
+                        hipStream_t st) {
+    const Tup* rels[2] = {R, S};
+    uint64_t ns[2] = {nR, nS};
+    Tup* outs[2] = {sortedR, sortedS};
+    device_bucket(ws, rels, ns, 2, outs, fanout_bits, hint_min, hint_max, count_dev, st);
 }
 
 // ---------------------------------------------------------------------------

@@ -27,6 +27,8 @@ def main():
     p.add_argument("--shift", type=int, default=0)
     p.add_argument("--reps", type=int, default=5)
     p.add_argument("--dist", default="uniform")
+    p.add_argument("--nohint", action="store_true",
+                   help="join without the key-range hint (the reference API path)")
     a = p.parse_args()
     lib = smj.load(a.width)
     n = a.n
@@ -65,7 +67,8 @@ def main():
             lib.dev_gen_zipf(S, 0, n, 0.75, 54321)
         sR, sS = lib.empty(n), lib.empty(n)
         cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
-        f = lambda: lib.dev_join(R, S, sR, sS, cnt, a.bits, 1, n)
+        kmax = 0 if a.nohint else n
+        f = lambda: lib.dev_join(R, S, sR, sS, cnt, a.bits, 1, kmax)
         alg = 5 * 2 * n * a.width
     f()
     torch.cuda.synchronize()
