@@ -259,6 +259,198 @@ k_scatter(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_arg,
     }
 }
 
+// ---------------------------------------------------------------------------
+// Stable scatter with write combining (partition_relation[_optimized]): the
+// ranks of k_scatter (ballot matching, per-wave counters: input order kept
+// inside every digit), the tile's runs prepended with each partition's carry
+// (the tail of this workgroup's output that does not yet end on a 64-byte
+// boundary), and SEG consecutive lanes write one aligned 64-byte segment --
+// the reference's cache-line write-combining buffers
+// (src/partition/partition.c:38-46, 191-206) with whole-segment stores.  The
+// next tile is loaded while the current one is ranked and written.
+template <int THREADS, int ITEMS>
+struct SwcGeom {
+    static constexpr uint32_t SEG = 64 / sizeof(Tup);
+    static constexpr uint32_t TILE = THREADS * ITEMS;
+    static constexpr uint32_t WAVES = THREADS / 64;
+    static __host__ __device__ constexpr uint32_t max_segs(uint32_t nbins) {
+        return (TILE + nbins * (SEG - 1)) / SEG + 2 * nbins;
+    }
+    // stage Tup[TILE] | carry Tup[nbins * (SEG-1)] | run u64[nbins] |
+    // tstart, kc, segpre, emit u32[nbins] | wcnt u16[WAVES * nbins] |
+    // segown u16[max_segs] | scan scratch
+    static __host__ __device__ constexpr size_t lds_bytes(uint32_t nbins) {
+        return (size_t)TILE * sizeof(Tup) + (size_t)nbins * (SEG - 1) * sizeof(Tup) +
+               (size_t)nbins * (8 + 4 * 4) + (size_t)WAVES * nbins * 2 +
+               ((size_t)max_segs(nbins) * 2 + 15) / 16 * 16 + 64;
+    }
+};
+
+template <int THREADS, int ITEMS, class Digit>
+__global__ void __launch_bounds__(THREADS)
+k_scatter_swc(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_arg,
+              uint32_t nbins, uint32_t dbits, const uint32_t* __restrict__ counts,
+              uint32_t nwg, const uint64_t* __restrict__ starts, Tup* __restrict__ out) {
+    typedef SwcGeom<THREADS, ITEMS> Geo;
+    constexpr uint32_t SEG = Geo::SEG;
+    constexpr uint32_t CW = SEG - 1;  // carry slots per partition
+    constexpr int TILE = (int)Geo::TILE;
+    constexpr int WAVES = (int)Geo::WAVES;
+    const auto dig = dig_arg.load();
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    Tup* stage = reinterpret_cast<Tup*>(lds_raw);
+    Tup* carry = stage + TILE;
+    uint64_t* run = reinterpret_cast<uint64_t*>(carry + (size_t)nbins * CW);
+    uint32_t* tstart = reinterpret_cast<uint32_t*>(run + nbins);
+    uint32_t* kc = tstart + nbins;
+    uint32_t* segpre = kc + nbins;
+    uint32_t* emit = segpre + nbins;
+    uint16_t* wcnt = reinterpret_cast<uint16_t*>(emit + nbins);
+    uint16_t* segown = wcnt + (size_t)WAVES * nbins;
+    uint32_t* scr = reinterpret_cast<uint32_t*>(
+        reinterpret_cast<unsigned char*>(segown) + ((size_t)Geo::max_segs(nbins) * 2 + 15) / 16 * 16);
+
+    const int lane = lane_id();
+    const int wid = threadIdx.x >> 6;
+    const uint64_t lt = lanemask_lt();
+    for (uint32_t d = threadIdx.x; d < nbins; d += THREADS) {
+        run[d] = starts[d] + counts[(uint64_t)d * nwg + blockIdx.x];
+        kc[d] = 0;
+#pragma unroll
+        for (int w = 0; w < WAVES; w++) wcnt[w * nbins + d] = 0;
+    }
+    const uint64_t beg = (uint64_t)blockIdx.x * chunk;
+    uint64_t end = beg + chunk;
+    if (end > n) end = n;
+    const uint32_t dper = (nbins + THREADS - 1) / THREADS;
+    const uint32_t d0 = threadIdx.x * dper;
+    // wave `wid` owns items [wid*64*ITEMS, (wid+1)*64*ITEMS) of a tile
+    const uint32_t wbase = wid * 64 * ITEMS;
+    Tup v[ITEMS], nv[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; j++) {
+        const uint64_t i = beg + wbase + j * 64 + lane;
+        if (i < end) v[j] = in[i];
+    }
+    __syncthreads();
+    for (uint64_t base = beg; base < end; base += TILE) {
+        const uint32_t tcount =
+            (uint32_t)((end - base) < (uint64_t)TILE ? (end - base) : TILE);
+        __builtin_amdgcn_s_waitcnt(0x0f70);  // this tile's loads have landed
+        uint32_t dg[ITEMS], rk[ITEMS];
+        uint16_t* mycnt = wcnt + wid * nbins;
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint32_t li = wbase + j * 64 + lane;
+            dg[j] = li < tcount ? dig(v[j]) : 0xffffffffu;
+            const bool valid = dg[j] != 0xffffffffu;
+            uint64_t peers = __ballot(valid);
+            const uint32_t d = valid ? dg[j] : 0;
+            for (uint32_t b = 0; b < dbits; b++) {
+                const bool bit = (d >> b) & 1u;
+                const uint64_t bal = __ballot(bit);
+                peers &= bit ? bal : ~bal;
+            }
+            uint32_t before = 0;
+            if (valid) before = mycnt[d];
+            const uint32_t r = (uint32_t)__popcll(peers & lt);
+            if (valid && r == 0) mycnt[d] = (uint16_t)(before + __popcll(peers));
+            rk[j] = before + r;
+        }
+        __syncthreads();
+        // ---- per digit: tile count, stage start, per-wave offsets, and the
+        // emission: everything up to the last 64-byte boundary (E of the
+        // T = carry + tile elements) as whole aligned segments
+        uint32_t c[4], E[4], ns[4];  // dper <= 4 (nbins <= 4 * THREADS)
+        uint32_t loc = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            const uint32_t d = d0 + k;
+            c[k] = E[k] = ns[k] = 0;
+            if (k < dper && d < nbins) {
+#pragma unroll
+                for (int w = 0; w < WAVES; w++) c[k] += wcnt[w * nbins + d];
+                const uint64_t p = run[d];
+                const uint32_t T = kc[d] + c[k];
+                const uint32_t m = (uint32_t)((p + T) % SEG);
+                E[k] = m <= T ? T - m : 0u;
+                ns[k] = E[k] ? (uint32_t)((p + E[k] - (p - p % SEG)) / SEG) : 0u;
+                loc += c[k] | (ns[k] << 16);
+            }
+        }
+        uint32_t tot;
+        uint32_t ex = block_exclusive_scan(loc, scr, &tot);
+        const uint32_t nsegT = tot >> 16;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            const uint32_t d = d0 + k;
+            if (k < dper && d < nbins) {
+                tstart[d] = ex & 0xffffu;
+                segpre[d] = ex >> 16;
+                emit[d] = E[k];
+                uint32_t o = ex & 0xffffu;
+#pragma unroll
+                for (int w = 0; w < WAVES; w++) {
+                    const uint32_t cw = wcnt[w * nbins + d];
+                    wcnt[w * nbins + d] = (uint16_t)o;
+                    o += cw;
+                }
+                for (uint32_t q = 0; q < ns[k]; q++) segown[(ex >> 16) + q] = (uint16_t)d;
+                ex += c[k] | (ns[k] << 16);
+            }
+        }
+        // prefetch the next tile
+        const uint64_t nb = base + TILE;
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint64_t i = nb + wbase + j * 64 + lane;
+            if (i < end) nv[j] = in[i];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++)
+            if (dg[j] != 0xffffffffu) stage[mycnt[dg[j]] + rk[j]] = v[j];
+        __syncthreads();
+        // ---- whole segments: SEG consecutive lanes per aligned 64-byte block
+        for (uint32_t q = threadIdx.x; q < nsegT * SEG; q += THREADS) {
+            const uint32_t sg = q / SEG;
+            const uint32_t d = segown[sg];
+            const uint64_t p = run[d];
+            const uint64_t addr = p - p % SEG + (uint64_t)(sg - segpre[d]) * SEG + q % SEG;
+            if (addr >= p && addr < p + emit[d]) {
+                const uint32_t e = (uint32_t)(addr - p);
+                const uint32_t k = kc[d];
+                out[addr] = e < k ? carry[d * CW + e] : stage[tstart[d] + e - k];
+            }
+        }
+        __syncthreads();
+        // ---- leftovers (< SEG) become the carry; counters for the next tile
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            const uint32_t d = d0 + k;
+            if (k < dper && d < nbins) {
+                const uint32_t kk = kc[d];
+                const uint32_t T = kk + c[k];
+                for (uint32_t e = E[k]; e < T; e++)
+                    carry[d * CW + (e - E[k])] =
+                        e < kk ? carry[d * CW + e] : stage[tstart[d] + e - kk];
+                run[d] += E[k];
+                kc[d] = T - E[k];
+#pragma unroll
+                for (int w = 0; w < WAVES; w++) wcnt[w * nbins + d] = 0;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) v[j] = nv[j];
+        __syncthreads();
+    }
+    // ---- the partial last segments of this workgroup's regions
+    for (uint32_t q = threadIdx.x; q < nbins * CW; q += THREADS) {
+        const uint32_t d = q / CW, j = q % CW;
+        if (j < kc[d]) out[run[d] + j] = carry[q];
+    }
+}
+
 // Unstable scatter for the join's level-1 partition (the join re-sorts every
 // bucket completely, so the order inside a partition is free).  Ranks come
 // from LDS atomics on tile-level digit counters -- two ds_add per tuple instead
@@ -859,6 +1051,16 @@ static int scatter_mode() {
     return m;
 }
 
+// write-combining stable scatter (k_scatter_swc); SMJ_STABLE_WC=0 keeps k_scatter
+static bool stable_wc() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("SMJ_STABLE_WC");
+        v = e ? atoi(e) : 1;
+    }
+    return v != 0;
+}
+
 static int pt_variant() {
     static int v = -1;
     if (v < 0) {
@@ -922,6 +1124,27 @@ static void stable_partition_t(Workspace* ws, const Tup* in, uint64_t n,
         SMJ_CHECK(hipGetLastError());
         return;
     } else {
+        // write-combining stable scatter (its own 512x8 geometry)
+        typedef SwcGeom<512, 8> SG;
+        if (stable_wc() && nbins <= 4 * 512 && SG::lds_bytes(nbins) <= 160 * 1024 &&
+            scatter_mode() == 0) {
+            const uint64_t tiles = (n + SG::TILE - 1) / SG::TILE;
+            uint32_t wg2 = nwg;  // the histogram's chunking: counts[d][wg] match
+            (void)tiles;
+            static bool attr_w = false;
+            if (!attr_w) {
+                SMJ_CHECK(hipFuncSetAttribute(
+                    (const void*)k_scatter_swc<512, 8, Digit>,
+                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+                attr_w = true;
+            }
+            TraceScope ts(ws, "k_scatter", st);
+            hipLaunchKernelGGL((k_scatter_swc<512, 8, Digit>), dim3(wg2), dim3(512),
+                               SG::lds_bytes(nbins), st, in, n, chunk, dig, nbins, dbits,
+                               counts, nwg, starts_dev, out);
+            SMJ_CHECK(hipGetLastError());
+            return;
+        }
         const size_t lds = scatter_lds<THREADS, ITEMS>(nbins);
         static bool attr_set = false;
         if (!attr_set) {
