@@ -1092,6 +1092,13 @@ void smj_dev_merge_join_count(const tuple_t* r, uint64_t nr, const tuple_t* s,
                      (hipStream_t)stream);
 }
 
+uint64_t smj_dev_materialize(smj_workspace* ws, const tuple_t* sortedR, uint64_t nR,
+                             const tuple_t* sortedS, uint64_t nS, tuple_t* out,
+                             uint64_t out_cap, smj_stream_t stream) {
+    return materialize((Workspace*)ws, (const Tup*)sortedR, nR, (const Tup*)sortedS,
+                       nS, (Tup*)out, out_cap, (hipStream_t)stream);
+}
+
 void smj_dev_join(smj_workspace* ws, const tuple_t* R, uint64_t nR,
                   const tuple_t* S, uint64_t nS, tuple_t* sortedR,
                   tuple_t* sortedS, uint32_t fanout_bits, int64_t key_min,

@@ -1,0 +1,293 @@
+// materialize.hip -- materialised merge-join output.
+//
+// Reference: src/joins/joincommon.c:239-312 (merge_join built with
+// JOIN_MATERIALIZE): for every match the reference appends <S.key, S.payload>
+// to a chained tuple buffer, R-major -- for each R tuple of a key run, the
+// whole S run of that key (joincommon.c:267-287).  Over sorted inputs the
+// output of key k is therefore the S run of k repeated |R_k| times, keys in
+// ascending order.  (The chained buffer's header, tuple_buffer.h, is absent
+// from the reference tree; the output here is one flat tuple array.)
+//
+// GPU form, three launches over sorted R and S:
+//   k_mat_count  one workgroup per S tile: |R_k| of every S element (a
+//                galloping search through the R window of the tile's key
+//                range), summed per tile;
+//   k_mat_scan   one workgroup: tile output offsets, and the work items (each
+//                tile's output cut into pieces of kMatPiece outputs);
+//   k_mat_write  one workgroup per work item: recomputes its tile's counts,
+//                scans them in LDS and writes its piece output-major, so the
+//                stores are coalesced and a hot key spreads over many
+//                workgroups instead of serialising one thread.
+#include "smj_common.hpp"
+#include "smj_internal.hpp"
+
+namespace smj {
+
+constexpr int MT_THREADS = 256;
+constexpr int MT_IPT = 8;
+constexpr uint32_t MT_TILE = MT_THREADS * MT_IPT;  // S elements per tile
+constexpr uint64_t kMatPiece = 8192;                // outputs per work item
+
+// first index of [lo, hi) whose key is >= k (UPPER: > k)
+template <bool UPPER>
+__device__ __forceinline__ uint64_t key_search(const Tup* a, uint64_t lo,
+                                               uint64_t hi, int64_t k) {
+    while (lo < hi) {
+        const uint64_t m = (lo + hi) >> 1;
+        const int64_t x = tup_key(a[m]);
+        if (UPPER ? x <= k : x < k) lo = m + 1; else hi = m;
+    }
+    return lo;
+}
+
+// the same answer, galloping forward from lo (answers near lo are cheap:
+// consecutive keys of a tile sit close together in R)
+template <bool UPPER>
+__device__ __forceinline__ uint64_t key_gallop(const Tup* a, uint64_t lo,
+                                               uint64_t hi, int64_t k) {
+    uint64_t step = 1;
+    while (true) {
+        const uint64_t e = lo + step - 1;
+        if (e >= hi) return key_search<UPPER>(a, lo, hi, k);
+        const int64_t x = tup_key(a[e]);
+        if (!(UPPER ? x <= k : x < k)) return key_search<UPPER>(a, lo, e, k);
+        lo = e + 1;
+        step <<= 1;
+    }
+}
+
+struct MatLDS {
+    int64_t key[MT_TILE];
+    uint64_t rc[MT_TILE];  // |R_k| of the element; inclusive prefix (write)
+    int64_t s0[MT_TILE];   // S index where the element's key run starts
+    int64_t se[MT_TILE];   // S index where it ends
+    uint64_t ends[4];      // R window [lo, hi), first run start, last run end
+    uint64_t wsum[MT_THREADS / 64 + 1];
+};
+
+// key runs and R match counts of S[tb, tb + len)
+__device__ void mat_tile(const Tup* __restrict__ R, uint64_t nR,
+                         const Tup* __restrict__ S, uint64_t nS, uint64_t tb,
+                         uint32_t len, MatLDS& L) {
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t i = tid; i < len; i += MT_THREADS) L.key[i] = tup_key(S[tb + i]);
+    __syncthreads();
+    const int64_t kf = L.key[0], kl = L.key[len - 1];
+    if (tid == 0) L.ends[0] = key_search<false>(R, 0, nR, kf);
+    if (tid == 64) L.ends[1] = key_search<true>(R, 0, nR, kl);
+    if (tid == 128)
+        L.ends[2] = (tb > 0 && tup_key(S[tb - 1]) == kf) ? key_search<false>(S, 0, tb, kf) : tb;
+    if (tid == 192)
+        L.ends[3] = (tb + len < nS && tup_key(S[tb + len]) == kl)
+                        ? key_search<true>(S, tb + len, nS, kl)
+                        : tb + len;
+    __syncthreads();
+    const uint32_t i0 = tid * MT_IPT;
+    if (i0 >= len) return;
+    const uint32_t i1 = min(i0 + (uint32_t)MT_IPT, len);
+    const uint64_t Rhi = max(L.ends[0], L.ends[1]);
+    // run start of the thread's first element, run end of its last (LDS)
+    uint32_t a = 0, b = i0;
+    {
+        const int64_t k = L.key[i0];
+        while (a < b) {
+            const uint32_t m = (a + b) >> 1;
+            if (L.key[m] < k) a = m + 1; else b = m;
+        }
+    }
+    uint32_t c = i1, d = len;
+    {
+        const int64_t k = L.key[i1 - 1];
+        while (c < d) {
+            const uint32_t m = (c + d) >> 1;
+            if (L.key[m] <= k) c = m + 1; else d = m;
+        }
+    }
+    const int64_t last_end = c == len ? (int64_t)L.ends[3] : (int64_t)(tb + c);
+    int64_t s0 = a == 0 ? (int64_t)L.ends[2] : (int64_t)(tb + a);
+    uint64_t rlo, rhi = L.ends[0];
+    uint32_t i = i0;
+    while (i < i1) {
+        const int64_t k = L.key[i];
+        uint32_t j = i + 1;
+        while (j < i1 && L.key[j] == k) j++;
+        if (i != i0) s0 = (int64_t)(tb + i);
+        rlo = key_gallop<false>(R, rhi, Rhi, k);
+        rhi = key_gallop<true>(R, rlo, Rhi, k);
+        const int64_t e = j < i1 ? (int64_t)(tb + j) : last_end;
+        for (uint32_t u = i; u < j; u++) {
+            L.rc[u] = rhi - rlo;
+            L.s0[u] = s0;
+            L.se[u] = e;
+        }
+        i = j;
+    }
+}
+
+// block-wide exclusive scan of one uint64 per thread
+__device__ __forceinline__ uint64_t block_scan64(uint64_t v, uint64_t* wsum,
+                                                 uint64_t* total) {
+    const int lane = lane_id(), wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    uint64_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up((unsigned long long)x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t run = 0;
+        for (int w = 0; w < nw; w++) {
+            const uint64_t t = wsum[w];
+            wsum[w] = run;
+            run += t;
+        }
+        wsum[nw] = run;
+    }
+    __syncthreads();
+    const uint64_t res = wsum[wid] + x - v;
+    if (total) *total = wsum[nw];
+    __syncthreads();
+    return res;
+}
+
+__global__ void __launch_bounds__(MT_THREADS)
+k_mat_count(const Tup* __restrict__ R, uint64_t nR, const Tup* __restrict__ S,
+            uint64_t nS, uint64_t* __restrict__ tile_out) {
+    __shared__ MatLDS L;
+    const uint64_t tb = (uint64_t)blockIdx.x * MT_TILE;
+    const uint32_t len = (uint32_t)min((uint64_t)MT_TILE, nS - tb);
+    mat_tile(R, nR, S, nS, tb, len, L);
+    uint64_t s = 0;
+    const uint32_t i0 = threadIdx.x * MT_IPT;
+    for (uint32_t u = i0; u < min(i0 + (uint32_t)MT_IPT, len); u++) s += L.rc[u];
+    s = wave_sum(s);
+    if (lane_id() == 0) L.wsum[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t t = 0;
+        for (int w = 0; w < MT_THREADS / 64; w++) t += L.wsum[w];
+        tile_out[blockIdx.x] = t;
+    }
+}
+
+// tile output bases and work-item bases (exclusive), totals into tot[0..1]
+__global__ void __launch_bounds__(1024)
+k_mat_scan(const uint64_t* __restrict__ cnt, uint64_t ntiles,
+           uint64_t* __restrict__ base, uint64_t* __restrict__ ibase,
+           uint64_t* __restrict__ tot) {
+    __shared__ uint64_t ws[1024 / 64 + 1];
+    const uint64_t per = (ntiles + 1023) / 1024;
+    const uint64_t t0 = min(ntiles, (uint64_t)threadIdx.x * per);
+    const uint64_t t1 = min(ntiles, t0 + per);
+    uint64_t so = 0, si = 0;
+    for (uint64_t t = t0; t < t1; t++) {
+        so += cnt[t];
+        si += (cnt[t] + kMatPiece - 1) / kMatPiece;
+    }
+    uint64_t to, ti;
+    uint64_t eo = block_scan64(so, ws, &to);
+    uint64_t ei = block_scan64(si, ws, &ti);
+    for (uint64_t t = t0; t < t1; t++) {
+        base[t] = eo;
+        ibase[t] = ei;
+        eo += cnt[t];
+        ei += (cnt[t] + kMatPiece - 1) / kMatPiece;
+    }
+    if (threadIdx.x == 0) {
+        tot[0] = to;
+        tot[1] = ti;
+    }
+}
+
+__global__ void __launch_bounds__(MT_THREADS)
+k_mat_write(const Tup* __restrict__ R, uint64_t nR, const Tup* __restrict__ S,
+            uint64_t nS, const uint64_t* __restrict__ cnt,
+            const uint64_t* __restrict__ base, const uint64_t* __restrict__ ibase,
+            uint64_t ntiles, Tup* __restrict__ out, uint64_t out_cap) {
+    __shared__ MatLDS L;
+    __shared__ uint64_t sh_t;
+    const uint64_t w = blockIdx.x;
+    if (threadIdx.x == 0) {
+        // the last tile whose first item is <= w owns item w
+        uint64_t lo = 0, hi = ntiles;
+        while (lo < hi) {
+            const uint64_t m = (lo + hi) >> 1;
+            if (ibase[m] <= w) lo = m + 1; else hi = m;
+        }
+        sh_t = lo - 1;
+    }
+    __syncthreads();
+    const uint64_t t = sh_t;
+    const uint64_t q0 = (w - ibase[t]) * kMatPiece;
+    const uint64_t q1 = min(q0 + kMatPiece, cnt[t]);
+    const uint64_t ob = base[t];
+    if (ob + q0 >= out_cap) return;  // uniform over the workgroup
+    const uint64_t tb = t * MT_TILE;
+    const uint32_t len = (uint32_t)min((uint64_t)MT_TILE, nS - tb);
+    mat_tile(R, nR, S, nS, tb, len, L);
+    // inclusive prefix of the counts over the tile
+    const uint32_t i0 = threadIdx.x * MT_IPT;
+    const uint32_t i1 = min(i0 + (uint32_t)MT_IPT, len);
+    uint64_t s = 0;
+    for (uint32_t u = i0; u < i1; u++) s += L.rc[u];
+    uint64_t run = block_scan64(s, L.wsum, nullptr);
+    for (uint32_t u = i0; u < i1; u++) {
+        run += L.rc[u];
+        L.rc[u] = run;
+    }
+    __syncthreads();
+    for (uint64_t q = q0 + threadIdx.x; q < q1; q += MT_THREADS) {
+        if (ob + q >= out_cap) break;
+        // element j: the first inclusive prefix above q
+        uint32_t lo = 0, hi = len - 1;
+        while (lo < hi) {
+            const uint32_t m = (lo + hi) >> 1;
+            if (L.rc[m] <= q) lo = m + 1; else hi = m;
+        }
+        const uint32_t j = lo;
+        const uint64_t excl = j ? L.rc[j - 1] : 0;
+        const uint64_t rcj = L.rc[j] - excl;
+        const int64_t s0 = L.s0[j];
+        const uint64_t sc = (uint64_t)(L.se[j] - s0);
+        // the run's output starts (tb + j - s0) * rcj outputs before element
+        // j's first (mod 2^64 when the run began in an earlier tile)
+        const uint64_t off = q - (excl - (uint64_t)((int64_t)(tb + j) - s0) * rcj);
+        const uint64_t src = (uint64_t)s0 + (sc == 1 ? 0 : off % sc);
+        st_stream(out + ob + q, S[src]);
+    }
+}
+
+uint64_t materialize(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
+                     uint64_t nS, Tup* out, uint64_t out_cap, hipStream_t st) {
+    if (nR == 0 || nS == 0) return 0;
+    const uint64_t ntiles = (nS + MT_TILE - 1) / MT_TILE;
+    uint64_t* tab = (uint64_t*)ws->scratch("mat_tab", (3 * ntiles + 2) * 8);
+    uint64_t* cnt = tab;
+    uint64_t* base = tab + ntiles;
+    uint64_t* ibase = tab + 2 * ntiles;
+    uint64_t* tot = tab + 3 * ntiles;
+    {
+        TraceScope ts(ws, "k_mat_count", st);
+        hipLaunchKernelGGL(k_mat_count, dim3((uint32_t)ntiles), dim3(MT_THREADS), 0,
+                           st, R, nR, S, nS, cnt);
+        SMJ_CHECK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_mat_scan, dim3(1), dim3(1024), 0, st, cnt, ntiles, base,
+                       ibase, tot);
+    SMJ_CHECK(hipGetLastError());
+    uint64_t* h = (uint64_t*)ws->host_pinned("mat_tot_h", 16);
+    SMJ_CHECK(hipMemcpyAsync(h, tot, 16, hipMemcpyDeviceToHost, st));
+    SMJ_CHECK(hipStreamSynchronize(st));
+    const uint64_t total = h[0], items = h[1];
+    if (items && out_cap) {
+        TraceScope ts(ws, "k_mat_write", st);
+        hipLaunchKernelGGL(k_mat_write, dim3((uint32_t)items), dim3(MT_THREADS), 0,
+                           st, R, nR, S, nS, cnt, base, ibase, ntiles, out, out_cap);
+        SMJ_CHECK(hipGetLastError());
+    }
+    return total;
+}
+
+}  // namespace smj

@@ -233,6 +233,12 @@ void multiway_merge(Workspace* ws, const Tup* const* runs_host,
                     const uint64_t* lens_host, uint32_t k, Tup* out,
                     hipStream_t st);
 
+// ---- materialize.hip : merge-join output tuples (sorted R and S)
+// Writes the first min(total, out_cap) output tuples and returns the total
+// (synchronises `st` once, for the launch size of the write pass).
+uint64_t materialize(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
+                     uint64_t nS, Tup* out, uint64_t out_cap, hipStream_t st);
+
 // ---- datagen.hip
 void gen_pk(Tup* out, uint64_t n, uint64_t first, uint64_t total,
             uint64_t seed, hipStream_t st);

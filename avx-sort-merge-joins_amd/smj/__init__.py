@@ -56,7 +56,7 @@ DEVICE_SYMBOLS = [
     "smj_dev_join", "smj_join_phase_ms", "smj_dev_gen_pk", "smj_dev_gen_fk",
     "smj_dev_gen_zipf", "smj_dev_synchronize", "smj_dev_partition_range",
     "smj_trace_enable", "smj_trace_reset", "smj_trace_read", "smj_dev_join_segmented",
-    "smj_dev_partition_range_packed",
+    "smj_dev_partition_range_packed", "smj_dev_materialize",
 ]
 
 
@@ -155,6 +155,7 @@ class Library:
                                               _I64, _I64, _U32, _P, _P, _P, _P]),
             "smj_dev_partition_range_packed": (C.c_int, [_P, _P, _U64, _P, _U32, _I64, _I64,
                                                          _P, _P, _P]),
+            "smj_dev_materialize": (_U64, [_P, _P, _U64, _P, _U64, _P, _U64, _P]),
             "smj_trace_enable": (None, [_P, C.c_int]),
             "smj_trace_reset": (None, [_P]),
             "smj_trace_read": (C.c_int, [_P, C.c_char_p, C.c_int, _P, _P, C.c_int]),
@@ -319,6 +320,14 @@ class Library:
     def dev_merge_join_count(self, r, s, count):
         self.lib.smj_dev_merge_join_count(r.data_ptr(), r.shape[0], s.data_ptr(),
                                           s.shape[0], count.data_ptr(), self.stream_ptr())
+
+    def dev_materialize(self, sortedR, sortedS, out=None):
+        """Materialised merge join (smj_dev_materialize): writes the first
+        len(out) output tuples <S.key, S.payload> and returns the total."""
+        cap = 0 if out is None else out.shape[0]
+        return int(self.lib.smj_dev_materialize(
+            self.ws, sortedR.data_ptr(), sortedR.shape[0], sortedS.data_ptr(),
+            sortedS.shape[0], out.data_ptr() if cap else None, cap, self.stream_ptr()))
 
     def dev_join(self, R, S, sortedR, sortedS, count, fanout_bits=10,
                  key_min=1, key_max=0):

@@ -363,6 +363,17 @@ void smj_dev_merge_join_count(const tuple_t * r, uint64_t nr,
                               unsigned long long * count_dev,
                               smj_stream_t stream);
 
+/* Materialised merge join of two sorted relations: the output of
+ * merge_join built with JOIN_MATERIALIZE (src/joins/joincommon.c:256-289),
+ * one <S.key, S.payload> tuple per match, R-major -- per key, the S run
+ * repeated |R_k| times, keys ascending -- as one flat array (the reference's
+ * chained buffer, tuple_buffer.h, is not in its tree).  Writes the first
+ * min(total, out_cap) tuples to `out` (device) and returns the total number
+ * of matches; out_cap = 0 only counts.  Synchronises `stream` once. */
+uint64_t smj_dev_materialize(smj_workspace * ws, const tuple_t * sortedR,
+                             uint64_t nR, const tuple_t * sortedS, uint64_t nS,
+                             tuple_t * out, uint64_t out_cap, smj_stream_t stream);
+
 /* The m-way join on one device.  R and S are left untouched; sortedR/sortedS
  * (n tuples each) receive the fully sorted relations; the match count is
  * written to *count_dev.  key_min <= key_max is an optional hint of the key

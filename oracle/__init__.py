@@ -154,6 +154,14 @@ class Oracle(_Lib):
         return int(self.fn("merge_join", _U64, _P, _P, _U64, _U64)(
             _ptr(r), _ptr(s), len(r), len(s)))
 
+    def merge_join_materialize(self, r: np.ndarray, s: np.ndarray) -> np.ndarray:
+        """Output tuples of merge_join with JOIN_MATERIALIZE (sorted r, s)."""
+        f = self.fn("merge_join_materialize", _U64, _P, _P, _U64, _U64, _P, _U64)
+        n = int(f(_ptr(r), _ptr(s), len(r), len(s), None, 0))
+        out = np.zeros(n, self.dtype)
+        f(_ptr(r), _ptr(s), len(r), len(s), _ptr(out), n)
+        return out
+
     def sortmergejoin(self, r: np.ndarray, s: np.ndarray):
         sr = np.zeros(len(r), self.dtype)
         ss = np.zeros(len(s), self.dtype)

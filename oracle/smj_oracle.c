@@ -301,6 +301,35 @@ uint64_t orc_merge_join(const tuple_t *R, const tuple_t *S, uint64_t nR,
     return matches;
 }
 
+/* src/joins/joincommon.c:256-289 merge_join built with JOIN_MATERIALIZE: the
+ * same loop, appending <S.key, S.payload> per match (here into a flat array,
+ * the first `cap` matches); returns the match count */
+uint64_t orc_merge_join_materialize(const tuple_t *R, const tuple_t *S,
+                                    uint64_t nR, uint64_t nS, tuple_t *out,
+                                    uint64_t cap) {
+    uint64_t i = 0, j = 0, matches = 0;
+    while (i < nR && j < nS) {
+        if (R[i].key < S[j].key) {
+            i++;
+        } else if (R[i].key > S[j].key) {
+            j++;
+        } else {
+            uint64_t jj;
+            do {
+                jj = j;
+                do {
+                    if (matches < cap) out[matches] = S[jj];
+                    matches++;
+                    jj++;
+                } while (jj < nS && R[i].key == S[jj].key);
+                i++;
+            } while (i < nR && R[i].key == S[j].key);
+            j = jj;
+        }
+    }
+    return matches;
+}
+
 /* src/joins/sortmergejoin_multiway.c:129-328 with one thread: partition,
  * sort every partition, join partition pairs.  Because the count does not
  * depend on the partitioning, this sorts the whole relations (the sorted
