@@ -8,10 +8,13 @@
 // ascending order.  (The chained buffer's header, tuple_buffer.h, is absent
 // from the reference tree; the output here is one flat tuple array.)
 //
-// GPU form, three launches over sorted R and S:
-//   k_mat_count  one workgroup per S tile: |R_k| of every S element (a
-//                galloping search through the R window of the tile's key
-//                range), summed per tile;
+// GPU form, four launches over sorted R and S:
+//   k_mat_bounds one thread per S tile: the tile's R window (the R range of
+//                its key range) and the S extent of its first and last key
+//                runs -- the long binary searches, all in flight at once;
+//   k_mat_count  one workgroup per S tile: |R_k| of every S element, searched
+//                in the R window staged in LDS (galloping from the previous
+//                key), summed per tile;
 //   k_mat_scan   one workgroup: tile output offsets, and the work items (each
 //                tile's output cut into pieces of kMatPiece outputs);
 //   k_mat_write  one workgroup per work item: recomputes its tile's counts,
@@ -26,66 +29,76 @@ namespace smj {
 constexpr int MT_THREADS = 256;
 constexpr int MT_IPT = 8;
 constexpr uint32_t MT_TILE = MT_THREADS * MT_IPT;  // S elements per tile
+constexpr uint32_t MT_RWIN = 4096;                 // R keys staged in LDS
 constexpr uint64_t kMatPiece = 8192;                // outputs per work item
 
-// first index of [lo, hi) whose key is >= k (UPPER: > k)
-template <bool UPPER>
-__device__ __forceinline__ uint64_t key_search(const Tup* a, uint64_t lo,
-                                               uint64_t hi, int64_t k) {
+// first index of [lo, hi) whose key is >= k (UPPER: > k); K(i) = key i
+template <bool UPPER, class K>
+__device__ __forceinline__ uint64_t key_search(K key, uint64_t lo, uint64_t hi,
+                                               int64_t k) {
     while (lo < hi) {
         const uint64_t m = (lo + hi) >> 1;
-        const int64_t x = tup_key(a[m]);
+        const int64_t x = key(m);
         if (UPPER ? x <= k : x < k) lo = m + 1; else hi = m;
     }
     return lo;
 }
 
-// the same answer, galloping forward from lo (answers near lo are cheap:
-// consecutive keys of a tile sit close together in R)
-template <bool UPPER>
-__device__ __forceinline__ uint64_t key_gallop(const Tup* a, uint64_t lo,
-                                               uint64_t hi, int64_t k) {
+// the same answer, galloping forward from lo (consecutive keys of a tile sit
+// close together in R)
+template <bool UPPER, class K>
+__device__ __forceinline__ uint64_t key_gallop(K key, uint64_t lo, uint64_t hi,
+                                               int64_t k) {
     uint64_t step = 1;
     while (true) {
         const uint64_t e = lo + step - 1;
-        if (e >= hi) return key_search<UPPER>(a, lo, hi, k);
-        const int64_t x = tup_key(a[e]);
-        if (!(UPPER ? x <= k : x < k)) return key_search<UPPER>(a, lo, e, k);
+        if (e >= hi) return key_search<UPPER>(key, lo, hi, k);
+        const int64_t x = key(e);
+        if (!(UPPER ? x <= k : x < k)) return key_search<UPPER>(key, lo, e, k);
         lo = e + 1;
         step <<= 1;
     }
 }
 
+struct TupKey {
+    const Tup* a;
+    __device__ __forceinline__ int64_t operator()(uint64_t i) const { return tup_key(a[i]); }
+};
+
+// per tile: R window [lo, hi), S start of the first key run, S end of the last
+__global__ void __launch_bounds__(256)
+k_mat_bounds(const Tup* __restrict__ R, uint64_t nR, const Tup* __restrict__ S,
+             uint64_t nS, uint64_t ntiles, uint64_t* __restrict__ bounds) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ntiles) return;
+    const uint64_t tb = t * MT_TILE;
+    const uint64_t te = min(tb + MT_TILE, nS);
+    const TupKey rk{R}, sk{S};
+    const int64_t kf = sk(tb), kl = sk(te - 1);
+    const uint64_t rlo = key_search<false>(rk, 0, nR, kf);
+    const uint64_t rhi = key_search<true>(rk, rlo, nR, kl);
+    const uint64_t s0 = (tb > 0 && sk(tb - 1) == kf) ? key_search<false>(sk, 0, tb, kf) : tb;
+    const uint64_t se = (te < nS && sk(te) == kl) ? key_search<true>(sk, te, nS, kl) : te;
+    bounds[4 * t + 0] = rlo;
+    bounds[4 * t + 1] = rhi;
+    bounds[4 * t + 2] = s0;
+    bounds[4 * t + 3] = se;
+}
+
 struct MatLDS {
     int64_t key[MT_TILE];
-    uint64_t rc[MT_TILE];  // |R_k| of the element; inclusive prefix (write)
-    int64_t s0[MT_TILE];   // S index where the element's key run starts
-    int64_t se[MT_TILE];   // S index where it ends
-    uint64_t ends[4];      // R window [lo, hi), first run start, last run end
+    uint64_t rc[MT_TILE];    // |R_k| of the element; inclusive prefix (write)
+    uint16_t s0[MT_TILE];    // tile index of the element's run start (0: ends[2])
+    uint16_t se[MT_TILE];    // tile index of its run end (MT_TILE... len: ends[3])
+    int64_t rkey[MT_RWIN];   // the R window's keys, when it fits
+    uint64_t ends[4];
     uint64_t wsum[MT_THREADS / 64 + 1];
 };
 
-// key runs and R match counts of S[tb, tb + len)
-__device__ void mat_tile(const Tup* __restrict__ R, uint64_t nR,
-                         const Tup* __restrict__ S, uint64_t nS, uint64_t tb,
-                         uint32_t len, MatLDS& L) {
-    const uint32_t tid = threadIdx.x;
-    for (uint32_t i = tid; i < len; i += MT_THREADS) L.key[i] = tup_key(S[tb + i]);
-    __syncthreads();
-    const int64_t kf = L.key[0], kl = L.key[len - 1];
-    if (tid == 0) L.ends[0] = key_search<false>(R, 0, nR, kf);
-    if (tid == 64) L.ends[1] = key_search<true>(R, 0, nR, kl);
-    if (tid == 128)
-        L.ends[2] = (tb > 0 && tup_key(S[tb - 1]) == kf) ? key_search<false>(S, 0, tb, kf) : tb;
-    if (tid == 192)
-        L.ends[3] = (tb + len < nS && tup_key(S[tb + len]) == kl)
-                        ? key_search<true>(S, tb + len, nS, kl)
-                        : tb + len;
-    __syncthreads();
-    const uint32_t i0 = tid * MT_IPT;
-    if (i0 >= len) return;
-    const uint32_t i1 = min(i0 + (uint32_t)MT_IPT, len);
-    const uint64_t Rhi = max(L.ends[0], L.ends[1]);
+template <class K>
+__device__ __forceinline__ void mat_runs(K rkey, uint64_t Rlo, uint64_t Rhi,
+                                         uint32_t i0, uint32_t i1, uint32_t len,
+                                         MatLDS& L) {
     // run start of the thread's first element, run end of its last (LDS)
     uint32_t a = 0, b = i0;
     {
@@ -103,24 +116,47 @@ __device__ void mat_tile(const Tup* __restrict__ R, uint64_t nR,
             if (L.key[m] <= k) c = m + 1; else d = m;
         }
     }
-    const int64_t last_end = c == len ? (int64_t)L.ends[3] : (int64_t)(tb + c);
-    int64_t s0 = a == 0 ? (int64_t)L.ends[2] : (int64_t)(tb + a);
-    uint64_t rlo, rhi = L.ends[0];
+    uint32_t s0 = a;
+    uint64_t rlo, rhi = Rlo;
     uint32_t i = i0;
     while (i < i1) {
         const int64_t k = L.key[i];
         uint32_t j = i + 1;
         while (j < i1 && L.key[j] == k) j++;
-        if (i != i0) s0 = (int64_t)(tb + i);
-        rlo = key_gallop<false>(R, rhi, Rhi, k);
-        rhi = key_gallop<true>(R, rlo, Rhi, k);
-        const int64_t e = j < i1 ? (int64_t)(tb + j) : last_end;
+        if (i != i0) s0 = i;
+        rlo = key_gallop<false>(rkey, rhi, Rhi, k);
+        rhi = key_gallop<true>(rkey, rlo, Rhi, k);
+        const uint32_t e = j < i1 ? j : c;
         for (uint32_t u = i; u < j; u++) {
             L.rc[u] = rhi - rlo;
-            L.s0[u] = s0;
-            L.se[u] = e;
+            L.s0[u] = (uint16_t)s0;
+            L.se[u] = (uint16_t)e;
         }
         i = j;
+    }
+}
+
+// key runs and R match counts of S[tb, tb + len)
+__device__ void mat_tile(const Tup* __restrict__ R, const Tup* __restrict__ S,
+                         const uint64_t* __restrict__ bounds, uint64_t t,
+                         uint64_t tb, uint32_t len, MatLDS& L) {
+    const uint32_t tid = threadIdx.x;
+    if (tid < 4) L.ends[tid] = bounds[4 * t + tid];
+    for (uint32_t i = tid; i < len; i += MT_THREADS) L.key[i] = tup_key(S[tb + i]);
+    __syncthreads();
+    const uint64_t Rlo = L.ends[0], Rhi = L.ends[1];
+    const bool staged = Rhi - Rlo <= MT_RWIN;
+    if (staged)
+        for (uint32_t i = tid; i < Rhi - Rlo; i += MT_THREADS) L.rkey[i] = tup_key(R[Rlo + i]);
+    __syncthreads();
+    const uint32_t i0 = tid * MT_IPT;
+    if (i0 >= len) return;
+    const uint32_t i1 = min(i0 + (uint32_t)MT_IPT, len);
+    if (staged) {
+        const int64_t* rk = L.rkey;
+        mat_runs([rk](uint64_t i) { return rk[i]; }, 0, Rhi - Rlo, i0, i1, len, L);
+    } else {
+        mat_runs(TupKey{R}, Rlo, Rhi, i0, i1, len, L);
     }
 }
 
@@ -153,12 +189,12 @@ __device__ __forceinline__ uint64_t block_scan64(uint64_t v, uint64_t* wsum,
 }
 
 __global__ void __launch_bounds__(MT_THREADS)
-k_mat_count(const Tup* __restrict__ R, uint64_t nR, const Tup* __restrict__ S,
-            uint64_t nS, uint64_t* __restrict__ tile_out) {
+k_mat_count(const Tup* __restrict__ R, const Tup* __restrict__ S, uint64_t nS,
+            const uint64_t* __restrict__ bounds, uint64_t* __restrict__ tile_out) {
     __shared__ MatLDS L;
     const uint64_t tb = (uint64_t)blockIdx.x * MT_TILE;
     const uint32_t len = (uint32_t)min((uint64_t)MT_TILE, nS - tb);
-    mat_tile(R, nR, S, nS, tb, len, L);
+    mat_tile(R, S, bounds, blockIdx.x, tb, len, L);
     uint64_t s = 0;
     const uint32_t i0 = threadIdx.x * MT_IPT;
     for (uint32_t u = i0; u < min(i0 + (uint32_t)MT_IPT, len); u++) s += L.rc[u];
@@ -202,8 +238,8 @@ k_mat_scan(const uint64_t* __restrict__ cnt, uint64_t ntiles,
 }
 
 __global__ void __launch_bounds__(MT_THREADS)
-k_mat_write(const Tup* __restrict__ R, uint64_t nR, const Tup* __restrict__ S,
-            uint64_t nS, const uint64_t* __restrict__ cnt,
+k_mat_write(const Tup* __restrict__ R, const Tup* __restrict__ S, uint64_t nS,
+            const uint64_t* __restrict__ bounds, const uint64_t* __restrict__ cnt,
             const uint64_t* __restrict__ base, const uint64_t* __restrict__ ibase,
             uint64_t ntiles, Tup* __restrict__ out, uint64_t out_cap) {
     __shared__ MatLDS L;
@@ -226,7 +262,7 @@ k_mat_write(const Tup* __restrict__ R, uint64_t nR, const Tup* __restrict__ S,
     if (ob + q0 >= out_cap) return;  // uniform over the workgroup
     const uint64_t tb = t * MT_TILE;
     const uint32_t len = (uint32_t)min((uint64_t)MT_TILE, nS - tb);
-    mat_tile(R, nR, S, nS, tb, len, L);
+    mat_tile(R, S, bounds, t, tb, len, L);
     // inclusive prefix of the counts over the tile
     const uint32_t i0 = threadIdx.x * MT_IPT;
     const uint32_t i1 = min(i0 + (uint32_t)MT_IPT, len);
@@ -238,6 +274,7 @@ k_mat_write(const Tup* __restrict__ R, uint64_t nR, const Tup* __restrict__ S,
         L.rc[u] = run;
     }
     __syncthreads();
+    const int64_t first_s0 = (int64_t)L.ends[2], last_se = (int64_t)L.ends[3];
     for (uint64_t q = q0 + threadIdx.x; q < q1; q += MT_THREADS) {
         if (ob + q >= out_cap) break;
         // element j: the first inclusive prefix above q
@@ -249,8 +286,10 @@ k_mat_write(const Tup* __restrict__ R, uint64_t nR, const Tup* __restrict__ S,
         const uint32_t j = lo;
         const uint64_t excl = j ? L.rc[j - 1] : 0;
         const uint64_t rcj = L.rc[j] - excl;
-        const int64_t s0 = L.s0[j];
-        const uint64_t sc = (uint64_t)(L.se[j] - s0);
+        const uint32_t a = L.s0[j], c = L.se[j];
+        const int64_t s0 = a == 0 ? first_s0 : (int64_t)(tb + a);
+        const int64_t se = c == len ? last_se : (int64_t)(tb + c);
+        const uint64_t sc = (uint64_t)(se - s0);
         // the run's output starts (tb + j - s0) * rcj outputs before element
         // j's first (mod 2^64 when the run began in an earlier tile)
         const uint64_t off = q - (excl - (uint64_t)((int64_t)(tb + j) - s0) * rcj);
@@ -263,15 +302,19 @@ uint64_t materialize(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
                      uint64_t nS, Tup* out, uint64_t out_cap, hipStream_t st) {
     if (nR == 0 || nS == 0) return 0;
     const uint64_t ntiles = (nS + MT_TILE - 1) / MT_TILE;
-    uint64_t* tab = (uint64_t*)ws->scratch("mat_tab", (3 * ntiles + 2) * 8);
+    uint64_t* tab = (uint64_t*)ws->scratch("mat_tab", (7 * ntiles + 2) * 8);
     uint64_t* cnt = tab;
     uint64_t* base = tab + ntiles;
     uint64_t* ibase = tab + 2 * ntiles;
-    uint64_t* tot = tab + 3 * ntiles;
+    uint64_t* bounds = tab + 3 * ntiles;  // 4 per tile
+    uint64_t* tot = tab + 7 * ntiles;
+    hipLaunchKernelGGL(k_mat_bounds, dim3((uint32_t)((ntiles + 255) / 256)), dim3(256), 0,
+                       st, R, nR, S, nS, ntiles, bounds);
+    SMJ_CHECK(hipGetLastError());
     {
         TraceScope ts(ws, "k_mat_count", st);
         hipLaunchKernelGGL(k_mat_count, dim3((uint32_t)ntiles), dim3(MT_THREADS), 0,
-                           st, R, nR, S, nS, cnt);
+                           st, R, S, nS, bounds, cnt);
         SMJ_CHECK(hipGetLastError());
     }
     hipLaunchKernelGGL(k_mat_scan, dim3(1), dim3(1024), 0, st, cnt, ntiles, base,
@@ -284,7 +327,7 @@ uint64_t materialize(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
     if (items && out_cap) {
         TraceScope ts(ws, "k_mat_write", st);
         hipLaunchKernelGGL(k_mat_write, dim3((uint32_t)items), dim3(MT_THREADS), 0,
-                           st, R, nR, S, nS, cnt, base, ibase, ntiles, out, out_cap);
+                           st, R, S, nS, bounds, cnt, base, ibase, ntiles, out, out_cap);
         SMJ_CHECK(hipGetLastError());
     }
     return total;
