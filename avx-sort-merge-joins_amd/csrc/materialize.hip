@@ -27,9 +27,11 @@
 namespace smj {
 
 constexpr int MT_THREADS = 256;
-constexpr int MT_IPT = 8;
+// small tiles keep the LDS per workgroup at 36 KB (4 workgroups per CU), so
+// the staging loads of some workgroups overlap the searches of others
+constexpr int MT_IPT = 4;
 constexpr uint32_t MT_TILE = MT_THREADS * MT_IPT;  // S elements per tile
-constexpr uint32_t MT_RWIN = 4096;                 // R keys staged in LDS
+constexpr uint32_t MT_RWIN = 2 * MT_TILE;          // R keys staged in LDS
 constexpr uint64_t kMatPiece = 8192;                // outputs per work item
 
 // first index of [lo, hi) whose key is >= k (UPPER: > k); K(i) = key i
