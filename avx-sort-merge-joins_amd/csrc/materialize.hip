@@ -27,9 +27,10 @@
 namespace smj {
 
 constexpr int MT_THREADS = 256;
-// small tiles keep the LDS per workgroup at 36 KB (4 workgroups per CU), so
+// small tiles keep the LDS per workgroup at 18 KB (8 workgroups per CU), so
 // the staging loads of some workgroups overlap the searches of others
-constexpr int MT_IPT = 4;
+// (2048-element tiles: 6.6 ms at 128M x 128M, 1024: 4.6 ms, 512: 4.2 ms)
+constexpr int MT_IPT = 2;
 constexpr uint32_t MT_TILE = MT_THREADS * MT_IPT;  // S elements per tile
 constexpr uint32_t MT_RWIN = 2 * MT_TILE;          // R keys staged in LDS
 constexpr uint64_t kMatPiece = 8192;                // outputs per work item
