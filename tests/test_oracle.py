@@ -98,6 +98,19 @@ def test_merge_join(case):
     np.testing.assert_array_equal(got, g["mj_counts"])
 
 
+def test_merge_join_materialize(case):
+    """The materialising restatement (joincommon.c:256-289) on the golden
+    merge-join inputs: as many tuples as the reference counted, equal to an
+    independent numpy construction (per key, the S run repeated |R_k| times)."""
+    from test_gpu_materialize import numpy_materialize
+    w, orc, g = case
+    for s, count in zip((1, 2, 3), g["mj_counts"].tolist()):
+        R, S = g[f"mj{s}_R"], g[f"mj{s}_S"]
+        out = orc.merge_join_materialize(R, S)
+        assert len(out) == count
+        assert np.array_equal(out, numpy_materialize(R, S))
+
+
 def join_inputs(gen, kind, nr, ns):
     """Same inputs as tests/golden/make_golden.py:join_inputs."""
     gen.seed(12345)
