@@ -8,14 +8,14 @@
 // ascending order.  (The chained buffer's header, tuple_buffer.h, is absent
 // from the reference tree; the output here is one flat tuple array.)
 //
-// GPU form, four launches over sorted R and S:
+// GPU form, over sorted R and S:
 //   k_mat_bounds one thread per S tile: the tile's R window (the R range of
 //                its key range) and the S extent of its first and last key
 //                runs -- the long binary searches, all in flight at once;
 //   k_mat_count  one workgroup per S tile: |R_k| of every S element, searched
 //                in the R window staged in LDS (galloping from the previous
 //                key), summed per tile;
-//   k_mat_scan   one workgroup: tile output offsets, and the work items (each
+//   k_mat_part/pscan/down  tile output offsets, and the work items (each
 //                tile's output cut into pieces of kMatPiece outputs);
 //   k_mat_write  one workgroup per work item: recomputes its tile's counts,
 //                scans them in LDS and writes its piece output-major, so the
@@ -211,32 +211,68 @@ k_mat_count(const Tup* __restrict__ R, const Tup* __restrict__ S, uint64_t nS,
     }
 }
 
-// tile output bases and work-item bases (exclusive), totals into tot[0..1]
-__global__ void __launch_bounds__(1024)
-k_mat_scan(const uint64_t* __restrict__ cnt, uint64_t ntiles,
-           uint64_t* __restrict__ base, uint64_t* __restrict__ ibase,
-           uint64_t* __restrict__ tot) {
-    __shared__ uint64_t ws[1024 / 64 + 1];
-    const uint64_t per = (ntiles + 1023) / 1024;
-    const uint64_t t0 = min(ntiles, (uint64_t)threadIdx.x * per);
-    const uint64_t t1 = min(ntiles, t0 + per);
-    uint64_t so = 0, si = 0;
-    for (uint64_t t = t0; t < t1; t++) {
-        so += cnt[t];
-        si += (cnt[t] + kMatPiece - 1) / kMatPiece;
+__device__ __forceinline__ uint64_t mat_items(uint64_t c) {
+    return (c + kMatPiece - 1) / kMatPiece;
+}
+
+// tile output bases and work-item bases (exclusive) in three launches:
+// per 1024 tiles the sums (k_mat_part), one workgroup scanning those
+// (k_mat_pscan, totals into tot[0..1]), per 1024 tiles the bases (k_mat_down)
+constexpr uint32_t MS_BLOCK = 1024;
+
+__global__ void __launch_bounds__(MS_BLOCK)
+k_mat_part(const uint64_t* __restrict__ cnt, uint64_t ntiles, uint64_t* __restrict__ part) {
+    __shared__ uint64_t ws[2][MS_BLOCK / 64];
+    const uint64_t t = (uint64_t)blockIdx.x * MS_BLOCK + threadIdx.x;
+    const uint64_t c = t < ntiles ? cnt[t] : 0;
+    const uint64_t so = wave_sum(c), si = wave_sum(mat_items(c));
+    if (lane_id() == 0) {
+        ws[0][threadIdx.x >> 6] = so;
+        ws[1][threadIdx.x >> 6] = si;
     }
-    uint64_t to, ti;
-    uint64_t eo = block_scan64(so, ws, &to);
-    uint64_t ei = block_scan64(si, ws, &ti);
-    for (uint64_t t = t0; t < t1; t++) {
-        base[t] = eo;
-        ibase[t] = ei;
-        eo += cnt[t];
-        ei += (cnt[t] + kMatPiece - 1) / kMatPiece;
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        uint64_t a = 0;
+        for (uint32_t w = 0; w < MS_BLOCK / 64; w++) a += ws[threadIdx.x][w];
+        part[2 * blockIdx.x + threadIdx.x] = a;
+    }
+}
+
+// exclusive scan of the (outputs, items) pairs of nb blocks, in place
+__global__ void __launch_bounds__(MS_BLOCK)
+k_mat_pscan(uint64_t* __restrict__ part, uint32_t nb, uint64_t* __restrict__ tot) {
+    __shared__ uint64_t ws[MS_BLOCK / 64 + 1];
+    uint64_t carry_o = 0, carry_i = 0;
+    for (uint32_t r0 = 0; r0 < nb; r0 += MS_BLOCK) {
+        const uint32_t b = r0 + threadIdx.x;
+        const uint64_t vo = b < nb ? part[2 * b] : 0, vi = b < nb ? part[2 * b + 1] : 0;
+        uint64_t to, ti;
+        const uint64_t eo = block_scan64(vo, ws, &to), ei = block_scan64(vi, ws, &ti);
+        if (b < nb) {
+            part[2 * b] = carry_o + eo;
+            part[2 * b + 1] = carry_i + ei;
+        }
+        carry_o += to;
+        carry_i += ti;
     }
     if (threadIdx.x == 0) {
-        tot[0] = to;
-        tot[1] = ti;
+        tot[0] = carry_o;
+        tot[1] = carry_i;
+    }
+}
+
+__global__ void __launch_bounds__(MS_BLOCK)
+k_mat_down(const uint64_t* __restrict__ cnt, uint64_t ntiles,
+           const uint64_t* __restrict__ part, uint64_t* __restrict__ base,
+           uint64_t* __restrict__ ibase) {
+    __shared__ uint64_t ws[MS_BLOCK / 64 + 1];
+    const uint64_t t = (uint64_t)blockIdx.x * MS_BLOCK + threadIdx.x;
+    const uint64_t c = t < ntiles ? cnt[t] : 0;
+    const uint64_t eo = block_scan64(c, ws, nullptr);
+    const uint64_t ei = block_scan64(mat_items(c), ws, nullptr);
+    if (t < ntiles) {
+        base[t] = part[2 * blockIdx.x] + eo;
+        ibase[t] = part[2 * blockIdx.x + 1] + ei;
     }
 }
 
@@ -311,18 +347,30 @@ uint64_t materialize(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
     uint64_t* ibase = tab + 2 * ntiles;
     uint64_t* bounds = tab + 3 * ntiles;  // 4 per tile
     uint64_t* tot = tab + 7 * ntiles;
-    hipLaunchKernelGGL(k_mat_bounds, dim3((uint32_t)((ntiles + 255) / 256)), dim3(256), 0,
-                       st, R, nR, S, nS, ntiles, bounds);
-    SMJ_CHECK(hipGetLastError());
+    {
+        TraceScope ts(ws, "k_mat_bounds", st);
+        hipLaunchKernelGGL(k_mat_bounds, dim3((uint32_t)((ntiles + 255) / 256)), dim3(256),
+                           0, st, R, nR, S, nS, ntiles, bounds);
+        SMJ_CHECK(hipGetLastError());
+    }
     {
         TraceScope ts(ws, "k_mat_count", st);
         hipLaunchKernelGGL(k_mat_count, dim3((uint32_t)ntiles), dim3(MT_THREADS), 0,
                            st, R, S, nS, bounds, cnt);
         SMJ_CHECK(hipGetLastError());
     }
-    hipLaunchKernelGGL(k_mat_scan, dim3(1), dim3(1024), 0, st, cnt, ntiles, base,
-                       ibase, tot);
-    SMJ_CHECK(hipGetLastError());
+    {
+        TraceScope ts(ws, "k_mat_scan", st);
+        const uint32_t nb = (uint32_t)((ntiles + MS_BLOCK - 1) / MS_BLOCK);
+        uint64_t* part = (uint64_t*)ws->scratch("mat_part", (size_t)nb * 16);
+        hipLaunchKernelGGL(k_mat_part, dim3(nb), dim3(MS_BLOCK), 0, st, cnt, ntiles, part);
+        SMJ_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(k_mat_pscan, dim3(1), dim3(MS_BLOCK), 0, st, part, nb, tot);
+        SMJ_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(k_mat_down, dim3(nb), dim3(MS_BLOCK), 0, st, cnt, ntiles, part,
+                           base, ibase);
+        SMJ_CHECK(hipGetLastError());
+    }
     uint64_t* h = (uint64_t*)ws->host_pinned("mat_tot_h", 16);
     SMJ_CHECK(hipMemcpyAsync(h, tot, 16, hipMemcpyDeviceToHost, st));
     SMJ_CHECK(hipStreamSynchronize(st));
