@@ -193,14 +193,31 @@ __device__ __forceinline__ uint64_t block_scan64(uint64_t v, uint64_t* wsum,
 
 __global__ void __launch_bounds__(MT_THREADS)
 k_mat_count(const Tup* __restrict__ R, const Tup* __restrict__ S, uint64_t nS,
-            const uint64_t* __restrict__ bounds, uint64_t* __restrict__ tile_out) {
+            const uint64_t* __restrict__ bounds, uint64_t* __restrict__ tile_out,
+            uint64_t* __restrict__ bitmap, uint32_t* __restrict__ multi_out) {
     __shared__ MatLDS L;
     const uint64_t tb = (uint64_t)blockIdx.x * MT_TILE;
     const uint32_t len = (uint32_t)min((uint64_t)MT_TILE, nS - tb);
     mat_tile(R, S, bounds, blockIdx.x, tb, len, L);
     uint64_t s = 0;
+    int multi = 0;
     const uint32_t i0 = threadIdx.x * MT_IPT;
-    for (uint32_t u = i0; u < min(i0 + (uint32_t)MT_IPT, len); u++) s += L.rc[u];
+    for (uint32_t u = i0; u < min(i0 + (uint32_t)MT_IPT, len); u++) {
+        s += L.rc[u];
+        multi |= L.rc[u] > 1;
+    }
+    multi = __syncthreads_or(multi);
+    if (!multi) {
+        // every element matches at most once (a key join): its matches as a
+        // bitmap, so the write pass copies them without the R window
+#pragma unroll
+        for (uint32_t p = 0; p < MT_IPT; p++) {
+            const uint32_t e = p * MT_THREADS + threadIdx.x;
+            const uint64_t bal = __ballot(e < len && L.rc[e] != 0);
+            if (lane_id() == 0) bitmap[blockIdx.x * (MT_TILE / 64) + e / 64] = bal;
+        }
+    }
+    if (threadIdx.x == 0) multi_out[blockIdx.x] = (uint32_t)multi;
     s = wave_sum(s);
     if (lane_id() == 0) L.wsum[threadIdx.x >> 6] = s;
     __syncthreads();
@@ -280,7 +297,8 @@ __global__ void __launch_bounds__(MT_THREADS)
 k_mat_write(const Tup* __restrict__ R, const Tup* __restrict__ S, uint64_t nS,
             const uint64_t* __restrict__ bounds, const uint64_t* __restrict__ cnt,
             const uint64_t* __restrict__ base, const uint64_t* __restrict__ ibase,
-            uint64_t ntiles, Tup* __restrict__ out, uint64_t out_cap) {
+            uint64_t ntiles, const uint64_t* __restrict__ bitmap,
+            const uint32_t* __restrict__ multi, Tup* __restrict__ out, uint64_t out_cap) {
     __shared__ MatLDS L;
     __shared__ uint64_t sh_t;
     const uint64_t w = blockIdx.x;
@@ -301,6 +319,29 @@ k_mat_write(const Tup* __restrict__ R, const Tup* __restrict__ S, uint64_t nS,
     if (ob + q0 >= out_cap) return;  // uniform over the workgroup
     const uint64_t tb = t * MT_TILE;
     const uint32_t len = (uint32_t)min((uint64_t)MT_TILE, nS - tb);
+    if (!multi[t]) {
+        // key join tile (one piece): copy the matching elements in order
+        constexpr uint32_t NW = MT_TILE / 64;
+        uint64_t bw[NW];
+#pragma unroll
+        for (uint32_t k = 0; k < NW; k++) bw[k] = bitmap[t * NW + k];
+#pragma unroll
+        for (uint32_t p = 0; p < MT_IPT; p++) {
+            const uint32_t e = p * MT_THREADS + threadIdx.x;
+            uint32_t rank = 0;
+            bool hit = false;
+#pragma unroll
+            for (uint32_t k = 0; k < NW; k++) {
+                if (k < e / 64) rank += __popcll(bw[k]);
+                if (k == e / 64) {
+                    rank += __popcll(bw[k] & ((1ull << (e & 63)) - 1));
+                    hit = (bw[k] >> (e & 63)) & 1;
+                }
+            }
+            if (hit && e < len && ob + rank < out_cap) st_stream(out + ob + rank, S[tb + e]);
+        }
+        return;
+    }
     mat_tile(R, S, bounds, t, tb, len, L);
     // inclusive prefix of the counts over the tile
     const uint32_t i0 = threadIdx.x * MT_IPT;
@@ -342,6 +383,8 @@ uint64_t materialize(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
     if (nR == 0 || nS == 0) return 0;
     const uint64_t ntiles = (nS + MT_TILE - 1) / MT_TILE;
     uint64_t* tab = (uint64_t*)ws->scratch("mat_tab", (7 * ntiles + 2) * 8);
+    uint64_t* bitmap = (uint64_t*)ws->scratch("mat_bits", ntiles * (MT_TILE / 8));
+    uint32_t* multi = (uint32_t*)ws->scratch("mat_multi", ntiles * 4);
     uint64_t* cnt = tab;
     uint64_t* base = tab + ntiles;
     uint64_t* ibase = tab + 2 * ntiles;
@@ -356,7 +399,7 @@ uint64_t materialize(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
     {
         TraceScope ts(ws, "k_mat_count", st);
         hipLaunchKernelGGL(k_mat_count, dim3((uint32_t)ntiles), dim3(MT_THREADS), 0,
-                           st, R, S, nS, bounds, cnt);
+                           st, R, S, nS, bounds, cnt, bitmap, multi);
         SMJ_CHECK(hipGetLastError());
     }
     {
@@ -378,7 +421,8 @@ uint64_t materialize(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
     if (items && out_cap) {
         TraceScope ts(ws, "k_mat_write", st);
         hipLaunchKernelGGL(k_mat_write, dim3((uint32_t)items), dim3(MT_THREADS), 0,
-                           st, R, S, nS, bounds, cnt, base, ibase, ntiles, out, out_cap);
+                           st, R, S, nS, bounds, cnt, base, ibase, ntiles, bitmap, multi,
+                           out, out_cap);
         SMJ_CHECK(hipGetLastError());
     }
     return total;
