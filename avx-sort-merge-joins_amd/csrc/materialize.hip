@@ -14,13 +14,15 @@
 //                runs -- the long binary searches, all in flight at once;
 //   k_mat_count  one workgroup per S tile: |R_k| of every S element, searched
 //                in the R window staged in LDS (galloping from the previous
-//                key), summed per tile;
+//                key), summed per tile; a tile whose elements match at most
+//                once (R unique) also leaves its match bitmap;
 //   k_mat_part/pscan/down  tile output offsets, and the work items (each
 //                tile's output cut into pieces of kMatPiece outputs);
 //   k_mat_write  one workgroup per work item: recomputes its tile's counts,
 //                scans them in LDS and writes its piece output-major, so the
 //                stores are coalesced and a hot key spreads over many
-//                workgroups instead of serialising one thread.
+//                workgroups instead of serialising one thread (bitmap tiles:
+//                an ordered copy of the set elements, nothing recomputed).
 #include "smj_common.hpp"
 #include "smj_internal.hpp"
 
