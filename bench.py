@@ -132,6 +132,11 @@ def load_traffic(kernel, cfg_key):
 # --------------------------------------------------------------------------
 def main():
     a = parse()
+    # stdout carries exactly the one JSON line: native libraries (RCCL prints
+    # a version banner at communicator setup) write to stderr instead
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -281,7 +286,7 @@ def main():
             "exchange": xchg,
         },
     }
-    print(json.dumps(out))
+    print(json.dumps(out), file=json_out, flush=True)
     if dist:
         dist.destroy_process_group()
 
