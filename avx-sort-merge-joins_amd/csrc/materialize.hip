@@ -31,7 +31,9 @@ namespace smj {
 constexpr int MT_THREADS = 256;
 // small tiles keep the LDS per workgroup at 18 KB (8 workgroups per CU), so
 // the staging loads of some workgroups overlap the searches of others
-// (2048-element tiles: 6.6 ms at 128M x 128M, 1024: 4.6 ms, 512: 4.2 ms)
+// (16 B, 128M x 128M, before the bitmap path: 2048-element tiles 6.6 ms,
+// 1024: 4.6 ms, 512: 4.2 ms; with it: 1024: 2.9 ms, 512: 2.4 ms, 256: 3.7 ms
+// -- more, smaller tiles lose to the per-tile searches and launch width)
 constexpr int MT_IPT = 2;
 constexpr uint32_t MT_TILE = MT_THREADS * MT_IPT;  // S elements per tile
 constexpr uint32_t MT_RWIN = 2 * MT_TILE;          // R keys staged in LDS
