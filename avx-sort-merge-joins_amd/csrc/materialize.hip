@@ -422,9 +422,15 @@ uint64_t materialize(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
     SMJ_CHECK(hipMemcpyAsync(h, tot, 16, hipMemcpyDeviceToHost, st));
     SMJ_CHECK(hipStreamSynchronize(st));
     const uint64_t total = h[0], items = h[1];
-    if (items && out_cap) {
+    // work items run in output order and every tile's items but its last
+    // hold kMatPiece outputs: the items below out_cap number at most one per
+    // tile plus out_cap / kMatPiece (a small buffer for a huge skewed join
+    // launches no more than that)
+    const uint64_t need = ntiles + out_cap / kMatPiece + 1;
+    const uint64_t launch = items < need ? items : need;
+    if (launch && out_cap) {
         TraceScope ts(ws, "k_mat_write", st);
-        hipLaunchKernelGGL(k_mat_write, dim3((uint32_t)items), dim3(MT_THREADS), 0,
+        hipLaunchKernelGGL(k_mat_write, dim3((uint32_t)launch), dim3(MT_THREADS), 0,
                            st, R, S, nS, bounds, cnt, base, ibase, ntiles, bitmap, multi,
                            out, out_cap);
         SMJ_CHECK(hipGetLastError());

@@ -39,6 +39,7 @@ import torch.distributed as dist
 # exact scatter costs 0.96 / 1.09 / 1.53 / 3.32 ms per 128M 16-byte tuples at
 # 9 / 10 / 11 / 12 bits (tools/bench_xpart.py): 12 bits scatter too thinly.
 MAX_PARTITION_BITS = 11
+INT64_MAX = (1 << 63) - 1
 # Largest single message of the row exchange.  RCCL 2.26 (torch 2.10 ROCm)
 # corrupts all_to_all_single messages of 1.6 GB and more (tools/debug_a2a.py);
 # larger exchanges go as chunked point-to-point sends in one group.
@@ -84,6 +85,32 @@ def range_digit(keys: torch.Tensor, key_min: int, key_max: int, bits: int) -> to
 
 def ceil_log2(x: int) -> int:
     return max(x - 1, 0).bit_length()
+
+
+def local_range(key_min: int, key_max: int, pbits: int, world: int, rank: int):
+    """(plan base, key_lo, key_hi, lbits) of `rank`.
+
+    The global plan covers [base, base + 2^L) with L the bit length of
+    key_max - key_min; near INT64_MAX that top would pass the int64 range, so
+    the base moves down instead (the width keeps its bit length L; every rank
+    computes the same base).  The rank's partitions [p_lo, p_hi) are the
+    level-1 buckets of its local plan, 2^lbits of them; [key_lo, key_hi] only
+    fixes that plan's bit length s1 + lbits (make_plan), and the smallest such
+    width keeps key_hi inside the global range, so inside int64."""
+    L = max(key_max - key_min, 0).bit_length()
+    if key_min + (1 << L) - 1 > INT64_MAX:
+        key_min = INT64_MAX - (1 << L) + 1
+    F = 1 << pbits
+    p_lo, p_hi = owned(F, world, rank)
+    lbits = ceil_log2(max(p_hi - p_lo, 1))
+    s1 = plan_shift(key_min, key_max, pbits)
+    key_lo = key_min + (p_lo << s1)
+    key_hi = key_lo + (1 << (s1 + lbits - 1)) if lbits else key_lo + (1 << s1) - 1
+    # with fewer keys than partitions (s1 = 0) the top partitions hold no key:
+    # a narrower local range keeps s1 = 0 and stays inside int64
+    top = key_min + (1 << L) - 1
+    key_lo, key_hi = min(key_lo, top), min(key_hi, top)
+    return key_min, key_lo, key_hi, lbits
 
 
 def send_counts(hist: torch.Tensor, world: int) -> torch.Tensor:
@@ -139,16 +166,12 @@ class DistributedJoin:
         self.fanout = 1 << self.pbits
         if self.fanout < self.world:
             raise ValueError(f"fanout 2^{self.pbits} < world size {self.world}")
-        self.key_min = key_min
+        self.key_min, self.key_lo, self.key_hi, self.lbits = local_range(
+            key_min, key_max, self.pbits, self.world, self.rank)
         self.key_max = key_max
         F, G = self.fanout, self.world
         self.per_rank = [owned(F, G, g)[1] - owned(F, G, g)[0] for g in range(G)]
         self.p_lo, self.p_hi = owned(F, G, self.rank)
-        # the local plan: this rank's partitions are its level-1 buckets
-        self.lbits = ceil_log2(max(self.p_hi - self.p_lo, 1))
-        s1 = plan_shift(key_min, key_max, self.pbits)
-        self.key_lo = key_min + (self.p_lo << s1)
-        self.key_hi = self.key_lo + (1 << (s1 + self.lbits)) - 1
         self.buf = {}
         self.last_recv = {}
         self.last_packed = False  # the layout of the last step's exchange
@@ -263,9 +286,15 @@ class DistributedJoin:
             e1.record()
             self._ev.append((eS, e1))
         self.stats["steps"] += 1
-        if pR != pS:  # S could not be packed: R again, as tuples
+        # both relations must reach the local join in one layout: the one
+        # that went out packed is exchanged again as tuples
+        if pR and not pS:
             rR, segR, wR, pR = self._exchange(R, "R", allow_pack=False)
             wR.wait()
+        elif pS and not pR:
+            rS, segS, wS, pS = self._exchange(S, "S", allow_pack=False)
+            wS.wait()
+        assert pR == pS
         self.last_packed = pR
         sR = self._grow("sortR", rR.shape[0])
         sS = self._grow("sortS", rS.shape[0])

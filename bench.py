@@ -35,13 +35,24 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--n", type=int, default=128_000_000,
-                   help="tuples per relation per GPU")
-    p.add_argument("--width", type=int, default=16, choices=(8, 16))
+    p.add_argument("--op", default="join", choices=("join", "sort", "partition"),
+                   help="join: sortmergejoin_multiway (the headline); sort: bench_sort's "
+                        "avxsort_tuples on 2^27 tuples; partition: bench_partitioning's "
+                        "partition_relation_optimized on 2^27 tuples")
+    p.add_argument("--n", type=int, default=None,
+                   help="tuples per relation per GPU (join: 128M; sort/partition: 2^27)")
+    p.add_argument("--n-total", type=int, default=None,
+                   help="join: tuples per relation over ALL GPUs (strong scaling: each "
+                        "GPU gets n_total / N)")
+    p.add_argument("--width", type=int, default=None, choices=(8, 16),
+                   help="tuple bytes (join: 16 = the reference's KEY_8B build; "
+                        "sort/partition: 8 = the reference's default tuple)")
+    p.add_argument("--bits", type=int, default=10, help="partition: radix bits")
+    p.add_argument("--shift", type=int, default=0, help="partition: shift bits")
     p.add_argument("--dist", default="uniform", choices=("uniform", "zipf"))
     p.add_argument("--theta", type=float, default=0.75)
     p.add_argument("--fanout-bits", type=int, default=9)
-    p.add_argument("--cpu-n", type=int, default=64_000_000,
+    p.add_argument("--cpu-n", type=int, default=128_000_000,
                    help="tuples per relation of the bounded CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--check", action="store_true",
@@ -53,66 +64,107 @@ def parse():
 
 
 # --------------------------------------------------------------------------
-def alg_bytes_per_launch(name, n_rel, nR, nS, w):
+def alg_bytes_per_launch(name, n_rel, nR, nS, w, op="join"):
     """Algorithmic HBM bytes of one launch: a materialising
-    pass reads and writes every tuple once (2w), a histogram reads once (w)."""
+    pass reads and writes every tuple once (2w), a histogram reads once (w).
+    The join's tile and group passes take R and S in one launch; a sort's
+    take its one relation."""
+    both = (nR + nS) if op == "join" else n_rel
     return {
         "k_hist": n_rel * w,                 # one relation per launch
         "k_scatter": 2 * n_rel * w,          # one relation per launch
-        "k_tilepass": 2 * (nR + nS) * w,     # R and S in one launch
-        "k_groupsort": 2 * (nR + nS) * w,    # R and S in one launch
+        "k_tilepass": 2 * both * w,
+        "k_groupsort": 2 * both * w,
     }.get(name)
 
 
-def cpu_baseline(width, n):
-    """Reference m-way join on the host cores (oracle/_ref/cpu_baseline*)."""
-    exe = os.path.join(ROOT, "oracle", "_ref", f"cpu_baseline{width}")
-    threads = 1
-    cores = os.cpu_count() or 1
-    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or cores
-    cores = min(cores, cap)
-    while threads * 2 <= cores and threads * 2 <= 1024:
-        threads *= 2
-    if os.path.exists(exe):
-        try:
-            r = subprocess.run([exe, str(n), str(n), str(threads), "128"],
-                               capture_output=True, text=True, timeout=600,
-                               cwd="/tmp")
-            m = re.search(r"SMJ_CPU_BASELINE (\{.*\})", r.stdout)
-            if m:
-                d = json.loads(m.group(1))
-                t = d["seconds"]
-                m2 = re.search(r"TOTAL-TIME-USECS = ([0-9.]+)", r.stderr)
-                if m2:  # the reference's own timer (joincommon.c:214-227)
-                    t = float(m2.group(1)) * 1e-6
-                ok = d["count"] == n
-                return {"value": round(2 * n / t / 1e6, 3), "unit": "Mtuples/s",
-                        "cores": threads, "kind": "reference",
-                        "sample": f"sortmergejoin_multiway {n}x{n} {width}B tuples, "
-                                  f"{threads} threads, PK/FK uniform, "
-                                  f"{'scalar' if width == 16 else 'AVX'} path, "
-                                  f"count {'ok' if ok else 'MISMATCH'}"}
-        except Exception as e:  # pragma: no cover
-            print(f"[bench] reference CPU baseline failed: {e}", file=sys.stderr)
-    # fall back to the single-threaded C restatement
-    import numpy as np
-    import oracle
+def _ref_exe(name):
+    """A reference binary built by oracle/build_ref.sh (shipped in-tree).  The
+    CPU baseline is the reference itself: no silent fallback."""
+    exe = os.path.join(ROOT, "oracle", "_ref", name)
+    if not os.path.exists(exe):
+        raise FileNotFoundError(
+            f"{exe} missing: run oracle/build_ref.sh where /root/reference exists "
+            "(or pass --no-cpu-baseline)")
+    return exe
+
+
+def host_cores():
+    """(threads this job may use, cores lscpu reports for the whole host)."""
+    share = os.cpu_count() or 1
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if cap:
+        share = min(share, cap)
+    lscpu = None
     try:
-        orc = oracle.Oracle(width)
-    except FileNotFoundError:
-        oracle.build()
-        orc = oracle.Oracle(width)
-    m = min(n, 8_000_000)
-    orc.seed(12345)
-    R = orc.create_relation_mway(m, m)
-    orc.seed(54321)
-    S = orc.create_relation_mway(m, m)
-    t0 = time.time()
-    c, _, _ = orc.sortmergejoin(R, S)
-    t = time.time() - t0
-    return {"value": round(2 * m / t / 1e6, 3), "unit": "Mtuples/s", "cores": 1,
-            "kind": "port", "sample": f"oracle restatement {m}x{m} {width}B tuples, "
-                                      f"count {'ok' if c == m else 'MISMATCH'}"}
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=30).stdout
+        per = re.search(r"Core\(s\) per socket:\s+(\d+)", out)
+        sock = re.search(r"Socket\(s\):\s+(\d+)", out)
+        if per and sock:
+            lscpu = int(per.group(1)) * int(sock.group(1))
+    except Exception:  # pragma: no cover
+        pass
+    return share, lscpu
+
+
+def _join_once(exe, n, threads):
+    r = subprocess.run([exe, str(n), str(n), str(threads), "128"],
+                       capture_output=True, text=True, timeout=900, cwd="/tmp")
+    m = re.search(r"SMJ_CPU_BASELINE (\{.*\})", r.stdout)
+    if not m:
+        raise RuntimeError(f"{exe} printed no result (rc {r.returncode}): {r.stderr[-400:]}")
+    d = json.loads(m.group(1))
+    t = d["seconds"]
+    m2 = re.search(r"TOTAL-TIME-USECS = ([0-9.]+)", r.stderr)
+    if m2:  # the reference's own timer (joincommon.c:214-227)
+        t = float(m2.group(1)) * 1e-6
+    return t, d["count"] == n
+
+
+def cpu_baseline(width, n):
+    """The reference m-way join (oracle/_ref/cpu_baseline*: compiled from the
+    reference's sources) on this host: T = the largest power of two within
+    the job's CPU share, and T = 1.  16-byte tuples take the
+    reference's scalar path, 8-byte tuples its AVX path."""
+    exe = _ref_exe(f"cpu_baseline{width}")
+    share, lscpu = host_cores()
+    threads = 1
+    while threads * 2 <= share and threads * 2 <= 1024:
+        threads *= 2
+    t, ok = _join_once(exe, n, threads)
+    # T = 1 on a quarter of the sample (a 128M single-thread run alone takes
+    # about 40 s with its generation)
+    n1 = max(n // 4, 1)
+    t1, ok1 = _join_once(exe, n1, 1)
+    path = "scalar" if width == 16 else "AVX"
+    return {"value": round(2 * n / t / 1e6, 3), "unit": "Mtuples/s",
+            "cores": threads, "kind": "reference",
+            "host_cores_lscpu": lscpu,
+            "t1_value": round(2 * n1 / t1 / 1e6, 3),
+            "sample": f"sortmergejoin_multiway {n}x{n} {width}B tuples, {threads} threads "
+                      f"(t1_value: 1 thread on {n1}x{n1}), PK/FK uniform, {path} path, "
+                      f"count {'ok' if ok and ok1 else 'MISMATCH'}"}
+
+
+def cpu_baseline_op(op, width, n, bits, shift):
+    """The reference's single-core partition_relation_optimized / avxsort_tuples
+    (oracle/_ref/cpu_baseline_ops*) on create_relation_pk(n), seed 12345."""
+    exe = _ref_exe(f"cpu_baseline_ops{width}")
+    args = [exe, op, str(n)] + ([str(bits), str(shift)] if op == "partition" else [])
+    r = subprocess.run(args, capture_output=True, text=True, timeout=900, cwd="/tmp")
+    m = re.search(r"SMJ_CPU_OPS (\{.*\})", r.stdout)
+    if not m:
+        raise RuntimeError(f"{exe} printed no result (rc {r.returncode}): {r.stderr[-400:]}")
+    d = json.loads(m.group(1))
+    _, lscpu = host_cores()
+    what = (f"partition_relation_optimized {n} tuples, {bits} bits, shift {shift}"
+            if op == "partition" else
+            f"{'avxsort_tuples' if width == 8 else 'scalarsort_tuples'} {n} tuples")
+    return {"value": round(n / d["seconds"] / 1e6, 3), "unit": "Mtuples/s", "cores": 1,
+            "kind": "reference", "host_cores_lscpu": lscpu,
+            "sample": f"{what}, {width}B tuples, create_relation_pk seed 12345, "
+                      f"single core (as the reference bench), "
+                      f"{'ok' if d['ok'] else 'FAILED'}"}
 
 
 def load_traffic(kernel, cfg_key):
@@ -145,7 +197,11 @@ def main():
         print(f"[bench] --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     torch.cuda.set_device(local)
     dist = None
-    exchange = N > 1 or a.exchange_path
+    exchange = a.op == "join" and (N > 1 or a.exchange_path)
+    if a.op != "join" and N > 1:  # replicas: a process group for the barrier and max
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     if exchange:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -155,11 +211,24 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import smj
+    if a.width is None:
+        a.width = 16 if a.op == "join" else 8
+    if a.n is None:
+        a.n = 128_000_000 if a.op == "join" else 1 << 27
     lib = smj.load(a.width)
+    if a.op != "join":
+        run_op(a, lib, json_out, dist, N, rank)
+        return
     w = a.width
-    n = a.n
-    total = n * N
-    first = n * rank
+    if a.n_total is not None:  # strong scaling: the total is fixed
+        total = a.n_total
+        base = total // N
+        first = base * rank
+        n = base if rank < N - 1 else total - base * (N - 1)
+    else:  # weak scaling: n per GPU
+        n = a.n
+        total = n * N
+        first = n * rank
     R = lib.empty(n)
     S = lib.empty(n)
     lib.dev_gen_pk(R, first, total, 12345)
@@ -182,27 +251,11 @@ def main():
         def step():
             dj.step(R, S, count)
 
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    if exchange:
-        dj.stats_reset()
-    lib.trace(True)
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kern = lib.trace_read()
-    lib.trace(False)
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    def reset():
+        if exchange:
+            dj.stats_reset()
+
+    elapsed, kern = timed_loop(a, lib, dist, step, reset)
 
     xchg = None
     if exchange:
@@ -228,32 +281,15 @@ def main():
             dist.destroy_process_group()
         return
 
-    # dominant kernel roofline (this rank's trace over the timed region)
-    best = None
-    for name, (ms, launches) in kern.items():
-        nrel = n if N == 1 else None
-        b = alg_bytes_per_launch(name, n, n, n, w)
-        if b is None:
-            continue
-        if best is None or ms > best[1]:
-            best = (name, ms, launches, b)
-    roof = None
-    if best:
-        name, ms, launches, b = best
-        avg_s = ms / launches / 1e3
-        ach = b / avg_s / 1e9
-        cfg_key = f"n{n}_w{w}_{a.dist}"
-        tr = load_traffic(name, cfg_key)
-        roof = {"bound": "hbm", "kernel": name, "achieved": round(ach, 1),
-                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                "traffic": tr, "alg_bytes_per_launch": b,
-                "avg_launch_ms": round(ms / launches, 4)}
+    roof = dominant_roofline(kern, lambda name: alg_bytes_per_launch(name, n, n, n, w),
+                             f"n{n}_w{w}_{a.dist}")
     pipeline_gbs = 5 * 2 * total * w / (elapsed / a.steps) / 1e9
 
     cpu = None
     if N == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(w, a.cpu_n)
 
+    strong = a.n_total is not None
     out = {
         "metric": "join throughput Mtuples/s (R⋈S) + achieved HBM GB/s, 128M⋈128M at 1/2/4/8 GPU",
         "value": round(value, 2),
@@ -263,15 +299,18 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(ms_step, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "int64" if w == 16 else "int32",
         "data": "synthetic",
-        "config": {"workload": f"sortmergejoin_multiway R={n} S={n} per GPU, "
-                               f"{w}-byte tuples, {a.dist}"
+        "config": {"workload": (f"sortmergejoin_multiway R={total} S={total} over {N} GPU(s)"
+                                if strong else
+                                f"sortmergejoin_multiway R={n} S={n} per GPU")
+                               + f", {w}-byte tuples, {a.dist}"
                                + (f" theta={a.theta}" if a.dist == "zipf" else "")
                                + ", PK/FK keys 1..|R|",
-                   "tuples_per_relation_per_gpu": n, "tuple_bytes": w,
+                   "tuples_per_relation_per_gpu": n, "tuples_per_relation_total": total,
+                   "tuple_bytes": w,
                    "distribution": a.dist, "parallelism": f"range-partition x{N}"},
         "roofline": roof,
         "cpu_baseline": cpu,
@@ -287,6 +326,132 @@ def main():
         },
     }
     print(json.dumps(out), file=json_out, flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def timed_loop(a, lib, dist, step, reset=None):
+    """W untimed warm-up steps, then exactly K steps between a barrier +
+    synchronize on both sides; returns (max-over-ranks seconds, kernel trace)."""
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    if reset:
+        reset()
+    lib.trace(True)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern = lib.trace_read()
+    lib.trace(False)
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, kern
+
+
+def dominant_roofline(kern, bytes_of, cfg_key):
+    """Roofline of the kernel with the largest summed time over the timed
+    region: its algorithmic bytes per launch / its average launch time (HIP
+    events on the library's stream), plus the PMC traffic when profiled."""
+    best = None
+    for name, (ms, launches) in kern.items():
+        b = bytes_of(name)
+        if b is None:
+            continue
+        if best is None or ms > best[1]:
+            best = (name, ms, launches, b)
+    if not best:
+        return None
+    name, ms, launches, b = best
+    ach = b / (ms / launches / 1e3) / 1e9
+    return {"bound": "hbm", "kernel": name, "achieved": round(ach, 1),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+            "traffic": load_traffic(name, cfg_key), "alg_bytes_per_launch": b,
+            "avg_launch_ms": round(ms / launches, 4)}
+
+
+def run_op(a, lib, json_out, dist, N, rank):
+    """bench_sort / bench_partitioning on the device (BASELINE configs 2 and
+    3): one step = one smj_dev_sort (avxsort_tuples' device form) or one
+    smj_dev_partition (partition_relation_optimized: stable, 64-byte padded)
+    over a device-resident relation of n tuples, keys 1..n permuted (the
+    shape of create_relation_pk), payload 0.  N GPUs run N independent
+    replicas (the ops do not shard across GPUs: scaling "weak")."""
+    w, n = a.width, a.n
+    R = lib.empty(n)
+    lib.dev_gen_pk(R, 0, n, 12345, with_payload=False)
+    if a.op == "sort":
+        out = lib.empty(n)
+
+        def step():
+            lib.dev_sort(R, out)
+    else:
+        fan = 1 << a.bits
+        out = lib.empty(n + fan * 64 // w)
+        hist = torch.zeros(fan, dtype=torch.int64, device="cuda")
+        off = torch.zeros_like(hist)
+
+        def step():
+            lib.dev_partition(R, out, a.bits, a.shift, True, hist, off)
+    torch.cuda.synchronize()
+    elapsed, kern = timed_loop(a, lib, dist, step)
+    if a.op == "sort":
+        keys = out[:, 1]
+        ok = bool((keys[1:] >= keys[:-1]).all().item()) if n > 1 else True
+    else:
+        ok = int(hist.sum().item()) == n
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+    ms_step = elapsed / a.steps * 1e3
+    value = N * n / (elapsed / a.steps) / 1e6
+    roof = dominant_roofline(kern, lambda name: alg_bytes_per_launch(name, n, n, 0, w, a.op),
+                             f"{a.op}_n{n}_w{w}")
+    alg = 2 * n * w  # SURVEY.md §8(d): 2·N·w for bench_sort and bench_partitioning
+    cpu = None
+    if N == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline_op(a.op, w, n, a.bits, a.shift)
+    ref = ("src/bench/sortbench.c:85-202 (avxsort_tuples)" if a.op == "sort" else
+           "src/bench/partitioningbench.c:128-196 (partition_relation_optimized)")
+    out_line = {
+        "metric": (f"bench_sort throughput Mtuples/s + achieved HBM GB/s (2·N·w)" if a.op == "sort"
+                   else "bench_partitioning throughput Mtuples/s + achieved HBM GB/s (2·N·w)"),
+        "value": round(value, 2),
+        "unit": "Mtuples/s",
+        "n_gpus": N,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int64" if w == 16 else "int32",
+        "data": "synthetic",
+        "config": {"workload": (f"{a.op} of {n} {w}-byte tuples" +
+                                (f", {a.bits} radix bits, shift {a.shift}, 64-byte padded, stable"
+                                 if a.op == "partition" else ", full (key, payload) order")
+                                + ", keys 1..N permuted, payload 0; reference " + ref),
+                   "tuples": n, "tuple_bytes": w, "parallelism": f"replicas x{N}"},
+        "roofline": roof,
+        "cpu_baseline": cpu,
+        "result_ok": ok,
+        "detail": {
+            "alg_GBps_2Nw": round(alg / (elapsed / a.steps) / 1e9, 1),
+            "alg_frac_2Nw": round(alg / (elapsed / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
+            "kernels_ms_per_step": {k: round(v[0] / a.steps, 4) for k, v in kern.items()},
+            "device": lib.lib.smj_device_name().decode(),
+        },
+    }
+    print(json.dumps(out_line), file=json_out, flush=True)
     if dist:
         dist.destroy_process_group()
 

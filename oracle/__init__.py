@@ -114,6 +114,12 @@ class Oracle(_Lib):
         self.fn("sort_tuples", None, _P, _I64)(_ptr(a), len(a))
         return a
 
+    def sort_radix(self, t: np.ndarray) -> np.ndarray:
+        """sort()'s order by a stable LSD radix sort (the full-size checker)."""
+        a = np.ascontiguousarray(t).copy()
+        self.fn("sort_tuples_radix", None, _P, _I64)(_ptr(a), len(a))
+        return a
+
     def sort_int64(self, a: np.ndarray) -> np.ndarray:
         b = np.ascontiguousarray(a, dtype=np.int64).copy()
         self.fn("sort_int64", None, _P, _I64)(_ptr(b), len(b))

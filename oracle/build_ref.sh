@@ -47,6 +47,8 @@ for w in 8 16; do
     $CXX -shared -Wl,-Bsymbolic $objs "$objdir/ref_shim.o" -o "$HERE/_ref/libref$w.so" -lpthread -lm
     $CXX -O2 $def $INC -c "$HERE/cpu_baseline.cpp" -o "$objdir/cpu_baseline.o" -w
     $CXX $objs "$objdir/cpu_baseline.o" -o "$HERE/_ref/cpu_baseline$w" -lpthread -lm
+    $CXX -O2 $def $INC -c "$HERE/cpu_baseline_ops.cpp" -o "$objdir/cpu_baseline_ops.o" -w
+    $CXX $objs "$objdir/cpu_baseline_ops.o" -o "$HERE/_ref/cpu_baseline_ops$w" -lpthread -lm
     # the reference's own driver (src/main.c) on the reference objects: the
     # A side of tests/test_dropin.py's A/B run against oracle/_ref/dropin/
     for f in $S/joins/sortmergejoin_multipass.c $S/joins/sortmergejoin_mpsm.c $S/main.c; do

@@ -119,6 +119,8 @@ def _worker(rank, world, port, n, q, s_payload="negative"):
         # negative S payloads cannot be packed: R goes packed first, then both
         # as tuples; non-negative ones: both relations travel as packed words
         S["payload"] = -np.arange(total) if s_payload == "negative" else np.arange(total)
+        if s_payload == "r_negative":  # R cannot be packed, S can
+            R["payload"] = -np.arange(total)
         expect = orc.merge_join(np.sort(R, order="key"), np.sort(S, order="key"))
 
         def rows(t):
@@ -157,12 +159,13 @@ def _free_port():
 
 @pytest.mark.parametrize("world,chunk_mb,s_payload", [
     (2, None, "negative"), (3, None, "negative"), (2, 0, "negative"), (3, 0, "rowid"),
-    (2, None, "rowid"), (3, None, "rowid")])
+    (2, None, "rowid"), (3, None, "rowid"), (2, None, "r_negative"), (3, None, "r_negative")])
 def test_distributed_join_gloo(world, chunk_mb, s_payload, oracles, monkeypatch):
     """chunk_mb 0: every row message over the chunk limit, so the exchange
     takes the chunked isend/irecv path (the one RCCL needs for >1.6 GB).
     s_payload "rowid": both relations exchanged as packed words; "negative":
-    S cannot be packed, every rank falls back to tuples for both."""
+    S cannot be packed, every rank falls back to tuples for both; "r_negative":
+    R cannot be packed but S can (S goes again, as tuples)."""
     if chunk_mb is not None:
         monkeypatch.setenv("SMJ_A2A_CHUNK_MB", str(chunk_mb))
     ctx = mp.get_context("spawn")
@@ -197,3 +200,30 @@ def test_owners_and_send_counts():
     h = torch.arange(8)
     assert send_counts(h, 2).tolist() == [6, 22]
     assert send_counts(h, 3).tolist() == [3, 12, 13]
+
+
+def test_local_range_int64_edges():
+    """Every rank's local plan has the global partition width (its buckets
+    ARE the exchanged partitions) and stays inside int64, also for key
+    ranges that reach INT64_MIN / INT64_MAX."""
+    import sys
+    sys.path.insert(0, PKG)
+    from smj.dist import INT64_MAX, local_range, owned, plan_shift
+    lo64 = -(1 << 63)
+    cases = [(1, 128_000_000), (lo64, INT64_MAX), (1, (1 << 62) + 1), (lo64, 5),
+             (INT64_MAX - 1000, INT64_MAX), (7, 7)]
+    for kmin, kmax in cases:
+        for pbits, world in ((9, 1), (10, 2), (11, 3), (11, 8), (4, 5)):
+            base, s1 = None, None
+            for rank in range(world):
+                b, klo, khi, lbits = local_range(kmin, kmax, pbits, world, rank)
+                assert base is None or b == base  # one base on every rank
+                base = b
+                assert b <= kmin and lo64 <= klo <= khi <= INT64_MAX
+                gs1 = plan_shift(b, kmax, pbits)
+                assert plan_shift(klo, khi, lbits) == gs1  # same partition width
+                p_lo, p_hi = owned(1 << pbits, world, rank)
+                if (p_lo << gs1) < (1 << max(kmax - kmin, 0).bit_length()):
+                    assert klo == b + (p_lo << gs1)
+                assert (1 << lbits) >= p_hi - p_lo
+            assert kmax - base < (1 << max(kmax - kmin, 0).bit_length())

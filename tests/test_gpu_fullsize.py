@@ -1,0 +1,106 @@
+"""BASELINE configs at their full sizes, bit-compared with the oracle
+restatement (oracle/smj_oracle.c, pinned to the reference by tests/golden/):
+
+* bench_sort on 1 MI355X: 2^27 tuples through smj_dev_sort (the device form of
+  avxsort_tuples, src/bench/sortbench.c:85-202);
+* bench_partitioning on 1 MI355X: 2^27 tuples, 10 radix bits, shift 0,
+  through smj_dev_partition (partition_relation_optimized: stable, 64-byte
+  padded, src/bench/partitioningbench.c:128-196);
+* sortmergejoin_multiway 128M x 128M: sorted R, sorted S and the count.
+
+Inputs come from the device generators (keys 1..N permuted, the shape of
+create_relation_pk) and are copied to the host for the oracle.  The oracle's
+sorts are its stable LSD radix sort (orc_sort_tuples_radix, checked against
+the qsort restatement in tests/test_oracle.py); the join's two run on two host
+threads (ctypes drops the GIL).
+"""
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+
+N27 = 1 << 27
+
+
+def _free(torch):
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("payload", [False, True], ids=["payload0", "payload"])
+def test_bench_sort_full(libs, oracles, width, payload):
+    import torch
+    lib, orc = libs[width], oracles[width]
+    R = lib.empty(N27)
+    # bench_sort leaves the payload 0 (create_relation_pk); the second case
+    # carries payloads 5+i so that the (key, payload) order is exercised too
+    lib.dev_gen_pk(R, 0, N27, 12345, with_payload=payload)
+    out = lib.empty(N27)
+    lib.dev_sort(R, out)
+    torch.cuda.synchronize()
+    host_in = lib.to_host(R)
+    got = lib.to_host(out)
+    del R, out
+    _free(torch)
+    want = orc.sort_radix(host_in)
+    np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("bits,shift", [(10, 0), (10, 7)])
+def test_bench_partition_full(libs, oracles, width, bits, shift):
+    import torch
+    lib, orc = libs[width], oracles[width]
+    fan = 1 << bits
+    R = lib.empty(N27)
+    lib.dev_gen_pk(R, 0, N27, 12345, with_payload=True)
+    out = lib.empty(N27 + fan * 64 // width)
+    hist = torch.zeros(fan, dtype=torch.int64, device="cuda")
+    off = torch.zeros_like(hist)
+    lib.dev_partition(R, out, bits, shift, True, hist, off)
+    torch.cuda.synchronize()
+    host_in = lib.to_host(R)
+    got = lib.to_host(out)
+    cnt, offs = hist.cpu().numpy(), off.cpu().numpy()
+    del R, out
+    _free(torch)
+    want, wcnt, woff = orc.partition(host_in, bits, shift, True)
+    np.testing.assert_array_equal(cnt, wcnt)
+    np.testing.assert_array_equal(offs, woff)
+    # every partition's tuples, in order (the padding between them is unset)
+    mask = np.zeros(len(want), bool)
+    for o, c in zip(woff.tolist(), wcnt.tolist()):
+        mask[o:o + c] = True
+    np.testing.assert_array_equal(got[:len(want)][mask], want[mask])
+
+
+@pytest.mark.parametrize("dist_", ["uniform", "zipf"])
+def test_headline_join_full_bitexact(libs, oracles, width, dist_):
+    """BASELINE configs[3] (R = S = 128M): the device join's sorted R, sorted S
+    and count against the oracle's sortmergejoin on the same inputs."""
+    import torch
+    lib, orc = libs[width], oracles[width]
+    n = 128_000_000
+    R, S = lib.empty(n), lib.empty(n)
+    lib.dev_gen_pk(R, 0, n, 12345)
+    if dist_ == "uniform":
+        lib.dev_gen_fk(S, 0, n, n, 54321)
+    else:
+        lib.dev_gen_zipf(S, 0, n, 0.75, 54321)
+    sR, sS = lib.empty(n), lib.empty(n)
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    lib.dev_join(R, S, sR, sS, cnt, 9, 1, n)
+    torch.cuda.synchronize()
+    count = int(cnt.item())
+    hR, hS = lib.to_host(R), lib.to_host(S)
+    gR, gS = lib.to_host(sR), lib.to_host(sS)
+    del R, S, sR, sS
+    _free(torch)
+    with ThreadPoolExecutor(2) as ex:
+        fR = ex.submit(orc.sort_radix, hR)
+        fS = ex.submit(orc.sort_radix, hS)
+        wR, wS = fR.result(), fS.result()
+    assert count == orc.merge_join(wR, wS) == n
+    np.testing.assert_array_equal(gR, wR)
+    np.testing.assert_array_equal(gS, wS)

@@ -77,6 +77,29 @@ def test_sort(case, n):
     same_order(w, orc.sort(g[f"sort_in_{n}"]), g[f"sort_out_{n}"])
 
 
+@pytest.mark.parametrize("n", SORT_NS)
+def test_sort_radix_golden(case, n):
+    """The full-size checker (LSD radix) on the reference's sort vectors."""
+    w, orc, g = case
+    same_order(w, orc.sort_radix(g[f"sort_in_{n}"]), g[f"sort_out_{n}"])
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_sort_radix_matches_sort(case, seed):
+    """sort_radix == sort (qsort on tup_cmp) bit for bit: signed keys and
+    payloads, heavy duplicates, both halves of the words varying."""
+    w, orc, _ = case
+    rng = np.random.default_rng(seed)
+    n = 200_003
+    t = np.zeros(n, orc.dtype)
+    info = np.iinfo(t["key"].dtype)
+    t["key"] = rng.integers(info.min, info.max, n, endpoint=True)
+    t["key"][: n // 2] = rng.integers(-50, 50, n // 2)
+    t["payload"] = rng.integers(info.min, info.max, n, endpoint=True)
+    t["payload"][n // 3:] = rng.integers(-3, 3, n - n // 3)
+    np.testing.assert_array_equal(orc.sort_radix(t), orc.sort(t))
+
+
 def test_merge(case):
     w, orc, g = case
     same_order(w, orc.merge(g["merge_a"], g["merge_b"]), g["merge_out"])
