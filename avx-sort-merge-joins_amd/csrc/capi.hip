@@ -1300,6 +1300,10 @@ int smj_dev_partition_range_packed(smj_workspace* wsp, const tuple_t* in, uint64
 #endif
 }
 
+uint64_t smj_selfcheck_lds_order(smj_workspace* ws, smj_stream_t stream) {
+    return lds_order_selfcheck((Workspace*)ws, (hipStream_t)stream);
+}
+
 void smj_trace_enable(smj_workspace* wsp, int on) {
     ((Workspace*)wsp)->trace_on = on != 0;
 }

@@ -23,6 +23,7 @@
 // Digits wider than 12 bits are done as two stable LSD passes plus a
 // padding copy (stable_partition below).
 #include <stdlib.h>
+#include <string.h>
 
 #include "smj_common.hpp"
 #include "smj_internal.hpp"
@@ -449,6 +450,250 @@ k_scatter_swc(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
         const uint32_t d = q / CW, j = q % CW;
         if (j < kc[d]) out[run[d] + j] = carry[q];
     }
+}
+
+// ---------------------------------------------------------------------------
+// Stable scatter with write combining and ATOMIC ranks (partition_relation
+// [_optimized] for 1..10 radix bits; src/partition/partition.c:152-219).
+//
+// Ranks: a wave ranks its items step by step (item j of every lane = input
+// elements wbase + 64 j + lane, in input order) with one LDS atomic add per
+// element on a per-wave 16-bit digit counter (two digits per 32-bit word).
+// When several lanes of one ds_add_rtn instruction hit the same word, gfx950
+// returns their old values in lane order (tools/ldsorder.hip: 0 violations in
+// ~1.6e10 colliding lane updates; tests/test_gpu_parity.py re-checks it
+// through smj_selfcheck_lds_order), so the returned count is the element's
+// stable rank inside the wave -- one LDS op per element instead of one ballot
+// per digit bit.  Per-wave counts -> tile offsets by the owner of each digit
+// pair (thread t owns digits 2t, 2t+1) and one packed scan.
+//
+// Writes: each digit's output region of this workgroup is emitted in whole
+// aligned 64-byte segments, SEG consecutive lanes per segment; the tail of a
+// tile that does not fill a segment stays in an LDS carry and leads the
+// digit's next segment (the reference's cache-line write-combining buffers,
+// src/partition/partition.c:38-46).  Only the region's first and last segment
+// are partial.
+//
+// MI355X, 2^27 tuples, 10 bits (tools/partlab.hip): 8 B 0.73 ms, 16 B 1.14 ms
+// for this scatter, against 1.46 / 1.51 ms for k_scatter_swc (ballot ranks)
+// and 0.84 ms for the same atomic ranks without the carry (34 % extra write
+// bytes, 41 % partial write requests).
+template <int THREADS, int ITEMS>
+struct SwaGeom {
+    static constexpr int W = THREADS / 64;
+    static constexpr int TILE = THREADS * ITEMS;
+    static constexpr uint32_t SEG = 64 / sizeof(Tup);
+    static constexpr uint32_t CW = SEG - 1;
+    // stage Tup[TILE] | carry Tup[B][CW] | counters u32[W][B/2] | info u32x4[B] |
+    // segown u16[TILE/SEG + 2B] | scan scratch
+    static __host__ __device__ constexpr size_t lds_bytes(uint32_t B) {
+        return (size_t)TILE * sizeof(Tup) + (size_t)B * CW * sizeof(Tup) + (size_t)W * B * 2 +
+               (size_t)B * 16 + ((size_t)(TILE / SEG + 2 * B) * 2 + 15) / 16 * 16 + 128;
+    }
+};
+
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+template <int THREADS, int ITEMS, class Digit>
+__global__ void __launch_bounds__(THREADS)
+k_scatter_swa(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_arg,
+              uint32_t nbins, const uint32_t* __restrict__ counts, uint32_t nwg,
+              const uint64_t* __restrict__ starts, Tup* __restrict__ out) {
+    typedef SwaGeom<THREADS, ITEMS> G;
+    constexpr int W = G::W;
+    constexpr int TILE = G::TILE;
+    constexpr uint32_t SEG = G::SEG;
+    constexpr uint32_t CW = G::CW;
+    const auto dig = dig_arg.load();
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    Tup* stage = reinterpret_cast<Tup*>(lds_raw);
+    Tup* carry = stage + TILE;
+    uint32_t* w32 = reinterpret_cast<uint32_t*>(carry + (size_t)nbins * CW);
+    const uint32_t hb = nbins / 2;
+    u32x4_t* info = reinterpret_cast<u32x4_t*>(w32 + (size_t)W * hb);
+    uint16_t* segown = reinterpret_cast<uint16_t*>(info + nbins);
+    uint32_t* scr = reinterpret_cast<uint32_t*>(
+        (reinterpret_cast<uintptr_t>(segown + (TILE / SEG + 2 * nbins)) + 15) & ~uintptr_t(15));
+
+    const int lane = lane_id();
+    const int wid = threadIdx.x >> 6;
+    const uint32_t t2 = threadIdx.x;
+    const bool owner = t2 < hb;
+    // the owner's state of digits 2 t2 and 2 t2 + 1: output cursor, carry size
+    uint32_t pos[2] = {0, 0}, kc[2] = {0, 0};
+    if (owner) {
+#pragma unroll
+        for (int h = 0; h < 2; h++)
+            pos[h] = (uint32_t)(starts[2 * t2 + h] +
+                                counts[(uint64_t)(2 * t2 + h) * nwg + blockIdx.x]);
+    }
+    for (uint32_t q = threadIdx.x; q < W * hb; q += THREADS) w32[q] = 0;
+    const uint64_t beg = (uint64_t)blockIdx.x * chunk;
+    const uint64_t end = min(beg + chunk, n);
+    const uint32_t wbase = wid * 64 * ITEMS;
+    Tup v[ITEMS], nv[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; j++) {
+        const uint64_t i = beg + wbase + j * 64 + lane;
+        if (i < end) v[j] = in[i];
+    }
+    __syncthreads();
+    for (uint64_t base = beg; base < end; base += TILE) {
+        const uint32_t tcount = (uint32_t)min((uint64_t)TILE, end - base);
+        // ---- ranks (lane-ordered atomics, see the header)
+        uint32_t dg[ITEMS], rk[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const bool valid = wbase + j * 64 + lane < tcount;
+            dg[j] = valid ? dig(v[j]) : 0xffffffffu;
+            const uint32_t d = valid ? dg[j] : 0;
+            const uint32_t sh = (d & 1u) * 16u;
+            uint32_t old = 0;
+            if (valid) old = atomicAdd(&w32[wid * hb + (d >> 1)], 1u << sh);
+            rk[j] = (old >> sh) & 0xffffu;
+        }
+        __syncthreads();
+        // ---- owner: tile counts, emission sizes (up to the last segment
+        // boundary of carry + tile), stage offsets and segment numbers in one
+        // packed scan (both sums stay below 2^16)
+        uint32_t cw[W];
+        uint32_t c[2] = {0, 0}, E[2] = {0, 0}, ns[2] = {0, 0};
+        if (owner) {
+#pragma unroll
+            for (int w = 0; w < W; w++) {
+                cw[w] = w32[w * hb + t2];
+                c[0] += cw[w] & 0xffffu;
+                c[1] += cw[w] >> 16;
+            }
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const uint32_t T = kc[h] + c[h];
+                const uint32_t m = (pos[h] + T) % SEG;
+                E[h] = m <= T ? T - m : 0u;
+                ns[h] = E[h] ? (pos[h] + E[h]) / SEG - pos[h] / SEG : 0u;
+            }
+        }
+        uint32_t tot;
+        const uint32_t ex =
+            block_exclusive_scan((c[0] + c[1]) | ((ns[0] + ns[1]) << 16), scr, &tot);
+        const uint32_t nsegT = tot >> 16;
+        uint32_t ts[2] = {0, 0};
+        if (owner) {
+            ts[0] = ex & 0xffffu;
+            ts[1] = ts[0] + c[0];
+            const uint32_t sp[2] = {ex >> 16, (ex >> 16) + ns[0]};
+            uint32_t o0 = ts[0], o1 = ts[1];
+#pragma unroll
+            for (int w = 0; w < W; w++) {
+                const uint32_t x = cw[w];
+                w32[w * hb + t2] = o0 | (o1 << 16);
+                o0 += x & 0xffffu;
+                o1 += x >> 16;
+            }
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const uint32_t d = 2 * t2 + h;
+                u32x4_t I;
+                I[0] = pos[h];
+                I[1] = E[h];
+                I[2] = ts[h];
+                I[3] = sp[h] | (kc[h] << 16);
+                info[d] = I;
+                for (uint32_t k = 0; k < ns[h]; k++) segown[sp[h] + k] = (uint16_t)d;
+            }
+        }
+        // prefetch the next tile
+        const uint64_t nb = base + TILE;
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint64_t i = nb + wbase + j * 64 + lane;
+            if (i < end) nv[j] = in[i];
+        }
+        __syncthreads();
+        // ---- stage the tile in digit order
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++)
+            if (dg[j] != 0xffffffffu) {
+                const uint32_t d = dg[j];
+                const uint32_t wo = (w32[wid * hb + (d >> 1)] >> ((d & 1u) * 16u)) & 0xffffu;
+                stage[wo + rk[j]] = v[j];
+            }
+        __syncthreads();
+        // ---- whole aligned segments, SEG consecutive lanes each; element e
+        // of a digit's emission is its carry (e < kc) or its staged run
+        if (owner) {
+#pragma unroll
+            for (int w = 0; w < W; w++) w32[w * hb + t2] = 0;
+        }
+        for (uint32_t q = threadIdx.x; q < nsegT * SEG; q += THREADS) {
+            const uint32_t sg = q / SEG;
+            const uint32_t d = segown[sg];
+            const u32x4_t I = info[d];
+            const uint32_t p = I[0];
+            const uint32_t addr = (p / SEG + (sg - (I[3] & 0xffffu))) * SEG + q % SEG;
+            if (addr >= p && addr < p + I[1]) {
+                const uint32_t e = addr - p;
+                const uint32_t k = I[3] >> 16;
+                out[addr] = e < k ? carry[d * CW + e] : stage[I[2] + e - k];
+            }
+        }
+        __syncthreads();
+        // ---- owner: the leftovers (< SEG) become the carry
+        if (owner) {
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const uint32_t d = 2 * t2 + h;
+                const uint32_t T = kc[h] + c[h];
+                for (uint32_t e = E[h]; e < T; e++)
+                    carry[d * CW + (e - E[h])] =
+                        e < kc[h] ? carry[d * CW + e] : stage[ts[h] + e - kc[h]];
+                pos[h] += E[h];
+                kc[h] = T - E[h];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) v[j] = nv[j];
+    }
+    // ---- the partial last segment of every region
+    if (owner) {
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const uint32_t d = 2 * t2 + h;
+            for (uint32_t e = 0; e < kc[h]; e++) out[pos[h] + e] = carry[d * CW + e];
+        }
+    }
+}
+
+// Histogram of the stable write-combining partition: counts[d][wg] of each
+// workgroup's chunk (the scatter's chunking).  Loads are unconditional
+// (clamped to the chunk) so that every load of a tile is in flight at once.
+template <int THREADS, int ITEMS, class Digit>
+__global__ void __launch_bounds__(THREADS)
+k_hist_c(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_arg,
+         uint32_t nbins, uint32_t* __restrict__ counts, uint32_t nwg) {
+    const auto dig = dig_arg.load();
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_hc[];
+    for (uint32_t d = threadIdx.x; d < nbins; d += THREADS) lds_hc[d] = 0;
+    __syncthreads();
+    const uint64_t beg = (uint64_t)blockIdx.x * chunk;
+    const uint64_t end = min(beg + chunk, n);
+    constexpr int TILE = THREADS * ITEMS;
+    for (uint64_t base = beg; base < end; base += TILE) {
+        Tup v[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint64_t i = base + (uint64_t)j * THREADS + threadIdx.x;
+            v[j] = in[i < end ? i : end - 1];
+        }
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint64_t i = base + (uint64_t)j * THREADS + threadIdx.x;
+            if (i < end) atomicAdd(&lds_hc[dig(v[j])], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < nbins; d += THREADS)
+        counts[(uint64_t)d * nwg + blockIdx.x] = lds_hc[d];
 }
 
 // Unstable scatter for the join's level-1 partition (the join re-sorts every
@@ -1167,12 +1412,74 @@ static void stable_partition_t(Workspace* ws, const Tup* in, uint64_t n,
     SMJ_CHECK(hipGetLastError());
 }
 
+// ranks of the stable partition: lane-ordered LDS atomics (k_scatter_swa,
+// default) or ballot matching (k_scatter_swc: SMJ_STABLE_RANK=ballot)
+static bool atomic_ranks() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("SMJ_STABLE_RANK");
+        v = (e && !strcmp(e, "ballot")) ? 0 : 1;
+    }
+    return v != 0;
+}
+
+// histogram + scan + k_scatter_swa, one workgroup per CU (1 <= dbits <= 10)
+template <class Digit>
+static void stable_partition_swa(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
+                                 const Digit& dig, uint32_t dbits, int padded,
+                                 uint64_t* starts_dev, int64_t* hist_out, int64_t* off_out,
+                                 hipStream_t st) {
+    constexpr int THREADS = 512;
+    constexpr int ITEMS = sizeof(Tup) == 16 ? 8 : 16;
+    typedef SwaGeom<THREADS, ITEMS> G;
+    const uint32_t nbins = 1u << dbits;
+    uint64_t ntiles = (n + G::TILE - 1) / G::TILE;
+    if (ntiles == 0) ntiles = 1;
+    uint32_t nwg = (uint32_t)(ntiles < 256 ? ntiles : 256);
+    const uint64_t tiles_per_wg = (ntiles + nwg - 1) / nwg;
+    const uint64_t chunk = tiles_per_wg * G::TILE;
+    nwg = (uint32_t)((ntiles + tiles_per_wg - 1) / tiles_per_wg);
+    uint32_t* counts = (uint32_t*)ws->scratch("pt_counts", (size_t)nbins * nwg * 4);
+    uint64_t* totals = (uint64_t*)ws->scratch("pt_totals", (size_t)nbins * 8);
+    {
+        TraceScope ts(ws, "k_hist", st);
+        hipLaunchKernelGGL((k_hist_c<512, 16, Digit>), dim3(nwg), dim3(512),
+                           nbins * sizeof(uint32_t), st, in, n, chunk, dig, nbins, counts, nwg);
+    }
+    {
+        TraceScope ts(ws, "k_scan", st);
+        hipLaunchKernelGGL(k_scanrow, dim3(nbins), dim3(256), 0, st, counts, nwg, totals);
+        hipLaunchKernelGGL(k_scandig, dim3(1), dim3(256), 0, st, totals, nbins, padded,
+                           starts_dev, hist_out, off_out);
+    }
+    if (n == 0) return;
+    static bool attr = false;
+    if (!attr) {
+        SMJ_CHECK(hipFuncSetAttribute((const void*)k_scatter_swa<THREADS, ITEMS, Digit>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr = true;
+    }
+    TraceScope ts(ws, "k_scatter", st);
+    hipLaunchKernelGGL((k_scatter_swa<THREADS, ITEMS, Digit>), dim3(nwg), dim3(THREADS),
+                       G::lds_bytes(nbins), st, in, n, chunk, dig, nbins, counts, nwg,
+                       starts_dev, out);
+    SMJ_CHECK(hipGetLastError());
+}
+
 template <class Digit>
 static void stable_partition_narrow(Workspace* ws, const Tup* in, uint64_t n,
                                     Tup* out, const Digit& dig, uint32_t dbits,
                                     int padded, uint64_t* starts_dev,
                                     int64_t* hist_out, int64_t* off_out,
                                     hipStream_t st) {
+    // positions are 32-bit inside k_scatter_swa; its LDS holds 2^10 digits
+    typedef SwaGeom<512, sizeof(Tup) == 16 ? 8 : 16> SG;
+    if (atomic_ranks() && dbits >= 1 && dbits <= 10 && scatter_mode() == 0 &&
+        n + ((uint64_t)64 << dbits) < (1ull << 32) && SG::lds_bytes(1u << dbits) <= 160 * 1024) {
+        stable_partition_swa(ws, in, n, out, dig, dbits, padded, starts_dev, hist_out,
+                             off_out, st);
+        return;
+    }
     // the big tiles need the 16-bit per-wave counters and <= 160 KiB LDS
     const int v = dbits > 10 ? 0 : pt_variant();
     if (v == 2)
@@ -1452,6 +1759,50 @@ void sampled_partition(Workspace* ws, const Tup* in, uint64_t n, void* out,
     hipLaunchKernelGGL(k_regions_done, dim3(1), dim3(256), 0, st, seg_start, cursor,
                        cap_end, nbins, hist_out, seg_cnt, flag_dev);
     SMJ_CHECK(hipGetLastError());
+}
+
+// Self-check of the hardware property k_scatter_swa's ranks rely on: the old
+// values an LDS atomic add returns to lanes of one instruction that hit the
+// same word are in lane order.  Every wave draws digits from K values (many
+// collisions), compares each returned value with the ballot-matched
+// expectation and counts violations (must be 0).
+__global__ void __launch_bounds__(1024)
+k_lds_order(uint32_t K, uint32_t iters, unsigned long long* bad) {
+    __shared__ uint32_t ctr[16][64];
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
+    ctr[wid][lane] = 0;
+    __syncthreads();
+    const uint64_t lt = lanemask_lt();
+    unsigned long long nb = 0;
+    uint32_t h = blockIdx.x * 7919u + threadIdx.x * 104729u + K;
+    for (uint32_t it = 0; it < iters; it++) {
+        h = h * 1664525u + 1013904223u;
+        const uint32_t d = (h >> 8) % K;
+        uint64_t peers = ~0ull;
+        for (int b = 0; b < 6; b++) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bal = __ballot(bit);
+            peers &= bit ? bal : ~bal;
+        }
+        const uint32_t snap = ctr[wid][d];
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t old = atomicAdd(&ctr[wid][d], 1u);
+        __builtin_amdgcn_wave_barrier();
+        nb += old != snap + (uint32_t)__popcll(peers & lt);
+    }
+    if (nb) atomicAdd(bad, nb);
+}
+
+uint64_t lds_order_selfcheck(Workspace* ws, hipStream_t st) {
+    unsigned long long* bad = (unsigned long long*)ws->scratch("lds_order_bad", 8);
+    SMJ_CHECK(hipMemsetAsync(bad, 0, 8, st));
+    for (uint32_t K : {1u, 2u, 5u, 16u, 64u})
+        hipLaunchKernelGGL(k_lds_order, dim3(512), dim3(1024), 0, st, K, 256u, bad);
+    SMJ_CHECK(hipGetLastError());
+    unsigned long long* h = (unsigned long long*)ws->host_pinned("lds_order_h", 8);
+    SMJ_CHECK(hipMemcpyAsync(h, bad, 8, hipMemcpyDeviceToHost, st));
+    SMJ_CHECK(hipStreamSynchronize(st));
+    return *h;
 }
 
 // histogram-only pass + plain copy (histogram_memcpy_bench)

@@ -167,6 +167,8 @@ void sampled_partition(Workspace* ws, const Tup* in, uint64_t n, void* out,
                        unsigned int* pack_bad = nullptr);
 void hist_memcpy(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
                  uint32_t dbits, hipStream_t st);
+// lane order of LDS atomic returns (k_scatter_swa's ranks): violations, 0 expected
+uint64_t lds_order_selfcheck(Workspace* ws, hipStream_t st);
 
 // ---- bucketsort.hip : MSD bucket sort (+ fused merge-join count)
 extern const uint32_t kGroupTarget;  // expected tuples per group of the plan

@@ -56,7 +56,7 @@ DEVICE_SYMBOLS = [
     "smj_dev_join", "smj_join_phase_ms", "smj_dev_gen_pk", "smj_dev_gen_fk",
     "smj_dev_gen_zipf", "smj_dev_synchronize", "smj_dev_partition_range",
     "smj_trace_enable", "smj_trace_reset", "smj_trace_read", "smj_dev_join_segmented",
-    "smj_dev_partition_range_packed", "smj_dev_materialize",
+    "smj_dev_partition_range_packed", "smj_dev_materialize", "smj_selfcheck_lds_order",
 ]
 
 
@@ -156,6 +156,7 @@ class Library:
             "smj_dev_partition_range_packed": (C.c_int, [_P, _P, _U64, _P, _U32, _I64, _I64,
                                                          _P, _P, _P]),
             "smj_dev_materialize": (_U64, [_P, _P, _U64, _P, _U64, _P, _U64, _P]),
+            "smj_selfcheck_lds_order": (_U64, [_P, _P]),
             "smj_trace_enable": (None, [_P, C.c_int]),
             "smj_trace_reset": (None, [_P]),
             "smj_trace_read": (C.c_int, [_P, C.c_char_p, C.c_int, _P, _P, C.c_int]),
@@ -362,6 +363,10 @@ class Library:
         self.lib.smj_dev_partition_range(self.ws, inp.data_ptr(), inp.shape[0],
                                          out.data_ptr(), nbits, key_min, key_max,
                                          hist.data_ptr(), self.stream_ptr())
+
+    def selfcheck_lds_order(self) -> int:
+        """Violations of lane-ordered LDS atomic returns (0 expected)."""
+        return int(self.lib.smj_selfcheck_lds_order(self.ws, self.stream_ptr()))
 
     def trace(self, on: bool):
         self.lib.smj_trace_enable(self.ws, int(on))

@@ -436,8 +436,9 @@ int smj_dev_partition_range_packed(smj_workspace * ws, const tuple_t * in, uint6
  * S are the receive buffers: for every source GPU s in order, its range
  * partitions 0..2^bucket_bits-1 back to back, seg[s * 2^bucket_bits + b]
  * elements each (device int64).  Every partition b covers the keys
- * [key_lo + b * w, key_lo + (b + 1) * w) with 2^bucket_bits * w =
- * key_hi - key_lo + 1 (a power of two), so the partitions are the level-1
+ * [key_lo + b * w, key_lo + (b + 1) * w) with 2^bucket_bits * w = 2^L, L the
+ * bit length of key_hi - key_lo (any key_hi in [key_lo + 2^(L-1),
+ * key_lo + 2^L - 1] gives the same plan), so the partitions are the level-1
  * buckets of the local sort: no local partition pass.  The elements are
  * tuples, or (flags & SMJ_SEG_PACKED) the words of
  * smj_dev_partition_range_packed for the same w.  R and S are used as
@@ -450,6 +451,12 @@ void smj_dev_join_segmented(smj_workspace * ws, void * R, uint64_t nR,
                             uint32_t bucket_bits, int64_t key_lo, int64_t key_hi,
                             uint32_t flags, tuple_t * sortedR, tuple_t * sortedS,
                             unsigned long long * count_dev, smj_stream_t stream);
+
+/* Self-check of the hardware property behind the stable partition's ranks:
+ * LDS atomic adds return their old values to the lanes of one instruction
+ * that hit the same word in lane order (partition.hip, k_scatter_swa).
+ * Returns the number of violations (0 expected; synchronises `stream`). */
+uint64_t smj_selfcheck_lds_order(smj_workspace * ws, smj_stream_t stream);
 
 /* Per-kernel HIP-event trace of the join pipeline (bench.py roofline). */
 void smj_trace_enable(smj_workspace * ws, int on);

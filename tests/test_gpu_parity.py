@@ -57,6 +57,42 @@ def test_partition_matches_oracle(libs, oracles, width, n, nbits, shift, variant
         assert np.array_equal(a, b), f"partition {i} differs"
 
 
+def test_lds_order_selfcheck(libs, width):
+    """The hardware property the stable partition's ranks rely on
+    (k_scatter_swa): lane-ordered returns of colliding LDS atomic adds."""
+    assert libs[width].selfcheck_lds_order() == 0
+
+
+@pytest.mark.parametrize("n,nbits,shift,kind", [
+    (5_000_003, 10, 0, "pk"),         # several tiles per workgroup chunk
+    (3_000_017, 1, 0, "pk"),          # two partitions, long runs
+    (2_500_000, 10, 0, "hot"),        # 90 % of the tuples in one partition
+    (2_000_001, 9, 4, "dups"),        # few distinct keys: equal digits everywhere
+    (777_777, 10, 22, "pk"),          # digit above every key: one partition
+])
+def test_partition_stable_large(libs, oracles, width, n, nbits, shift, kind):
+    """Multi-tile chunks, carries that live over many tiles, skew: the stable
+    write-combining scatter against the oracle, every partition in order."""
+    orc, lib = oracles[width], libs[width]
+    orc.seed(4242 + n)
+    t = orc.create_relation_pk(n)
+    rng = np.random.default_rng(n)
+    if kind == "hot":
+        hot = rng.random(n) < 0.9
+        t["key"][hot] = 1 + (t["key"][hot] << nbits)  # digit 0 (key - 1 = k << nbits)
+    elif kind == "dups":
+        t["key"] = rng.integers(1, 40, n)
+    t["payload"] = np.arange(n) - n // 2
+    out, cnt, off = lib.partition(t, nbits, shift, 1)
+    eout, ecnt, eoff = orc.partition(t, nbits, shift, padded=True)
+    np.testing.assert_array_equal(cnt, ecnt)
+    np.testing.assert_array_equal(off, eoff)
+    mask = np.zeros(len(eout), bool)
+    for o, c in zip(eoff.tolist(), ecnt.tolist()):
+        mask[o:o + c] = True
+    np.testing.assert_array_equal(out[:len(eout)][mask], eout[mask])
+
+
 def test_partition_random_keys(libs, oracles, width):
     orc, lib = oracles[width], libs[width]
     t = rand_tuples(width, 123457, 7)

@@ -1,15 +1,21 @@
 #!/usr/bin/env bash
-# One gpurun call: GPU parity tests, the 1-GPU bench (16- and 8-byte tuples)
-# and a rocprofv3 kernel-trace summary of the bench.  Stops at the first GPU
-# fault / abort / timeout (a plain test failure still lets the bench run).
+# pytest subset ($TESTS, -k $K) then optional bench commands ($BENCH: ';'-separated
+# bench.py argument lists), each under its own time limit; stops at the first failure.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
-OUT=${OUT:-gpurun_out}
-mkdir -p "$OUT"
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > "$OUT/pytest_gpu.log" 2>&1
-rc=$?
-echo "pytest exit $rc" >> "$OUT/pytest_gpu.log"
-case $rc in 0|1) ;; *) echo "stopping after pytest rc=$rc"; exit $rc;; esac
-timeout -k 10 300 python bench.py --steps 5 --warmup 2 > "$OUT/bench16.log" 2>&1 && \
-timeout -k 10 300 python bench.py --steps 5 --warmup 2 --width 8 --no-cpu-baseline > "$OUT/bench8.log" 2>&1 && \
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof16" -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/prof16.log" 2>&1
+O=gpurun_out/${TAG:-chk}
+mkdir -p $O
+if [ -n "$TESTS" ]; then
+  timeout -k 10 ${PT_TIMEOUT:-900} python -u -m pytest $TESTS ${K:+-k "$K"} -x -q --timeout 240 --timeout-method thread > $O/pytest.log 2>&1
+  rc=$?; tail -4 $O/pytest.log
+  [ $rc = 0 ] || { grep -E "Error|assert|FAIL" $O/pytest.log | head -20; exit $rc; }
+fi
+if [ -n "$BENCH" ]; then
+  IFS=';' read -ra BL <<< "$BENCH"
+  i=0
+  for b in "${BL[@]}"; do
+    i=$((i+1))
+    timeout -k 10 300 python bench.py $b > $O/bench$i.json 2> $O/bench$i.err || { tail -5 $O/bench$i.err; exit 1; }
+    python3 -c "import json,sys; d=json.load(open('$O/bench$i.json')); r=d.get('roofline') or {}; print('$b', '|', d['ms_per_step'], 'ms', d['value'], d['unit'], 'ok' if d.get('result_ok') else 'BAD', '| kernels', d['detail']['kernels_ms_per_step'], '| frac', r.get('frac'), r.get('kernel'))"
+  done
+fi
