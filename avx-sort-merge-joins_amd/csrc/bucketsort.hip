@@ -148,6 +148,7 @@ struct TilePassArgs {
     RangePlan plan;  // by value: kernel arguments live in SGPRs
     uint32_t nb2;
     const unsigned int* pack_bad;  // set: the packed partition is void, exit
+    uint32_t d2_fast;              // Lay::fast_ok for the level-2 digit (host)
 };
 
 template <class Lay>
@@ -181,12 +182,26 @@ k_tilepass(TilePassArgs A) {
         if (i < len) v[j] = part[off + i];
     }
     __syncthreads();
+    // keys outside the plan range (clamped by plan_rel) only sit in the first
+    // and the last bucket: every other tile takes the 32-bit digit
+    if (A.d2_fast && b != 0 && b != (1u << P.D1) - 1) {
+        const uint32_t base_lo = (uint32_t)P.base, mask = nb2 - 1;
 #pragma unroll
-    for (int j = 0; j < TP_ITEMS; j++) {
-        uint32_t i = j * TP_THREADS + threadIdx.x;
-        if (i < len) {
-            dg[j] = plan_d2(P, Lay::rel(P, v[j], b), b);
-            atomicAdd(&hist[dg[j]], 1u);
+        for (int j = 0; j < TP_ITEMS; j++) {
+            uint32_t i = j * TP_THREADS + threadIdx.x;
+            if (i < len) {
+                dg[j] = Lay::digit_fast(v[j], base_lo, P.s1, P.s2, mask);
+                atomicAdd(&hist[dg[j]], 1u);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < TP_ITEMS; j++) {
+            uint32_t i = j * TP_THREADS + threadIdx.x;
+            if (i < len) {
+                dg[j] = plan_d2(P, Lay::rel(P, v[j], b), b);
+                atomicAdd(&hist[dg[j]], 1u);
+            }
         }
     }
     __syncthreads();
@@ -274,6 +289,7 @@ struct GroupArgs {
     uint32_t* novf;
     uint32_t ovf_cap;
     const unsigned int* pack_bad;  // set: the packed partition is void, exit
+    uint32_t d3_fast;              // Lay::fast_ok for the level-3 digit (host)
 };
 
 // threadIdx.x behind an empty asm: per-thread LDS addresses are recomputed
@@ -290,11 +306,11 @@ struct GroupLDS {
     W B[GS_CAP + 1];                      // one relation's group (+ a dump slot)
     uint32_t cnt[2][GS_NB3 / 2];          // d3 histograms of R and S (2 x u16)
     uint32_t cur[GS_NB3 / 2];             // placement cursors (2 x u16)
-    uint32_t runoff[2][GS_TMAX + 1];      // run t starts at position runoff[t]
-    uint32_t runsrc[2][GS_TMAX];          // run t's offset in its bucket
+    // the group's non-empty tile runs, numbered in position order: run k
+    // starts at group position (uint32)run[k] and at bucket offset run[k] >> 32
+    unsigned long long run[2][GS_TMAX];
     unsigned long long smap[2][GS_WIN];   // bit j: a run starts at position j
-    uint8_t stile[2][GS_CAP];             // tile of the run starting at j
-    uint8_t wtile[2][GS_WIN];             // tile holding position 64 * w
+    uint32_t wk[2][GS_WIN];               // runs starting before position 64 * w
     uint32_t wtot[GS_THREADS / 64];
     unsigned long long scan64[GS_THREADS / 64 + 1];
     uint32_t n[2];
@@ -427,8 +443,11 @@ __device__ __forceinline__ void insertion_sort(typename Lay::W* a, uint32_t n) {
     }
 }
 
-// Group tables in LDS: wave r builds relation r's run table, run-start bitmap
-// and window tiles (no block barrier inside; one at the end).
+// Group tables in LDS: wave r builds relation r's table of non-empty runs
+// (compacted by ballot), the run-start bitmap and, per 64-position window,
+// the number of runs that start before it (no block barrier inside; one at
+// the end).  The run of position j is then wk[j/64] + (starts in its window
+// up to j) - 1: two LDS round trips per gathered element, no search.
 template <class LDS>
 __device__ __forceinline__ void build_tables(const GroupArgs& A, LDS& L,
                                              const GroupMeta& M) {
@@ -445,38 +464,26 @@ __device__ __forceinline__ void build_tables(const GroupArgs& A, LDS& L,
         const unsigned long long i1 = wave_incl_scan64(p1) + tot0;
         const unsigned long long tot = __shfl(i1, 63, 64);
         const uint32_t sA = (uint32_t)(i0 - p0), sB = (uint32_t)(i1 - p1);
-        if (lane < nt) {
-            L.runoff[r][lane] = sA;
-            L.runsrc[r][lane] = M.toff[0] + M.lo[0];
-        }
-        if (lane + 64 < nt) {
-            L.runoff[r][lane + 64] = sB;
-            L.runsrc[r][lane + 64] = M.toff[1] + M.lo[1];
-        }
+        // non-empty runs in tile order = position order; run starts at or
+        // past GS_CAP only occur in groups that overflow (never gathered)
+        const bool eA = lane < nt && M.len[0] > 0 && sA < GS_CAP;
+        const bool eB = lane + 64 < nt && M.len[1] > 0 && sB < GS_CAP;
+        const uint64_t bA = __ballot(eA), bB = __ballot(eB);
+        const uint32_t kA = (uint32_t)__popcll(bA & lanemask_lt());
+        const uint32_t kB = (uint32_t)__popcll(bA) + (uint32_t)__popcll(bB & lanemask_lt());
+        if (eA) L.run[r][kA] = ((unsigned long long)(M.toff[0] + M.lo[0]) << 32) | sA;
+        if (eB) L.run[r][kB] = ((unsigned long long)(M.toff[1] + M.lo[1]) << 32) | sB;
         if (lane == 0) {
-            L.runoff[r][nt <= GS_TMAX ? nt : 0] = (uint32_t)tot;
             L.n[r] = nt <= GS_TMAX ? (uint32_t)tot : 0xffffffffu;
             L.off[r] = (uint32_t)(tot >> 32);
         }
         wave_lds_sync();
-        // run starts at or past GS_CAP only occur in groups that overflow
-        // (they never reach the gather): keep them out of the LDS tables
-        if (lane < nt && M.len[0] > 0 && sA < GS_CAP) {
-            atomicOr(&L.smap[r][sA >> 6], 1ull << (sA & 63));
-            L.stile[r][sA] = (uint8_t)lane;
-        }
-        if (lane + 64 < nt && M.len[1] > 0 && sB < GS_CAP) {
-            atomicOr(&L.smap[r][sB >> 6], 1ull << (sB & 63));
-            L.stile[r][sB] = (uint8_t)(lane + 64);
-        }
-        if (lane < GS_WIN && nt > 0 && nt <= GS_TMAX) {
-            const uint32_t pos = lane * 64;
-            uint32_t t = 0;
-#pragma unroll
-            for (uint32_t step = GS_TMAX / 2; step; step >>= 1)
-                if (t + step < nt && L.runoff[r][t + step] <= pos) t += step;
-            L.wtile[r][lane] = (uint8_t)t;
-        }
+        if (eA) atomicOr(&L.smap[r][sA >> 6], 1ull << (sA & 63));
+        if (eB) atomicOr(&L.smap[r][sB >> 6], 1ull << (sB & 63));
+        wave_lds_sync();
+        const uint32_t c = lane < GS_WIN ? (uint32_t)__popcll(L.smap[r][lane]) : 0u;
+        const uint32_t incl = wave_incl_scan32(c);
+        if (lane < GS_WIN) L.wk[r][lane] = incl - c;
     }
     __syncthreads();
 }
@@ -526,7 +533,10 @@ __device__ __forceinline__ void group_overflow(const GroupArgs& A, LDS& L,
 }
 
 // gather relation r's group into registers (loads only: every load in
-// flight at once); lanes past the end re-read the last element
+// flight at once); lanes past the end re-read the last element.  Position j
+// = k * GS_THREADS + thread: a wave's 64 positions share one bitmap window
+// (broadcast reads), its run is found with a lane count of the window's
+// run starts.
 template <class Lay>
 __device__ __forceinline__ void gather_group(const GroupArgs& A, GroupLDS<typename Lay::W>& L,
                                              const GroupMeta& C, int r, uint32_t n,
@@ -539,9 +549,9 @@ __device__ __forceinline__ void gather_group(const GroupArgs& A, GroupLDS<typena
         const uint32_t j = min(k * GS_THREADS + otid(), last);
         const uint32_t w = j >> 6;
         const unsigned long long bits = L.smap[r][w] & (~0ull >> (63 - (j & 63)));
-        const uint32_t t = bits ? L.stile[r][(w << 6) + 63 - __clzll(bits)]
-                                : L.wtile[r][w];
-        v[k] = tp[L.runsrc[r][t] + (j - L.runoff[r][t])];
+        const uint32_t q = L.wk[r][w] + (uint32_t)__popcll(bits) - 1u;
+        const unsigned long long e = L.run[r][q];
+        v[k] = tp[(uint32_t)(e >> 32) + (j - (uint32_t)e)];
     }
 }
 
@@ -571,14 +581,28 @@ __device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS<typename
         return true;
     }
 #endif
-    // ---- level-3 digits, histogram (two u16 counters per word)
+    // ---- level-3 digits, histogram (two u16 counters per word).  Only the
+    // first and the last group of the plan can hold keys outside its range
+    // (plan_rel clamps them there); every other group takes the 32-bit digit.
     uint32_t dg[GS_ITEMS];
+    const bool edge = (C.b == 0 && C.g == 0) ||
+                      (C.b == (1u << P.D1) - 1 && C.g == A.nb2 - 1);
+    if (A.d3_fast && !edge) {
+        const uint32_t base_lo = (uint32_t)P.base, mask = (1u << P.D3) - 1;
 #pragma unroll
-    for (int k = 0; k < GS_ITEMS; k++) {
-        const bool valid = k * GS_THREADS + tid < nr;
-        clamped |= valid && Lay::clamped(P, v[k]);
-        dg[k] = plan_d3(P, Lay::rel(P, v[k], C.b), d12);
-        if (valid) atomicAdd(&L.cnt[r][dg[k] >> 1], 1u << ((dg[k] & 1) * 16));
+        for (int k = 0; k < GS_ITEMS; k++) {
+            const bool valid = k * GS_THREADS + tid < nr;
+            dg[k] = Lay::digit_fast(v[k], base_lo, P.s1, P.s3, mask);
+            if (valid) atomicAdd(&L.cnt[r][dg[k] >> 1], 1u << ((dg[k] & 1) * 16));
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < GS_ITEMS; k++) {
+            const bool valid = k * GS_THREADS + tid < nr;
+            clamped |= valid && Lay::clamped(P, v[k]);
+            dg[k] = plan_d3(P, Lay::rel(P, v[k], C.b), d12);
+            if (valid) atomicAdd(&L.cnt[r][dg[k] >> 1], 1u << ((dg[k] & 1) * 16));
+        }
     }
     __syncthreads();
     // ---- exclusive scan of the bins: thread owns GS_BPT consecutive bins;
@@ -1518,7 +1542,9 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
     T.plan = *a.host_plan;
     T.nb2 = nb2;
     T.pack_bad = a.pack_bad;
+    T.d2_fast = a.digit_fast && Lay::fast_ok(T.plan, T.plan.s2, T.plan.D2);
     G.pack_bad = a.pack_bad;
+    G.d3_fast = a.digit_fast && Lay::fast_ok(T.plan, T.plan.s3, T.plan.D3);
     {
         TraceScope ts(ws, "k_tilepass", st);
         const size_t tp_lds = TILE2 * sizeof(W) + nb2 * 4 + 64;
@@ -1690,7 +1716,9 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
     T.plan = *hplan;
     T.nb2 = nb2;
     T.pack_bad = nullptr;
+    T.d2_fast = a.digit_fast && LayTup::fast_ok(*hplan, hplan->s2, hplan->D2);
     G.pack_bad = nullptr;
+    G.d3_fast = a.digit_fast && LayTup::fast_ok(*hplan, hplan->s3, hplan->D3);
     G.nrel = nrel;
     G.plan = *hplan;
     G.count_dev = a.count_dev;

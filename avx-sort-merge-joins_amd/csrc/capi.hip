@@ -1217,6 +1217,7 @@ void smj_dev_join_segmented(smj_workspace* wsp, void* R, uint64_t nR,
     a.part_flag = flag;  // never set: the buckets are exact
     a.host_plan = &hplan;
     a.packed = packed;  // checked packable before the exchange: no pack_bad here
+    a.digit_fast = packed;  // packed words never lie outside the plan
     if (!bucket_sort(ws, a, st)) {
         fprintf(stderr, "[ERROR] smj_dev_join_segmented: unexpected partition flag\n");
         abort();

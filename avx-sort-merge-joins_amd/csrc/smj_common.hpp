@@ -218,6 +218,17 @@ struct LayTup {
     __device__ static __forceinline__ Tup unpack(const RangePlan&, const W& w, uint32_t) {
         return w;
     }
+    // Digit `sh`/`mask` of an element whose key lies inside the plan range
+    // (no clamping: every group but the first and the last): the low 32 bits
+    // of rel = key - base are exact modulo 2^32, so 32-bit arithmetic gives
+    // bits [sh, sh + width) when sh + width <= 32 (fast_ok).
+    __device__ static __forceinline__ uint32_t digit_fast(const W& w, uint32_t base_lo,
+                                                          uint32_t, uint32_t sh, uint32_t mask) {
+        return (((uint32_t)tup_key(w) - base_lo) >> sh) & mask;
+    }
+    __host__ static bool fast_ok(const RangePlan& P, uint32_t sh, uint32_t width) {
+        return sh + width <= 32;
+    }
     // equal keys: the elements are identical iff these values are
     __device__ static __forceinline__ uint64_t same_key_id(const W& w) {
 #ifdef KEY_8B
@@ -238,6 +249,14 @@ struct LayPacked {
     __device__ static __forceinline__ bool clamped(const RangePlan&, const W&) { return false; }
     __device__ static __forceinline__ bool less(const W& a, const W& b) { return a < b; }
     __device__ static __forceinline__ uint64_t same_key_id(const W& w) { return w; }
+    // bits [sh, sh + width) of rel (sh + width <= s1, inside the word)
+    __device__ static __forceinline__ uint32_t digit_fast(const W& w, uint32_t, uint32_t s1,
+                                                          uint32_t sh, uint32_t mask) {
+        return (uint32_t)(w >> (64 - s1 + sh)) & mask;
+    }
+    __host__ static bool fast_ok(const RangePlan& P, uint32_t sh, uint32_t width) {
+        return sh + width <= P.s1;
+    }
     __device__ static __forceinline__ Tup unpack(const RangePlan& P, const W& w, uint32_t b) {
         Tup t;
         t.payload = (int64_t)(w & (~0ull >> P.s1));

@@ -201,6 +201,11 @@ struct BucketSortArgs {
     // pack_bad, [2] = the skew queue length (read back in one copy)
     unsigned int* status = nullptr;
     const unsigned int* pack_bad = nullptr;  // set by the partition: not packable
+    // the 32-bit digit fast path of the tile and group passes (keys outside
+    // the plan range only in the first and the last bucket); the segmented
+    // join turns it off for tuples (a caller's key outside its range could sit
+    // in the last non-empty bucket instead)
+    bool digit_fast = true;
     hipEvent_t ev_tile = nullptr;   // optional phase markers
     hipEvent_t ev_bucket = nullptr;
     hipEvent_t ev_ovf = nullptr;
