@@ -1400,10 +1400,24 @@ const uint32_t kGroupTarget = GS_CAP * 4 / 5 >= 2048 ? 2048 : (GS_CAP * 4 / 5 >=
 // device-side tile numbering of a segmented (sampled) partition: per bucket
 // the tiles of its segments, their exclusive scan (btile0, total in
 // btile0[nb] and *ntiles) and the dense output start of every bucket
+struct SegRel {
+    const int64_t* seg_cnt[2];
+    const int64_t* bcount[2];
+    const uint64_t* bstart[2];
+    const uint64_t* seg_start[2];
+    uint32_t* ntiles[2];
+    uint64_t* ostart[2];
+    TileTable tt[2];
+};
+
+// blockIdx.x = relation
 __global__ void __launch_bounds__(256)
-k_seg_scan(const int64_t* __restrict__ seg_cnt, const int64_t* __restrict__ bcount,
-           uint32_t nb, uint32_t nseg, uint32_t* __restrict__ btile0,
-           uint32_t* __restrict__ ntiles, uint64_t* __restrict__ ostart) {
+k_seg_scan(SegRel S, uint32_t nb, uint32_t nseg) {
+    const int r = blockIdx.x;
+    const int64_t* __restrict__ seg_cnt = S.seg_cnt[r];
+    const int64_t* __restrict__ bcount = S.bcount[r];
+    uint32_t* __restrict__ btile0 = S.tt[r].btile0;
+    uint64_t* __restrict__ ostart = S.ostart[r];
     __shared__ unsigned long long scr[5];
     __shared__ unsigned long long base;
     if (threadIdx.x == 0) base = 0;
@@ -1432,7 +1446,29 @@ k_seg_scan(const int64_t* __restrict__ seg_cnt, const int64_t* __restrict__ bcou
     }
     if (threadIdx.x == 0) {
         btile0[nb] = (uint32_t)(base >> 40);
-        *ntiles = (uint32_t)(base >> 40);
+        *S.ntiles[r] = (uint32_t)(base >> 40);
+    }
+}
+
+// k_tiles of both relations (blockIdx.y = relation)
+__global__ void __launch_bounds__(64)
+k_tiles2(SegRel S, uint32_t nseg) {
+    const int r = blockIdx.y;
+    const uint32_t b = blockIdx.x;
+    const TileTable& tt = S.tt[r];
+    uint32_t t0 = tt.btile0[b];
+    for (uint32_t q = 0; q < nseg; q++) {
+        const uint64_t s0 = S.seg_start[r] ? S.seg_start[r][(size_t)b * nseg + q] : S.bstart[r][b];
+        const int64_t cnt = S.seg_cnt[r] ? S.seg_cnt[r][(size_t)b * nseg + q] : S.bcount[r][b];
+        const uint32_t nt = (uint32_t)((cnt + TILE2 - 1) / TILE2);
+        for (uint32_t i = threadIdx.x; i < nt; i += 64) {
+            const uint64_t o = (uint64_t)i * TILE2;
+            const int64_t rem = cnt - (int64_t)o;
+            tt.off[t0 + i] = s0 + o;
+            tt.len[t0 + i] = (uint32_t)(rem < TILE2 ? rem : TILE2);
+            tt.bucket[t0 + i] = b;
+        }
+        t0 += nt;
     }
 }
 
@@ -1510,12 +1546,24 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
         tt[r].tstride = ub[r];
         ostart[r] = (uint64_t*)ws->scratch(names[r][5], (size_t)nb * 8);
         ntiles[r] = (uint32_t*)ws->scratch(names[r][6], 4);
-        hipLaunchKernelGGL(k_seg_scan, dim3(1), dim3(256), 0, st, a.seg_cnt[r],
-                           a.bcount[r], nb, a.nseg, tt[r].btile0, ntiles[r], ostart[r]);
-        hipLaunchKernelGGL(k_tiles, dim3(nb), dim3(64), 0, st, a.bstart[r],
-                           a.bcount[r], a.seg_start[r], a.seg_cnt[r], a.nseg, tt[r]);
     }
     if (nrel == 1) tt[1] = tt[0];
+    {
+        // tile numbering of both relations: two launches
+        SegRel S;
+        for (int r = 0; r < 2; r++) {
+            const int rr = r < nrel ? r : 0;
+            S.seg_cnt[r] = a.seg_cnt[rr];
+            S.bcount[r] = a.bcount[rr];
+            S.bstart[r] = a.bstart[rr];
+            S.seg_start[r] = a.seg_start[rr];
+            S.ntiles[r] = ntiles[rr];
+            S.ostart[r] = ostart[rr];
+            S.tt[r] = tt[rr];
+        }
+        hipLaunchKernelGGL(k_seg_scan, dim3(nrel), dim3(256), 0, st, S, nb, a.nseg);
+        hipLaunchKernelGGL(k_tiles2, dim3(nb, nrel), dim3(64), 0, st, S, a.nseg);
+    }
     if (a.ev_tile) SMJ_CHECK(hipEventRecord(a.ev_tile, st));
 
     const uint32_t ngroups = nb * nb2;

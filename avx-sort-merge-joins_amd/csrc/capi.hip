@@ -18,15 +18,18 @@
 
 __global__ void k_setplan(smj::RangePlan* p, smj::RangePlan v) { *p = v; }
 
-// start of a join attempt: the plan (when known on the host), the count and
-// the 4-word status block (BucketSortArgs::status) in one launch
-__global__ void k_join_begin(smj::RangePlan* p, smj::RangePlan v, int set_plan,
-                             unsigned long long* count, unsigned int* status) {
+// start of a join attempt: the plan (when known on the host), the count, the
+// 4-word status block (BucketSortArgs::status) and the sampled partition's
+// sample counters (nzero words, every attempt) in one launch
+__global__ void __launch_bounds__(256)
+k_join_begin(smj::RangePlan* p, smj::RangePlan v, int set_plan, unsigned long long* count,
+             unsigned int* status, unsigned int* zero, uint32_t nzero) {
     if (threadIdx.x == 0) {
         if (set_plan) *p = v;
         *count = 0;
     }
     if (threadIdx.x < 4) status[threadIdx.x] = 0;
+    for (uint32_t i = threadIdx.x; i < nzero; i += 256) zero[i] = 0;
 }
 
 namespace smj {
@@ -263,6 +266,9 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
     }
     // [0] region overflow, [1] not packable, [2] skew queue length
     unsigned int* status = (unsigned int*)ws->scratch("join_status", 16);
+    // the sampled partition's counters: zeroed by k_join_begin on every
+    // attempt (never assumed zero from an earlier call)
+    unsigned int* sample = (unsigned int*)ws->scratch("sp_sample", (size_t)nrel * nb * 4);
     unsigned long long* cnt = count_dev
         ? count_dev : (unsigned long long*)ws->scratch("sort_cnt", 8);
     // attempts: sampled + packed words, sampled tuples, exact tuples; a later
@@ -271,14 +277,15 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
     // discarded: the count restarts from 0)
     for (int mode = can_pack ? 0 : (sampled ? 1 : 2); mode <= 2; mode++) {
         const bool packed = mode == 0;
-        hipLaunchKernelGGL(k_join_begin, dim3(1), dim3(64), 0, st, plan, hplan,
-                           plan_on_host ? 1 : 0, cnt, status);
-        for (int r = 0; r < nrel; r++) {
-            if (mode < 2)
-                sampled_partition(ws, rels[r], ns[r], part[r], plan, D1, bst[r], bh[r],
-                                  sgs[r], sgc[r], status, st, packed ? &hplan : nullptr,
-                                  status + 1);
-            else
+        hipLaunchKernelGGL(k_join_begin, dim3(1), dim3(256), 0, st, plan, hplan,
+                           plan_on_host ? 1 : 0, cnt, status, sample,
+                           mode < 2 ? (uint32_t)nrel * nb : 0u);
+        if (mode < 2) {
+            void* outs_v[2] = {part[0], part[nrel > 1 ? 1 : 0]};
+            sampled_partition(ws, nrel, rels, ns, outs_v, plan, D1, sample, bst, bh, sgs, sgc,
+                              status, st, packed ? &hplan : nullptr, status + 1);
+        } else {
+            for (int r = 0; r < nrel; r++)
                 plan_partition(ws, rels[r], ns[r], part[r], plan, D1, bst[r], bh[r], st);
         }
         SMJ_CHECK(hipEventRecord(ws->ev[1], st));

@@ -964,11 +964,20 @@ k_scatter_wc(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_a
 // region start (unstable order), followed by unused slack.  A region that
 // would overflow raises a flag and the caller repeats the exact
 // (histogram) partition.
+// the relations of one sampled partition launch (blockIdx.y = relation)
+struct SampleRel {
+    const Tup* in[2];
+    uint64_t n[2];
+    unsigned int* hist[2];  // nbins counters each, zeroed by the caller
+};
+
 template <class Digit>
 __global__ void __launch_bounds__(256)
-k_sample_hist(const Tup* __restrict__ in, uint64_t n, uint32_t stride,
-              Digit dig_arg, uint32_t nbins, unsigned int* __restrict__ hist) {
+k_sample_hist(SampleRel S, uint32_t stride, Digit dig_arg, uint32_t nbins) {
     const auto dig = dig_arg.load();
+    const Tup* __restrict__ in = S.in[blockIdx.y];
+    const uint64_t n = S.n[blockIdx.y];
+    unsigned int* __restrict__ hist = S.hist[blockIdx.y];
     extern __shared__ unsigned int sh_hist[];
     for (uint32_t d = threadIdx.x; d < nbins; d += 256) sh_hist[d] = 0;
     __syncthreads();
@@ -1002,11 +1011,25 @@ k_sample_hist(const Tup* __restrict__ in, uint64_t n, uint32_t stride,
 #endif
 constexpr uint32_t kSegBytes = SMJ_SC_SEG;
 
+// per-relation region tables of one sampled partition launch
+struct RegionRel {
+    const unsigned int* sample[2];
+    uint64_t* base[2];
+    uint64_t* seg_start[2];
+    unsigned long long* cursor[2];
+    uint64_t* cap_end[2];
+    int64_t* hist_out[2];
+    int64_t* seg_cnt[2];
+};
+
 __global__ void __launch_bounds__(256)
-k_regions(const unsigned int* __restrict__ sample, uint32_t nbins,
-          uint32_t stride, uint64_t slack, uint64_t* __restrict__ base,
-          uint64_t* __restrict__ seg_start, unsigned long long* __restrict__ cursor,
-          uint64_t* __restrict__ cap_end, uint32_t elem_bytes) {
+k_regions(RegionRel R, uint32_t nbins, uint32_t stride, uint64_t slack, uint32_t elem_bytes) {
+    const int r = blockIdx.x;
+    const unsigned int* __restrict__ sample = R.sample[r];
+    uint64_t* __restrict__ base = R.base[r];
+    uint64_t* __restrict__ seg_start = R.seg_start[r];
+    unsigned long long* __restrict__ cursor = R.cursor[r];
+    uint64_t* __restrict__ cap_end = R.cap_end[r];
     __shared__ uint64_t sh[256];
     const uint64_t SEG = kSegBytes / elem_bytes;
     const uint32_t per = (nbins + 255) / 256;
@@ -1047,12 +1070,13 @@ k_regions(const unsigned int* __restrict__ sample, uint32_t nbins,
 }
 
 // partition and shard sizes from the cursors; flag = 1 when a shard overflowed
+// (blockIdx.x = relation)
 __global__ void __launch_bounds__(256)
-k_regions_done(const uint64_t* __restrict__ seg_start,
-               const unsigned long long* __restrict__ cursor,
-               const uint64_t* __restrict__ cap_end, uint32_t nbins,
-               int64_t* __restrict__ hist_out, int64_t* __restrict__ seg_cnt,
-               unsigned int* __restrict__ flag) {
+k_regions_done(RegionRel R, uint32_t nbins, unsigned int* __restrict__ flag) {
+    const int r = blockIdx.x;
+    const uint64_t* __restrict__ seg_start = R.seg_start[r];
+    const unsigned long long* __restrict__ cursor = R.cursor[r];
+    const uint64_t* __restrict__ cap_end = R.cap_end[r];
     for (uint32_t d = threadIdx.x; d < nbins; d += 256) {
         int64_t tot = 0;
         for (uint32_t q = 0; q < kShards; q++) {
@@ -1061,11 +1085,11 @@ k_regions_done(const uint64_t* __restrict__ seg_start,
             // describe memory inside the region
             const uint64_t e = cursor[i] < cap_end[i] ? cursor[i] : cap_end[i];
             const int64_t c = (int64_t)(e - seg_start[i]);
-            seg_cnt[i] = c;
+            R.seg_cnt[r][i] = c;
             tot += c;
             if (cursor[i] > cap_end[i]) atomicOr(flag, 1u);
         }
-        hist_out[d] = tot;
+        R.hist_out[r][d] = tot;
     }
 }
 
@@ -1654,10 +1678,13 @@ void plan_partition_packed(Workspace* ws, const Tup* in, uint64_t n, uint64_t* o
 #define SMJ_SC_THREADS 1024
 #endif
 #ifndef SMJ_SC_ITEMS16
-#define SMJ_SC_ITEMS16 4
+#define SMJ_SC_ITEMS16 4   // 16-byte tuples staged as tuples
+#endif
+#ifndef SMJ_SC_ITEMS16P
+#define SMJ_SC_ITEMS16P 8  // 16-byte tuples staged as packed 8-byte words
 #endif
 #ifndef SMJ_SC_ITEMS8
-#define SMJ_SC_ITEMS8 8
+#define SMJ_SC_ITEMS8 13
 #endif
 #ifndef SMJ_SC_WG_PER_CU
 #define SMJ_SC_WG_PER_CU 1
@@ -1672,22 +1699,21 @@ uint64_t sampled_capacity(uint64_t n, uint32_t dbits) {
            ((uint64_t)1 << dbits) * kShards * (kRegionSlack + 2 * SEG);
 }
 
-template <class Pack>
-static void sampled_scatter(Workspace* ws, const Tup* in, uint64_t n, void* out,
-                            const PlanDigit1& dig, uint32_t nbins,
-                            unsigned long long* cursor, const uint64_t* cap_end,
-                            const Pack& pk, unsigned int* bad_flag, hipStream_t st) {
+template <int ITEMS, class Pack>
+static bool sampled_scatter_t(Workspace* ws, const Tup* in, uint64_t n, void* out,
+                              const PlanDigit1& dig, uint32_t nbins,
+                              unsigned long long* cursor, const uint64_t* cap_end,
+                              const Pack& pk, unsigned int* bad_flag, hipStream_t st) {
     constexpr int THREADS = SMJ_SC_THREADS;
-    constexpr int ITEMS = sizeof(Tup) == 16 ? SMJ_SC_ITEMS16 : SMJ_SC_ITEMS8;
     constexpr int TILE = THREADS * ITEMS;
+    const size_t lds = ScatterGeom<THREADS, ITEMS, typename Pack::OutT>::lds_bytes(nbins);
+    if (lds > 160 * 1024) return false;
     uint64_t ntiles = (n + TILE - 1) / TILE;
     const uint32_t maxwg = 256 * SMJ_SC_WG_PER_CU;
     uint32_t nwg = (uint32_t)(ntiles < maxwg ? ntiles : maxwg);
     const uint64_t tiles_per_wg = (ntiles + nwg - 1) / nwg;
     const uint64_t chunk = tiles_per_wg * TILE;
     nwg = (uint32_t)((ntiles + tiles_per_wg - 1) / tiles_per_wg);
-    const size_t lds =
-        ScatterGeom<THREADS, ITEMS, typename Pack::OutT>::lds_bytes(nbins);
     static bool attr = false;
     if (!attr) {
         SMJ_CHECK(hipFuncSetAttribute(
@@ -1695,25 +1721,43 @@ static void sampled_scatter(Workspace* ws, const Tup* in, uint64_t n, void* out,
             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr = true;
     }
-    if (lds > 160 * 1024) {
-        fprintf(stderr, "[ERROR] smj: scatter LDS %zu > 160 KiB\n", lds);
-        abort();
-    }
-    if (nbins > (uint32_t)THREADS) {
-        fprintf(stderr, "[ERROR] smj: sampled scatter needs <= %d partitions\n", THREADS);
-        abort();
-    }
     TraceScope ts(ws, "k_scatter", st);
     hipLaunchKernelGGL((k_scatter_res<THREADS, ITEMS, PlanDigit1, Pack>), dim3(nwg),
                        dim3(THREADS), lds, st, in, n, chunk, dig, nbins, cursor,
                        cap_end, (typename Pack::OutT*)out, pk, bad_flag);
+    return true;
 }
 
-void sampled_partition(Workspace* ws, const Tup* in, uint64_t n, void* out,
-                       const RangePlan* plan_dev, uint32_t dbits,
-                       uint64_t* starts_dev, int64_t* hist_out,
-                       uint64_t* seg_start, int64_t* seg_cnt,
-                       unsigned int* flag_dev, hipStream_t st,
+// The LDS stage holds OutT and the carry 64 bytes per partition: the widest
+// tile that fits (8-byte tuples: 13 x 1024 at 512 partitions, 8 x 1024 at
+// 1024; packed words 8 / 4 x 1024; 16-byte tuples 4 x 1024), measured best.
+template <class Pack>
+static void sampled_scatter(Workspace* ws, const Tup* in, uint64_t n, void* out,
+                            const PlanDigit1& dig, uint32_t nbins,
+                            unsigned long long* cursor, const uint64_t* cap_end,
+                            const Pack& pk, unsigned int* bad_flag, hipStream_t st) {
+    constexpr int THREADS = SMJ_SC_THREADS;
+    if (nbins > (uint32_t)THREADS) {
+        fprintf(stderr, "[ERROR] smj: sampled scatter needs <= %d partitions\n", THREADS);
+        abort();
+    }
+    constexpr int BIG = sizeof(Tup) == 16
+        ? (sizeof(typename Pack::OutT) == 8 ? SMJ_SC_ITEMS16P : SMJ_SC_ITEMS16)
+        : SMJ_SC_ITEMS8;
+    constexpr int SMALL = sizeof(Tup) == 16 ? 4 : 8;
+    if (sampled_scatter_t<BIG>(ws, in, n, out, dig, nbins, cursor, cap_end, pk, bad_flag, st))
+        return;
+    if (sampled_scatter_t<SMALL>(ws, in, n, out, dig, nbins, cursor, cap_end, pk, bad_flag, st))
+        return;
+    fprintf(stderr, "[ERROR] smj: sampled scatter LDS exceeds 160 KiB (%u partitions)\n", nbins);
+    abort();
+}
+
+void sampled_partition(Workspace* ws, int nrel, const Tup* const* in, const uint64_t* n,
+                       void* const* out, const RangePlan* plan_dev, uint32_t dbits,
+                       unsigned int* sample, uint64_t* const* starts_dev,
+                       int64_t* const* hist_out, uint64_t* const* seg_start,
+                       int64_t* const* seg_cnt, unsigned int* flag_dev, hipStream_t st,
                        const RangePlan* pack_plan, unsigned int* pack_bad) {
     PlanDigit1 dig{plan_dev};
     const uint32_t nbins = 1u << dbits;
@@ -1722,42 +1766,60 @@ void sampled_partition(Workspace* ws, const Tup* in, uint64_t n, void* out,
 #else
     const bool packed = false;
 #endif
-    unsigned int* sample = (unsigned int*)ws->scratch("sp_sample", (size_t)nbins * 4);
-    unsigned long long* cursor =
-        (unsigned long long*)ws->scratch("sp_cursor", (size_t)nbins * kShards * 8);
-    uint64_t* cap_end = (uint64_t*)ws->scratch("sp_capend", (size_t)nbins * kShards * 8);
-    SMJ_CHECK(hipMemsetAsync(sample, 0, (size_t)nbins * 4, st));
+    static const char* cn[2] = {"sp_cursor0", "sp_cursor1"};
+    static const char* en[2] = {"sp_capend0", "sp_capend1"};
+    SampleRel S;
+    RegionRel R;
+    uint64_t nmax = 0;
+    for (int r = 0; r < 2; r++) {
+        const int rr = r < nrel ? r : 0;
+        S.in[r] = in[rr];
+        S.n[r] = n[rr];
+        S.hist[r] = sample + (size_t)rr * nbins;
+        R.sample[r] = S.hist[r];
+        R.base[r] = starts_dev[rr];
+        R.seg_start[r] = seg_start[rr];
+        R.hist_out[r] = hist_out[rr];
+        R.seg_cnt[r] = seg_cnt[rr];
+        if (r < nrel) {
+            R.cursor[r] = (unsigned long long*)ws->scratch(cn[r], (size_t)nbins * kShards * 8);
+            R.cap_end[r] = (uint64_t*)ws->scratch(en[r], (size_t)nbins * kShards * 8);
+            nmax = n[r] > nmax ? n[r] : nmax;
+        } else {
+            R.cursor[r] = R.cursor[0];
+            R.cap_end[r] = R.cap_end[0];
+        }
+    }
     {
         TraceScope ts(ws, "k_sample", st);
-        const uint64_t ns = (n + 4 * kSampleStride - 1) / (4 * kSampleStride);
-        uint32_t g = (uint32_t)((ns + 255) / 256);
+        const uint64_t npts = (nmax + 4 * kSampleStride - 1) / (4 * kSampleStride);
+        uint32_t g = (uint32_t)((npts + 255) / 256);
         if (g > 1024) g = 1024;
         if (g == 0) g = 1;
-        hipLaunchKernelGGL((k_sample_hist<PlanDigit1>), dim3(g), dim3(256),
-                           nbins * sizeof(unsigned int), st, in, n, kSampleStride,
-                           dig, nbins, sample);
-        hipLaunchKernelGGL(k_regions, dim3(1), dim3(256), 0, st, sample, nbins,
-                           kSampleStride, kRegionSlack, starts_dev, seg_start, cursor,
-                           cap_end, packed ? 8u : (uint32_t)sizeof(Tup));
+        hipLaunchKernelGGL((k_sample_hist<PlanDigit1>), dim3(g, nrel), dim3(256),
+                           nbins * sizeof(unsigned int), st, S, kSampleStride, dig, nbins);
+        hipLaunchKernelGGL(k_regions, dim3(nrel), dim3(256), 0, st, R, nbins, kSampleStride,
+                           kRegionSlack, packed ? 8u : (uint32_t)sizeof(Tup));
     }
-    if (n) {
+    for (int r = 0; r < nrel; r++) {
+        if (!n[r]) continue;
 #ifdef KEY_8B
         if (packed) {
             LayPacked::Pack pk;
             pk.bu = key_u(pack_plan->base);
             pk.span = pack_plan->span;
             pk.s1 = pack_plan->s1;
-            sampled_scatter(ws, in, n, out, dig, nbins, cursor, cap_end, pk, pack_bad, st);
+            sampled_scatter(ws, in[r], n[r], out[r], dig, nbins, R.cursor[r], R.cap_end[r], pk,
+                            pack_bad, st);
         } else
 #endif
         {
             (void)pack_bad;
-            sampled_scatter(ws, in, n, out, dig, nbins, cursor, cap_end, PackNone(),
-                            (unsigned int*)nullptr, st);
+            sampled_scatter(ws, in[r], n[r], out[r], dig, nbins, R.cursor[r], R.cap_end[r],
+                            PackNone(), (unsigned int*)nullptr, st);
         }
     }
-    hipLaunchKernelGGL(k_regions_done, dim3(1), dim3(256), 0, st, seg_start, cursor,
-                       cap_end, nbins, hist_out, seg_cnt, flag_dev);
+    hipLaunchKernelGGL(k_regions_done, dim3(nrel), dim3(256), 0, st, R, nbins, flag_dev);
     SMJ_CHECK(hipGetLastError());
 }
 

@@ -154,15 +154,20 @@ void plan_partition_packed(Workspace* ws, const Tup* in, uint64_t n, uint64_t* o
 // sampled level-1 partition (join): regions with slack, no histogram pass
 uint64_t sampled_capacity(uint64_t n, uint32_t dbits);
 // every partition is kShards segments: seg_start/seg_cnt[d * kShards + q]
-constexpr uint32_t kShards = 8;
-// `out` holds sampled_capacity() elements: tuples, or (pack_plan != nullptr,
+#ifndef SMJ_SHARDS
+#define SMJ_SHARDS 8
+#endif
+constexpr uint32_t kShards = SMJ_SHARDS;
+// Sampled level-1 partition of nrel (1 or 2) relations in shared launches.
+// out[r] holds sampled_capacity() elements: tuples, or (pack_plan != nullptr,
 // 16-byte tuples only) LayPacked words for that plan; *pack_bad is OR-ed with
 // 1 when a tuple cannot be packed (the caller then repeats on tuples).
-void sampled_partition(Workspace* ws, const Tup* in, uint64_t n, void* out,
-                       const RangePlan* plan_dev, uint32_t dbits,
-                       uint64_t* starts_dev, int64_t* hist_out,
-                       uint64_t* seg_start, int64_t* seg_cnt,
-                       unsigned int* flag_dev, hipStream_t st,
+// `sample` = nrel * 2^dbits counters, zeroed by the caller (k_join_begin).
+void sampled_partition(Workspace* ws, int nrel, const Tup* const* in, const uint64_t* n,
+                       void* const* out, const RangePlan* plan_dev, uint32_t dbits,
+                       unsigned int* sample, uint64_t* const* starts_dev,
+                       int64_t* const* hist_out, uint64_t* const* seg_start,
+                       int64_t* const* seg_cnt, unsigned int* flag_dev, hipStream_t st,
                        const RangePlan* pack_plan = nullptr,
                        unsigned int* pack_bad = nullptr);
 void hist_memcpy(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
