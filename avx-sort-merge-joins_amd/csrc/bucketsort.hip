@@ -79,7 +79,9 @@ constexpr int GS_CAP = GS_THREADS * GS_ITEMS;   // tuples per group per relation
 constexpr int GS_D3MAX = GS_CAP >= 2048 ? 11 : 10;  // level-3 bits sorted in LDS
 constexpr int GS_BPT = (1 << GS_D3MAX) / GS_THREADS;  // d3 bins per thread
 constexpr int GS_NB3 = 1 << GS_D3MAX;
-constexpr int GS_TMAX = 128;    // tiles per bucket on the fast path (two per lane of one wave)
+// tiles per bucket on the fast path: TPL per lane of the relation's wave
+// (k_groupsort<Lay, TPL>, TPL = 2 or 4: 128 or 256 tiles)
+constexpr int GS_TMAX = 256;
 constexpr int GS_WIN = GS_CAP / 64;
 constexpr int GS_RUNMAX = 32;   // longest equal-digit run fixed serially
 static_assert(GS_CAP % 64 == 0 && GS_CAP % GS_THREADS == 0, "group capacity");
@@ -319,17 +321,19 @@ struct GroupLDS {
 
 // A group and, for the calling thread, its tile run: wave r < nrel owns
 // relation r, lane t its tile t (lo = run start in the tile, len = length).
+template <int TPL>
 struct GroupMeta {
     uint32_t b, g;
     uint32_t t0[2], nt[2];  // first tile and tile count of the bucket
     uint64_t bst[2];        // bucket start (partition buffer)
     uint64_t ost[2];        // bucket start (output)
-    uint32_t lo[2], len[2];  // tiles lane and lane + 64
-    uint32_t toff[2];        // their offsets from the bucket start
+    uint32_t lo[TPL], len[TPL];  // tiles lane + 64 h
+    uint32_t toff[TPL];          // their offsets from the bucket start
 };
 
+template <int TPL>
 __device__ __forceinline__ void load_meta(const GroupArgs& A, uint32_t gi,
-                                          GroupMeta& M, bool same_bucket) {
+                                          GroupMeta<TPL>& M, bool same_bucket) {
     const uint32_t b = gi / A.nb2;
     M.g = gi % A.nb2;
     const bool newb = !same_bucket || b != M.b;
@@ -354,16 +358,16 @@ __device__ __forceinline__ void load_meta(const GroupArgs& A, uint32_t gi,
     M.b = b;
     // the wave index is uniform: table pointers stay scalar
     const uint32_t wid = __builtin_amdgcn_readfirstlane(otid() >> 6), lane = otid() & 63;
-    M.lo[0] = M.len[0] = M.lo[1] = M.len[1] = 0;
-    M.toff[0] = M.toff[1] = 0;
+#pragma unroll
+    for (int h = 0; h < TPL; h++) M.lo[h] = M.len[h] = M.toff[h] = 0;
     if (wid < (uint32_t)A.nrel) {
         const uint32_t nt = wid ? M.nt[1] : M.nt[0];
         const uint32_t t0 = wid ? M.t0[1] : M.t0[0];
         const uint32_t ts = A.tt[wid].tstride;
 #pragma unroll
-        for (int h = 0; h < 2; h++) {
+        for (int h = 0; h < TPL; h++) {
             const uint32_t t = lane + 64 * h;
-            if (nt <= GS_TMAX && t < nt) {
+            if (nt <= 64 * TPL && t < nt) {
 #if SMJ_PREFT
                 // digit-major prefix: lanes read consecutive entries
                 const uint16_t* pf = A.tt[wid].prefT + (uint64_t)M.g * ts + t0 + t;
@@ -448,38 +452,43 @@ __device__ __forceinline__ void insertion_sort(typename Lay::W* a, uint32_t n) {
 // the number of runs that start before it (no block barrier inside; one at
 // the end).  The run of position j is then wk[j/64] + (starts in its window
 // up to j) - 1: two LDS round trips per gathered element, no search.
-template <class LDS>
+template <int TPL, class LDS>
 __device__ __forceinline__ void build_tables(const GroupArgs& A, LDS& L,
-                                             const GroupMeta& M) {
+                                             const GroupMeta<TPL>& M) {
     const uint32_t wid = otid() >> 6, lane = otid() & 63;
     if (wid < (uint32_t)A.nrel) {
         const int r = wid;
         const uint32_t nt = r ? M.nt[1] : M.nt[0];
         if (lane < GS_WIN) L.smap[r][lane] = 0ull;
-        // tiles lane and lane + 64: scan of (start in tile << 32 | length)
-        const unsigned long long p0 = ((unsigned long long)M.lo[0] << 32) | M.len[0];
-        const unsigned long long p1 = ((unsigned long long)M.lo[1] << 32) | M.len[1];
-        const unsigned long long i0 = wave_incl_scan64(p0);
-        const unsigned long long tot0 = __shfl(i0, 63, 64);
-        const unsigned long long i1 = wave_incl_scan64(p1) + tot0;
-        const unsigned long long tot = __shfl(i1, 63, 64);
-        const uint32_t sA = (uint32_t)(i0 - p0), sB = (uint32_t)(i1 - p1);
-        // non-empty runs in tile order = position order; run starts at or
-        // past GS_CAP only occur in groups that overflow (never gathered)
-        const bool eA = lane < nt && M.len[0] > 0 && sA < GS_CAP;
-        const bool eB = lane + 64 < nt && M.len[1] > 0 && sB < GS_CAP;
-        const uint64_t bA = __ballot(eA), bB = __ballot(eB);
-        const uint32_t kA = (uint32_t)__popcll(bA & lanemask_lt());
-        const uint32_t kB = (uint32_t)__popcll(bA) + (uint32_t)__popcll(bB & lanemask_lt());
-        if (eA) L.run[r][kA] = ((unsigned long long)(M.toff[0] + M.lo[0]) << 32) | sA;
-        if (eB) L.run[r][kB] = ((unsigned long long)(M.toff[1] + M.lo[1]) << 32) | sB;
+        // tiles lane + 64 h: scan of (start in tile << 32 | length), and the
+        // non-empty runs compacted in tile order = position order (run starts
+        // at or past GS_CAP only occur in groups that overflow: never gathered)
+        unsigned long long acc = 0;
+        uint32_t kacc = 0;
+        uint32_t s[TPL], k[TPL];
+        bool e[TPL];
+#pragma unroll
+        for (int h = 0; h < TPL; h++) {
+            const unsigned long long p = ((unsigned long long)M.lo[h] << 32) | M.len[h];
+            const unsigned long long incl = wave_incl_scan64(p) + acc;
+            acc = __shfl(incl, 63, 64);
+            s[h] = (uint32_t)(incl - p);
+            e[h] = lane + 64 * h < nt && M.len[h] > 0 && s[h] < GS_CAP;
+            const uint64_t bal = __ballot(e[h]);
+            k[h] = kacc + (uint32_t)__popcll(bal & lanemask_lt());
+            kacc += (uint32_t)__popcll(bal);
+        }
+#pragma unroll
+        for (int h = 0; h < TPL; h++)
+            if (e[h]) L.run[r][k[h]] = ((unsigned long long)(M.toff[h] + M.lo[h]) << 32) | s[h];
         if (lane == 0) {
-            L.n[r] = nt <= GS_TMAX ? (uint32_t)tot : 0xffffffffu;
-            L.off[r] = (uint32_t)(tot >> 32);
+            L.n[r] = nt <= 64 * TPL ? (uint32_t)acc : 0xffffffffu;
+            L.off[r] = (uint32_t)(acc >> 32);
         }
         wave_lds_sync();
-        if (eA) atomicOr(&L.smap[r][sA >> 6], 1ull << (sA & 63));
-        if (eB) atomicOr(&L.smap[r][sB >> 6], 1ull << (sB & 63));
+#pragma unroll
+        for (int h = 0; h < TPL; h++)
+            if (e[h]) atomicOr(&L.smap[r][s[h] >> 6], 1ull << (s[h] & 63));
         wave_lds_sync();
         const uint32_t c = lane < GS_WIN ? (uint32_t)__popcll(L.smap[r][lane]) : 0u;
         const uint32_t incl = wave_incl_scan32(c);
@@ -492,9 +501,9 @@ __device__ __forceinline__ void build_tables(const GroupArgs& A, LDS& L,
 // queued: its size and offset in each relation come from the prefix table,
 // its tuples are sorted and counted afterwards by the skew kernels below, over
 // many workgroups.  Called by the whole workgroup (uniform control flow).
-template <class LDS>
+template <class LDS, class Meta>
 __device__ __forceinline__ void group_overflow(const GroupArgs& A, LDS& L,
-                                               const GroupMeta& M) {
+                                               const Meta& M) {
     uint32_t nn[2] = {0, 0};
     uint64_t oo[2] = {0, 0};
     const uint32_t tid = otid();
@@ -537,9 +546,9 @@ __device__ __forceinline__ void group_overflow(const GroupArgs& A, LDS& L,
 // = k * GS_THREADS + thread: a wave's 64 positions share one bitmap window
 // (broadcast reads), its run is found with a lane count of the window's
 // run starts.
-template <class Lay>
+template <class Lay, class Meta>
 __device__ __forceinline__ void gather_group(const GroupArgs& A, GroupLDS<typename Lay::W>& L,
-                                             const GroupMeta& C, int r, uint32_t n,
+                                             const Meta& C, int r, uint32_t n,
                                              typename Lay::W (&v)[GS_ITEMS]) {
     if (n == 0) return;
     const typename Lay::W* tp = static_cast<const typename Lay::W*>(A.tmp[r]) + C.bst[r];
@@ -560,9 +569,9 @@ __device__ __forceinline__ void gather_group(const GroupArgs& A, GroupLDS<typena
 // as the elements sit in LDS (the registers are free): the persistent loop
 // issues the next group's gather there.  Returns false when the group must
 // take the skew path.
-template <class Lay, typename Hook>
+template <class Lay, class Meta, typename Hook>
 __device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS<typename Lay::W>& L,
-                                           const GroupMeta& C, const RangePlan& P,
+                                           const Meta& C, const RangePlan& P,
                                            int r, uint32_t nr, uint32_t off,
                                            typename Lay::W (&v)[GS_ITEMS], bool& clamped,
                                            Hook&& after_place) {
@@ -690,7 +699,7 @@ __device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS<typename
 // g's data is in registers, g+1's R is gathered as soon as g's R sits in LDS
 // and g+1's S as soon as g's S does, so both gathers fly under g's sort,
 // write-out and count; g+2's tile runs are loaded one group further ahead.
-template <class Lay>
+template <class Lay, int TPL>
 __global__ void __launch_bounds__(GS_THREADS, gs_wg_per_cu<typename Lay::W>() * GS_THREADS / 256)
 k_groupsort(GroupArgs A) {
     typedef typename Lay::W W;
@@ -706,10 +715,10 @@ k_groupsort(GroupArgs A) {
     if (gbeg >= gend) return;
 
     for (uint32_t i = tid; i < GS_NB3; i += GS_THREADS) (&L.cnt[0][0])[i] = 0u;
-    GroupMeta M;
+    GroupMeta<TPL> M;
     load_meta(A, gbeg, M, false);
     build_tables(A, L, M);
-    GroupMeta C = M;
+    GroupMeta<TPL> C = M;
     uint32_t cn[2], co[2];
 #pragma unroll
     for (int r = 0; r < 2; r++) {
@@ -728,7 +737,7 @@ k_groupsort(GroupArgs A) {
         const bool has_next = gi + 1 < gend;
         // every lane's gather of group gi has read the tables: rebuild them
         __syncthreads();
-        const GroupMeta N = M;
+        const GroupMeta<TPL> N = M;
         uint32_t nn[2] = {0, 0}, no[2] = {0, 0};
         if (has_next) {
             build_tables(A, L, N);
@@ -1511,10 +1520,32 @@ static void set_pass_attrs() {
     SMJ_CHECK(hipFuncSetAttribute((const void*)k_tilepass<Lay>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     // several workgroups per CU (launch bounds): ask for what one needs
-    SMJ_CHECK(hipFuncSetAttribute((const void*)k_groupsort<Lay>,
+    SMJ_CHECK(hipFuncSetAttribute((const void*)k_groupsort<Lay, 2>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)sizeof(GroupLDS<typename Lay::W>)));
+    SMJ_CHECK(hipFuncSetAttribute((const void*)k_groupsort<Lay, 4>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)sizeof(GroupLDS<typename Lay::W>)));
     done = true;
+}
+
+// Tile runs per lane of the group pass: 2 (128 tiles per bucket) unless the
+// expected largest bucket (mean + 1/4, plus one partial tile per segment)
+// needs more, then 4 (256).  A bucket beyond that takes the skew path.
+static int group_tpl(uint64_t nmax, uint32_t nb, uint32_t nseg) {
+    const uint64_t per = nmax / (nb ? nb : 1);
+    const uint64_t tiles = (per + per / 4) / TILE2 + nseg + 1;
+    return tiles <= 128 ? 2 : 4;
+}
+
+template <class Lay>
+static void launch_groupsort(int tpl, uint32_t nwg, hipStream_t st, const GroupArgs& G) {
+    if (tpl == 4)
+        hipLaunchKernelGGL((k_groupsort<Lay, 4>), dim3(nwg), dim3(GS_THREADS),
+                           sizeof(GroupLDS<typename Lay::W>), st, G);
+    else
+        hipLaunchKernelGGL((k_groupsort<Lay, 2>), dim3(nwg), dim3(GS_THREADS),
+                           sizeof(GroupLDS<typename Lay::W>), st, G);
 }
 
 // Bucket pass without a host synchronisation before the kernels (sampled
@@ -1615,8 +1646,8 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
     {
         const uint32_t nwg = (ngroups + G.per - 1) / G.per;
         TraceScope ts(ws, "k_groupsort", st);
-        hipLaunchKernelGGL(k_groupsort<Lay>, dim3(nwg), dim3(GS_THREADS),
-                           sizeof(GroupLDS<W>), st, G);
+        const uint64_t nmax = nrel > 1 && a.n[1] > a.n[0] ? a.n[1] : a.n[0];
+        launch_groupsort<Lay>(group_tpl(nmax, nb, a.nseg), nwg, st, G);
     }
     SMJ_CHECK(hipGetLastError());
     if (a.ev_ovf) SMJ_CHECK(hipEventRecord(a.ev_ovf, st));
@@ -1658,7 +1689,7 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
     if (!attr) {
         SMJ_CHECK(hipFuncSetAttribute((const void*)k_preft,
                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      PT_TILES * ((1 << 9) + 1) * 2));
+                                      PT_TILES * ((1 << kMaxD2) + 1) * 2));
         attr = true;
     }
     set_pass_attrs<LayTup>();
@@ -1802,8 +1833,8 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
         G.per = (ng + maxwg - 1) / maxwg;
         const uint32_t nwg = (ng + G.per - 1) / G.per;
         TraceScope ts(ws, "k_groupsort", st);
-        hipLaunchKernelGGL(k_groupsort<LayTup>, dim3(nwg), dim3(GS_THREADS),
-                           sizeof(GroupLDS<Tup>), st, G);
+        const uint64_t nmax = nrel > 1 && a.n[1] > a.n[0] ? a.n[1] : a.n[0];
+        launch_groupsort<LayTup>(group_tpl(nmax, nb, nseg), nwg, st, G);
     }
     SMJ_CHECK(hipGetLastError());
     if (a.ev_ovf) SMJ_CHECK(hipEventRecord(a.ev_ovf, st));

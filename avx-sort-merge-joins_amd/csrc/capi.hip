@@ -130,18 +130,20 @@ static void choose_levels(uint64_t n, uint32_t want_d1, uint32_t* D1,
     const uint64_t target = kGroupTarget;
     uint32_t B = n > target ? ceil_log2((n + target - 1) / target) : 0;
     // level 1: 512 partitions by default (the scatter's write streams stay
-    // long enough), more when a bucket would exceed ~96 tiles of the tile pass
+    // long enough), more when a bucket would exceed ~192 tiles of the tile
+    // pass (the group pass takes up to 256 per bucket): N1024 keeps 2^10
+    // partitions, within the sampled scatter's LDS carries
     uint32_t d1 = want_d1 ? want_d1 : 9;
-    const uint64_t bucket_cap = 96ull * kTileTuples;
+    const uint64_t bucket_cap = 192ull * kTileTuples;
     while (d1 < kNarrowDigitBits && (n >> d1) > bucket_cap) d1++;
     if (d1 > B) d1 = B;
     if (d1 > kNarrowDigitBits) d1 = kNarrowDigitBits;
     uint32_t d2 = B > d1 ? B - d1 : 0;
-    if (d2 > 9) d2 = 9;
+    if (d2 > kMaxD2) d2 = kMaxD2;
     *D1 = d1;
     *D2 = d2;
     // the plan may add up to two level-2 bits to make the last digit exact
-    *D2cap = d2 + 2 > 9 ? (d2 > 9 ? d2 : 9) : d2 + 2;
+    *D2cap = d2 + 2 < kMaxD2 ? d2 + 2 : (d2 > kMaxD2 ? d2 : kMaxD2);
 }
 
 // level-1 partition of sorts and joins: sampled regions (no histogram pass)
@@ -1171,8 +1173,8 @@ void smj_dev_join_segmented(smj_workspace* wsp, void* R, uint64_t nR,
     const uint32_t tot_bits = D1 + D2;
     D1 = bucket_bits;
     D2 = tot_bits > D1 ? tot_bits - D1 : 0;
-    if (D2 > 9) D2 = 9;
-    D2cap = D2 + 2 > 9 ? (D2 > 9 ? D2 : 9) : D2 + 2;
+    if (D2 > kMaxD2) D2 = kMaxD2;
+    D2cap = D2 + 2 < kMaxD2 ? D2 + 2 : (D2 > kMaxD2 ? D2 : kMaxD2);
     RangePlan hplan = make_plan(key_lo, key_hi, D1, D2, D2cap, kGroupD3Max);
     const bool packed = (flags & SMJ_SEG_PACKED) != 0;
 #ifdef KEY_8B

@@ -1689,7 +1689,10 @@ void plan_partition_packed(Workspace* ws, const Tup* in, uint64_t n, uint64_t* o
 #ifndef SMJ_SC_WG_PER_CU
 #define SMJ_SC_WG_PER_CU 1
 #endif
-static constexpr uint32_t kSampleStride = 128;
+#ifndef SMJ_SAMPLE_STRIDE
+#define SMJ_SAMPLE_STRIDE 128
+#endif
+static constexpr uint32_t kSampleStride = SMJ_SAMPLE_STRIDE;
 static constexpr uint64_t kRegionSlack = 1024;  // per shard
 
 uint64_t sampled_capacity(uint64_t n, uint32_t dbits) {

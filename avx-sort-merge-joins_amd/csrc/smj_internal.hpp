@@ -10,6 +10,9 @@
 namespace smj {
 
 constexpr uint32_t kNarrowDigitBits = 12;  // widest digit of a single pass
+// widest level-2 digit (groups per bucket): k_preft stages 64 prefix rows of
+// 2^kMaxD2 + 1 entries in LDS
+constexpr uint32_t kMaxD2 = 10;
 
 // reference partition digit (runtime mask/shift), see smj_common.hpp
 typedef RefDigit Digit32;

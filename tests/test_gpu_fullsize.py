@@ -104,3 +104,45 @@ def test_headline_join_full_bitexact(libs, oracles, width, dist_):
     assert count == orc.merge_join(wR, wS) == n
     np.testing.assert_array_equal(gR, wR)
     np.testing.assert_array_equal(gS, wS)
+
+
+def _checksum(torch, t):
+    """Order-independent checksum of (n, 2) rows (wrapping int64 sums)."""
+    k = t[:, 1].to(torch.int64)
+    p = t[:, 0].to(torch.int64)
+    mix = (k * 0x9E3779B1) ^ (p * 0x85EBCA77 + 0x165667B1)
+    return (int(k.sum()), int(p.sum()), int(mix.sum()))
+
+
+@pytest.mark.parametrize("dist_", ["uniform", "zipf"])
+def test_n1024_join_properties(libs, dist_):
+    """BASELINE configs[4] on one GPU (its 1-GPU point): R = S = 1024M
+    16-byte tuples, S uniform or Zipf 0.75.  The plan keeps 2^10 level-1
+    partitions (the sampled, packed path) with up to 256 tiles per bucket.
+    Count = |S|, outputs sorted by (key, payload), each a permutation of its
+    input (checksums); the oracle would need minutes on the host at this size."""
+    import torch
+    lib = libs[16]
+    n = 1_024_000_000
+    R, S = lib.empty(n), lib.empty(n)
+    lib.dev_gen_pk(R, 0, n, 12345)
+    if dist_ == "uniform":
+        lib.dev_gen_fk(S, 0, n, n, 54321)
+    else:
+        lib.dev_gen_zipf(S, 0, n, 0.75, 54321)
+    sR, sS = lib.empty(n), lib.empty(n)
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    lib.dev_join(R, S, sR, sS, cnt, 9, 1, n)
+    torch.cuda.synchronize()
+    assert int(cnt.item()) == n
+    for src, out in ((R, sR), (S, sS)):
+        k = out[:, 1]
+        dk = k[1:] - k[:-1]
+        assert bool((dk >= 0).all())
+        tie = dk == 0
+        p = out[:, 0]
+        assert bool((p[1:][tie] >= p[:-1][tie]).all())
+        del dk, tie
+        assert _checksum(torch, src) == _checksum(torch, out)
+    del R, S, sR, sS
+    _free(torch)
