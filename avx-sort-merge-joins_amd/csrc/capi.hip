@@ -758,16 +758,126 @@ uint64_t scalar_multiway_merge_bitand(tuple_t* output, relation_t** parts,
 // joins (reference src/joins/joincommon.c:239-312,
 // src/joins/sortmergejoin_multiway.c:50-61)
 // ---------------------------------------------------------------------------
-uint64_t merge_join(tuple_t* rtuples, tuple_t* stuples, const uint64_t numR,
-                    const uint64_t numS, void* output) {
-    if (output) {
-        fprintf(stderr, "[ERROR] smj: join materialisation is not supported "
-                        "(the reference's tuple_buffer.h is absent too)\n");
+// ---- materialised output (JOIN_MATERIALIZE; smj.h documents the buffer)
+chainedtuplebuffer_t* chainedtuplebuffer_init(void) {
+    return (chainedtuplebuffer_t*)calloc(1, sizeof(chainedtuplebuffer_t));
+}
+
+void chainedtuplebuffer_free(chainedtuplebuffer_t* cb) {
+    if (!cb) return;
+    free(cb->tuples);
+    free(cb);
+}
+
+uint64_t chainedtuplebuffer_tuples(chainedtuplebuffer_t* cb) { return cb ? cb->numtuples : 0; }
+
+// room for k more tuples at the end; returns where they go
+static tuple_t* cb_reserve(chainedtuplebuffer_t* cb, uint64_t k) {
+    if (cb->numtuples + k > cb->capacity) {
+        uint64_t cap = cb->capacity ? cb->capacity : 1024;
+        while (cap < cb->numtuples + k) cap *= 2;
+        tuple_t* t = (tuple_t*)realloc(cb->tuples, cap * sizeof(tuple_t));
+        if (!t) {
+            fprintf(stderr, "[ERROR] smj: cannot grow the result buffer to %llu tuples\n",
+                    (unsigned long long)cap);
+            abort();
+        }
+        cb->tuples = t;
+        cb->capacity = cap;
+    }
+    tuple_t* at = cb->tuples + cb->numtuples;
+    cb->numtuples += k;
+    return at;
+}
+
+tuple_t* cb_next_writepos(chainedtuplebuffer_t* cb) { return cb_reserve(cb, 1); }
+
+// the matches of sorted device runs R and S, appended to cb (two device
+// passes: the count sizes the device buffer, the second writes it)
+static uint64_t materialize_append(const Tup* r, uint64_t nR, const Tup* s, uint64_t nS,
+                                   chainedtuplebuffer_t* cb) {
+    Ctx& c = ctx();
+    smj_workspace* ws = (smj_workspace*)&c.ws;
+    const uint64_t total = smj_dev_materialize(ws, (const tuple_t*)r, nR, (const tuple_t*)s,
+                                               nS, nullptr, 0, c.st);
+    if (total == 0) return 0;
+    Tup* o = (Tup*)c.ws.scratch("api_mat", total * sizeof(Tup));
+    const uint64_t got = smj_dev_materialize(ws, (const tuple_t*)r, nR, (const tuple_t*)s, nS,
+                                             (tuple_t*)o, total, c.st);
+    if (got != total) {
+        fprintf(stderr, "[ERROR] smj: materialisation count changed (%llu, %llu)\n",
+                (unsigned long long)total, (unsigned long long)got);
         abort();
     }
+    tuple_t* dst = cb_reserve(cb, total);
+    SMJ_CHECK(hipMemcpyAsync(dst, o, total * sizeof(Tup), hipMemcpyDeviceToHost, c.st));
+    sync();
+    return total;
+}
+
+static int g_materialize = -1;  // -1: not decided yet (SMJ_MATERIALIZE)
+
+void smj_set_materialize(int on) { g_materialize = on ? 1 : 0; }
+
+static bool materialize_on() {
+    if (g_materialize < 0) {
+        const char* e = getenv("SMJ_MATERIALIZE");
+        g_materialize = (e && atoi(e) != 0) ? 1 : 0;
+    }
+    return g_materialize > 0;
+}
+
+// decimal of a signed 32-bit value into p; returns the end
+static char* put_i32(char* p, int32_t v) {
+    char tmp[12];
+    int k = 0;
+    uint32_t u = v < 0 ? 0u - (uint32_t)v : (uint32_t)v;
+    do {
+        tmp[k++] = (char)('0' + u % 10);
+        u /= 10;
+    } while (u);
+    if (v < 0) *p++ = '-';
+    while (k) *p++ = tmp[--k];
+    return p;
+}
+
+void write_result_relation(result_t* result, const char* filename) {
+    if (!result) return;
+    FILE* fp = fopen(filename, "a");
+    if (!fp) {
+        perror("write_result_relation");
+        return;
+    }
+    fprintf(fp, "#KEY, VAL\n");
+    const int T = result->nthreads > 0 ? result->nthreads : 1;
+    std::vector<char> buf(1 << 20);
+    for (int i = 0; i < T && result->resultlist; i++) {
+        chainedtuplebuffer_t* cb = (chainedtuplebuffer_t*)result->resultlist[i].results;
+        if (!cb) continue;
+        char* p = buf.data();
+        for (uint64_t j = 0; j < cb->numtuples; j++) {
+            if (p - buf.data() > (ptrdiff_t)buf.size() - 32) {
+                fwrite(buf.data(), 1, p - buf.data(), fp);
+                p = buf.data();
+            }
+            // generator.c:210 prints key and payload with %d
+            p = put_i32(p, (int32_t)cb->tuples[j].key);
+            *p++ = ' ';
+            p = put_i32(p, (int32_t)cb->tuples[j].payload);
+            *p++ = '\n';
+        }
+        fwrite(buf.data(), 1, p - buf.data(), fp);
+    }
+    fclose(fp);
+}
+
+uint64_t merge_join(tuple_t* rtuples, tuple_t* stuples, const uint64_t numR,
+                    const uint64_t numS, void* output) {
     Ctx& c = ctx();
     DevBuf r = dev_in(rtuples, numR, "api_jr", true);
     DevBuf s = dev_in(stuples, numS, "api_js", true);
+    if (output)  // JOIN_MATERIALIZE: output is the caller's chainedtuplebuffer_t
+        return materialize_append(r.d, numR, s.d, numS, (chainedtuplebuffer_t*)output);
     unsigned long long* cnt =
         (unsigned long long*)c.ws.scratch("api_cnt", sizeof(unsigned long long));
     SMJ_CHECK(hipMemsetAsync(cnt, 0, 8, c.st));
@@ -955,6 +1065,11 @@ static result_t* join_api(relation_t* relR, relation_t* relS,
         (threadresult_t*)calloc(joincfg->NTHREADS > 0 ? joincfg->NTHREADS : 1,
                                 sizeof(threadresult_t));
     res->resultlist[0].nresults = (int64_t)h;
+    if (materialize_on()) {
+        chainedtuplebuffer_t* cb = chainedtuplebuffer_init();
+        materialize_append(sR, nR, sS, nS, cb);
+        res->resultlist[0].results = cb;
+    }
     if (!getenv("SMJ_QUIET")) {
         float ms[5];
         smj_join_phase_ms((smj_workspace*)&c.ws, ms);
@@ -1035,6 +1150,11 @@ result_t* sortmergejoin_multipass(relation_t* relR, relation_t* relS,
         (threadresult_t*)calloc(joincfg->NTHREADS > 0 ? joincfg->NTHREADS : 1,
                                 sizeof(threadresult_t));
     res->resultlist[0].nresults = (int64_t)h;
+    if (materialize_on()) {
+        chainedtuplebuffer_t* cb = chainedtuplebuffer_init();
+        materialize_append(sR, nR, sS, nS, cb);
+        res->resultlist[0].results = cb;
+    }
     if (!getenv("SMJ_QUIET")) {
         double us = (t1.tv_sec - t0.tv_sec) * 1e6 + (t1.tv_usec - t0.tv_usec);
         fprintf(stderr, "NUM-TUPLES = %lld TOTAL-TIME-USECS = %.4lf ", (long long)nS, us);

@@ -150,8 +150,7 @@ k_scatter(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_arg,
     uint64_t* run = reinterpret_cast<uint64_t*>(lds_raw + TILE * sizeof(Tup));
     uint32_t* tstart = reinterpret_cast<uint32_t*>(run + nbins);
     uint16_t* wcnt = reinterpret_cast<uint16_t*>(tstart + nbins);
-    uint32_t* scr = reinterpret_cast<uint32_t*>(
-        (reinterpret_cast<uintptr_t>(wcnt + WAVES * nbins) + 15) & ~uintptr_t(15));
+    uint32_t* scr = reinterpret_cast<uint32_t*>(wcnt + ((WAVES * nbins + 7) & ~7u));
 
     const int lane = lane_id();
     const int wid = threadIdx.x >> 6;
@@ -512,8 +511,9 @@ k_scatter_swa(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
     const uint32_t hb = nbins / 2;
     u32x4_t* info = reinterpret_cast<u32x4_t*>(w32 + (size_t)W * hb);
     uint16_t* segown = reinterpret_cast<uint16_t*>(info + nbins);
-    uint32_t* scr = reinterpret_cast<uint32_t*>(
-        (reinterpret_cast<uintptr_t>(segown + (TILE / SEG + 2 * nbins)) + 15) & ~uintptr_t(15));
+    // plain pointer arithmetic (no integer casts): the scan scratch stays an
+    // LDS pointer, not a flat one that every vmcnt wait would have to cover
+    uint32_t* scr = reinterpret_cast<uint32_t*>(segown + ((TILE / SEG + 2 * nbins + 7) & ~7u));
 
     const int lane = lane_id();
     const int wid = threadIdx.x >> 6;
@@ -535,8 +535,12 @@ k_scatter_swa(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
 #pragma unroll
     for (int j = 0; j < ITEMS; j++) {
         const uint64_t i = beg + wbase + j * 64 + lane;
-        if (i < end) v[j] = in[i];
+        v[j] = in[i < end ? i : end - 1];
     }
+    // the first tile has landed: without this explicit wait the compiler's
+    // bookkeeping merges these loads into the loop header and re-waits with
+    // vmcnt(0) -- stores included -- at every tile
+    __builtin_amdgcn_s_waitcnt(0x0f70);
     __syncthreads();
     for (uint64_t base = beg; base < end; base += TILE) {
         const uint32_t tcount = (uint32_t)min((uint64_t)TILE, end - base);
@@ -607,7 +611,7 @@ k_scatter_swa(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
 #pragma unroll
         for (int j = 0; j < ITEMS; j++) {
             const uint64_t i = nb + wbase + j * 64 + lane;
-            if (i < end) nv[j] = in[i];
+            nv[j] = in[i < end ? i : end - 1];  // unconditional: a fixed count in flight
         }
         __syncthreads();
         // ---- stage the tile in digit order
@@ -625,6 +629,10 @@ k_scatter_swa(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
 #pragma unroll
             for (int w = 0; w < W; w++) w32[w * hb + t2] = 0;
         }
+        // the prefetch has landed (it flew under the ranking and staging): wait
+        // here, before the segment stores, so that the next tile does not wait
+        // for those stores to drain
+        __builtin_amdgcn_s_waitcnt(0x0f70);
         for (uint32_t q = threadIdx.x; q < nsegT * SEG; q += THREADS) {
             const uint32_t sg = q / SEG;
             const uint32_t d = segown[sg];

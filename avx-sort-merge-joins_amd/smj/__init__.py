@@ -48,6 +48,8 @@ REFERENCE_SYMBOLS = [
     "scalar_multiway_merge_modulo", "scalar_multiway_merge_bitand",
     "merge_join", "merge_join_interpolation", "print_timing", "sortmergejoin_multiway",
     "sortmergejoin_multipass", "sortmergejoin_mpsm", "sortmergejoin_initrun",
+    "chainedtuplebuffer_init", "chainedtuplebuffer_free", "chainedtuplebuffer_tuples",
+    "cb_next_writepos", "write_result_relation",
 ]
 DEVICE_SYMBOLS = [
     "smj_tuple_bytes", "smj_device_name", "smj_workspace_create",
@@ -57,6 +59,7 @@ DEVICE_SYMBOLS = [
     "smj_dev_gen_zipf", "smj_dev_synchronize", "smj_dev_partition_range",
     "smj_trace_enable", "smj_trace_reset", "smj_trace_read", "smj_dev_join_segmented",
     "smj_dev_partition_range_packed", "smj_dev_materialize", "smj_selfcheck_lds_order",
+    "smj_set_materialize",
 ]
 
 
@@ -88,6 +91,12 @@ class ThreadResult(C.Structure):
 class Result(C.Structure):
     _fields_ = [("totalresults", C.c_int64),
                 ("resultlist", C.POINTER(ThreadResult)), ("nthreads", C.c_int)]
+
+
+class ChainedTupleBuffer(C.Structure):
+    """include/smj.h: the library's chainedtuplebuffer_t (one growable array)."""
+    _fields_ = [("tuples", C.c_void_p), ("numtuples", C.c_uint64),
+                ("capacity", C.c_uint64)]
 
 
 _P = C.c_void_p
@@ -135,6 +144,12 @@ class Library:
             "sortmergejoin_multiway": (C.POINTER(Result), [_P, _P, _P]),
             "sortmergejoin_multipass": (C.POINTER(Result), [_P, _P, _P]),
             "sortmergejoin_mpsm": (C.POINTER(Result), [_P, _P, _P]),
+            "chainedtuplebuffer_init": (C.POINTER(ChainedTupleBuffer), []),
+            "chainedtuplebuffer_free": (None, [_P]),
+            "chainedtuplebuffer_tuples": (_U64, [_P]),
+            "cb_next_writepos": (_P, [_P]),
+            "write_result_relation": (None, [_P, C.c_char_p]),
+            "smj_set_materialize": (None, [C.c_int]),
             "smj_tuple_bytes": (C.c_int, []),
             "smj_device_name": (C.c_char_p, []),
             "smj_workspace_create": (_P, []),
@@ -246,10 +261,38 @@ class Library:
         s = np.ascontiguousarray(s, dtype=self.dtype)
         return int(self.lib.merge_join(_ptr(r), _ptr(s), len(r), len(s), None))
 
+    def _take_buffer(self, cb) -> np.ndarray:
+        """Copy a chainedtuplebuffer_t's tuples out (the buffer is not freed)."""
+        n = int(self.lib.chainedtuplebuffer_tuples(cb))
+        if n == 0:
+            return np.zeros(0, self.dtype)
+        b = C.cast(cb, C.POINTER(ChainedTupleBuffer)).contents
+        raw = C.string_at(b.tuples, n * self.width)
+        return np.frombuffer(raw, dtype=self.dtype).copy()
+
+    def merge_join_materialize(self, r, s, prefix=None):
+        """merge_join with an output buffer (JOIN_MATERIALIZE).  `prefix`:
+        tuples written into the buffer with cb_next_writepos first (the
+        matches are appended after them).  Returns (count, buffer tuples)."""
+        r = np.ascontiguousarray(r, dtype=self.dtype)
+        s = np.ascontiguousarray(s, dtype=self.dtype)
+        cb = self.lib.chainedtuplebuffer_init()
+        try:
+            for t in (prefix if prefix is not None else []):
+                p = self.lib.cb_next_writepos(cb)
+                C.memmove(p, np.array([t], self.dtype).ctypes.data, self.width)
+            n = int(self.lib.merge_join(_ptr(r), _ptr(s), len(r), len(s), cb))
+            return n, self._take_buffer(cb)
+        finally:
+            self.lib.chainedtuplebuffer_free(cb)
+
     def sortmergejoin_multiway(self, R, S, nthreads=1, fanout=128, mpsm=False,
-                               algo=None):
+                               algo=None, materialize=False, persist=None):
         """algo: "m-way" (default), "m-pass" or "mpsm" -- the reference's
-        sortmergejoins -a choices (src/main.c:455-466)."""
+        sortmergejoins -a choices (src/main.c:455-466).  materialize: also
+        return the output tuples (JOIN_MATERIALIZE); persist: a file name the
+        result is appended to with write_result_relation (PERSIST_RELATIONS).
+        Returns the count, or (count, output tuples)."""
         R = np.ascontiguousarray(R, dtype=self.dtype)
         S = np.ascontiguousarray(S, dtype=self.dtype)
         cfg = JoinConfig(nthreads, fanout, int(self.width == 16), int(self.width == 16),
@@ -259,16 +302,31 @@ class Library:
         fn = {"m-way": self.lib.sortmergejoin_multiway,
               "m-pass": self.lib.sortmergejoin_multipass,
               "mpsm": self.lib.sortmergejoin_mpsm}[algo]
-        res = fn(C.byref(rr), C.byref(rs), C.byref(cfg))
+        if materialize or persist:
+            self.lib.smj_set_materialize(1)
+        try:
+            res = fn(C.byref(rr), C.byref(rs), C.byref(cfg))
+        finally:
+            if materialize or persist:
+                self.lib.smj_set_materialize(0)
         if not res:
             return None
         total = int(res.contents.totalresults)
+        out = None
+        if materialize or persist:
+            if persist:  # main.c:609-614
+                self.lib.write_result_relation(C.cast(res, _P), os.fsencode(persist))
+            lists = [res.contents.resultlist[i].results for i in range(max(nthreads, 1))]
+            out = np.concatenate([self._take_buffer(cb) for cb in lists if cb] or
+                                 [np.zeros(0, self.dtype)])
+            for cb in lists:  # main.c:621-626
+                self.lib.chainedtuplebuffer_free(cb)
         # the caller frees the result (src/main.c:629-632)
         libc = C.CDLL(None)
         libc.free.argtypes = [C.c_void_p]
         libc.free(res.contents.resultlist)
         libc.free(C.cast(res, C.c_void_p))
-        return total
+        return total if out is None else (total, out)
 
     # ---------------------------------------------------------------- device
     @property

@@ -228,11 +228,50 @@ uint64_t scalar_multiway_merge_bitand(tuple_t * output, relation_t ** parts,
 /* src/joins/sortmergejoin_multiway.h:37-38, sortmergejoin_mpsm.h).          */
 /* ------------------------------------------------------------------------ */
 
+/* Materialised join output (the reference's JOIN_MATERIALIZE build,
+ * joincommon.c:256-289, sortmergejoin_multiway.c:565-598, main.c:609-626).
+ * The reference takes chainedtuplebuffer_t and its functions from
+ * tuple_buffer.h, which is not in its tree, so this is the library's own
+ * definition of that interface: one growable host array holding one
+ * <S.key, S.payload> tuple per match, in merge_join's R-major order (per key,
+ * the S run repeated |R_k| times, keys ascending).  A pointer returned by
+ * cb_next_writepos stays valid until the next write. */
+#ifndef SMJ_TUPLE_BUFFER
+#define SMJ_TUPLE_BUFFER
+typedef struct chainedtuplebuffer_t {
+    tuple_t * tuples;
+    uint64_t  numtuples;
+    uint64_t  capacity;
+} chainedtuplebuffer_t;
+chainedtuplebuffer_t * chainedtuplebuffer_init(void);
+/* NULL is a no-op (main.c:621-626 frees every thread's list) */
+void chainedtuplebuffer_free(chainedtuplebuffer_t * cb);
+uint64_t chainedtuplebuffer_tuples(chainedtuplebuffer_t * cb);
+tuple_t * cb_next_writepos(chainedtuplebuffer_t * cb);
+#endif /* SMJ_TUPLE_BUFFER */
+
 /* joincommon.c:239-312: number of (r, s) pairs with equal key between two
- * sorted runs, duplicates on both sides included. `output` must be NULL
- * (materialisation does not build in the reference either). */
+ * sorted runs, duplicates on both sides included.  A non-NULL `output` is a
+ * chainedtuplebuffer_t that receives the matches appended (JOIN_MATERIALIZE);
+ * they are produced on the device (smj_dev_materialize) and copied back. */
 uint64_t merge_join(tuple_t * rtuples, tuple_t * stuples, const uint64_t numR,
                     const uint64_t numS, void * output);
+
+/* Materialisation switch of the join entry points (the reference decides it
+ * at compile time with -DJOIN_MATERIALIZE; the library cannot see the
+ * caller's flags): on, sortmergejoin_multiway / _multipass / _mpsm hand the
+ * whole output in result->resultlist[0].results as a chainedtuplebuffer_t
+ * (the other threads' lists stay NULL).  Default: the environment variable
+ * SMJ_MATERIALIZE (unset = off). */
+void smj_set_materialize(int on);
+
+/* main.c:609-614 (PERSIST_RELATIONS + JOIN_MATERIALIZE): append the
+ * materialised result to `filename` in the text format of write_relation
+ * (src/datagen/generator.c:200-213): a "#KEY, VAL" line, then "key payload"
+ * per tuple, both printed with %d as the reference does (for 16-byte tuples
+ * that is the low 32 bits of each field, what its int64 arguments print as
+ * on x86-64).  The reference calls this function but never defines it. */
+void write_result_relation(result_t * result, const char * filename);
 
 /* joincommon.c:214-227: the drivers' timing line ("NUM-TUPLES = ...
  * TOTAL-TIME-USECS = ... TUPLES-PER-SECOND = ..."), host-side.  Declared in

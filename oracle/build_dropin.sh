@@ -44,6 +44,10 @@ for w in 8 16; do
     build bench_multiwaymerge $w "$S/bench/multiwaymergebench.c" "$T/testutil.c"
     build sortmergejoins $w "$S/main.c" $GEN "$S/util/memalloc.c" "$S/util/numa_shuffle.c"
     build tputbench $w "$S/bench/tputbench.c" $GEN "$S/util/memalloc.c" "$S/util/numa_shuffle.c"
+    # main.c as built with --enable-materialize --enable-persist (Makefile.am:44-50):
+    # R.tbl / S.tbl from the generators, the join output in Out.tbl
+    build sortmergejoins_mat $w -DJOIN_MATERIALIZE -DPERSIST_RELATIONS "$S/main.c" $GEN \
+        "$S/util/memalloc.c" "$S/util/numa_shuffle.c"
 done
 # sortbench.c sorts 8-byte items with avxsort_int64/avxsortmultiway_int64
 buildxx bench_sort 8 "$S/bench/sortbench.c" "$T/testutil.c" $GEN

@@ -9,6 +9,8 @@ import os
 import re
 import subprocess
 
+import numpy as np
+
 import pytest
 
 from conftest import ROOT
@@ -135,3 +137,40 @@ def test_tputbench_ab_against_reference(w, nthreads):
     args = ["-a", "tputbench", "-n", str(nthreads), "-r", "1000000", "-s", "1000000",
             "--non-unique"] + SCALAR[w]
     assert results(run([exe] + args)) == results(run([ref] + args))
+
+
+def _table(path):
+    """a write_relation file (generator.c:200-213): '#KEY, VAL' + 'key payload'"""
+    lines = open(path).read().splitlines()
+    assert lines[0] == "#KEY, VAL"
+    a = np.array([ln.split() for ln in lines[1:]], dtype=np.int64).reshape(-1, 2)
+    t = np.zeros(len(a), [("payload", "<i8"), ("key", "<i8")])
+    t["key"], t["payload"] = a[:, 0], a[:, 1]
+    return t
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w", [8, 16])
+def test_reference_driver_materialize_persist(w, tmp_path):
+    """src/main.c built with JOIN_MATERIALIZE + PERSIST_RELATIONS (the
+    reference's --enable-materialize --enable-persist) on the MI355X library:
+    it writes its generated R.tbl and S.tbl, joins, and persists the matches
+    with write_result_relation to Out.tbl.  Out.tbl must hold, per key in
+    ascending order, the S run (in (key, payload) order) |R_k| times --
+    merge_join's R-major output (joincommon.c:267-287) over the sorted
+    relations the driver itself wrote."""
+    from test_gpu_materialize import numpy_materialize
+    exe = binary(f"sortmergejoins_mat{w}")
+    env = dict(os.environ, SMJ_QUIET="1")
+    r = subprocess.run([exe, "-a", "m-way", "-n", "4", "-r", "200000", "-s", "300000"]
+                       + SCALAR[w], capture_output=True, text=True, timeout=300,
+                       cwd=str(tmp_path), env=env)
+    total = results(r)
+    R, S = _table(tmp_path / "R.tbl"), _table(tmp_path / "S.tbl")
+    assert len(R) == 200000 and len(S) == 300000
+    out = _table(tmp_path / "Out.tbl")
+    exp = numpy_materialize(np.sort(R, order=["key", "payload"]),
+                            np.sort(S, order=["key", "payload"]))
+    assert total == len(exp) == len(out)
+    assert np.array_equal(out["key"], exp["key"])
+    assert np.array_equal(out["payload"], exp["payload"])
