@@ -62,17 +62,22 @@ constexpr int GS_THREADS = SMJ_GS_THREADS;      // one workgroup per group
 // resident group-pass workgroups per CU: 16-byte elements (LDS- and
 // VGPR-bound) and 8-byte ones (tuples or packed words)
 #ifndef SMJ_GS_WG_PER_CU
-#define SMJ_GS_WG_PER_CU 4
+#define SMJ_GS_WG_PER_CU 2
 #endif
 #ifndef SMJ_GS_WG_PER_CU8
-#define SMJ_GS_WG_PER_CU8 5
+#define SMJ_GS_WG_PER_CU8 4
 #endif
 template <class W>
 constexpr int gs_wg_per_cu() {
     return sizeof(W) == 16 ? SMJ_GS_WG_PER_CU : SMJ_GS_WG_PER_CU8;
 }
+// 2560 elements per relation: the plan's groups average 2048, so a group's
+// run in an 8192-element tile is ~64 words (512 B) and the gathers waste less
+// of the partial 128-byte lines at run ends than with 1280 (1024 on average,
+// 256 B runs): 128M x 128M join, group pass 16 B 1.50 -> 1.39 ms, 8 B 1.29 ->
+// 1.16 ms; 3072 loses (3 workgroups per CU)
 #ifndef SMJ_GS_ITEMS
-#define SMJ_GS_ITEMS (1280 / SMJ_GS_THREADS)
+#define SMJ_GS_ITEMS (2560 / SMJ_GS_THREADS)
 #endif
 constexpr int GS_ITEMS = SMJ_GS_ITEMS;          // tuples per thread per relation
 constexpr int GS_CAP = GS_THREADS * GS_ITEMS;   // tuples per group per relation

@@ -420,7 +420,8 @@ k_swa_lab(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_arg,
             if (addr >= p && addr < p + I[1]) {
                 const uint32_t e = addr - p;
                 const uint32_t k = I[3] >> 16;
-                out[addr] = e < k ? carry[d * CW + e] : stage[I[2] + e - k];
+                const Tup x = e < k ? carry[d * CW + e] : stage[I[2] + e - k];
+                if (!(FIX & 8) || addr == 0xffffffffu) out[addr] = x;  // 8: no stores
             }
         }
         __syncthreads();
@@ -441,6 +442,257 @@ k_swa_lab(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_arg,
         for (int j = 0; j < ITEMS; j++) v[j] = nv[j];
     }
     // ---- the partial last segment of every region
+    if (owner) {
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const uint32_t d = 2 * t2 + h;
+            for (uint32_t e = 0; e < kc[h]; e++) out[pos[h] + e] = carry[d * CW + e];
+        }
+    }
+}
+
+// k_swb: k_swa_lab restructured for LDS latency -- every LDS phase issues
+// its reads as a batch before using them (no per-item branches on full
+// tiles, invalid items go to a dump slot), the segment-store loop handles 4
+// stores per thread per trip, the carry is read into registers before it is
+// rewritten.  FIX 8: no global stores (measurement only).
+template <int THREADS, int ITEMS>
+struct SwbGeom {
+    static constexpr int W = THREADS / 64;
+    static constexpr int TILE = THREADS * ITEMS;
+    static constexpr uint32_t SEG = 64 / sizeof(Tup);
+    static constexpr uint32_t CW = SEG - 1;
+    // stage Tup[TILE + SEG] (dump slot) | carry Tup[B][CW] | counters u32[W][B/2] |
+    // info u32x4[B] | segown u16[TILE/SEG + 2B] | scan scratch
+    static __host__ __device__ constexpr size_t lds_bytes(uint32_t B) {
+        return (size_t)(TILE + SEG) * sizeof(Tup) + (size_t)B * CW * sizeof(Tup) +
+               (size_t)W * B * 2 + (size_t)B * 16 +
+               ((size_t)(TILE / SEG + 2 * B) * 2 + 15) / 16 * 16 + 128;
+    }
+};
+
+template <bool FULL, int THREADS, int ITEMS, class DigitL>
+__device__ __forceinline__ void swb_rank(const Tup (&v)[ITEMS], uint32_t (&dg)[ITEMS],
+                                         uint32_t (&rk)[ITEMS], uint32_t* w32, uint32_t hb,
+                                         uint32_t wbase, uint32_t tcount, const DigitL& dig) {
+    const int lane = lane_id();
+    const int wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int j = 0; j < ITEMS; j++) {
+        const bool valid = FULL || wbase + j * 64 + lane < tcount;
+        const uint32_t d = dig(v[j]);
+        const uint32_t sh = (d & 1u) * 16u;
+        const uint32_t old = atomicAdd(&w32[wid * hb + (d >> 1)], valid ? 1u << sh : 0u);
+        rk[j] = (old >> sh) & 0xffffu;
+        dg[j] = valid ? d : 0xffffffffu;
+    }
+}
+
+template <int THREADS, int ITEMS, class Digit, int FIX>
+__global__ void __launch_bounds__(THREADS)
+k_swb(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_arg,
+      uint32_t nbins, const uint32_t* __restrict__ counts, uint32_t nwg,
+      const uint64_t* __restrict__ starts, Tup* __restrict__ out, uint32_t hsub) {
+    typedef SwbGeom<THREADS, ITEMS> G;
+    constexpr int W = G::W;
+    constexpr int TILE = G::TILE;
+    constexpr uint32_t SEG = G::SEG;
+    constexpr uint32_t CW = G::CW;
+    constexpr int U = 4;  // segment stores per thread per trip
+    const auto dig = dig_arg.load();
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    Tup* stage = reinterpret_cast<Tup*>(lds_raw);
+    Tup* carry = stage + TILE + SEG;
+    uint32_t* w32 = reinterpret_cast<uint32_t*>(carry + (size_t)nbins * CW);
+    const uint32_t hb = nbins / 2;
+    u32x4_t* info = reinterpret_cast<u32x4_t*>(w32 + (size_t)W * hb);
+    uint16_t* segown = reinterpret_cast<uint16_t*>(info + nbins);
+    uint32_t* scr = reinterpret_cast<uint32_t*>(segown + ((TILE / SEG + 2 * nbins + 7) & ~7u));
+
+    const int lane = lane_id();
+    const int wid = threadIdx.x >> 6;
+    const uint32_t t2 = threadIdx.x;
+    const bool owner = t2 < hb;
+    uint32_t pos[2] = {0, 0}, kc[2] = {0, 0};
+    if (owner) {
+#pragma unroll
+        for (int h = 0; h < 2; h++)
+            pos[h] = (uint32_t)(starts[2 * t2 + h] +
+                                counts[(uint64_t)(2 * t2 + h) * nwg * hsub + blockIdx.x * hsub]);
+    }
+    for (uint32_t q = threadIdx.x; q < W * hb; q += THREADS) w32[q] = 0;
+    const uint64_t beg = (uint64_t)blockIdx.x * chunk;
+    const uint64_t end = min(beg + chunk, n);
+    const uint32_t wbase = wid * 64 * ITEMS;
+    Tup v[ITEMS], nv[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; j++) {
+        const uint64_t i = beg + wbase + j * 64 + lane;
+        v[j] = in[i < end ? i : end - 1];
+    }
+    __builtin_amdgcn_s_waitcnt(0x0f70);
+    __syncthreads();
+    for (uint64_t base = beg; base < end; base += TILE) {
+        const uint32_t tcount = (uint32_t)min((uint64_t)TILE, end - base);
+        uint32_t dg[ITEMS], rk[ITEMS];
+        if (tcount == TILE)
+            swb_rank<true, THREADS, ITEMS>(v, dg, rk, w32, hb, wbase, tcount, dig);
+        else
+            swb_rank<false, THREADS, ITEMS>(v, dg, rk, w32, hb, wbase, tcount, dig);
+        __syncthreads();
+        uint32_t cw[W];
+        uint32_t c[2] = {0, 0}, E[2] = {0, 0}, ns[2] = {0, 0};
+        if (owner) {
+#pragma unroll
+            for (int w = 0; w < W; w++) {
+                cw[w] = w32[w * hb + t2];
+                c[0] += cw[w] & 0xffffu;
+                c[1] += cw[w] >> 16;
+            }
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const uint32_t T = kc[h] + c[h];
+                const uint32_t m = (pos[h] + T) % SEG;
+                E[h] = m <= T ? T - m : 0u;
+                ns[h] = E[h] ? (pos[h] + E[h]) / SEG - pos[h] / SEG : 0u;
+            }
+        }
+        uint32_t tot, ex;
+        if (FIX & 16) {
+            // wave scan, wave totals through LDS: one barrier (scr is not
+            // touched again before the next tile's barriers)
+            const uint32_t loc = (c[0] + c[1]) | ((ns[0] + ns[1]) << 16);
+            uint32_t x = loc;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(x, o, 64);
+                if (lane >= o) x += y;
+            }
+            if (lane == 63) scr[wid] = x;
+            __syncthreads();
+            ex = x - loc;
+            tot = 0;
+#pragma unroll
+            for (int w = 0; w < W; w++) {
+                const uint32_t t = scr[w];
+                if (w < wid) ex += t;
+                tot += t;
+            }
+        } else {
+            ex = block_exclusive_scan((c[0] + c[1]) | ((ns[0] + ns[1]) << 16), scr, &tot);
+        }
+        const uint32_t nsegT = tot >> 16;
+        uint32_t ts[2] = {0, 0};
+        if (owner) {
+            ts[0] = ex & 0xffffu;
+            ts[1] = ts[0] + c[0];
+            const uint32_t sp[2] = {ex >> 16, (ex >> 16) + ns[0]};
+            uint32_t o0 = ts[0], o1 = ts[1];
+#pragma unroll
+            for (int w = 0; w < W; w++) {
+                const uint32_t x = cw[w];
+                w32[w * hb + t2] = o0 | (o1 << 16);
+                o0 += x & 0xffffu;
+                o1 += x >> 16;
+            }
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const uint32_t d = 2 * t2 + h;
+                u32x4_t I;
+                I[0] = pos[h];
+                I[1] = E[h];
+                I[2] = ts[h];
+                I[3] = sp[h] | (kc[h] << 16);
+                info[d] = I;
+                for (uint32_t k = 0; k < ns[h]; k++) segown[sp[h] + k] = (uint16_t)d;
+            }
+        }
+        const uint64_t nb = base + TILE;
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint64_t i = nb + wbase + j * 64 + lane;
+            nv[j] = in[i < end ? i : end - 1];
+        }
+        __syncthreads();
+        // ---- stage: all counter reads first, then all stores (dump slot for
+        // invalid items)
+        {
+            uint32_t wo[ITEMS];
+#pragma unroll
+            for (int j = 0; j < ITEMS; j++) {
+                const uint32_t d = dg[j] == 0xffffffffu ? 0u : dg[j];
+                wo[j] = w32[wid * hb + (d >> 1)];
+            }
+#pragma unroll
+            for (int j = 0; j < ITEMS; j++) {
+                const uint32_t d = dg[j];
+                const uint32_t p = d == 0xffffffffu
+                                       ? (uint32_t)TILE
+                                       : ((wo[j] >> ((d & 1u) * 16u)) & 0xffffu) + rk[j];
+                stage[p] = v[j];
+            }
+        }
+        __syncthreads();
+        if (owner) {
+#pragma unroll
+            for (int w = 0; w < W; w++) w32[w * hb + t2] = 0;
+        }
+        // ---- whole aligned segments, U per thread per trip: the segment
+        // owners, then the infos, then the data, then the stores
+        const uint32_t nq = nsegT * SEG;
+        for (uint32_t q0 = threadIdx.x; q0 < nq; q0 += U * THREADS) {
+            uint32_t dd[U], addr[U];
+            bool ok[U];
+            Tup x[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint32_t q = min(q0 + u * THREADS, nq - 1);
+                dd[u] = segown[q / SEG];
+            }
+            u32x4_t I[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) I[u] = info[dd[u]];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint32_t q = q0 + u * THREADS;
+                const uint32_t qc = min(q, nq - 1);
+                const uint32_t sg = qc / SEG;
+                const uint32_t p = I[u][0];
+                addr[u] = (p / SEG + (sg - (I[u][3] & 0xffffu))) * SEG + qc % SEG;
+                ok[u] = q < nq && addr[u] >= p && addr[u] < p + I[u][1];
+                const uint32_t e = ok[u] ? addr[u] - p : 0u;
+                const uint32_t k = I[u][3] >> 16;
+                x[u] = e < k ? carry[dd[u] * CW + e] : stage[I[u][2] + e - k];
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                if (ok[u] && (!(FIX & 8) || addr[u] == 0xffffffffu)) out[addr[u]] = x[u];
+        }
+        __syncthreads();
+        // ---- owner: the leftovers (< SEG) become the carry: read, then write
+        if (owner) {
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const uint32_t d = 2 * t2 + h;
+                const uint32_t T = kc[h] + c[h];
+                const uint32_t left = T - E[h];
+                Tup tmp[CW];
+#pragma unroll
+                for (uint32_t e = 0; e < CW; e++) {
+                    const uint32_t idx = E[h] + e;
+                    tmp[e] = idx < kc[h] ? carry[d * CW + idx]
+                                         : stage[e < left ? ts[h] + idx - kc[h] : 0u];
+                }
+#pragma unroll
+                for (uint32_t e = 0; e < CW; e++)
+                    if (e < left) carry[d * CW + e] = tmp[e];
+                pos[h] += E[h];
+                kc[h] = left;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) v[j] = nv[j];
+    }
     if (owner) {
 #pragma unroll
         for (int h = 0; h < 2; h++) {
@@ -541,21 +793,28 @@ static void run_v6(Ctx& c, int reps, const char* label) {
     SMJ_CHECK(hipFree(starts));
 }
 
-template <int THREADS, int ITEMS, int FIX>
+template <int THREADS, int ITEMS, int FIX, bool B = false, int HS = 1>
 static void run_swa(Ctx& c, int reps, const char* label) {
     typedef SwaGeom<THREADS, ITEMS> G;
+    typedef SwbGeom<THREADS, ITEMS> GB;
     uint64_t ntiles = (c.n + G::TILE - 1) / G::TILE;
     uint32_t nwg = (uint32_t)std::min<uint64_t>(ntiles, 256);
     const uint64_t tpw = (ntiles + nwg - 1) / nwg;
     const uint64_t chunk = tpw * G::TILE;
     nwg = (uint32_t)((ntiles + tpw - 1) / tpw);
-    const size_t lds = G::lds_bytes(c.nbins);
+    const size_t lds = B ? GB::lds_bytes(c.nbins) : G::lds_bytes(c.nbins);
+    if (lds > 160 * 1024) {
+        printf("%s: LDS %zu too big\n", label, lds);
+        return;
+    }
     uint32_t* counts;
     uint64_t *totals, *starts;
-    SMJ_CHECK(hipMalloc(&counts, (size_t)c.nbins * nwg * 4));
+    SMJ_CHECK(hipMalloc(&counts, (size_t)c.nbins * nwg * HS * 4));
     SMJ_CHECK(hipMalloc(&totals, c.nbins * 8));
     SMJ_CHECK(hipMalloc(&starts, c.nbins * 8));
     SMJ_CHECK(hipFuncSetAttribute((const void*)k_swa_lab<THREADS, ITEMS, RefDigit, FIX>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    SMJ_CHECK(hipFuncSetAttribute((const void*)k_swb<THREADS, ITEMS, RefDigit, FIX>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     const uint32_t mask = (uint32_t)(((1ull << c.bits) - 1) << c.shift);
     RefDigit dig{mask, c.shift};
@@ -565,14 +824,18 @@ static void run_swa(Ctx& c, int reps, const char* label) {
     SMJ_CHECK(hipMemset(c.dout, 0, c.cap * sizeof(Tup)));
     for (int r = -1; r < reps; r++) {
         SMJ_CHECK(hipEventRecord(e[0]));
-        hipLaunchKernelGGL((k_h6<512, 16, false>), dim3(nwg), dim3(512), c.nbins * 4, 0, c.din, c.n,
-                           chunk, dig, c.nbins, counts, nwg);
+        hipLaunchKernelGGL((k_h6<512, 16, false>), dim3(nwg * HS), dim3(512), c.nbins * 4, 0, c.din,
+                           c.n, chunk / HS, dig, c.nbins, counts, nwg * HS);
         SMJ_CHECK(hipEventRecord(e[1]));
-        hipLaunchKernelGGL(k_scanrow6, dim3(c.nbins), dim3(256), 0, 0, counts, nwg, totals);
+        hipLaunchKernelGGL(k_scanrow6, dim3(c.nbins), dim3(256), 0, 0, counts, nwg * HS, totals);
         hipLaunchKernelGGL(k_scandig6, dim3(1), dim3(256), 0, 0, totals, c.nbins, starts);
         SMJ_CHECK(hipEventRecord(e[2]));
-        hipLaunchKernelGGL((k_swa_lab<THREADS, ITEMS, RefDigit, FIX>), dim3(nwg), dim3(THREADS), lds, 0,
-                           c.din, c.n, chunk, dig, c.nbins, counts, nwg, starts, c.dout);
+        if (B)
+            hipLaunchKernelGGL((k_swb<THREADS, ITEMS, RefDigit, FIX>), dim3(nwg), dim3(THREADS), lds, 0,
+                               c.din, c.n, chunk, dig, c.nbins, counts, nwg, starts, c.dout, (uint32_t)HS);
+        else
+            hipLaunchKernelGGL((k_swa_lab<THREADS, ITEMS, RefDigit, FIX>), dim3(nwg), dim3(THREADS), lds, 0,
+                               c.din, c.n, chunk, dig, c.nbins, counts, nwg, starts, c.dout);
         SMJ_CHECK(hipEventRecord(e[3]));
         SMJ_CHECK(hipEventSynchronize(e[3]));
         SMJ_CHECK(hipGetLastError());
@@ -652,31 +915,24 @@ int argc, char** argv) {
     if (only.empty() || only == name) run_v6<T, I, K, XM, NT>(c, reps, name);
 #define SWA(T, I, F, name) \
     if (only.empty() || only == name) run_swa<T, I, F>(c, reps, name);
+#define SWB(T, I, F, name) \
+    if (only.empty() || only == name) run_swa<T, I, F, true>(c, reps, name);
+#define SWBH(T, I, F, H, name) \
+    if (only.empty() || only == name) run_swa<T, I, F, true, H>(c, reps, name);
 #ifdef KEY_8B
-    SWA(512, 8, 0, "swa 512x8 fix0");
     SWA(512, 8, 1, "swa 512x8 fix1");
-    SWA(512, 8, 3, "swa 512x8 fix3");
-    SWA(512, 8, 7, "swa 512x8 fix7");
-    V6(512, 8, 8, true, 1, "v6 512x8 K8 xm nt");
-    V6(512, 8, 8, true, 0, "v6 512x8 K8 xm");
-    V6(512, 8, 16, true, 1, "v6 512x8 K16 xm nt");
-    V6(512, 8, 4, true, 1, "v6 512x8 K4 xm nt");
-    V6(512, 8, 8, false, 1, "v6 512x8 K8 nt");
-    V6(512, 12, 8, true, 1, "v6 512x12 K8 xm nt");
-    V6(256, 16, 8, true, 1, "v6 256x16 K8 xm nt");
+    SWB(512, 8, 1, "swb 512x8");
+    SWB(512, 8, 17, "swb 512x8 scan1");
+    SWBH(512, 8, 17, 4, "swb 512x8 scan1 h4");
+    SWB(1024, 3, 17, "swb 1024x3 scan1");
 #else
-    SWA(512, 16, 0, "swa 512x16 fix0");
     SWA(512, 16, 1, "swa 512x16 fix1");
-    SWA(512, 16, 3, "swa 512x16 fix3");
-    SWA(512, 16, 7, "swa 512x16 fix7");
-    V6(512, 16, 8, true, 1, "v6 512x16 K8 xm nt");
-    V6(512, 16, 8, true, 0, "v6 512x16 K8 xm");
-    V6(512, 16, 4, true, 1, "v6 512x16 K4 xm nt");
-    V6(512, 16, 16, true, 1, "v6 512x16 K16 xm nt");
-    V6(512, 16, 8, false, 1, "v6 512x16 K8 nt");
-    V6(512, 8, 16, true, 1, "v6 512x8 K16 xm nt");
-    V6(512, 8, 8, true, 1, "v6 512x8 K8 xm nt");
-    V6(1024, 8, 8, true, 1, "v6 1024x8 K8 xm nt");
+    SWB(512, 16, 1, "swb 512x16");
+    SWB(512, 16, 17, "swb 512x16 scan1");
+    SWB(1024, 6, 1, "swb 1024x6");
+    SWB(1024, 6, 17, "swb 1024x6 scan1");
+    SWBH(1024, 6, 17, 4, "swb 1024x6 scan1 h4");
+    SWBH(1024, 6, 17, 8, "swb 1024x6 scan1 h8");
 #endif
     return 0;
 }
