@@ -348,12 +348,290 @@ void segmented_sort(Workspace* ws, Tup* data, const uint64_t* seg_off,
     }
 }
 
-// k-way merge as a tree of 2-way merge-path passes.
+// ---------------------------------------------------------------------------
+// One-pass k-way merge (avx_multiway_merge, src/merge/avx_multiwaymerge.c:
+// 199-338).  The reference streams k runs through an L3-resident FIFO tree;
+// here the key range of the runs is cut into 2^D value buckets and, because
+// every run is sorted, the part of run i in bucket b is ONE contiguous slice
+// whose ends are two binary searches away.  So:
+//   k_km_range  : key range from the runs' first and last elements;
+//   k_km_bounds : off[b][i] = first element of run i in bucket >= b (k x (B+1)
+//                 binary searches, no data pass);
+//   k_km_sizes  : bucket sizes (a wave per bucket) and their exclusive scan;
+//   k_km_merge  : one workgroup per bucket gathers its k slices into LDS with
+//                 coalesced loads, merges them there pairwise (ceil(log2 k)
+//                 rounds; an element's new place = its index + its rank in
+//                 the partner slice, by binary search in LDS) and writes the
+//                 bucket to its place in the output in one stream.
+// Traffic: each tuple read once and written once (2w).  A bucket larger than
+// LDS (a hot key) flags the merge, which then runs as the merge-path tree.
+constexpr int KM_THREADS = 256;
+constexpr uint32_t KM_CAP = sizeof(Tup) == 8 ? 4096 : 2048;  // bucket capacity (32 KB)
+constexpr uint32_t KM_IPT = KM_CAP / KM_THREADS;
+constexpr uint32_t KM_KMAX = KM_THREADS;  // runs per one-pass merge
+
+struct KmRun {
+    const Tup* p;
+    uint64_t n;
+};
+
+__global__ void __launch_bounds__(256)
+k_km_range(const KmRun* __restrict__ runs, uint32_t k, unsigned long long* __restrict__ mm) {
+    uint64_t lo = ~0ull, hi = 0;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < k; i += gridDim.x * 256) {
+        const KmRun r = runs[i];
+        if (r.n == 0) continue;
+        lo = min(lo, key_u(tup_key(r.p[0])));
+        hi = max(hi, key_u(tup_key(r.p[r.n - 1])));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t a = __shfl_xor(lo, o, 64), c = __shfl_xor(hi, o, 64);
+        lo = a < lo ? a : lo;
+        hi = c > hi ? c : hi;
+    }
+    if (lane_id() == 0) {
+        atomicMin(&mm[0], (unsigned long long)lo);
+        atomicMax(&mm[1], (unsigned long long)hi);
+    }
+}
+
+// bucket shift: 2^D buckets over the key range [mm[0], mm[1]]
+__device__ __forceinline__ uint32_t km_shift(const unsigned long long* mm, uint32_t D) {
+    const uint64_t w = mm[1] >= mm[0] ? mm[1] - mm[0] : 0;
+    const uint32_t L = w ? 64 - __clzll((long long)w) : 0;
+    return L > D ? L - D : 0;
+}
+
+__global__ void __launch_bounds__(256)
+k_km_bounds(const KmRun* __restrict__ runs, uint32_t k, uint32_t D,
+            const unsigned long long* __restrict__ mm, uint32_t* __restrict__ off) {
+    const uint32_t B = 1u << D;
+    const uint64_t idx = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (uint64_t)(B + 1) * k) return;
+    const uint32_t b = (uint32_t)(idx / k), i = (uint32_t)(idx % k);
+    const KmRun r = runs[i];
+    uint64_t pos;
+    if (b == 0) {
+        pos = 0;
+    } else if (b == B) {
+        pos = r.n;
+    } else {
+        const uint64_t minu = mm[0];
+        const uint32_t s = km_shift(mm, D);
+        uint64_t lo = 0, hi = r.n;
+        while (lo < hi) {  // first element whose bucket is >= b
+            const uint64_t m = (lo + hi) >> 1;
+            if (((key_u(tup_key(r.p[m])) - minu) >> s) < b) lo = m + 1; else hi = m;
+        }
+        pos = lo;
+    }
+    off[(uint64_t)b * k + i] = (uint32_t)pos;
+}
+
+// sizes of buckets [blockIdx.x * 4, +4) (a wave each), overflow flag
+__global__ void __launch_bounds__(256)
+k_km_sizes(const uint32_t* __restrict__ off, uint32_t k, uint32_t B,
+           uint64_t* __restrict__ size, unsigned int* __restrict__ flag) {
+    const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b >= B) return;
+    uint64_t s = 0;
+    for (uint32_t i = lane_id(); i < k; i += 64)
+        s += off[(uint64_t)(b + 1) * k + i] - off[(uint64_t)b * k + i];
+    s = wave_sum(s);
+    if (lane_id() == 0) {
+        size[b] = s;
+        if (s > KM_CAP) atomicOr(flag, 1u);
+    }
+}
+
+// one workgroup: exclusive scan of the B bucket sizes in place
+__global__ void __launch_bounds__(1024)
+k_km_scan(uint64_t* __restrict__ size, uint32_t B) {
+    __shared__ unsigned long long wt[17];
+    const uint32_t per = (B + 1023) / 1024;
+    const uint32_t b0 = threadIdx.x * per;
+    unsigned long long loc = 0;
+    for (uint32_t q = 0; q < per; q++)
+        if (b0 + q < B) loc += size[b0 + q];
+    unsigned long long x = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long y = __shfl_up(x, o, 64);
+        if (lane_id() >= o) x += y;
+    }
+    const int wid = threadIdx.x >> 6;
+    if (lane_id() == 63) wt[wid] = x;
+    __syncthreads();
+    unsigned long long ex = x - loc;
+    for (int w = 0; w < wid; w++) ex += wt[w];
+    for (uint32_t q = 0; q < per; q++) {
+        if (b0 + q < B) {
+            const unsigned long long c = size[b0 + q];
+            size[b0 + q] = ex;
+            ex += c;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(KM_THREADS)
+k_km_merge(const KmRun* __restrict__ runs, uint32_t k, const uint32_t* __restrict__ off,
+           const uint64_t* __restrict__ ostart, const unsigned int* __restrict__ flag,
+           Tup* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) Tup buf[KM_CAP];
+    __shared__ uint32_t spos[KM_KMAX + 1];  // slice starts in buf (run order), + total
+    __shared__ const Tup* sptr[KM_KMAX];    // run i's element for bucket position j: sptr[i][j]
+    __shared__ uint32_t wt[KM_THREADS / 64];
+    if (*flag) return;  // some bucket overflows: the caller merges another way
+    const uint32_t b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    // ---- slices: run tid's part of bucket b, scanned into LDS positions
+    uint32_t lo = 0, len = 0;
+    if (tid < k) {
+        lo = off[(uint64_t)b * k + tid];
+        len = off[(uint64_t)(b + 1) * k + tid] - lo;
+    }
+    uint32_t x = len;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wt[wid] = x;
+    __syncthreads();
+    uint32_t ex = x - len, total = 0;
+#pragma unroll
+    for (int w = 0; w < KM_THREADS / 64; w++) {
+        if (w < (int)wid) ex += wt[w];
+        total += wt[w];
+    }
+    if (tid <= k) spos[tid] = tid < k ? ex : total;
+    if (tid < k) sptr[tid] = runs[tid].p + ((int64_t)lo - (int64_t)ex);
+    __syncthreads();
+    // ---- gather: element j of the bucket comes from the run whose slice
+    // holds position j (binary search over the slice starts)
+    const uint32_t rounds = k > 1 ? 32 - __clz(k - 1) : 0;
+    Tup v[KM_IPT];
+    uint32_t rn[KM_IPT];
+#pragma unroll
+    for (int q = 0; q < (int)KM_IPT; q++) {
+        const uint32_t j = q * KM_THREADS + tid;
+        rn[q] = 0;
+        if (j < total) {
+            uint32_t l = 0, h = k;  // last run with spos <= j
+            while (h - l > 1) {
+                const uint32_t m = (l + h) >> 1;
+                if (spos[m] <= j) l = m; else h = m;
+            }
+            rn[q] = l;
+            v[q] = sptr[l][j];
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < (int)KM_IPT; q++) {
+        const uint32_t j = q * KM_THREADS + tid;
+        if (j < total) buf[j] = v[q];
+    }
+    __syncthreads();
+    // ---- pairwise merge rounds in LDS: in round r, slice s covers runs
+    // [s 2^r, (s+1) 2^r); slice pairs (2m, 2m+1) merge; an element's new place
+    // = pair start + its index in its slice + its rank in the partner slice
+    // (left elements count partner elements < x, right ones <= x: left first)
+    uint32_t pos[KM_IPT];
+#pragma unroll
+    for (int q = 0; q < (int)KM_IPT; q++) pos[q] = q * KM_THREADS + tid;
+    for (uint32_t r = 0; r < rounds; r++) {
+        uint32_t dst[KM_IPT];
+#pragma unroll
+        for (int q = 0; q < (int)KM_IPT; q++) {
+            dst[q] = pos[q];
+            if (pos[q] < total) {
+                const uint32_t sl = rn[q] >> r;
+                const bool left = (sl & 1) == 0;
+                const uint32_t pl = sl ^ 1;
+                const uint32_t s0 = spos[min((sl & ~1u) << r, k)];
+                const uint32_t my0 = spos[min(sl << r, k)];
+                uint32_t plo = spos[min(pl << r, k)], phi = spos[min((pl + 1) << r, k)];
+                const Tup xv = v[q];
+                while (plo < phi) {
+                    const uint32_t m = (plo + phi) >> 1;
+                    const bool before = left ? tup_less(buf[m], xv) : !tup_less(xv, buf[m]);
+                    if (before) plo = m + 1; else phi = m;
+                }
+                const uint32_t pstart = spos[min(pl << r, k)];
+                dst[q] = s0 + (pos[q] - my0) + (plo - pstart);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < (int)KM_IPT; q++)
+            if (pos[q] < total) {
+                buf[dst[q]] = v[q];
+                pos[q] = dst[q];
+            }
+        __syncthreads();
+    }
+    // ---- the bucket, in order, to its place in the output
+    const uint64_t o = ostart[b];
+    for (uint32_t j = tid; j < total; j += KM_THREADS) out[o + j] = buf[j];
+}
+
+// true when the one-pass merge ran; false: a bucket overflowed (or k is
+// outside the one-pass range) and nothing was written
+static bool multiway_merge_buckets(Workspace* ws, const Tup* const* runs, const uint64_t* lens,
+                                   uint32_t k, uint64_t total, Tup* out, hipStream_t st) {
+    if (k < 3 || k > KM_KMAX) return false;
+    for (uint32_t i = 0; i < k; i++)
+        if (lens[i] >= (1ull << 32)) return false;
+    // buckets of KM_CAP / 2 tuples on average
+    uint32_t D = 0;
+    while (D < 24 && (total >> D) > KM_CAP / 2) D++;
+    const uint32_t B = 1u << D;
+    std::vector<KmRun> h(k);
+    for (uint32_t i = 0; i < k; i++) h[i] = KmRun{runs[i], lens[i]};
+    KmRun* dr = (KmRun*)ws->scratch("km_runs", k * sizeof(KmRun));
+    unsigned long long* mm = (unsigned long long*)ws->scratch("km_mm", 32);
+    unsigned int* flag = (unsigned int*)(mm + 2);
+    uint32_t* off = (uint32_t*)ws->scratch("km_off", (size_t)(B + 1) * k * 4);
+    uint64_t* size = (uint64_t*)ws->scratch("km_size", (size_t)B * 8);
+    unsigned long long* hinit = (unsigned long long*)ws->host_pinned("km_init", 32);
+    unsigned int* hflag = (unsigned int*)ws->host_pinned("km_flag", 16);
+    // the pinned buffers are free: every call ends with a synchronisation
+    hinit[0] = ~0ull;
+    hinit[1] = 0;
+    hinit[2] = 0;
+    hinit[3] = 0;
+    // pageable table: copied out before hipMemcpyAsync returns
+    SMJ_CHECK(hipMemcpyAsync(dr, h.data(), k * sizeof(KmRun), hipMemcpyHostToDevice, st));
+    SMJ_CHECK(hipMemcpyAsync(mm, hinit, 32, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_km_range, dim3((k + 255) / 256), dim3(256), 0, st, dr, k, mm);
+    const uint64_t nb = (uint64_t)(B + 1) * k;
+    {
+        TraceScope ts(ws, "k_km_bounds", st);
+        hipLaunchKernelGGL(k_km_bounds, dim3((uint32_t)((nb + 255) / 256)), dim3(256), 0, st, dr,
+                           k, D, mm, off);
+    }
+    hipLaunchKernelGGL(k_km_sizes, dim3((B + 3) / 4), dim3(256), 0, st, off, k, B, size, flag);
+    hipLaunchKernelGGL(k_km_scan, dim3(1), dim3(1024), 0, st, size, B);
+    {
+        TraceScope ts(ws, "k_km_merge", st);
+        hipLaunchKernelGGL(k_km_merge, dim3(B), dim3(KM_THREADS), 0, st, dr, k, off, size, flag,
+                           out);
+    }
+    SMJ_CHECK(hipGetLastError());
+    SMJ_CHECK(hipMemcpyAsync(hflag, flag, 4, hipMemcpyDeviceToHost, st));
+    SMJ_CHECK(hipStreamSynchronize(st));
+    return hflag[0] == 0;
+}
+
+// k-way merge: one pass by value buckets (above); otherwise (k > 256, one
+// run, two runs, or a bucket too big for LDS) a tree of 2-way merge-path
+// passes.
 void multiway_merge(Workspace* ws, const Tup* const* runs, const uint64_t* lens,
                     uint32_t k, Tup* out, hipStream_t st) {
     uint64_t total = 0;
     for (uint32_t i = 0; i < k; i++) total += lens[i];
     if (total == 0) return;
+    if (multiway_merge_buckets(ws, runs, lens, k, total, out, st)) return;
     std::vector<const Tup*> cur(runs, runs + k);
     std::vector<uint64_t> cl(lens, lens + k);
     Tup* bufs[2] = {(Tup*)ws->scratch("mw_a", total * sizeof(Tup)),

@@ -35,10 +35,11 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--op", default="join", choices=("join", "sort", "partition"),
+    p.add_argument("--op", default="join", choices=("join", "sort", "partition", "merge"),
                    help="join: sortmergejoin_multiway (the headline); sort: bench_sort's "
                         "avxsort_tuples on 2^27 tuples; partition: bench_partitioning's "
-                        "partition_relation_optimized on 2^27 tuples")
+                        "partition_relation_optimized on 2^27 tuples; merge: "
+                        "bench_multiwaymerge's avx_multiway_merge, --fanin runs of --n")
     p.add_argument("--n", type=int, default=None,
                    help="tuples per relation per GPU (join: 128M; sort/partition: 2^27)")
     p.add_argument("--n-total", type=int, default=None,
@@ -48,6 +49,7 @@ def parse():
                    help="tuple bytes (join: 16 = the reference's KEY_8B build; "
                         "sort/partition: 8 = the reference's default tuple)")
     p.add_argument("--bits", type=int, default=10, help="partition: radix bits")
+    p.add_argument("--fanin", type=int, default=64, help="merge: number of sorted runs")
     p.add_argument("--shift", type=int, default=0, help="partition: shift bits")
     p.add_argument("--dist", default="uniform", choices=("uniform", "zipf"))
     p.add_argument("--theta", type=float, default=0.75)
@@ -75,6 +77,7 @@ def alg_bytes_per_launch(name, n_rel, nR, nS, w, op="join"):
         "k_scatter": 2 * n_rel * w,          # one relation per launch
         "k_tilepass": 2 * both * w,
         "k_groupsort": 2 * both * w,
+        "k_km_merge": 2 * n_rel * w,         # every tuple of the runs, once
     }.get(name)
 
 
@@ -146,20 +149,24 @@ def cpu_baseline(width, n):
                       f"count {'ok' if ok and ok1 else 'MISMATCH'}"}
 
 
-def cpu_baseline_op(op, width, n, bits, shift):
+def cpu_baseline_op(op, width, n, bits, shift, fanin=64):
     """The reference's single-core partition_relation_optimized / avxsort_tuples
     (oracle/_ref/cpu_baseline_ops*) on create_relation_pk(n), seed 12345."""
     exe = _ref_exe(f"cpu_baseline_ops{width}")
-    args = [exe, op, str(n)] + ([str(bits), str(shift)] if op == "partition" else [])
+    args = [exe, op, str(n)] + ([str(bits), str(shift)] if op == "partition" else
+                                [str(fanin)] if op == "merge" else [])
     r = subprocess.run(args, capture_output=True, text=True, timeout=900, cwd="/tmp")
     m = re.search(r"SMJ_CPU_OPS (\{.*\})", r.stdout)
     if not m:
         raise RuntimeError(f"{exe} printed no result (rc {r.returncode}): {r.stderr[-400:]}")
     d = json.loads(m.group(1))
     _, lscpu = host_cores()
-    what = (f"partition_relation_optimized {n} tuples, {bits} bits, shift {shift}"
-            if op == "partition" else
-            f"{'avxsort_tuples' if width == 8 else 'scalarsort_tuples'} {n} tuples")
+    what = {"partition": f"partition_relation_optimized {n} tuples, {bits} bits, shift {shift}",
+            "sort": f"{'avxsort_tuples' if width == 8 else 'scalarsort_tuples'} {n} tuples",
+            "merge": f"{'avx' if width == 8 else 'scalar'}_multiway_merge of {fanin} runs "
+                     f"of {n} (generate_rand_ordered_tuples), 4 MiB FIFO"}[op]
+    if op == "merge":
+        n = n * fanin
     return {"value": round(n / d["seconds"] / 1e6, 3), "unit": "Mtuples/s", "cores": 1,
             "kind": "reference", "host_cores_lscpu": lscpu,
             "sample": f"{what}, {width}B tuples, create_relation_pk seed 12345, "
@@ -214,7 +221,7 @@ def main():
     if a.width is None:
         a.width = 16 if a.op == "join" else 8
     if a.n is None:
-        a.n = 128_000_000 if a.op == "join" else 1 << 27
+        a.n = {"join": 128_000_000, "merge": 65536}.get(a.op, 1 << 27)
     lib = smj.load(a.width)
     if a.op != "join":
         run_op(a, lib, json_out, dist, N, rank)
@@ -386,9 +393,33 @@ def run_op(a, lib, json_out, dist, N, rank):
     shape of create_relation_pk), payload 0.  N GPUs run N independent
     replicas (the ops do not shard across GPUs: scaling "weak")."""
     w, n = a.width, a.n
+    if a.op == "merge":  # n tuples per run
+        n = a.n * a.fanin
     R = lib.empty(n)
     lib.dev_gen_pk(R, 0, n, 12345, with_payload=False)
-    if a.op == "sort":
+    if a.op == "merge":
+        # --fanin runs of increasing keys, random steps in [0, 100) as
+        # generate_rand_ordered_tuples (tests/testutil.c:266-287); separate
+        # allocations, as the reference bench mallocs every run
+        dt = torch.int32 if w == 8 else torch.int64
+        g = torch.Generator(device="cuda").manual_seed(2012)
+        steps = torch.randint(0, 100, (a.fanin, a.n), device="cuda", generator=g,
+                              dtype=torch.int64)
+        steps[:, 0] = torch.randint(1, 101, (a.fanin,), device="cuda", generator=g)
+        keys = steps.cumsum(dim=1).clamp_(max=(1 << 31) - 101).to(dt)
+        del steps
+        runs = []
+        for i in range(a.fanin):
+            t = lib.empty(a.n)
+            t[:, 0] = 0
+            t[:, 1] = keys[i]
+            runs.append(t)
+        del keys
+        out = lib.empty(n)
+
+        def step():
+            lib.dev_multiway_merge(runs, out)
+    elif a.op == "sort":
         out = lib.empty(n)
 
         def step():
@@ -403,7 +434,7 @@ def run_op(a, lib, json_out, dist, N, rank):
             lib.dev_partition(R, out, a.bits, a.shift, True, hist, off)
     torch.cuda.synchronize()
     elapsed, kern = timed_loop(a, lib, dist, step)
-    if a.op == "sort":
+    if a.op in ("sort", "merge"):
         keys = out[:, 1]
         ok = bool((keys[1:] >= keys[:-1]).all().item()) if n > 1 else True
     else:
@@ -419,12 +450,14 @@ def run_op(a, lib, json_out, dist, N, rank):
     alg = 2 * n * w  # 2·N·w for bench_sort and bench_partitioning
     cpu = None
     if N == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline_op(a.op, w, n, a.bits, a.shift)
-    ref = ("src/bench/sortbench.c:85-202 (avxsort_tuples)" if a.op == "sort" else
-           "src/bench/partitioningbench.c:128-196 (partition_relation_optimized)")
+        cpu = cpu_baseline_op(a.op, w, a.n if a.op == "merge" else n, a.bits, a.shift, a.fanin)
+    ref = {"sort": "src/bench/sortbench.c:85-202 (avxsort_tuples)",
+           "merge": "src/bench/multiwaymergebench.c:48-120 (avx_multiway_merge)",
+           "partition": "src/bench/partitioningbench.c:128-196 (partition_relation_optimized)"}[a.op]
     out_line = {
-        "metric": (f"bench_sort throughput Mtuples/s + achieved HBM GB/s (2·N·w)" if a.op == "sort"
-                   else "bench_partitioning throughput Mtuples/s + achieved HBM GB/s (2·N·w)"),
+        "metric": {"sort": "bench_sort", "partition": "bench_partitioning",
+                   "merge": "bench_multiwaymerge"}[a.op]
+                  + " throughput Mtuples/s + achieved HBM GB/s (2·N·w)",
         "value": round(value, 2),
         "unit": "Mtuples/s",
         "n_gpus": N,
@@ -437,9 +470,13 @@ def run_op(a, lib, json_out, dist, N, rank):
         "dtype": "int64" if w == 16 else "int32",
         "data": "synthetic",
         "config": {"workload": (f"{a.op} of {n} {w}-byte tuples" +
-                                (f", {a.bits} radix bits, shift {a.shift}, 64-byte padded, stable"
-                                 if a.op == "partition" else ", full (key, payload) order")
-                                + ", keys 1..N permuted, payload 0; reference " + ref),
+                                {"partition": f", {a.bits} radix bits, shift {a.shift}, "
+                                              "64-byte padded, stable",
+                                 "sort": ", full (key, payload) order",
+                                 "merge": f", {a.fanin} sorted runs of {a.n}"}[a.op]
+                                + (", keys in random steps, payload 0" if a.op == "merge" else
+                                   ", keys 1..N permuted, payload 0")
+                                + "; reference " + ref),
                    "tuples": n, "tuple_bytes": w, "parallelism": f"replicas x{N}"},
         "roofline": roof,
         "cpu_baseline": cpu,

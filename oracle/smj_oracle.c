@@ -318,18 +318,41 @@ uint64_t orc_merge_tuples(const tuple_t *A, const tuple_t *B, tuple_t *out,
  * the merge tree's output is the sorted union of the runs. */
 uint64_t orc_multiway_merge(tuple_t *out, const tuple_t *const *runs,
                             const uint64_t *lens, uint32_t k) {
-    uint64_t *pos = (uint64_t *)calloc(k, sizeof(uint64_t));
+    /* a binary heap of the runs' heads, ordered by (tuple, run index): the
+     * same output as the reference's merge tree for a total order, in
+     * O(N log k) */
+    uint64_t *pos = (uint64_t *)calloc(k ? k : 1, sizeof(uint64_t));
+    uint32_t *heap = (uint32_t *)malloc(sizeof(uint32_t) * (k ? k : 1));
+    uint32_t hn = 0;
     uint64_t total = 0;
-    for (uint32_t r = 0; r < k; r++) total += lens[r];
-    for (uint64_t o = 0; o < total; o++) {
-        int best = -1;
-        for (uint32_t r = 0; r < k; r++) {
-            if (pos[r] >= lens[r]) continue;
-            if (best < 0 || tup_cmp(&runs[r][pos[r]], &runs[best][pos[best]]) < 0)
-                best = (int)r;
+#define HLESS(a, b) (tup_cmp(&runs[a][pos[a]], &runs[b][pos[b]]) < 0 || \
+                     (tup_cmp(&runs[a][pos[a]], &runs[b][pos[b]]) == 0 && (a) < (b)))
+    for (uint32_t r = 0; r < k; r++) {
+        total += lens[r];
+        if (!lens[r]) continue;
+        uint32_t i = hn++;
+        heap[i] = r;
+        while (i > 0 && HLESS(heap[i], heap[(i - 1) / 2])) {
+            uint32_t t = heap[i]; heap[i] = heap[(i - 1) / 2]; heap[(i - 1) / 2] = t;
+            i = (i - 1) / 2;
         }
-        out[o] = runs[best][pos[best]++];
     }
+    for (uint64_t o = 0; o < total; o++) {
+        const uint32_t r = heap[0];
+        out[o] = runs[r][pos[r]++];
+        if (pos[r] >= lens[r]) heap[0] = heap[--hn];
+        uint32_t i = 0;
+        for (;;) {  /* sift down */
+            uint32_t l = 2 * i + 1, m = i;
+            if (l < hn && HLESS(heap[l], heap[m])) m = l;
+            if (l + 1 < hn && HLESS(heap[l + 1], heap[m])) m = l + 1;
+            if (m == i) break;
+            uint32_t t = heap[i]; heap[i] = heap[m]; heap[m] = t;
+            i = m;
+        }
+    }
+#undef HLESS
+    free(heap);
     free(pos);
     return total;
 }

@@ -10,7 +10,9 @@ them.  Nothing here runs on the GPU box.
 
     python tests/golden/make_golden.py           # golden_w8/w16.npz
     python tests/golden/make_golden.py --int64   # golden_int64.npz
+    python tests/golden/make_golden.py --big     # golden_big.npz (digests)
 """
+import hashlib
 import os
 import re
 import subprocess
@@ -153,6 +155,53 @@ def main():
         print(f"wrote {path} ({os.path.getsize(path) / 1e6:.2f} MB, {len(out)} arrays)")
 
 
+BIG_SORT_N = 1 << 20            # sorts up to 2^20
+BIG_MW = [(128, 900), (1024, 200), (2048, 100)]  # fan-in, max run length
+
+
+def digest(a) -> np.ndarray:
+    """SHA-256 of an array's bytes, as 32 uint8 (fixtures stay small)."""
+    return np.frombuffer(hashlib.sha256(np.ascontiguousarray(a).tobytes()).digest(), np.uint8)
+
+
+def big_sort_input(gen, n=BIG_SORT_N):
+    """the 2^20 sort case: create_relation_nonunique(n, n/2), seed 4242"""
+    gen.seed(4242)
+    return gen.create_relation_nonunique(n, n // 2)
+
+
+def big_fixtures():
+    """Reference outputs too big to commit, kept as digests: the inputs are
+    regenerated by the tests (the seeded generator restatement, pinned by
+    golden_w*.npz, and sorted_runs over numpy's seeded generator); the
+    fixture holds the reference's output digest, length and head/tail."""
+    out = {}
+    for w in (8, 16):
+        ref = oracle.Reference(w)
+        t = big_sort_input(ref)
+        o = ref.sort(t, "avxsort_tuples" if w == 8 else "scalarsort_tuples")
+        out[f"w{w}_sort_in_digest"] = digest(t)
+        # exact order (8-byte tuples: the packed word is a total order), and
+        # for both widths the key column and the (key, payload) multiset (the
+        # 16-byte path leaves equal keys in an implementation order)
+        out[f"w{w}_sort_out_digest"] = digest(o)
+        out[f"w{w}_sort_out_key_digest"] = digest(o["key"])
+        out[f"w{w}_sort_out_canon_digest"] = digest(np.sort(o, order=["key", "payload"]))
+        out[f"w{w}_sort_out_head"] = o[:64]
+        out[f"w{w}_sort_out_tail"] = o[-64:]
+        for k, maxlen in BIG_MW:
+            runs = sorted_runs(np.random.default_rng(k), k, maxlen, ref.dtype)
+            mo, mn = ref.multiway_merge(runs, 4 << 20, scalar=(w == 16))
+            out[f"w{w}_mw{k}_in_digest"] = digest(np.concatenate(runs))
+            out[f"w{w}_mw{k}_out_digest"] = digest(mo)
+            out[f"w{w}_mw{k}_out_key_digest"] = digest(mo["key"])
+            out[f"w{w}_mw{k}_out_canon_digest"] = digest(np.sort(mo, order=["key", "payload"]))
+            out[f"w{w}_mw{k}_n"] = np.array([mn, len(mo)], np.int64)
+    path = os.path.join(HERE, "golden_big.npz")
+    np.savez_compressed(path, **out)
+    print(f"wrote {path} ({os.path.getsize(path) / 1e6:.2f} MB, {len(out)} arrays)")
+
+
 def carriers(rng, n):
     """This fork's (key, ptr) int64 carriers with signed keys, built as
     src/bench/sortbench.c:267-298 does (gen_random_int, SetPtr, SetKeyInt):
@@ -205,5 +254,7 @@ if __name__ == "__main__":
         join_case(*map(int, sys.argv[2:]))
     elif len(sys.argv) == 2 and sys.argv[1] == "--int64":
         int64_fixtures()
+    elif len(sys.argv) == 2 and sys.argv[1] == "--big":
+        big_fixtures()
     else:
         main()

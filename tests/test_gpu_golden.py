@@ -153,3 +153,24 @@ def test_zipf_join_repeatable(libs, width, fanout_bits):
         assert torch.equal(sS[:, 1].to(torch.int64), ref)
     del R, S, sR, sS, ref
     torch.cuda.empty_cache()
+
+
+# ---- large cases pinned by digests of the reference's outputs
+# (tests/golden/golden_big.npz): 2^20 sort, multiway merges of fan-in 128..2048
+def test_golden_big_sort(width, libs, oracles):
+    from test_oracle import _big, _mg, check_big
+    g, mg = _big(), _mg()
+    t = mg.big_sort_input(oracles[width])
+    assert bytes(mg.digest(t)) == bytes(g[f"w{width}_sort_in_digest"])
+    check_big(width, libs[width].avxsort_tuples(t), g, f"w{width}_sort")
+
+
+@pytest.mark.parametrize("k,maxlen", [(128, 900), (1024, 200), (2048, 100)])
+def test_golden_big_multiway(width, libs, oracles, k, maxlen):
+    from test_oracle import _big, _mg, check_big
+    g, mg = _big(), _mg()
+    runs = mg.sorted_runs(np.random.default_rng(k), k, maxlen, libs[width].dtype)
+    assert bytes(mg.digest(np.concatenate(runs))) == bytes(g[f"w{width}_mw{k}_in_digest"])
+    out, n, consumed = libs[width].avx_multiway_merge(runs)
+    assert n == int(g[f"w{width}_mw{k}_n"][0]) and consumed
+    check_big(width, out, g, f"w{width}_mw{k}")

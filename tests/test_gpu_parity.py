@@ -210,17 +210,39 @@ def test_merge2(libs, oracles, width, la, lb):
         assert np.array_equal(lib.avx_merge_tuples(a, b, fn), exp)
 
 
-@pytest.mark.parametrize("k", [1, 2, 4, 5, 64, 128])
+@pytest.mark.parametrize("k", [1, 2, 3, 4, 5, 64, 128, 255, 256, 257, 1024, 2048])
 def test_multiway_merge(libs, oracles, width, k):
     orc, lib = oracles[width], libs[width]
     rng = np.random.default_rng(k)
-    runs = [orc.sort(rand_tuples(width, int(rng.integers(0, 3000)), 100 * k + i, 0, 10000))
+    maxlen = 3000 if k <= 256 else 300
+    runs = [orc.sort(rand_tuples(width, int(rng.integers(0, maxlen)), 100 * k + i, 0, 10000))
             for i in range(k)]
     exp = orc.multiway_merge(runs)
     for fn in ("avx_multiway_merge", "scalar_multiway_merge"):
         out, n, consumed = lib.avx_multiway_merge(runs, fn)
         assert n == len(exp)
         assert consumed  # parts[] advanced like avx_multiwaymerge.c:268-272
+        assert np.array_equal(out, exp)
+
+
+def test_multiway_merge_skew_and_large(libs, oracles, width):
+    """One hot key over every run (a value bucket larger than LDS: the merge
+    takes the merge-path tree), keys spanning the whole signed range, empty
+    runs between full ones, and the bench_multiwaymerge shape 64 x 65536."""
+    orc, lib = oracles[width], libs[width]
+    rng = np.random.default_rng(77)
+    hot = []
+    for i in range(8):
+        t = rand_tuples(width, 5000, 300 + i, 7, 8)
+        hot.append(orc.sort(t))
+    lo, hi = (-2 ** 31, 2 ** 31 - 1) if width == 8 else (-2 ** 62, 2 ** 62)
+    wide = [orc.sort(rand_tuples(width, int(rng.integers(0, 4000)), 400 + i, lo, hi))
+            if i % 3 else np.zeros(0, lib.dtype) for i in range(40)]
+    big = [orc.sort(rand_tuples(width, 65536, 500 + i, 1, 1 << 30)) for i in range(64)]
+    for runs in (hot, wide, big):
+        exp = orc.multiway_merge(runs)
+        out, n, consumed = lib.avx_multiway_merge(runs)
+        assert n == len(exp) and consumed
         assert np.array_equal(out, exp)
 
 

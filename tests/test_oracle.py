@@ -228,3 +228,44 @@ def test_int64_fp64_order_live_reference(oracles):
     w = (np.abs(key).astype(np.int64) << 20) | (np.arange(40000) & 0xFFFFF)
     v = np.where(key < 0, w | np.int64(-2 ** 63), w).astype(np.int64)
     np.testing.assert_array_equal(oracles[8].sort_int64_fp64(v), ref.sort_int64(v))
+
+
+# ---- large cases pinned by digests (tests/golden/golden_big.npz): the sort of
+# 2^20 tuples and multiway merges of fan-in 128..2048
+def _big():
+    with np.load(os.path.join(GOLD, "golden_big.npz"), allow_pickle=False) as d:
+        return {k: d[k] for k in d.files}
+
+
+def _mg():
+    import importlib
+    import sys
+    sys.path.insert(0, GOLD)
+    return importlib.import_module("make_golden")
+
+
+def check_big(w, got, g, tag):
+    mg = _mg()
+    if w == 8:
+        assert bytes(mg.digest(got)) == bytes(g[f"{tag}_out_digest"])
+    assert bytes(mg.digest(got["key"])) == bytes(g[f"{tag}_out_key_digest"])
+    assert bytes(mg.digest(canon(got))) == bytes(g[f"{tag}_out_canon_digest"])
+
+
+@pytest.mark.parametrize("w", [8, 16])
+def test_big_sort(w, oracles):
+    g, mg, orc = _big(), _mg(), oracles[w]
+    t = mg.big_sort_input(orc)
+    assert bytes(mg.digest(t)) == bytes(g[f"w{w}_sort_in_digest"])
+    check_big(w, orc.sort(t), g, f"w{w}_sort")
+
+
+@pytest.mark.parametrize("w", [8, 16])
+@pytest.mark.parametrize("k,maxlen", [(128, 900), (1024, 200), (2048, 100)])
+def test_big_multiway(w, k, maxlen, oracles):
+    g, mg, orc = _big(), _mg(), oracles[w]
+    runs = mg.sorted_runs(np.random.default_rng(k), k, maxlen, orc.dtype)
+    assert bytes(mg.digest(np.concatenate(runs))) == bytes(g[f"w{w}_mw{k}_in_digest"])
+    out = orc.multiway_merge(runs)
+    assert len(out) == int(g[f"w{w}_mw{k}_n"][0])
+    check_big(w, out, g, f"w{w}_mw{k}")
