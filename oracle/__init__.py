@@ -98,6 +98,19 @@ class Oracle(_Lib):
             _ptr(t), n, maxid, theta)
         return t
 
+    # the library's device generators, restated (datagen.hip) ---------------
+    def dev_gen_perm(self, n, first, total, maxid, seed, payload=True) -> np.ndarray:
+        t = np.zeros(n, self.dtype)
+        self.fn("dev_gen_perm", None, _P, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
+                C.c_uint64, C.c_int)(_ptr(t), n, first, total, maxid, seed, int(payload))
+        return t
+
+    def dev_gen_zipf(self, n, first, maxid, theta, seed) -> np.ndarray:
+        t = np.zeros(n, self.dtype)
+        self.fn("dev_gen_zipf", None, _P, C.c_uint64, C.c_uint64, C.c_uint64, C.c_double,
+                C.c_uint64)(_ptr(t), n, first, maxid, theta, seed)
+        return t
+
     # path -------------------------------------------------------------------
     def partition(self, t: np.ndarray, nbits: int, shift: int, padded: bool):
         fan = 1 << nbits

@@ -423,3 +423,121 @@ uint64_t orc_sortmergejoin(const tuple_t *R, const tuple_t *S, uint64_t nR,
     orc_sort_tuples(sortedS, (int64_t)nS);
     return orc_merge_join(sortedR, sortedS, nR, nS);
 }
+
+/* ------------------------------------------------------------------------ */
+/* The library's own device generators (avx-sort-merge-joins_amd/csrc/       */
+/* datagen.hip), restated on the CPU so that the GPU relations of the bench  */
+/* and the full-size tests are pinned.  They are not */
+/* the reference's generators (which draw from a time-seeded glibc rand()    */
+/* stream, src/datagen/generator.c:254-350, genzipf.c:97-159): they keep the */
+/* same shapes -- keys 1..N once each, payload 5 + index; FK keys            */
+/* perm(i) % maxid + 1; Zipf(theta) over 1..maxid with hot ranks spread by a */
+/* bijection -- but are evaluated per index so that a GPU can make any shard.*/
+/* ------------------------------------------------------------------------ */
+static uint64_t g_mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+typedef struct {
+    uint64_t total;
+    uint32_t half;
+    uint64_t key[4];
+} gperm_t;
+
+/* datagen.hip make_perm: 4-round Feistel network over 2*half bits */
+static gperm_t g_make_perm(uint64_t total, uint64_t seed) {
+    gperm_t p;
+    p.total = total ? total : 1;
+    uint32_t bits = 2;
+    while (bits < 64 && (1ull << bits) < p.total) bits++;
+    if (bits & 1) bits++;
+    p.half = bits / 2;
+    for (int i = 0; i < 4; i++) p.key[i] = g_mix64(seed * 4 + i + 0x5151);
+    return p;
+}
+
+static uint64_t g_feistel(const gperm_t *p, uint64_t x) {
+    const uint64_t m = (1ull << p->half) - 1;
+    uint64_t l = x >> p->half, r = x & m;
+    for (int i = 0; i < 4; i++) {
+        const uint64_t f = g_mix64(r ^ p->key[i]) & m;
+        const uint64_t nl = r;
+        r = l ^ f;
+        l = nl;
+    }
+    return (l << p->half) | r;
+}
+
+/* cycle walking: the bijection of [0, total) */
+static uint64_t g_perm(const gperm_t *p, uint64_t x) {
+    uint64_t y = g_feistel(p, x);
+    while (y >= p->total) y = g_feistel(p, y);
+    return y;
+}
+
+static tuple_t g_tuple(int64_t key, int64_t pay) {
+    tuple_t t;
+    t.key = (intkey_t)key;
+    t.payload = (value_t)pay;
+    return t;
+}
+
+/* k_gen_perm: gen_pk (maxid = total), gen_fk, gen_pk_nopayload (payload 0) */
+void orc_dev_gen_perm(tuple_t *out, uint64_t n, uint64_t first, uint64_t total,
+                      uint64_t maxid, uint64_t seed, int payload_mode) {
+    const gperm_t p = g_make_perm(total, seed);
+    if (!maxid) maxid = 1;
+    for (uint64_t i = 0; i < n; i++) {
+        const uint64_t g = first + i;
+        out[i] = g_tuple((int64_t)(g_perm(&p, g) % maxid) + 1,
+                         payload_mode ? (int64_t)(5 + g) : 0);
+    }
+}
+
+/* k_gen_zipf: rejection-inversion (Hormann & Derflinger) */
+static double g_h1(double x) {
+    return fabs(x) > 1e-8 ? log1p(x) / x : 1.0 - x * (0.5 - x * (1.0 / 3.0 - 0.25 * x));
+}
+static double g_h2(double x) {
+    return fabs(x) > 1e-8 ? expm1(x) / x
+                          : 1.0 + x * 0.5 * (1.0 + x * (1.0 / 3.0) * (1.0 + 0.25 * x));
+}
+static double g_H(double s, double x) {
+    const double lx = log(x);
+    return g_h2((1.0 - s) * lx) * lx;
+}
+static double g_hh(double s, double x) { return exp(-s * log(x)); }
+static double g_Hinv(double s, double x) {
+    double t = x * (1.0 - s);
+    if (t < -1.0) t = -1.0;
+    return exp(g_h1(t) * x);
+}
+
+void orc_dev_gen_zipf(tuple_t *out, uint64_t n, uint64_t first, uint64_t maxid,
+                      double theta, uint64_t seed) {
+    const uint64_t N = maxid ? maxid : 1;
+    const double s = theta;
+    const double hX1 = g_H(s, 1.5) - 1.0, hN = g_H(s, (double)N + 0.5);
+    const double sStar = 2.0 - g_Hinv(s, g_H(s, 2.5) - g_hh(s, 2.0));
+    const gperm_t alpha = g_make_perm(N, seed ^ 0xA1FA);
+    for (uint64_t i = 0; i < n; i++) {
+        const uint64_t g = first + i;
+        uint64_t k = 1;
+        for (uint32_t att = 0; att < 1000; att++) {
+            const uint64_t a = seed * 0x100000001B3ull + att;
+            const double u01 = (double)(g_mix64(a ^ g_mix64(g)) >> 11) *
+                               (1.0 / 9007199254740992.0);
+            const double u = hN + u01 * (hX1 - hN);
+            const double x = g_Hinv(s, u);
+            double kd = floor(x + 0.5);
+            if (kd < 1.0) kd = 1.0;
+            if (kd > (double)N) kd = (double)N;
+            k = (uint64_t)kd;
+            if (kd - x <= sStar || u >= g_H(s, kd + 0.5) - g_hh(s, kd)) break;
+        }
+        out[i] = g_tuple((int64_t)g_perm(&alpha, k - 1) + 1, 0);
+    }
+}

@@ -342,6 +342,48 @@ def test_device_generators(libs, width):
     assert abs(top[0] / n - 1 / H) < 0.15 / H
 
 
+@pytest.mark.parametrize("first,n,total,maxid,seed", [
+    (0, 1 << 20, 1 << 20, 1 << 20, 12345),          # PK
+    (777777, 300001, 128000000, 128000000, 12345),  # a shard of the 128M bench R
+    (5, 200000, 1000000, 333333, 54321)])           # FK over a smaller domain
+def test_device_generators_vs_restatement(libs, oracles, width, first, n, total, maxid, seed):
+    """datagen.hip against its C restatement (oracle orc_dev_gen_*): the
+    integer generators are bit-exact for every shard."""
+    import torch
+    lib, orc = libs[width], oracles[width]
+    t = lib.empty(n)
+    if maxid == total:
+        lib.dev_gen_pk(t, first, total, seed)
+    else:
+        lib.dev_gen_fk(t, first, total, maxid, seed)
+    torch.cuda.synchronize()
+    assert np.array_equal(lib.to_host(t), orc.dev_gen_perm(n, first, total, maxid, seed))
+    lib.dev_gen_pk(t, first, total, seed, with_payload=False)
+    torch.cuda.synchronize()
+    assert np.array_equal(lib.to_host(t), orc.dev_gen_perm(n, first, total, total, seed, False))
+
+
+@pytest.mark.parametrize("theta,maxid", [(0.75, 100000), (0.75, 128000000), (0.25, 5000),
+                                         (1.0, 1 << 20)])
+def test_device_zipf_vs_restatement(libs, oracles, width, theta, maxid):
+    """Zipf by rejection-inversion against the restatement: the sample
+    decisions rest on libm log/exp/log1p/expm1, which the device library may
+    round differently from glibc by an ulp, so an accept/reject near a
+    boundary can flip; the draws must agree except for such rare flips
+    (tolerance: 1 in 10^5 of the draws)."""
+    import torch
+    lib, orc = libs[width], oracles[width]
+    n, first = 1 << 20, 4242
+    z = lib.empty(n)
+    lib.dev_gen_zipf(z, first, maxid, theta, 54321)
+    torch.cuda.synchronize()
+    got = lib.to_host(z)
+    exp = orc.dev_gen_zipf(n, first, maxid, theta, 54321)
+    assert np.array_equal(got["payload"], exp["payload"])
+    bad = int(np.count_nonzero(got["key"] != exp["key"]))
+    assert bad <= n // 100000, bad
+
+
 # ------------------------------------------------------------ skew path
 def _hot_inputs(orc, width, n, payload):
     """R = PK 1..n; half of S is key 7 (one group far beyond LDS: the split
