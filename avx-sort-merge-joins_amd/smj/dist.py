@@ -40,9 +40,14 @@ import torch.distributed as dist
 # 9 / 10 / 11 / 12 bits (tools/bench_xpart.py): 12 bits scatter too thinly.
 MAX_PARTITION_BITS = 11
 INT64_MAX = (1 << 63) - 1
-# Largest single message of the row exchange.  RCCL 2.26 (torch 2.10 ROCm)
-# corrupts all_to_all_single messages of 1.6 GB and more (tools/debug_a2a.py);
-# larger exchanges go as chunked point-to-point sends in one group.
+# Largest single message of the row exchange.  RCCL 2.26.6 (torch 2.10 ROCm)
+# on a one-rank group leaves the second half of an all_to_all_single message
+# unwritten once the message exceeds 1 GiB: tools/a2a_bisect.py steps the
+# size in bytes for uint8, int32 and int64 elements and the first bad byte is
+# exactly half the message every time, from 1100 MiB up (1024 MiB is exact),
+# so the limit is a byte count inside RCCL, not an element count of ours
+# (profiles/r02_a2a_bisect.txt).  Larger exchanges go as chunked
+# point-to-point sends in one group.
 CHUNK_BYTES = int(os.environ.get("SMJ_A2A_CHUNK_MB", "512")) << 20
 
 
