@@ -1113,11 +1113,19 @@ void print_timing(uint64_t numtuples, struct timeval* start, struct timeval* end
     fflush(out);
 }
 
-// m-pass (src/joins/sortmergejoin_multipass.c:51-736): the reference sorts
-// the partitions, merges the sorted runs pass by pass with 2-way merges and
-// only then scans for matches.  The device form keeps that phase structure:
-// R and S are each fully sorted (device_sort), then one merge-path
-// merge-join scan counts the matches -- the phases m-way fuses.
+// m-pass (src/joins/sortmergejoin_multipass.c:51-736) in the reference's
+// phases, on the device:
+//   mpass_partitioning_phase (:295-335)  radix partition of R and S into
+//       PARTFANOUT partitions on the low key bits (the stable partition of
+//       partition_relation, partition.c:29);
+//   mpass_sorting_phase (:337-409)      every partition sorted on its own
+//       (segmented sort: LDS block sorts, then 2-way merge passes per run);
+//   mpass_firstnumamerge_phase + mpass_fullmultipassmerge_phase (:411-708)
+//       the PARTFANOUT sorted runs merged pass by pass with 2-way merges
+//       (the merge-path tree, ceil(log2 PARTFANOUT) passes);
+//   mpass_mergejoin_phase (:711-736)    one merge-join scan.
+// Unlike m-way (one multi-way merge, fused here into the bucket sort) every
+// merge pass reads and writes both relations once more.
 result_t* sortmergejoin_multipass(relation_t* relR, relation_t* relS,
                                   joinconfig_t* joincfg) {
     if ((joincfg->NTHREADS & (joincfg->NTHREADS - 1)) != 0) {
@@ -1135,9 +1143,35 @@ result_t* sortmergejoin_multipass(relation_t* relR, relation_t* relS,
     Tup* sS = (Tup*)c.ws.scratch("api_sortedS", (nS ? nS : 1) * sizeof(Tup));
     unsigned long long* cnt =
         (unsigned long long*)c.ws.scratch("api_cnt", sizeof(unsigned long long));
+    const uint32_t fan = joincfg->PARTFANOUT > 1 ? (uint32_t)joincfg->PARTFANOUT : 2;
+    const uint32_t bits = ceil_log2(fan);
+    const uint32_t F = 1u << bits;
+    const Digit32 dig{(uint32_t)(F - 1), 0};
+    int64_t* hist = (int64_t*)c.ws.scratch("mp_hist", (size_t)F * 8);
+    int64_t* off = (int64_t*)c.ws.scratch("mp_off", (size_t)F * 8);
+    const DevBuf* rels[2] = {&r, &s};
+    Tup* sorted[2] = {sR, sS};
+    const uint64_t ns[2] = {nR, nS};
+    static const char* pn[2] = {"mp_partR", "mp_partS"};
+    for (int q = 0; q < 2; q++) {
+        if (ns[q] == 0) continue;
+        Tup* part = (Tup*)c.ws.scratch(pn[q], ns[q] * sizeof(Tup));
+        stable_partition(&c.ws, rels[q]->d, ns[q], part, dig, bits, 0, hist, off, c.st);
+        std::vector<int64_t> hh(F), ho(F);
+        SMJ_CHECK(hipMemcpyAsync(hh.data(), hist, F * 8, hipMemcpyDeviceToHost, c.st));
+        SMJ_CHECK(hipMemcpyAsync(ho.data(), off, F * 8, hipMemcpyDeviceToHost, c.st));
+        sync();
+        std::vector<uint64_t> so(F), sl(F);
+        std::vector<const Tup*> runs(F);
+        for (uint32_t i = 0; i < F; i++) {
+            so[i] = (uint64_t)ho[i];
+            sl[i] = (uint64_t)hh[i];
+            runs[i] = part + so[i];
+        }
+        segmented_sort(&c.ws, part, so.data(), sl.data(), F, c.st);
+        multiway_merge_tree(&c.ws, runs.data(), sl.data(), F, sorted[q], c.st);
+    }
     SMJ_CHECK(hipMemsetAsync(cnt, 0, 8, c.st));
-    device_sort(&c.ws, r.d, nR, sR, c.st);
-    device_sort(&c.ws, s.d, nS, sS, c.st);
     merge_join_count(sR, nR, sS, nS, cnt, c.st);
     unsigned long long h = 0;
     SMJ_CHECK(hipMemcpyAsync(&h, cnt, 8, hipMemcpyDeviceToHost, c.st));

@@ -707,6 +707,15 @@ void multiway_merge(Workspace* ws, const Tup* const* runs, const uint64_t* lens,
     for (uint32_t i = 0; i < k; i++) total += lens[i];
     if (total == 0) return;
     if (multiway_merge_buckets(ws, runs, lens, k, total, out, st)) return;
+    multiway_merge_tree(ws, runs, lens, k, out, st);
+}
+
+// the merge-path tree alone: ceil(log2 k) passes of pairwise 2-way merges
+void multiway_merge_tree(Workspace* ws, const Tup* const* runs, const uint64_t* lens,
+                         uint32_t k, Tup* out, hipStream_t st) {
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < k; i++) total += lens[i];
+    if (total == 0) return;
     std::vector<const Tup*> cur(runs, runs + k);
     std::vector<uint64_t> cl(lens, lens + k);
     Tup* bufs[2] = {(Tup*)ws->scratch("mw_a", total * sizeof(Tup)),

@@ -247,6 +247,10 @@ void merge_join_count_batch(Workspace* ws, const Tup* const* r, const uint64_t* 
 void multiway_merge(Workspace* ws, const Tup* const* runs_host,
                     const uint64_t* lens_host, uint32_t k, Tup* out,
                     hipStream_t st);
+// the 2-way merge-path tree only (the m-pass join's multi-pass merging)
+void multiway_merge_tree(Workspace* ws, const Tup* const* runs_host,
+                         const uint64_t* lens_host, uint32_t k, Tup* out,
+                         hipStream_t st);
 
 // ---- materialize.hip : merge-join output tuples (sorted R and S)
 // Writes the first min(total, out_cap) output tuples and returns the total
