@@ -35,11 +35,14 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--op", default="join", choices=("join", "sort", "partition", "merge"),
+    p.add_argument("--op", default="join",
+                   choices=("join", "sort", "partition", "merge", "exchange"),
                    help="join: sortmergejoin_multiway (the headline); sort: bench_sort's "
                         "avxsort_tuples on 2^27 tuples; partition: bench_partitioning's "
                         "partition_relation_optimized on 2^27 tuples; merge: "
-                        "bench_multiwaymerge's avx_multiway_merge, --fanin runs of --n")
+                        "bench_multiwaymerge's avx_multiway_merge, --fanin runs of --n; "
+                        "exchange: the join's row all-to-all alone (numabench's memory "
+                        "bandwidth study, tputbench.c:665-1171, as xGMI bandwidth)")
     p.add_argument("--n", type=int, default=None,
                    help="tuples per relation per GPU (join: 128M; sort/partition: 2^27)")
     p.add_argument("--n-total", type=int, default=None,
@@ -217,6 +220,9 @@ def main():
         os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
+    if a.op == "exchange":
+        run_exchange(a, json_out, N, rank, local)
+        return
     import smj
     if a.width is None:
         a.width = 16 if a.op == "join" else 8
@@ -383,6 +389,68 @@ def dominant_roofline(kern, bytes_of, cfg_key):
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
             "traffic": load_traffic(name, cfg_key), "alg_bytes_per_launch": b,
             "avg_launch_ms": round(ms / launches, 4)}
+
+
+def run_exchange(a, json_out, N, rank, local):
+    """The multi-GPU join's exchange step alone: every rank sends --n packed
+    64-bit words (the 16-byte join's exchange layout; default 128M, one
+    relation's worth per GPU) split evenly over all ranks with one
+    all_to_all_single per step (RCCL over xGMI; at N=1 a device-local copy).
+    value = bytes that crossed to OTHER ranks, all ranks, per second."""
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29533")
+    os.environ.setdefault("RANK", "0")
+    os.environ.setdefault("WORLD_SIZE", "1")
+    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    n = (a.n or 128_000_000) // N * N
+    # one message per destination, below RCCL's 1 GiB limit (DESIGN.md §8)
+    assert n // N * 8 <= 512 << 20 or N == 1, "message above 512 MB: use --n smaller"
+    src = torch.arange(n, dtype=torch.int64, device="cuda") + rank * n
+    dst = torch.empty_like(src)
+    sizes = [n // N] * N
+
+    def step():
+        dist.all_to_all_single(dst, src, sizes, sizes)
+
+    class _NoTrace:
+        def trace(self, on):
+            pass
+
+        def trace_read(self):
+            return {}
+    elapsed, _ = timed_loop(a, _NoTrace(), dist if N > 1 else None, step)
+    # every rank received block `rank` of every source, in source order
+    expect = torch.cat([torch.arange(n // N, dtype=torch.int64, device="cuda") + g * n
+                        + rank * (n // N) for g in range(N)])
+    ok = bool(torch.equal(dst, expect))
+    t = elapsed / a.steps
+    cross = 8 * (n - n // N) * N  # bytes leaving their rank, all ranks
+    moved = 8 * n * N             # all bytes, the local block included
+    if rank == 0:
+        xgmi_peak = 7 * 153.0  # GB/s per GPU, one direction (MI355X_MICROARCH.md)
+        per_gpu = (cross / N) / t / 1e9 if N > 1 else None
+        out = {
+            "metric": "exchange (row all-to-all) GB/s per GPU over xGMI",
+            "value": round(per_gpu if per_gpu is not None else moved / t / 1e9, 1),
+            "unit": "GB/s", "n_gpus": N, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(t * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "int64", "data": "synthetic",
+            "config": {"workload": f"all_to_all_single of {n} 8-byte words per GPU "
+                                   f"({n // N} to each of {N} ranks)",
+                       "words_per_gpu": n, "parallelism": f"all-to-all x{N}"},
+            "roofline": ({"bound": "xgmi", "achieved": round(per_gpu, 1), "peak": xgmi_peak,
+                          "unit": "GB/s", "frac": round(per_gpu / xgmi_peak, 4), "traffic": None}
+                         if per_gpu is not None else
+                         {"bound": "hbm", "achieved": round(2 * moved / t / 1e9, 1),
+                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": round(2 * moved / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                          "note": "N=1: a device-local copy (read + write)"}),
+            "cpu_baseline": None,
+            "result_ok": ok,
+        }
+        print(json.dumps(out), file=json_out, flush=True)
+    dist.destroy_process_group()
 
 
 def run_op(a, lib, json_out, dist, N, rank):
