@@ -793,12 +793,13 @@ static void run_v6(Ctx& c, int reps, const char* label) {
     SMJ_CHECK(hipFree(starts));
 }
 
-template <int THREADS, int ITEMS, int FIX, bool B = false, int HS = 1>
+template <int THREADS, int ITEMS, int FIX, bool B = false, int HS = 1, int WPC = 1,
+          int HT = 512, int HI = 16>
 static void run_swa(Ctx& c, int reps, const char* label) {
     typedef SwaGeom<THREADS, ITEMS> G;
     typedef SwbGeom<THREADS, ITEMS> GB;
     uint64_t ntiles = (c.n + G::TILE - 1) / G::TILE;
-    uint32_t nwg = (uint32_t)std::min<uint64_t>(ntiles, 256);
+    uint32_t nwg = (uint32_t)std::min<uint64_t>(ntiles, 256 * WPC);
     const uint64_t tpw = (ntiles + nwg - 1) / nwg;
     const uint64_t chunk = tpw * G::TILE;
     nwg = (uint32_t)((ntiles + tpw - 1) / tpw);
@@ -824,7 +825,7 @@ static void run_swa(Ctx& c, int reps, const char* label) {
     SMJ_CHECK(hipMemset(c.dout, 0, c.cap * sizeof(Tup)));
     for (int r = -1; r < reps; r++) {
         SMJ_CHECK(hipEventRecord(e[0]));
-        hipLaunchKernelGGL((k_h6<512, 16, false>), dim3(nwg * HS), dim3(512), c.nbins * 4, 0, c.din,
+        hipLaunchKernelGGL((k_h6<HT, HI, false>), dim3(nwg * HS), dim3(HT), c.nbins * 4, 0, c.din,
                            c.n, chunk / HS, dig, c.nbins, counts, nwg * HS);
         SMJ_CHECK(hipEventRecord(e[1]));
         hipLaunchKernelGGL(k_scanrow6, dim3(c.nbins), dim3(256), 0, 0, counts, nwg * HS, totals);
@@ -917,6 +918,10 @@ int argc, char** argv) {
     if (only.empty() || only == name) run_swa<T, I, F>(c, reps, name);
 #define SWB(T, I, F, name) \
     if (only.empty() || only == name) run_swa<T, I, F, true>(c, reps, name);
+#define SWAW(T, I, F, W, name) \
+    if (only.empty() || only == name) run_swa<T, I, F, false, 1, W>(c, reps, name);
+#define SWAH(HT, HI, name) \
+    if (only.empty() || only == name) run_swa<512, 16, 1, false, 1, 1, HT, HI>(c, reps, name);
 #define SWBH(T, I, F, H, name) \
     if (only.empty() || only == name) run_swa<T, I, F, true, H>(c, reps, name);
 #ifdef KEY_8B
@@ -927,6 +932,15 @@ int argc, char** argv) {
     SWB(1024, 3, 17, "swb 1024x3 scan1");
 #else
     SWA(512, 16, 1, "swa 512x16 fix1");
+    SWAH(1024, 16, "hist 1024x16");
+    SWAH(1024, 8, "hist 1024x8");
+    SWAH(1024, 32, "hist 1024x32");
+    SWAH(512, 32, "hist 512x32");
+    SWAW(512, 8, 1, 1, "swa 512x8 1/cu");
+    SWAW(512, 8, 1, 2, "swa 512x8 2/cu");
+    SWAW(256, 16, 1, 1, "swa 256x16 1/cu");
+    SWAW(256, 16, 1, 2, "swa 256x16 2/cu");
+    SWAW(256, 8, 1, 3, "swa 256x8 3/cu");
     SWB(512, 16, 1, "swb 512x16");
     SWB(512, 16, 17, "swb 512x16 scan1");
     SWB(1024, 6, 1, "swb 1024x6");
