@@ -622,7 +622,7 @@ static uint64_t merge_tuples_common(const void* A, const void* B, void* O,
     DevBuf a = dev_in(A, la, "api_ma", true);
     DevBuf b = dev_in(B, lb, "api_mb", true);
     DevBuf o = dev_in(O, la + lb, "api_mo", false);
-    merge2(a.d, la, b.d, lb, o.d, c.st);
+    merge2(&c.ws, a.d, la, b.d, lb, o.d, c.st);
     dev_out(o, la + lb);
     sync();
     return la + lb;
@@ -656,7 +656,7 @@ static uint64_t merge_int64_common(const int64_t* A, const int64_t* B, int64_t* 
 #ifndef KEY_8B
     if (la) hipLaunchKernelGGL(k_fp64_ord, dim3(grid_n(la)), dim3(256), 0, c.st, da, da, la);
     if (lb) hipLaunchKernelGGL(k_fp64_ord, dim3(grid_n(lb)), dim3(256), 0, c.st, db, db, lb);
-    merge2((const Tup*)da, la, (const Tup*)db, lb, (Tup*)dn, c.st);
+    merge2(&c.ws, (const Tup*)da, la, (const Tup*)db, lb, (Tup*)dn, c.st);
     hipLaunchKernelGGL(k_fp64_ord, dim3(grid_n(n)), dim3(256), 0, c.st, dn, dn, n);
 #else
     Tup* ta = (Tup*)c.ws.scratch("api_mi_ta", (la ? la : 1) * sizeof(Tup));
@@ -664,7 +664,7 @@ static uint64_t merge_int64_common(const int64_t* A, const int64_t* B, int64_t* 
     Tup* to = (Tup*)c.ws.scratch("api_mi_to", n * sizeof(Tup));
     if (la) hipLaunchKernelGGL(k_expand_i64, dim3(grid_n(la)), dim3(256), 0, c.st, da, ta, la, fp64);
     if (lb) hipLaunchKernelGGL(k_expand_i64, dim3(grid_n(lb)), dim3(256), 0, c.st, db, tb, lb, fp64);
-    merge2(ta, la, tb, lb, to, c.st);
+    merge2(&c.ws, ta, la, tb, lb, to, c.st);
     hipLaunchKernelGGL(k_compact_i64, dim3(grid_n(n)), dim3(256), 0, c.st, to, dn, n, fp64);
 #endif
     SMJ_CHECK(hipMemcpyAsync(O, dn, n * 8, hipMemcpyDefault, c.st));
@@ -1238,7 +1238,7 @@ void smj_dev_sort(smj_workspace* ws, const tuple_t* in, uint64_t n,
 
 void smj_dev_merge2(const tuple_t* a, uint64_t na, const tuple_t* b,
                     uint64_t nb, tuple_t* out, smj_stream_t stream) {
-    merge2((const Tup*)a, na, (const Tup*)b, nb, (Tup*)out, (hipStream_t)stream);
+    merge2(&ctx().ws, (const Tup*)a, na, (const Tup*)b, nb, (Tup*)out, (hipStream_t)stream);
 }
 
 void smj_dev_multiway_merge_host(smj_workspace* ws, const tuple_t* const* runs,

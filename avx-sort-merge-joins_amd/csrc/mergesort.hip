@@ -11,7 +11,8 @@
 // (co-rank binary search on the two inputs), so each workgroup reads exactly
 // the slices of A and B that produce its 2048 outputs with coalesced 16-byte
 // lane loads, merges them in LDS and writes a contiguous output tile.  Block
-// sorts run a bitonic sorting network over an LDS tile.
+// sorts run a bitonic network in registers (lane shuffles, LDS only across
+// waves).
 #include <algorithm>
 
 #include "smj_common.hpp"
@@ -104,34 +105,87 @@ struct SortBlock {
     uint32_t len;
 };
 
+__device__ __forceinline__ Tup shfl_xor_tup(const Tup& v, int m) {
+#ifdef KEY_8B
+    Tup r;
+    r.payload = __shfl_xor(v.payload, m, 64);
+    r.key = __shfl_xor(v.key, m, 64);
+    return r;
+#else
+    return (Tup)__shfl_xor((unsigned long long)v, m, 64);
+#endif
+}
+
+// compare-exchange of element e with its partner of stage (k, j): keep the
+// minimum when e is the pair's lower index of an ascending run (or the upper
+// index of a descending one), else the maximum
+__device__ __forceinline__ void bs_keep(Tup& x, const Tup& y, uint32_t e, uint32_t j,
+                                        uint32_t k) {
+    const bool keep_min = ((e & j) == 0) == ((e & k) == 0);
+    if (keep_min ? tup_less(y, x) : tup_less(x, y)) x = y;
+}
+
+// Bitonic sort of one block of up to BS_BLOCK tuples, in registers: thread t
+// holds elements [BS_IPT t, BS_IPT (t + 1)); stages whose partner is inside
+// the thread swap registers, stages with a partner in another lane of the
+// wave exchange through __shfl_xor, and only the stages across waves
+// (j >= 64 BS_IPT: three of the 66 at 2048 elements) go through LDS.
+// (avxsort_core.h:1276-1399 sorts its cache-sized blocks with in-register
+// AVX networks the same way.)
+constexpr uint32_t BS_IPT = BS_BLOCK / BS_THREADS;
 __global__ void __launch_bounds__(BS_THREADS)
 k_blocksort(Tup* __restrict__ data, const SortBlock* __restrict__ blocks) {
     __shared__ __attribute__((aligned(16))) Tup sm[BS_BLOCK];
     const SortBlock blk = blocks[blockIdx.x];
-    uint32_t P2 = 2;
-    while (P2 < blk.len) P2 <<= 1;
     const Tup sent = tup_max_sentinel();
-    for (uint32_t i = threadIdx.x; i < P2; i += BS_THREADS)
+    const uint32_t t = threadIdx.x;
+    // coalesced load (sentinels past the end), then BS_IPT consecutive
+    // elements per thread
+    for (uint32_t i = t; i < BS_BLOCK; i += BS_THREADS)
         sm[i] = i < blk.len ? data[blk.off + i] : sent;
     __syncthreads();
-    // bitonic sorting network over P2 items (ascending)
-    for (uint32_t k = 2; k <= P2; k <<= 1) {
+    Tup v[BS_IPT];
+#pragma unroll
+    for (uint32_t i = 0; i < BS_IPT; i++) v[i] = sm[t * BS_IPT + i];
+    for (uint32_t k = 2; k <= BS_BLOCK; k <<= 1) {
         for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t t = threadIdx.x; t < P2 / 2; t += BS_THREADS) {
-                const uint32_t i = 2 * t - (t & (j - 1));  // lower index
-                const uint32_t l = i + j;
-                const bool up = (i & k) == 0;
-                Tup x = sm[i], y = sm[l];
-                if (tup_less(y, x) == up) {
-                    sm[i] = y;
-                    sm[l] = x;
+            if (j >= 64 * BS_IPT) {  // partner in another wave
+                __syncthreads();
+#pragma unroll
+                for (uint32_t i = 0; i < BS_IPT; i++) sm[t * BS_IPT + i] = v[i];
+                __syncthreads();
+#pragma unroll
+                for (uint32_t i = 0; i < BS_IPT; i++) {
+                    const uint32_t e = t * BS_IPT + i;
+                    bs_keep(v[i], sm[e ^ j], e, j, k);
+                }
+            } else if (j >= BS_IPT) {  // partner in lane ^ (j / BS_IPT)
+#pragma unroll
+                for (uint32_t i = 0; i < BS_IPT; i++) {
+                    const uint32_t e = t * BS_IPT + i;
+                    bs_keep(v[i], shfl_xor_tup(v[i], (int)(j / BS_IPT)), e, j, k);
+                }
+            } else {  // partner in this thread
+#pragma unroll
+                for (uint32_t i = 0; i < BS_IPT; i++) {
+                    const uint32_t i2 = i ^ j;
+                    if (i2 > i) {
+                        const bool up = ((t * BS_IPT + i) & k) == 0;
+                        if (tup_less(v[i2], v[i]) == up) {
+                            const Tup x = v[i];
+                            v[i] = v[i2];
+                            v[i2] = x;
+                        }
+                    }
                 }
             }
-            __syncthreads();
         }
     }
-    for (uint32_t i = threadIdx.x; i < blk.len; i += BS_THREADS)
-        data[blk.off + i] = sm[i];
+    __syncthreads();
+#pragma unroll
+    for (uint32_t i = 0; i < BS_IPT; i++) sm[t * BS_IPT + i] = v[i];
+    __syncthreads();
+    for (uint32_t i = t; i < blk.len; i += BS_THREADS) data[blk.off + i] = sm[i];
 }
 
 // ---------------------------------------------------------------------------
@@ -226,10 +280,11 @@ static void launch_tiles(Workspace* ws, const std::vector<MergeTile>& tiles,
     // pinned memory so the upload is stream ordered
     const size_t bytes = tiles.size() * sizeof(MergeTile);
     MergeTile* dev = (MergeTile*)ws->scratch("mg_tiles", bytes);
-    MergeTile* h = (MergeTile*)ws->host_pinned("mg_tiles_h", bytes);
-    SMJ_CHECK(hipStreamSynchronize(st));  // pinned staging buffer is reused
+    uint32_t slot;
+    MergeTile* h = (MergeTile*)ws->ring_acquire("mg_tiles_h", bytes, &slot);
     std::copy(tiles.begin(), tiles.end(), h);
     SMJ_CHECK(hipMemcpyAsync(dev, h, bytes, hipMemcpyHostToDevice, st));
+    ws->ring_release("mg_tiles_h", slot, st);
     hipLaunchKernelGGL(k_mergetile, dim3((uint32_t)tiles.size()),
                        dim3(MG_THREADS), 0, st, dev);
     SMJ_CHECK(hipGetLastError());
@@ -251,12 +306,11 @@ static void add_pair_tiles(std::vector<MergeTile>& v, const Tup* a,
     }
 }
 
-void merge2(const Tup* a, uint64_t na, const Tup* b, uint64_t nb, Tup* out,
+void merge2(Workspace* ws, const Tup* a, uint64_t na, const Tup* b, uint64_t nb, Tup* out,
             hipStream_t st) {
-    static Workspace ws2;
     std::vector<MergeTile> v;
     add_pair_tiles(v, a, na, b, nb, out);
-    launch_tiles(&ws2, v, st);
+    launch_tiles(ws, v, st);  // the caller's workspace: one per thread/stream
 }
 
 void merge_join_count(const Tup* r, uint64_t nr, const Tup* s, uint64_t ns,
@@ -275,10 +329,11 @@ void merge_join_count_batch(Workspace* ws, const Tup* const* r, const uint64_t* 
     if (k == 0) return;
     const size_t bytes = (size_t)k * sizeof(JoinPair);
     JoinPair* dev = (JoinPair*)ws->scratch("mj_pairs", bytes);
-    JoinPair* h = (JoinPair*)ws->host_pinned("mj_pairs_h", bytes);
-    SMJ_CHECK(hipStreamSynchronize(st));  // the pinned table is reused
+    uint32_t slot;
+    JoinPair* h = (JoinPair*)ws->ring_acquire("mj_pairs_h", bytes, &slot);
     for (uint32_t i = 0; i < k; i++) h[i] = JoinPair{r[i], s[i], nr[i], ns[i]};
     SMJ_CHECK(hipMemcpyAsync(dev, h, bytes, hipMemcpyHostToDevice, st));
+    ws->ring_release("mj_pairs_h", slot, st);
     hipLaunchKernelGGL(k_mjcount_batch, dim3(k), dim3(256), 0, st, dev, count_dev);
     SMJ_CHECK(hipGetLastError());
 }
@@ -302,10 +357,11 @@ void segmented_sort(Workspace* ws, Tup* data, const uint64_t* seg_off,
     {
         const size_t bytes = blocks.size() * sizeof(SortBlock);
         SortBlock* dev = (SortBlock*)ws->scratch("ms_blocks", bytes);
-        SortBlock* h = (SortBlock*)ws->host_pinned("ms_blocks_h", bytes);
-        SMJ_CHECK(hipStreamSynchronize(st));
+        uint32_t slot;
+        SortBlock* h = (SortBlock*)ws->ring_acquire("ms_blocks_h", bytes, &slot);
         std::copy(blocks.begin(), blocks.end(), h);
         SMJ_CHECK(hipMemcpyAsync(dev, h, bytes, hipMemcpyHostToDevice, st));
+        ws->ring_release("ms_blocks_h", slot, st);
         hipLaunchKernelGGL(k_blocksort, dim3((uint32_t)blocks.size()),
                            dim3(BS_THREADS), 0, st, data, dev);
         SMJ_CHECK(hipGetLastError());

@@ -86,6 +86,39 @@ struct Workspace {
         pinned[name] = {p, bytes};
         return p;
     }
+    // Rings of pinned staging slots for host-built tables that are uploaded
+    // stream-ordered before a launch: a slot is rewritten only after the copy
+    // that used it kNRing uploads ago has finished (its event), so
+    // consecutive launches never wait for the stream to drain.
+    static constexpr uint32_t kNRing = 8;
+    struct RingSlot {
+        void* p = nullptr;
+        size_t cap = 0;
+        hipEvent_t ev = nullptr;
+        bool used = false;
+    };
+    std::map<std::string, std::pair<std::vector<RingSlot>, uint32_t>> rings;
+    void* ring_acquire(const char* name, size_t bytes, uint32_t* slot) {
+        auto& r = rings[name];
+        if (r.first.empty()) r.first.resize(kNRing);
+        const uint32_t i = r.second++ % kNRing;
+        RingSlot& s = r.first[i];
+        if (s.used) SMJ_CHECK(hipEventSynchronize(s.ev));
+        if (s.cap < bytes) {
+            if (s.p) SMJ_CHECK(hipHostFree(s.p));
+            SMJ_CHECK(hipHostMalloc(&s.p, bytes ? bytes : 16, hipHostMallocDefault));
+            s.cap = bytes;
+        }
+        if (!s.ev) SMJ_CHECK(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
+        *slot = i;
+        return s.p;
+    }
+    // after the hipMemcpyAsync that reads the slot
+    void ring_release(const char* name, uint32_t slot, hipStream_t st) {
+        RingSlot& s = rings[name].first[slot];
+        SMJ_CHECK(hipEventRecord(s.ev, st));
+        s.used = true;
+    }
     void events() {
         if (!ev_init) {
             for (auto& e : ev) SMJ_CHECK(hipEventCreate(&e));
@@ -236,7 +269,7 @@ void plan_from_sample(Workspace* ws, const Tup* const* rels,
 // ---- mergesort.hip : general segmented merge sort + merge path kernels
 void segmented_sort(Workspace* ws, Tup* data, const uint64_t* seg_off_host,
                     const uint64_t* seg_len_host, uint32_t nseg, hipStream_t st);
-void merge2(const Tup* a, uint64_t na, const Tup* b, uint64_t nb, Tup* out,
+void merge2(Workspace* ws, const Tup* a, uint64_t na, const Tup* b, uint64_t nb, Tup* out,
             hipStream_t st);
 void merge_join_count(const Tup* r, uint64_t nr, const Tup* s, uint64_t ns,
                       unsigned long long* count_dev, hipStream_t st);
