@@ -129,11 +129,13 @@ static void choose_levels(uint64_t n, uint32_t want_d1, uint32_t* D1,
                           uint32_t* D2, uint32_t* D2cap) {
     const uint64_t target = kGroupTarget;
     uint32_t B = n > target ? ceil_log2((n + target - 1) / target) : 0;
-    // level 1: 512 partitions by default (the scatter's write streams stay
-    // long enough), more when a bucket would exceed ~192 tiles of the tile
-    // pass (the group pass takes up to 256 per bucket): N1024 keeps 2^10
-    // partitions, within the sampled scatter's LDS carries
-    uint32_t d1 = want_d1 ? want_d1 : 9;
+    // level 1: 256 partitions by default, more when a bucket would exceed
+    // ~192 tiles of the tile pass (the group pass takes up to 256 per bucket):
+    // N1024 keeps 2^10 partitions, within the sampled scatter's LDS carries.
+    // 128M x 128M, interleaved A/B on one box (tools/ab_fanout.sh): 256
+    // partitions 3.57 / 3.09 ms (16 / 8 B) against 3.63 / 3.16 ms with 512 --
+    // longer scatter streams and tile-pass runs, a slightly slower group pass
+    uint32_t d1 = want_d1 ? want_d1 : 8;
     const uint64_t bucket_cap = 192ull * kTileTuples;
     while (d1 < kNarrowDigitBits && (n >> d1) > bucket_cap) d1++;
     if (d1 > B) d1 = B;
@@ -1052,7 +1054,7 @@ static result_t* join_api(relation_t* relR, relation_t* relS,
     if (joincfg->PARTFANOUT > 0) fb = ceil_log2((uint64_t)joincfg->PARTFANOUT);
     // the reference fan-out (128 by default) only sizes the level-1 pass here;
     // choose_levels raises it as the relation size needs
-    if (fb < 9) fb = 9;
+    if (fb < 8) fb = 8;
     device_join(&c.ws, r.d, nR, s.d, nS, sR, sS, fb, 1, 0, cnt, c.st);
     unsigned long long h = 0;
     SMJ_CHECK(hipMemcpyAsync(&h, cnt, 8, hipMemcpyDeviceToHost, c.st));

@@ -34,11 +34,14 @@ import os
 import torch
 import torch.distributed as dist
 
-# Widest exchange partition: 2^11 partitions (at 8 GPUs 256 per rank, each
-# ~61 tiles of the local tile pass, within its 128-tile bucket limit).  The
-# exact scatter costs 0.96 / 1.09 / 1.53 / 3.32 ms per 128M 16-byte tuples at
-# 9 / 10 / 11 / 12 bits (tools/bench_xpart.py): 12 bits scatter too thinly.
-MAX_PARTITION_BITS = 11
+# Widest exchange partition: 2^10 partitions.  At 8 GPUs that is 128 per
+# rank, each ~1M tuples of a relation in 8 source segments (~130 tiles of the
+# local tile pass: the group pass takes up to 256 per bucket, and the 1-GPU
+# join with 2^7 sampled partitions runs exactly that shape).  The exact
+# scatter costs 0.96 / 1.09 / 1.53 / 3.32 ms per 128M 16-byte tuples at
+# 9 / 10 / 11 / 12 bits (tools/bench_xpart.py): wider exchange partitions
+# scatter too thinly.
+MAX_PARTITION_BITS = 10
 INT64_MAX = (1 << 63) - 1
 # Largest single message of the row exchange.  RCCL 2.26.6 (torch 2.10 ROCm)
 # on a one-rank group leaves the second half of an all_to_all_single message

@@ -56,7 +56,9 @@ def parse():
     p.add_argument("--shift", type=int, default=0, help="partition: shift bits")
     p.add_argument("--dist", default="uniform", choices=("uniform", "zipf"))
     p.add_argument("--theta", type=float, default=0.75)
-    p.add_argument("--fanout-bits", type=int, default=9)
+    p.add_argument("--fanout-bits", type=int, default=8,
+                   help="level-1 partitions (2^bits) of the join; the library raises it "
+                        "as the relation size needs")
     p.add_argument("--cpu-n", type=int, default=128_000_000,
                    help="tuples per relation of the bounded CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
