@@ -160,26 +160,54 @@ static bool use_sampled() {
 }
 
 // exact key range [min, max] of the relations (one read pass); min > max
-// when they are empty
+// when they are empty.  16-byte non-temporal loads, KR_U of them in flight per
+// thread (the scalar 8-byte loads of the first version reached 3.0 TB/s on
+// 2^27 x 8 B), one pair of atomics per workgroup.
+typedef unsigned long long KrVec __attribute__((ext_vector_type(2)));
+constexpr int KR_U = 8;
+
+__device__ __forceinline__ void kr_acc(uint64_t u, uint64_t& lo, uint64_t& hi) {
+    lo = u < lo ? u : lo;
+    hi = u > hi ? u : hi;
+}
+
+__device__ __forceinline__ void kr_vec(const KrVec& v, uint64_t& lo, uint64_t& hi) {
+#ifdef KEY_8B
+    kr_acc(key_u((int64_t)v.y), lo, hi);  // Tup {payload, key}
+#else
+    kr_acc(key_u(tup_key((Tup)v.x)), lo, hi);
+    kr_acc(key_u(tup_key((Tup)v.y)), lo, hi);
+#endif
+}
+
 __global__ void __launch_bounds__(256)
 k_keyrange(const Tup* __restrict__ r0, uint64_t n0, const Tup* __restrict__ r1, uint64_t n1,
            unsigned long long* __restrict__ mm) {
+    __shared__ unsigned long long sl[4], sh[4];
     uint64_t lo = ~0ull, hi = 0;  // key_u order
-    const uint64_t stride = (uint64_t)gridDim.x * 256 * 4;
+    const uint64_t gt = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t G = (uint64_t)gridDim.x * 256;
     for (int rel = 0; rel < 2; rel++) {
         const Tup* p = rel ? r1 : r0;
         const uint64_t n = rel ? n1 : n0;
-        if (!p) continue;
-        for (uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += stride) {
-            Tup t[4];
+        if (!p || n == 0) continue;
+        if (((uintptr_t)p & 15) == 0) {
+            const KrVec* v = reinterpret_cast<const KrVec*>(p);
+            const uint64_t nv = n * sizeof(Tup) / 16;
+            for (uint64_t i0 = gt; i0 < nv; i0 += G * KR_U) {
+                KrVec x[KR_U];
 #pragma unroll
-            for (int k = 0; k < 4; k++) t[k] = p[i + k < n ? i + k : n - 1];
+                for (int u = 0; u < KR_U; u++) {
+                    const uint64_t i = i0 + u * G;
+                    x[u] = __builtin_nontemporal_load(v + (i < nv ? i : nv - 1));
+                }
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const uint64_t u = key_u(tup_key(t[k]));
-                lo = u < lo ? u : lo;
-                hi = u > hi ? u : hi;
+                for (int u = 0; u < KR_U; u++) kr_vec(x[u], lo, hi);
             }
+            // 8-byte tuples: an odd last one
+            if (gt == 0 && nv * 16 / sizeof(Tup) < n) kr_acc(key_u(tup_key(p[n - 1])), lo, hi);
+        } else {
+            for (uint64_t i = gt; i < n; i += G) kr_acc(key_u(tup_key(p[i])), lo, hi);
         }
     }
 #pragma unroll
@@ -189,6 +217,15 @@ k_keyrange(const Tup* __restrict__ r0, uint64_t n0, const Tup* __restrict__ r1, 
         hi = c > hi ? c : hi;
     }
     if (lane_id() == 0) {
+        sl[threadIdx.x >> 6] = lo;
+        sh[threadIdx.x >> 6] = hi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 4; w++) {
+            lo = sl[w] < lo ? sl[w] : lo;
+            hi = sh[w] > hi ? sh[w] : hi;
+        }
         atomicMin(&mm[0], (unsigned long long)lo);
         atomicMax(&mm[1], (unsigned long long)hi);
     }
@@ -201,10 +238,11 @@ static bool key_range(Workspace* ws, const Tup* const* rels, const uint64_t* ns,
     const unsigned long long init[2] = {~0ull, 0ull};
     SMJ_CHECK(hipMemcpyAsync(mm, init, 16, hipMemcpyHostToDevice, st));
     const uint64_t n = ns[0] + (nrel > 1 ? ns[1] : 0);
-    uint32_t g = (uint32_t)((n + 1023) / 1024);
-    if (g > 2048) g = 2048;
+    // 4 workgroups per CU, each thread KR_U vectors per round
+    uint64_t g = (n * sizeof(Tup) / 16 + 256 * KR_U - 1) / (256 * KR_U);
+    if (g > 1024) g = 1024;
     if (g == 0) g = 1;
-    hipLaunchKernelGGL(k_keyrange, dim3(g), dim3(256), 0, st, rels[0], ns[0],
+    hipLaunchKernelGGL(k_keyrange, dim3((uint32_t)g), dim3(256), 0, st, rels[0], ns[0],
                        nrel > 1 ? rels[1] : (const Tup*)nullptr, nrel > 1 ? ns[1] : 0, mm);
     SMJ_CHECK(hipMemcpyAsync(h, mm, 16, hipMemcpyDeviceToHost, st));
     SMJ_CHECK(hipStreamSynchronize(st));

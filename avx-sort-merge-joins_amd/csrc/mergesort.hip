@@ -59,15 +59,15 @@ k_mergetile(const MergeTile* __restrict__ tiles) {
     if (threadIdx.x < 2) {
         const uint64_t d = threadIdx.x == 0 ? T.d0 : T.d1;
         sh_ab[threadIdx.x] = corank(
-            d, T.na, T.nb, [&](uint64_t i) { return T.a[i]; },
-            [&](uint64_t i) { return T.b[i]; });
+            d, T.na, T.nb, [&](uint64_t i) { return ld_g(T.a + i); },
+            [&](uint64_t i) { return ld_g(T.b + i); });
     }
     __syncthreads();
     const uint64_t a0 = sh_ab[0], a1 = sh_ab[1];
     const uint64_t b0 = T.d0 - a0, b1 = T.d1 - a1;
     const uint32_t la = (uint32_t)(a1 - a0), lb = (uint32_t)(b1 - b0);
-    for (uint32_t i = threadIdx.x; i < la; i += MG_THREADS) sm[i] = T.a[a0 + i];
-    for (uint32_t i = threadIdx.x; i < lb; i += MG_THREADS) sm[la + i] = T.b[b0 + i];
+    for (uint32_t i = threadIdx.x; i < la; i += MG_THREADS) sm[i] = ld_g(T.a + a0 + i);
+    for (uint32_t i = threadIdx.x; i < lb; i += MG_THREADS) sm[la + i] = ld_g(T.b + b0 + i);
     __syncthreads();
     const Tup* As = sm;
     const Tup* Bs = sm + la;
@@ -79,16 +79,17 @@ k_mergetile(const MergeTile* __restrict__ tiles) {
             p, la, lb, [&](uint64_t x) { return As[x]; },
             [&](uint64_t x) { return Bs[x]; });
         uint32_t j = p - i;
+        // branch-free, selecting values (selecting LDS references sent res
+        // to scratch); past the end both runs are exhausted and the result
+        // is not stored
 #pragma unroll
         for (int k = 0; k < MG_IPT; k++) {
-            if (p + k < len) {
-                bool takeA;
-                if (i >= la) takeA = false;
-                else if (j >= lb) takeA = true;
-                else takeA = !tup_less(Bs[j], As[i]);
-                res[k] = takeA ? As[i] : Bs[j];
-                if (takeA) i++; else j++;
-            }
+            const Tup av = sm[min(i, len - 1)];
+            const Tup bv = sm[min(la + j, len - 1)];
+            const bool takeA = i < la && (j >= lb || !tup_less(bv, av));
+            res[k] = tup_sel(takeA, av, bv);
+            i += takeA ? 1 : 0;
+            j += takeA ? 0 : 1;
         }
     }
     __syncthreads();
@@ -96,7 +97,7 @@ k_mergetile(const MergeTile* __restrict__ tiles) {
     for (int k = 0; k < MG_IPT; k++)
         if (p + k < len) sm[p + k] = res[k];
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < len; i += MG_THREADS) T.out[T.d0 + i] = sm[i];
+    for (uint32_t i = threadIdx.x; i < len; i += MG_THREADS) st_g(T.out + T.d0 + i, sm[i]);
 }
 
 // ---------------------------------------------------------------------------
@@ -133,6 +134,22 @@ __device__ __forceinline__ void bs_keep(Tup& x, const Tup& y, uint32_t e, uint32
 // (avxsort_core.h:1276-1399 sorts its cache-sized blocks with in-register
 // AVX networks the same way.)
 constexpr uint32_t BS_IPT = BS_BLOCK / BS_THREADS;
+static_assert(BS_IPT == 8, "k_blocksort's in-thread stages are j = 4, 2, 1");
+template <uint32_t J>
+__device__ __forceinline__ void bs_inthread(Tup (&v)[BS_IPT], uint32_t t, uint32_t k) {
+#pragma unroll
+    for (uint32_t i = 0; i < BS_IPT; i++) {
+        const uint32_t i2 = i ^ J;
+        if (i2 > i) {
+            const bool up = ((t * BS_IPT + i) & k) == 0;
+            if (tup_less(v[i2], v[i]) == up) {
+                const Tup x = v[i];
+                v[i] = v[i2];
+                v[i2] = x;
+            }
+        }
+    }
+}
 __global__ void __launch_bounds__(BS_THREADS)
 k_blocksort(Tup* __restrict__ data, const SortBlock* __restrict__ blocks) {
     __shared__ __attribute__((aligned(16))) Tup sm[BS_BLOCK];
@@ -141,8 +158,11 @@ k_blocksort(Tup* __restrict__ data, const SortBlock* __restrict__ blocks) {
     const uint32_t t = threadIdx.x;
     // coalesced load (sentinels past the end), then BS_IPT consecutive
     // elements per thread
-    for (uint32_t i = t; i < BS_BLOCK; i += BS_THREADS)
-        sm[i] = i < blk.len ? data[blk.off + i] : sent;
+    for (uint32_t i = t; i < BS_BLOCK; i += BS_THREADS) {
+        Tup x = sent;  // a value, not a select between references (scratch)
+        if (i < blk.len) x = ld_g(data + blk.off + i);
+        sm[i] = x;
+    }
     __syncthreads();
     Tup v[BS_IPT];
 #pragma unroll
@@ -165,19 +185,11 @@ k_blocksort(Tup* __restrict__ data, const SortBlock* __restrict__ blocks) {
                     const uint32_t e = t * BS_IPT + i;
                     bs_keep(v[i], shfl_xor_tup(v[i], (int)(j / BS_IPT)), e, j, k);
                 }
-            } else {  // partner in this thread
-#pragma unroll
-                for (uint32_t i = 0; i < BS_IPT; i++) {
-                    const uint32_t i2 = i ^ j;
-                    if (i2 > i) {
-                        const bool up = ((t * BS_IPT + i) & k) == 0;
-                        if (tup_less(v[i2], v[i]) == up) {
-                            const Tup x = v[i];
-                            v[i] = v[i2];
-                            v[i2] = x;
-                        }
-                    }
-                }
+            } else {  // partner in this thread: a compile-time j, so that v
+                      // stays in registers (a runtime index sends it to scratch)
+                if (j == 4) bs_inthread<4>(v, t, k);
+                else if (j == 2) bs_inthread<2>(v, t, k);
+                else bs_inthread<1>(v, t, k);
             }
         }
     }
@@ -236,25 +248,25 @@ k_mjcount_batch(const JoinPair* __restrict__ pairs, unsigned long long* __restri
     const JoinPair P = pairs[blockIdx.x];
     unsigned long long c = 0;
     for (uint64_t i = threadIdx.x; i < P.ns; i += 256) {
-        const int64_t k = tup_key(P.s[i]);
-        if (i > 0 && tup_key(P.s[i - 1]) == k) continue;
+        const int64_t k = tup_key(ld_g(P.s + i));
+        if (i > 0 && tup_key(ld_g(P.s + i - 1)) == k) continue;
         uint64_t lo = i + 1, hi = P.ns;
         while (lo < hi) {
             const uint64_t m = (lo + hi) >> 1;
-            if (tup_key(P.s[m]) <= k) lo = m + 1; else hi = m;
+            if (tup_key(ld_g(P.s + m)) <= k) lo = m + 1; else hi = m;
         }
         const uint64_t sc = lo - i;
         lo = 0;
         hi = P.nr;
         while (lo < hi) {
             const uint64_t m = (lo + hi) >> 1;
-            if (tup_key(P.r[m]) < k) lo = m + 1; else hi = m;
+            if (tup_key(ld_g(P.r + m)) < k) lo = m + 1; else hi = m;
         }
         const uint64_t rl = lo;
         hi = P.nr;
         while (lo < hi) {
             const uint64_t m = (lo + hi) >> 1;
-            if (tup_key(P.r[m]) <= k) lo = m + 1; else hi = m;
+            if (tup_key(ld_g(P.r + m)) <= k) lo = m + 1; else hi = m;
         }
         c += (unsigned long long)(lo - rl) * sc;
     }
@@ -410,13 +422,13 @@ void segmented_sort(Workspace* ws, Tup* data, const uint64_t* seg_off,
 // here the key range of the runs is cut into 2^D value buckets and, because
 // every run is sorted, the part of run i in bucket b is ONE contiguous slice
 // whose ends are two binary searches away.  So:
-//   k_km_range  : key range from the runs' first and last elements;
-//   k_km_bounds : off[i][b] = first element of run i in bucket >= b (k x (B+1)
+//   k_km_bounds : the key range from the runs' first and last elements, and
+//                 off[i][b] = first element of run i in bucket >= b (k x (B+1)
 //                 binary searches, no data pass; a streaming pass that wrote
 //                 the boundaries where consecutive buckets differ measured
 //                 slower: 0.76 against 0.57 ms for 64 runs of 2M);
-//   k_km_sizes  : bucket sizes (a wave per bucket) and their exclusive scan;
-//   k_km_merge  : one workgroup per bucket gathers its k slices with
+//   k_km_merge  : one workgroup per bucket sums its slice starts (= its place
+//                 in the output: no size / scan kernels), gathers its k slices with
 //                 coalesced loads (all in flight), counting-sorts them in LDS
 //                 by the top 12 bits of the key's offset in the bucket (the
 //                 exact key when the bucket spans <= 4096 keys), fixes the
@@ -439,14 +451,18 @@ struct KmRun {
     uint64_t n;
 };
 
-__global__ void __launch_bounds__(256)
-k_km_range(const KmRun* __restrict__ runs, uint32_t k, unsigned long long* __restrict__ mm) {
-    uint64_t lo = ~0ull, hi = 0;
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < k; i += gridDim.x * 256) {
+// the runs' key range (their first and last elements), computed by every
+// workgroup for itself (k <= 256 cached loads) instead of by a kernel of its own
+__device__ __forceinline__ void km_range(const KmRun* __restrict__ runs, uint32_t k,
+                                         uint64_t& lo, uint64_t& hi) {
+    __shared__ unsigned long long rl[KM_THREADS / 64], rh[KM_THREADS / 64];
+    lo = ~0ull;
+    hi = 0;
+    for (uint32_t i = threadIdx.x; i < k; i += KM_THREADS) {
         const KmRun r = runs[i];
         if (r.n == 0) continue;
-        lo = min(lo, key_u(tup_key(r.p[0])));
-        hi = max(hi, key_u(tup_key(r.p[r.n - 1])));
+        lo = min(lo, key_u(tup_key(ld_g(r.p))));
+        hi = max(hi, key_u(tup_key(ld_g(r.p + r.n - 1))));
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -455,26 +471,39 @@ k_km_range(const KmRun* __restrict__ runs, uint32_t k, unsigned long long* __res
         hi = c > hi ? c : hi;
     }
     if (lane_id() == 0) {
-        atomicMin(&mm[0], (unsigned long long)lo);
-        atomicMax(&mm[1], (unsigned long long)hi);
+        rl[threadIdx.x >> 6] = lo;
+        rh[threadIdx.x >> 6] = hi;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < KM_THREADS / 64; w++) {
+        lo = rl[w] < lo ? rl[w] : lo;
+        hi = rh[w] > hi ? rh[w] : hi;
     }
 }
 
-// bucket shift: 2^D buckets over the key range [mm[0], mm[1]]
-__device__ __forceinline__ uint32_t km_shift(const unsigned long long* mm, uint32_t D) {
-    const uint64_t w = mm[1] >= mm[0] ? mm[1] - mm[0] : 0;
+// bucket shift: 2^D buckets over the key range [lo, hi]
+__device__ __forceinline__ uint32_t km_shift(uint64_t lo, uint64_t hi, uint32_t D) {
+    const uint64_t w = hi >= lo ? hi - lo : 0;
     const uint32_t L = w ? 64 - __clzll((long long)w) : 0;
     return L > D ? L - D : 0;
 }
 
 // off[i][b] = first element of run i in bucket >= b (binary search); thread
 // i * (B + 1) + b, so the lanes of a wave search neighbouring ranges of one
-// run and store adjacent entries (run-major table)
-__global__ void __launch_bounds__(256)
+// run and store adjacent entries (run-major table).  Workgroup 0 publishes
+// the key range for k_km_merge.
+__global__ void __launch_bounds__(KM_THREADS)
 k_km_bounds(const KmRun* __restrict__ runs, uint32_t k, uint32_t D,
-            const unsigned long long* __restrict__ mm, uint32_t* __restrict__ off) {
+            unsigned long long* __restrict__ mm, uint32_t* __restrict__ off) {
+    uint64_t minu, maxu;
+    km_range(runs, k, minu, maxu);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        mm[0] = minu;
+        mm[1] = maxu;
+    }
     const uint32_t B = 1u << D;
-    const uint64_t idx = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t idx = (uint64_t)blockIdx.x * KM_THREADS + threadIdx.x;
     if (idx >= (uint64_t)(B + 1) * k) return;
     const uint32_t i = (uint32_t)(idx / (B + 1)), b = (uint32_t)(idx % (B + 1));
     const KmRun r = runs[i];
@@ -484,69 +513,22 @@ k_km_bounds(const KmRun* __restrict__ runs, uint32_t k, uint32_t D,
     } else if (b == B) {
         pos = r.n;
     } else {
-        const uint64_t minu = mm[0];
-        const uint32_t s = km_shift(mm, D);
+        const uint32_t s = km_shift(minu, maxu, D);
         uint64_t lo = 0, hi = r.n;
         while (lo < hi) {  // first element whose bucket is >= b
             const uint64_t m = (lo + hi) >> 1;
-            if (((key_u(tup_key(r.p[m])) - minu) >> s) < b) lo = m + 1; else hi = m;
+            if (((key_u(tup_key(ld_g(r.p + m))) - minu) >> s) < b) lo = m + 1; else hi = m;
         }
         pos = lo;
     }
     off[idx] = (uint32_t)pos;
 }
 
-// sizes of buckets [blockIdx.x * 4, +4) (a wave each), overflow flag
-__global__ void __launch_bounds__(256)
-k_km_sizes(const uint32_t* __restrict__ off, uint32_t k, uint32_t B,
-           uint64_t* __restrict__ size, unsigned int* __restrict__ flag) {
-    const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (b >= B) return;
-    uint64_t s = 0;
-    for (uint32_t i = lane_id(); i < k; i += 64)
-        s += off[(uint64_t)i * (B + 1) + b + 1] - off[(uint64_t)i * (B + 1) + b];
-    s = wave_sum(s);
-    if (lane_id() == 0) {
-        size[b] = s;
-        if (s > KM_CAP) atomicOr(flag, 1u);
-    }
-}
-
-// one workgroup: exclusive scan of the B bucket sizes in place
-__global__ void __launch_bounds__(1024)
-k_km_scan(uint64_t* __restrict__ size, uint32_t B) {
-    __shared__ unsigned long long wt[17];
-    const uint32_t per = (B + 1023) / 1024;
-    const uint32_t b0 = threadIdx.x * per;
-    unsigned long long loc = 0;
-    for (uint32_t q = 0; q < per; q++)
-        if (b0 + q < B) loc += size[b0 + q];
-    unsigned long long x = loc;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const unsigned long long y = __shfl_up(x, o, 64);
-        if (lane_id() >= o) x += y;
-    }
-    const int wid = threadIdx.x >> 6;
-    if (lane_id() == 63) wt[wid] = x;
-    __syncthreads();
-    unsigned long long ex = x - loc;
-    for (int w = 0; w < wid; w++) ex += wt[w];
-    for (uint32_t q = 0; q < per; q++) {
-        if (b0 + q < B) {
-            const unsigned long long c = size[b0 + q];
-            size[b0 + q] = ex;
-            ex += c;
-        }
-    }
-}
-
 __global__ void __launch_bounds__(KM_THREADS)
 k_km_merge(const KmRun* __restrict__ runs, uint32_t k, uint32_t D,
            const unsigned long long* __restrict__ mm, const uint32_t* __restrict__ off,
-           const uint64_t* __restrict__ ostart, unsigned int* __restrict__ flag,
-           Tup* __restrict__ out) {
-    __shared__ __attribute__((aligned(16))) Tup buf[KM_CAP + 1];  // + a dump slot
+           unsigned int* __restrict__ flag, Tup* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) Tup buf[KM_CAP];
     __shared__ uint32_t cnt[KM_NB / 2];     // digit histogram, two u16 per word
     __shared__ uint32_t cur[KM_NB / 2];     // placement cursors
     // the non-empty slices in run (= position) order: slice q's element for
@@ -556,38 +538,49 @@ k_km_merge(const KmRun* __restrict__ runs, uint32_t k, uint32_t D,
     __shared__ unsigned long long smap[KM_CAP / 64];
     __shared__ uint32_t wk[KM_CAP / 64];
     __shared__ uint32_t wt[KM_THREADS / 64];
-    if (flag[0]) return;  // some bucket overflows: the caller merges another way
+    __shared__ unsigned long long wo[KM_THREADS / 64];
     const uint32_t b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     for (uint32_t i = tid; i < KM_NB / 2; i += KM_THREADS) cnt[i] = 0;
     for (uint32_t i = tid; i < KM_CAP / 64; i += KM_THREADS) smap[i] = 0ull;
     // ---- slices: run tid's part of bucket b; one scan gives its position in
-    // the bucket (low half) and its index among the non-empty slices (high)
+    // the bucket (low 21 bits; lengths clamped to KM_CAP + 1, so a sum over
+    // 256 runs fits) and its index among the non-empty slices (high bits).
+    // The bucket's place in the output is the sum of the slice starts: every
+    // element before it lies in a lower bucket of some run.
     uint32_t lo = 0, len = 0;
     if (tid < k) {
         const uint32_t* orow = off + (uint64_t)tid * ((1u << D) + 1);
         lo = orow[b];
         len = orow[b + 1] - lo;
     }
-    const uint32_t pk = len | ((len ? 1u : 0u) << 16);  // total <= KM_CAP < 2^16
+    const uint32_t pk = min(len, KM_CAP + 1) | ((len ? 1u : 0u) << 21);
     uint32_t x = pk;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t y = __shfl_up(x, o, 64);
         if (lane >= o) x += y;
     }
+    const uint64_t lsum = wave_sum((uint64_t)lo);
     if (lane == 63) wt[wid] = x;
+    if (lane == 0) wo[wid] = lsum;
     __syncthreads();
     uint32_t ex = x - pk, tot2 = 0;
+    uint64_t o = 0;
 #pragma unroll
     for (int w = 0; w < KM_THREADS / 64; w++) {
         if (w < (int)wid) ex += wt[w];
         tot2 += wt[w];
+        o += wo[w];
     }
-    const uint32_t total = tot2 & 0xffffu;
+    const uint32_t total = tot2 & 0x1fffffu;
     if (total == 0) return;  // uniform: an empty bucket
+    if (total > KM_CAP) {    // a bucket larger than LDS: the caller merges another way
+        if (tid == 0) atomicOr(&flag[0], 1u);
+        return;
+    }
     if (len) {
-        const uint32_t p0 = ex & 0xffffu;
-        sptr[ex >> 16] = runs[tid].p + ((int64_t)lo - (int64_t)p0);
+        const uint32_t p0 = ex & 0x1fffffu;
+        sptr[ex >> 21] = runs[tid].p + ((int64_t)lo - (int64_t)p0);
         atomicOr(&smap[p0 >> 6], 1ull << (p0 & 63));
     }
     __syncthreads();
@@ -606,20 +599,29 @@ k_km_merge(const KmRun* __restrict__ runs, uint32_t k, uint32_t D,
     // fixed-step search over the slice starts) and the level digit: the
     // bucket's key offset, its top KM_LOGNB bits (exact keys for buckets no
     // wider than KM_NB keys)
-    const uint32_t s = km_shift(mm, D);
+    const uint32_t s = km_shift(mm[0], mm[1], D);
     const uint64_t base = mm[0] + ((uint64_t)b << s);
     const uint32_t s3 = s > KM_LOGNB ? s - KM_LOGNB : 0;
     Tup v[KM_IPT];
     uint32_t dg[KM_IPT];
-#pragma unroll
-    for (int q = 0; q < (int)KM_IPT; q++) {
+    auto gather = [&](int q) {
         const uint32_t j = min(q * KM_THREADS + tid, total - 1);
         const uint32_t w = j >> 6;
         const uint32_t sl = wk[w] + (uint32_t)__popcll(smap[w] & (~0ull >> (63 - (j & 63)))) - 1u;
-        v[q] = sptr[sl][j];
+        v[q] = ld_g(sptr[sl] + j);
+    };
+    // buckets average KM_CAP / 2: the upper half of the loads (and of the
+    // counting and placing below) only when the bucket reaches it; rows past
+    // the end would otherwise be same-address LDS atomics, serialised
+#pragma unroll
+    for (int q = 0; q < (int)KM_IPT / 2; q++) gather(q);
+    if (total > KM_CAP / 2) {
+#pragma unroll
+        for (int q = KM_IPT / 2; q < (int)KM_IPT; q++) gather(q);
     }
 #pragma unroll
     for (int q = 0; q < (int)KM_IPT; q++) {
+        if (q * KM_THREADS >= total) break;  // uniform
         const bool valid = q * KM_THREADS + tid < total;
         dg[q] = (uint32_t)min((key_u(tup_key(v[q])) - base) >> s3, (uint64_t)KM_NB - 1);
         if (valid) atomicAdd(&cnt[dg[q] >> 1], 1u << ((dg[q] & 1) * 16));
@@ -658,13 +660,15 @@ k_km_merge(const KmRun* __restrict__ runs, uint32_t k, uint32_t D,
         ex += c[2 * q + 1];
     }
     __syncthreads();
-    // ---- place (lanes past the end drop their element in the dump slot)
+    // ---- place
 #pragma unroll
     for (int q = 0; q < (int)KM_IPT; q++) {
-        const bool valid = q * KM_THREADS + tid < total;
-        const uint32_t sh = (dg[q] & 1) * 16;
-        const uint32_t old = atomicAdd(&cur[dg[q] >> 1], valid ? 1u << sh : 0u);
-        buf[valid ? (old >> sh) & 0xffffu : KM_CAP] = v[q];
+        if (q * KM_THREADS >= total) break;  // uniform
+        if (q * KM_THREADS + tid < total) {
+            const uint32_t sh = (dg[q] & 1) * 16;
+            const uint32_t old = atomicAdd(&cur[dg[q] >> 1], 1u << sh);
+            buf[(old >> sh) & 0xffffu] = v[q];
+        }
     }
     __syncthreads();
     if (dup) {
@@ -702,7 +706,6 @@ k_km_merge(const KmRun* __restrict__ runs, uint32_t k, uint32_t D,
         }
     }
     // ---- the bucket, in order, to its place in the output
-    const uint64_t o = ostart[b];
     for (uint32_t j = tid; j < total; j += KM_THREADS) out[o + j] = buf[j];
 }
 
@@ -717,38 +720,34 @@ static bool multiway_merge_buckets(Workspace* ws, const Tup* const* runs, const 
     uint32_t D = 0;
     while (D < 24 && (total >> D) > KM_CAP / 2) D++;
     const uint32_t B = 1u << D;
-    std::vector<KmRun> h(k);
-    for (uint32_t i = 0; i < k; i++) h[i] = KmRun{runs[i], lens[i]};
-    KmRun* dr = (KmRun*)ws->scratch("km_runs", k * sizeof(KmRun));
-    unsigned long long* mm = (unsigned long long*)ws->scratch("km_mm", 32);
+    // one pinned block, one copy: the key-range / flag words, then the runs
+    const size_t hdr = 32, bytes = hdr + (size_t)k * sizeof(KmRun);
+    unsigned long long* mm = (unsigned long long*)ws->scratch("km_hdr", bytes);
     unsigned int* flag = (unsigned int*)(mm + 2);
+    const KmRun* dr = (const KmRun*)((char*)mm + hdr);
     uint32_t* off = (uint32_t*)ws->scratch("km_off", (size_t)(B + 1) * k * 4);
-    uint64_t* size = (uint64_t*)ws->scratch("km_size", (size_t)B * 8);
-    unsigned long long* hinit = (unsigned long long*)ws->host_pinned("km_init", 32);
-    unsigned int* hflag = (unsigned int*)ws->host_pinned("km_flag", 16);
-    // the pinned buffers are free: every call ends with a synchronisation
-    hinit[0] = ~0ull;
-    hinit[1] = 0;
-    hinit[2] = 0;
-    hinit[3] = 0;
-    // pageable table: copied out before hipMemcpyAsync returns
-    SMJ_CHECK(hipMemcpyAsync(dr, h.data(), k * sizeof(KmRun), hipMemcpyHostToDevice, st));
-    SMJ_CHECK(hipMemcpyAsync(mm, hinit, 32, hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(k_km_range, dim3((k + 255) / 256), dim3(256), 0, st, dr, k, mm);
+    // the pinned block is free again after the synchronisation below
+    unsigned long long* h = (unsigned long long*)ws->host_pinned("km_hdr_h", bytes);
+    h[0] = ~0ull;
+    h[1] = 0;
+    h[2] = 0;  // flag[0]: a bucket overflows; flag[1]: a long unsorted equal-digit run
+    h[3] = 0;
+    KmRun* hr = (KmRun*)((char*)h + hdr);
+    for (uint32_t i = 0; i < k; i++) hr[i] = KmRun{runs[i], lens[i]};
+    SMJ_CHECK(hipMemcpyAsync(mm, h, bytes, hipMemcpyHostToDevice, st));
     const uint64_t nb = (uint64_t)(B + 1) * k;
     {
         TraceScope ts(ws, "k_km_bounds", st);
-        hipLaunchKernelGGL(k_km_bounds, dim3((uint32_t)((nb + 255) / 256)), dim3(256), 0, st, dr,
-                           k, D, mm, off);
+        hipLaunchKernelGGL(k_km_bounds, dim3((uint32_t)((nb + KM_THREADS - 1) / KM_THREADS)),
+                           dim3(KM_THREADS), 0, st, dr, k, D, mm, off);
     }
-    hipLaunchKernelGGL(k_km_sizes, dim3((B + 3) / 4), dim3(256), 0, st, off, k, B, size, flag);
-    hipLaunchKernelGGL(k_km_scan, dim3(1), dim3(1024), 0, st, size, B);
     {
         TraceScope ts(ws, "k_km_merge", st);
-        hipLaunchKernelGGL(k_km_merge, dim3(B), dim3(KM_THREADS), 0, st, dr, k, D, mm, off, size,
+        hipLaunchKernelGGL(k_km_merge, dim3(B), dim3(KM_THREADS), 0, st, dr, k, D, mm, off,
                            flag, out);
     }
     SMJ_CHECK(hipGetLastError());
+    unsigned int* hflag = (unsigned int*)ws->host_pinned("km_flag", 16);
     SMJ_CHECK(hipMemcpyAsync(hflag, flag, 8, hipMemcpyDeviceToHost, st));
     SMJ_CHECK(hipStreamSynchronize(st));
     return hflag[0] == 0 && hflag[1] == 0;

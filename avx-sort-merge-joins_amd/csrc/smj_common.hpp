@@ -104,6 +104,34 @@ __device__ __forceinline__ Tup ld_nt(const Tup* p) {
 #endif
 }
 
+// Load through a pointer the compiler cannot prove global (read from LDS or
+// from a table in device memory): left alone it becomes a flat load, which
+// also counts against lgkmcnt, so every later LDS wait waits for it too and
+// gathers lose their overlap.  The cast keeps it a global_load.
+typedef const __attribute__((address_space(1))) uint64_t* GlobalU64Ptr;
+__device__ __forceinline__ Tup ld_g(const Tup* p) {
+#ifdef KEY_8B
+    typedef const __attribute__((address_space(1))) TupVec* GV;
+    const TupVec x = *(GV)p;
+    Tup t;
+    t.payload = x.x;
+    t.key = x.y;
+    return t;
+#else
+    return *(GlobalU64Ptr)p;
+#endif
+}
+
+__device__ __forceinline__ void st_g(Tup* p, const Tup& v) {
+#ifdef KEY_8B
+    typedef __attribute__((address_space(1))) TupVec* GV;
+    TupVec x = {v.payload, v.key};
+    *(GV)p = x;
+#else
+    *(__attribute__((address_space(1))) uint64_t*)p = v;
+#endif
+}
+
 __host__ __device__ __forceinline__ int64_t tup_key(const Tup& t) {
 #ifdef KEY_8B
     return t.key;
@@ -118,6 +146,19 @@ __host__ __device__ __forceinline__ bool tup_less(const Tup& a, const Tup& b) {
     return (a.key < b.key) || (a.key == b.key && a.payload < b.payload);
 #else
     return (int64_t)a < (int64_t)b;
+#endif
+}
+
+// c ? a : b field by field: a ternary on the 16-byte struct can become a
+// select between the addresses of two stack copies (scratch memory)
+__host__ __device__ __forceinline__ Tup tup_sel(bool c, const Tup& a, const Tup& b) {
+#ifdef KEY_8B
+    Tup r;
+    r.payload = c ? a.payload : b.payload;
+    r.key = c ? a.key : b.key;
+    return r;
+#else
+    return c ? a : b;
 #endif
 }
 

@@ -380,14 +380,22 @@ class Library:
         self.lib.smj_dev_merge_join_count(r.data_ptr(), r.shape[0], s.data_ptr(),
                                           s.shape[0], count.data_ptr(), self.stream_ptr())
 
-    def dev_multiway_merge(self, runs, out):
-        """k-way merge of sorted device runs (list of (n_i, 2) tensors) into
-        `out` (smj_dev_multiway_merge_host; synchronises the stream)."""
+    @staticmethod
+    def run_table(runs):
+        """(pointer array, length array, k) of a list of device runs, built
+        once for callers that merge the same runs repeatedly."""
         k = len(runs)
         ptrs = (C.c_void_p * k)(*[r.data_ptr() for r in runs])
         lens = (C.c_uint64 * k)(*[r.shape[0] for r in runs])
-        self.lib.smj_dev_multiway_merge_host(self.ws, C.cast(ptrs, _P), C.cast(lens, _P), k,
-                                             out.data_ptr(), self.stream_ptr())
+        return C.cast(ptrs, _P), C.cast(lens, _P), k, (ptrs, lens)
+
+    def dev_multiway_merge(self, runs, out):
+        """k-way merge of sorted device runs (list of (n_i, 2) tensors, or a
+        run_table of them) into `out` (smj_dev_multiway_merge_host;
+        synchronises the stream)."""
+        ptrs, lens, k, _keep = runs if isinstance(runs, tuple) else self.run_table(runs)
+        self.lib.smj_dev_multiway_merge_host(self.ws, ptrs, lens, k, out.data_ptr(),
+                                             self.stream_ptr())
 
     def dev_materialize(self, sortedR, sortedS, out=None):
         """Materialised merge join (smj_dev_materialize): writes the first

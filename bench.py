@@ -486,9 +486,10 @@ def run_op(a, lib, json_out, dist, N, rank):
             runs.append(t)
         del keys
         out = lib.empty(n)
+        table = lib.run_table(runs)  # the reference's driver builds its run array once too
 
         def step():
-            lib.dev_multiway_merge(runs, out)
+            lib.dev_multiway_merge(table, out)
     elif a.op == "sort":
         out = lib.empty(n)
 
