@@ -909,8 +909,9 @@ __device__ __forceinline__ void skew_for_each(const GroupArgs& G, const SkewSmal
             W v[SK_ITEMS];
 #pragma unroll
             for (int k = 0; k < SK_ITEMS; k++) {
-                const uint32_t j = c + k * SK_THREADS + threadIdx.x;
-                if (j < n) v[k] = *skew_elem(L, r, static_cast<const W*>(G.tmp[r]), nt, j);
+                // unconditional (clamped) loads: a conditional one waits alone
+                const uint32_t j = min(c + k * SK_THREADS + threadIdx.x, n - 1);
+                v[k] = *skew_elem(L, r, static_cast<const W*>(G.tmp[r]), nt, j);
             }
 #pragma unroll
             for (int k = 0; k < SK_ITEMS; k++) f(v[k], c + k * SK_THREADS + threadIdx.x < n);
@@ -934,11 +935,9 @@ __device__ __forceinline__ bool skew_inversion(const Tup* dst, uint32_t lo, uint
         Tup a[SK_ITEMS], b[SK_ITEMS];
 #pragma unroll
         for (int k = 0; k < SK_ITEMS; k++) {
-            const uint32_t i = c + k * SK_THREADS + threadIdx.x;
-            if (i < hi) {
-                a[k] = dst[i - 1];
-                b[k] = dst[i];
-            }
+            const uint32_t i = min(c + k * SK_THREADS + threadIdx.x, hi - 1);
+            a[k] = dst[i - 1];
+            b[k] = dst[i];
         }
 #pragma unroll
         for (int k = 0; k < SK_ITEMS; k++)
@@ -1066,7 +1065,7 @@ k_skew_hist(SkewArgs K) {
     const RangePlan& P = G.plan;
     const uint4 it = K.items[blockIdx.x];
     const uint32_t qi = it.x, sl = it.y, r = it.z >> 16, s = it.z & 0xffffu, ts = it.w;
-    const OvfEntry& e = K.q[qi];
+    const OvfEntry e = K.q[qi];  // a copy: a reference is re-read after every store
     const uint32_t t0 = G.tt[r].btile0[e.bucket];
     const uint32_t nt = G.tt[r].btile0[e.bucket + 1] - t0;
     if (s >= nt) return;
@@ -1082,7 +1081,7 @@ k_skew_hist(SkewArgs K) {
 #pragma unroll
             for (int k = 0; k < SK_ITEMS; k++) {
                 const uint32_t i = c + k * SK_THREADS + threadIdx.x;
-                if (i < len) v[k] = src[i];
+                v[k] = src[i < len ? i : len - 1];  // unconditional: all in flight
             }
 #pragma unroll
             for (int k = 0; k < SK_ITEMS; k++) {
@@ -1146,7 +1145,7 @@ k_skew_place(SkewArgs K) {
     const RangePlan& P = G.plan;
     const uint4 it = K.items[blockIdx.x];
     const uint32_t qi = it.x, sl = it.y, r = it.z >> 16, s = it.z & 0xffffu, ts = it.w;
-    const OvfEntry& e = K.q[qi];
+    const OvfEntry e = K.q[qi];  // a copy: a reference is re-read after every store
     const uint32_t t0 = G.tt[r].btile0[e.bucket];
     const uint32_t nt = G.tt[r].btile0[e.bucket + 1] - t0;
     if (s >= nt) return;
@@ -1182,7 +1181,7 @@ k_skew_place(SkewArgs K) {
 #pragma unroll
             for (int k = 0; k < SK_ITEMS; k++) {
                 const uint32_t i = c + k * SK_THREADS + threadIdx.x;
-                if (i < len) v[k] = src[i];
+                v[k] = src[i < len ? i : len - 1];  // unconditional: all in flight
             }
             __syncthreads();
 #pragma unroll
@@ -1214,7 +1213,7 @@ k_skew_check(SkewArgs K) {
     const uint32_t qi = it.x, r = it.z >> 16, s = it.z & 0xffffu, ts = it.w;
     const RangePlan& P = K.G.plan;
     if (!(P.s3 == 0 && !(K.gflag[qi] & 1u))) return;
-    const OvfEntry& e = K.q[qi];
+    const OvfEntry e = K.q[qi];  // a copy: a reference is re-read after every store
     const Tup* dst = K.G.out[r] + K.G.ostart[r][e.bucket] + e.off[r];
     const uint32_t n = e.nr[r];
     const uint32_t lo = max(1u, (uint32_t)((uint64_t)n * s / ts));

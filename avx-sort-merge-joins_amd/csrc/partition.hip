@@ -45,10 +45,11 @@ k_hist(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_arg,
     if (end > n) end = n;
     for (uint64_t base = beg; base < end; base += TILE) {
         Tup v[ITEMS];
+        // unconditional (clamped) loads: all in flight at once
 #pragma unroll
         for (int j = 0; j < ITEMS; j++) {
-            uint64_t i = base + (uint64_t)j * THREADS + threadIdx.x;
-            if (i < end) v[j] = in[i];
+            const uint64_t i = base + (uint64_t)j * THREADS + threadIdx.x;
+            v[j] = in[i < end ? i : end - 1];
         }
 #pragma unroll
         for (int j = 0; j < ITEMS; j++) {
