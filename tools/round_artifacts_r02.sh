@@ -1,5 +1,6 @@
 #!/usr/bin/env bash
-# Round-2 artifacts on one MI355X (no pytest: run separately): the bench
+# Round-2 artifacts on one MI355X (no pytest: run separately), PHASE=runs
+# (bench lines) or PHASE=prof (rocprofv3 traces and PMC passes): the bench
 # lines (join 16/8 B, Zipf, and the sort / partition / merge ops with their
 # CPU baselines), rocprofv3 --kernel-trace --stats of the same commands, and
 # the PMC traffic passes (FETCH_SIZE and WRITE_SIZE in separate runs).  Every
@@ -27,8 +28,9 @@ pmc() {  # cfgkey name args...
   python3 tools/make_traffic.py "$key" "$OUT/fetch_$name" "$OUT/write_$name" "$OUT/pmc_traffic.json" > /dev/null || exit 1
   echo "pmc $name"
 }
+if [ "${PHASE:-runs}" = runs ]; then
 run bench16 $B
-run bench8 $B --width 8 --no-cpu-baseline
+run bench8 $B --width 8
 run bench16_zipf $B --dist zipf --no-cpu-baseline
 run part8 --op partition --width 8
 run part16 --op partition --width 16 --no-cpu-baseline
@@ -36,6 +38,11 @@ run sort8 --op sort --width 8
 run sort16 --op sort --width 16 --no-cpu-baseline
 run merge8 --op merge --width 8
 run merge8_64x2M --op merge --width 8 --n 2097152 --no-cpu-baseline
+run bench16_exchange_path $B --exchange-path --no-cpu-baseline
+run exchange_n1 --op exchange --no-cpu-baseline
+run n1024_uniform --n-total 1024000000 --no-cpu-baseline
+run n1024_zipf --n-total 1024000000 --dist zipf --no-cpu-baseline
+else
 prof bench16 $B
 prof part8 --op partition --width 8
 prof sort8 --op sort --width 8
@@ -44,3 +51,4 @@ pmc n128000000_w16_uniform bench16 $B
 pmc n128000000_w8_uniform bench8 $B --width 8
 pmc partition_n134217728_w8 part8 --op partition --width 8
 pmc sort_n134217728_w8 sort8 --op sort --width 8
+fi
