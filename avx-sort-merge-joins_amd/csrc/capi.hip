@@ -1346,20 +1346,32 @@ k_seg_tables(const int64_t* __restrict__ cnt, uint32_t nseg, uint32_t nb,
     }
 }
 
-void smj_dev_join_segmented(smj_workspace* wsp, void* R, uint64_t nR,
-                            const int64_t* segR, void* S, uint64_t nS,
-                            const int64_t* segS, uint32_t nseg, uint32_t bucket_bits,
-                            int64_t key_lo, int64_t key_hi, uint32_t flags,
-                            tuple_t* sortedR, tuple_t* sortedS,
-                            unsigned long long* count_dev, smj_stream_t stream) {
-    Workspace* ws = (Workspace*)wsp;
-    hipStream_t st = (hipStream_t)stream;
-    if (nseg == 0 || bucket_bits > 10 || nR >= (1ull << 32) || nS >= (1ull << 32)) {
-        fprintf(stderr, "[ERROR] smj_dev_join_segmented: nseg %u, bucket_bits %u "
-                "(<= 10), nR %llu, nS %llu (< 2^32)\n", nseg, bucket_bits,
-                (unsigned long long)nR, (unsigned long long)nS);
-        abort();
+// Bucket totals of explicit segment tables (bucket-major, nseg per bucket);
+// bucket starts are 0 (segment offsets are absolute).  blockIdx.x = relation.
+__global__ void __launch_bounds__(256)
+k_seg_totals(const int64_t* __restrict__ cnt0, const int64_t* __restrict__ cnt1,
+             uint32_t nseg, uint32_t nb, int64_t* __restrict__ bcount0,
+             int64_t* __restrict__ bcount1, uint64_t* __restrict__ bstart0,
+             uint64_t* __restrict__ bstart1) {
+    const int64_t* cnt = blockIdx.x ? cnt1 : cnt0;
+    int64_t* bcount = blockIdx.x ? bcount1 : bcount0;
+    uint64_t* bstart = blockIdx.x ? bstart1 : bstart0;
+    for (uint32_t b = threadIdx.x; b < nb; b += 256) {
+        int64_t t = 0;
+        for (uint32_t j = 0; j < nseg; j++) t += cnt[(size_t)b * nseg + j];
+        bcount[b] = t;
+        bstart[b] = 0;
     }
+}
+
+// The local join of the exchanged relations from their segment tables
+// (seg_start / seg_cnt [b * nseg + j], element offsets into R / S): the
+// buckets are the exchanged partitions, so the join starts at its tile pass.
+static void join_segmented_core(Workspace* ws, void* R, uint64_t nR, void* S, uint64_t nS,
+                                uint64_t* const* ss, int64_t* const* sc, uint32_t nseg,
+                                uint32_t bucket_bits, int64_t key_lo, int64_t key_hi,
+                                uint32_t flags, tuple_t* sortedR, tuple_t* sortedS,
+                                unsigned long long* count_dev, hipStream_t st) {
     SMJ_CHECK(hipMemsetAsync(count_dev, 0, sizeof(unsigned long long), st));
     uint32_t D1, D2, D2cap;
     choose_levels(nR > nS ? nR : nS, bucket_bits, &D1, &D2, &D2cap);
@@ -1388,23 +1400,23 @@ void smj_dev_join_segmented(smj_workspace* wsp, void* R, uint64_t nR,
     hipLaunchKernelGGL(k_setplan, dim3(1), dim3(1), 0, st, plan, hplan);
     const uint32_t nb = 1u << D1;
     void* rel[2] = {R, S};
-    const int64_t* seg[2] = {segR, segS};
-    static const char* nm[2][4] = {{"xs_startR", "xs_cntR", "xs_bcR", "xs_bsR"},
-                                   {"xs_startS", "xs_cntS", "xs_bcS", "xs_bsS"}};
+    static const char* nm[2][2] = {{"xs_bcR", "xs_bsR"}, {"xs_bcS", "xs_bsS"}};
+    int64_t* bc[2];
+    uint64_t* bs[2];
+    for (int r = 0; r < 2; r++) {
+        bc[r] = (int64_t*)ws->scratch(nm[r][0], (size_t)nb * 8);
+        bs[r] = (uint64_t*)ws->scratch(nm[r][1], (size_t)nb * 8);
+    }
+    hipLaunchKernelGGL(k_seg_totals, dim3(2), dim3(256), 0, st, sc[0], sc[1], nseg, nb, bc[0],
+                       bc[1], bs[0], bs[1]);
     BucketSortArgs a;
     for (int r = 0; r < 2; r++) {
-        uint64_t* ss = (uint64_t*)ws->scratch(nm[r][0], (size_t)nb * nseg * 8);
-        int64_t* sc = (int64_t*)ws->scratch(nm[r][1], (size_t)nb * nseg * 8);
-        int64_t* bc = (int64_t*)ws->scratch(nm[r][2], (size_t)nb * 8);
-        uint64_t* bs = (uint64_t*)ws->scratch(nm[r][3], (size_t)nb * 8);
-        hipLaunchKernelGGL(k_seg_tables, dim3(1), dim3(256), 0, st, seg[r], nseg, nb,
-                           ss, sc, bc, bs);
         a.part[r] = rel[r];
         a.tmp[r] = rel[r];  // the tile pass works in place in the receive buffer
-        a.bstart[r] = bs;
-        a.bcount[r] = bc;
-        a.seg_start[r] = ss;
-        a.seg_cnt[r] = sc;
+        a.bstart[r] = bs[r];
+        a.bcount[r] = bc[r];
+        a.seg_start[r] = ss[r];
+        a.seg_cnt[r] = sc[r];
     }
     a.nseg = nseg;
     a.out[0] = (Tup*)sortedR;
@@ -1425,6 +1437,57 @@ void smj_dev_join_segmented(smj_workspace* wsp, void* R, uint64_t nR,
         fprintf(stderr, "[ERROR] smj_dev_join_segmented: unexpected partition flag\n");
         abort();
     }
+}
+
+static void check_segmented(const char* fn, uint32_t nseg, uint32_t bucket_bits, uint64_t nR,
+                            uint64_t nS) {
+    if (nseg == 0 || bucket_bits > 10 || nR >= (1ull << 32) || nS >= (1ull << 32)) {
+        fprintf(stderr, "[ERROR] %s: nseg %u, bucket_bits %u (<= 10), nR %llu, nS %llu "
+                "(< 2^32)\n", fn, nseg, bucket_bits, (unsigned long long)nR,
+                (unsigned long long)nS);
+        abort();
+    }
+}
+
+void smj_dev_join_segmented(smj_workspace* wsp, void* R, uint64_t nR,
+                            const int64_t* segR, void* S, uint64_t nS,
+                            const int64_t* segS, uint32_t nseg, uint32_t bucket_bits,
+                            int64_t key_lo, int64_t key_hi, uint32_t flags,
+                            tuple_t* sortedR, tuple_t* sortedS,
+                            unsigned long long* count_dev, smj_stream_t stream) {
+    Workspace* ws = (Workspace*)wsp;
+    hipStream_t st = (hipStream_t)stream;
+    check_segmented("smj_dev_join_segmented", nseg, bucket_bits, nR, nS);
+    const uint32_t nb = 1u << bucket_bits;
+    const int64_t* seg[2] = {segR, segS};
+    static const char* nm[2][4] = {{"xs_startR", "xs_cntR", "xs_bcR", "xs_bsR"},
+                                   {"xs_startS", "xs_cntS", "xs_bcS", "xs_bsS"}};
+    uint64_t* ss[2];
+    int64_t* sc[2];
+    for (int r = 0; r < 2; r++) {
+        ss[r] = (uint64_t*)ws->scratch(nm[r][0], (size_t)nb * nseg * 8);
+        sc[r] = (int64_t*)ws->scratch(nm[r][1], (size_t)nb * nseg * 8);
+        int64_t* bc = (int64_t*)ws->scratch(nm[r][2], (size_t)nb * 8);
+        uint64_t* bs = (uint64_t*)ws->scratch(nm[r][3], (size_t)nb * 8);
+        hipLaunchKernelGGL(k_seg_tables, dim3(1), dim3(256), 0, st, seg[r], nseg, nb,
+                           ss[r], sc[r], bc, bs);
+    }
+    join_segmented_core(ws, R, nR, S, nS, ss, sc, nseg, bucket_bits, key_lo, key_hi, flags,
+                        sortedR, sortedS, count_dev, st);
+}
+
+void smj_dev_join_segmented_tables(smj_workspace* wsp, void* R, uint64_t nR,
+                                   const int64_t* startR, const int64_t* cntR, void* S,
+                                   uint64_t nS, const int64_t* startS, const int64_t* cntS,
+                                   uint32_t nseg, uint32_t bucket_bits, int64_t key_lo,
+                                   int64_t key_hi, uint32_t flags, tuple_t* sortedR,
+                                   tuple_t* sortedS, unsigned long long* count_dev,
+                                   smj_stream_t stream) {
+    check_segmented("smj_dev_join_segmented_tables", nseg, bucket_bits, nR, nS);
+    uint64_t* ss[2] = {(uint64_t*)startR, (uint64_t*)startS};
+    int64_t* sc[2] = {(int64_t*)cntR, (int64_t*)cntS};
+    join_segmented_core((Workspace*)wsp, R, nR, S, nS, ss, sc, nseg, bucket_bits, key_lo,
+                        key_hi, flags, sortedR, sortedS, count_dev, (hipStream_t)stream);
 }
 
 void smj_join_phase_ms(smj_workspace* wsp, float* ms5) {
@@ -1502,6 +1565,44 @@ int smj_dev_partition_range_packed(smj_workspace* wsp, const tuple_t* in, uint64
     (void)hist_out; (void)bad_flag; (void)stream;
     return 0;
 #endif
+}
+
+uint64_t smj_sampled_capacity(uint64_t n, uint32_t nbits) { return sampled_capacity(n, nbits); }
+
+uint32_t smj_sampled_shards(void) { return kShards; }
+
+int smj_dev_partition_range_sampled(smj_workspace* wsp, const tuple_t* in, uint64_t n,
+                                    void* out, uint32_t nbits, int64_t key_min,
+                                    int64_t key_max, int packed, int64_t* seg_start_out,
+                                    int64_t* seg_cnt_out, unsigned int* flags,
+                                    smj_stream_t stream) {
+    Workspace* ws = (Workspace*)wsp;
+    hipStream_t st = (hipStream_t)stream;
+    if (nbits > 10 || n >= (1ull << 32)) return 0;  // LDS carries: up to 1024 partitions
+    RangePlan h = make_plan(key_min, key_max, nbits, 0, 0, 0);
+#ifdef KEY_8B
+    if (packed && !LayPacked::usable(h)) return 0;
+#else
+    if (packed) return 0;
+#endif
+    const uint32_t nbins = 1u << nbits;
+    RangePlan* plan = (RangePlan*)ws->scratch("xp_plan", sizeof(RangePlan));
+    hipLaunchKernelGGL(k_setplan, dim3(1), dim3(1), 0, st, plan, h);
+    unsigned int* sample = (unsigned int*)ws->scratch("xp_sample", (size_t)nbins * 4);
+    SMJ_CHECK(hipMemsetAsync(sample, 0, (size_t)nbins * 4, st));
+    SMJ_CHECK(hipMemsetAsync(flags, 0, 8, st));
+    uint64_t* starts = (uint64_t*)ws->scratch("xp_starts", (size_t)nbins * 8);
+    int64_t* hist = (int64_t*)ws->scratch("xp_hist", (size_t)nbins * 8);
+    const Tup* rels[1] = {(const Tup*)in};
+    const uint64_t ns[1] = {n};
+    void* outs[1] = {out};
+    uint64_t* st_[1] = {starts};
+    int64_t* h_[1] = {hist};
+    uint64_t* ss[1] = {(uint64_t*)seg_start_out};
+    int64_t* sc[1] = {seg_cnt_out};
+    sampled_partition(ws, 1, rels, ns, outs, plan, nbits, sample, st_, h_, ss, sc, flags, st,
+                      packed ? &h : nullptr, flags + 1);
+    return 1;
 }
 
 uint64_t smj_selfcheck_lds_order(smj_workspace* ws, smj_stream_t stream) {

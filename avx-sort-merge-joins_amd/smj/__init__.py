@@ -59,7 +59,8 @@ DEVICE_SYMBOLS = [
     "smj_dev_gen_zipf", "smj_dev_synchronize", "smj_dev_partition_range",
     "smj_trace_enable", "smj_trace_reset", "smj_trace_read", "smj_dev_join_segmented",
     "smj_dev_partition_range_packed", "smj_dev_materialize", "smj_selfcheck_lds_order",
-    "smj_set_materialize",
+    "smj_set_materialize", "smj_dev_join_segmented_tables", "smj_dev_partition_range_sampled",
+    "smj_sampled_capacity", "smj_sampled_shards",
 ]
 
 
@@ -170,6 +171,13 @@ class Library:
                                               _I64, _I64, _U32, _P, _P, _P, _P]),
             "smj_dev_partition_range_packed": (C.c_int, [_P, _P, _U64, _P, _U32, _I64, _I64,
                                                          _P, _P, _P]),
+            "smj_dev_join_segmented_tables": (None, [_P, _P, _U64, _P, _P, _P, _U64, _P, _P,
+                                                     _U32, _U32, _I64, _I64, _U32, _P, _P,
+                                                     _P, _P]),
+            "smj_dev_partition_range_sampled": (C.c_int, [_P, _P, _U64, _P, _U32, _I64, _I64,
+                                                          C.c_int, _P, _P, _P, _P]),
+            "smj_sampled_capacity": (_U64, [_U64, _U32]),
+            "smj_sampled_shards": (_U32, []),
             "smj_dev_materialize": (_U64, [_P, _P, _U64, _P, _U64, _P, _U64, _P]),
             "smj_selfcheck_lds_order": (_U64, [_P, _P]),
             "smj_trace_enable": (None, [_P, C.c_int]),
@@ -426,6 +434,36 @@ class Library:
             S.shape[0], segS.data_ptr(), segR.shape[0], bucket_bits, key_lo, key_hi,
             1 if packed else 0, sortedR.data_ptr(), sortedS.data_ptr(), count.data_ptr(),
             self.stream_ptr())
+
+    def dev_join_segmented_tables(self, R, nR, startR, cntR, S, nS, startS, cntS, bucket_bits,
+                                  key_lo, key_hi, sortedR, sortedS, count, packed=False):
+        """smj_dev_join_segmented from explicit segment tables: start/cnt are
+        int64 (2^bucket_bits, nseg) device tensors (element offsets into R /
+        S and counts); nR / nS count the elements inside the segments."""
+        for t in (startR, cntR, startS, cntS):
+            assert t.is_contiguous() and t.shape == startR.shape
+        assert startR.shape[0] == 1 << bucket_bits
+        self.lib.smj_dev_join_segmented_tables(
+            self.ws, R.data_ptr(), nR, startR.data_ptr(), cntR.data_ptr(), S.data_ptr(), nS,
+            startS.data_ptr(), cntS.data_ptr(), startR.shape[1], bucket_bits, key_lo, key_hi,
+            1 if packed else 0, sortedR.data_ptr(), sortedS.data_ptr(), count.data_ptr(),
+            self.stream_ptr())
+
+    def sampled_capacity(self, n, nbits):
+        return int(self.lib.smj_sampled_capacity(n, nbits))
+
+    def sampled_shards(self):
+        return int(self.lib.smj_sampled_shards())
+
+    def dev_partition_range_sampled(self, inp, out, nbits, key_min, key_max, packed,
+                                    seg_start, seg_cnt, flags):
+        """smj_dev_partition_range_sampled: seg_start/seg_cnt int64 device
+        tensors of 2^nbits * shards, flags int32[2]; False when the form does
+        not apply (nothing launched)."""
+        return bool(self.lib.smj_dev_partition_range_sampled(
+            self.ws, inp.data_ptr(), inp.shape[0], out.data_ptr(), nbits, key_min, key_max,
+            1 if packed else 0, seg_start.data_ptr(), seg_cnt.data_ptr(), flags.data_ptr(),
+            self.stream_ptr()))
 
     def dev_partition_range_packed(self, inp, out_words, nbits, key_min, key_max, hist, bad):
         """smj_dev_partition_range writing packed int64 words; False (nothing

@@ -155,6 +155,30 @@ class DeviceOps:
         self.lib.dev_join_segmented(R, segR, S, segS, bucket_bits, key_lo, key_hi,
                                     sR, sS, count, packed=packed)
 
+    # the sampled exchange partition (smj_dev_partition_range_sampled): the
+    # 1-GPU join's level-1 scatter, no histogram pass; SMJ_XSAMPLED=0 keeps
+    # the exact partition
+    @property
+    def can_sample(self):
+        return os.environ.get("SMJ_XSAMPLED", "1") != "0"
+
+    def shards(self):
+        return self.lib.sampled_shards()
+
+    def sampled_capacity(self, n, nbits):
+        return self.lib.sampled_capacity(n, nbits)
+
+    def partition_range_sampled(self, inp, out, nbits, key_min, key_max, packed, seg_start,
+                                seg_cnt, flags):
+        return self.lib.dev_partition_range_sampled(inp, out, nbits, key_min, key_max, packed,
+                                                    seg_start, seg_cnt, flags)
+
+    def join_segmented_tables(self, R, nR, startR, cntR, S, nS, startS, cntS, bucket_bits,
+                              key_lo, key_hi, sR, sS, count, packed=False):
+        self.lib.dev_join_segmented_tables(R, nR, startR, cntR, S, nS, startS, cntS,
+                                           bucket_bits, key_lo, key_hi, sR, sS, count,
+                                           packed=packed)
+
 
 class DistributedJoin:
     """One process per device; `step` joins the local slices of R and S
@@ -180,6 +204,10 @@ class DistributedJoin:
         F, G = self.fanout, self.world
         self.per_rank = [owned(F, G, g)[1] - owned(F, G, g)[0] for g in range(G)]
         self.p_lo, self.p_hi = owned(F, G, self.rank)
+        self.sampled = bool(getattr(ops, "can_sample", False))
+        # segment-table width: the same on every rank whichever form a rank's
+        # partition takes
+        self.shards = ops.shards() if hasattr(ops, "shards") else 1
         self.buf = {}
         self.last_recv = {}
         self.last_packed = False  # the layout of the last step's exchange
@@ -189,7 +217,7 @@ class DistributedJoin:
         """Exchange statistics since the last reset: bytes this rank sent to
         other ranks, steps, and (GPU) the time of S's row exchange -- from
         its issue to its completion, with nothing else queued behind it."""
-        self.stats = {"steps": 0, "sent_B": 0, "recv_B": 0, "xS_ms": 0.0}
+        self.stats = {"steps": 0, "sent_B": 0, "recv_B": 0, "gap_B": 0, "xS_ms": 0.0}
         self._ev = []
 
     def _grow(self, key, n, words=False):
@@ -200,58 +228,126 @@ class DistributedJoin:
         return b[:n]
 
     def _partition(self, rel, key, packed):
-        """Range-partition `rel` (packed words or tuples).  Returns (buffer,
-        histogram, whether every rank packed) -- the last is only known after
-        the size exchange, so it is returned as a device flag."""
+        """Exact range partition of `rel` (packed words or tuples), partitions
+        back to back.  Returns (buffer, per-partition start (F, K) and count
+        (F, K) with only shard 0 used, flags int64 [not packable, 0])."""
         dev = rel.device
-        hist = torch.zeros(self.fanout, dtype=torch.int64, device=dev)
+        F, K = self.fanout, self.shards
+        hist = torch.zeros(F, dtype=torch.int64, device=dev)
+        bad_flag = torch.zeros(2, dtype=torch.int64, device=dev)
+        part = None
         if packed:
             part = self._grow("pw" + key, rel.shape[0], words=True)
             bad = torch.zeros(1, dtype=torch.int32, device=dev)
             if self.ops.partition_range_packed(rel, part, self.pbits, self.key_min,
                                                self.key_max, hist, bad):
-                return part, hist, bad.to(torch.int64)
-        part = self._grow("part" + key, rel.shape[0])
-        self.ops.partition_range(rel, part, self.pbits, self.key_min, self.key_max, hist)
-        return part, hist, torch.full((1,), -1, dtype=torch.int64, device=dev)
+                bad_flag[0] = bad[0]
+            else:
+                part = None
+                bad_flag[0] = 1  # not packable at all: tuples
+        if part is None:
+            part = self._grow("part" + key, rel.shape[0])
+            self.ops.partition_range(rel, part, self.pbits, self.key_min, self.key_max, hist)
+        start = torch.zeros(F, K, dtype=torch.int64, device=dev)
+        cnt = torch.zeros(F, K, dtype=torch.int64, device=dev)
+        start[:, 0] = torch.cumsum(hist, 0) - hist
+        cnt[:, 0] = hist
+        return part, start, cnt, bad_flag
+
+    def _sampled(self, rel, key, packed):
+        """Sampled range partition (no histogram pass): partition p is K
+        consecutive shard regions with slack after each.  Returns (buffer,
+        start (F, K), count (F, K), flags int64 [not packable, overflow]), or
+        None when the form does not apply."""
+        dev = rel.device
+        F, K = self.fanout, self.shards
+        cap = self.ops.sampled_capacity(rel.shape[0], self.pbits)
+        part = self._grow(("sw" if packed else "st") + key, cap, words=packed)
+        ss = torch.empty(F * K, dtype=torch.int64, device=dev)
+        sc = torch.empty(F * K, dtype=torch.int64, device=dev)
+        flags = torch.zeros(2, dtype=torch.int32, device=dev)
+        if not self.ops.partition_range_sampled(rel, part, self.pbits, self.key_min,
+                                                self.key_max, packed, ss, sc, flags):
+            return None
+        f = flags.to(torch.int64)
+        return part, ss.view(F, K), sc.view(F, K), torch.stack([f[1], f[0]])
 
     def _exchange(self, rel, key, allow_pack=True):
-        """Partition `rel`, swap partition sizes, start the row all-to-all.
-        Returns (receive buffer, per-source sizes of the owned partitions
-        (world, 2^lbits) padded with empty buckets, async work, packed?)."""
+        """Partition `rel`, swap the segment tables, start the row all-to-all.
+        Every attempt agrees across ranks (one MAX all-reduce inside the table
+        exchange): a sampled region overflow anywhere -> every rank
+        partitions exactly; an unpackable tuple anywhere -> every rank sends
+        tuples.  Returns (receive buffer, start and count tables
+        (2^lbits, world * K) for the local join, elements inside the segments,
+        async work, packed?)."""
         G = self.world
         dev = rel.device
+        F, K = self.fanout, self.shards
         mine = self.p_hi - self.p_lo
+        own = owners(F, G).to(dev)
+        lo_of = torch.tensor([owned(F, G, g)[0] for g in range(G)], dtype=torch.int64,
+                             device=dev)
         packed = allow_pack and bool(getattr(self.ops, "can_pack", False))
+        sampled = self.sampled
         while True:
-            part, hist, flag = self._partition(rel, key, packed)
-            # any rank that could not pack (1) or did not try (-1): all ranks
-            # send tuples.  MAX over ranks of (flag != 0).
-            agree = flag.ne(0).to(torch.int64)
-            dist.all_reduce(agree, op=dist.ReduceOp.MAX, group=self.group)
-            seg = torch.empty(G * mine, dtype=torch.int64, device=dev)
-            dist.all_to_all_single(seg, hist, [mine] * G, self.per_rank, group=self.group)
-            seg = seg.view(G, mine)
-            sizes = torch.cat([send_counts(hist, G), seg.sum(1), agree]).tolist()  # one sync
-            if packed and sizes[-1]:
+            res = self._sampled(rel, key, packed) if sampled else None
+            if res is None:  # exact partition (the receivers read either form)
+                res = self._partition(rel, key, packed)
+            part, start, cnt, fl = res
+            # per destination g: its chunk of `part` is [cstart[g], cstart[g + 1])
+            # (region slack included); the tables give each owned segment's
+            # offset inside that chunk
+            cstart = start[lo_of, 0]
+            cend = (start + cnt).max()
+            csize = torch.cat([cstart[1:], cend.view(1)]) - cstart
+            used = torch.zeros(G, dtype=torch.int64, device=dev).index_add_(0, own, cnt.sum(1))
+            rel_start = torch.where(cnt > 0, start - cstart[own].view(F, 1), 0)
+            head = torch.stack([csize, used], 1)  # (G, 2)
+            msgs = []
+            for g in range(G):
+                lo, hi = owned(F, G, g)
+                msgs += [head[g], rel_start[lo:hi].reshape(-1), cnt[lo:hi].reshape(-1)]
+            # [not packable, region overflow], MAX over ranks
+            dist.all_reduce(fl, op=dist.ReduceOp.MAX, group=self.group)
+            inp = torch.cat(msgs)
+            per_in = [2 + 2 * n * K for n in self.per_rank]
+            out_msg = torch.empty(G * (2 + 2 * mine * K), dtype=torch.int64, device=dev)
+            dist.all_to_all_single(out_msg, inp, [2 + 2 * mine * K] * G, per_in,
+                                   group=self.group)
+            msg = out_msg.view(G, 2 + 2 * mine * K)
+            host = torch.cat([csize, msg[:, 0], msg[:, 1], fl]).tolist()  # one sync
+            sl, rl, ru = host[:G], host[G:2 * G], host[2 * G:3 * G]
+            bad, ovf = host[3 * G:]
+            if ovf:
+                sampled = False  # a region overflowed somewhere: every rank exact
+                continue
+            if packed and bad:
                 packed = False  # repeat on tuples, on every rank
                 continue
             break
-        sl, rl = sizes[:G], sizes[G:2 * G]
         out = self._grow(("rw" if packed else "recv") + key, sum(rl), words=packed)
         row = 8 if packed else part.element_size() * (part.shape[1] if part.dim() > 1 else 1)
         self.stats["sent_B"] += row * (sum(sl) - sl[self.rank])
         self.stats["recv_B"] += row * (sum(rl) - rl[self.rank])
+        self.stats["gap_B"] += row * (sum(rl) - sum(ru))
         ev = None
         if key == "S" and out.is_cuda:
             ev = torch.cuda.Event(enable_timing=True)
             ev.record()
-        work = self._rows(out, part, rl, sl)
+        work = self._rows(out, part[:sum(sl)], rl, sl)  # part may hold unused capacity
         self.last_recv[key] = (sl, rl)
-        pad = torch.zeros(G, 1 << self.lbits, dtype=torch.int64, device=dev)
-        pad[:, :mine] = seg
+        # receive tables: segment (bucket b, source s, shard q) at offset
+        # ro[s] + its offset in s's chunk
+        ro = torch.tensor([sum(rl[:g]) for g in range(G)], dtype=torch.int64, device=dev)
+        rs = msg[:, 2:2 + mine * K].view(G, mine, K) + ro.view(G, 1, 1)
+        rc = msg[:, 2 + mine * K:].view(G, mine, K)
+        nb = 1 << self.lbits
+        tstart = torch.zeros(nb, G * K, dtype=torch.int64, device=dev)
+        tcnt = torch.zeros(nb, G * K, dtype=torch.int64, device=dev)
+        tstart[:mine] = rs.permute(1, 0, 2).reshape(mine, G * K)
+        tcnt[:mine] = rc.permute(1, 0, 2).reshape(mine, G * K)
         self._ev_issue = ev
-        return out, pad, work, packed
+        return out, tstart, tcnt, sum(ru), work, packed
 
     def _rows(self, out, inp, rl, sl):
         """Asynchronous row all-to-all: `inp` holds sl[g] rows for rank g in
@@ -284,8 +380,8 @@ class DistributedJoin:
 
     def step(self, R, S, count):
         # the row exchange of R overlaps the partition of S
-        rR, segR, wR, pR = self._exchange(R, "R")
-        rS, segS, wS, pS = self._exchange(S, "S")
+        rR, tR, cR, nR, wR, pR = self._exchange(R, "R")
+        rS, tS, cS, nS, wS, pS = self._exchange(S, "S")
         eS = self._ev_issue
         wR.wait()
         wS.wait()
@@ -297,17 +393,17 @@ class DistributedJoin:
         # both relations must reach the local join in one layout: the one
         # that went out packed is exchanged again as tuples
         if pR and not pS:
-            rR, segR, wR, pR = self._exchange(R, "R", allow_pack=False)
+            rR, tR, cR, nR, wR, pR = self._exchange(R, "R", allow_pack=False)
             wR.wait()
         elif pS and not pR:
-            rS, segS, wS, pS = self._exchange(S, "S", allow_pack=False)
+            rS, tS, cS, nS, wS, pS = self._exchange(S, "S", allow_pack=False)
             wS.wait()
         assert pR == pS
         self.last_packed = pR
-        sR = self._grow("sortR", rR.shape[0])
-        sS = self._grow("sortS", rS.shape[0])
-        self.ops.join_segmented(rR, segR, rS, segS, self.lbits, self.key_lo,
-                                self.key_hi, sR, sS, count, packed=pR)
+        sR = self._grow("sortR", nR)
+        sS = self._grow("sortS", nS)
+        self.ops.join_segmented_tables(rR, nR, tR, cR, rS, nS, tS, cS, self.lbits,
+                                       self.key_lo, self.key_hi, sR, sS, count, packed=pR)
         dist.all_reduce(count, group=self.group)
         return sR, sS
 

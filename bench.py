@@ -280,6 +280,9 @@ def main():
         # §8(d): against 7 links x 153 GB/s, not HBM)
         xchg = {"xgmi_bytes_sent_per_gpu": st["sent_B"] // k,
                 "xgmi_bytes_recv_per_gpu": st["recv_B"] // k,
+                # region slack of the sampled exchange partition received
+                # with the rows (own rows included)
+                "slack_bytes_recv_per_gpu": st.get("gap_B", 0) // k,
                 "packed_words": bool(dj.last_packed),
                 "exchange_S_ms": round(st["xS_ms"] / k, 3),
                 "exchange_S_GBps": round(st["sent_B"] / 2 / k / (st["xS_ms"] / k * 1e-3) / 1e9, 1)

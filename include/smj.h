@@ -491,6 +491,37 @@ void smj_dev_join_segmented(smj_workspace * ws, void * R, uint64_t nR,
                             uint32_t flags, tuple_t * sortedR, tuple_t * sortedS,
                             unsigned long long * count_dev, smj_stream_t stream);
 
+/* The local join of smj_dev_join_segmented from explicit segment tables:
+ * bucket b (b < 2^bucket_bits) is the nseg segments startX/cntX[b * nseg + j]
+ * (device int64, element offsets into X and element counts), so a receive
+ * buffer may hold unused gaps between segments (the sampled exchange below).
+ * nR / nS count the elements inside the segments. */
+void smj_dev_join_segmented_tables(smj_workspace * ws, void * R, uint64_t nR,
+                                   const int64_t * startR, const int64_t * cntR,
+                                   void * S, uint64_t nS, const int64_t * startS,
+                                   const int64_t * cntS, uint32_t nseg,
+                                   uint32_t bucket_bits, int64_t key_lo, int64_t key_hi,
+                                   uint32_t flags, tuple_t * sortedR, tuple_t * sortedS,
+                                   unsigned long long * count_dev, smj_stream_t stream);
+
+/* Range partition of smj_dev_partition_range by the 1-GPU join's sampled
+ * scatter (no histogram pass; packed words when `packed`).  Partition p is
+ * smj_sampled_shards() consecutive regions, p's before p + 1's; region
+ * i = p * shards + q holds seg_cnt[i] elements from element offset
+ * seg_start[i] of `out` and is followed by unused slack, so `out` must hold
+ * smj_sampled_capacity(n, nbits) elements (tuples, or 8-byte words).
+ * flags (device uint32[2], zeroed here): [0] = 1 when a region overflowed
+ * (the output is incomplete: use the exact partition), [1] = 1 when packed
+ * and some tuple did not pack.  Returns 0 (nothing launched) when the form
+ * does not apply: nbits > 10, n >= 2^32, or packed words unusable. */
+int smj_dev_partition_range_sampled(smj_workspace * ws, const tuple_t * in, uint64_t n,
+                                    void * out, uint32_t nbits, int64_t key_min,
+                                    int64_t key_max, int packed, int64_t * seg_start,
+                                    int64_t * seg_cnt, unsigned int * flags,
+                                    smj_stream_t stream);
+uint64_t smj_sampled_capacity(uint64_t n, uint32_t nbits);
+uint32_t smj_sampled_shards(void);
+
 /* Self-check of the hardware property behind the stable partition's ranks:
  * LDS atomic adds return their old values to the lanes of one instruction
  * that hit the same word in lane order (partition.hip, k_scatter_swa).

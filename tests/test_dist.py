@@ -23,9 +23,82 @@ class HostOps:
     packed exchange as int64 words, like smj_dev_partition_range_packed)."""
 
     can_pack = True
+    K = 3  # shards of the sampled layout (the device uses smj_sampled_shards())
 
-    def __init__(self, orc):
+    def __init__(self, orc, sampled=True, overflow=False, not_applicable=False):
         self.orc = orc
+        self.can_sample = sampled
+        self.overflow = overflow  # report a region overflow from the sampled form
+        self.not_applicable = not_applicable  # the sampled form returns False
+
+    def shards(self):
+        return self.K
+
+    def sampled_capacity(self, n, nbits):
+        return n + n // 8 + (1 << nbits) * self.K * 5 + 16
+
+    def partition_range_sampled(self, inp, out, nbits, key_min, key_max, packed, seg_start,
+                                seg_cnt, flags):
+        """The device's sampled layout: partition p is K consecutive shard
+        regions (shard = position / n * K), each followed by slack that holds
+        garbage; partitions in order."""
+        from smj.dist import range_digit
+        F, K, n = 1 << nbits, self.K, inp.shape[0]
+        if self.not_applicable:
+            return False
+        if packed:
+            words = torch.empty(n, dtype=torch.int64)
+            hist = torch.zeros(F, dtype=torch.int64)
+            bad = torch.zeros(1, dtype=torch.int32)
+            if not self.partition_range_packed(inp, words, nbits, key_min, key_max, hist, bad):
+                return False
+            flags[1] = int(bad[0])
+            # back in input order: the packed partition above sorted by digit
+            d = range_digit(inp[:, 1], key_min, key_max, nbits)
+            vals = torch.empty_like(words)
+            vals[torch.argsort(d, stable=True)] = words
+        else:
+            vals = inp
+        d = range_digit(inp[:, 1], key_min, key_max, nbits)
+        q = torch.arange(n) * K // max(n, 1)
+        idx = d * K + q
+        cnt = torch.bincount(idx, minlength=F * K)
+        cap = cnt + cnt // 8 + torch.arange(F * K) % 5
+        start = torch.cumsum(cap, 0) - cap
+        order = torch.argsort(idx, stable=True)
+        first = torch.cumsum(cnt, 0) - cnt
+        si = idx[order]
+        pos = start[si] + torch.arange(n) - first[si]
+        out.fill_(-7)  # the slack must never be read
+        out[pos] = vals[order]
+        seg_start.copy_(start)
+        seg_cnt.copy_(cnt)
+        if self.overflow:
+            flags[0] = 1
+        return True
+
+    def join_segmented_tables(self, R, nR, startR, cntR, S, nS, startS, cntS, bucket_bits,
+                              key_lo, key_hi, sR, sS, count, packed=False):
+        """Gather every bucket's segments (bucket-major) and join the dense
+        relations with the checks of join_segmented."""
+        dense = []
+        for X, n, st, ct in ((R, nR, startR, cntR), (S, nS, startS, cntS)):
+            assert st.shape == ct.shape and st.shape[0] == 1 << bucket_bits
+            rows, seg = [], torch.zeros(1, st.shape[0], dtype=torch.int64)
+            for b in range(st.shape[0]):
+                for j in range(st.shape[1]):
+                    a, c = int(st[b, j]), int(ct[b, j])
+                    if c:
+                        rows.append(X[a:a + c])
+                        seg[0, b] += c
+            Xd = torch.cat(rows) if rows else X[:0]
+            assert Xd.shape[0] == n
+            if not packed:
+                assert bool((Xd[:, 1] != -7).all()), "a gap was read"  # keys are >= 1
+            dense.append((Xd, seg))
+        (Rd, segR), (Sd, segS) = dense
+        self.join_segmented(Rd, segR, Sd, segS, bucket_bits, key_lo, key_hi, sR, sS, count,
+                            packed=packed)
 
     def empty(self, n):
         return torch.empty((n, 2), dtype=torch.int64)
@@ -98,7 +171,7 @@ class HostOps:
         count.fill_(c)
 
 
-def _worker(rank, world, port, n, q, s_payload="negative"):
+def _worker(rank, world, port, n, q, s_payload="negative", mode="sampled"):
     import sys
     for p in (ROOT, PKG):
         sys.path.insert(0, p)
@@ -126,7 +199,12 @@ def _worker(rank, world, port, n, q, s_payload="negative"):
         def rows(t):
             return torch.from_numpy(t[rank * n:(rank + 1) * n].view(np.int64).reshape(-1, 2).copy())
 
-        dj = DistributedJoin(HostOps(orc), 6, 1, total)
+        # mode: "sampled" (every rank), "exact", "mixed" (rank 0 exact, the
+        # others sampled: receivers read either form), "overflow" (rank 1's
+        # sampled regions overflow: every rank repeats exactly)
+        ops = HostOps(orc, sampled=mode != "exact", overflow=mode == "overflow" and rank == 1,
+                      not_applicable=mode == "mixed" and rank == 0)
+        dj = DistributedJoin(ops, 6, 1, total)
         count = torch.zeros(1, dtype=torch.int64)
         for _ in range(2):  # second step reuses the grown buffers
             sR, sS = dj.step(rows(R), rows(S), count)
@@ -157,12 +235,19 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world,chunk_mb,s_payload", [
-    (2, None, "negative"), (3, None, "negative"), (2, 0, "negative"), (3, 0, "rowid"),
-    (2, None, "rowid"), (3, None, "rowid"), (2, None, "r_negative"), (3, None, "r_negative")])
-def test_distributed_join_gloo(world, chunk_mb, s_payload, oracles, monkeypatch):
+@pytest.mark.parametrize("world,chunk_mb,s_payload,mode", [
+    (2, None, "negative", "sampled"), (3, None, "negative", "sampled"),
+    (2, 0, "negative", "sampled"), (3, 0, "rowid", "sampled"),
+    (2, None, "rowid", "sampled"), (3, None, "rowid", "sampled"),
+    (2, None, "r_negative", "sampled"), (3, None, "r_negative", "sampled"),
+    (2, None, "rowid", "exact"), (3, None, "negative", "exact"),
+    (3, None, "rowid", "mixed"), (2, None, "negative", "mixed"),
+    (3, None, "rowid", "overflow")])
+def test_distributed_join_gloo(world, chunk_mb, s_payload, mode, oracles, monkeypatch):
     """chunk_mb 0: every row message over the chunk limit, so the exchange
-    takes the chunked isend/irecv path (the one RCCL needs for >1.6 GB).
+    takes the chunked isend/irecv path (the one RCCL needs for >1 GiB).
+    mode: the exchange partition's form (sampled with gaps, exact, a mix of
+    the two, or a sampled overflow that sends every rank back to exact).
     s_payload "rowid": both relations exchanged as packed words; "negative":
     S cannot be packed, every rank falls back to tuples for both; "r_negative":
     R cannot be packed but S can (S goes again, as tuples)."""
@@ -171,7 +256,7 @@ def test_distributed_join_gloo(world, chunk_mb, s_payload, oracles, monkeypatch)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, 5000, q, s_payload))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, 5000, q, s_payload, mode))
              for r in range(world)]
     for p in procs:
         p.start()

@@ -4,6 +4,8 @@
   its slice with smj_dev_partition_range, the receive buffer of a rank is the
   concatenation of the sources' owned partitions, and smj_dev_join_segmented
   joins it; per-rank counts and sorted outputs are checked against the oracle.
+* The same for the sampled exchange partition (regions with slack, gaps on
+  the wire) and the table-driven local join.
 * DistributedJoin itself runs over a one-rank NCCL (RCCL) group: the same
   code path bench.py --gpus N runs, with the collectives degenerate.
 """
@@ -96,17 +98,104 @@ def test_segmented_join_simulated_exchange(libs, oracles, width, world, kind, pa
     assert got_total == total
 
 
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("kind", ["pk_fk", "zipf"])
+@pytest.mark.parametrize("packed", [False, True])
+def test_sampled_exchange_simulated(libs, oracles, width, world, kind, packed):
+    """The sampled exchange partition (smj_dev_partition_range_sampled: K shard
+    regions per partition, slack between them) simulated on one GPU: rank g
+    receives from every source the chunk [start of its first owned region,
+    start of the next rank's first region) -- gaps included -- and joins it
+    through smj_dev_join_segmented_tables with the sources' region tables."""
+    import torch
+    from smj.dist import ceil_log2, owned, plan_shift
+    orc, lib = oracles[width], libs[width]
+    if packed and width != 16:
+        pytest.skip("packed words are the 16-byte layout")
+    n = 600_000
+    R, S = _inputs(orc, kind, n)
+    total, _, _ = orc.sortmergejoin(R, S)
+    bucket_bits = 6
+    pbits = min(bucket_bits + ceil_log2(world), 10)
+    F, K = 1 << pbits, lib.sampled_shards()
+    s1 = plan_shift(1, n, pbits)
+    parts = {}
+    for key, rel in (("R", R), ("S", S)):
+        for s in range(world):
+            sl = rel[s * n // world:(s + 1) * n // world]
+            d_in = lib.to_device(sl)
+            cap = lib.sampled_capacity(len(sl), pbits)
+            out = (torch.full((cap,), -7, dtype=torch.int64, device="cuda") if packed
+                   else lib.empty(cap))
+            ss = torch.empty(F * K, dtype=torch.int64, device="cuda")
+            sc = torch.empty(F * K, dtype=torch.int64, device="cuda")
+            fl = torch.ones(2, dtype=torch.int32, device="cuda")
+            assert lib.dev_partition_range_sampled(d_in, out, pbits, 1, n, packed, ss, sc, fl)
+            torch.cuda.synchronize()
+            assert fl.tolist() == [0, 0]
+            assert int(sc.sum()) == len(sl)
+            ss, sc = ss.view(F, K), sc.view(F, K)
+            # regions in (partition, shard) order, no overlap
+            ends = (ss + sc).reshape(-1)
+            assert bool((ends[:-1] <= ss.reshape(-1)[1:]).all())
+            parts[key, s] = (out, ss, sc)
+    got_total = 0
+    for g in range(world):
+        p_lo, p_hi = owned(F, world, g)
+        mine = p_hi - p_lo
+        lbits = ceil_log2(max(mine, 1))
+        key_lo = 1 + (p_lo << s1)
+        key_hi = key_lo + (1 << (s1 + lbits)) - 1
+        recv, tabs, used = {}, {}, {}
+        for key in ("R", "S"):
+            rows, tst, tct, base, nused = [], [], [], 0, 0
+            for s in range(world):
+                out, ss, sc = parts[key, s]
+                c0 = int(ss[p_lo, 0])
+                c1 = int(ss[p_hi, 0]) if p_hi < F else int((ss + sc).max())
+                rows.append(out[c0:c1])
+                tst.append(ss[p_lo:p_hi] - c0 + base)
+                tct.append(sc[p_lo:p_hi])
+                base += c1 - c0
+                nused += int(sc[p_lo:p_hi].sum())
+            recv[key] = torch.cat(rows).contiguous()
+            st_ = torch.zeros(1 << lbits, world * K, dtype=torch.int64, device="cuda")
+            ct_ = torch.zeros_like(st_)
+            st_[:mine] = torch.stack(tst, 1).reshape(mine, world * K)
+            ct_[:mine] = torch.stack(tct, 1).reshape(mine, world * K)
+            tabs[key] = (st_.contiguous(), ct_.contiguous())
+            used[key] = nused
+        sR, sS = lib.empty(used["R"]), lib.empty(used["S"])
+        cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+        lib.dev_join_segmented_tables(recv["R"], used["R"], *tabs["R"], recv["S"], used["S"],
+                                      *tabs["S"], lbits, key_lo, key_hi, sR, sS, cnt,
+                                      packed=packed)
+        torch.cuda.synchronize()
+        lo_k, hi_k = 1 + (p_lo << s1), 1 + (p_hi << s1)
+        mR = R[(R["key"] >= lo_k) & (R["key"] < hi_k)] if g < world - 1 else R[R["key"] >= lo_k]
+        mS = S[(S["key"] >= lo_k) & (S["key"] < hi_k)] if g < world - 1 else S[S["key"] >= lo_k]
+        exp, eR, eS = orc.sortmergejoin(mR, mS)
+        assert int(cnt.item()) == exp, (g, int(cnt.item()), exp)
+        assert np.array_equal(lib.to_host(sR), eR)
+        assert np.array_equal(lib.to_host(sS), eS)
+        got_total += exp
+    assert got_total == total
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
 
 
-def test_distributed_join_one_rank_rccl(libs, width):
-    """DistributedJoin over a one-rank RCCL group, device ops, 4M x 4M."""
+@pytest.mark.parametrize("xsampled", ["1", "0"])
+def test_distributed_join_one_rank_rccl(libs, width, xsampled, monkeypatch):
+    """DistributedJoin over a one-rank RCCL group, device ops, 4M x 4M, with
+    the sampled (1) and the exact (0) exchange partition."""
     import torch
     import torch.distributed as dist
     from smj.dist import DeviceOps, DistributedJoin
+    monkeypatch.setenv("SMJ_XSAMPLED", xsampled)
     lib = libs[width]
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ["MASTER_PORT"] = str(_free_port())
