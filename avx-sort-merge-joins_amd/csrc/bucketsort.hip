@@ -1191,11 +1191,20 @@ k_skew_place(SkewArgs K) {
                 if (i < len) atomicAdd(&h[dg[k]], 1u);
             }
             __syncthreads();
-            // reserve this chunk's share of every digit at the cursors
-            for (uint32_t d = threadIdx.x; d < GS_NB3; d += SK_THREADS) {
+            // reserve this chunk's share of every digit at the cursors: a
+            // thread's atomics all in flight, their results used only after
+            // the last one (one returned atomic at a time waited ~8 global
+            // round trips per chunk)
+            constexpr int RPT = GS_NB3 / SK_THREADS;
+            uint32_t res[RPT];
+#pragma unroll
+            for (int k = 0; k < RPT; k++) {
+                const uint32_t d = threadIdx.x + k * SK_THREADS;
                 const uint32_t n = h[d];
-                if (n) h[d] = atomicAdd(&gcur[d], n);
+                res[k] = n ? atomicAdd(&gcur[d], n) : 0u;
             }
+#pragma unroll
+            for (int k = 0; k < RPT; k++) h[threadIdx.x + k * SK_THREADS] = res[k];
             __syncthreads();
 #pragma unroll
             for (int k = 0; k < SK_ITEMS; k++) {
