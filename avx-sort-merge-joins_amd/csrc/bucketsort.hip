@@ -849,7 +849,10 @@ k_groupsort(GroupArgs A) {
 //   k_skew_check : per group: equal-key runs in (key, payload) order?
 // What is left (inexact digits, equal-key runs out of payload order) goes to
 // the host-driven merge sort and merge-join count.
-constexpr int SK_THREADS = 256;
+#ifndef SMJ_SK_THREADS
+#define SMJ_SK_THREADS 256
+#endif
+constexpr int SK_THREADS = SMJ_SK_THREADS;
 constexpr int SK_ITEMS = 8;
 constexpr int SK_CHUNK = SK_THREADS * SK_ITEMS;
 constexpr uint32_t kSkewSmall = 16384;  // tuples per relation, one workgroup
@@ -1263,6 +1266,14 @@ static void skew_path(Workspace* ws, const GroupArgs& G, OvfEntry* ovf, uint32_t
         }
     }
     const size_t nl = large.size();
+    if (getenv("SMJ_SKEW_STATS")) {  // measurements only
+        uint64_t ts = 0, tl = 0;
+        for (uint32_t i : small) ts += he[i].nr[0] + (nrel > 1 ? he[i].nr[1] : 0);
+        for (uint32_t i : large) tl += he[i].nr[0] + (nrel > 1 ? he[i].nr[1] : 0);
+        fprintf(stderr, "[skew] %zu small groups (%llu tuples), %zu large (%llu tuples), "
+                "%zu items\n", small.size(), (unsigned long long)ts, nl,
+                (unsigned long long)tl, items.size());
+    }
     const size_t lbytes = (small.size() + 2 * nl) * 4;
     const size_t ibytes = items.size() * sizeof(uint4);
     unsigned char* hbuf = (unsigned char*)ws->host_pinned("sk_h", lbytes + ibytes + 16);
