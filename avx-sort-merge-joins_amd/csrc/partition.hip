@@ -673,6 +673,314 @@ k_scatter_swa(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
     }
 }
 
+// s_waitcnt immediate for vmcnt(N), expcnt and lgkmcnt left free (gfx9 layout:
+// vmcnt[3:0] + vmcnt[5:4] at bits 15:14)
+constexpr int vmcnt_imm(int n) { return (n & 15) | ((n >> 4) << 14) | 0x0f70; }
+
+// k_scatter_swa with the next-but-one tile's loads in flight: three register
+// tiles rotate (the loop is unrolled by three so that no tile is copied
+// between registers -- a copy would wait for its loads), and the wait before a
+// tile's segment stores is vmcnt(ITEMS): everything but the loads issued in
+// this tile (the next-but-one) has landed, i.e. the next tile and the previous
+// tile's stores.  The loads thus fly under a whole tile of LDS work instead of
+// the stage phase alone.  Same ranks, layout and results as k_scatter_swa.
+template <int THREADS, int ITEMS, class DigitL, bool NT>
+struct SwpTile {
+    typedef SwaGeom<THREADS, ITEMS> G;
+    static constexpr int W = G::W;
+    static constexpr int TILE = G::TILE;
+    static constexpr uint32_t SEG = G::SEG;
+    static constexpr uint32_t CW = G::CW;
+    const Tup* __restrict__ in;
+    Tup* __restrict__ out;
+    DigitL dig;
+    Tup* stage;
+    Tup* carry;
+    uint32_t* w32;
+    u32x4_t* info;
+    uint16_t* segown;
+    uint32_t* scr;
+    uint32_t hb, t2, wbase;
+    int lane, wid;
+    bool owner;
+    uint64_t end;
+    uint32_t pos[2], kc[2];
+
+    __device__ __forceinline__ void load(Tup (&v)[ITEMS], uint64_t base) const {
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint64_t i = base + wbase + j * 64 + lane;
+            const uint64_t c = i < end ? i : end - 1;  // unconditional: a fixed count in flight
+            v[j] = NT ? ld_nt(in + c) : in[c];
+        }
+    }
+
+    __device__ __forceinline__ void tile(const Tup (&v)[ITEMS], Tup (&pre)[ITEMS],
+                                         uint64_t base) {
+        const uint32_t tcount = (uint32_t)min((uint64_t)TILE, end - base);
+        uint32_t dg[ITEMS], rk[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const bool valid = wbase + j * 64 + lane < tcount;
+            dg[j] = valid ? dig(v[j]) : 0xffffffffu;
+            const uint32_t d = valid ? dg[j] : 0;
+            const uint32_t sh = (d & 1u) * 16u;
+            uint32_t old = 0;
+            if (valid) old = atomicAdd(&w32[wid * hb + (d >> 1)], 1u << sh);
+            rk[j] = (old >> sh) & 0xffffu;
+        }
+        __syncthreads();
+        uint32_t cw[W];
+        uint32_t c[2] = {0, 0}, E[2] = {0, 0}, ns[2] = {0, 0};
+        if (owner) {
+#pragma unroll
+            for (int w = 0; w < W; w++) {
+                cw[w] = w32[w * hb + t2];
+                c[0] += cw[w] & 0xffffu;
+                c[1] += cw[w] >> 16;
+            }
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const uint32_t T = kc[h] + c[h];
+                const uint32_t m = (pos[h] + T) % SEG;
+                E[h] = m <= T ? T - m : 0u;
+                ns[h] = E[h] ? (pos[h] + E[h]) / SEG - pos[h] / SEG : 0u;
+            }
+        }
+        uint32_t tot;
+        const uint32_t ex =
+            block_exclusive_scan((c[0] + c[1]) | ((ns[0] + ns[1]) << 16), scr, &tot);
+        const uint32_t nsegT = tot >> 16;
+        uint32_t ts[2] = {0, 0};
+        if (owner) {
+            ts[0] = ex & 0xffffu;
+            ts[1] = ts[0] + c[0];
+            const uint32_t sp[2] = {ex >> 16, (ex >> 16) + ns[0]};
+            uint32_t o0 = ts[0], o1 = ts[1];
+#pragma unroll
+            for (int w = 0; w < W; w++) {
+                const uint32_t x = cw[w];
+                w32[w * hb + t2] = o0 | (o1 << 16);
+                o0 += x & 0xffffu;
+                o1 += x >> 16;
+            }
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const uint32_t d = 2 * t2 + h;
+                u32x4_t I;
+                I[0] = pos[h];
+                I[1] = E[h];
+                I[2] = ts[h];
+                I[3] = sp[h] | (kc[h] << 16);
+                info[d] = I;
+                for (uint32_t k = 0; k < ns[h]; k++) segown[sp[h] + k] = (uint16_t)d;
+            }
+        }
+        // the next-but-one tile (its registers held the previous tile)
+        load(pre, base + 2 * (uint64_t)TILE);
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++)
+            if (dg[j] != 0xffffffffu) {
+                const uint32_t d = dg[j];
+                const uint32_t wo = (w32[wid * hb + (d >> 1)] >> ((d & 1u) * 16u)) & 0xffffu;
+                stage[wo + rk[j]] = v[j];
+            }
+        __syncthreads();
+        if (owner) {
+#pragma unroll
+            for (int w = 0; w < W; w++) w32[w * hb + t2] = 0;
+        }
+        // the next tile and the previous tile's stores have landed; the
+        // next-but-one tile's ITEMS loads stay in flight
+        __builtin_amdgcn_s_waitcnt(vmcnt_imm(ITEMS));
+        for (uint32_t q = threadIdx.x; q < nsegT * SEG; q += THREADS) {
+            const uint32_t sg = q / SEG;
+            const uint32_t d = segown[sg];
+            const u32x4_t I = info[d];
+            const uint32_t p = I[0];
+            const uint32_t addr = (p / SEG + (sg - (I[3] & 0xffffu))) * SEG + q % SEG;
+            if (addr >= p && addr < p + I[1]) {
+                const uint32_t e = addr - p;
+                const uint32_t k = I[3] >> 16;
+                const Tup x = e < k ? carry[d * CW + e] : stage[I[2] + e - k];
+                if (NT)
+                    st_stream(out + addr, x);
+                else
+                    out[addr] = x;
+            }
+        }
+        __syncthreads();
+        if (owner) {
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const uint32_t d = 2 * t2 + h;
+                const uint32_t T = kc[h] + c[h];
+                for (uint32_t e = E[h]; e < T; e++)
+                    carry[d * CW + (e - E[h])] =
+                        e < kc[h] ? carry[d * CW + e] : stage[ts[h] + e - kc[h]];
+                pos[h] += E[h];
+                kc[h] = T - E[h];
+            }
+        }
+    }
+};
+
+template <int THREADS, int ITEMS, class Digit, bool NT>
+__global__ void __launch_bounds__(THREADS)
+k_scatter_swp(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_arg,
+              uint32_t nbins, const uint32_t* __restrict__ counts, uint32_t nwg,
+              const uint64_t* __restrict__ starts, Tup* __restrict__ out) {
+    typedef SwpTile<THREADS, ITEMS, decltype(dig_arg.load()), NT> P;
+    constexpr int W = P::W;
+    constexpr int TILE = P::TILE;
+    constexpr uint32_t SEG = P::SEG;
+    constexpr uint32_t CW = P::CW;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    P s;
+    s.in = in;
+    s.out = out;
+    s.dig = dig_arg.load();
+    s.stage = reinterpret_cast<Tup*>(lds_raw);
+    s.carry = s.stage + TILE;
+    s.w32 = reinterpret_cast<uint32_t*>(s.carry + (size_t)nbins * CW);
+    s.hb = nbins / 2;
+    s.info = reinterpret_cast<u32x4_t*>(s.w32 + (size_t)W * s.hb);
+    s.segown = reinterpret_cast<uint16_t*>(s.info + nbins);
+    s.scr = reinterpret_cast<uint32_t*>(s.segown + ((TILE / SEG + 2 * nbins + 7) & ~7u));
+    s.lane = lane_id();
+    s.wid = threadIdx.x >> 6;
+    s.t2 = threadIdx.x;
+    s.owner = s.t2 < s.hb;
+    s.pos[0] = s.pos[1] = s.kc[0] = s.kc[1] = 0;
+    if (s.owner) {
+#pragma unroll
+        for (int h = 0; h < 2; h++)
+            s.pos[h] = (uint32_t)(starts[2 * s.t2 + h] +
+                                  counts[(uint64_t)(2 * s.t2 + h) * nwg + blockIdx.x]);
+    }
+    for (uint32_t q = threadIdx.x; q < W * s.hb; q += THREADS) s.w32[q] = 0;
+    const uint64_t beg = (uint64_t)blockIdx.x * chunk;
+    s.end = min(beg + chunk, n);
+    s.wbase = s.wid * 64 * ITEMS;
+    Tup a[ITEMS], b[ITEMS], c[ITEMS];
+    s.load(a, beg);
+    s.load(b, beg + TILE);
+    __builtin_amdgcn_s_waitcnt(vmcnt_imm(ITEMS));  // the first tile
+    __syncthreads();
+    for (uint64_t base = beg;;) {
+        s.tile(a, c, base);
+        if ((base += TILE) >= s.end) break;
+        s.tile(b, a, base);
+        if ((base += TILE) >= s.end) break;
+        s.tile(c, b, base);
+        if ((base += TILE) >= s.end) break;
+    }
+    // the partial last segment of every region
+    if (s.owner) {
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const uint32_t d = 2 * s.t2 + h;
+            for (uint32_t e = 0; e < s.kc[h]; e++) out[s.pos[h] + e] = s.carry[d * CW + e];
+        }
+    }
+}
+
+// Histogram of the stable write-combining partition with two register tiles
+// alternating (the next tile's loads fly while this one is counted).  Same
+// counts as k_hist_c.
+template <int THREADS, int ITEMS, class Digit, bool NT>
+__global__ void __launch_bounds__(THREADS)
+k_hist_p(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_arg,
+         uint32_t nbins, uint32_t* __restrict__ counts, uint32_t nwg) {
+    const auto dig = dig_arg.load();
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_hp[];
+    for (uint32_t d = threadIdx.x; d < nbins; d += THREADS) lds_hp[d] = 0;
+    __syncthreads();
+    const uint64_t beg = (uint64_t)blockIdx.x * chunk;
+    const uint64_t end = min(beg + chunk, n);
+    constexpr int TILE = THREADS * ITEMS;
+    Tup a[ITEMS], b[ITEMS];
+    auto load = [&](Tup (&v)[ITEMS], uint64_t base) {
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint64_t i = base + (uint64_t)j * THREADS + threadIdx.x;
+            const uint64_t c = i < end ? i : end - 1;
+            v[j] = NT ? ld_nt(in + c) : in[c];
+        }
+    };
+    auto count = [&](const Tup (&v)[ITEMS], uint64_t base) {
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint64_t i = base + (uint64_t)j * THREADS + threadIdx.x;
+            if (i < end) atomicAdd(&lds_hp[dig(v[j])], 1u);
+        }
+    };
+    if (beg < end) load(a, beg);
+    for (uint64_t base = beg; base < end;) {
+        load(b, base + TILE);
+        count(a, base);
+        if ((base += TILE) >= end) break;
+        load(a, base + TILE);
+        count(b, base);
+        base += TILE;
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < nbins; d += THREADS)
+        counts[(uint64_t)d * nwg + blockIdx.x] = lds_hp[d];
+}
+
+// 8-byte tuples: k_hist_p with 16-byte loads (two tuples per lane and load,
+// non-temporal), for a 16-byte aligned input and even chunks; the odd last
+// tuple of the input is counted by thread 0 of the last workgroup.
+typedef unsigned long long HvVec __attribute__((ext_vector_type(2)));
+template <int THREADS, int VITEMS, class Digit>
+__global__ void __launch_bounds__(THREADS)
+k_hist_v(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_arg,
+         uint32_t nbins, uint32_t* __restrict__ counts, uint32_t nwg) {
+    static_assert(sizeof(Tup) == 8, "8-byte tuples");
+    const auto dig = dig_arg.load();
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_hv[];
+    for (uint32_t d = threadIdx.x; d < nbins; d += THREADS) lds_hv[d] = 0;
+    __syncthreads();
+    const uint64_t beg = (uint64_t)blockIdx.x * chunk;
+    const uint64_t end = min(beg + chunk, n);
+    const HvVec* __restrict__ vin = reinterpret_cast<const HvVec*>(in);
+    const uint64_t vb = beg / 2, ve = end / 2;  // whole pairs of the chunk
+    constexpr int TILE = THREADS * VITEMS;
+    HvVec a[VITEMS], b[VITEMS];
+    auto load = [&](HvVec (&v)[VITEMS], uint64_t base) {
+#pragma unroll
+        for (int j = 0; j < VITEMS; j++) {
+            const uint64_t i = base + (uint64_t)j * THREADS + threadIdx.x;
+            v[j] = __builtin_nontemporal_load(vin + (i < ve ? i : ve - 1));
+        }
+    };
+    auto count = [&](const HvVec (&v)[VITEMS], uint64_t base) {
+#pragma unroll
+        for (int j = 0; j < VITEMS; j++) {
+            const uint64_t i = base + (uint64_t)j * THREADS + threadIdx.x;
+            if (i < ve) {
+                atomicAdd(&lds_hv[dig((Tup)v[j].x)], 1u);
+                atomicAdd(&lds_hv[dig((Tup)v[j].y)], 1u);
+            }
+        }
+    };
+    if (vb < ve) load(a, vb);
+    for (uint64_t base = vb; base < ve;) {
+        load(b, base + TILE);
+        count(a, base);
+        if ((base += TILE) >= ve) break;
+        load(a, base + TILE);
+        count(b, base);
+        base += TILE;
+    }
+    if (threadIdx.x == 0 && (end & 1) && end > beg) atomicAdd(&lds_hv[dig(in[end - 1])], 1u);
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < nbins; d += THREADS)
+        counts[(uint64_t)d * nwg + blockIdx.x] = lds_hv[d];
+}
+
 // Histogram of the stable write-combining partition: counts[d][wg] of each
 // workgroup's chunk (the scatter's chunking).  Loads are unconditional
 // (clamped to the chunk) so that every load of a tile is in flight at once.
@@ -1456,6 +1764,22 @@ static bool atomic_ranks() {
     return v != 0;
 }
 
+// software-pipelined loads (k_hist_p: bit 0, k_scatter_swp: bit 1, k_hist_v's
+// 16-byte loads for 8-byte tuples: bit 2, non-temporal loads and stores in
+// k_scatter_swp and k_hist_p: bit 3); SMJ_SWA_PIPE selects, default 15 (0 =
+// the round-2 kernels k_hist_c + k_scatter_swa).  bench_partitioning 2^27 x 10
+// bits on MI355X, interleaved (tools/ab_swa.sh): 8 B 0.90 -> 0.82 ms (k_hist
+// 0.236 -> 0.160: 16-byte loads), 16 B 1.58 -> 1.49 ms (k_hist 0.424 -> 0.317:
+// non-temporal loads); the scatter itself gains 2-3 %
+static int swa_pipelined() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("SMJ_SWA_PIPE");
+        v = e ? atoi(e) : 15;
+    }
+    return v;
+}
+
 // histogram + scan + k_scatter_swa, one workgroup per CU (1 <= dbits <= 10)
 template <class Digit>
 static void stable_partition_swa(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
@@ -1476,8 +1800,27 @@ static void stable_partition_swa(Workspace* ws, const Tup* in, uint64_t n, Tup* 
     uint64_t* totals = (uint64_t*)ws->scratch("pt_totals", (size_t)nbins * 8);
     {
         TraceScope ts(ws, "k_hist", st);
-        hipLaunchKernelGGL((k_hist_c<512, 16, Digit>), dim3(nwg), dim3(512),
-                           nbins * sizeof(uint32_t), st, in, n, chunk, dig, nbins, counts, nwg);
+        bool vec = false;
+        if constexpr (sizeof(Tup) == 8) {
+            vec = (swa_pipelined() & 4) && ((uintptr_t)in & 15) == 0 && (chunk & 1) == 0;
+            if (vec)
+                hipLaunchKernelGGL((k_hist_v<512, 8, Digit>), dim3(nwg), dim3(512),
+                                   nbins * sizeof(uint32_t), st, in, n, chunk, dig, nbins,
+                                   counts, nwg);
+        }
+        if (vec) {
+        } else if (swa_pipelined() & 8)
+            hipLaunchKernelGGL((k_hist_p<512, 16, Digit, true>), dim3(nwg), dim3(512),
+                               nbins * sizeof(uint32_t), st, in, n, chunk, dig, nbins, counts,
+                               nwg);
+        else if (swa_pipelined() & 1)
+            hipLaunchKernelGGL((k_hist_p<512, 16, Digit, false>), dim3(nwg), dim3(512),
+                               nbins * sizeof(uint32_t), st, in, n, chunk, dig, nbins, counts,
+                               nwg);
+        else
+            hipLaunchKernelGGL((k_hist_c<512, 16, Digit>), dim3(nwg), dim3(512),
+                               nbins * sizeof(uint32_t), st, in, n, chunk, dig, nbins, counts,
+                               nwg);
     }
     {
         TraceScope ts(ws, "k_scan", st);
@@ -1490,12 +1833,25 @@ static void stable_partition_swa(Workspace* ws, const Tup* in, uint64_t n, Tup* 
     if (!attr) {
         SMJ_CHECK(hipFuncSetAttribute((const void*)k_scatter_swa<THREADS, ITEMS, Digit>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        SMJ_CHECK(hipFuncSetAttribute((const void*)k_scatter_swp<THREADS, ITEMS, Digit, false>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        SMJ_CHECK(hipFuncSetAttribute((const void*)k_scatter_swp<THREADS, ITEMS, Digit, true>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr = true;
     }
     TraceScope ts(ws, "k_scatter", st);
-    hipLaunchKernelGGL((k_scatter_swa<THREADS, ITEMS, Digit>), dim3(nwg), dim3(THREADS),
-                       G::lds_bytes(nbins), st, in, n, chunk, dig, nbins, counts, nwg,
-                       starts_dev, out);
+    if (swa_pipelined() & 8)
+        hipLaunchKernelGGL((k_scatter_swp<THREADS, ITEMS, Digit, true>), dim3(nwg), dim3(THREADS),
+                           G::lds_bytes(nbins), st, in, n, chunk, dig, nbins, counts, nwg,
+                           starts_dev, out);
+    else if (swa_pipelined() & 2)
+        hipLaunchKernelGGL((k_scatter_swp<THREADS, ITEMS, Digit, false>), dim3(nwg), dim3(THREADS),
+                           G::lds_bytes(nbins), st, in, n, chunk, dig, nbins, counts, nwg,
+                           starts_dev, out);
+    else
+        hipLaunchKernelGGL((k_scatter_swa<THREADS, ITEMS, Digit>), dim3(nwg), dim3(THREADS),
+                           G::lds_bytes(nbins), st, in, n, chunk, dig, nbins, counts, nwg,
+                           starts_dev, out);
     SMJ_CHECK(hipGetLastError());
 }
 
