@@ -684,8 +684,33 @@ constexpr int vmcnt_imm(int n) { return (n & 15) | ((n >> 4) << 14) | 0x0f70; }
 // this tile (the next-but-one) has landed, i.e. the next tile and the previous
 // tile's stores.  The loads thus fly under a whole tile of LDS work instead of
 // the stage phase alone.  Same ranks, layout and results as k_scatter_swa.
+#ifdef SMJ_SWP_PROF
+// lab build only: per-phase cycle counts of k_scatter_swp, summed over the
+// workgroups' thread 0 (read by smj_swp_prof)
+__device__ unsigned long long g_swp_prof[16];
+#define SWP_MARK(k)                                            \
+    do {                                                       \
+        const uint64_t t_ = __builtin_readcyclecounter();      \
+        prof[k] += t_ - tprev;                                 \
+        tprev = t_;                                            \
+    } while (0)
+#else
+#define SWP_MARK(k) \
+    do {            \
+    } while (0)
+#endif
+
 template <int THREADS, int ITEMS, class DigitL, bool NT>
 struct SwpTile {
+    // info[d][3] = segment start (12 bits) | carry size (3) | emission + carry (17)
+    static_assert(SwaGeom<THREADS, ITEMS>::TILE / SwaGeom<THREADS, ITEMS>::SEG + 2 * 1024 <= 4096,
+                  "segment numbers fit 12 bits");
+    static_assert(SwaGeom<THREADS, ITEMS>::CW <= 7, "carry size fits 3 bits");
+    static_assert(SwaGeom<THREADS, ITEMS>::TILE + 8 < (1 << 17), "T fits 17 bits");
+#ifdef SMJ_SWP_PROF
+    uint64_t prof[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t tprev = 0;
+#endif
     typedef SwaGeom<THREADS, ITEMS> G;
     static constexpr int W = G::W;
     static constexpr int TILE = G::TILE;
@@ -706,6 +731,29 @@ struct SwpTile {
     uint64_t end;
     uint32_t pos[2], kc[2];
 
+    // exclusive scan over the workgroup (v < 2^32 in total): wave scan by
+    // shuffles, wave totals through LDS, one barrier (the scratch is next
+    // written a tile later, after several barriers)
+    __device__ __forceinline__ uint32_t scan(uint32_t v, uint32_t* total) const {
+        uint32_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) scr[wid] = x;
+        __syncthreads();
+        uint32_t before = 0, all = 0;
+#pragma unroll
+        for (int w = 0; w < W; w++) {
+            const uint32_t t = scr[w];
+            before += w < wid ? t : 0u;
+            all += t;
+        }
+        *total = all;
+        return before + x - v;
+    }
+
     __device__ __forceinline__ void load(Tup (&v)[ITEMS], uint64_t base) const {
 #pragma unroll
         for (int j = 0; j < ITEMS; j++) {
@@ -717,6 +765,9 @@ struct SwpTile {
 
     __device__ __forceinline__ void tile(const Tup (&v)[ITEMS], Tup (&pre)[ITEMS],
                                          uint64_t base) {
+#ifdef SMJ_SWP_PROF
+        tprev = __builtin_readcyclecounter();
+#endif
         const uint32_t tcount = (uint32_t)min((uint64_t)TILE, end - base);
         uint32_t dg[ITEMS], rk[ITEMS];
 #pragma unroll
@@ -729,7 +780,9 @@ struct SwpTile {
             if (valid) old = atomicAdd(&w32[wid * hb + (d >> 1)], 1u << sh);
             rk[j] = (old >> sh) & 0xffffu;
         }
+        SWP_MARK(0);
         __syncthreads();
+        SWP_MARK(1);
         uint32_t cw[W];
         uint32_t c[2] = {0, 0}, E[2] = {0, 0}, ns[2] = {0, 0};
         if (owner) {
@@ -748,8 +801,7 @@ struct SwpTile {
             }
         }
         uint32_t tot;
-        const uint32_t ex =
-            block_exclusive_scan((c[0] + c[1]) | ((ns[0] + ns[1]) << 16), scr, &tot);
+        const uint32_t ex = scan((c[0] + c[1]) | ((ns[0] + ns[1]) << 16), &tot);
         const uint32_t nsegT = tot >> 16;
         uint32_t ts[2] = {0, 0};
         if (owner) {
@@ -771,14 +823,16 @@ struct SwpTile {
                 I[0] = pos[h];
                 I[1] = E[h];
                 I[2] = ts[h];
-                I[3] = sp[h] | (kc[h] << 16);
+                I[3] = sp[h] | (kc[h] << 12) | ((kc[h] + c[h]) << 15);
                 info[d] = I;
                 for (uint32_t k = 0; k < ns[h]; k++) segown[sp[h] + k] = (uint16_t)d;
             }
         }
+        SWP_MARK(2);
         // the next-but-one tile (its registers held the previous tile)
         load(pre, base + 2 * (uint64_t)TILE);
         __syncthreads();
+        SWP_MARK(3);
 #pragma unroll
         for (int j = 0; j < ITEMS; j++)
             if (dg[j] != 0xffffffffu) {
@@ -787,6 +841,7 @@ struct SwpTile {
                 stage[wo + rk[j]] = v[j];
             }
         __syncthreads();
+        SWP_MARK(4);
         if (owner) {
 #pragma unroll
             for (int w = 0; w < W; w++) w32[w * hb + t2] = 0;
@@ -794,15 +849,16 @@ struct SwpTile {
         // the next tile and the previous tile's stores have landed; the
         // next-but-one tile's ITEMS loads stay in flight
         __builtin_amdgcn_s_waitcnt(vmcnt_imm(ITEMS));
+        SWP_MARK(5);
         for (uint32_t q = threadIdx.x; q < nsegT * SEG; q += THREADS) {
             const uint32_t sg = q / SEG;
             const uint32_t d = segown[sg];
             const u32x4_t I = info[d];
             const uint32_t p = I[0];
-            const uint32_t addr = (p / SEG + (sg - (I[3] & 0xffffu))) * SEG + q % SEG;
+            const uint32_t addr = (p / SEG + (sg - (I[3] & 0xfffu))) * SEG + q % SEG;
             if (addr >= p && addr < p + I[1]) {
                 const uint32_t e = addr - p;
-                const uint32_t k = I[3] >> 16;
+                const uint32_t k = (I[3] >> 12) & 7u;
                 const Tup x = e < k ? carry[d * CW + e] : stage[I[2] + e - k];
                 if (NT)
                     st_stream(out + addr, x);
@@ -810,19 +866,35 @@ struct SwpTile {
                     out[addr] = x;
             }
         }
+        SWP_MARK(6);
         __syncthreads();
+        SWP_MARK(7);
+        // ---- the owner's leftovers (< SEG) become the carry.  An emission
+        // (E > 0) ends on a segment boundary past the old carry (E > kc), so
+        // the new carry comes from the stage alone; without one the old carry
+        // stays in place and the tile's elements follow it.  All stage reads
+        // are issued before the carry writes (no read-after-write chain).
         if (owner) {
 #pragma unroll
             for (int h = 0; h < 2; h++) {
                 const uint32_t d = 2 * t2 + h;
                 const uint32_t T = kc[h] + c[h];
-                for (uint32_t e = E[h]; e < T; e++)
-                    carry[d * CW + (e - E[h])] =
-                        e < kc[h] ? carry[d * CW + e] : stage[ts[h] + e - kc[h]];
+                Tup x[CW];
+#pragma unroll
+                for (uint32_t j = 0; j < CW; j++) {
+                    const uint32_t e = E[h] + j;
+                    x[j] = stage[e >= kc[h] && e < T ? ts[h] + e - kc[h] : 0u];
+                }
+#pragma unroll
+                for (uint32_t j = 0; j < CW; j++) {
+                    const uint32_t e = E[h] + j;
+                    if (e >= kc[h] && e < T) carry[d * CW + j] = x[j];
+                }
                 pos[h] += E[h];
                 kc[h] = T - E[h];
             }
         }
+        SWP_MARK(8);
     }
 };
 
@@ -876,7 +948,9 @@ k_scatter_swp(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
         s.tile(c, b, base);
         if ((base += TILE) >= s.end) break;
     }
-    // the partial last segment of every region
+    // the partial last segment of every region (carry slots are written by
+    // every thread of the last tile's carry phase)
+    __syncthreads();
     if (s.owner) {
 #pragma unroll
         for (int h = 0; h < 2; h++) {
@@ -884,7 +958,20 @@ k_scatter_swp(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
             for (uint32_t e = 0; e < s.kc[h]; e++) out[s.pos[h] + e] = s.carry[d * CW + e];
         }
     }
+#ifdef SMJ_SWP_PROF
+    if (threadIdx.x == 0)
+        for (int k = 0; k < 9; k++) atomicAdd(&g_swp_prof[k], (unsigned long long)s.prof[k]);
+#endif
 }
+
+#ifdef SMJ_SWP_PROF
+extern "C" void smj_swp_prof(unsigned long long* out) {
+    SMJ_CHECK(hipDeviceSynchronize());
+    SMJ_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_swp_prof), 16 * 8));
+    static const unsigned long long z[16] = {0};
+    SMJ_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_swp_prof), z, 16 * 8));
+}
+#endif
 
 // Histogram of the stable write-combining partition with two register tiles
 // alternating (the next tile's loads fly while this one is counted).  Same
