@@ -53,4 +53,8 @@ done
 buildxx bench_sort 8 "$S/bench/sortbench.c" "$T/testutil.c" $GEN
 # avxsort only exists for 8-byte tuples (the reference forces scalar for 16 B)
 build check_avxsort 8 "$T/check_avxsort.c" "$T/testutil.c"
+# check_merge: 2-way, multiway (fan-in 2^2..2^11) and the AVX kernel tests,
+# whose avxsort_core.h kernels map onto the device merge/sort
+# (include/compat/avxsort_core.h)
+build check_merge 8 "$T/check_merge.c" "$T/testutil.c"
 echo "[build_dropin] built $(ls "$OUT" | wc -l) binaries in oracle/_ref/dropin"

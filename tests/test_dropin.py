@@ -34,7 +34,7 @@ def run(args, timeout=300):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["check_partitioning8", "check_partitioning16",
                                   "check_scalarsort8", "check_scalarsort16",
-                                  "check_avxsort8"])
+                                  "check_avxsort8", "check_merge8"])
 def test_reference_check_suite(name):
     r = run([binary(name)])
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
