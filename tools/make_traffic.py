@@ -18,7 +18,8 @@ from collections import defaultdict
 
 ALIAS = {"k_scatter_res": "k_scatter", "k_scatter_wc": "k_scatter",
          "k_scatter_u": "k_scatter", "k_sample_hist": "k_sample",
-         "k_scatter_swa": "k_scatter", "k_hist_c": "k_hist"}
+         "k_scatter_swa": "k_scatter", "k_hist_c": "k_hist",
+         "k_scatter_swp": "k_scatter", "k_hist_p": "k_hist", "k_hist_v": "k_hist"}
 
 
 def short(name):
