@@ -1515,7 +1515,10 @@ struct ScatterGeom {
     }
 };
 
-template <int THREADS, int ITEMS, class Digit, class Pack>
+// VEC (8-byte tuples, ITEMS even): item pair (2p, 2p+1) of a thread is one
+// 16-byte load of two adjacent tuples -- the order inside a partition is free
+// here, so the pairing needs no transpose
+template <int THREADS, int ITEMS, class Digit, class Pack, bool VEC>
 __global__ void __launch_bounds__(THREADS)
 k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_arg,
               uint32_t nbins, unsigned long long* __restrict__ cursor_all,
@@ -1558,12 +1561,38 @@ k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
     const uint64_t my_cap = own ? cap_end[(size_t)d0 * kShards] : 0;
     uint32_t my_kc = 0;
 
-    Tup v[ITEMS], nv[ITEMS];
+    static_assert(!VEC || (sizeof(Tup) == 8 && ITEMS % 2 == 0), "VEC: 8-byte tuples, ITEMS even");
+    // tile position of item j (VEC: pairs of adjacent tuples per thread)
+    auto item_pos = [](int j) -> uint32_t {
+        return VEC ? 2u * ((uint32_t)(j / 2) * THREADS + threadIdx.x) + (uint32_t)(j & 1)
+                   : (uint32_t)j * THREADS + threadIdx.x;
+    };
+    typedef unsigned long long V2 __attribute__((ext_vector_type(2)));
+    // clamped loads of the tile at b0 (VEC: n and the chunks are even)
+    auto load_tile = [&](Tup (&x)[ITEMS], uint64_t b0) {
+#ifndef KEY_8B
+        if constexpr (VEC) {
+            const V2* __restrict__ vin = reinterpret_cast<const V2*>(in);
+            const uint64_t vl = end / 2 - 1;
 #pragma unroll
-    for (int j = 0; j < ITEMS; j++) {
-        const uint64_t i = beg + (uint64_t)j * THREADS + threadIdx.x;
-        if (i < end) v[j] = ld_stream(in + i);
-    }
+            for (int p = 0; p < ITEMS / 2; p++) {
+                const uint64_t vi = b0 / 2 + (uint64_t)p * THREADS + threadIdx.x;
+                const V2 y = vin[vi < vl ? vi : vl];
+                x[2 * p] = (Tup)y.x;
+                x[2 * p + 1] = (Tup)y.y;
+            }
+        } else
+#endif
+        {
+#pragma unroll
+            for (int j = 0; j < ITEMS; j++) {
+                const uint64_t i = b0 + (uint64_t)j * THREADS + threadIdx.x;
+                x[j] = ld_stream(in + (i < end ? i : end - 1));
+            }
+        }
+    };
+    Tup v[ITEMS], nv[ITEMS];
+    if (beg < end) load_tile(v, beg);
     __syncthreads();
     for (uint64_t base = beg; base < end; base += TILE) {
         const uint32_t tcount =
@@ -1577,7 +1606,7 @@ k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
         uint32_t dg[ITEMS];
 #pragma unroll
         for (int j = 0; j < ITEMS; j++) {
-            const uint32_t li = j * THREADS + threadIdx.x;
+            const uint32_t li = item_pos(j);
             dg[j] = li < tcount ? dig(v[j]) : 0xffffffffu;
             if (dg[j] != 0xffffffffu) atomicAdd(&tfill[dg[j]], 1u);
         }
@@ -1603,11 +1632,7 @@ k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
         }
         // unconditional (clamped) loads: a fixed count in flight lets the
         // reservation results be waited for with vmcnt(ITEMS)
-#pragma unroll
-        for (int j = 0; j < ITEMS; j++) {
-            const uint64_t i = nb + (uint64_t)j * THREADS + threadIdx.x;
-            nv[j] = ld_stream(in + (i < end ? i : end - 1));
-        }
+        load_tile(nv, nb);
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < ITEMS; j++)
@@ -2136,7 +2161,10 @@ void plan_partition_packed(Workspace* ws, const Tup* in, uint64_t n, uint64_t* o
 #define SMJ_SC_ITEMS16P 8  // 16-byte tuples staged as packed 8-byte words
 #endif
 #ifndef SMJ_SC_ITEMS8
-#define SMJ_SC_ITEMS8 13
+// even, for the 16-byte pair loads (k_scatter_res VEC): 128M x 128M 8 B join
+// 3.20-3.24 -> 3.04-3.07 ms against 13 items of 8-byte loads (interleaved,
+// tools/ab_scvec.sh; 14 items with pair loads 3.12-3.17)
+#define SMJ_SC_ITEMS8 12
 #endif
 #ifndef SMJ_SC_WG_PER_CU
 #define SMJ_SC_WG_PER_CU 1
@@ -2152,6 +2180,16 @@ uint64_t sampled_capacity(uint64_t n, uint32_t dbits) {
     const uint64_t SEG = kSegBytes / 8;
     return n + n / 8 + 2 * kSampleStride +
            ((uint64_t)1 << dbits) * kShards * (kRegionSlack + 2 * SEG);
+}
+
+// 16-byte loads of tuple pairs in the 8-byte scatter (SMJ_SC_VEC=0: 8-byte loads)
+static bool sc_vec() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("SMJ_SC_VEC");
+        v = e ? atoi(e) : 1;
+    }
+    return v != 0;
 }
 
 template <int ITEMS, class Pack>
@@ -2170,21 +2208,35 @@ static bool sampled_scatter_t(Workspace* ws, const Tup* in, uint64_t n, void* ou
     const uint64_t chunk = tiles_per_wg * TILE;
     nwg = (uint32_t)((ntiles + tiles_per_wg - 1) / tiles_per_wg);
     static bool attr = false;
+    constexpr bool VEC_OK = sizeof(Tup) == 8 && ITEMS % 2 == 0;
     if (!attr) {
         SMJ_CHECK(hipFuncSetAttribute(
-            (const void*)k_scatter_res<THREADS, ITEMS, PlanDigit1, Pack>,
+            (const void*)k_scatter_res<THREADS, ITEMS, PlanDigit1, Pack, false>,
             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        if constexpr (VEC_OK)
+            SMJ_CHECK(hipFuncSetAttribute(
+                (const void*)k_scatter_res<THREADS, ITEMS, PlanDigit1, Pack, true>,
+                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr = true;
     }
     TraceScope ts(ws, "k_scatter", st);
-    hipLaunchKernelGGL((k_scatter_res<THREADS, ITEMS, PlanDigit1, Pack>), dim3(nwg),
-                       dim3(THREADS), lds, st, in, n, chunk, dig, nbins, cursor,
-                       cap_end, (typename Pack::OutT*)out, pk, bad_flag);
+    bool vec = false;
+    if constexpr (VEC_OK) {
+        vec = sc_vec() && n % 2 == 0 && chunk % 2 == 0 && ((uintptr_t)in & 15) == 0;
+        if (vec)
+            hipLaunchKernelGGL((k_scatter_res<THREADS, ITEMS, PlanDigit1, Pack, true>), dim3(nwg),
+                               dim3(THREADS), lds, st, in, n, chunk, dig, nbins, cursor,
+                               cap_end, (typename Pack::OutT*)out, pk, bad_flag);
+    }
+    if (!vec)
+        hipLaunchKernelGGL((k_scatter_res<THREADS, ITEMS, PlanDigit1, Pack, false>), dim3(nwg),
+                           dim3(THREADS), lds, st, in, n, chunk, dig, nbins, cursor,
+                           cap_end, (typename Pack::OutT*)out, pk, bad_flag);
     return true;
 }
 
 // The LDS stage holds OutT and the carry 64 bytes per partition: the widest
-// tile that fits (8-byte tuples: 13 x 1024 at 512 partitions, 8 x 1024 at
+// tile that fits (8-byte tuples: 12 x 1024 up to 512 partitions, 8 x 1024 at
 // 1024; packed words 8 / 4 x 1024; 16-byte tuples 4 x 1024), measured best.
 template <class Pack>
 static void sampled_scatter(Workspace* ws, const Tup* in, uint64_t n, void* out,
