@@ -1577,7 +1577,11 @@ k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
 #pragma unroll
             for (int p = 0; p < ITEMS / 2; p++) {
                 const uint64_t vi = b0 / 2 + (uint64_t)p * THREADS + threadIdx.x;
+#if SMJ_NT_LOADS
+                const V2 y = __builtin_nontemporal_load(vin + (vi < vl ? vi : vl));
+#else
                 const V2 y = vin[vi < vl ? vi : vl];
+#endif
                 x[2 * p] = (Tup)y.x;
                 x[2 * p + 1] = (Tup)y.y;
             }
