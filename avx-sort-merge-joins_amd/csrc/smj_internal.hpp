@@ -59,6 +59,10 @@ struct PlanDigit1 {
 struct Workspace {
     std::map<std::string, std::pair<void*, size_t>> bufs;
     std::map<std::string, std::pair<void*, size_t>> pinned;
+    // the k-way merge's run table as last uploaded, and where (a repeated
+    // merge of the same runs skips the upload)
+    std::vector<unsigned char> km_last;
+    const void* km_last_dev = nullptr;
     hipEvent_t ev[8] = {};
     bool ev_init = false;
     float phase_ms[5] = {0, 0, 0, 0, 0};
