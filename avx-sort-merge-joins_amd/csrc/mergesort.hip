@@ -579,7 +579,7 @@ k_km_merge(const KmRun* __restrict__ runs, uint32_t k, uint32_t D,
     const uint32_t total = tot2 & 0x1fffffu;
     if (total == 0) return;  // uniform: an empty bucket
     if (total > KM_CAP) {    // a bucket larger than LDS: the caller merges another way
-        if (tid == 0) atomicOr(&flag[0], 1u);
+        if (tid == 0) flag[0] = 1u;  // host-mapped: plain stores, every writer stores 1
         return;
     }
     if (len) {
@@ -704,7 +704,7 @@ k_km_merge(const KmRun* __restrict__ runs, uint32_t k, uint32_t D,
             for (uint32_t i = tid + 1; i < total; i += KM_THREADS)
                 ok &= !tup_less(buf[i], buf[i - 1]);
             if (__syncthreads_or(!ok)) {
-                if (tid == 0) atomicOr(&flag[1], 1u);
+                if (tid == 0) flag[1] = 1u;
                 return;
             }
         }
@@ -753,14 +753,19 @@ static bool multiway_merge_buckets(Workspace* ws, const Tup* const* runs, const 
         hipLaunchKernelGGL(k_km_bounds, dim3((uint32_t)((nb + KM_THREADS - 1) / KM_THREADS)),
                            dim3(KM_THREADS), 0, st, dr, k, D, mm, off);
     }
+    // the flags live in pinned host memory the kernel writes directly, so
+    // the synchronisation needs no copy behind the kernels
+    volatile unsigned int* hflag = (volatile unsigned int*)ws->host_pinned("km_flag", 16);
+    hflag[0] = 0;
+    hflag[1] = 0;
+    unsigned int* dflag = nullptr;
+    SMJ_CHECK(hipHostGetDevicePointer((void**)&dflag, (void*)hflag, 0));
     {
         TraceScope ts(ws, "k_km_merge", st);
         hipLaunchKernelGGL(k_km_merge, dim3(B), dim3(KM_THREADS), 0, st, dr, k, D, mm, off,
-                           flag, out);
+                           dflag, out);
     }
     SMJ_CHECK(hipGetLastError());
-    unsigned int* hflag = (unsigned int*)ws->host_pinned("km_flag", 16);
-    SMJ_CHECK(hipMemcpyAsync(hflag, flag, 8, hipMemcpyDeviceToHost, st));
     SMJ_CHECK(hipStreamSynchronize(st));
     return hflag[0] == 0 && hflag[1] == 0;
 }
