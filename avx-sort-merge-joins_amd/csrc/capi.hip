@@ -160,11 +160,13 @@ static bool use_sampled() {
 }
 
 // exact key range [min, max] of the relations (one read pass); min > max
-// when they are empty.  16-byte non-temporal loads, KR_U of them in flight per
-// thread (the scalar 8-byte loads of the first version reached 3.0 TB/s on
-// 2^27 x 8 B), one pair of atomics per workgroup.
+// when they are empty.  16-byte non-temporal loads over one contiguous chunk
+// per workgroup, two register tiles of KR_U alternating (the scalar 8-byte
+// loads of the first version reached 3.0 TB/s on 2^27 x 8 B, the grid-stride
+// 16-byte form 5.3 TB/s), one pair of atomics per workgroup.
 typedef unsigned long long KrVec __attribute__((ext_vector_type(2)));
 constexpr int KR_U = 8;
+constexpr int KR_THREADS = 512;
 
 __device__ __forceinline__ void kr_acc(uint64_t u, uint64_t& lo, uint64_t& hi) {
     lo = u < lo ? u : lo;
@@ -180,30 +182,54 @@ __device__ __forceinline__ void kr_vec(const KrVec& v, uint64_t& lo, uint64_t& h
 #endif
 }
 
-__global__ void __launch_bounds__(256)
+// One contiguous chunk of 16-byte vectors per workgroup, two register tiles
+// alternating (the next tile's loads fly while this one is reduced): the
+// stable histogram's pattern (k_hist_v), which streams at ~6.5 TB/s.
+__device__ __forceinline__ void kr_chunk(const KrVec* __restrict__ v, uint64_t nv,
+                                         uint64_t& lo, uint64_t& hi) {
+    const uint64_t per = (nv + gridDim.x - 1) / gridDim.x;
+    const uint64_t beg = (uint64_t)blockIdx.x * per;
+    const uint64_t end = beg + per < nv ? beg + per : nv;
+    constexpr int TILE = KR_THREADS * KR_U;
+    KrVec a[KR_U], b[KR_U];
+    auto load = [&](KrVec (&x)[KR_U], uint64_t base) {
+#pragma unroll
+        for (int u = 0; u < KR_U; u++) {
+            const uint64_t i = base + (uint64_t)u * KR_THREADS + threadIdx.x;
+            x[u] = __builtin_nontemporal_load(v + (i < end ? i : end - 1));
+        }
+    };
+    auto reduce = [&](const KrVec (&x)[KR_U], uint64_t base) {
+#pragma unroll
+        for (int u = 0; u < KR_U; u++)
+            if (base + (uint64_t)u * KR_THREADS + threadIdx.x < end) kr_vec(x[u], lo, hi);
+    };
+    if (beg >= end) return;
+    load(a, beg);
+    for (uint64_t base = beg; base < end;) {
+        load(b, base + TILE);
+        reduce(a, base);
+        if ((base += TILE) >= end) break;
+        load(a, base + TILE);
+        reduce(b, base);
+        base += TILE;
+    }
+}
+
+__global__ void __launch_bounds__(KR_THREADS)
 k_keyrange(const Tup* __restrict__ r0, uint64_t n0, const Tup* __restrict__ r1, uint64_t n1,
            unsigned long long* __restrict__ mm) {
-    __shared__ unsigned long long sl[4], sh[4];
+    __shared__ unsigned long long sl[KR_THREADS / 64], sh[KR_THREADS / 64];
     uint64_t lo = ~0ull, hi = 0;  // key_u order
-    const uint64_t gt = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    const uint64_t G = (uint64_t)gridDim.x * 256;
+    const uint64_t gt = (uint64_t)blockIdx.x * KR_THREADS + threadIdx.x;
+    const uint64_t G = (uint64_t)gridDim.x * KR_THREADS;
     for (int rel = 0; rel < 2; rel++) {
         const Tup* p = rel ? r1 : r0;
         const uint64_t n = rel ? n1 : n0;
         if (!p || n == 0) continue;
         if (((uintptr_t)p & 15) == 0) {
-            const KrVec* v = reinterpret_cast<const KrVec*>(p);
             const uint64_t nv = n * sizeof(Tup) / 16;
-            for (uint64_t i0 = gt; i0 < nv; i0 += G * KR_U) {
-                KrVec x[KR_U];
-#pragma unroll
-                for (int u = 0; u < KR_U; u++) {
-                    const uint64_t i = i0 + u * G;
-                    x[u] = __builtin_nontemporal_load(v + (i < nv ? i : nv - 1));
-                }
-#pragma unroll
-                for (int u = 0; u < KR_U; u++) kr_vec(x[u], lo, hi);
-            }
+            kr_chunk(reinterpret_cast<const KrVec*>(p), nv, lo, hi);
             // 8-byte tuples: an odd last one
             if (gt == 0 && nv * 16 / sizeof(Tup) < n) kr_acc(key_u(tup_key(p[n - 1])), lo, hi);
         } else {
@@ -222,7 +248,7 @@ k_keyrange(const Tup* __restrict__ r0, uint64_t n0, const Tup* __restrict__ r1, 
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        for (int w = 1; w < 4; w++) {
+        for (int w = 1; w < KR_THREADS / 64; w++) {
             lo = sl[w] < lo ? sl[w] : lo;
             hi = sh[w] > hi ? sh[w] : hi;
         }
@@ -238,11 +264,11 @@ static bool key_range(Workspace* ws, const Tup* const* rels, const uint64_t* ns,
     const unsigned long long init[2] = {~0ull, 0ull};
     SMJ_CHECK(hipMemcpyAsync(mm, init, 16, hipMemcpyHostToDevice, st));
     const uint64_t n = ns[0] + (nrel > 1 ? ns[1] : 0);
-    // 4 workgroups per CU, each thread KR_U vectors per round
-    uint64_t g = (n * sizeof(Tup) / 16 + 256 * KR_U - 1) / (256 * KR_U);
-    if (g > 1024) g = 1024;
+    // one workgroup per CU, a contiguous chunk each (fewer for small inputs)
+    uint64_t g = (n * sizeof(Tup) / 16 + KR_THREADS * KR_U - 1) / (KR_THREADS * KR_U);
+    if (g > 256) g = 256;
     if (g == 0) g = 1;
-    hipLaunchKernelGGL(k_keyrange, dim3((uint32_t)g), dim3(256), 0, st, rels[0], ns[0],
+    hipLaunchKernelGGL(k_keyrange, dim3((uint32_t)g), dim3(KR_THREADS), 0, st, rels[0], ns[0],
                        nrel > 1 ? rels[1] : (const Tup*)nullptr, nrel > 1 ? ns[1] : 0, mm);
     SMJ_CHECK(hipMemcpyAsync(h, mm, 16, hipMemcpyDeviceToHost, st));
     SMJ_CHECK(hipStreamSynchronize(st));
