@@ -728,6 +728,7 @@ struct SwpTile {
     uint32_t hb, t2, wbase;
     int lane, wid;
     bool owner;
+    bool pairs;  // 8-byte tuples, 16-byte aligned output: pair stores
     uint64_t end;
     uint32_t pos[2], kc[2];
 
@@ -850,6 +851,38 @@ struct SwpTile {
         // next-but-one tile's ITEMS loads stay in flight
         __builtin_amdgcn_s_waitcnt(vmcnt_imm(ITEMS));
         SWP_MARK(5);
+#ifndef KEY_8B
+        // 8-byte tuples: a lane writes two adjacent tuples of a segment with
+        // one 16-byte store (SEG / 2 lanes per segment); a pair cut by its
+        // region's first or last partial segment stores its one tuple alone
+        if (NT && pairs) {
+            typedef unsigned long long V2 __attribute__((ext_vector_type(2)));
+            constexpr uint32_t PS = SEG / 2;
+            for (uint32_t q = threadIdx.x; q < nsegT * PS; q += THREADS) {
+                const uint32_t sg = q / PS;
+                const uint32_t d = segown[sg];
+                const u32x4_t I = info[d];
+                const uint32_t p = I[0];
+                const uint32_t a0 = (p / SEG + (sg - (I[3] & 0xfffu))) * SEG + 2 * (q % PS);
+                const uint32_t k = (I[3] >> 12) & 7u;
+                const bool v0 = a0 >= p && a0 < p + I[1];
+                const bool v1 = a0 + 1 >= p && a0 + 1 < p + I[1];
+                const uint32_t e0 = a0 - p, e1 = a0 + 1 - p;
+                const Tup x0 = e0 < k ? carry[d * CW + e0] : stage[v0 ? I[2] + e0 - k : 0u];
+                const Tup x1 = e1 < k ? carry[d * CW + e1] : stage[v1 ? I[2] + e1 - k : 0u];
+                if (v0 && v1) {
+                    V2 y;
+                    y.x = x0;
+                    y.y = x1;
+                    __builtin_nontemporal_store(y, reinterpret_cast<V2*>(out + a0));
+                } else if (v0) {
+                    st_stream(out + a0, x0);
+                } else if (v1) {
+                    st_stream(out + a0 + 1, x1);
+                }
+            }
+        } else
+#endif
         for (uint32_t q = threadIdx.x; q < nsegT * SEG; q += THREADS) {
             const uint32_t sg = q / SEG;
             const uint32_t d = segown[sg];
@@ -902,7 +935,7 @@ template <int THREADS, int ITEMS, class Digit, bool NT>
 __global__ void __launch_bounds__(THREADS)
 k_scatter_swp(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_arg,
               uint32_t nbins, const uint32_t* __restrict__ counts, uint32_t nwg,
-              const uint64_t* __restrict__ starts, Tup* __restrict__ out) {
+              const uint64_t* __restrict__ starts, Tup* __restrict__ out, int pairs_ok) {
     typedef SwpTile<THREADS, ITEMS, decltype(dig_arg.load()), NT> P;
     constexpr int W = P::W;
     constexpr int TILE = P::TILE;
@@ -924,6 +957,7 @@ k_scatter_swp(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
     s.wid = threadIdx.x >> 6;
     s.t2 = threadIdx.x;
     s.owner = s.t2 < s.hb;
+    s.pairs = sizeof(Tup) == 8 && pairs_ok && ((uintptr_t)out & 15) == 0;
     s.pos[0] = s.pos[1] = s.kc[0] = s.kc[1] = 0;
     if (s.owner) {
 #pragma unroll
@@ -1956,14 +1990,15 @@ static void stable_partition_swa(Workspace* ws, const Tup* in, uint64_t n, Tup* 
         attr = true;
     }
     TraceScope ts(ws, "k_scatter", st);
+    const int pairs_ok = (swa_pipelined() & 16) ? 0 : 1;
     if (swa_pipelined() & 8)
         hipLaunchKernelGGL((k_scatter_swp<THREADS, ITEMS, Digit, true>), dim3(nwg), dim3(THREADS),
                            G::lds_bytes(nbins), st, in, n, chunk, dig, nbins, counts, nwg,
-                           starts_dev, out);
+                           starts_dev, out, pairs_ok);
     else if (swa_pipelined() & 2)
         hipLaunchKernelGGL((k_scatter_swp<THREADS, ITEMS, Digit, false>), dim3(nwg), dim3(THREADS),
                            G::lds_bytes(nbins), st, in, n, chunk, dig, nbins, counts, nwg,
-                           starts_dev, out);
+                           starts_dev, out, pairs_ok);
     else
         hipLaunchKernelGGL((k_scatter_swa<THREADS, ITEMS, Digit>), dim3(nwg), dim3(THREADS),
                            G::lds_bytes(nbins), st, in, n, chunk, dig, nbins, counts, nwg,
