@@ -1423,11 +1423,11 @@ k_sample_hist(SampleRel S, uint32_t stride, Digit dig_arg, uint32_t nbins) {
     // 64-byte read for 16-byte tuples): 1/stride of the input
     const uint64_t pstride = 4ull * stride;
     const uint64_t step = (uint64_t)gridDim.x * 256 * pstride;
+    // clamped, unconditional loads (a conditional load waits alone)
     for (uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * pstride; i < n; i += step) {
         Tup t[4];
 #pragma unroll
-        for (int k = 0; k < 4; k++)
-            if (i + k < n) t[k] = in[i + k];
+        for (int k = 0; k < 4; k++) t[k] = in[i + k < n ? i + k : n - 1];
 #pragma unroll
         for (int k = 0; k < 4; k++)
             if (i + k < n) atomicAdd(&sh_hist[dig(t[k])], 1u);
@@ -2212,6 +2212,10 @@ void plan_partition_packed(Workspace* ws, const Tup* in, uint64_t n, uint64_t* o
 #define SMJ_SAMPLE_STRIDE 128
 #endif
 static constexpr uint32_t kSampleStride = SMJ_SAMPLE_STRIDE;
+#ifndef SMJ_SAMPLE_WG
+#define SMJ_SAMPLE_WG 128
+#endif
+static constexpr uint32_t kSampleWg = SMJ_SAMPLE_WG;
 static constexpr uint64_t kRegionSlack = 1024;  // per shard
 
 uint64_t sampled_capacity(uint64_t n, uint32_t dbits) {
@@ -2340,7 +2344,12 @@ void sampled_partition(Workspace* ws, int nrel, const Tup* const* in, const uint
         TraceScope ts(ws, "k_sample", st);
         const uint64_t npts = (nmax + 4 * kSampleStride - 1) / (4 * kSampleStride);
         uint32_t g = (uint32_t)((npts + 255) / 256);
-        if (g > 1024) g = 1024;
+        // each workgroup ends with one global add per partition: at most
+        // SMJ_SAMPLE_WG workgroups per relation keep those adds (contended,
+        // nbins addresses) few.  128M x 128M join, interleaved
+        // (tools/ab_sample.sh): k_sample + k_regions 0.057 ms at 1024
+        // workgroups, 0.038 at 256, 0.031 at 128
+        if (g > kSampleWg) g = kSampleWg;
         if (g == 0) g = 1;
         hipLaunchKernelGGL((k_sample_hist<PlanDigit1>), dim3(g, nrel), dim3(256),
                            nbins * sizeof(unsigned int), st, S, kSampleStride, dig, nbins);
