@@ -1688,8 +1688,13 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
             SMJ_CHECK(hipMemcpyAsync(h + 1, a.pack_bad, 4, hipMemcpyDeviceToHost, st));
     }
     SMJ_CHECK(hipStreamSynchronize(st));
-    // the caller repeats with exact partitions (region overflow) or on tuples
-    // (not packable); the tile and group passes exited at once on the latter
+    if (a.status_out) {
+        a.status_out[0] = h[0];
+        a.status_out[1] = h[1];
+    }
+    // the caller repeats with exact partitions (region overflow), on tuples
+    // (not packable) or with the exact plan (a key outside a guessed one); the
+    // tile and group passes exited at once on the latter two
     if (h[0] || h[1]) return false;
     const uint32_t no = h[2];
     if (no == 0) return true;

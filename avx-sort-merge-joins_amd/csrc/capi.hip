@@ -291,12 +291,19 @@ static bool use_packing() {
 
 // Sort of one relation (nrel 1) or sort + merge-join count of two (nrel 2):
 // range plan -> sampled level-1 partition -> tile pass -> group pass.  The
-// plan comes from the caller's key-range hint, or else from one exact
-// min/max pass (so that it is known on the host: no mid-pipeline
-// synchronisation, and 16-byte tuples travel as packed words).
+// plan must be known on the host (no mid-pipeline synchronisation, and 16-byte
+// tuples travel as packed words).  It comes from
+//   - the caller's key-range hint (hint_min <= hint_max), else
+//   - the relation size (size_guess > 0): keys 1..size_guess, the reference's
+//     own assumption (its partitioning_phase derives the radix shift from
+//     |R| * T, src/joins/sortmergejoin_multiway.c:372-376).  The level-1
+//     scatter, which reads every key anyway, verifies it (kBadRange); a key
+//     outside sends the call back to the exact plan below, else
+//   - one exact min/max pass (key_range: one read and a host round trip).
+// Keys outside a hinted plan are legal: they clamp to the end digits.
 static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t* ns,
                           int nrel, Tup* const* outs, uint32_t fanout_bits,
-                          int64_t hint_min, int64_t hint_max,
+                          int64_t hint_min, int64_t hint_max, uint64_t size_guess,
                           unsigned long long* count_dev, hipStream_t st) {
     static const char* nm[2][6] = {{"bk_part0", "bk_st0", "bk_h0", "bk_sgs0", "bk_sgc0", ""},
                                    {"bk_part1", "bk_st1", "bk_h1", "bk_sgs1", "bk_sgc1", ""}};
@@ -306,16 +313,23 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
     uint32_t D1, D2, D2cap;
     choose_levels(nmax, fanout_bits, &D1, &D2, &D2cap);
     RangePlan* plan = (RangePlan*)ws->scratch("plan", sizeof(RangePlan));
+    const uint32_t nb = 1u << D1;
+    const bool sampled = use_sampled() && D1 <= 10;  // LDS carries up to 1024
     bool plan_on_host = hint_min <= hint_max;
+    // a guessed plan is verified by the sampled scatter only
+    bool guessed = false;
+    if (!plan_on_host && size_guess > 0 && sampled && !getenv("SMJ_SAMPLED_PLAN")) {
+        hint_min = 1;
+        hint_max = (int64_t)(size_guess < (uint64_t)INT64_MAX ? size_guess : INT64_MAX);
+        plan_on_host = guessed = true;
+    }
     if (!plan_on_host && !getenv("SMJ_SAMPLED_PLAN"))
         plan_on_host = key_range(ws, rels, ns, nrel, &hint_min, &hint_max, st);
     RangePlan hplan = make_plan(hint_min, hint_max, D1, D2, D2cap, kGroupD3Max);
     if (!plan_on_host)
         plan_from_sample(ws, rels, ns, nrel, D1, D2, D2cap, hint_min, hint_max, plan, st);
-    const uint32_t nb = 1u << D1;
-    const bool sampled = use_sampled() && D1 <= 10;  // LDS carries up to 1024
 #ifdef KEY_8B
-    const bool can_pack = sampled && plan_on_host && use_packing() && LayPacked::usable(hplan);
+    bool can_pack = sampled && plan_on_host && use_packing() && LayPacked::usable(hplan);
 #else
     const bool can_pack = false;
 #endif
@@ -332,7 +346,8 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
         sgs[r] = (uint64_t*)ws->scratch(nm[r][3], (size_t)nb * kShards * 8);
         sgc[r] = (int64_t*)ws->scratch(nm[r][4], (size_t)nb * kShards * 8);
     }
-    // [0] region overflow, [1] not packable, [2] skew queue length
+    // [0] region overflow, [1] bad tuple (kBadPayload | kBadRange), [2] skew
+    // queue length
     unsigned int* status = (unsigned int*)ws->scratch("join_status", 16);
     // the sampled partition's counters: zeroed by k_join_begin on every
     // attempt (never assumed zero from an earlier call)
@@ -342,16 +357,21 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
     // attempts: sampled + packed words, sampled tuples, exact tuples; a later
     // one runs only when the one before reported a region overflow or an
     // unpackable tuple (its tile and group passes then did nothing or are
-    // discarded: the count restarts from 0)
-    for (int mode = can_pack ? 0 : (sampled ? 1 : 2); mode <= 2; mode++) {
+    // discarded: the count restarts from 0).  A guessed plan that a key falls
+    // outside of is replaced by the exact one and the attempts restart.
+    int mode = can_pack ? 0 : (sampled ? 1 : 2);
+    while (mode <= 2) {
         const bool packed = mode == 0;
+        // the status word the tile and group passes exit on (sampled modes)
+        const bool check = packed || (guessed && mode == 1);
         hipLaunchKernelGGL(k_join_begin, dim3(1), dim3(256), 0, st, plan, hplan,
                            plan_on_host ? 1 : 0, cnt, status, sample,
                            mode < 2 ? (uint32_t)nrel * nb : 0u);
         if (mode < 2) {
             void* outs_v[2] = {part[0], part[nrel > 1 ? 1 : 0]};
             sampled_partition(ws, nrel, rels, ns, outs_v, plan, D1, sample, bst, bh, sgs, sgc,
-                              status, st, packed ? &hplan : nullptr, status + 1);
+                              status, st, plan_on_host ? &hplan : nullptr, packed,
+                              check ? status + 1 : nullptr);
         } else {
             for (int r = 0; r < nrel; r++)
                 plan_partition(ws, rels[r], ns[r], part[r], plan, D1, bst[r], bh[r], st);
@@ -379,32 +399,52 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
         a.ev_ovf = ws->ev[3];
         a.host_plan = plan_on_host ? &hplan : nullptr;
         a.packed = packed;
-        a.pack_bad = packed ? status + 1 : nullptr;
+        a.pack_bad = check ? status + 1 : nullptr;
         a.status = status;
         if (mode < 2) a.part_flag = status;
+        uint32_t why[2] = {0, 0};
+        a.status_out = why;
         if (bucket_sort(ws, a, st)) break;
+        if (guessed && (why[1] & kBadRange)) {
+            // a key outside 1..size_guess: the exact plan, attempts from the top
+            guessed = false;
+            plan_on_host = key_range(ws, rels, ns, nrel, &hint_min, &hint_max, st);
+            hplan = make_plan(hint_min, hint_max, D1, D2, D2cap, kGroupD3Max);
+            if (!plan_on_host)  // empty relations never report a bad key
+                plan_from_sample(ws, rels, ns, nrel, D1, D2, D2cap, hint_min, hint_max, plan,
+                                 st);
+#ifdef KEY_8B
+            can_pack = sampled && plan_on_host && use_packing() && LayPacked::usable(hplan);
+#endif
+            mode = can_pack ? 0 : (sampled ? 1 : 2);
+            continue;
+        }
+        mode++;
     }
     SMJ_CHECK(hipEventRecord(ws->ev[4], st));
 }
 
+// avxsort_tuples and friends: the plan is guessed from the size (keys 1..n,
+// the shape of create_relation_pk) and verified, like the join's
 static void device_sort(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
                         hipStream_t st) {
     if (n == 0) return;
     const Tup* rels[1] = {in};
     uint64_t ns[1] = {n};
     Tup* outs[1] = {out};
-    device_bucket(ws, rels, ns, 1, outs, 0, 1, 0, nullptr, st);
+    device_bucket(ws, rels, ns, 1, outs, 0, 1, 0, n, nullptr, st);
 }
 
 static void device_join(Workspace* ws, const Tup* R, uint64_t nR, const Tup* S,
                         uint64_t nS, Tup* sortedR, Tup* sortedS,
                         uint32_t fanout_bits, int64_t hint_min,
                         int64_t hint_max, unsigned long long* count_dev,
-                        hipStream_t st) {
+                        hipStream_t st, uint64_t size_guess = 0) {
     const Tup* rels[2] = {R, S};
     uint64_t ns[2] = {nR, nS};
     Tup* outs[2] = {sortedR, sortedS};
-    device_bucket(ws, rels, ns, 2, outs, fanout_bits, hint_min, hint_max, count_dev, st);
+    device_bucket(ws, rels, ns, 2, outs, fanout_bits, hint_min, hint_max, size_guess,
+                  count_dev, st);
 }
 
 // ---------------------------------------------------------------------------
@@ -1119,7 +1159,9 @@ static result_t* join_api(relation_t* relR, relation_t* relS,
     // the reference fan-out (128 by default) only sizes the level-1 pass here;
     // choose_levels raises it as the relation size needs
     if (fb < 8) fb = 8;
-    device_join(&c.ws, r.d, nR, s.d, nS, sR, sS, fb, 1, 0, cnt, c.st);
+    // no key-range hint: the plan is guessed from |R| as the reference does
+    // (keys 1..|R|) and verified by the level-1 scatter
+    device_join(&c.ws, r.d, nR, s.d, nS, sR, sS, fb, 1, 0, cnt, c.st, nR);
     unsigned long long h = 0;
     SMJ_CHECK(hipMemcpyAsync(&h, cnt, 8, hipMemcpyDeviceToHost, c.st));
     sync();
@@ -1627,13 +1669,15 @@ int smj_dev_partition_range_sampled(smj_workspace* wsp, const tuple_t* in, uint6
     uint64_t* ss[1] = {(uint64_t*)seg_start_out};
     int64_t* sc[1] = {seg_cnt_out};
     sampled_partition(ws, 1, rels, ns, outs, plan, nbits, sample, st_, h_, ss, sc, flags, st,
-                      packed ? &h : nullptr, flags + 1);
+                      &h, packed != 0, packed ? flags + 1 : nullptr);
     return 1;
 }
 
 uint64_t smj_selfcheck_lds_order(smj_workspace* ws, smj_stream_t stream) {
     return lds_order_selfcheck((Workspace*)ws, (hipStream_t)stream);
 }
+
+smj_workspace* smj_context_workspace(void) { return (smj_workspace*)&ctx().ws; }
 
 void smj_trace_enable(smj_workspace* wsp, int on) {
     ((Workspace*)wsp)->trace_on = on != 0;

@@ -749,9 +749,9 @@ static bool multiway_merge_buckets(Workspace* ws, const Tup* const* runs, const 
     }
     const uint64_t nb = (uint64_t)(B + 1) * k;
     {
-        TraceScope ts(ws, "k_km_bounds", st);
-        hipLaunchKernelGGL(k_km_bounds, dim3((uint32_t)((nb + KM_THREADS - 1) / KM_THREADS)),
-                           dim3(KM_THREADS), 0, st, dr, k, D, mm, off);
+        traced_launch(ws, "k_km_bounds", k_km_bounds,
+                      dim3((uint32_t)((nb + KM_THREADS - 1) / KM_THREADS)), dim3(KM_THREADS), 0,
+                      st, dr, k, D, mm, off);
     }
     // the flags live in pinned host memory the kernel writes directly, so
     // the synchronisation needs no copy behind the kernels
@@ -761,9 +761,8 @@ static bool multiway_merge_buckets(Workspace* ws, const Tup* const* runs, const 
     unsigned int* dflag = nullptr;
     SMJ_CHECK(hipHostGetDevicePointer((void**)&dflag, (void*)hflag, 0));
     {
-        TraceScope ts(ws, "k_km_merge", st);
-        hipLaunchKernelGGL(k_km_merge, dim3(B), dim3(KM_THREADS), 0, st, dr, k, D, mm, off,
-                           dflag, out);
+        traced_launch(ws, "k_km_merge", k_km_merge, dim3(B), dim3(KM_THREADS), 0, st, dr, k,
+                      D, mm, off, dflag, out);
     }
     SMJ_CHECK(hipGetLastError());
     SMJ_CHECK(hipStreamSynchronize(st));

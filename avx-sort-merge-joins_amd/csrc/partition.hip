@@ -142,7 +142,7 @@ __global__ void __launch_bounds__(THREADS)
 k_scatter(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_arg,
           uint32_t nbins, uint32_t dbits, const uint32_t* __restrict__ counts,
           uint32_t nwg, const uint64_t* __restrict__ starts,
-          Tup* __restrict__ out, int mode) {
+          Tup* __restrict__ out) {
     const auto dig = dig_arg.load();
     constexpr int TILE = THREADS * ITEMS;
     constexpr int WAVES = THREADS / 64;
@@ -242,9 +242,7 @@ k_scatter(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_arg,
         for (uint32_t i = threadIdx.x; i < tcount; i += THREADS) {
             Tup t = stage[i];
             uint32_t d = dig(t);
-            if (mode == 0) out[run[d] + (i - tstart[d])] = t;
-            else if (mode == 1) out[base + i] = t;  // ablation: linear write
-            else if (tup_key(t) == -12345) out[0] = t;  // ablation: no write
+            out[run[d] + (i - tstart[d])] = t;
         }
         __syncthreads();
         for (uint32_t k = 0; k < dper; k++) {
@@ -475,9 +473,9 @@ k_scatter_swc(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
 // are partial.
 //
 // MI355X, 2^27 tuples, 10 bits (tools/partlab.hip): 8 B 0.73 ms, 16 B 1.14 ms
-// for this scatter, against 1.46 / 1.51 ms for k_scatter_swc (ballot ranks)
-// and 0.84 ms for the same atomic ranks without the carry (34 % extra write
-// bytes, 41 % partial write requests).
+// for the first form of this scatter, against 1.46 / 1.51 ms for
+// k_scatter_swc (ballot ranks) and 0.84 ms for the same atomic ranks without
+// the carry (34 % extra write bytes, 41 % partial write requests).
 template <int THREADS, int ITEMS>
 struct SwaGeom {
     static constexpr int W = THREADS / 64;
@@ -494,196 +492,18 @@ struct SwaGeom {
 
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
-template <int THREADS, int ITEMS, class Digit>
-__global__ void __launch_bounds__(THREADS)
-k_scatter_swa(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_arg,
-              uint32_t nbins, const uint32_t* __restrict__ counts, uint32_t nwg,
-              const uint64_t* __restrict__ starts, Tup* __restrict__ out) {
-    typedef SwaGeom<THREADS, ITEMS> G;
-    constexpr int W = G::W;
-    constexpr int TILE = G::TILE;
-    constexpr uint32_t SEG = G::SEG;
-    constexpr uint32_t CW = G::CW;
-    const auto dig = dig_arg.load();
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
-    Tup* stage = reinterpret_cast<Tup*>(lds_raw);
-    Tup* carry = stage + TILE;
-    uint32_t* w32 = reinterpret_cast<uint32_t*>(carry + (size_t)nbins * CW);
-    const uint32_t hb = nbins / 2;
-    u32x4_t* info = reinterpret_cast<u32x4_t*>(w32 + (size_t)W * hb);
-    uint16_t* segown = reinterpret_cast<uint16_t*>(info + nbins);
-    // plain pointer arithmetic (no integer casts): the scan scratch stays an
-    // LDS pointer, not a flat one that every vmcnt wait would have to cover
-    uint32_t* scr = reinterpret_cast<uint32_t*>(segown + ((TILE / SEG + 2 * nbins + 7) & ~7u));
-
-    const int lane = lane_id();
-    const int wid = threadIdx.x >> 6;
-    const uint32_t t2 = threadIdx.x;
-    const bool owner = t2 < hb;
-    // the owner's state of digits 2 t2 and 2 t2 + 1: output cursor, carry size
-    uint32_t pos[2] = {0, 0}, kc[2] = {0, 0};
-    if (owner) {
-#pragma unroll
-        for (int h = 0; h < 2; h++)
-            pos[h] = (uint32_t)(starts[2 * t2 + h] +
-                                counts[(uint64_t)(2 * t2 + h) * nwg + blockIdx.x]);
-    }
-    for (uint32_t q = threadIdx.x; q < W * hb; q += THREADS) w32[q] = 0;
-    const uint64_t beg = (uint64_t)blockIdx.x * chunk;
-    const uint64_t end = min(beg + chunk, n);
-    const uint32_t wbase = wid * 64 * ITEMS;
-    Tup v[ITEMS], nv[ITEMS];
-#pragma unroll
-    for (int j = 0; j < ITEMS; j++) {
-        const uint64_t i = beg + wbase + j * 64 + lane;
-        v[j] = in[i < end ? i : end - 1];
-    }
-    // the first tile has landed: without this explicit wait the compiler's
-    // bookkeeping merges these loads into the loop header and re-waits with
-    // vmcnt(0) -- stores included -- at every tile
-    __builtin_amdgcn_s_waitcnt(0x0f70);
-    __syncthreads();
-    for (uint64_t base = beg; base < end; base += TILE) {
-        const uint32_t tcount = (uint32_t)min((uint64_t)TILE, end - base);
-        // ---- ranks (lane-ordered atomics, see the header)
-        uint32_t dg[ITEMS], rk[ITEMS];
-#pragma unroll
-        for (int j = 0; j < ITEMS; j++) {
-            const bool valid = wbase + j * 64 + lane < tcount;
-            dg[j] = valid ? dig(v[j]) : 0xffffffffu;
-            const uint32_t d = valid ? dg[j] : 0;
-            const uint32_t sh = (d & 1u) * 16u;
-            uint32_t old = 0;
-            if (valid) old = atomicAdd(&w32[wid * hb + (d >> 1)], 1u << sh);
-            rk[j] = (old >> sh) & 0xffffu;
-        }
-        __syncthreads();
-        // ---- owner: tile counts, emission sizes (up to the last segment
-        // boundary of carry + tile), stage offsets and segment numbers in one
-        // packed scan (both sums stay below 2^16)
-        uint32_t cw[W];
-        uint32_t c[2] = {0, 0}, E[2] = {0, 0}, ns[2] = {0, 0};
-        if (owner) {
-#pragma unroll
-            for (int w = 0; w < W; w++) {
-                cw[w] = w32[w * hb + t2];
-                c[0] += cw[w] & 0xffffu;
-                c[1] += cw[w] >> 16;
-            }
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const uint32_t T = kc[h] + c[h];
-                const uint32_t m = (pos[h] + T) % SEG;
-                E[h] = m <= T ? T - m : 0u;
-                ns[h] = E[h] ? (pos[h] + E[h]) / SEG - pos[h] / SEG : 0u;
-            }
-        }
-        uint32_t tot;
-        const uint32_t ex =
-            block_exclusive_scan((c[0] + c[1]) | ((ns[0] + ns[1]) << 16), scr, &tot);
-        const uint32_t nsegT = tot >> 16;
-        uint32_t ts[2] = {0, 0};
-        if (owner) {
-            ts[0] = ex & 0xffffu;
-            ts[1] = ts[0] + c[0];
-            const uint32_t sp[2] = {ex >> 16, (ex >> 16) + ns[0]};
-            uint32_t o0 = ts[0], o1 = ts[1];
-#pragma unroll
-            for (int w = 0; w < W; w++) {
-                const uint32_t x = cw[w];
-                w32[w * hb + t2] = o0 | (o1 << 16);
-                o0 += x & 0xffffu;
-                o1 += x >> 16;
-            }
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const uint32_t d = 2 * t2 + h;
-                u32x4_t I;
-                I[0] = pos[h];
-                I[1] = E[h];
-                I[2] = ts[h];
-                I[3] = sp[h] | (kc[h] << 16);
-                info[d] = I;
-                for (uint32_t k = 0; k < ns[h]; k++) segown[sp[h] + k] = (uint16_t)d;
-            }
-        }
-        // prefetch the next tile
-        const uint64_t nb = base + TILE;
-#pragma unroll
-        for (int j = 0; j < ITEMS; j++) {
-            const uint64_t i = nb + wbase + j * 64 + lane;
-            nv[j] = in[i < end ? i : end - 1];  // unconditional: a fixed count in flight
-        }
-        __syncthreads();
-        // ---- stage the tile in digit order
-#pragma unroll
-        for (int j = 0; j < ITEMS; j++)
-            if (dg[j] != 0xffffffffu) {
-                const uint32_t d = dg[j];
-                const uint32_t wo = (w32[wid * hb + (d >> 1)] >> ((d & 1u) * 16u)) & 0xffffu;
-                stage[wo + rk[j]] = v[j];
-            }
-        __syncthreads();
-        // ---- whole aligned segments, SEG consecutive lanes each; element e
-        // of a digit's emission is its carry (e < kc) or its staged run
-        if (owner) {
-#pragma unroll
-            for (int w = 0; w < W; w++) w32[w * hb + t2] = 0;
-        }
-        // the prefetch has landed (it flew under the ranking and staging): wait
-        // here, before the segment stores, so that the next tile does not wait
-        // for those stores to drain
-        __builtin_amdgcn_s_waitcnt(0x0f70);
-        for (uint32_t q = threadIdx.x; q < nsegT * SEG; q += THREADS) {
-            const uint32_t sg = q / SEG;
-            const uint32_t d = segown[sg];
-            const u32x4_t I = info[d];
-            const uint32_t p = I[0];
-            const uint32_t addr = (p / SEG + (sg - (I[3] & 0xffffu))) * SEG + q % SEG;
-            if (addr >= p && addr < p + I[1]) {
-                const uint32_t e = addr - p;
-                const uint32_t k = I[3] >> 16;
-                out[addr] = e < k ? carry[d * CW + e] : stage[I[2] + e - k];
-            }
-        }
-        __syncthreads();
-        // ---- owner: the leftovers (< SEG) become the carry
-        if (owner) {
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const uint32_t d = 2 * t2 + h;
-                const uint32_t T = kc[h] + c[h];
-                for (uint32_t e = E[h]; e < T; e++)
-                    carry[d * CW + (e - E[h])] =
-                        e < kc[h] ? carry[d * CW + e] : stage[ts[h] + e - kc[h]];
-                pos[h] += E[h];
-                kc[h] = T - E[h];
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < ITEMS; j++) v[j] = nv[j];
-    }
-    // ---- the partial last segment of every region
-    if (owner) {
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const uint32_t d = 2 * t2 + h;
-            for (uint32_t e = 0; e < kc[h]; e++) out[pos[h] + e] = carry[d * CW + e];
-        }
-    }
-}
-
 // s_waitcnt immediate for vmcnt(N), expcnt and lgkmcnt left free (gfx9 layout:
 // vmcnt[3:0] + vmcnt[5:4] at bits 15:14)
 constexpr int vmcnt_imm(int n) { return (n & 15) | ((n >> 4) << 14) | 0x0f70; }
 
-// k_scatter_swa with the next-but-one tile's loads in flight: three register
+// k_scatter_swp: the next-but-one tile's loads are in flight: three register
 // tiles rotate (the loop is unrolled by three so that no tile is copied
 // between registers -- a copy would wait for its loads), and the wait before a
 // tile's segment stores is vmcnt(ITEMS): everything but the loads issued in
 // this tile (the next-but-one) has landed, i.e. the next tile and the previous
 // tile's stores.  The loads thus fly under a whole tile of LDS work instead of
-// the stage phase alone.  Same ranks, layout and results as k_scatter_swa.
+// the stage phase alone.  Loads are non-temporal (NT; the input is read
+// once), 8-byte tuples leave in 16-byte pair stores.
 #ifdef SMJ_SWP_PROF
 // lab build only: per-phase cycle counts of k_scatter_swp, summed over the
 // workgroups' thread 0 (read by smj_swp_prof)
@@ -1007,9 +827,11 @@ extern "C" void smj_swp_prof(unsigned long long* out) {
 }
 #endif
 
-// Histogram of the stable write-combining partition with two register tiles
-// alternating (the next tile's loads fly while this one is counted).  Same
-// counts as k_hist_c.
+// Histogram of the stable write-combining partition: counts[d][wg] of each
+// workgroup's chunk (the scatter's chunking), two register tiles alternating
+// (the next tile's loads fly while this one is counted).  Loads are
+// unconditional (clamped to the chunk) so that every load of a tile is in
+// flight at once.
 template <int THREADS, int ITEMS, class Digit, bool NT>
 __global__ void __launch_bounds__(THREADS)
 k_hist_p(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_arg,
@@ -1102,38 +924,6 @@ k_hist_v(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_arg,
         counts[(uint64_t)d * nwg + blockIdx.x] = lds_hv[d];
 }
 
-// Histogram of the stable write-combining partition: counts[d][wg] of each
-// workgroup's chunk (the scatter's chunking).  Loads are unconditional
-// (clamped to the chunk) so that every load of a tile is in flight at once.
-template <int THREADS, int ITEMS, class Digit>
-__global__ void __launch_bounds__(THREADS)
-k_hist_c(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_arg,
-         uint32_t nbins, uint32_t* __restrict__ counts, uint32_t nwg) {
-    const auto dig = dig_arg.load();
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds_hc[];
-    for (uint32_t d = threadIdx.x; d < nbins; d += THREADS) lds_hc[d] = 0;
-    __syncthreads();
-    const uint64_t beg = (uint64_t)blockIdx.x * chunk;
-    const uint64_t end = min(beg + chunk, n);
-    constexpr int TILE = THREADS * ITEMS;
-    for (uint64_t base = beg; base < end; base += TILE) {
-        Tup v[ITEMS];
-#pragma unroll
-        for (int j = 0; j < ITEMS; j++) {
-            const uint64_t i = base + (uint64_t)j * THREADS + threadIdx.x;
-            v[j] = in[i < end ? i : end - 1];
-        }
-#pragma unroll
-        for (int j = 0; j < ITEMS; j++) {
-            const uint64_t i = base + (uint64_t)j * THREADS + threadIdx.x;
-            if (i < end) atomicAdd(&lds_hc[dig(v[j])], 1u);
-        }
-    }
-    __syncthreads();
-    for (uint32_t d = threadIdx.x; d < nbins; d += THREADS)
-        counts[(uint64_t)d * nwg + blockIdx.x] = lds_hc[d];
-}
-
 // Unstable scatter for the join's level-1 partition (the join re-sorts every
 // bucket completely, so the order inside a partition is free).  Ranks come
 // from LDS atomics on tile-level digit counters -- two ds_add per tuple instead
@@ -1150,9 +940,9 @@ __global__ void __launch_bounds__(THREADS)
 k_scatter_u(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_arg,
             uint32_t nbins, const uint32_t* __restrict__ counts, uint32_t nwg,
             const uint64_t* __restrict__ starts, typename Pack::OutT* __restrict__ out,
-            int mode, Pack pk = Pack(), unsigned int* __restrict__ bad_flag = nullptr) {
+            Pack pk = Pack(), unsigned int* __restrict__ bad_flag = nullptr) {
     const auto dig = dig_arg.load();
-    bool bad = false;
+    uint32_t bad = 0;
     constexpr int TILE = THREADS * ITEMS;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     Tup* stage = reinterpret_cast<Tup*>(lds_raw);
@@ -1220,9 +1010,7 @@ k_scatter_u(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_ar
         for (uint32_t i = threadIdx.x; i < tcount; i += THREADS) {
             const Tup t = stage[i];
             const uint32_t d = dig(t);
-            if (mode == 0) out[run[d] + (i - tstart[d])] = pk(t, bad);
-            else if (mode == 1) out[base + i] = pk(t, bad);  // ablation: linear write
-            else if (tup_key(t) == -12345) out[0] = pk(t, bad);  // ablation: no write
+            out[run[d] + (i - tstart[d])] = pk(t, bad);
         }
         __syncthreads();
         for (uint32_t k = 0; k < dper; k++) {
@@ -1236,7 +1024,7 @@ k_scatter_u(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_ar
         for (int j = 0; j < ITEMS; j++) v[j] = nv[j];
         __syncthreads();
     }
-    if (bad_flag && bad) atomicOr(bad_flag, 1u);
+    if (bad_flag && bad) atomicOr(bad_flag, bad);
 }
 
 // Write-combining scatter for the join's level-1 partition (order inside a
@@ -1563,7 +1351,7 @@ k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
     typedef ScatterGeom<THREADS, ITEMS, OutT> Geo;
     constexpr uint32_t SEG = Geo::SEG;
     constexpr int TILE = (int)Geo::TILE;
-    bool bad = false;
+    uint32_t bad = 0;
     const auto dig = dig_arg.load();
     // this workgroup's shard of every partition: cursor[d * kShards + shard]
     const uint32_t shard = blockIdx.x % kShards;
@@ -1724,7 +1512,7 @@ k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
         const uint32_t d = q / SEG, j = q % SEG;
         if (j < kc[d] && pos[d] != ~0ull) out[pos[d] + j] = carry[q];
     }
-    if (bad_flag && bad) atomicOr(bad_flag, 1u);
+    if (bad_flag && bad) atomicOr(bad_flag, bad);
 }
 
 // pad copy for wide digits: item at unpadded position i of digit d moves to
@@ -1774,46 +1562,17 @@ struct HighBits {
     }
 };
 
-// Scatter geometry (threads x items per thread = LDS tile).  Selected by
-// SMJ_PT_VARIANT for experiments; the default is the measured best.
-// ablation switch for measurements only (SMJ_SCATTER_MODE=1 linear write,
-// 2 no write); the default 0 is the real scatter
-static int scatter_mode() {
-    static int m = -1;
-    if (m < 0) {
-        const char* e = getenv("SMJ_SCATTER_MODE");
-        m = e ? atoi(e) : 0;
-    }
-    return m;
-}
-
-// write-combining stable scatter (k_scatter_swc); SMJ_STABLE_WC=0 keeps k_scatter
-static bool stable_wc() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("SMJ_STABLE_WC");
-        v = e ? atoi(e) : 1;
-    }
-    return v != 0;
-}
-
-static int pt_variant() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("SMJ_PT_VARIANT");
-        v = e ? atoi(e) : 2;
-        if (v < 0 || v > 2) v = 2;
-    }
-    return v;
-}
-
+// Histogram + scan + scatter over THREADS x ITEMS tiles, up to 8 workgroups
+// per CU.  STABLE: k_scatter_swc (ballot ranks, write combining) where its
+// LDS fits, else k_scatter; unstable: k_scatter_u (the join's exact level-1
+// partition of 8-byte tuples and the exchange's packed partition).
 template <int THREADS, int ITEMS, bool STABLE, class Digit, class Pack = PackNone>
-static void stable_partition_t(Workspace* ws, const Tup* in, uint64_t n,
-                               typename Pack::OutT* out, const Digit& dig, uint32_t dbits,
-                               int padded, uint64_t* starts_dev,
-                               int64_t* hist_out, int64_t* off_out,
-                               hipStream_t st, const Pack& pk = Pack(),
-                               unsigned int* bad_flag = nullptr) {
+static void partition_hist_scatter(Workspace* ws, const Tup* in, uint64_t n,
+                                   typename Pack::OutT* out, const Digit& dig, uint32_t dbits,
+                                   int padded, uint64_t* starts_dev,
+                                   int64_t* hist_out, int64_t* off_out,
+                                   hipStream_t st, const Pack& pk = Pack(),
+                                   unsigned int* bad_flag = nullptr) {
     constexpr int TILE = THREADS * ITEMS;
     const uint32_t nbins = 1u << dbits;
     uint64_t ntiles = (n + TILE - 1) / TILE;
@@ -1856,17 +1615,14 @@ static void stable_partition_t(Workspace* ws, const Tup* in, uint64_t n,
         TraceScope ts(ws, "k_scatter", st);
         hipLaunchKernelGGL((k_scatter_u<THREADS, ITEMS, Digit, Pack>), dim3(nwg),
                            dim3(THREADS), ldsu, st, in, n, chunk, dig, nbins,
-                           counts, nwg, starts_dev, out, scatter_mode(), pk, bad_flag);
+                           counts, nwg, starts_dev, out, pk, bad_flag);
         SMJ_CHECK(hipGetLastError());
         return;
     } else {
-        // write-combining stable scatter (its own 512x8 geometry)
+        // write-combining stable scatter (its own 512x8 geometry; the
+        // histogram's chunking, so counts[d][wg] match)
         typedef SwcGeom<512, 8> SG;
-        if (stable_wc() && nbins <= 4 * 512 && SG::lds_bytes(nbins) <= 160 * 1024 &&
-            scatter_mode() == 0) {
-            const uint64_t tiles = (n + SG::TILE - 1) / SG::TILE;
-            uint32_t wg2 = nwg;  // the histogram's chunking: counts[d][wg] match
-            (void)tiles;
+        if (nbins <= 4 * 512 && SG::lds_bytes(nbins) <= 160 * 1024) {
             static bool attr_w = false;
             if (!attr_w) {
                 SMJ_CHECK(hipFuncSetAttribute(
@@ -1875,7 +1631,7 @@ static void stable_partition_t(Workspace* ws, const Tup* in, uint64_t n,
                 attr_w = true;
             }
             TraceScope ts(ws, "k_scatter", st);
-            hipLaunchKernelGGL((k_scatter_swc<512, 8, Digit>), dim3(wg2), dim3(512),
+            hipLaunchKernelGGL((k_scatter_swc<512, 8, Digit>), dim3(nwg), dim3(512),
                                SG::lds_bytes(nbins), st, in, n, chunk, dig, nbins, dbits,
                                counts, nwg, starts_dev, out);
             SMJ_CHECK(hipGetLastError());
@@ -1897,42 +1653,34 @@ static void stable_partition_t(Workspace* ws, const Tup* in, uint64_t n,
             TraceScope ts(ws, "k_scatter", st);
             hipLaunchKernelGGL((k_scatter<THREADS, ITEMS, Digit>), dim3(nwg),
                                dim3(THREADS), lds, st, in, n, chunk, dig, nbins, dbits,
-                               counts, nwg, starts_dev, out, scatter_mode());
+                               counts, nwg, starts_dev, out);
         }
     }
     SMJ_CHECK(hipGetLastError());
 }
 
-// ranks of the stable partition: lane-ordered LDS atomics (k_scatter_swa,
-// default) or ballot matching (k_scatter_swc: SMJ_STABLE_RANK=ballot)
-static bool atomic_ranks() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("SMJ_STABLE_RANK");
-        v = (e && !strcmp(e, "ballot")) ? 0 : 1;
-    }
-    return v != 0;
+// The ranks of k_scatter_swp rely on a hardware property (lanes of one LDS
+// atomic that hit the same word get their old values in lane order).  It is
+// checked on the device once per process, the first time a stable partition
+// runs; a device without it takes the ballot ranks of k_scatter_swc.
+static bool lds_order_ok(Workspace* ws, hipStream_t st) {
+    static const bool ok = [&] {
+        const uint64_t bad = lds_order_selfcheck(ws, st);
+        if (bad)
+            fprintf(stderr, "[WARN] smj: LDS atomics return %llu values out of lane order: "
+                            "the stable partition uses ballot ranks\n",
+                    (unsigned long long)bad);
+        return bad == 0;
+    }();
+    return ok;
 }
 
-// software-pipelined loads (k_hist_p: bit 0, k_scatter_swp: bit 1, k_hist_v's
-// 16-byte loads for 8-byte tuples: bit 2, non-temporal loads and stores in
-// k_scatter_swp and k_hist_p: bit 3); SMJ_SWA_PIPE selects, default 15 (0 =
-// the round-2 kernels k_hist_c + k_scatter_swa).  bench_partitioning 2^27 x 10
-// bits on MI355X, interleaved (tools/ab_swa.sh): 8 B 0.90 -> 0.82 ms (k_hist
-// 0.236 -> 0.160: 16-byte loads), 16 B 1.58 -> 1.49 ms (k_hist 0.424 -> 0.317:
-// non-temporal loads); the scatter itself gains 2-3 %
-static int swa_pipelined() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("SMJ_SWA_PIPE");
-        v = e ? atoi(e) : 15;
-    }
-    return v;
-}
-
-// histogram + scan + k_scatter_swa, one workgroup per CU (1 <= dbits <= 10)
+// histogram + scan + k_scatter_swp, one workgroup per CU (1 <= dbits <= 10).
+// bench_partitioning 2^27 x 10 bits on MI355X (round 2, tools/ab_swa.sh): the
+// 16-byte loads of k_hist_v took 8-byte tuples' histogram from 0.236 to
+// 0.160 ms, non-temporal loads 16-byte tuples' from 0.424 to 0.317 ms.
 template <class Digit>
-static void stable_partition_swa(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
+static void stable_partition_swp(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
                                  const Digit& dig, uint32_t dbits, int padded,
                                  uint64_t* starts_dev, int64_t* hist_out, int64_t* off_out,
                                  hipStream_t st) {
@@ -1952,23 +1700,14 @@ static void stable_partition_swa(Workspace* ws, const Tup* in, uint64_t n, Tup* 
         TraceScope ts(ws, "k_hist", st);
         bool vec = false;
         if constexpr (sizeof(Tup) == 8) {
-            vec = (swa_pipelined() & 4) && ((uintptr_t)in & 15) == 0 && (chunk & 1) == 0;
+            vec = ((uintptr_t)in & 15) == 0 && (chunk & 1) == 0;
             if (vec)
                 hipLaunchKernelGGL((k_hist_v<512, 8, Digit>), dim3(nwg), dim3(512),
                                    nbins * sizeof(uint32_t), st, in, n, chunk, dig, nbins,
                                    counts, nwg);
         }
-        if (vec) {
-        } else if (swa_pipelined() & 8)
+        if (!vec)
             hipLaunchKernelGGL((k_hist_p<512, 16, Digit, true>), dim3(nwg), dim3(512),
-                               nbins * sizeof(uint32_t), st, in, n, chunk, dig, nbins, counts,
-                               nwg);
-        else if (swa_pipelined() & 1)
-            hipLaunchKernelGGL((k_hist_p<512, 16, Digit, false>), dim3(nwg), dim3(512),
-                               nbins * sizeof(uint32_t), st, in, n, chunk, dig, nbins, counts,
-                               nwg);
-        else
-            hipLaunchKernelGGL((k_hist_c<512, 16, Digit>), dim3(nwg), dim3(512),
                                nbins * sizeof(uint32_t), st, in, n, chunk, dig, nbins, counts,
                                nwg);
     }
@@ -1981,28 +1720,14 @@ static void stable_partition_swa(Workspace* ws, const Tup* in, uint64_t n, Tup* 
     if (n == 0) return;
     static bool attr = false;
     if (!attr) {
-        SMJ_CHECK(hipFuncSetAttribute((const void*)k_scatter_swa<THREADS, ITEMS, Digit>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        SMJ_CHECK(hipFuncSetAttribute((const void*)k_scatter_swp<THREADS, ITEMS, Digit, false>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         SMJ_CHECK(hipFuncSetAttribute((const void*)k_scatter_swp<THREADS, ITEMS, Digit, true>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr = true;
     }
     TraceScope ts(ws, "k_scatter", st);
-    const int pairs_ok = (swa_pipelined() & 16) ? 0 : 1;
-    if (swa_pipelined() & 8)
-        hipLaunchKernelGGL((k_scatter_swp<THREADS, ITEMS, Digit, true>), dim3(nwg), dim3(THREADS),
-                           G::lds_bytes(nbins), st, in, n, chunk, dig, nbins, counts, nwg,
-                           starts_dev, out, pairs_ok);
-    else if (swa_pipelined() & 2)
-        hipLaunchKernelGGL((k_scatter_swp<THREADS, ITEMS, Digit, false>), dim3(nwg), dim3(THREADS),
-                           G::lds_bytes(nbins), st, in, n, chunk, dig, nbins, counts, nwg,
-                           starts_dev, out, pairs_ok);
-    else
-        hipLaunchKernelGGL((k_scatter_swa<THREADS, ITEMS, Digit>), dim3(nwg), dim3(THREADS),
-                           G::lds_bytes(nbins), st, in, n, chunk, dig, nbins, counts, nwg,
-                           starts_dev, out);
+    hipLaunchKernelGGL((k_scatter_swp<THREADS, ITEMS, Digit, true>), dim3(nwg), dim3(THREADS),
+                       G::lds_bytes(nbins), st, in, n, chunk, dig, nbins, counts, nwg,
+                       starts_dev, out, 1);
     SMJ_CHECK(hipGetLastError());
 }
 
@@ -2012,53 +1737,36 @@ static void stable_partition_narrow(Workspace* ws, const Tup* in, uint64_t n,
                                     int padded, uint64_t* starts_dev,
                                     int64_t* hist_out, int64_t* off_out,
                                     hipStream_t st) {
-    // positions are 32-bit inside k_scatter_swa; its LDS holds 2^10 digits
+    // positions are 32-bit inside k_scatter_swp; its LDS holds 2^10 digits
     typedef SwaGeom<512, sizeof(Tup) == 16 ? 8 : 16> SG;
-    if (atomic_ranks() && dbits >= 1 && dbits <= 10 && scatter_mode() == 0 &&
-        n + ((uint64_t)64 << dbits) < (1ull << 32) && SG::lds_bytes(1u << dbits) <= 160 * 1024) {
-        stable_partition_swa(ws, in, n, out, dig, dbits, padded, starts_dev, hist_out,
+    if (dbits >= 1 && dbits <= 10 && n + ((uint64_t)64 << dbits) < (1ull << 32) &&
+        SG::lds_bytes(1u << dbits) <= 160 * 1024 && lds_order_ok(ws, st)) {
+        stable_partition_swp(ws, in, n, out, dig, dbits, padded, starts_dev, hist_out,
                              off_out, st);
         return;
     }
     // the big tiles need the 16-bit per-wave counters and <= 160 KiB LDS
-    const int v = dbits > 10 ? 0 : pt_variant();
-    if (v == 2)
-        stable_partition_t<512, 16, true>(ws, in, n, out, dig, dbits, padded,
-                                          starts_dev, hist_out, off_out, st);
-    else if (v == 1)
-        stable_partition_t<256, 16, true>(ws, in, n, out, dig, dbits, padded,
-                                          starts_dev, hist_out, off_out, st);
+    if (dbits <= 10)
+        partition_hist_scatter<512, 16, true>(ws, in, n, out, dig, dbits, padded,
+                                              starts_dev, hist_out, off_out, st);
     else
-        stable_partition_t<256, 8, true>(ws, in, n, out, dig, dbits, padded,
-                                         starts_dev, hist_out, off_out, st);
+        partition_hist_scatter<256, 8, true>(ws, in, n, out, dig, dbits, padded,
+                                             starts_dev, hist_out, off_out, st);
 }
 
-// unstable variant (join level 1); SMJ_PTU_VARIANT picks the tile geometry
-static int ptu_variant() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("SMJ_PTU_VARIANT");
-        v = e ? atoi(e) : 2;  // measured: 512x16 tiles are fastest
-        if (v < 0 || v > 2) v = 2;
-    }
-    return v;
-}
-
+// unstable variant (the join's exact level-1 partition): 512 x 16 tiles
+// measured fastest (round 1)
 template <class Digit>
 static void unstable_partition(Workspace* ws, const Tup* in, uint64_t n,
                                Tup* out, const Digit& dig, uint32_t dbits,
                                uint64_t* starts_dev, int64_t* hist_out,
                                hipStream_t st) {
-    const int v = dbits > 10 ? 0 : ptu_variant();
-    if (v == 2)
-        stable_partition_t<512, 16, false>(ws, in, n, out, dig, dbits, 0, starts_dev,
-                                           hist_out, nullptr, st);
-    else if (v == 1)
-        stable_partition_t<256, 16, false>(ws, in, n, out, dig, dbits, 0, starts_dev,
-                                           hist_out, nullptr, st);
+    if (dbits <= 10)
+        partition_hist_scatter<512, 16, false>(ws, in, n, out, dig, dbits, 0, starts_dev,
+                                               hist_out, nullptr, st);
     else
-        stable_partition_t<256, 8, false>(ws, in, n, out, dig, dbits, 0, starts_dev,
-                                          hist_out, nullptr, st);
+        partition_hist_scatter<256, 8, false>(ws, in, n, out, dig, dbits, 0, starts_dev,
+                                              hist_out, nullptr, st);
 }
 
 void stable_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
@@ -2096,21 +1804,12 @@ void stable_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
     SMJ_CHECK(hipGetLastError());
 }
 
-// level-1 partition of the join/sort: range-plan digit, unpadded; the order
-// inside a partition is free (every bucket is fully sorted afterwards).
-// Histogram + write-combining scatter, one workgroup per CU and a long chunk
-// per workgroup (the carries pay off over many tiles).
-// measured: write combining pays for 16-byte tuples (4-tuple segments), not
-// for 8-byte ones; SMJ_SCATTER_WC overrides
-static int wc_enabled() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("SMJ_SCATTER_WC");
-        v = e ? atoi(e) : (sizeof(Tup) == 16 ? 1 : 0);
-    }
-    return v;
-}
-
+// Exact level-1 partition of the join/sort (range-plan digit, unpadded; the
+// order inside a partition is free: every bucket is fully sorted afterwards).
+// 16-byte tuples: histogram + write-combining scatter (4-tuple segments), one
+// workgroup per CU and a long chunk per workgroup (the carries pay off over
+// many tiles).  8-byte tuples: k_scatter_u (write combining measured no gain
+// for them, round 1).
 void plan_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
                     const RangePlan* plan_dev, uint32_t dbits,
                     uint64_t* starts_dev, int64_t* hist_out, hipStream_t st) {
@@ -2120,7 +1819,7 @@ void plan_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
     constexpr int ITEMS = sizeof(Tup) == 16 ? 8 : 16;
     constexpr int TILE = THREADS * ITEMS;
     const size_t lds = scatter_wc_lds<THREADS, ITEMS>(nbins);
-    if (!wc_enabled() || dbits > 10 || lds > 160 * 1024 || scatter_mode() != 0) {
+    if (sizeof(Tup) != 16 || dbits > 10 || lds > 160 * 1024) {
         unstable_partition(ws, in, n, out, dig, dbits, starts_dev, hist_out, st);
         return;
     }
@@ -2177,10 +1876,10 @@ void plan_partition_packed(Workspace* ws, const Tup* in, uint64_t n, uint64_t* o
     pk.s1 = pack_plan.s1;
     // the 16-byte stage of 512x16 tiles and 2^12 bins would exceed 160 KiB
     if (dbits > 10)
-        stable_partition_t<256, 8, false, PlanDigit1, LayPacked::Pack>(
+        partition_hist_scatter<256, 8, false, PlanDigit1, LayPacked::Pack>(
             ws, in, n, out, dig, dbits, 0, starts_dev, hist_out, nullptr, st, pk, pack_bad);
     else
-        stable_partition_t<512, 16, false, PlanDigit1, LayPacked::Pack>(
+        partition_hist_scatter<512, 16, false, PlanDigit1, LayPacked::Pack>(
             ws, in, n, out, dig, dbits, 0, starts_dev, hist_out, nullptr, st, pk, pack_bad);
 }
 #endif
@@ -2218,21 +1917,16 @@ static constexpr uint32_t kSampleStride = SMJ_SAMPLE_STRIDE;
 static constexpr uint32_t kSampleWg = SMJ_SAMPLE_WG;
 static constexpr uint64_t kRegionSlack = 1024;  // per shard
 
+// Upper bound of the regions k_regions lays out, in elements of the smallest
+// layout (8-byte words: the most per segment).  The blocked sample counts 4
+// tuples at every 4*stride-th position, so sample[] sums to at most
+// n/stride + 4 and the estimates to n + 4*stride; a shard's capacity is 9/8
+// of its estimate plus the slack, rounded up to a segment:
+//     sum <= (n + 4*stride) * 9/8 + 2^dbits * kShards * (slack + SEG - 1).
 uint64_t sampled_capacity(uint64_t n, uint32_t dbits) {
-    // in elements of the smallest layout (8-byte words: the most per segment)
     const uint64_t SEG = kSegBytes / 8;
-    return n + n / 8 + 2 * kSampleStride +
-           ((uint64_t)1 << dbits) * kShards * (kRegionSlack + 2 * SEG);
-}
-
-// 16-byte loads of tuple pairs in the 8-byte scatter (SMJ_SC_VEC=0: 8-byte loads)
-static bool sc_vec() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("SMJ_SC_VEC");
-        v = e ? atoi(e) : 1;
-    }
-    return v != 0;
+    return n + n / 8 + 5 * kSampleStride + 1 +
+           ((uint64_t)1 << dbits) * kShards * (kRegionSlack + SEG);
 }
 
 template <int ITEMS, class Pack>
@@ -2265,7 +1959,7 @@ static bool sampled_scatter_t(Workspace* ws, const Tup* in, uint64_t n, void* ou
     TraceScope ts(ws, "k_scatter", st);
     bool vec = false;
     if constexpr (VEC_OK) {
-        vec = sc_vec() && n % 2 == 0 && chunk % 2 == 0 && ((uintptr_t)in & 15) == 0;
+        vec = n % 2 == 0 && chunk % 2 == 0 && ((uintptr_t)in & 15) == 0;
         if (vec)
             hipLaunchKernelGGL((k_scatter_res<THREADS, ITEMS, PlanDigit1, Pack, true>), dim3(nwg),
                                dim3(THREADS), lds, st, in, n, chunk, dig, nbins, cursor,
@@ -2308,14 +2002,16 @@ void sampled_partition(Workspace* ws, int nrel, const Tup* const* in, const uint
                        unsigned int* sample, uint64_t* const* starts_dev,
                        int64_t* const* hist_out, uint64_t* const* seg_start,
                        int64_t* const* seg_cnt, unsigned int* flag_dev, hipStream_t st,
-                       const RangePlan* pack_plan, unsigned int* pack_bad) {
+                       const RangePlan* host_plan, bool packed, unsigned int* bad) {
     PlanDigit1 dig{plan_dev};
     const uint32_t nbins = 1u << dbits;
-#ifdef KEY_8B
-    const bool packed = pack_plan != nullptr;
-#else
-    const bool packed = false;
+#ifndef KEY_8B
+    packed = false;
 #endif
+    if (packed && !host_plan) {
+        fprintf(stderr, "[ERROR] smj: packed partition needs the host plan\n");
+        abort();
+    }
     static const char* cn[2] = {"sp_cursor0", "sp_cursor1"};
     static const char* en[2] = {"sp_capend0", "sp_capend1"};
     SampleRel S;
@@ -2361,18 +2057,22 @@ void sampled_partition(Workspace* ws, int nrel, const Tup* const* in, const uint
 #ifdef KEY_8B
         if (packed) {
             LayPacked::Pack pk;
-            pk.bu = key_u(pack_plan->base);
-            pk.span = pack_plan->span;
-            pk.s1 = pack_plan->s1;
+            pk.bu = key_u(host_plan->base);
+            pk.span = host_plan->span;
+            pk.s1 = host_plan->s1;
             sampled_scatter(ws, in[r], n[r], out[r], dig, nbins, R.cursor[r], R.cap_end[r], pk,
-                            pack_bad, st);
-        } else
-#endif
-        {
-            (void)pack_bad;
-            sampled_scatter(ws, in[r], n[r], out[r], dig, nbins, R.cursor[r], R.cap_end[r],
-                            PackNone(), (unsigned int*)nullptr, st);
+                            bad, st);
+            continue;
         }
+#endif
+        // tuples: range-checked against the host plan when a flag is given
+        PackRange pk{0ull, ~0ull};
+        if (bad && host_plan) {
+            pk.bu = key_u(host_plan->base);
+            pk.span = host_plan->span;
+        }
+        sampled_scatter(ws, in[r], n[r], out[r], dig, nbins, R.cursor[r], R.cap_end[r], pk,
+                        bad && host_plan ? bad : (unsigned int*)nullptr, st);
     }
     hipLaunchKernelGGL(k_regions_done, dim3(nrel), dim3(256), 0, st, R, nbins, flag_dev);
     SMJ_CHECK(hipGetLastError());

@@ -209,6 +209,10 @@ struct RefDigit {
 //   level-2 digit  d2 = (rel >> s2) - (d1 << D2)        (2^D2 per bucket)
 //   level-3 digit  d3 = (rel >> s3) - ((d1<<D2|d2) << D3)
 // ---------------------------------------------------------------------------
+// bits of a partition's "bad tuple" flag (status word 1 of a join)
+constexpr uint32_t kBadPayload = 1;  // a payload does not fit a packed word
+constexpr uint32_t kBadRange = 2;    // a key lies outside the plan range
+
 struct RangePlan {
     int64_t base;     // smallest key of the range
     uint64_t span;    // 2^L - 1 (all-ones of width L), L <= 64
@@ -305,17 +309,18 @@ struct LayPacked {
         return t;
     }
     // the level-1 partition's packing of tuple t into bucket rel >> s1;
-    // `bad` is set when t cannot be packed (key outside the plan, payload
-    // outside [0, 2^pb))
+    // `bad` gets kBadPayload when the payload lies outside [0, 2^pb) and
+    // kBadRange when the key lies outside the plan (t cannot be packed)
     struct Pack {
         typedef uint64_t OutT;
         uint64_t bu, span;
         uint32_t s1;
-        __device__ __forceinline__ uint64_t operator()(const Tup& t, bool& bad) const {
+        __device__ __forceinline__ uint64_t operator()(const Tup& t, uint32_t& bad) const {
             const uint64_t ku = key_u(t.key);
             const uint64_t r = ku - bu;
             const uint32_t pb = 64 - s1;
-            bad |= ku < bu || r > span || ((uint64_t)t.payload >> pb) != 0;
+            bad |= (ku < bu || r > span) ? kBadRange : 0u;
+            bad |= ((uint64_t)t.payload >> pb) != 0 ? kBadPayload : 0u;
             return ((r & ((1ull << s1) - 1)) << pb) | (uint64_t)t.payload;
         }
     };
@@ -327,7 +332,21 @@ struct LayPacked {
 // identity "packing" of the plain layout
 struct PackNone {
     typedef Tup OutT;
-    __device__ __forceinline__ Tup operator()(const Tup& t, bool&) const { return t; }
+    __device__ __forceinline__ Tup operator()(const Tup& t, uint32_t&) const { return t; }
+};
+
+// the plain layout with a range check: kBadRange when the key lies outside
+// [bu, bu + span] (key_u order).  A plan guessed from the relation size (the
+// reference's own assumption, keys <= |R|) is verified this way in the pass
+// that reads every key anyway; bu = 0, span = ~0 checks nothing.
+struct PackRange {
+    typedef Tup OutT;
+    uint64_t bu, span;
+    __device__ __forceinline__ Tup operator()(const Tup& t, uint32_t& bad) const {
+        const uint64_t ku = key_u(tup_key(t));
+        bad |= (ku < bu || ku - bu > span) ? kBadRange : 0u;
+        return t;
+    }
 };
 
 __host__ __device__ __forceinline__ uint32_t plan_d2(const RangePlan& p,

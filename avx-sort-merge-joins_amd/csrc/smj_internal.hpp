@@ -5,6 +5,8 @@
 #include <string>
 #include <vector>
 
+#include <hip/hip_ext.h>
+
 #include "smj_common.hpp"
 
 namespace smj {
@@ -154,6 +156,22 @@ struct Workspace {
     void trace_end(int idx, hipStream_t st) {
         if (idx >= 0) SMJ_CHECK(hipEventRecord(trace[idx].b, st));
     }
+    // a trace record whose events the runtime stamps at the kernel's own start
+    // and end (hipExtLaunchKernelGGL): no event-record gap around short kernels
+    bool trace_ext(const char* name, hipEvent_t* a, hipEvent_t* b) {
+        if (!trace_on) return false;
+        if (trace_n == trace.size()) {
+            TraceRec r;
+            SMJ_CHECK(hipEventCreate(&r.a));
+            SMJ_CHECK(hipEventCreate(&r.b));
+            trace.push_back(r);
+        }
+        trace[trace_n].name = name;
+        *a = trace[trace_n].a;
+        *b = trace[trace_n].b;
+        trace_n++;
+        return true;
+    }
 
     ~Workspace() {
         for (auto& r : trace) {
@@ -178,6 +196,19 @@ struct TraceScope {
     }
 };
 
+// One traced kernel launch: with tracing on, the trace events are stamped by
+// the launch itself (kernel-exact, like the profiler's kernel trace).
+template <typename... KArgs, typename... Args>
+inline void traced_launch(Workspace* ws, const char* name, void (*kernel)(KArgs...),
+                          dim3 grid, dim3 block, uint32_t shmem, hipStream_t st,
+                          Args... args) {
+    hipEvent_t a, b;
+    if (ws && ws->trace_ext(name, &a, &b))
+        hipExtLaunchKernelGGL(kernel, grid, block, shmem, st, a, b, 0u, (KArgs)args...);
+    else
+        hipLaunchKernelGGL(kernel, grid, block, shmem, st, (KArgs)args...);
+}
+
 // ---- partition.hip
 void stable_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
                       const Digit32& dig, uint32_t dbits, int padded,
@@ -199,20 +230,22 @@ uint64_t sampled_capacity(uint64_t n, uint32_t dbits);
 #endif
 constexpr uint32_t kShards = SMJ_SHARDS;
 // Sampled level-1 partition of nrel (1 or 2) relations in shared launches.
-// out[r] holds sampled_capacity() elements: tuples, or (pack_plan != nullptr,
-// 16-byte tuples only) LayPacked words for that plan; *pack_bad is OR-ed with
-// 1 when a tuple cannot be packed (the caller then repeats on tuples).
-// `sample` = nrel * 2^dbits counters, zeroed by the caller (k_join_begin).
+// out[r] holds sampled_capacity() elements: tuples, or (packed, 16-byte tuples
+// only) LayPacked words for host_plan.  When `bad` is given, *bad is OR-ed
+// with kBadPayload (a payload does not pack) and kBadRange (a key lies
+// outside host_plan): packed words need both, tuples are range-checked when
+// the plan was guessed.  `sample` = nrel * 2^dbits counters, zeroed by the
+// caller (k_join_begin).
 void sampled_partition(Workspace* ws, int nrel, const Tup* const* in, const uint64_t* n,
                        void* const* out, const RangePlan* plan_dev, uint32_t dbits,
                        unsigned int* sample, uint64_t* const* starts_dev,
                        int64_t* const* hist_out, uint64_t* const* seg_start,
                        int64_t* const* seg_cnt, unsigned int* flag_dev, hipStream_t st,
-                       const RangePlan* pack_plan = nullptr,
-                       unsigned int* pack_bad = nullptr);
+                       const RangePlan* host_plan = nullptr, bool packed = false,
+                       unsigned int* bad = nullptr);
 void hist_memcpy(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
                  uint32_t dbits, hipStream_t st);
-// lane order of LDS atomic returns (k_scatter_swa's ranks): violations, 0 expected
+// lane order of LDS atomic returns (k_scatter_swp's ranks): violations, 0 expected
 uint64_t lds_order_selfcheck(Workspace* ws, hipStream_t st);
 
 // ---- bucketsort.hip : MSD bucket sort (+ fused merge-join count)
@@ -246,6 +279,9 @@ struct BucketSortArgs {
     // pack_bad, [2] = the skew queue length (read back in one copy)
     unsigned int* status = nullptr;
     const unsigned int* pack_bad = nullptr;  // set by the partition: not packable
+    // host copy of status words [0] and [1] after a false return (why the
+    // attempt was void: overflow, kBadPayload / kBadRange)
+    uint32_t* status_out = nullptr;
     // the 32-bit digit fast path of the tile and group passes (keys outside
     // the plan range only in the first and the last bucket); the segmented
     // join turns it off for tuples (a caller's key outside its range could sit

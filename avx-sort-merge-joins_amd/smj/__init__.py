@@ -60,7 +60,7 @@ DEVICE_SYMBOLS = [
     "smj_trace_enable", "smj_trace_reset", "smj_trace_read", "smj_dev_join_segmented",
     "smj_dev_partition_range_packed", "smj_dev_materialize", "smj_selfcheck_lds_order",
     "smj_set_materialize", "smj_dev_join_segmented_tables", "smj_dev_partition_range_sampled",
-    "smj_sampled_capacity", "smj_sampled_shards",
+    "smj_sampled_capacity", "smj_sampled_shards", "smj_context_workspace",
 ]
 
 
@@ -180,6 +180,7 @@ class Library:
             "smj_sampled_shards": (_U32, []),
             "smj_dev_materialize": (_U64, [_P, _P, _U64, _P, _U64, _P, _U64, _P]),
             "smj_selfcheck_lds_order": (_U64, [_P, _P]),
+            "smj_context_workspace": (_P, []),
             "smj_trace_enable": (None, [_P, C.c_int]),
             "smj_trace_reset": (None, [_P]),
             "smj_trace_read": (C.c_int, [_P, C.c_char_p, C.c_int, _P, _P, C.c_int]),

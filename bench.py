@@ -67,6 +67,11 @@ def parse():
     p.add_argument("--exchange-path", action="store_true",
                    help="run the multi-GPU code path (range partition, all-to-all, "
                         "segmented local join) even at N=1 (a one-rank RCCL group)")
+    p.add_argument("--api", action="store_true",
+                   help="join: time the reference-named entry point sortmergejoin_multiway "
+                        "(relation_t over device-resident tuples, no key-range hint: the "
+                        "plan is derived from |R| as the reference does) instead of "
+                        "smj_dev_join")
     return p.parse_args()
 
 
@@ -254,7 +259,29 @@ def main():
     torch.cuda.synchronize()
 
     count = torch.zeros(1, dtype=torch.int64, device="cuda")
-    if not exchange:
+    tracer = lib
+    if a.api and not exchange:
+        # sortmergejoin_multiway(relation_t*, relation_t*, joinconfig_t*) on
+        # hipMalloc'd tuples (used in place, no PCIe); the reference's default
+        # configuration (src/main.c: PARTFANOUT 128), one thread
+        import ctypes
+        os.environ["SMJ_QUIET"] = "1"  # no per-call stats lines in the timed loop
+        rR = smj.Relation(R.data_ptr(), n)
+        rS = smj.Relation(S.data_ptr(), n)
+        cfg = smj.JoinConfig(1, 128, int(w == 16), int(w == 16), 20 << 20, 2)
+        libc = ctypes.CDLL(None)
+        libc.free.argtypes = [ctypes.c_void_p]
+        api_count = [0]
+
+        def step():
+            res = lib.lib.sortmergejoin_multiway(ctypes.byref(rR), ctypes.byref(rS),
+                                                 ctypes.byref(cfg))
+            api_count[0] = int(res.contents.totalresults)
+            libc.free(res.contents.resultlist)
+            libc.free(ctypes.cast(res, ctypes.c_void_p))
+
+        tracer = _WsTracer(lib, lib.lib.smj_context_workspace())
+    elif not exchange:
         sR, sS = lib.empty(n), lib.empty(n)
 
         def step():
@@ -270,7 +297,9 @@ def main():
         if exchange:
             dj.stats_reset()
 
-    elapsed, kern = timed_loop(a, lib, dist, step, reset)
+    elapsed, kern = timed_loop(a, tracer, dist, step, reset)
+    if a.api and not exchange:
+        count.fill_(api_count[0])
 
     xchg = None
     if exchange:
@@ -325,6 +354,8 @@ def main():
                                 if strong else
                                 f"sortmergejoin_multiway R={n} S={n} per GPU")
                                + f", {w}-byte tuples, {a.dist}"
+                               + (" (reference entry point sortmergejoin_multiway, "
+                                  "no key-range hint)" if a.api else "")
                                + (f" theta={a.theta}" if a.dist == "zipf" else "")
                                + ", PK/FK keys 1..|R|",
                    "tuples_per_relation_per_gpu": n, "tuples_per_relation_total": total,
@@ -346,6 +377,25 @@ def main():
     print(json.dumps(out), file=json_out, flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+class _WsTracer:
+    """smj_trace_* on another workspace of the library (the calling thread's
+    context behind the reference-named entry points)."""
+
+    def __init__(self, lib, ws):
+        self.lib, self.ws = lib, ws
+
+    def trace(self, on):
+        self.lib.lib.smj_trace_enable(self.ws, int(on))
+        self.lib.lib.smj_trace_reset(self.ws)
+
+    def trace_read(self):
+        saved, self.lib._ws = self.lib._ws, self.ws
+        try:
+            return self.lib.trace_read()
+        finally:
+            self.lib._ws = saved
 
 
 def timed_loop(a, lib, dist, step, reset=None):

@@ -524,9 +524,16 @@ uint32_t smj_sampled_shards(void);
 
 /* Self-check of the hardware property behind the stable partition's ranks:
  * LDS atomic adds return their old values to the lanes of one instruction
- * that hit the same word in lane order (partition.hip, k_scatter_swa).
- * Returns the number of violations (0 expected; synchronises `stream`). */
+ * that hit the same word in lane order (partition.hip, k_scatter_swp).
+ * Returns the number of violations (0 expected; synchronises `stream`).  The
+ * library runs it once per process before its first stable partition and
+ * falls back to ballot ranks on a device without the property. */
 uint64_t smj_selfcheck_lds_order(smj_workspace * ws, smj_stream_t stream);
+
+/* The calling thread's workspace behind the reference-named entry points
+ * (sortmergejoin_multiway, avxsort_tuples, ...): lets a caller trace their
+ * kernels with smj_trace_* (bench.py --api). */
+smj_workspace * smj_context_workspace(void);
 
 /* Per-kernel HIP-event trace of the join pipeline (bench.py roofline). */
 void smj_trace_enable(smj_workspace * ws, int on);

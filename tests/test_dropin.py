@@ -3,8 +3,10 @@ compiled unchanged from their sources against include/compat/ and linked with
 libsmj_hip[_k8].so (oracle/build_dropin.sh, run by __graft_entry__.build()
 where /root/reference exists; the binaries travel with the tree).
 
-check_merge.c is not built: it unit-tests the reference's AVX merge kernels
-through avxsort_core.h (internal to the AVX implementation), not the API."""
+check_merge.c unit-tests the reference's AVX merge kernels through
+avxsort_core.h, internal to the AVX implementation; include/compat/
+avxsort_core.h maps those kernel names onto the device merges, so it is built
+and run too (check_merge8)."""
 import os
 import re
 import subprocess

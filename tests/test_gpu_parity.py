@@ -8,6 +8,8 @@ tests/golden/), plus the edge cases those suites never hit: empty and tiny
 inputs, ragged sizes, negative/full-range keys, heavy duplicates (Zipf), wide
 digits.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -470,3 +472,114 @@ def test_device_join_packed_words(libs, oracles, width, payload):
         assert int(cnt.item()) == exp
         assert np.array_equal(lib.to_host(sR), eR)
         assert np.array_equal(lib.to_host(sS), eS)
+
+
+# ------------------------------------------- reference entry points, no hint
+def _api_join_device(lib, dR, dS, nthreads=1):
+    """sortmergejoin_multiway on relation_t over device-resident tuples (the
+    library uses them in place, bench.py --api)."""
+    import ctypes
+    import smj
+    os.environ["SMJ_QUIET"] = "1"
+    rR = smj.Relation(dR.data_ptr(), dR.shape[0])
+    rS = smj.Relation(dS.data_ptr(), dS.shape[0])
+    cfg = smj.JoinConfig(nthreads, 128, int(lib.width == 16), int(lib.width == 16), 20 << 20, 2)
+    res = lib.lib.sortmergejoin_multiway(ctypes.byref(rR), ctypes.byref(rS), ctypes.byref(cfg))
+    total = int(res.contents.totalresults)
+    libc = ctypes.CDLL(None)
+    libc.free.argtypes = [ctypes.c_void_p]
+    libc.free(res.contents.resultlist)
+    libc.free(ctypes.cast(res, ctypes.c_void_p))
+    return total
+
+
+@pytest.mark.parametrize("case", ["pk_fk", "s_above", "r_negative", "wide_payload", "zipf"])
+def test_api_join_size_guess(libs, oracles, width, case):
+    """sortmergejoin_multiway takes no key-range hint: its plan is guessed from
+    |R| (keys 1..|R|, the reference's own assumption,
+    src/joins/sortmergejoin_multiway.c:372-376) and verified by the level-1
+    scatter.  Keys outside the guess (above |R|, negative) send the join back
+    to the exact key range; an unpackable payload (16 B) to tuples.  The count
+    and the device-resident form must match the oracle either way."""
+    import torch
+    orc, lib = oracles[width], libs[width]
+    n = 400_000
+    R, S = make_join_inputs(orc, width, "zipf" if case == "zipf" else "pk_fk", n, n)
+    if case == "s_above":
+        S["key"][::1000] = n + 17
+    elif case == "r_negative":
+        R["key"][5] = -3
+    elif case == "wide_payload" and width == 16:
+        R["payload"][9] = np.int64(1) << 61
+    exp, _, _ = orc.sortmergejoin(R, S)
+    assert lib.sortmergejoin_multiway(R, S) == exp  # host buffers (staged)
+    dR, dS = lib.to_device(R), lib.to_device(S)
+    for _ in range(2):  # the second call reuses the context's workspace
+        assert _api_join_device(lib, dR, dS) == exp
+    torch.cuda.synchronize()
+    assert np.array_equal(lib.to_host(dR), R)  # inputs untouched
+
+
+@pytest.mark.parametrize("case", ["pk", "one_above", "negative", "wide_payload"])
+def test_sort_size_guess(libs, oracles, width, case):
+    """avxsort_tuples guesses keys 1..n (create_relation_pk's shape) and falls
+    back to the exact key range when a key lies outside."""
+    orc, lib = oracles[width], libs[width]
+    n = 300_001
+    orc.seed(777)
+    t = orc.create_relation_pk(n)
+    t["payload"] = np.arange(n) + 5
+    if case == "one_above":
+        t["key"][n // 2] = 3 * n
+    elif case == "negative":
+        t["key"][:10] = -np.arange(10)
+    elif case == "wide_payload" and width == 16:
+        t["payload"][3] = np.int64(1) << 62
+    assert np.array_equal(lib.avxsort_tuples(t), orc.sort(t))
+
+
+@pytest.mark.parametrize("nbits", [0, 1, 2, 3])
+@pytest.mark.parametrize("n", [1, 513, 4097, 65536 + 511, 1 << 20])
+@pytest.mark.parametrize("packed", [False, True])
+def test_partition_range_sampled_small_bits(libs, oracles, width, nbits, n, packed):
+    """smj_dev_partition_range_sampled at few partitions, where the sample's
+    overestimate is largest against the per-region slack: every region must
+    stay inside smj_sampled_capacity() (a canary after it stays intact) and
+    the partitions must hold exactly the input, each key in its range."""
+    import torch
+    orc, lib = oracles[width], libs[width]
+    if packed and width != 16:
+        pytest.skip("packed words are the 16-byte layout")
+    orc.seed(99 + n)
+    t = orc.create_relation_pk(n)
+    d_in = lib.to_device(t)
+    F, K = 1 << nbits, lib.sampled_shards()
+    cap = lib.sampled_capacity(n, nbits)
+    canary = 4096
+    if packed:
+        buf = torch.full((cap + canary,), -7, dtype=torch.int64, device="cuda")
+    else:
+        buf = lib.empty(cap + canary)
+        buf.fill_(-7)
+    ss = torch.empty(F * K, dtype=torch.int64, device="cuda")
+    sc = torch.empty(F * K, dtype=torch.int64, device="cuda")
+    fl = torch.ones(2, dtype=torch.int32, device="cuda")
+    assert lib.dev_partition_range_sampled(d_in, buf, nbits, 1, n, packed, ss, sc, fl)
+    torch.cuda.synchronize()
+    assert fl.tolist() == [0, 0]
+    assert int(sc.sum()) == n
+    assert bool((buf[cap:] == -7).all())
+    ssh, sch = ss.cpu().numpy(), sc.cpu().numpy()
+    assert int((ssh + sch).max()) <= cap
+    if packed:
+        return  # the word layout is covered by the exchange tests
+    h = lib.to_host(buf[:cap])
+    keys = []
+    s1 = max(int(n - 1).bit_length() - nbits, 0)  # make_plan over [1, n]
+    for i in range(F * K):
+        seg = h[ssh[i]:ssh[i] + sch[i]]
+        p = i // K
+        rel = seg["key"].astype(np.int64) - 1
+        assert np.all(np.minimum(rel >> s1, F - 1) == p)
+        keys.append(seg["key"])
+    assert np.array_equal(np.sort(np.concatenate(keys)), np.arange(1, n + 1))
