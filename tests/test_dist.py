@@ -217,6 +217,15 @@ def _worker(rank, world, port, n, q, s_payload="negative", mode="sampled"):
             assert bool((own[d] == rank).all())
             k = got[:, 1]
             assert bool((k[1:] >= k[:-1]).all())
+        # the row exchange alone (bench.py --op exchange repeats it): the last
+        # step's transfer again lands the same rows in the same places, and the
+        # own chunk is never copied
+        xb, cap, cs, sl, rl = dj.last_rows["S"]
+        remote = sum(rl) - rl[rank]
+        before = xb[:cap + remote].clone()
+        xb[cap:cap + remote] = -9
+        dj._rows(xb, cap, cs, sl, rl).wait()
+        assert torch.equal(xb[:cap + remote], before)
         # no row lost or duplicated
         sizes = torch.tensor([sR.shape[0], sS.shape[0]])
         dist.all_reduce(sizes)

@@ -566,9 +566,14 @@ def test_partition_range_sampled_small_bits(libs, oracles, width, nbits, n, pack
     fl = torch.ones(2, dtype=torch.int32, device="cuda")
     assert lib.dev_partition_range_sampled(d_in, buf, nbits, 1, n, packed, ss, sc, fl)
     torch.cuda.synchronize()
+    assert bool((buf[cap:] == -7).all())
+    if fl[0]:
+        # a region overflowed (few workgroups fill few of a partition's shards:
+        # the join then repeats the exact partition); nothing passed the buffer
+        assert n < 1 << 20
+        return
     assert fl.tolist() == [0, 0]
     assert int(sc.sum()) == n
-    assert bool((buf[cap:] == -7).all())
     ssh, sch = ss.cpu().numpy(), sc.cpu().numpy()
     assert int((ssh + sch).max()) <= cap
     if packed:
