@@ -1595,6 +1595,22 @@ void smj_dev_gen_zipf(smj_workspace* ws, tuple_t* out, uint64_t n,
              (hipStream_t)stream);
 }
 
+void smj_dev_gen_nonunique(smj_workspace* ws, tuple_t* out, uint64_t n, uint64_t first,
+                           uint64_t total, int64_t maxid, uint32_t seed, uint64_t skip,
+                           smj_stream_t stream) {
+    gen_nonunique_ref((Workspace*)ws, (Tup*)out, n, first, total, maxid, seed, skip,
+                      (hipStream_t)stream);
+}
+
+void smj_dev_gen_zipf_ref(smj_workspace* ws, tuple_t* out, uint64_t n, uint64_t first,
+                          uint64_t maxid, double theta, uint32_t seed, uint64_t skip,
+                          smj_stream_t stream) {
+    gen_zipf_ref((Workspace*)ws, (Tup*)out, n, first, maxid, theta, seed, skip,
+                 (hipStream_t)stream);
+}
+
+uint32_t smj_glibc_rand(uint32_t seed, uint64_t k) { return glibc_rand_at(seed, k); }
+
 void smj_dev_synchronize(smj_stream_t stream) {
     SMJ_CHECK(hipStreamSynchronize((hipStream_t)stream));
 }

@@ -209,6 +209,13 @@ inline void traced_launch(Workspace* ws, const char* name, void (*kernel)(KArgs.
         hipLaunchKernelGGL(kernel, grid, block, shmem, st, (KArgs)args...);
 }
 
+// ---- refgen.hip : the reference's rand()-driven generators, bit-exact
+uint32_t glibc_rand_at(uint32_t seed, uint64_t k);  // the k-th rand() after srand(seed)
+void gen_nonunique_ref(Workspace* ws, Tup* out, uint64_t n, uint64_t first, uint64_t total,
+                       int64_t maxid, uint32_t seed, uint64_t skip, hipStream_t st);
+void gen_zipf_ref(Workspace* ws, Tup* out, uint64_t n, uint64_t first, uint64_t maxid,
+                  double theta, uint32_t seed, uint64_t skip, hipStream_t st);
+
 // ---- partition.hip
 void stable_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
                       const Digit32& dig, uint32_t dbits, int padded,

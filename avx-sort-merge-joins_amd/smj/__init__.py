@@ -61,6 +61,7 @@ DEVICE_SYMBOLS = [
     "smj_dev_partition_range_packed", "smj_dev_materialize", "smj_selfcheck_lds_order",
     "smj_set_materialize", "smj_dev_join_segmented_tables", "smj_dev_partition_range_sampled",
     "smj_sampled_capacity", "smj_sampled_shards", "smj_context_workspace",
+    "smj_dev_gen_nonunique", "smj_dev_gen_zipf_ref", "smj_glibc_rand",
 ]
 
 
@@ -181,6 +182,10 @@ class Library:
             "smj_dev_materialize": (_U64, [_P, _P, _U64, _P, _U64, _P, _U64, _P]),
             "smj_selfcheck_lds_order": (_U64, [_P, _P]),
             "smj_context_workspace": (_P, []),
+            "smj_dev_gen_nonunique": (None, [_P, _P, _U64, _U64, _U64, _I64, _U32, _U64, _P]),
+            "smj_dev_gen_zipf_ref": (None, [_P, _P, _U64, _U64, _U64, C.c_double, _U32, _U64,
+                                            _P]),
+            "smj_glibc_rand": (_U32, [_U32, _U64]),
             "smj_trace_enable": (None, [_P, C.c_int]),
             "smj_trace_reset": (None, [_P]),
             "smj_trace_read": (C.c_int, [_P, C.c_char_p, C.c_int, _P, _P, C.c_int]),
@@ -371,6 +376,21 @@ class Library:
     def dev_gen_zipf(self, out, first, maxid, theta, seed):
         self.lib.smj_dev_gen_zipf(self.ws, out.data_ptr(), out.shape[0], first, maxid,
                                   theta, seed, self.stream_ptr())
+
+    def dev_gen_nonunique(self, out, first, total, maxid, seed, skip=0):
+        """create_relation_nonunique after srand(seed) and `skip` rand() calls,
+        tuples [first, first + len(out)) of `total` (bit-exact, refgen.hip)."""
+        self.lib.smj_dev_gen_nonunique(self.ws, out.data_ptr(), out.shape[0], first, total,
+                                       maxid, seed, skip, self.stream_ptr())
+
+    def dev_gen_zipf_ref(self, out, first, maxid, theta, seed, skip=0):
+        """create_relation_zipf after srand(seed) and `skip` rand() calls
+        (bit-exact; the payload is 0)."""
+        self.lib.smj_dev_gen_zipf_ref(self.ws, out.data_ptr(), out.shape[0], first, maxid,
+                                      theta, seed, skip, self.stream_ptr())
+
+    def glibc_rand(self, seed, k):
+        return int(self.lib.smj_glibc_rand(seed, k))
 
     def dev_sort(self, inp, out):
         self.lib.smj_dev_sort(self.ws, inp.data_ptr(), inp.shape[0], out.data_ptr(),

@@ -56,6 +56,10 @@ def parse():
     p.add_argument("--shift", type=int, default=0, help="partition: shift bits")
     p.add_argument("--dist", default="uniform", choices=("uniform", "zipf"))
     p.add_argument("--theta", type=float, default=0.75)
+    p.add_argument("--zipf-gen", default="reference", choices=("reference", "fast"),
+                   help="zipf S: the reference's own create_relation_zipf after "
+                        "srand(54321), bit-exact (refgen.hip; the alphabet and CDF table "
+                        "are built on the host), or the fast rejection-inversion sampler")
     p.add_argument("--fanout-bits", type=int, default=8,
                    help="level-1 partitions (2^bits) of the join; the library raises it "
                         "as the relation size needs")
@@ -254,6 +258,8 @@ def main():
     lib.dev_gen_pk(R, first, total, 12345)
     if a.dist == "uniform":
         lib.dev_gen_fk(S, first, total, total, 54321)
+    elif a.zipf_gen == "reference":
+        lib.dev_gen_zipf_ref(S, first, total, a.theta, 54321)
     else:
         lib.dev_gen_zipf(S, first, total, a.theta, 54321)
     torch.cuda.synchronize()
@@ -356,7 +362,8 @@ def main():
                                + f", {w}-byte tuples, {a.dist}"
                                + (" (reference entry point sortmergejoin_multiway, "
                                   "no key-range hint)" if a.api else "")
-                               + (f" theta={a.theta}" if a.dist == "zipf" else "")
+                               + (f" theta={a.theta} ({'create_relation_zipf, srand(54321)' if a.zipf_gen == 'reference' else 'rejection-inversion sampler'})"
+                                  if a.dist == "zipf" else "")
                                + ", PK/FK keys 1..|R|",
                    "tuples_per_relation_per_gpu": n, "tuples_per_relation_total": total,
                    "tuple_bytes": w,

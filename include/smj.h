@@ -444,6 +444,26 @@ void smj_dev_gen_zipf(smj_workspace * ws, tuple_t * out, uint64_t n,
                       uint64_t first, uint64_t maxid, double theta,
                       uint64_t seed, smj_stream_t stream);
 
+/* The reference's own rand()-driven generators, bit-exact (refgen.hip): the
+ * relation create_relation_nonunique / create_relation_zipf would produce
+ * after srand(seed) and `skip` earlier rand() calls (generator.c:220-231,
+ * 490-505; genzipf.c:28-159, generator.c:517-534), shard [first, first + n) of
+ * a relation of `total` tuples.  glibc rand()'s additive stream is jumped
+ * ahead per shard (31 x 31 matrix powers); the Zipf alphabet and CDF table are
+ * built on the host in the reference's order and cached per workspace.
+ * nonunique: key = RAND_RANGE(maxid), payload = total - index, avoid_NaN;
+ * zipf_ref : key = alphabet[CDF^-1(rand() / RAND_MAX)], payload 0
+ *            (maxid < 2^32). */
+void smj_dev_gen_nonunique(smj_workspace * ws, tuple_t * out, uint64_t n, uint64_t first,
+                           uint64_t total, int64_t maxid, uint32_t seed, uint64_t skip,
+                           smj_stream_t stream);
+void smj_dev_gen_zipf_ref(smj_workspace * ws, tuple_t * out, uint64_t n, uint64_t first,
+                          uint64_t maxid, double theta, uint32_t seed, uint64_t skip,
+                          smj_stream_t stream);
+/* The k-th rand() value after srand(seed) (k = 0 is the first call), by the
+ * same jump-ahead, on the host (no device needed). */
+uint32_t smj_glibc_rand(uint32_t seed, uint64_t k);
+
 void smj_dev_synchronize(smj_stream_t stream);
 
 /* Multi-GPU building block: stable partition of a device relation into

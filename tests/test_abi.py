@@ -66,3 +66,24 @@ def test_product_does_not_reference_oracle():
             if f.endswith((".py", ".hip", ".hpp", ".h", ".cpp")) or f == "Makefile":
                 text = open(os.path.join(root, f), errors="ignore").read()
                 assert "oracle" not in text.replace("no oracle", ""), os.path.join(root, f)
+
+
+@pytest.mark.parametrize("width", [8, 16])
+def test_glibc_rand_jump_ahead(smj_mod, width):
+    """smj_glibc_rand (the jump-ahead behind the reference-exact device
+    generators, refgen.hip) against glibc's own srand/rand, host only: every
+    position of the first 4000 draws for several seeds (0 is glibc's 1), and
+    deep positions reached by stepping glibc itself."""
+    L = smj_mod.Library(width)
+    libc = ctypes.CDLL(None)
+    libc.srand.argtypes = [ctypes.c_uint]
+    for seed in (0, 1, 777, 12345, 54321, 2 ** 31 + 5):
+        libc.srand(seed)
+        ref = [libc.rand() for _ in range(4000)]
+        got = [L.glibc_rand(seed, k) for k in range(0, 4000, 7)]
+        assert got == ref[::7], seed
+    libc.srand(4242)
+    for k in range(1_000_000):
+        x = libc.rand()
+        if k in (65535, 65536, 999_999):
+            assert L.glibc_rand(4242, k) == x, k

@@ -174,3 +174,27 @@ def test_golden_big_multiway(width, libs, oracles, k, maxlen):
     out, n, consumed = libs[width].avx_multiway_merge(runs)
     assert n == int(g[f"w{width}_mw{k}_n"][0]) and consumed
     check_big(width, out, g, f"w{width}_mw{k}")
+
+
+def test_reference_generators_on_device(gcase):
+    """The reference's create_relation_nonunique and create_relation_zipf
+    reproduced on the device (refgen.hip: glibc rand() jumped ahead per shard)
+    against the vectors the compiled reference wrote (make_golden.py: srand
+    then one call, skip 0): bit-exact, also when generated as two shards."""
+    import torch
+    _, lib, g = gcase
+    exp = g["gen_nonunique"]
+    t = lib.empty(len(exp))
+    lib.dev_gen_nonunique(t, 0, len(exp), 300, 54321)
+    torch.cuda.synchronize()
+    assert np.array_equal(lib.to_host(t), exp)
+    a, b = lib.empty(333), lib.empty(len(exp) - 333)
+    lib.dev_gen_nonunique(a, 0, len(exp), 300, 54321)
+    lib.dev_gen_nonunique(b, 333, len(exp), 300, 54321)
+    torch.cuda.synchronize()
+    assert np.array_equal(np.concatenate([lib.to_host(a), lib.to_host(b)]), exp)
+    exp = g["gen_zipf"]
+    z = lib.empty(len(exp))
+    lib.dev_gen_zipf_ref(z, 0, 500, 0.75, 777)
+    torch.cuda.synchronize()
+    assert np.array_equal(lib.to_host(z), exp)

@@ -588,3 +588,33 @@ def test_partition_range_sampled_small_bits(libs, oracles, width, nbits, n, pack
         assert np.all(np.minimum(rel >> s1, F - 1) == p)
         keys.append(seg["key"])
     assert np.array_equal(np.sort(np.concatenate(keys)), np.arange(1, n + 1))
+
+
+@pytest.mark.parametrize("kind,n,maxid,skip,first", [
+    ("nonunique", 1 << 20, 1 << 20, 0, 0), ("nonunique", 1 << 20, 1000, 17, 0),
+    ("nonunique", 300001, 1 << 20, 0, 700000), ("zipf", 1 << 20, 1 << 20, 0, 0),
+    ("zipf", 250000, 100000, 5, 123457)])
+def test_reference_generators_vs_oracle(libs, oracles, width, kind, n, maxid, skip, first):
+    """refgen.hip against the oracle's glibc-driven restatement of the
+    reference generators (pinned to the compiled reference by the golden
+    vectors): a 1M-tuple relation, an inner shard [first, first + n) of a
+    larger one, and `skip` rand() calls consumed before the relation."""
+    import ctypes
+    import torch
+    lib, orc = libs[width], oracles[width]
+    total = first + n + 1000
+    libc = ctypes.CDLL(None)
+    orc.seed(4242)
+    for _ in range(skip):
+        libc.rand()
+    if kind == "nonunique":
+        exp = orc.create_relation_nonunique(total, maxid)
+    else:
+        exp = orc.create_relation_zipf(total, maxid, 0.75)
+    t = lib.empty(n)
+    if kind == "nonunique":
+        lib.dev_gen_nonunique(t, first, total, maxid, 4242, skip)
+    else:
+        lib.dev_gen_zipf_ref(t, first, maxid, 0.75, 4242, skip)
+    torch.cuda.synchronize()
+    assert np.array_equal(lib.to_host(t), exp[first:first + n])
