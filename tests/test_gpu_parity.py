@@ -564,7 +564,10 @@ def test_partition_range_sampled_small_bits(libs, oracles, width, nbits, n, pack
     ss = torch.empty(F * K, dtype=torch.int64, device="cuda")
     sc = torch.empty(F * K, dtype=torch.int64, device="cuda")
     fl = torch.ones(2, dtype=torch.int32, device="cuda")
-    assert lib.dev_partition_range_sampled(d_in, buf, nbits, 1, n, packed, ss, sc, fl)
+    if not lib.dev_partition_range_sampled(d_in, buf, nbits, 1, n, packed, ss, sc, fl):
+        # packed words need 1 <= s1 <= 32: a one-key range has s1 = 0
+        assert packed and int(n - 1).bit_length() - nbits < 1
+        return
     torch.cuda.synchronize()
     assert bool((buf[cap:] == -7).all())
     if fl[0]:
