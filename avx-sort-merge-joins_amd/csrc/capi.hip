@@ -1222,16 +1222,22 @@ void print_timing(uint64_t numtuples, struct timeval* start, struct timeval* end
 }
 
 // m-pass (src/joins/sortmergejoin_multipass.c:51-736) in the reference's
-// phases, on the device:
-//   mpass_partitioning_phase (:295-335)  radix partition of R and S into
-//       PARTFANOUT partitions on the low key bits (the stable partition of
-//       partition_relation, partition.c:29);
-//   mpass_sorting_phase (:337-409)      every partition sorted on its own
-//       (segmented sort: LDS block sorts, then 2-way merge passes per run);
-//   mpass_firstnumamerge_phase + mpass_fullmultipassmerge_phase (:411-708)
-//       the PARTFANOUT sorted runs merged pass by pass with 2-way merges
-//       (the merge-path tree, ceil(log2 PARTFANOUT) passes);
-//   mpass_mergejoin_phase (:711-736)    one merge-join scan.
+// phases, for its T = NTHREADS threads (each a chunk of n / T tuples, the
+// last one the rest, joincommon.c), on the device:
+//   mpass_partitioning_phase (:295-335)  every chunk radix-partitioned into
+//       F = PARTFANOUT partitions on the key bits above
+//       shift = ceil(log2(chunk * T)) - log2(F) - 1 (:323-328; the digit of
+//       partition.c:29, ((key - 1) & mask) >> shift);
+//   mpass_sorting_phase (:337-409)      every (chunk, partition) run sorted on
+//       its own (segmented sort: LDS block sorts, then 2-way merge passes);
+//   mpass_firstnumamerge_phase (:411-619) thread t owns partitions
+//       [t F / T, (t + 1) F / T); their runs from the T chunks are merged
+//       pairwise (chunks 2i, 2i + 1 of one partition), then
+//   mpass_fullmultipassmerge_phase (:621-708) thread t's runs are merged pass
+//       by pass with 2-way merges into one sorted relation per thread (both
+//       phases: the merge-path tree over the runs in that order);
+//   mpass_mergejoin_phase (:711-736)    one merge-join scan per thread, the
+//       counts summed.
 // Unlike m-way (one multi-way merge, fused here into the bucket sort) every
 // merge pass reads and writes both relations once more.
 result_t* sortmergejoin_multipass(relation_t* relR, relation_t* relS,
@@ -1251,51 +1257,104 @@ result_t* sortmergejoin_multipass(relation_t* relR, relation_t* relS,
     Tup* sS = (Tup*)c.ws.scratch("api_sortedS", (nS ? nS : 1) * sizeof(Tup));
     unsigned long long* cnt =
         (unsigned long long*)c.ws.scratch("api_cnt", sizeof(unsigned long long));
+    const uint32_t T = joincfg->NTHREADS > 0 ? (uint32_t)joincfg->NTHREADS : 1;
     const uint32_t fan = joincfg->PARTFANOUT > 1 ? (uint32_t)joincfg->PARTFANOUT : 2;
-    const uint32_t bits = ceil_log2(fan);
-    const uint32_t F = 1u << bits;
-    const Digit32 dig{(uint32_t)(F - 1), 0};
-    int64_t* hist = (int64_t*)c.ws.scratch("mp_hist", (size_t)F * 8);
-    int64_t* off = (int64_t*)c.ws.scratch("mp_off", (size_t)F * 8);
+    const uint32_t D = ceil_log2(fan);
+    // partitions per thread: the reference needs PARTFANOUT >= NTHREADS
+    const uint32_t F = (1u << D) >= T ? (1u << D) : T;
+    const uint32_t bits = ceil_log2(F);
+    int64_t* hist = (int64_t*)c.ws.scratch("mp_hist", (size_t)T * F * 8);
+    int64_t* off = (int64_t*)c.ws.scratch("mp_off", (size_t)T * F * 8);
     const DevBuf* rels[2] = {&r, &s};
     Tup* sorted[2] = {sR, sS};
     const uint64_t ns[2] = {nR, nS};
     static const char* pn[2] = {"mp_partR", "mp_partS"};
+    // per relation and thread: the thread's merged relation in sorted[q]
+    std::vector<uint64_t> toff[2], tlen[2];
     for (int q = 0; q < 2; q++) {
+        toff[q].assign(T, 0);
+        tlen[q].assign(T, 0);
         if (ns[q] == 0) continue;
         Tup* part = (Tup*)c.ws.scratch(pn[q], ns[q] * sizeof(Tup));
-        stable_partition(&c.ws, rels[q]->d, ns[q], part, dig, bits, 0, hist, off, c.st);
-        std::vector<int64_t> hh(F), ho(F);
-        SMJ_CHECK(hipMemcpyAsync(hh.data(), hist, F * 8, hipMemcpyDeviceToHost, c.st));
-        SMJ_CHECK(hipMemcpyAsync(ho.data(), off, F * 8, hipMemcpyDeviceToHost, c.st));
-        sync();
-        std::vector<uint64_t> so(F), sl(F);
-        std::vector<const Tup*> runs(F);
-        for (uint32_t i = 0; i < F; i++) {
-            so[i] = (uint64_t)ho[i];
-            sl[i] = (uint64_t)hh[i];
-            runs[i] = part + so[i];
+        const uint64_t chunk = ns[q] / T;
+        std::vector<uint64_t> c0(T), cl(T);
+        for (uint32_t t = 0; t < T; t++) {
+            c0[t] = t * chunk;
+            cl[t] = t + 1 == T ? ns[q] - c0[t] : chunk;
+            if (!cl[t]) continue;
+            // the reference's shift from its thread's chunk of R, for R and S
+            // alike (:323-328)
+            const uint64_t rchunk = t + 1 == T ? nR - (uint64_t)t * (nR / T) : nR / T;
+            const int64_t sh = rchunk ? (int64_t)ceil(log2((double)(rchunk * T))) - (int64_t)bits - 1
+                                      : 0;
+            const uint32_t shift = sh > 0 ? (uint32_t)sh : 0u;
+            const uint32_t mask = shift + bits <= 32
+                ? (uint32_t)(((1ull << bits) - 1) << shift) : 0xffffffffu;
+            const Digit32 dig{mask, shift};
+            stable_partition(&c.ws, rels[q]->d + c0[t], cl[t], part + c0[t], dig, bits, 0,
+                             hist + (size_t)t * F, off + (size_t)t * F, c.st);
         }
-        segmented_sort(&c.ws, part, so.data(), sl.data(), F, c.st);
-        multiway_merge_tree(&c.ws, runs.data(), sl.data(), F, sorted[q], c.st);
+        std::vector<int64_t> hh((size_t)T * F, 0), ho((size_t)T * F, 0);
+        for (uint32_t t = 0; t < T; t++) {
+            if (!cl[t]) continue;
+            SMJ_CHECK(hipMemcpyAsync(hh.data() + (size_t)t * F, hist + (size_t)t * F, F * 8,
+                                     hipMemcpyDeviceToHost, c.st));
+            SMJ_CHECK(hipMemcpyAsync(ho.data() + (size_t)t * F, off + (size_t)t * F, F * 8,
+                                     hipMemcpyDeviceToHost, c.st));
+        }
+        sync();
+        std::vector<uint64_t> so((size_t)T * F), sl((size_t)T * F);
+        for (uint32_t t = 0; t < T; t++)
+            for (uint32_t j = 0; j < F; j++) {
+                so[(size_t)t * F + j] = c0[t] + (uint64_t)ho[(size_t)t * F + j];
+                sl[(size_t)t * F + j] = (uint64_t)hh[(size_t)t * F + j];
+            }
+        segmented_sort(&c.ws, part, so.data(), sl.data(), T * F, c.st);
+        const uint32_t per = F / T;
+        uint64_t o = 0;
+        for (uint32_t t = 0; t < T; t++) {
+            std::vector<const Tup*> runs;
+            std::vector<uint64_t> lens;
+            for (uint32_t j = t * per; j < (t + 1) * per; j++)
+                for (uint32_t i = 0; i < T; i++) {
+                    runs.push_back(part + so[(size_t)i * F + j]);
+                    lens.push_back(sl[(size_t)i * F + j]);
+                }
+            uint64_t tot = 0;
+            for (uint64_t x : lens) tot += x;
+            toff[q][t] = o;
+            tlen[q][t] = tot;
+            if (tot) multiway_merge_tree(&c.ws, runs.data(), lens.data(), (uint32_t)runs.size(),
+                                         sorted[q] + o, c.st);
+            o += tot;
+        }
     }
-    SMJ_CHECK(hipMemsetAsync(cnt, 0, 8, c.st));
-    merge_join_count(sR, nR, sS, nS, cnt, c.st);
-    unsigned long long h = 0;
-    SMJ_CHECK(hipMemcpyAsync(&h, cnt, 8, hipMemcpyDeviceToHost, c.st));
+    // one counter per thread (the reference's per-thread result lists)
+    unsigned long long* tcnt =
+        (unsigned long long*)c.ws.scratch("mp_cnt", (size_t)T * sizeof(unsigned long long));
+    SMJ_CHECK(hipMemsetAsync(tcnt, 0, (size_t)T * 8, c.st));
+    for (uint32_t t = 0; t < T; t++)
+        merge_join_count(sR + toff[0][t], tlen[0][t], sS + toff[1][t], tlen[1][t], tcnt + t,
+                         c.st);
+    std::vector<unsigned long long> h(T, 0);
+    SMJ_CHECK(hipMemcpyAsync(h.data(), tcnt, (size_t)T * 8, hipMemcpyDeviceToHost, c.st));
     sync();
+    (void)cnt;
     gettimeofday(&t1, NULL);
     result_t* res = (result_t*)malloc(sizeof(result_t));
-    res->totalresults = (int64_t)h;
+    res->totalresults = 0;
     res->nthreads = joincfg->NTHREADS;
-    res->resultlist =
-        (threadresult_t*)calloc(joincfg->NTHREADS > 0 ? joincfg->NTHREADS : 1,
-                                sizeof(threadresult_t));
-    res->resultlist[0].nresults = (int64_t)h;
-    if (materialize_on()) {
-        chainedtuplebuffer_t* cb = chainedtuplebuffer_init();
-        materialize_append(sR, nR, sS, nS, cb);
-        res->resultlist[0].results = cb;
+    res->resultlist = (threadresult_t*)calloc(T, sizeof(threadresult_t));
+    for (uint32_t t = 0; t < T; t++) {
+        res->totalresults += (int64_t)h[t];
+        res->resultlist[t].nresults = (int64_t)h[t];
+        res->resultlist[t].threadid = t;
+        if (materialize_on()) {
+            // the thread's own sorted relations (its partitions), R-major
+            chainedtuplebuffer_t* cb = chainedtuplebuffer_init();
+            materialize_append(sR + toff[0][t], tlen[0][t], sS + toff[1][t], tlen[1][t], cb);
+            res->resultlist[t].results = cb;
+        }
     }
     if (!getenv("SMJ_QUIET")) {
         double us = (t1.tv_sec - t0.tv_sec) * 1e6 + (t1.tv_usec - t0.tv_usec);

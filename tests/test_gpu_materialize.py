@@ -136,6 +136,31 @@ def low32(a):
     return np.asarray(a, dtype=np.int64).astype(np.int32).astype(np.int64)
 
 
+def mpass_expected(orc, R, S, T, F):
+    """m-pass output order (src/joins/sortmergejoin_multipass.c): thread t owns
+    partitions [t F / T, (t + 1) F / T) of the digit ((key - 1) & mask) >>
+    shift, shift = ceil(log2(chunk * T)) - log2(F) - 1 (:323-328), and writes
+    the R-major matches of its own sorted relations; the threads' lists
+    follow one another."""
+    import math
+    bits = int(math.log2(F))
+
+    # the shift comes from each thread's chunk of R, for R and S alike
+    chunk = len(R) // T
+    sh = [max(math.ceil(math.log2(c * T)) - bits - 1, 0) if c else 0
+          for c in [chunk] * (T - 1) + [len(R) - chunk * (T - 1)]]
+    assert len(set(sh)) == 1 or len(R) < T
+
+    def owner(rel):
+        d = ((rel["key"].astype(np.int64) - 1) & (((1 << bits) - 1) << sh[0])) >> sh[0]
+        return d // (F // T)
+
+    oR, oS = owner(R), owner(S)
+    parts = [orc.merge_join_materialize(orc.sort(R[oR == t]), orc.sort(S[oS == t]))
+             for t in range(T)]
+    return np.concatenate(parts)
+
+
 @pytest.mark.parametrize("algo", ["m-way", "m-pass", "mpsm"])
 @pytest.mark.parametrize("kind,nr,ns", MAT_CASES)
 def test_join_materialize_and_persist(libs, oracles, width, algo, kind, nr, ns, tmp_path):
@@ -144,7 +169,10 @@ def test_join_materialize_and_persist(libs, oracles, width, algo, kind, nr, ns, 
     (main.c:609-614) in write_relation's format (generator.c:200-213)."""
     orc, lib = oracles[width], libs[width]
     R, S = make_join_inputs(orc, width, kind, nr, ns)
-    exp = orc.merge_join_materialize(orc.sort(R), orc.sort(S))
+    if algo == "m-pass":
+        exp = mpass_expected(orc, R, S, 4, 128)
+    else:
+        exp = orc.merge_join_materialize(orc.sort(R), orc.sort(S))
     out = tmp_path / "Out.tbl"
     n, got = lib.sortmergejoin_multiway(R, S, nthreads=4, algo=algo, materialize=True,
                                         persist=str(out))
