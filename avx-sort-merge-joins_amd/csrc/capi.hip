@@ -1,3 +1,4 @@
+#include <atomic>
 // capi.hip -- the C ABI of libsmj_hip[_k8].so (declared in include/smj.h).
 //
 // Reference-named entry points keep the reference's signatures, pointer-swap
@@ -921,16 +922,23 @@ static uint64_t materialize_append(const Tup* r, uint64_t nR, const Tup* s, uint
     return total;
 }
 
-static int g_materialize = -1;  // -1: not decided yet (SMJ_MATERIALIZE)
+// Process-wide, like the reference's compile-time -DJOIN_MATERIALIZE that it
+// stands for: every join of the process sees the last value set (atomic, so
+// concurrent callers read a whole value; callers that need different modes
+// at once must not share a process).  -1: not decided yet (SMJ_MATERIALIZE).
+static std::atomic<int> g_materialize{-1};
 
-void smj_set_materialize(int on) { g_materialize = on ? 1 : 0; }
+void smj_set_materialize(int on) { g_materialize.store(on ? 1 : 0); }
 
 static bool materialize_on() {
-    if (g_materialize < 0) {
+    int v = g_materialize.load();
+    if (v < 0) {
         const char* e = getenv("SMJ_MATERIALIZE");
-        g_materialize = (e && atoi(e) != 0) ? 1 : 0;
+        int want = (e && atoi(e) != 0) ? 1 : 0;
+        g_materialize.compare_exchange_strong(v, want);
+        v = g_materialize.load();
     }
-    return g_materialize > 0;
+    return v > 0;
 }
 
 // decimal of a signed 32-bit value into p; returns the end

@@ -261,8 +261,12 @@ uint64_t merge_join(tuple_t * rtuples, tuple_t * stuples, const uint64_t numR,
  * at compile time with -DJOIN_MATERIALIZE; the library cannot see the
  * caller's flags): on, sortmergejoin_multiway / _multipass / _mpsm hand the
  * whole output in result->resultlist[0].results as a chainedtuplebuffer_t
- * (the other threads' lists stay NULL).  Default: the environment variable
- * SMJ_MATERIALIZE (unset = off). */
+ * (the other threads' lists stay NULL; m-pass fills one list per thread, as
+ * its threads own disjoint partitions).  Default: the environment variable
+ * SMJ_MATERIALIZE (unset = off).  The switch is process-wide, like the
+ * compile-time flag it stands for: every join in the process sees the last
+ * value set (an atomic; concurrent joins that need different modes cannot
+ * share a process). */
 void smj_set_materialize(int on);
 
 /* main.c:609-614 (PERSIST_RELATIONS + JOIN_MATERIALIZE): append the

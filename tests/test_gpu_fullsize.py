@@ -14,6 +14,7 @@ sorts are its stable LSD radix sort (orc_sort_tuples_radix, checked against
 the qsort restatement in tests/test_oracle.py); the join's two run on two host
 threads (ctypes drops the GIL).
 """
+import os
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
@@ -107,11 +108,19 @@ def test_headline_join_full_bitexact(libs, oracles, width, dist_):
 
 
 def _checksum(torch, t):
-    """Order-independent checksum of (n, 2) rows (wrapping int64 sums)."""
+    """Order-independent checksum of (n, 2) rows: wrapping int64 sums of the
+    keys, the payloads and of two 64-bit avalanche hashes of each row (a row
+    lost and another duplicated changes the hash sums unless the two rows'
+    hashes collide: ~2^-64 per such pair)."""
     k = t[:, 1].to(torch.int64)
     p = t[:, 0].to(torch.int64)
-    mix = (k * 0x9E3779B1) ^ (p * 0x85EBCA77 + 0x165667B1)
-    return (int(k.sum()), int(p.sum()), int(mix.sum()))
+    z = (k * 0x2545F4914F6CDD1D) ^ (p + 0x632BE59BD9B4E019)
+    z = (z ^ (z >> 31)) * 0x1B873593CA5A7E35
+    z = (z ^ (z >> 29)) * 0x3C79AC492BA7B653
+    z = z ^ (z >> 32)
+    h1 = int(z.sum())
+    h2 = int((z * (z | 1)).sum())
+    return (int(k.sum()), int(p.sum()), h1, h2)
 
 
 @pytest.mark.parametrize("dist_", ["uniform", "zipf"])
@@ -145,4 +154,44 @@ def test_n1024_join_properties(libs, dist_):
         del dk, tie
         assert _checksum(torch, src) == _checksum(torch, out)
     del R, S, sR, sS
+    _free(torch)
+
+
+def test_distributed_join_n1024_one_rank():
+    """The multi-GPU code path (smj/dist.py DistributedJoin: range partition,
+    table exchange, the rank's own rows read in place, the segmented local
+    join) on BASELINE configs[4]'s size, R = S = 1024M 16-byte tuples, S
+    Zipf 0.75, over a one-rank RCCL group: count = |S|, both outputs sorted
+    and permutations of their inputs (checksums), two steps (buffer reuse)."""
+    import socket
+    import torch
+    import torch.distributed as dist
+    import smj
+    from smj.dist import DeviceOps, DistributedJoin
+    lib = smj.load(16)
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        n = 1_024_000_000
+        R, S = lib.empty(n), lib.empty(n)
+        lib.dev_gen_pk(R, 0, n, 12345)
+        lib.dev_gen_zipf(S, 0, n, 0.75, 54321)
+        dj = DistributedJoin(DeviceOps(lib), 9, 1, n)
+        count = torch.zeros(1, dtype=torch.int64, device="cuda")
+        for _ in range(2):
+            sR, sS = dj.step(R, S, count)
+            torch.cuda.synchronize()
+            assert int(count.item()) == n
+        for src, out in ((R, sR), (S, sS)):
+            assert out.shape[0] == n
+            k = out[:, 1]
+            assert bool((k[1:] >= k[:-1]).all())
+            assert _checksum(torch, src) == _checksum(torch, out)
+        del R, S, sR, sS, dj
+    finally:
+        dist.destroy_process_group()
     _free(torch)
