@@ -1655,6 +1655,13 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
                            tp_lds, st, T);
     }
     launch_preft(tt, nrel, ub, ntiles, nb2, st);
+#ifdef SMJ_LAB_FLUSH
+    {   // lab build only: evict the Infinity Cache between the tile and the
+        // group pass (1 GiB of stores), to measure what its residency buys
+        void* fl = ws->scratch("lab_flush", (size_t)1 << 30);
+        SMJ_CHECK(hipMemsetAsync(fl, SMJ_LAB_FLUSH, (size_t)1 << 30, st));
+    }
+#endif
     if (a.ev_bucket) SMJ_CHECK(hipEventRecord(a.ev_bucket, st));
     G.nrel = nrel;
     G.plan = *a.host_plan;

@@ -1722,6 +1722,29 @@ uint64_t smj_sampled_capacity(uint64_t n, uint32_t nbits) { return sampled_capac
 
 uint32_t smj_sampled_shards(void) { return kShards; }
 
+void smj_dev_xsend(const int64_t* start, const int64_t* cnt, const int64_t* flags, uint32_t F,
+                   uint32_t K, uint32_t world, int64_t* msg, int64_t* chunk,
+                   smj_stream_t stream) {
+    if (F > 1024 || world == 0 || world > 1024 || world > F) {
+        fprintf(stderr, "[ERROR] smj_dev_xsend: F %u, world %u (1 <= world <= F <= 1024)\n", F,
+                world);
+        abort();
+    }
+    xsend(start, cnt, flags, F, K, world, msg, chunk, (hipStream_t)stream);
+}
+
+void smj_dev_xrecv(const int64_t* msg, const int64_t* chunk, uint32_t world, uint32_t rank,
+                   uint32_t mine, uint32_t K, uint32_t nbuckets, uint64_t cap, int64_t* tstart,
+                   int64_t* tcnt, int64_t* summary, smj_stream_t stream) {
+    if (world == 0 || world > 1024 || rank >= world || mine > nbuckets) {
+        fprintf(stderr, "[ERROR] smj_dev_xrecv: world %u, rank %u, mine %u, nbuckets %u\n",
+                world, rank, mine, nbuckets);
+        abort();
+    }
+    xrecv(msg, chunk, world, rank, mine, K, nbuckets, cap, tstart, tcnt, summary,
+          (hipStream_t)stream);
+}
+
 int smj_dev_partition_range_sampled(smj_workspace* wsp, const tuple_t* in, uint64_t n,
                                     void* out, uint32_t nbits, int64_t key_min,
                                     int64_t key_max, int packed, int64_t* seg_start_out,

@@ -1,0 +1,138 @@
+// exchange.hip -- the table side of the multi-GPU join's exchange step
+// (smj/dist.py; the reference's analogue is the
+// redistribution of co-partitions between threads before the multiway merge,
+// src/joins/sortmergejoin_multiway.c:463-556).
+//
+// After a rank range-partitions a relation into F partitions (K shard regions
+// each, exact partitions use shard 0 only), partition p belongs to rank
+// owner(p) = p * G / F (contiguous ranges, dist.py owners()).  Two one-
+// workgroup kernels turn the region tables into
+//   xsend: the message to every rank g -- [chunk size, used elements, the
+//          sender's two flags, the owned regions' offsets inside the chunk,
+//          their counts] -- rank after rank, plus the chunk starts/sizes;
+//   xrecv: from the G messages received (an all-to-all), the local join's
+//          segment tables (bucket-major, G * K segments per bucket) with the
+//          rank's own chunk read in place inside its partition buffer and the
+//          other ranks' rows after it, and a small summary the host reads in
+//          one copy (chunk starts and sizes, receive sizes, used elements,
+//          the flags' maximum over ranks).
+// They replace two dozen small framework ops (and their host round trips) per
+// relation and step.
+#include "smj_common.hpp"
+#include "smj_internal.hpp"
+
+namespace smj {
+
+__device__ __forceinline__ uint32_t owned_lo(uint32_t F, uint32_t G, uint32_t g) {
+    return (uint32_t)(((uint64_t)g * F + G - 1) / G);
+}
+
+constexpr uint32_t kXHead = 4;  // chunk size, used, flag0 (not packable), flag1 (overflow)
+
+__global__ void __launch_bounds__(256)
+k_xsend(const int64_t* __restrict__ start, const int64_t* __restrict__ cnt,
+        const int64_t* __restrict__ flags, uint32_t F, uint32_t K, uint32_t G,
+        int64_t* __restrict__ msg, int64_t* __restrict__ chunk) {
+    __shared__ unsigned long long cend;
+    __shared__ int64_t used[1024];
+    if (threadIdx.x == 0) cend = 0;
+    for (uint32_t g = threadIdx.x; g < G; g += 256) used[g] = 0;
+    __syncthreads();
+    // end of the last region and every destination's used elements
+    for (uint32_t i = threadIdx.x; i < F * K; i += 256) {
+        const uint64_t e = (uint64_t)(start[i] + cnt[i]);
+        atomicMax(&cend, (unsigned long long)e);
+        const uint32_t p = i / K;
+        const uint32_t g = (uint32_t)((uint64_t)p * G / F);
+        if (cnt[i]) atomicAdd((unsigned long long*)&used[g], (unsigned long long)cnt[i]);
+    }
+    __syncthreads();
+    // chunk of g: from its first partition's first region to the next rank's
+    for (uint32_t g = threadIdx.x; g < G; g += 256) {
+        const int64_t cs = start[(size_t)owned_lo(F, G, g) * K];
+        const int64_t ce = g + 1 < G ? start[(size_t)owned_lo(F, G, g + 1) * K] : (int64_t)cend;
+        chunk[g] = cs;
+        chunk[G + g] = ce - cs;
+    }
+    // messages: rank g's at sum over earlier ranks of (head + 2 K owned)
+    for (uint32_t g = 0; g < G; g++) {
+        const uint32_t lo = owned_lo(F, G, g), hi = owned_lo(F, G, g + 1);
+        const uint64_t m0 = (uint64_t)g * kXHead + 2ull * K * lo;
+        const uint32_t nreg = (hi - lo) * K;
+        const int64_t cs = start[(size_t)lo * K];
+        if (threadIdx.x == 0) {
+            const int64_t ce = g + 1 < G ? start[(size_t)hi * K] : (int64_t)cend;
+            msg[m0 + 0] = ce - cs;
+            msg[m0 + 1] = used[g];
+            msg[m0 + 2] = flags[0];
+            msg[m0 + 3] = flags[1];
+        }
+        for (uint32_t j = threadIdx.x; j < nreg; j += 256) {
+            const size_t i = (size_t)lo * K + j;
+            msg[m0 + kXHead + j] = cnt[i] > 0 ? start[i] - cs : 0;
+            msg[m0 + kXHead + nreg + j] = cnt[i];
+        }
+    }
+}
+
+// msg: G rows of (head + 2 * mine * K), row s from rank s.  tstart/tcnt:
+// (2^lbits) x (G * K), bucket b = owned partition b, segment (s, q).
+// summary: [chunk start (G) | chunk size = send (G) | receive (G) | used
+// received (G) | max flag0 | max flag1]
+__global__ void __launch_bounds__(256)
+k_xrecv(const int64_t* __restrict__ msg, const int64_t* __restrict__ chunk, uint32_t G,
+        uint32_t rank, uint32_t mine, uint32_t K, uint32_t nb, uint64_t cap,
+        int64_t* __restrict__ tstart, int64_t* __restrict__ tcnt, int64_t* __restrict__ summary) {
+    const uint32_t row = kXHead + 2 * mine * K;
+    __shared__ int64_t base[1024];
+    if (threadIdx.x == 0) {
+        // the own chunk stays in place in the partition buffer; the others
+        // follow the partition buffer (its first `cap` elements), rank order
+        int64_t ro = (int64_t)cap, f0 = 0, f1 = 0;
+        for (uint32_t s = 0; s < G; s++) {
+            const int64_t rl = msg[(size_t)s * row];
+            base[s] = s == rank ? chunk[rank] : ro;
+            if (s != rank) ro += rl;
+            summary[2 * G + s] = rl;
+            summary[3 * G + s] = msg[(size_t)s * row + 1];
+            f0 = max(f0, msg[(size_t)s * row + 2]);
+            f1 = max(f1, msg[(size_t)s * row + 3]);
+        }
+        summary[4 * G] = f0;
+        summary[4 * G + 1] = f1;
+    }
+    for (uint32_t g = threadIdx.x; g < G; g += 256) {
+        summary[g] = chunk[g];
+        summary[G + g] = chunk[G + g];
+    }
+    __syncthreads();
+    const uint32_t GK = G * K;
+    for (uint32_t i = threadIdx.x; i < nb * GK; i += 256) {
+        const uint32_t b = i / GK, j = i % GK, s = j / K, q = j % K;
+        int64_t st = 0, ct = 0;
+        if (b < mine) {
+            const size_t m = (size_t)s * row + kXHead + (size_t)b * K + q;
+            ct = msg[m + (size_t)mine * K];
+            st = msg[m] + base[s];
+        }
+        tstart[i] = st;
+        tcnt[i] = ct;
+    }
+}
+
+void xsend(const int64_t* start, const int64_t* cnt, const int64_t* flags, uint32_t F,
+           uint32_t K, uint32_t G, int64_t* msg, int64_t* chunk, hipStream_t st) {
+    hipLaunchKernelGGL(k_xsend, dim3(1), dim3(256), 0, st, start, cnt, flags, F, K, G, msg,
+                       chunk);
+    SMJ_CHECK(hipGetLastError());
+}
+
+void xrecv(const int64_t* msg, const int64_t* chunk, uint32_t G, uint32_t rank, uint32_t mine,
+           uint32_t K, uint32_t nb, uint64_t cap, int64_t* tstart, int64_t* tcnt,
+           int64_t* summary, hipStream_t st) {
+    hipLaunchKernelGGL(k_xrecv, dim3(1), dim3(256), 0, st, msg, chunk, G, rank, mine, K, nb,
+                       cap, tstart, tcnt, summary);
+    SMJ_CHECK(hipGetLastError());
+}
+
+}  // namespace smj

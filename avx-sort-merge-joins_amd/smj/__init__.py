@@ -62,6 +62,7 @@ DEVICE_SYMBOLS = [
     "smj_set_materialize", "smj_dev_join_segmented_tables", "smj_dev_partition_range_sampled",
     "smj_sampled_capacity", "smj_sampled_shards", "smj_context_workspace",
     "smj_dev_gen_nonunique", "smj_dev_gen_zipf_ref", "smj_glibc_rand",
+    "smj_dev_xsend", "smj_dev_xrecv",
 ]
 
 
@@ -186,6 +187,9 @@ class Library:
             "smj_dev_gen_zipf_ref": (None, [_P, _P, _U64, _U64, _U64, C.c_double, _U32, _U64,
                                             _P]),
             "smj_glibc_rand": (_U32, [_U32, _U64]),
+            "smj_dev_xsend": (None, [_P, _P, _P, _U32, _U32, _U32, _P, _P, _P]),
+            "smj_dev_xrecv": (None, [_P, _P, _U32, _U32, _U32, _U32, _U32, _U64, _P, _P, _P,
+                                     _P]),
             "smj_trace_enable": (None, [_P, C.c_int]),
             "smj_trace_reset": (None, [_P]),
             "smj_trace_read": (C.c_int, [_P, C.c_char_p, C.c_int, _P, _P, C.c_int]),
@@ -388,6 +392,18 @@ class Library:
         (bit-exact; the payload is 0)."""
         self.lib.smj_dev_gen_zipf_ref(self.ws, out.data_ptr(), out.shape[0], first, maxid,
                                       theta, seed, skip, self.stream_ptr())
+
+    def dev_xsend(self, start, cnt, flags, world, msg, chunk):
+        """smj_dev_xsend: start/cnt (F, K) int64, flags int64[2]."""
+        F, K = start.shape
+        self.lib.smj_dev_xsend(start.data_ptr(), cnt.data_ptr(), flags.data_ptr(), F, K, world,
+                               msg.data_ptr(), chunk.data_ptr(), self.stream_ptr())
+
+    def dev_xrecv(self, msg, chunk, world, rank, mine, K, tstart, tcnt, cap, summary):
+        """smj_dev_xrecv: msg (world, 4 + 2 K mine), tstart/tcnt (nb, world K)."""
+        self.lib.smj_dev_xrecv(msg.data_ptr(), chunk.data_ptr(), world, rank, mine, K,
+                               tstart.shape[0], cap, tstart.data_ptr(), tcnt.data_ptr(),
+                               summary.data_ptr(), self.stream_ptr())
 
     def glibc_rand(self, seed, k):
         return int(self.lib.smj_glibc_rand(seed, k))

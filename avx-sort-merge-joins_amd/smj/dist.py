@@ -128,6 +128,60 @@ def send_counts(hist: torch.Tensor, world: int) -> torch.Tensor:
     return out.index_add_(0, own, hist.to(torch.int64))
 
 
+HEAD = 4  # message header: chunk size, used elements, flag0 (not packable), flag1 (overflow)
+
+
+def xsend_torch(start, cnt, flags, world, msg, chunk):
+    """smj_dev_xsend in framework ops (the CPU stand-ins use it; the GPU test
+    compares the kernel with it): the message to every rank, rank after rank,
+    [chunk size, used, flags, owned regions' offsets in the chunk, counts],
+    and chunk = [chunk starts | chunk sizes]."""
+    F, K = start.shape
+    G = world
+    dev = start.device
+    own = owners(F, G).to(dev)
+    lo_of = torch.tensor([owned(F, G, g)[0] for g in range(G)], dtype=torch.int64, device=dev)
+    cstart = start[lo_of, 0]
+    cend = (start + cnt).max()
+    csize = torch.cat([cstart[1:], cend.view(1)]) - cstart
+    used = torch.zeros(G, dtype=torch.int64, device=dev).index_add_(0, own, cnt.sum(1))
+    rel_start = torch.where(cnt > 0, start - cstart[own].view(F, 1), 0)
+    parts = []
+    for g in range(G):
+        lo, hi = owned(F, G, g)
+        parts += [torch.stack([csize[g], used[g], flags[0].to(torch.int64),
+                               flags[1].to(torch.int64)]),
+                  rel_start[lo:hi].reshape(-1), cnt[lo:hi].reshape(-1)]
+    msg.copy_(torch.cat(parts))
+    chunk[:G] = cstart
+    chunk[G:] = csize
+
+
+def xrecv_torch(msg, chunk, world, rank, mine, K, tstart, tcnt, cap, summary):
+    """smj_dev_xrecv in framework ops: the local join's segment tables (own
+    chunk in place, the other ranks' rows from `cap` on, rank order) and the
+    summary [chunk starts | sizes | receive sizes | used received | max
+    flags]."""
+    G = world
+    m = msg.view(G, HEAD + 2 * mine * K)
+    rl = m[:, 0].tolist()
+    base, ro = [], cap
+    for s in range(G):
+        base.append(int(chunk[rank]) if s == rank else ro)
+        ro += 0 if s == rank else rl[s]
+    bt = torch.tensor(base, dtype=torch.int64, device=msg.device)
+    rs = m[:, HEAD:HEAD + mine * K].view(G, mine, K) + bt.view(G, 1, 1)
+    rc = m[:, HEAD + mine * K:].view(G, mine, K)
+    tstart.zero_()
+    tcnt.zero_()
+    tstart[:mine] = rs.permute(1, 0, 2).reshape(mine, G * K)
+    tcnt[:mine] = rc.permute(1, 0, 2).reshape(mine, G * K)
+    summary[:2 * G] = chunk
+    summary[2 * G:3 * G] = m[:, 0]
+    summary[3 * G:4 * G] = m[:, 1]
+    summary[4 * G:] = m[:, 2:HEAD].max(0).values
+
+
 class DeviceOps:
     """The device implementation of the ops interface (libsmj_hip*.so).
     16-byte tuples travel as packed 64-bit words (smj_dev_partition_range_packed)
@@ -182,6 +236,12 @@ class DeviceOps:
         self.lib.dev_join_segmented_tables(R, nR, startR, cntR, S, nS, startS, cntS,
                                            bucket_bits, key_lo, key_hi, sR, sS, count,
                                            packed=packed)
+
+    def xsend(self, start, cnt, flags, world, msg, chunk):
+        self.lib.dev_xsend(start, cnt, flags, world, msg, chunk)
+
+    def xrecv(self, msg, chunk, world, rank, mine, K, tstart, tcnt, cap, summary):
+        self.lib.dev_xrecv(msg, chunk, world, rank, mine, K, tstart, tcnt, cap, summary)
 
 
 class DistributedJoin:
@@ -286,28 +346,29 @@ class DistributedJoin:
         f = flags.to(torch.int64)
         return ss.view(F, K), sc.view(F, K), torch.stack([f[1], f[0]])
 
-    # header of a rank's table message to each destination: chunk size, used
-    # elements, then the sender's flags (not packable, region overflow) -- the
-    # flags' MAX over ranks needs no collective of its own
-    HEAD = 4
-
     def _exchange(self, rel, key, allow_pack=True):
         """Partition `rel`, swap the segment tables, start the row exchange.
         Every attempt agrees across ranks (every rank sees every rank's flags
         in the table exchange): a sampled region overflow anywhere -> every
         rank partitions exactly; an unpackable tuple anywhere -> every rank
-        sends tuples.  Returns (exchange buffer, start and count tables
-        (2^lbits, world * K) for the local join, elements inside the
-        segments, async work, packed?)."""
+        sends tuples.  The tables are built on the device (smj_dev_xsend /
+        xrecv); the host reads one small summary per attempt.  Returns
+        (exchange buffer, start and count tables (2^lbits, world * K) for the
+        local join, elements inside the segments, async work, packed?)."""
         G, me = self.world, self.rank
         dev = rel.device
         F, K = self.fanout, self.shards
-        H = self.HEAD
         n = rel.shape[0]
         mine = self.p_hi - self.p_lo
-        own = owners(F, G).to(dev)
-        lo_of = torch.tensor([owned(F, G, g)[0] for g in range(G)], dtype=torch.int64,
-                             device=dev)
+        nb = 1 << self.lbits
+        xsend = getattr(self.ops, "xsend", xsend_torch)
+        xrecv = getattr(self.ops, "xrecv", xrecv_torch)
+        msg_len = sum(HEAD + 2 * K * m for m in self.per_rank)
+        inp = torch.empty(msg_len, dtype=torch.int64, device=dev)
+        chunk = torch.empty(2 * G, dtype=torch.int64, device=dev)
+        tstart = torch.empty(nb, G * K, dtype=torch.int64, device=dev)
+        tcnt = torch.empty(nb, G * K, dtype=torch.int64, device=dev)
+        summary = torch.empty(4 * G + 2, dtype=torch.int64, device=dev)
         packed = allow_pack and bool(getattr(self.ops, "can_pack", False))
         sampled = self.sampled
         while True:
@@ -324,31 +385,16 @@ class DistributedJoin:
                     packed = False
                     continue
             start, cnt, fl = res
-            # per destination g: its chunk of `part` is [cstart[g], cstart[g + 1])
-            # (region slack included); the tables give each owned segment's
-            # offset inside that chunk
-            cstart = start[lo_of, 0]
-            cend = (start + cnt).max()
-            csize = torch.cat([cstart[1:], cend.view(1)]) - cstart
-            used = torch.zeros(G, dtype=torch.int64, device=dev).index_add_(0, own, cnt.sum(1))
-            rel_start = torch.where(cnt > 0, start - cstart[own].view(F, 1), 0)
-            head = torch.cat([torch.stack([csize, used], 1), fl.view(1, 2).expand(G, 2)], 1)
-            msgs = []
-            for g in range(G):
-                lo, hi = owned(F, G, g)
-                msgs += [head[g], rel_start[lo:hi].reshape(-1), cnt[lo:hi].reshape(-1)]
-            inp = torch.cat(msgs)
+            xsend(start, cnt, fl, G, inp, chunk)
             if G == 1:
-                msg = inp.view(1, H + 2 * mine * K)
+                msg = inp
             else:
-                per_in = [H + 2 * m * K for m in self.per_rank]
-                out_msg = torch.empty(G * (H + 2 * mine * K), dtype=torch.int64, device=dev)
-                dist.all_to_all_single(out_msg, inp, [H + 2 * mine * K] * G, per_in,
+                per_in = [HEAD + 2 * m * K for m in self.per_rank]
+                msg = torch.empty(G * (HEAD + 2 * mine * K), dtype=torch.int64, device=dev)
+                dist.all_to_all_single(msg, inp, [HEAD + 2 * mine * K] * G, per_in,
                                        group=self.group)
-                msg = out_msg.view(G, H + 2 * mine * K)
-            # one host round trip: sizes for the row exchange, the flags' MAX
-            host = torch.cat([cstart, csize, msg[:, 0], msg[:, 1],
-                              msg[:, 2:H].max(0).values]).tolist()
+            xrecv(msg, chunk, G, me, mine, K, tstart, tcnt, cap, summary)
+            host = summary.tolist()  # the one host round trip of the attempt
             cs, sl, rl, ru = host[:G], host[G:2 * G], host[2 * G:3 * G], host[3 * G:4 * G]
             bad, ovf = host[4 * G:]
             if ovf:
@@ -372,21 +418,6 @@ class DistributedJoin:
         work = self._rows(xb, cap, cs, sl, rl)
         self.last_recv[key] = (sl, rl)
         self.last_rows[key] = (xb, cap, cs, sl, rl)  # bench.py --op exchange repeats it
-        # receive tables: segment (bucket b, source s, shard q) at its offset
-        # in s's chunk + where that chunk lies in the exchange buffer (the own
-        # chunk in place inside the partition, the others after it)
-        base, ro = [], cap
-        for g in range(G):
-            base.append(cs[me] if g == me else ro)
-            ro += 0 if g == me else rl[g]
-        bt = torch.tensor(base, dtype=torch.int64, device=dev)
-        rs = msg[:, H:H + mine * K].view(G, mine, K) + bt.view(G, 1, 1)
-        rc = msg[:, H + mine * K:].view(G, mine, K)
-        nb = 1 << self.lbits
-        tstart = torch.zeros(nb, G * K, dtype=torch.int64, device=dev)
-        tcnt = torch.zeros(nb, G * K, dtype=torch.int64, device=dev)
-        tstart[:mine] = rs.permute(1, 0, 2).reshape(mine, G * K)
-        tcnt[:mine] = rc.permute(1, 0, 2).reshape(mine, G * K)
         self._ev_issue = ev
         return xb, tstart, tcnt, sum(ru), work, packed
 

@@ -218,3 +218,49 @@ def test_distributed_join_one_rank_rccl(libs, width, xsampled, monkeypatch):
         assert torch.equal(sR[:, 1].to(torch.int64), torch.arange(1, n + 1, device="cuda"))
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("F,G", [(256, 1), (512, 2), (1024, 3), (1024, 8), (16, 16)])
+def test_exchange_table_kernels(libs, F, G):
+    """smj_dev_xsend / smj_dev_xrecv (exchange.hip) against their framework-op
+    statement in smj/dist.py (xsend_torch / xrecv_torch, which the gloo tests
+    run): random region tables with empty regions, every rank's view."""
+    import torch
+    from smj.dist import HEAD, owned, xrecv_torch, xsend_torch
+    lib = libs[16]
+    K = 8
+    g = torch.Generator().manual_seed(F * 31 + G)
+    cnt = torch.randint(0, 50, (F, K), generator=g, dtype=torch.int64)
+    cnt[torch.rand(F, K, generator=g) < 0.2] = 0
+    slack = torch.randint(0, 9, (F, K), generator=g, dtype=torch.int64)
+    size = cnt + slack
+    start = (torch.cumsum(size.reshape(-1), 0) - size.reshape(-1)).view(F, K)
+    flags = torch.tensor([1, 0], dtype=torch.int64)
+    per = [owned(F, G, r)[1] - owned(F, G, r)[0] for r in range(G)]
+    mlen = sum(HEAD + 2 * K * m for m in per)
+    want_msg, want_chunk = torch.empty(mlen, dtype=torch.int64), torch.empty(2 * G, dtype=torch.int64)
+    xsend_torch(start, cnt, flags, G, want_msg, want_chunk)
+    d = {k: v.cuda() for k, v in dict(start=start, cnt=cnt, flags=flags).items()}
+    msg = torch.full((mlen,), -5, dtype=torch.int64, device="cuda")
+    chunk = torch.empty(2 * G, dtype=torch.int64, device="cuda")
+    lib.dev_xsend(d["start"], d["cnt"], d["flags"], G, msg, chunk)
+    torch.cuda.synchronize()
+    assert torch.equal(msg.cpu(), want_msg) and torch.equal(chunk.cpu(), want_chunk)
+    # rank r receives, from every source, that source's message to r (here:
+    # the same sender's tables stand in for every source)
+    offs = [sum(HEAD + 2 * K * m for m in per[:r]) for r in range(G)]
+    for r in range(G):
+        mine = per[r]
+        one = want_msg[offs[r]:offs[r] + HEAD + 2 * K * mine]
+        rmsg = one.repeat(G)
+        nb = 1 << max(mine - 1, 0).bit_length()
+        cap = int((start + size).max()) + 3
+        wt, wc = torch.empty(nb, G * K, dtype=torch.int64), torch.empty(nb, G * K, dtype=torch.int64)
+        ws = torch.empty(4 * G + 2, dtype=torch.int64)
+        xrecv_torch(rmsg, want_chunk, G, r, mine, K, wt, wc, cap, ws)
+        t = torch.full((nb, G * K), -1, dtype=torch.int64, device="cuda")
+        c = torch.full((nb, G * K), -1, dtype=torch.int64, device="cuda")
+        sm = torch.empty(4 * G + 2, dtype=torch.int64, device="cuda")
+        lib.dev_xrecv(rmsg.cuda(), chunk, G, r, mine, K, t, c, cap, sm)
+        torch.cuda.synchronize()
+        assert torch.equal(t.cpu(), wt) and torch.equal(c.cpu(), wc) and torch.equal(sm.cpu(), ws)

@@ -1,0 +1,35 @@
+#!/usr/bin/env python3
+"""Tail of a rocprofv3 kernel trace as a timeline: every dispatch of the last
+`ms` milliseconds with the idle gap before it, and the totals.
+
+    python tools/timeline.py TRACE_CSV [ms] [OUT_CSV]
+"""
+import csv
+import sys
+
+
+def main(src, ms=10.0, dst=None):
+    rows = sorted(csv.DictReader(open(src)), key=lambda r: int(r["Start_Timestamp"]))
+    end = max(int(r["End_Timestamp"]) for r in rows)
+    rows = [r for r in rows if int(r["Start_Timestamp"]) >= end - ms * 1e6]
+    out = ["gap_before_us,duration_us,kernel"]
+    prev = None
+    gaps = busy = 0.0
+    for r in rows:
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        gap = (s - prev) / 1e3 if prev is not None else 0.0
+        gaps += max(gap, 0.0)
+        busy += (e - s) / 1e3
+        name = r["Kernel_Name"].split("(")[0].replace("void ", "")[:90]
+        out.append(f"{gap:.1f},{(e - s) / 1e3:.1f},{name}")
+        prev = e if prev is None else max(prev, e)
+    out.append(f"# {len(rows)} dispatches, busy {busy:.1f} us, gaps {gaps:.1f} us")
+    text = "\n".join(out)
+    if dst:
+        open(dst, "w").write(text + "\n")
+    print(text)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], float(sys.argv[2]) if len(sys.argv) > 2 else 10.0,
+         sys.argv[3] if len(sys.argv) > 3 else None)
