@@ -1722,7 +1722,7 @@ uint64_t smj_sampled_capacity(uint64_t n, uint32_t nbits) { return sampled_capac
 
 uint32_t smj_sampled_shards(void) { return kShards; }
 
-void smj_dev_xsend(const int64_t* start, const int64_t* cnt, const int64_t* flags, uint32_t F,
+void smj_dev_xsend(const int64_t* start, const int64_t* cnt, const unsigned int* flags, uint32_t F,
                    uint32_t K, uint32_t world, int64_t* msg, int64_t* chunk,
                    smj_stream_t stream) {
     if (F > 1024 || world == 0 || world > 1024 || world > F) {

@@ -31,47 +31,70 @@ constexpr uint32_t kXHead = 4;  // chunk size, used, flag0 (not packable), flag1
 
 __global__ void __launch_bounds__(256)
 k_xsend(const int64_t* __restrict__ start, const int64_t* __restrict__ cnt,
-        const int64_t* __restrict__ flags, uint32_t F, uint32_t K, uint32_t G,
+        const unsigned int* __restrict__ flags, uint32_t F, uint32_t K, uint32_t G,
         int64_t* __restrict__ msg, int64_t* __restrict__ chunk) {
-    __shared__ unsigned long long cend;
+    __shared__ unsigned long long wend[4];
     __shared__ int64_t used[1024];
-    if (threadIdx.x == 0) cend = 0;
     for (uint32_t g = threadIdx.x; g < G; g += 256) used[g] = 0;
     __syncthreads();
-    // end of the last region and every destination's used elements
-    for (uint32_t i = threadIdx.x; i < F * K; i += 256) {
-        const uint64_t e = (uint64_t)(start[i] + cnt[i]);
-        atomicMax(&cend, (unsigned long long)e);
-        const uint32_t p = i / K;
+    // end of the last region (thread maxima, then waves) and every
+    // destination's used elements: a thread's partitions are consecutive, so
+    // it adds one run per owner it meets
+    const uint32_t per = (F + 255) / 256;
+    const uint32_t p0 = threadIdx.x * per, p1 = min(p0 + per, F);
+    unsigned long long e = 0;
+    int64_t acc = 0;
+    uint32_t cur = 0xffffffffu;
+    for (uint32_t p = p0; p < p1; p++) {
         const uint32_t g = (uint32_t)((uint64_t)p * G / F);
-        if (cnt[i]) atomicAdd((unsigned long long*)&used[g], (unsigned long long)cnt[i]);
+        if (g != cur) {
+            if (acc) atomicAdd((unsigned long long*)&used[cur], (unsigned long long)acc);
+            cur = g;
+            acc = 0;
+        }
+        for (uint32_t q = 0; q < K; q++) {
+            const size_t i = (size_t)p * K + q;
+            e = max(e, (unsigned long long)(start[i] + cnt[i]));
+            acc += cnt[i];
+        }
     }
+    if (acc) atomicAdd((unsigned long long*)&used[cur], (unsigned long long)acc);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long x = __shfl_xor(e, o, 64);
+        e = x > e ? x : e;
+    }
+    if ((threadIdx.x & 63) == 0) wend[threadIdx.x >> 6] = e;
     __syncthreads();
+    const int64_t cend = (int64_t)max(max(wend[0], wend[1]), max(wend[2], wend[3]));
     // chunk of g: from its first partition's first region to the next rank's
     for (uint32_t g = threadIdx.x; g < G; g += 256) {
         const int64_t cs = start[(size_t)owned_lo(F, G, g) * K];
-        const int64_t ce = g + 1 < G ? start[(size_t)owned_lo(F, G, g + 1) * K] : (int64_t)cend;
+        const int64_t ce = g + 1 < G ? start[(size_t)owned_lo(F, G, g + 1) * K] : cend;
         chunk[g] = cs;
         chunk[G + g] = ce - cs;
     }
-    // messages: rank g's at sum over earlier ranks of (head + 2 K owned)
-    for (uint32_t g = 0; g < G; g++) {
+    // messages: rank g's at sum over earlier ranks of (head + 2 K owned); the
+    // region entries of all ranks in one sweep, the heads by one thread each
+    for (uint32_t i = threadIdx.x; i < F * K; i += 256) {
+        const uint32_t p = i / K;
+        const uint32_t g = (uint32_t)((uint64_t)p * G / F);
         const uint32_t lo = owned_lo(F, G, g), hi = owned_lo(F, G, g + 1);
         const uint64_t m0 = (uint64_t)g * kXHead + 2ull * K * lo;
-        const uint32_t nreg = (hi - lo) * K;
+        const uint32_t nreg = (hi - lo) * K, j = i - lo * K;
         const int64_t cs = start[(size_t)lo * K];
-        if (threadIdx.x == 0) {
-            const int64_t ce = g + 1 < G ? start[(size_t)hi * K] : (int64_t)cend;
-            msg[m0 + 0] = ce - cs;
-            msg[m0 + 1] = used[g];
-            msg[m0 + 2] = flags[0];
-            msg[m0 + 3] = flags[1];
-        }
-        for (uint32_t j = threadIdx.x; j < nreg; j += 256) {
-            const size_t i = (size_t)lo * K + j;
-            msg[m0 + kXHead + j] = cnt[i] > 0 ? start[i] - cs : 0;
-            msg[m0 + kXHead + nreg + j] = cnt[i];
-        }
+        msg[m0 + kXHead + j] = cnt[i] > 0 ? start[i] - cs : 0;
+        msg[m0 + kXHead + nreg + j] = cnt[i];
+    }
+    for (uint32_t g = threadIdx.x; g < G; g += 256) {
+        const uint32_t lo = owned_lo(F, G, g), hi = owned_lo(F, G, g + 1);
+        const uint64_t m0 = (uint64_t)g * kXHead + 2ull * K * lo;
+        const int64_t cs = start[(size_t)lo * K];
+        const int64_t ce = g + 1 < G ? start[(size_t)hi * K] : cend;
+        msg[m0 + 0] = ce - cs;
+        msg[m0 + 1] = used[g];
+        msg[m0 + 2] = flags[1];  // not packable
+        msg[m0 + 3] = flags[0];  // region overflow
     }
 }
 
@@ -120,7 +143,7 @@ k_xrecv(const int64_t* __restrict__ msg, const int64_t* __restrict__ chunk, uint
     }
 }
 
-void xsend(const int64_t* start, const int64_t* cnt, const int64_t* flags, uint32_t F,
+void xsend(const int64_t* start, const int64_t* cnt, const unsigned int* flags, uint32_t F,
            uint32_t K, uint32_t G, int64_t* msg, int64_t* chunk, hipStream_t st) {
     hipLaunchKernelGGL(k_xsend, dim3(1), dim3(256), 0, st, start, cnt, flags, F, K, G, msg,
                        chunk);

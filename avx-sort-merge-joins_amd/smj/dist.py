@@ -134,8 +134,9 @@ HEAD = 4  # message header: chunk size, used elements, flag0 (not packable), fla
 def xsend_torch(start, cnt, flags, world, msg, chunk):
     """smj_dev_xsend in framework ops (the CPU stand-ins use it; the GPU test
     compares the kernel with it): the message to every rank, rank after rank,
-    [chunk size, used, flags, owned regions' offsets in the chunk, counts],
-    and chunk = [chunk starts | chunk sizes]."""
+    [chunk size, used, not packable, overflow, owned regions' offsets in the
+    chunk, counts], and chunk = [chunk starts | chunk sizes].  flags: int32
+    [region overflow, not packable] as the sampled partition writes them."""
     F, K = start.shape
     G = world
     dev = start.device
@@ -149,8 +150,8 @@ def xsend_torch(start, cnt, flags, world, msg, chunk):
     parts = []
     for g in range(G):
         lo, hi = owned(F, G, g)
-        parts += [torch.stack([csize[g], used[g], flags[0].to(torch.int64),
-                               flags[1].to(torch.int64)]),
+        parts += [torch.stack([csize[g], used[g], flags[1].to(torch.int64),
+                               flags[0].to(torch.int64)]),
                   rel_start[lo:hi].reshape(-1), cnt[lo:hi].reshape(-1)]
     msg.copy_(torch.cat(parts))
     chunk[:G] = cstart
@@ -307,21 +308,27 @@ class DistributedJoin:
             self.buf[key] = b = nb
         return b
 
+    def _small(self, key, shape, dtype=torch.int64, dev=None):
+        """A small per-relation table, allocated once (reused every step)."""
+        t = self.buf.get(key)
+        if t is None or t.shape != torch.Size(shape) or t.dtype != dtype:
+            t = torch.empty(shape, dtype=dtype, device=dev)
+            self.buf[key] = t
+        return t
+
     def _partition(self, rel, part, packed):
         """Exact range partition of `rel` into `part` (packed words or tuples),
         partitions back to back.  Returns (per-partition start (F, K) and
-        count (F, K) with only shard 0 used, flags int64 [not packable,
-        overflow]), or None when packed words do not apply at all."""
+        count (F, K) with only shard 0 used, flags int32 [overflow (0), not
+        packable]), or None when packed words do not apply at all."""
         dev = rel.device
         F, K = self.fanout, self.shards
         hist = torch.zeros(F, dtype=torch.int64, device=dev)
-        flags = torch.zeros(2, dtype=torch.int64, device=dev)
+        flags = torch.zeros(2, dtype=torch.int32, device=dev)
         if packed:
-            bad = torch.zeros(1, dtype=torch.int32, device=dev)
             if not self.ops.partition_range_packed(rel, part, self.pbits, self.key_min,
-                                                   self.key_max, hist, bad):
+                                                   self.key_max, hist, flags[1:]):
                 return None
-            flags[0] = bad[0]
         else:
             self.ops.partition_range(rel, part, self.pbits, self.key_min, self.key_max, hist)
         start = torch.zeros(F, K, dtype=torch.int64, device=dev)
@@ -330,21 +337,20 @@ class DistributedJoin:
         cnt[:, 0] = hist
         return start, cnt, flags
 
-    def _sampled(self, rel, part, packed):
+    def _sampled(self, rel, part, packed, key):
         """Sampled range partition into `part` (no histogram pass): partition
         p is K consecutive shard regions with slack after each.  Returns
-        (start (F, K), count (F, K), flags int64 [not packable, overflow]), or
-        None when the form does not apply."""
+        (start (F, K), count (F, K), flags int32 [overflow, not packable],
+        zeroed by the partition), or None when the form does not apply."""
         dev = rel.device
         F, K = self.fanout, self.shards
-        ss = torch.empty(F * K, dtype=torch.int64, device=dev)
-        sc = torch.empty(F * K, dtype=torch.int64, device=dev)
-        flags = torch.zeros(2, dtype=torch.int32, device=dev)
+        ss = self._small("ss" + key, (F * K,), dev=dev)
+        sc = self._small("sc" + key, (F * K,), dev=dev)
+        flags = self._small("fl" + key, (2,), torch.int32, dev)
         if not self.ops.partition_range_sampled(rel, part, self.pbits, self.key_min,
                                                 self.key_max, packed, ss, sc, flags):
             return None
-        f = flags.to(torch.int64)
-        return ss.view(F, K), sc.view(F, K), torch.stack([f[1], f[0]])
+        return ss.view(F, K), sc.view(F, K), flags
 
     def _exchange(self, rel, key, allow_pack=True):
         """Partition `rel`, swap the segment tables, start the row exchange.
@@ -364,11 +370,11 @@ class DistributedJoin:
         xsend = getattr(self.ops, "xsend", xsend_torch)
         xrecv = getattr(self.ops, "xrecv", xrecv_torch)
         msg_len = sum(HEAD + 2 * K * m for m in self.per_rank)
-        inp = torch.empty(msg_len, dtype=torch.int64, device=dev)
-        chunk = torch.empty(2 * G, dtype=torch.int64, device=dev)
-        tstart = torch.empty(nb, G * K, dtype=torch.int64, device=dev)
-        tcnt = torch.empty(nb, G * K, dtype=torch.int64, device=dev)
-        summary = torch.empty(4 * G + 2, dtype=torch.int64, device=dev)
+        inp = self._small("xin" + key, (msg_len,), dev=dev)
+        chunk = self._small("xch" + key, (2 * G,), dev=dev)
+        tstart = self._small("xts" + key, (nb, G * K), dev=dev)
+        tcnt = self._small("xtc" + key, (nb, G * K), dev=dev)
+        summary = self._small("xsm" + key, (4 * G + 2,), dev=dev)
         packed = allow_pack and bool(getattr(self.ops, "can_pack", False))
         sampled = self.sampled
         while True:
@@ -378,7 +384,7 @@ class DistributedJoin:
             extra = self.recv_hint.get(xkey, (cap * (G - 1)) // G + cap // 8 if G > 1 else 0)
             xb = self._xbuf(xkey, cap + extra, packed)
             part = xb[:cap]
-            res = self._sampled(rel, part, packed) if sampled else None
+            res = self._sampled(rel, part, packed, key) if sampled else None
             if res is None:  # exact partition (the receivers read either form)
                 res = self._partition(rel, part[:n], packed)
                 if res is None:  # not packable at all: tuples, on every rank
@@ -390,7 +396,7 @@ class DistributedJoin:
                 msg = inp
             else:
                 per_in = [HEAD + 2 * m * K for m in self.per_rank]
-                msg = torch.empty(G * (HEAD + 2 * mine * K), dtype=torch.int64, device=dev)
+                msg = self._small("xmsg" + key, (G * (HEAD + 2 * mine * K),), dev=dev)
                 dist.all_to_all_single(msg, inp, [HEAD + 2 * mine * K] * G, per_in,
                                        group=self.group)
             xrecv(msg, chunk, G, me, mine, K, tstart, tcnt, cap, summary)

@@ -548,10 +548,11 @@ uint32_t smj_sampled_shards(void);
 
 /* The multi-GPU exchange's tables (smj/dist.py; exchange.hip).  A rank's
  * range partition into F partitions of K shard regions (start/cnt: F x K
- * int64, exact partitions use shard 0; flags: int64[2] = not packable,
- * region overflow) goes to `world` ranks, partition p to rank p*world/F.
+ * int64, exact partitions use shard 0; flags: uint32[2] = region overflow,
+ * not packable, as smj_dev_partition_range_sampled writes them) goes to
+ * `world` ranks, partition p to rank p*world/F.
  * smj_dev_xsend writes the message to every rank g, rank after rank
- * ([chunk size, used elements, flags[0], flags[1], the owned regions'
+ * ([chunk size, used elements, flags[1], flags[0], the owned regions'
  * offsets inside the chunk, their counts]: 4 + 2 K n_g int64 for n_g owned
  * partitions) and chunk[0..world) = chunk starts, chunk[world..2 world) =
  * chunk sizes.  smj_dev_xrecv takes the `world` messages received (each
@@ -559,8 +560,8 @@ uint32_t smj_sampled_shards(void);
  * tcnt: nbuckets x world*K, bucket-major; the rank's own chunk in place at
  * its chunk start, the others from element `cap` on, rank order) and
  * summary[4 world + 2] = chunk starts, chunk sizes (sends), receive sizes,
- * used elements received, max flags[0], max flags[1]. */
-void smj_dev_xsend(const int64_t * start, const int64_t * cnt, const int64_t * flags,
+ * used elements received, max not-packable flag, max overflow flag. */
+void smj_dev_xsend(const int64_t * start, const int64_t * cnt, const unsigned int * flags,
                    uint32_t F, uint32_t K, uint32_t world, int64_t * msg, int64_t * chunk,
                    smj_stream_t stream);
 void smj_dev_xrecv(const int64_t * msg, const int64_t * chunk, uint32_t world, uint32_t rank,

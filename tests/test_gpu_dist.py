@@ -235,7 +235,7 @@ def test_exchange_table_kernels(libs, F, G):
     slack = torch.randint(0, 9, (F, K), generator=g, dtype=torch.int64)
     size = cnt + slack
     start = (torch.cumsum(size.reshape(-1), 0) - size.reshape(-1)).view(F, K)
-    flags = torch.tensor([1, 0], dtype=torch.int64)
+    flags = torch.tensor([0, 1], dtype=torch.int32)  # [overflow, not packable]
     per = [owned(F, G, r)[1] - owned(F, G, r)[0] for r in range(G)]
     mlen = sum(HEAD + 2 * K * m for m in per)
     want_msg, want_chunk = torch.empty(mlen, dtype=torch.int64), torch.empty(2 * G, dtype=torch.int64)
