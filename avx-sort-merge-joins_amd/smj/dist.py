@@ -352,21 +352,31 @@ class DistributedJoin:
             return None
         return ss.view(F, K), sc.view(F, K), flags
 
-    def _exchange(self, rel, key, allow_pack=True):
-        """Partition `rel`, swap the segment tables, start the row exchange.
-        Every attempt agrees across ranks (every rank sees every rank's flags
-        in the table exchange): a sampled region overflow anywhere -> every
-        rank partitions exactly; an unpackable tuple anywhere -> every rank
-        sends tuples.  The tables are built on the device (smj_dev_xsend /
-        xrecv); the host reads one small summary per attempt.  Returns
-        (exchange buffer, start and count tables (2^lbits, world * K) for the
-        local join, elements inside the segments, async work, packed?)."""
+    def _attempt(self, rel, key, packed, sampled):
+        """Enqueue one exchange attempt of `rel`: its range partition (sampled
+        or exact, packed words or tuples), the table messages (device), their
+        all-to-all and the receive tables, and an asynchronous copy of the
+        small summary the host needs.  Returns the attempt's state (nothing
+        has been waited for), or None when packed words do not apply at all."""
         G, me = self.world, self.rank
         dev = rel.device
         F, K = self.fanout, self.shards
         n = rel.shape[0]
         mine = self.p_hi - self.p_lo
         nb = 1 << self.lbits
+        xkey = ("xw" if packed else "xt") + key
+        cap = self.ops.sampled_capacity(n, self.pbits) if sampled else n
+        # room for the remote rows: last step's, else an even share + 1/8
+        extra = self.recv_hint.get(xkey, (cap * (G - 1)) // G + cap // 8 if G > 1 else 0)
+        xb = self._xbuf(xkey, cap + extra, packed)
+        part = xb[:cap]
+        res = self._sampled(rel, part, packed, key) if sampled else None
+        if res is None:  # exact partition (the receivers read either form)
+            cap = n if sampled else cap
+            res = self._partition(rel, part[:n], packed)
+            if res is None:
+                return None
+        start, cnt, fl = res
         xsend = getattr(self.ops, "xsend", xsend_torch)
         xrecv = getattr(self.ops, "xrecv", xrecv_torch)
         msg_len = sum(HEAD + 2 * K * m for m in self.per_rank)
@@ -375,45 +385,56 @@ class DistributedJoin:
         tstart = self._small("xts" + key, (nb, G * K), dev=dev)
         tcnt = self._small("xtc" + key, (nb, G * K), dev=dev)
         summary = self._small("xsm" + key, (4 * G + 2,), dev=dev)
-        packed = allow_pack and bool(getattr(self.ops, "can_pack", False))
-        sampled = self.sampled
+        xsend(start, cnt, fl, G, inp, chunk)
+        if G == 1:
+            msg = inp
+        else:
+            per_in = [HEAD + 2 * m * K for m in self.per_rank]
+            msg = self._small("xmsg" + key, (G * (HEAD + 2 * mine * K),), dev=dev)
+            dist.all_to_all_single(msg, inp, [HEAD + 2 * mine * K] * G, per_in,
+                                   group=self.group)
+        xrecv(msg, chunk, G, me, mine, K, tstart, tcnt, cap, summary)
+        if summary.is_cuda:
+            hs = self.buf.get("xhost" + key)
+            if hs is None or hs.shape != summary.shape:
+                hs = torch.empty(summary.shape, dtype=torch.int64, pin_memory=True)
+                self.buf["xhost" + key] = hs
+            hs.copy_(summary, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        else:
+            hs, ev = summary, None
+        return dict(key=key, xkey=xkey, xb=xb, cap=cap, packed=packed, sampled=sampled,
+                    tstart=tstart, tcnt=tcnt, host=hs, ev=ev)
+
+    def _finish(self, rel, st, allow_pack=True):
+        """Wait for an attempt's summary; repeat the attempt until every rank
+        agrees it is valid (a sampled region overflow anywhere -> every rank
+        partitions exactly; an unpackable tuple anywhere -> every rank sends
+        tuples), then start its row exchange.  Returns (exchange buffer, start
+        and count tables (2^lbits, world * K) for the local join, elements
+        inside the segments, async work, packed?)."""
+        G, me = self.world, self.rank
+        key = st["key"] if st is not None else None
         while True:
-            xkey = ("xw" if packed else "xt") + key
-            cap = self.ops.sampled_capacity(n, self.pbits) if sampled else n
-            # room for the remote rows: last step's, else an even share + 1/8
-            extra = self.recv_hint.get(xkey, (cap * (G - 1)) // G + cap // 8 if G > 1 else 0)
-            xb = self._xbuf(xkey, cap + extra, packed)
-            part = xb[:cap]
-            res = self._sampled(rel, part, packed, key) if sampled else None
-            if res is None:  # exact partition (the receivers read either form)
-                res = self._partition(rel, part[:n], packed)
-                if res is None:  # not packable at all: tuples, on every rank
-                    packed = False
-                    continue
-            start, cnt, fl = res
-            xsend(start, cnt, fl, G, inp, chunk)
-            if G == 1:
-                msg = inp
-            else:
-                per_in = [HEAD + 2 * m * K for m in self.per_rank]
-                msg = self._small("xmsg" + key, (G * (HEAD + 2 * mine * K),), dev=dev)
-                dist.all_to_all_single(msg, inp, [HEAD + 2 * mine * K] * G, per_in,
-                                       group=self.group)
-            xrecv(msg, chunk, G, me, mine, K, tstart, tcnt, cap, summary)
-            host = summary.tolist()  # the one host round trip of the attempt
-            cs, sl, rl, ru = host[:G], host[G:2 * G], host[2 * G:3 * G], host[3 * G:4 * G]
-            bad, ovf = host[4 * G:]
-            if ovf:
-                sampled = False  # a region overflowed somewhere: every rank exact
-                continue
-            if packed and bad:
-                packed = False  # repeat on tuples, on every rank
-                continue
-            break
+            if st is not None:
+                if st["ev"] is not None:
+                    st["ev"].synchronize()
+                host = st["host"].tolist()
+                cs, sl, rl, ru = host[:G], host[G:2 * G], host[2 * G:3 * G], host[3 * G:4 * G]
+                bad, ovf = host[4 * G:]
+                if not ovf and not (st["packed"] and bad):
+                    break
+                packed = st["packed"] and not bad
+                sampled = st["sampled"] and not ovf
+            else:  # packed words did not apply at all: tuples, on every rank
+                packed, sampled = False, self.sampled
+            st = self._attempt(rel, key, packed, sampled)
+        xkey, cap = st["xkey"], st["cap"]
         remote = sum(rl) - rl[me]
         self.recv_hint[xkey] = max(remote, self.recv_hint.get(xkey, 0))
-        xb = self._xbuf(xkey, cap + remote, packed, keep=cap)
-        row = 8 if packed else xb.element_size() * (xb.shape[1] if xb.dim() > 1 else 1)
+        xb = self._xbuf(xkey, cap + remote, st["packed"], keep=cap)
+        row = 8 if st["packed"] else xb.element_size() * (xb.shape[1] if xb.dim() > 1 else 1)
         self.stats["sent_B"] += row * (sum(sl) - sl[me])
         self.stats["recv_B"] += row * remote
         self.stats["gap_B"] += row * (sum(rl) - sum(ru))
@@ -425,7 +446,15 @@ class DistributedJoin:
         self.last_recv[key] = (sl, rl)
         self.last_rows[key] = (xb, cap, cs, sl, rl)  # bench.py --op exchange repeats it
         self._ev_issue = ev
-        return xb, tstart, tcnt, sum(ru), work, packed
+        return xb, st["tstart"], st["tcnt"], sum(ru), work, st["packed"]
+
+    def _exchange(self, rel, key, allow_pack=True):
+        """One relation's exchange: attempt, wait, start the rows."""
+        packed = allow_pack and bool(getattr(self.ops, "can_pack", False))
+        st = self._attempt(rel, key, packed, self.sampled)
+        if st is None:
+            st = self._attempt(rel, key, False, self.sampled)
+        return self._finish(rel, st)
 
     def _rows(self, xb, cap, cs, sl, rl):
         """Asynchronous row exchange in one batch of point-to-point operations:
@@ -455,9 +484,22 @@ class DistributedJoin:
         return g if self.group is None else dist.get_global_rank(self.group, g)
 
     def step(self, R, S, count):
-        # the row exchange of R overlaps the partition of S
-        rR, tR, cR, nR, wR, pR = self._exchange(R, "R")
-        rS, tS, cS, nS, wS, pS = self._exchange(S, "S")
+        if self.world > 1:
+            # the row exchange of R overlaps the partition of S
+            rR, tR, cR, nR, wR, pR = self._exchange(R, "R")
+            rS, tS, cS, nS, wS, pS = self._exchange(S, "S")
+        else:
+            # one rank: no rows travel, so both partitions are queued before
+            # the one wait for their summaries
+            packed = bool(getattr(self.ops, "can_pack", False))
+            aR = self._attempt(R, "R", packed, self.sampled)
+            aS = self._attempt(S, "S", packed, self.sampled)
+            if aR is None:
+                aR = self._attempt(R, "R", False, self.sampled)
+            if aS is None:
+                aS = self._attempt(S, "S", False, self.sampled)
+            rR, tR, cR, nR, wR, pR = self._finish(R, aR)
+            rS, tS, cS, nS, wS, pS = self._finish(S, aS)
         eS = self._ev_issue
         wR.wait()
         wS.wait()

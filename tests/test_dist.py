@@ -245,6 +245,8 @@ def _free_port():
 
 
 @pytest.mark.parametrize("world,chunk_mb,s_payload,mode", [
+    (1, None, "negative", "sampled"), (1, None, "rowid", "exact"),
+    (1, None, "r_negative", "sampled"),
     (2, None, "negative", "sampled"), (3, None, "negative", "sampled"),
     (2, 0, "negative", "sampled"), (3, 0, "rowid", "sampled"),
     (2, None, "rowid", "sampled"), (3, None, "rowid", "sampled"),
