@@ -1236,6 +1236,8 @@ k_sample_hist(SampleRel S, uint32_t stride, Digit dig_arg, uint32_t nbins) {
 #define SMJ_SC_SEG 64
 #endif
 constexpr uint32_t kSegBytes = SMJ_SC_SEG;
+constexpr uint32_t kRegionAlign = 128;  // bytes; a multiple of kSegBytes
+static_assert(kRegionAlign % kSegBytes == 0, "regions hold whole segments");
 
 // per-relation region tables of one sampled partition launch
 struct RegionRel {
@@ -1257,13 +1259,16 @@ k_regions(RegionRel R, uint32_t nbins, uint32_t stride, uint64_t slack, uint32_t
     unsigned long long* __restrict__ cursor = R.cursor[r];
     uint64_t* __restrict__ cap_end = R.cap_end[r];
     __shared__ uint64_t sh[256];
-    const uint64_t SEG = kSegBytes / elem_bytes;
+    // shard capacities are whole 128-byte lines (a multiple of the scatter's
+    // segment), so every region starts on a line of its own: the tiles the
+    // bucket pass cuts from different regions never share a cache line
+    const uint64_t ALIGN = kRegionAlign / elem_bytes;
     const uint32_t per = (nbins + 255) / 256;
     const uint32_t b = threadIdx.x * per;
     // capacity of one shard of partition d
     auto cap = [&](uint32_t d) {
         const uint64_t est = (uint64_t)sample[d] * stride / kShards;
-        return (est + est / 8 + slack + SEG - 1) / SEG * SEG;
+        return (est + est / 8 + slack + ALIGN - 1) / ALIGN * ALIGN;
     };
     uint64_t loc = 0;
     for (uint32_t k = 0; k < per; k++)
@@ -1922,11 +1927,12 @@ static constexpr uint64_t kRegionSlack = 1024;  // per shard
 // tuples at every 4*stride-th position, so sample[] sums to at most
 // n/stride + 4 and the estimates to n + 4*stride; a shard's capacity is 9/8
 // of its estimate plus the slack, rounded up to a segment:
-//     sum <= (n + 4*stride) * 9/8 + 2^dbits * kShards * (slack + SEG - 1).
+//     sum <= (n + 4*stride) * 9/8 + 2^dbits * kShards * (slack + ALIGN - 1),
+// ALIGN = kRegionAlign in elements (the capacities' rounding).
 uint64_t sampled_capacity(uint64_t n, uint32_t dbits) {
-    const uint64_t SEG = kSegBytes / 8;
+    const uint64_t ALIGN = kRegionAlign / 8;
     return n + n / 8 + 5 * kSampleStride + 1 +
-           ((uint64_t)1 << dbits) * kShards * (kRegionSlack + SEG);
+           ((uint64_t)1 << dbits) * kShards * (kRegionSlack + ALIGN);
 }
 
 template <int ITEMS, class Pack>
