@@ -389,7 +389,13 @@ struct SrcFused {
         len = ld_sc1(pf + 1) - lo;
     }
     template <class W>
-    __device__ static __forceinline__ W load(const W* p) { return ld_w_sc1(p); }
+    __device__ static __forceinline__ W load(const W* p) {
+#ifdef SMJ_LAB_PLAIN_LD
+        return *p;  // lab build only: the cost of the sc1 loads (not coherent)
+#else
+        return ld_w_sc1(p);
+#endif
+    }
 };
 
 // A group and, for the calling thread, its tile run: wave r < nrel owns
