@@ -104,8 +104,6 @@ struct TileTable {
     uint32_t* btile0;  // first tile of every bucket (nbuckets + 1)
     uint16_t* pref;    // [tile][nb2 + 1] exclusive prefix, sentinel = length
     uint16_t* prefT;   // the same, digit-major: [d2][tstride] (k_preft)
-    uint32_t* pref32;  // k_fused: [tile][p32stride] exclusive prefix, uint32
-    uint32_t p32stride;  // nb2 + 1 rounded up to 128 bytes: rows share no line
     uint32_t tstride;  // tiles per prefT row (>= the tile count)
 };
 
@@ -326,49 +324,10 @@ struct GroupLDS {
     uint32_t off[2];
 };
 
-// Where the group pass reads a tile's prefix entries and elements.
-//   SrcPlain: after a separate tile pass -- the digit-major uint16 prefix
-//             table (k_preft) and plain loads;
-//   SrcFused: inside k_fused, right after other workgroups wrote them -- the
-//             row-major uint32 prefix rows and agent-scope (sc1) loads, which
-//             bypass the CU's L1 (the writers store sc1: write-through).
-__device__ __forceinline__ uint64_t ld_sc1(const uint64_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_sc1(uint64_t* p, uint64_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_sc1(uint32_t* p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <class W>
-__device__ __forceinline__ W ld_w_sc1(const W* p) {
-    if constexpr (sizeof(W) == 8) {
-        const uint64_t x = ld_sc1(reinterpret_cast<const uint64_t*>(p));
-        W w;
-        __builtin_memcpy(&w, &x, 8);
-        return w;
-    } else {
-        static_assert(sizeof(W) == 16, "8- or 16-byte elements");
-        const uint64_t* q = reinterpret_cast<const uint64_t*>(p);
-        const uint64_t x[2] = {ld_sc1(q), ld_sc1(q + 1)};
-        W w;
-        __builtin_memcpy(&w, x, 16);
-        return w;
-    }
-}
-template <class W>
-__device__ __forceinline__ void st_w_sc1(W* p, const W& w) {
-    uint64_t x[sizeof(W) / 8];
-    __builtin_memcpy(x, &w, sizeof(W));
-    uint64_t* q = reinterpret_cast<uint64_t*>(p);
-#pragma unroll
-    for (int i = 0; i < (int)(sizeof(W) / 8); i++) st_sc1(q + i, x[i]);
-}
-
+// Where the group pass reads a tile's prefix entries (the digit-major uint16
+// table of k_preft) and its elements.  A policy, so that another producer of
+// the tiles (an earlier, fused form of the two passes: DESIGN.md §4) could
+// plug in its own.
 struct SrcPlain {
     // run [lo, lo + len) of group g in tile t
     __device__ static __forceinline__ void run(const TileTable& tt, uint32_t nb2, uint32_t t,
@@ -379,23 +338,6 @@ struct SrcPlain {
     }
     template <class W>
     __device__ static __forceinline__ W load(const W* p) { return *p; }
-};
-
-struct SrcFused {
-    __device__ static __forceinline__ void run(const TileTable& tt, uint32_t nb2, uint32_t t,
-                                               uint32_t g, uint32_t& lo, uint32_t& len) {
-        const uint32_t* pf = tt.pref32 + (uint64_t)t * tt.p32stride + g;
-        lo = ld_sc1(pf);
-        len = ld_sc1(pf + 1) - lo;
-    }
-    template <class W>
-    __device__ static __forceinline__ W load(const W* p) {
-#ifdef SMJ_LAB_PLAIN_LD
-        return *p;  // lab build only: the cost of the sc1 loads (not coherent)
-#else
-        return ld_w_sc1(p);
-#endif
-    }
 };
 
 // A group and, for the calling thread, its tile run: wave r < nrel owns
@@ -901,201 +843,6 @@ k_groupsort(GroupArgs A) {
     if (A.nrel == 2) {
         matches = wave_sum(matches);
         if ((otid() & 63) == 0 && matches) atomicAdd(A.count_dev, matches);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// k_fused: the tile pass and the group pass in ONE persistent launch, so a
-// bucket's grouped tiles are read back while they are still in the Infinity
-// Cache (256 MiB) instead of from HBM after the whole relation has been
-// rewritten.  Work items, in the order of a precomputed schedule (k_sched):
-//   tile item  (t)     : k_tilepass on tile t (FTILE elements, in place),
-//                        prefix row written as uint32 (pref32) and uint16;
-//   group item (b, q)  : groups [q gpb, (q + 1) gpb) of bucket b (group_loop)
-//                        once every tile of b is done.
-// The tiles of bucket b + lag are scheduled before the groups of bucket b,
-// so a group item rarely waits.  Workgroups take items from one counter in
-// schedule order; an item waits only for items taken before it, which
-// running workgroups hold, so the schedule always drains.  Hand-off between
-// workgroups (any XCD): the tile item stores its elements and prefix row with
-// agent-scope (sc1, write-through) stores, every wave waits for its stores,
-// a barrier, then one lane adds to the bucket's counter; the group item polls
-// that counter with sc1 loads and reads the tiles with sc1 loads
-// (MI355X_MICROARCH.md, inter-workgroup visibility, first table row).  A poll
-// that does not complete within ~1 s sets `err` and the host reruns the
-// bucket pass with the separate kernels.
-constexpr int FT_ITEMS = 16;
-constexpr int FTILE = GS_THREADS * FT_ITEMS;  // elements per tile of k_fused
-constexpr uint32_t kItemGroup = 0x80000000u;
-
-struct FusedArgs {
-    GroupArgs G;        // G.tmp = the partition buffers (tiles grouped in place)
-    RangePlan plan;
-    uint32_t nb;        // buckets
-    uint32_t d2_fast;
-    uint32_t gpb;       // groups per group item
-    const uint32_t* sched;
-    const uint32_t* nitems;  // items in the schedule (device)
-    unsigned int* head;      // next item (zeroed)
-    unsigned int* done;      // per bucket: tiles grouped (zeroed)
-    unsigned int* err;       // a wait gave up
-};
-
-// schedule: block k = the tiles of bucket k (k < nb; R's, then S's), then the
-// group items of bucket k - lag (k >= lag); one thread per block
-__global__ void __launch_bounds__(256)
-k_sched(const uint32_t* __restrict__ bt0, const uint32_t* __restrict__ bt1, int nrel,
-        uint32_t nb, uint32_t lag, uint32_t gpi, uint32_t* __restrict__ sched,
-        uint32_t* __restrict__ nitems) {
-    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
-    if (k >= nb + lag) return;
-    auto tiles_before = [&](uint32_t x) {
-        return bt0[x] + (nrel > 1 ? bt1[x] : 0u);
-    };
-    uint64_t pos = tiles_before(k < nb ? k : nb) + (uint64_t)(k >= lag ? k - lag : 0) * gpi;
-    if (k < nb) {
-        for (uint32_t t = bt0[k]; t < bt0[k + 1]; t++) sched[pos++] = t;
-        if (nrel > 1)
-            for (uint32_t t = bt1[k]; t < bt1[k + 1]; t++) sched[pos++] = (1u << 30) | t;
-    }
-    if (k >= lag)
-        for (uint32_t q = 0; q < gpi; q++) sched[pos++] = kItemGroup | ((k - lag) << 11) | q;
-    if (k == 0) *nitems = tiles_before(nb) + nb * gpi;
-}
-
-// one tile of k_tilepass's work with GS_THREADS threads, FT_ITEMS elements each
-template <class Lay>
-__device__ __forceinline__ void fused_tile(const FusedArgs& A, unsigned char* lds, uint32_t item) {
-    typedef typename Lay::W W;
-    const RangePlan& P = A.plan;
-    const uint32_t nb2 = A.G.nb2;
-    const uint32_t tid = otid();
-    const int r = (item >> 30) & 1;
-    const uint32_t t = item & ((1u << 30) - 1);
-    const TileTable& tt = A.G.tt[r];
-    W* __restrict__ part = static_cast<W*>(const_cast<void*>(A.G.tmp[r]));
-    const uint64_t off = tt.off[t];
-    const uint32_t len = tt.len[t];
-    const uint32_t b = tt.bucket[t];
-    W* stage = reinterpret_cast<W*>(lds);
-    uint32_t* hist = reinterpret_cast<uint32_t*>(lds + FTILE * sizeof(W));
-    uint32_t* scr = hist + nb2 + 1;
-    for (uint32_t d = tid; d < nb2; d += GS_THREADS) hist[d] = 0;
-    W v[FT_ITEMS];
-    uint32_t dg[FT_ITEMS];
-#pragma unroll
-    for (int j = 0; j < FT_ITEMS; j++) {
-        const uint32_t i = j * GS_THREADS + tid;
-        v[j] = part[off + (i < len ? i : len - 1)];  // clamped: all loads in flight
-    }
-    __syncthreads();
-    if (A.d2_fast && b != 0 && b != (1u << P.D1) - 1) {
-        const uint32_t base_lo = (uint32_t)P.base, mask = nb2 - 1;
-#pragma unroll
-        for (int j = 0; j < FT_ITEMS; j++) {
-            dg[j] = Lay::digit_fast(v[j], base_lo, P.s1, P.s2, mask);
-            if (j * GS_THREADS + tid < len) atomicAdd(&hist[dg[j]], 1u);
-        }
-    } else {
-#pragma unroll
-        for (int j = 0; j < FT_ITEMS; j++) {
-            dg[j] = plan_d2(P, Lay::rel(P, v[j], b), b);
-            if (j * GS_THREADS + tid < len) atomicAdd(&hist[dg[j]], 1u);
-        }
-    }
-    __syncthreads();
-    const uint32_t per = (nb2 + GS_THREADS - 1) / GS_THREADS;
-    const uint32_t d0 = tid * per;
-    uint32_t loc = 0;
-    for (uint32_t k = 0; k < per; k++)
-        if (d0 + k < nb2) loc += hist[d0 + k];
-    uint32_t tot;
-    uint32_t ex = block_exclusive_scan(loc, scr, &tot);
-    uint32_t* pref32 = tt.pref32 + (uint64_t)t * tt.p32stride;
-    uint16_t* pref = tt.pref + (uint64_t)t * (nb2 + 1);
-    for (uint32_t k = 0; k < per; k++) {
-        const uint32_t d = d0 + k;
-        if (d < nb2) {
-            const uint32_t c = hist[d];
-            hist[d] = ex;
-            st_sc1(pref32 + d, ex);
-            pref[d] = (uint16_t)ex;  // for the skew kernels (a later launch)
-            ex += c;
-        }
-    }
-    if (tid == 0) {
-        st_sc1(pref32 + nb2, len);
-        pref[nb2] = (uint16_t)len;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < FT_ITEMS; j++)
-        if (j * GS_THREADS + tid < len) stage[atomicAdd(&hist[dg[j]], 1u)] = v[j];
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < FT_ITEMS; j++) {
-        const uint32_t i = j * GS_THREADS + tid;
-        if (i < len) st_w_sc1(part + off + i, stage[i]);
-    }
-    // every wave's stores are done, then one lane publishes the tile
-    __builtin_amdgcn_s_waitcnt(0x0f70);
-    __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(A.done + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <class Lay, int TPL>
-__global__ void __launch_bounds__(GS_THREADS, gs_wg_per_cu<typename Lay::W>() * GS_THREADS / 256)
-k_fused(FusedArgs A) {
-    typedef typename Lay::W W;
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
-    if (A.G.pack_bad && *A.G.pack_bad) return;
-    GroupLDS<W>& L = *reinterpret_cast<GroupLDS<W>*>(lds_raw);
-    __shared__ uint32_t sh_item;
-    const uint32_t tid = otid();
-    const uint32_t nitems = *A.nitems;
-    const uint32_t nb2 = A.G.nb2;
-    unsigned long long matches = 0;
-    for (;;) {
-        if (tid == 0) {
-            const uint32_t i = atomicAdd(A.head, 1u);
-            sh_item = i < nitems ? A.sched[i] : 0xffffffffu;
-        }
-        __syncthreads();
-        const uint32_t item = sh_item;
-        __syncthreads();
-        if (item == 0xffffffffu) break;
-        if (!(item & kItemGroup)) {
-            fused_tile<Lay>(A, lds_raw, item);
-            continue;
-        }
-        const uint32_t b = (item >> 11) & 0xfffffu, q = item & 2047u;
-        if (tid == 0) {
-            uint32_t need = A.G.tt[0].btile0[b + 1] - A.G.tt[0].btile0[b];
-            if (A.G.nrel > 1) need += A.G.tt[1].btile0[b + 1] - A.G.tt[1].btile0[b];
-            uint32_t spins = 0;
-            bool ok = true;
-            while (__hip_atomic_load(A.done + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-                __builtin_amdgcn_s_sleep(8);
-                if (++spins > (1u << 22)) {
-                    atomicOr(A.err, 1u);
-                    ok = false;
-                    break;
-                }
-            }
-            sh_item = ok ? 1u : 0u;
-        }
-        __syncthreads();
-        const bool ok = sh_item != 0;
-        __syncthreads();
-        if (!ok) break;
-        const uint32_t g0 = b * nb2 + q * A.gpb;
-        const uint32_t g1 = min(g0 + A.gpb, (b + 1) * nb2);
-        group_loop<Lay, TPL, SrcFused>(A.G, L, g0, g1, matches);
-        __syncthreads();
-    }
-    if (A.G.nrel == 2) {
-        matches = wave_sum(matches);
-        if ((tid & 63) == 0 && matches) atomicAdd(A.G.count_dev, matches);
     }
 }
 
@@ -1844,33 +1591,10 @@ static void launch_groupsort(int tpl, uint32_t nwg, hipStream_t st, const GroupA
                            sizeof(GroupLDS<typename Lay::W>), st, G);
 }
 
-#ifndef SMJ_FUSED
-#define SMJ_FUSED 1  // k_fused for the sampled 1-GPU path (0: separate passes)
-#endif
-#ifndef SMJ_FUSED_LAG
-#define SMJ_FUSED_LAG 3  // buckets whose tiles run ahead of a bucket's groups
-#endif
-#ifndef SMJ_FUSED_GPB
-#define SMJ_FUSED_GPB 4  // groups per group item
-#endif
-
-template <class Lay, int TPL>
-static void launch_fused(const FusedArgs& F, uint32_t nwg, size_t lds, hipStream_t st) {
-    static size_t attr = 0;
-    if (attr < lds) {
-        SMJ_CHECK(hipFuncSetAttribute((const void*)k_fused<Lay, TPL>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        attr = lds;
-    }
-    hipLaunchKernelGGL((k_fused<Lay, TPL>), dim3(nwg), dim3(GS_THREADS), lds, st, F);
-}
-
 // Bucket pass without a host synchronisation before the kernels (sampled
 // partition + host-known plan): launch sizes are upper bounds, the tile
 // numbering is computed on the device.  One synchronisation at the end (skew
-// queue and the partition's overflow flag).  The tile and group passes run
-// as k_fused where the layout allows it (a.fused_ok: regions on lines of their
-// own), else as k_tilepass + k_preft + k_groupsort.
+// queue and the partition's overflow flag).
 template <class Lay>
 static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
     typedef typename Lay::W W;
@@ -1879,18 +1603,11 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
     const int nrel = a.nrel;
     const uint32_t nb2 = 1u << a.host_plan->D2;
     const uint64_t nmax = nrel > 1 && a.n[1] > a.n[0] ? a.n[1] : a.n[0];
-    // k_fused cuts smaller tiles (GS_THREADS x FT_ITEMS); a bucket must keep
-    // within the group pass's 256 tiles
-    const bool fused = SMJ_FUSED && a.fused_ok && a.status &&
-                       expected_tiles(nmax, nb, a.nseg, FTILE) <= GS_TMAX - 16;
-    const uint32_t tsz = fused ? FTILE : TILE2;
-    const uint32_t p32 = ((nb2 + 1) + 31) & ~31u;  // 128-byte rows
+    const uint32_t tsz = TILE2;
     TileTable tt[2];
-    static const char* names[2][9] = {
-        {"bs_off0", "bs_len0", "bs_bkt0", "bs_bt00", "bs_pref0", "bs_ost0", "bs_nt0", "bs_preft0",
-         "bs_p320"},
-        {"bs_off1", "bs_len1", "bs_bkt1", "bs_bt01", "bs_pref1", "bs_ost1", "bs_nt1", "bs_preft1",
-         "bs_p321"}};
+    static const char* names[2][8] = {
+        {"bs_off0", "bs_len0", "bs_bkt0", "bs_bt00", "bs_pref0", "bs_ost0", "bs_nt0", "bs_preft0"},
+        {"bs_off1", "bs_len1", "bs_bkt1", "bs_bt01", "bs_pref1", "bs_ost1", "bs_nt1", "bs_preft1"}};
     uint64_t* ostart[2] = {nullptr, nullptr};
     uint32_t* ntiles[2] = {nullptr, nullptr};
     uint32_t ub[2] = {0, 0};
@@ -1902,9 +1619,6 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
         tt[r].btile0 = (uint32_t*)ws->scratch(names[r][3], (nb + 1) * 4);
         tt[r].pref = (uint16_t*)ws->scratch(names[r][4], (size_t)ub[r] * (nb2 + 1) * 2);
         tt[r].prefT = (uint16_t*)ws->scratch(names[r][7], (size_t)ub[r] * (nb2 + 1) * 2);
-        tt[r].pref32 = fused ? (uint32_t*)ws->scratch(names[r][8], (size_t)ub[r] * p32 * 4)
-                             : nullptr;
-        tt[r].p32stride = p32;
         tt[r].tstride = ub[r];
         ostart[r] = (uint64_t*)ws->scratch(names[r][5], (size_t)nb * 8);
         ntiles[r] = (uint32_t*)ws->scratch(names[r][6], 4);
@@ -1964,64 +1678,27 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
     G.ovf_cap = ovf_cap;
     G.g_begin = 0;
     G.g_end = ngroups;
-    const uint32_t maxwg = gs_wg_per_cu<W>() * 256;
-    // the separate passes (also the fused kernel's fallback)
-    auto separate = [&]() {
-        {
-            TraceScope ts(ws, "k_tilepass", st);
-            const size_t tp_lds = TILE2 * sizeof(W) + nb2 * 4 + 64;
-            hipLaunchKernelGGL(k_tilepass<Lay>, dim3(T.nt[0] + T.nt[1]), dim3(TP_THREADS),
-                               tp_lds, st, T);
-        }
-        launch_preft(tt, nrel, ub, ntiles, nb2, st);
+    {
+        TraceScope ts(ws, "k_tilepass", st);
+        const size_t tp_lds = TILE2 * sizeof(W) + nb2 * 4 + 64;
+        hipLaunchKernelGGL(k_tilepass<Lay>, dim3(T.nt[0] + T.nt[1]), dim3(TP_THREADS),
+                           tp_lds, st, T);
+    }
+    launch_preft(tt, nrel, ub, ntiles, nb2, st);
 #ifdef SMJ_LAB_FLUSH
-        {   // lab build only: evict the Infinity Cache between the tile and the
-            // group pass (1 GiB of stores), to measure what its residency buys
-            void* fl = ws->scratch("lab_flush", (size_t)1 << 30);
-            SMJ_CHECK(hipMemsetAsync(fl, SMJ_LAB_FLUSH, (size_t)1 << 30, st));
-        }
+    {   // lab build only: evict the Infinity Cache between the tile and the
+        // group pass (1 GiB of stores), to measure what its residency buys
+        void* fl = ws->scratch("lab_flush", (size_t)1 << 30);
+        SMJ_CHECK(hipMemsetAsync(fl, SMJ_LAB_FLUSH, (size_t)1 << 30, st));
+    }
 #endif
-        if (a.ev_bucket) SMJ_CHECK(hipEventRecord(a.ev_bucket, st));
-        GroupArgs Gs = G;
-        Gs.per = (ngroups + maxwg - 1) / maxwg;
-        const uint32_t nwg = (ngroups + Gs.per - 1) / Gs.per;
+    if (a.ev_bucket) SMJ_CHECK(hipEventRecord(a.ev_bucket, st));
+    {
+        const uint32_t maxwg = gs_wg_per_cu<W>() * 256;
+        G.per = (ngroups + maxwg - 1) / maxwg;
+        const uint32_t nwg = (ngroups + G.per - 1) / G.per;
         TraceScope ts(ws, "k_groupsort", st);
-        launch_groupsort<Lay>(group_tpl(nmax, nb, a.nseg, tsz), nwg, st, Gs);
-    };
-    if (fused) {
-        const uint32_t gpb = SMJ_FUSED_GPB < nb2 ? SMJ_FUSED_GPB : nb2;
-        const uint32_t gpi = (nb2 + gpb - 1) / gpb;
-        const uint32_t lag = SMJ_FUSED_LAG;
-        // [0] head, [1] items, [2..] per-bucket tile counters
-        unsigned int* ctr = (unsigned int*)ws->scratch("fz_ctr", (size_t)(nb + 2) * 4);
-        SMJ_CHECK(hipMemsetAsync(ctr, 0, (size_t)(nb + 2) * 4, st));
-        uint32_t* sched = (uint32_t*)ws->scratch(
-            "fz_sched", ((size_t)ub[0] + (nrel > 1 ? ub[1] : 0) + (size_t)nb * gpi) * 4);
-        hipLaunchKernelGGL(k_sched, dim3((nb + lag + 255) / 256), dim3(256), 0, st,
-                           tt[0].btile0, tt[nrel > 1 ? 1 : 0].btile0, nrel, nb, lag, gpi, sched,
-                           ctr + 1);
-        if (a.ev_bucket) SMJ_CHECK(hipEventRecord(a.ev_bucket, st));
-        FusedArgs F;
-        F.G = G;
-        F.plan = *a.host_plan;
-        F.nb = nb;
-        F.d2_fast = T.d2_fast;
-        F.gpb = gpb;
-        F.sched = sched;
-        F.nitems = ctr + 1;
-        F.head = ctr;
-        F.done = ctr + 2;
-        F.err = a.status + 3;
-        const size_t tile_lds = FTILE * sizeof(W) + ((size_t)nb2 + 1 + 16) * 4 + 64;
-        const size_t lds = std::max(sizeof(GroupLDS<W>), tile_lds);
-        const int tpl = expected_tiles(nmax, nb, a.nseg, FTILE) <= 128 ? 2 : 4;
-        TraceScope ts(ws, "k_fused", st);
-        if (tpl == 4)
-            launch_fused<Lay, 4>(F, maxwg, lds, st);
-        else
-            launch_fused<Lay, 2>(F, maxwg, lds, st);
-    } else {
-        separate();
+        launch_groupsort<Lay>(group_tpl(nmax, nb, a.nseg, tsz), nwg, st, G);
     }
     SMJ_CHECK(hipGetLastError());
     if (a.ev_ovf) SMJ_CHECK(hipEventRecord(a.ev_ovf, st));
@@ -2046,24 +1723,12 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
     // (not packable) or with the exact plan (a key outside a guessed one); the
     // tile and group passes exited at once on the latter two
     if (h[0] || h[1]) return false;
-    if (fused && h[3]) {
-        // a fused wait gave up (never expected): the separate passes, from
-        // the tiles as they are (regrouping a grouped tile changes nothing)
-        fprintf(stderr, "[WARN] smj: fused bucket pass timed out; separate passes\n");
-        if (a.count_dev) SMJ_CHECK(hipMemsetAsync(a.count_dev, 0, 8, st));
-        SMJ_CHECK(hipMemsetAsync(a.status + 2, 0, 8, st));
-        separate();
-        SMJ_CHECK(hipMemcpyAsync(h, a.status, 16, hipMemcpyDeviceToHost, st));
-        SMJ_CHECK(hipStreamSynchronize(st));
-    }
     const uint32_t no = h[2];
     if (no == 0) return true;
     if (no > ovf_cap) {
         fprintf(stderr, "[ERROR] smj: overflow table too small\n");
         abort();
     }
-    // the skew kernels read the digit-major prefix table
-    if (fused && !h[3]) launch_preft(tt, nrel, ub, ntiles, nb2, st);
     std::vector<uint64_t> hdst((size_t)2 * nb);
     for (int r = 0; r < nrel; r++)
         SMJ_CHECK(hipMemcpyAsync(hdst.data() + (size_t)r * nb, ostart[r], (size_t)nb * 8,

@@ -405,7 +405,6 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
         if (mode < 2) a.part_flag = status;
         uint32_t why[2] = {0, 0};
         a.status_out = why;
-        a.fused_ok = mode < 2;
         if (bucket_sort(ws, a, st)) break;
         if (guessed && (why[1] & kBadRange)) {
             // a key outside 1..size_guess: the exact plan, attempts from the top

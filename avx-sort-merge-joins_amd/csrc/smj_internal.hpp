@@ -296,10 +296,6 @@ struct BucketSortArgs {
     // host copy of status words [0] and [1] after a false return (why the
     // attempt was void: overflow, kBadPayload / kBadRange)
     uint32_t* status_out = nullptr;
-    // the partition regions start on 128-byte lines of their own (the sampled
-    // level-1 partition), so the tile and group passes may run fused (k_fused;
-    // status word [3] = its error flag)
-    bool fused_ok = false;
     // the 32-bit digit fast path of the tile and group passes (keys outside
     // the plan range only in the first and the last bucket); the segmented
     // join turns it off for tuples (a caller's key outside its range could sit

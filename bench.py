@@ -91,7 +91,6 @@ def alg_bytes_per_launch(name, n_rel, nR, nS, w, op="join"):
         "k_scatter": 2 * n_rel * w,          # one relation per launch
         "k_tilepass": 2 * both * w,
         "k_groupsort": 2 * both * w,
-        "k_fused": 4 * both * w,             # the tile pass + the group pass in one launch
         "k_km_merge": 2 * n_rel * w,         # every tuple of the runs, once
     }.get(name)
 
