@@ -457,17 +457,37 @@ class DistributedJoin:
         return self._finish(rel, st)
 
     def _rows(self, xb, cap, cs, sl, rl):
-        """Asynchronous row exchange in one batch of point-to-point operations:
-        rank g gets this rank's chunk xb[cs[g], cs[g] + sl[g]), the rows from
-        the other ranks land after the partition (xb[cap:], in rank order);
-        this rank's own chunk stays where it is.  Messages above CHUNK_BYTES
-        go in pieces (the RCCL message limit above)."""
-        me = self.rank
+        """Asynchronous row exchange: rank g gets this rank's chunk
+        xb[cs[g], cs[g] + sl[g]), the rows from the other ranks land after the
+        partition (xb[cap:], in rank order); this rank's own chunk stays where
+        it is.  Over RCCL: list all-to-alls on the group's communicator (self
+        empty), in rounds of at most CHUNK_BYTES per peer (the RCCL message
+        limit above); elsewhere (gloo) one batch of point-to-point pairs."""
+        me, G = self.rank, self.world
+        if G == 1:
+            return _Works([])
         row = xb.element_size() * (xb[0].numel() if xb.dim() > 1 else 1)
         step = max(CHUNK_BYTES // row, 1)
+        ro, roff = cap, []
+        for g in range(G):
+            roff.append(ro)
+            ro += 0 if g == me else rl[g]
+        if xb.is_cuda and dist.get_backend(self.group) == "nccl":
+            rounds = max(-(-max(sl[g], rl[g]) // step) for g in range(G) if g != me)
+            works = []
+            for k in range(max(rounds, 1)):
+                lo = k * step
+
+                def piece(start, n, g):
+                    if g == me or lo >= n:
+                        return xb[:0]
+                    return xb[start + lo:start + min(lo + step, n)]
+                ins = [piece(cs[g], sl[g], g) for g in range(G)]
+                outs = [piece(roff[g], rl[g], g) for g in range(G)]
+                works.append(dist.all_to_all(outs, ins, group=self.group, async_op=True))
+            return _Works(works)
         ops = []
-        ro = cap
-        for g in range(self.world):
+        for g in range(G):
             if g == me:
                 continue
             peer = self._global(g)
@@ -475,9 +495,8 @@ class DistributedJoin:
                 ops.append(dist.P2POp(dist.isend, xb[cs[g] + k:cs[g] + min(k + step, sl[g])],
                                       peer, group=self.group))
             for k in range(0, rl[g], step):
-                ops.append(dist.P2POp(dist.irecv, xb[ro + k:ro + min(k + step, rl[g])],
+                ops.append(dist.P2POp(dist.irecv, xb[roff[g] + k:roff[g] + min(k + step, rl[g])],
                                       peer, group=self.group))
-            ro += rl[g]
         return _Works(dist.batch_isend_irecv(ops) if ops else [])
 
     def _global(self, g):

@@ -264,3 +264,26 @@ def test_exchange_table_kernels(libs, F, G):
         lib.dev_xrecv(rmsg.cuda(), chunk, G, r, mine, K, t, c, cap, sm)
         torch.cuda.synchronize()
         assert torch.equal(t.cpu(), wt) and torch.equal(c.cpu(), wc) and torch.equal(sm.cpu(), ws)
+
+
+def test_rccl_list_all_to_all_views(libs, monkeypatch):
+    """The row exchange's RCCL form (smj/dist.py _rows: list all_to_all of
+    views into one buffer, empty views for ranks with nothing to send, several
+    rounds): on a one-rank group the call shape and the view semantics."""
+    import torch
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        buf = torch.arange(1000, dtype=torch.int64, device="cuda")
+        out = torch.full((1000,), -1, dtype=torch.int64, device="cuda")
+        for lo, hi in ((0, 300), (300, 300), (300, 1000)):  # a piece, an empty one, the rest
+            dist.all_to_all([out[lo:hi]], [buf[lo:hi]], async_op=True).wait()
+        torch.cuda.synchronize()
+        assert torch.equal(out, buf)
+        e = buf[:0]
+        dist.all_to_all([e], [e], async_op=True).wait()
+        torch.cuda.synchronize()
+    finally:
+        dist.destroy_process_group()
