@@ -180,7 +180,7 @@ def xrecv_torch(msg, chunk, world, rank, mine, K, tstart, tcnt, cap, summary):
     summary[:2 * G] = chunk
     summary[2 * G:3 * G] = m[:, 0]
     summary[3 * G:4 * G] = m[:, 1]
-    summary[4 * G:] = m[:, 2:HEAD].max(0).values
+    summary[4 * G:4 * G + 2] = m[:, 2:HEAD].max(0).values
 
 
 class DeviceOps:
@@ -384,7 +384,8 @@ class DistributedJoin:
         chunk = self._small("xch" + key, (2 * G,), dev=dev)
         tstart = self._small("xts" + key, (nb, G * K), dev=dev)
         tcnt = self._small("xtc" + key, (nb, G * K), dev=dev)
-        summary = self._small("xsm" + key, (4 * G + 2,), dev=dev)
+        # [4 G + 2]: the largest row message of any rank (all_to_all rounds)
+        summary = self._small("xsm" + key, (4 * G + 3,), dev=dev)
         xsend(start, cnt, fl, G, inp, chunk)
         if G == 1:
             msg = inp
@@ -394,6 +395,10 @@ class DistributedJoin:
             dist.all_to_all_single(msg, inp, [HEAD + 2 * mine * K] * G, per_in,
                                    group=self.group)
         xrecv(msg, chunk, G, me, mine, K, tstart, tcnt, cap, summary)
+        # every rank must run the same number of row all-to-all rounds
+        summary[4 * G + 2:] = summary[G:3 * G].max()
+        if G > 1:
+            dist.all_reduce(summary[4 * G + 2:], op=dist.ReduceOp.MAX, group=self.group)
         if summary.is_cuda:
             hs = self.buf.get("xhost" + key)
             if hs is None or hs.shape != summary.shape:
@@ -422,7 +427,7 @@ class DistributedJoin:
                     st["ev"].synchronize()
                 host = st["host"].tolist()
                 cs, sl, rl, ru = host[:G], host[G:2 * G], host[2 * G:3 * G], host[3 * G:4 * G]
-                bad, ovf = host[4 * G:]
+                bad, ovf, gmax = host[4 * G:]
                 if not ovf and not (st["packed"] and bad):
                     break
                 packed = st["packed"] and not bad
@@ -442,9 +447,9 @@ class DistributedJoin:
         if key == "S" and xb.is_cuda:
             ev = torch.cuda.Event(enable_timing=True)
             ev.record()
-        work = self._rows(xb, cap, cs, sl, rl)
+        work = self._rows(xb, cap, cs, sl, rl, gmax)
         self.last_recv[key] = (sl, rl)
-        self.last_rows[key] = (xb, cap, cs, sl, rl)  # bench.py --op exchange repeats it
+        self.last_rows[key] = (xb, cap, cs, sl, rl, gmax)  # bench.py --op exchange repeats it
         self._ev_issue = ev
         return xb, st["tstart"], st["tcnt"], sum(ru), work, st["packed"]
 
@@ -456,13 +461,15 @@ class DistributedJoin:
             st = self._attempt(rel, key, False, self.sampled)
         return self._finish(rel, st)
 
-    def _rows(self, xb, cap, cs, sl, rl):
+    def _rows(self, xb, cap, cs, sl, rl, gmax=None):
         """Asynchronous row exchange: rank g gets this rank's chunk
         xb[cs[g], cs[g] + sl[g]), the rows from the other ranks land after the
         partition (xb[cap:], in rank order); this rank's own chunk stays where
         it is.  Over RCCL: list all-to-alls on the group's communicator (self
         empty), in rounds of at most CHUNK_BYTES per peer (the RCCL message
-        limit above); elsewhere (gloo) one batch of point-to-point pairs."""
+        limit above; `gmax`, the largest message of any rank, fixes the
+        number of rounds on every rank); elsewhere (gloo) one batch of
+        point-to-point pairs."""
         me, G = self.rank, self.world
         if G == 1:
             return _Works([])
@@ -473,7 +480,9 @@ class DistributedJoin:
             roff.append(ro)
             ro += 0 if g == me else rl[g]
         if xb.is_cuda and dist.get_backend(self.group) == "nccl":
-            rounds = max(-(-max(sl[g], rl[g]) // step) for g in range(G) if g != me)
+            if gmax is None:
+                raise ValueError("the RCCL row exchange needs the global message maximum")
+            rounds = -(-gmax // step)
             works = []
             for k in range(max(rounds, 1)):
                 lo = k * step

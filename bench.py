@@ -482,11 +482,11 @@ def run_exchange(a, json_out, N, rank, local):
     _, _, _, _, work, packed = dj._exchange(S, "S")
     work.wait()
     torch.cuda.synchronize()
-    xb, cap, cs, sl, rl = dj.last_rows["S"]
+    xb, cap, cs, sl, rl, gmax = dj.last_rows["S"]
     row = 8 if packed else 2 * xb.element_size()
 
     def step():
-        dj._rows(xb, cap, cs, sl, rl).wait()
+        dj._rows(xb, cap, cs, sl, rl, gmax).wait()
 
     class _NoTrace:
         def trace(self, on):

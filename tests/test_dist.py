@@ -220,11 +220,15 @@ def _worker(rank, world, port, n, q, s_payload="negative", mode="sampled"):
         # the row exchange alone (bench.py --op exchange repeats it): the last
         # step's transfer again lands the same rows in the same places, and the
         # own chunk is never copied
-        xb, cap, cs, sl, rl = dj.last_rows["S"]
+        xb, cap, cs, sl, rl, gmax = dj.last_rows["S"]
         remote = sum(rl) - rl[rank]
         before = xb[:cap + remote].clone()
         xb[cap:cap + remote] = -9
-        dj._rows(xb, cap, cs, sl, rl).wait()
+        dj._rows(xb, cap, cs, sl, rl, gmax).wait()
+        # every rank agrees on the largest message (the RCCL rounds)
+        t = torch.tensor([gmax])
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        assert int(t) == gmax >= max(sl + rl)
         assert torch.equal(xb[:cap + remote], before)
         # no row lost or duplicated
         sizes = torch.tensor([sR.shape[0], sS.shape[0]])
