@@ -996,10 +996,10 @@ uint64_t merge_join(tuple_t* rtuples, tuple_t* stuples, const uint64_t numR,
         (unsigned long long*)c.ws.scratch("api_cnt", sizeof(unsigned long long));
     SMJ_CHECK(hipMemsetAsync(cnt, 0, 8, c.st));
     merge_join_count(r.d, numR, s.d, numS, cnt, c.st);
-    unsigned long long h = 0;
-    SMJ_CHECK(hipMemcpyAsync(&h, cnt, 8, hipMemcpyDeviceToHost, c.st));
+    unsigned long long* hc = (unsigned long long*)c.ws.host_pinned("mj_cnt_h", 8);
+    SMJ_CHECK(hipMemcpyAsync(hc, cnt, 8, hipMemcpyDeviceToHost, c.st));
     sync();
-    return h;
+    return *hc;
 }
 
 uint64_t merge_join_interpolation(tuple_t* rtuples, tuple_t* stuples,
@@ -1170,9 +1170,12 @@ static result_t* join_api(relation_t* relR, relation_t* relS,
     // no key-range hint: the plan is guessed from |R| as the reference does
     // (keys 1..|R|) and verified by the level-1 scatter
     device_join(&c.ws, r.d, nR, s.d, nS, sR, sS, fb, 1, 0, cnt, c.st, nR);
-    unsigned long long h = 0;
-    SMJ_CHECK(hipMemcpyAsync(&h, cnt, 8, hipMemcpyDeviceToHost, c.st));
+    // the count comes back through pinned memory (a pageable destination
+    // would stage the copy)
+    unsigned long long* hc = (unsigned long long*)c.ws.host_pinned("api_cnt_h", 8);
+    SMJ_CHECK(hipMemcpyAsync(hc, cnt, 8, hipMemcpyDeviceToHost, c.st));
     sync();
+    const unsigned long long h = *hc;
     gettimeofday(&t1, NULL);
     result_t* res = (result_t*)malloc(sizeof(result_t));
     res->totalresults = (int64_t)h;
