@@ -48,6 +48,9 @@ constexpr int TP_THREADS = SMJ_TP_THREADS;
 #ifndef SMJ_GATHER_NT
 #define SMJ_GATHER_NT 0
 #endif
+#ifndef SMJ_GS_XCD
+#define SMJ_GS_XCD 1  // XCD-aware group order in k_groupsort (0: a lab build's contiguous chunks)
+#endif
 #ifndef SMJ_GS_ABL
 #define SMJ_GS_ABL 0  // ablations for measurements only (1: no in-group sort)
 #endif
@@ -705,24 +708,25 @@ __device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS<typename
     return true;
 }
 
-// Groups [gbeg, gend) in order, software-pipelined across groups: group g+1's
-// tables are built while g's data is in registers, g+1's R is gathered as
-// soon as g's R sits in LDS and g+1's S as soon as g's S does, so both
-// gathers fly under g's sort, write-out and count; g+2's tile runs are loaded
-// one group further ahead.  Matches are added to `matches`.
+// Groups g0, g0 + stride, ... (cnt of them) in order, software-pipelined
+// across groups: the next group's tables are built while the current one's
+// data is in registers, its R is gathered as soon as the current R sits in
+// LDS and its S as soon as the current S does, so both gathers fly under the
+// current sort, write-out and count; the tile runs of the group after next are
+// loaded one group further ahead.  Matches are added to `matches`.
 template <class Lay, int TPL, class Src>
 __device__ __forceinline__ void group_loop(const GroupArgs& A, GroupLDS<typename Lay::W>& L,
-                                           uint32_t gbeg, uint32_t gend,
+                                           uint32_t g0, uint32_t stride, uint32_t cnt,
                                            unsigned long long& matches) {
     typedef typename Lay::W W;
     const RangePlan& P = A.plan;
     const uint32_t tid = otid();
     const int nrel = A.nrel;
-    if (gbeg >= gend) return;
+    if (cnt == 0) return;
 
     for (uint32_t i = tid; i < GS_NB3; i += GS_THREADS) (&L.cnt[0][0])[i] = 0u;
     GroupMeta<TPL> M;
-    load_meta<Src>(A, gbeg, M, false);
+    load_meta<Src>(A, g0, M, false);
     build_tables(A, L, M);
     GroupMeta<TPL> C = M;
     uint32_t cn[2], co[2];
@@ -737,10 +741,10 @@ __device__ __forceinline__ void group_loop(const GroupArgs& A, GroupLDS<typename
         gather_group<Lay, Src>(A, L, C, 0, cn[0], vr);
         if (nrel > 1) gather_group<Lay, Src>(A, L, C, 1, cn[1], vs);
     }
-    if (gbeg + 1 < gend) load_meta<Src>(A, gbeg + 1, M, true);
+    if (cnt > 1) load_meta<Src>(A, g0 + stride, M, true);
 
-    for (uint32_t gi = gbeg; gi < gend; gi++) {
-        const bool has_next = gi + 1 < gend;
+    for (uint32_t j = 0; j < cnt; j++) {
+        const bool has_next = j + 1 < cnt;
         // every lane's gather of group gi has read the tables: rebuild them
         __syncthreads();
         const GroupMeta<TPL> N = M;
@@ -753,7 +757,7 @@ __device__ __forceinline__ void group_loop(const GroupArgs& A, GroupLDS<typename
                 no[r] = r < nrel ? __builtin_amdgcn_readfirstlane(L.off[r]) : 0;
             }
         }
-        if (gi + 2 < gend) load_meta<Src>(A, gi + 2, M, true);
+        if (j + 2 < cnt) load_meta<Src>(A, g0 + (j + 2) * stride, M, true);
         const bool next_fits = has_next && nn[0] <= GS_CAP && nn[1] <= GS_CAP;
         auto gather_next_r = [&]() {
             if (next_fits) gather_group<Lay, Src>(A, L, N, 0, nn[0], vr);
@@ -826,8 +830,14 @@ __device__ __forceinline__ void group_loop(const GroupArgs& A, GroupLDS<typename
     }
 }
 
-// Persistent: workgroup w sorts groups [g_begin + w * per, ... + per) in
-// order (group_loop).
+// Persistent: every workgroup sorts `per` groups in order (group_loop).
+// XCD-aware: blocks b and b + 8 share an XCD and its L2 (MI355X_MICROARCH
+// [G]: observed placement, used for speed only).  The blocks of one XCD take
+// one contiguous range of groups, interleaved (block k of the XCD: groups
+// lo + k, lo + k + nx, ...), so at any moment they sort neighbouring groups:
+// the 128-byte line that two neighbouring groups' runs share in a tile is
+// fetched into that L2 once instead of once per XCD.  The grid is a multiple
+// of 8 (launch_groupsort).
 template <class Lay, int TPL>
 __global__ void __launch_bounds__(GS_THREADS, gs_wg_per_cu<typename Lay::W>() * GS_THREADS / 256)
 k_groupsort(GroupArgs A) {
@@ -835,11 +845,19 @@ k_groupsort(GroupArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     if (A.pack_bad && *A.pack_bad) return;
     GroupLDS<W>& L = *reinterpret_cast<GroupLDS<W>*>(lds_raw);
-    const uint32_t gbeg = A.g_begin + blockIdx.x * A.per;
-    const uint32_t gend = min(gbeg + A.per, A.g_end);
+#if SMJ_GS_XCD
+    const uint32_t nx = gridDim.x / 8, k = blockIdx.x / 8;
+    const uint32_t lo = A.g_begin + (blockIdx.x % 8) * nx * A.per;
+    const uint32_t g0 = lo + k, stride = nx;
+    const uint32_t hi = min(lo + nx * A.per, A.g_end);
+    const uint32_t cnt = g0 < hi ? (hi - g0 + nx - 1) / nx : 0u;
+#else
+    const uint32_t g0 = A.g_begin + blockIdx.x * A.per, stride = 1;
+    const uint32_t cnt = g0 < A.g_end ? min(A.per, A.g_end - g0) : 0u;
+#endif
     unsigned long long matches = 0;
-    if (gbeg >= gend) return;
-    group_loop<Lay, TPL, SrcPlain>(A, L, gbeg, gend, matches);
+    if (cnt == 0) return;
+    group_loop<Lay, TPL, SrcPlain>(A, L, g0, stride, cnt, matches);
     if (A.nrel == 2) {
         matches = wave_sum(matches);
         if ((otid() & 63) == 0 && matches) atomicAdd(A.count_dev, matches);
@@ -1581,6 +1599,15 @@ static int group_tpl(uint64_t nmax, uint32_t nb, uint32_t nseg, uint32_t tsz = T
     return expected_tiles(nmax, nb, nseg, tsz) <= 128 ? 2 : 4;
 }
 
+// persistent grid of the group pass: `per` groups per workgroup, at most
+// maxwg (a multiple of 8) workgroups, rounded up to a multiple of 8 for the
+// XCD-aware order (blocks past the last group exit)
+static uint32_t groupsort_grid(uint32_t ngroups, uint32_t maxwg, uint32_t& per) {
+    per = (ngroups + maxwg - 1) / maxwg;
+    const uint32_t nwg = (ngroups + per - 1) / per;
+    return (nwg + 7) & ~7u;
+}
+
 template <class Lay>
 static void launch_groupsort(int tpl, uint32_t nwg, hipStream_t st, const GroupArgs& G) {
     if (tpl == 4)
@@ -1695,8 +1722,7 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
     if (a.ev_bucket) SMJ_CHECK(hipEventRecord(a.ev_bucket, st));
     {
         const uint32_t maxwg = gs_wg_per_cu<W>() * 256;
-        G.per = (ngroups + maxwg - 1) / maxwg;
-        const uint32_t nwg = (ngroups + G.per - 1) / G.per;
+        const uint32_t nwg = groupsort_grid(ngroups, maxwg, G.per);
         TraceScope ts(ws, "k_groupsort", st);
         launch_groupsort<Lay>(group_tpl(nmax, nb, a.nseg, tsz), nwg, st, G);
     }
@@ -1886,8 +1912,7 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
         // persistent: gs_wg_per_cu workgroups per CU, consecutive groups each
         const uint32_t ng = G.g_end - G.g_begin;
         const uint32_t maxwg = gs_wg_per_cu<Tup>() * 256;
-        G.per = (ng + maxwg - 1) / maxwg;
-        const uint32_t nwg = (ng + G.per - 1) / G.per;
+        const uint32_t nwg = groupsort_grid(ng, maxwg, G.per);
         TraceScope ts(ws, "k_groupsort", st);
         const uint64_t nmax = nrel > 1 && a.n[1] > a.n[0] ? a.n[1] : a.n[0];
         launch_groupsort<LayTup>(group_tpl(nmax, nb, nseg), nwg, st, G);
