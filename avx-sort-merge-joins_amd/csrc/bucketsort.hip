@@ -316,11 +316,15 @@ struct GroupLDS {
     W B[GS_CAP + 1];                      // one relation's group (+ a dump slot)
     uint32_t cnt[2][GS_NB3 / 2];          // d3 histograms of R and S (2 x u16)
     uint32_t cur[GS_NB3 / 2];             // placement cursors (2 x u16)
-    // the group's non-empty tile runs, numbered in position order: run k
-    // starts at group position (uint32)run[k] and at bucket offset run[k] >> 32
-    unsigned long long run[2][GS_TMAX];
-    unsigned long long smap[2][GS_WIN];   // bit j: a run starts at position j
-    uint32_t wk[2][GS_WIN];               // runs starting before position 64 * w
+    // the group's non-empty tile runs, numbered in position order: group
+    // position j of run k sits at bucket offset j + run[k] (mod 2^32)
+    uint32_t run[2][GS_TMAX];
+    // per 64-position window w: bit i of m: a run starts at position 64 w + i;
+    // wk: runs starting before the window, minus one (one 16-byte LDS read)
+    struct Win {
+        unsigned long long m;
+        uint32_t wk, pad;
+    } win[2][GS_WIN];
     uint32_t wtot[GS_THREADS / 64];
     unsigned long long scan64[GS_THREADS / 64 + 1];
     uint32_t n[2];
@@ -474,7 +478,7 @@ __device__ __forceinline__ void build_tables(const GroupArgs& A, LDS& L,
     if (wid < (uint32_t)A.nrel) {
         const int r = wid;
         const uint32_t nt = r ? M.nt[1] : M.nt[0];
-        if (lane < GS_WIN) L.smap[r][lane] = 0ull;
+        if (lane < GS_WIN) L.win[r][lane].m = 0ull;
         // tiles lane + 64 h: scan of (start in tile << 32 | length), and the
         // non-empty runs compacted in tile order = position order (run starts
         // at or past GS_CAP only occur in groups that overflow: never gathered)
@@ -495,7 +499,7 @@ __device__ __forceinline__ void build_tables(const GroupArgs& A, LDS& L,
         }
 #pragma unroll
         for (int h = 0; h < TPL; h++)
-            if (e[h]) L.run[r][k[h]] = ((unsigned long long)(M.toff[h] + M.lo[h]) << 32) | s[h];
+            if (e[h]) L.run[r][k[h]] = M.toff[h] + M.lo[h] - s[h];
         if (lane == 0) {
             L.n[r] = nt <= 64 * TPL ? (uint32_t)acc : 0xffffffffu;
             L.off[r] = (uint32_t)(acc >> 32);
@@ -503,11 +507,11 @@ __device__ __forceinline__ void build_tables(const GroupArgs& A, LDS& L,
         wave_lds_sync();
 #pragma unroll
         for (int h = 0; h < TPL; h++)
-            if (e[h]) atomicOr(&L.smap[r][s[h] >> 6], 1ull << (s[h] & 63));
+            if (e[h]) atomicOr(&L.win[r][s[h] >> 6].m, 1ull << (s[h] & 63));
         wave_lds_sync();
-        const uint32_t c = lane < GS_WIN ? (uint32_t)__popcll(L.smap[r][lane]) : 0u;
+        const uint32_t c = lane < GS_WIN ? (uint32_t)__popcll(L.win[r][lane].m) : 0u;
         const uint32_t incl = wave_incl_scan32(c);
-        if (lane < GS_WIN) L.wk[r][lane] = incl - c;
+        if (lane < GS_WIN) L.win[r][lane].wk = incl - c - 1u;
     }
     __syncthreads();
 }
@@ -556,25 +560,30 @@ __device__ __forceinline__ void group_overflow(const GroupArgs& A, LDS& L,
 }
 
 // gather relation r's group into registers (loads only: every load in
-// flight at once); lanes past the end re-read the last element.  Position j
-// = k * GS_THREADS + thread: a wave's 64 positions share one bitmap window
-// (broadcast reads), its run is found with a lane count of the window's
-// run starts.
+// flight at once).  Position j = k * GS_THREADS + thread: a wave's 64
+// positions are one bitmap window (broadcast read), so the run of the lane's
+// position is the window's earlier runs plus the run starts below the lane
+// (mbcnt) and at it.  Lanes past the end re-read position 0.
 template <class Lay, class Src, class Meta>
 __device__ __forceinline__ void gather_group(const GroupArgs& A, GroupLDS<typename Lay::W>& L,
                                              const Meta& C, int r, uint32_t n,
                                              typename Lay::W (&v)[GS_ITEMS]) {
     if (n == 0) return;
     const typename Lay::W* tp = static_cast<const typename Lay::W*>(A.tmp[r]) + C.bst[r];
-    const uint32_t last = n - 1;
+    const uint32_t lane = lane_id();
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(otid() >> 6);
 #pragma unroll
     for (int k = 0; k < GS_ITEMS; k++) {
-        const uint32_t j = min(k * GS_THREADS + otid(), last);
-        const uint32_t w = j >> 6;
-        const unsigned long long bits = L.smap[r][w] & (~0ull >> (63 - (j & 63)));
-        const uint32_t q = L.wk[r][w] + (uint32_t)__popcll(bits) - 1u;
-        const unsigned long long e = L.run[r][q];
-        v[k] = Src::load(tp + ((uint32_t)(e >> 32) + (j - (uint32_t)e)));
+        const uint32_t w = k * (GS_THREADS / 64) + wid;  // uniform
+        const uint32_t j = w * 64 + lane;
+        const auto win = L.win[r][w];
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+            (uint32_t)(win.m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)win.m, 0u));
+        const uint32_t at = (uint32_t)(win.m >> lane) & 1u;
+        const bool ok = j < n;
+        const uint32_t q = ok ? win.wk + below + at : 0u;
+        const uint32_t p = ok ? j : 0u;
+        v[k] = Src::load(tp + (uint32_t)(p + L.run[r][q]));
     }
 }
 
