@@ -124,8 +124,8 @@ def host_cores():
     return share, lscpu
 
 
-def _join_once(exe, n, threads):
-    r = subprocess.run([exe, str(n), str(n), str(threads), "128"],
+def _join_once(exe, n, threads, skew=0.0):
+    r = subprocess.run([exe, str(n), str(n), str(threads), "128", str(skew)],
                        capture_output=True, text=True, timeout=900, cwd="/tmp")
     m = re.search(r"SMJ_CPU_BASELINE (\{.*\})", r.stdout)
     if not m:
@@ -138,28 +138,32 @@ def _join_once(exe, n, threads):
     return t, d["count"] == n
 
 
-def cpu_baseline(width, n):
+def cpu_baseline(width, n, skew=0.0):
     """The reference m-way join (oracle/_ref/cpu_baseline*: compiled from the
     reference's sources) on this host: T = the largest power of two within
     the job's CPU share, and T = 1.  16-byte tuples take the
-    reference's scalar path, 8-byte tuples its AVX path."""
+    reference's scalar path, 8-byte tuples its AVX path.  skew > 0: S is the
+    reference driver's --skew input (create_relation_zipf, srand(54321)), the
+    relation the GPU line joins with --dist zipf."""
     exe = _ref_exe(f"cpu_baseline{width}")
     share, lscpu = host_cores()
     threads = 1
     while threads * 2 <= share and threads * 2 <= 1024:
         threads *= 2
-    t, ok = _join_once(exe, n, threads)
+    t, ok = _join_once(exe, n, threads, skew)
     # T = 1 on a quarter of the sample (a 128M single-thread run alone takes
     # about 40 s with its generation)
     n1 = max(n // 4, 1)
-    t1, ok1 = _join_once(exe, n1, 1)
+    t1, ok1 = _join_once(exe, n1, 1, skew)
     path = "scalar" if width == 16 else "AVX"
     return {"value": round(2 * n / t / 1e6, 3), "unit": "Mtuples/s",
             "cores": threads, "kind": "reference",
             "host_cores_lscpu": lscpu,
             "t1_value": round(2 * n1 / t1 / 1e6, 3),
             "sample": f"sortmergejoin_multiway {n}x{n} {width}B tuples, {threads} threads "
-                      f"(t1_value: 1 thread on {n1}x{n1}), PK/FK uniform, {path} path, "
+                      f"(t1_value: 1 thread on {n1}x{n1}), "
+                      f"{f'PK / Zipf {skew} FK (create_relation_zipf)' if skew > 0 else 'PK/FK uniform'}, "
+                      f"{path} path, "
                       f"count {'ok' if ok and ok1 else 'MISMATCH'}"}
 
 
@@ -340,7 +344,7 @@ def main():
 
     cpu = None
     if N == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(w, a.cpu_n)
+        cpu = cpu_baseline(w, a.cpu_n, a.theta if a.dist == "zipf" else 0.0)
 
     strong = a.n_total is not None
     out = {

@@ -2,10 +2,12 @@
 // /root/reference/src by oracle/build_ref.sh into oracle/_ref/) on the host
 // cores, for bench.py's cpu_baseline leg.  Not part of the product.
 //
-// usage: cpu_baseline NR NS NTHREADS [FANOUT]
+// usage: cpu_baseline NR NS NTHREADS [FANOUT [SKEW]]
 // Inputs follow the reference driver (src/main.c:502-583): R = PK keys
 // 1..NR with payload 5+i (parallel_create_relation), S = uniform FK over
-// 1..NR.  Prints one line "SMJ_CPU_BASELINE {json}" on stdout at the end.
+// 1..NR, or with SKEW > 0 the driver's --skew input, create_relation_zipf
+// (main.c:572-575).  Prints one line "SMJ_CPU_BASELINE {json}" on stdout at
+// the end.
 #include <stdio.h>
 #include <stdlib.h>
 #include <sys/time.h>
@@ -25,6 +27,7 @@ int main(int argc, char** argv) {
     const int64_t nR = atoll(argv[1]), nS = atoll(argv[2]);
     const int nthr = atoi(argv[3]);
     const int fan = argc > 4 ? atoi(argv[4]) : 128;
+    const double skew = argc > 5 ? atof(argv[5]) : 0.0;
     cpu_mapping_init();
     joinconfig_t cfg;
     cfg.NTHREADS = nthr;
@@ -46,7 +49,10 @@ int main(int argc, char** argv) {
     seed_generator(12345);
     parallel_create_relation(&R, nR, nthr, nR);
     seed_generator(54321);
-    parallel_create_relation(&S, nS, nthr, nR);
+    if (skew > 0)
+        create_relation_zipf(&S, nS, nR, skew);
+    else
+        parallel_create_relation(&S, nS, nthr, nR);
     struct timeval t0, t1;
     gettimeofday(&t0, NULL);
     result_t* res = sortmergejoin_multiway(&R, &S, &cfg);
