@@ -463,8 +463,8 @@ def run_exchange(a, json_out, N, rank, local):
     default 128M, the join's slice) is range-partitioned once by
     DistributedJoin (packed words for 16-byte tuples); one step repeats that
     exchange's row transfer -- DistributedJoin._rows, the join's own code
-    path: one batch of point-to-point RCCL sends, chunked above 512 MB, the
-    own chunk read in place.  value = bytes that crossed to OTHER ranks, per
+    path: list all-to-alls on the RCCL communicator in rounds of at most
+    512 MB per peer, the own chunk read in place.  value = bytes that crossed to OTHER ranks, per
     GPU per second (N = 1: no row leaves the rank, nothing to time)."""
     import torch.distributed as dist
     import smj
