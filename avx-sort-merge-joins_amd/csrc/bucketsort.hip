@@ -51,8 +51,12 @@ constexpr int TP_THREADS = SMJ_TP_THREADS;
 #ifndef SMJ_GS_XCD
 #define SMJ_GS_XCD 1  // XCD-aware group order in k_groupsort (0: a lab build's contiguous chunks)
 #endif
+#ifndef SMJ_GS_PAIR
+#define SMJ_GS_PAIR 1  // one relation: two groups per group-pass iteration (0: a lab build's one)
+#endif
 #ifndef SMJ_GS_ABL
-#define SMJ_GS_ABL 0  // ablations for measurements only (1: no in-group sort)
+#define SMJ_GS_ABL 0  // ablations for measurements only (1: no in-group sort; 2: no
+                      // equal-digit run fixing; 3: no write-out)
 #endif
 constexpr int TP_ITEMS = 16;
 constexpr int TILE2 = TP_THREADS * TP_ITEMS;  // tuples per tile
@@ -300,6 +304,10 @@ struct GroupArgs {
     uint32_t ovf_cap;
     const unsigned int* pack_bad;  // set: the packed partition is void, exit
     uint32_t d3_fast;              // Lay::fast_ok for the level-3 digit (host)
+    // one relation (nrel == 1): two groups per loop iteration, one in each
+    // relation slot (the slots' tables alias relation 0), so that a group's
+    // gather flies under the other slot's sort as in the join
+    uint32_t pair;
 };
 
 // threadIdx.x behind an empty asm: per-thread LDS addresses are recomputed
@@ -347,11 +355,12 @@ struct SrcPlain {
     __device__ static __forceinline__ W load(const W* p) { return *p; }
 };
 
-// A group and, for the calling thread, its tile run: wave r < nrel owns
-// relation r, lane t its tile t (lo = run start in the tile, len = length).
+// A group and, for the calling thread, its tile run: wave r < nslot owns
+// slot r (relation r; in pair mode the r-th group of the iteration), lane t
+// its tile t (lo = run start in the tile, len = length).
 template <int TPL>
 struct GroupMeta {
-    uint32_t b, g;
+    uint32_t b[2], g[2];    // bucket and level-2 digit of slot r's group
     uint32_t t0[2], nt[2];  // first tile and tile count of the bucket
     uint64_t bst[2];        // bucket start (partition buffer)
     uint64_t ost[2];        // bucket start (output)
@@ -359,44 +368,75 @@ struct GroupMeta {
     uint32_t toff[TPL];          // their offsets from the bucket start
 };
 
-template <class Src, int TPL>
-__device__ __forceinline__ void load_meta(const GroupArgs& A, uint32_t gi,
-                                          GroupMeta<TPL>& M, bool same_bucket) {
-    const uint32_t b = gi / A.nb2;
-    M.g = gi % A.nb2;
-    const bool newb = !same_bucket || b != M.b;
-    if (newb) {
+// (PAIR, a template parameter of the kernel and the functions below, is the
+// launch's A.pair)
+template <bool PAIR>
+__device__ __forceinline__ int group_slots(const GroupArgs& A) { return PAIR ? 2 : A.nrel; }
+
+// Metadata of loop iteration j of a workgroup whose groups are g0, g0 +
+// stride, ... (cnt of them): slot r holds group j (both relations) or, in
+// pair mode, group 2j + r; a slot past the end is empty (no tiles).
+template <class Src, bool PAIR, int TPL>
+__device__ __forceinline__ void load_meta(const GroupArgs& A, uint32_t g0, uint32_t stride,
+                                          uint32_t cnt, uint32_t j, GroupMeta<TPL>& M,
+                                          bool same_bucket) {
+    const int nslot = group_slots<PAIR>(A);
+    auto bucket_meta = [&](int r, uint32_t b) {
+        // uniform: keep them in SGPRs
+        M.t0[r] = __builtin_amdgcn_readfirstlane(A.tt[r].btile0[b]);
+        M.nt[r] = __builtin_amdgcn_readfirstlane(A.tt[r].btile0[b + 1]) - M.t0[r];
+        const uint64_t bs = A.bstart[r][b];
+        M.bst[r] = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(bs >> 32)) << 32) |
+                   __builtin_amdgcn_readfirstlane((uint32_t)bs);
+        const uint64_t os = A.ostart[r][b];
+        M.ost[r] = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(os >> 32)) << 32) |
+                   __builtin_amdgcn_readfirstlane((uint32_t)os);
+    };
+    if (!PAIR) {
+        // both relations of one group: slot 0's b and g stand for both
+        const uint32_t gi = g0 + j * stride;
+        const uint32_t b = gi / A.nb2;
+        M.g[0] = gi % A.nb2;
+        if (!same_bucket || b != M.b[0]) {
 #pragma unroll
-        for (int r = 0; r < 2; r++) {
-            M.t0[r] = M.nt[r] = 0;
-            M.bst[r] = M.ost[r] = 0;
-            if (r < A.nrel) {
-                // uniform: keep them in SGPRs
-                M.t0[r] = __builtin_amdgcn_readfirstlane(A.tt[r].btile0[b]);
-                M.nt[r] = __builtin_amdgcn_readfirstlane(A.tt[r].btile0[b + 1]) - M.t0[r];
-                const uint64_t bs = A.bstart[r][b];
-                M.bst[r] = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(bs >> 32)) << 32) |
-                           __builtin_amdgcn_readfirstlane((uint32_t)bs);
-                const uint64_t os = A.ostart[r][b];
-                M.ost[r] = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(os >> 32)) << 32) |
-                           __builtin_amdgcn_readfirstlane((uint32_t)os);
+            for (int r = 0; r < 2; r++) {
+                M.t0[r] = M.nt[r] = 0;
+                M.bst[r] = M.ost[r] = 0;
+                if (r < A.nrel) bucket_meta(r, b);
             }
         }
+        M.b[0] = b;
+    } else {
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+            const uint32_t k = 2 * j + r;
+            const bool valid = k < cnt;  // uniform
+            const uint32_t gi = g0 + k * stride;
+            const uint32_t b = valid ? gi / A.nb2 : 0xffffffffu;
+            M.g[r] = valid ? gi % A.nb2 : 0u;
+            if (!valid) {
+                M.t0[r] = M.nt[r] = 0;
+                M.bst[r] = M.ost[r] = 0;
+            } else if (!same_bucket || b != M.b[r]) {
+                bucket_meta(r, b);
+            }
+            M.b[r] = b;
+        }
     }
-    M.b = b;
     // the wave index is uniform: table pointers stay scalar
     const uint32_t wid = __builtin_amdgcn_readfirstlane(otid() >> 6), lane = otid() & 63;
 #pragma unroll
     for (int h = 0; h < TPL; h++) M.lo[h] = M.len[h] = M.toff[h] = 0;
-    if (wid < (uint32_t)A.nrel) {
+    if (wid < (uint32_t)nslot) {
         const uint32_t nt = wid ? M.nt[1] : M.nt[0];
         const uint32_t t0 = wid ? M.t0[1] : M.t0[0];
+        const uint32_t g = PAIR && wid ? M.g[1] : M.g[0];
 #pragma unroll
         for (int h = 0; h < TPL; h++) {
             const uint32_t t = lane + 64 * h;
             if (nt <= 64 * TPL && t < nt) {
                 // digit-major prefix (SrcPlain): lanes read consecutive entries
-                Src::run(A.tt[wid], A.nb2, t0 + t, M.g, M.lo[h], M.len[h]);
+                Src::run(A.tt[wid], A.nb2, t0 + t, g, M.lo[h], M.len[h]);
                 M.toff[h] = (uint32_t)(A.tt[wid].off[t0 + t] - (wid ? M.bst[1] : M.bst[0]));
             }
         }
@@ -471,11 +511,11 @@ __device__ __forceinline__ void insertion_sort(typename Lay::W* a, uint32_t n) {
 // the number of runs that start before it (no block barrier inside; one at
 // the end).  The run of position j is then wk[j/64] + (starts in its window
 // up to j) - 1: two LDS round trips per gathered element, no search.
-template <int TPL, class LDS>
+template <bool PAIR, int TPL, class LDS>
 __device__ __forceinline__ void build_tables(const GroupArgs& A, LDS& L,
                                              const GroupMeta<TPL>& M) {
     const uint32_t wid = otid() >> 6, lane = otid() & 63;
-    if (wid < (uint32_t)A.nrel) {
+    if (wid < (uint32_t)group_slots<PAIR>(A)) {
         const int r = wid;
         const uint32_t nt = r ? M.nt[1] : M.nt[0];
         if (lane < GS_WIN) L.win[r][lane].m = 0ull;
@@ -520,33 +560,38 @@ __device__ __forceinline__ void build_tables(const GroupArgs& A, LDS& L,
 // queued: its size and offset in each relation come from the prefix table,
 // its tuples are sorted and counted afterwards by the skew kernels below, over
 // many workgroups.  Called by the whole workgroup (uniform control flow).
-template <class Src, class LDS, class Meta>
+// In pair mode `slot` names the one slot whose group is queued (as relation
+// 0 of its entry); otherwise both relations of the group are.
+template <class Src, bool PAIR, class LDS, class Meta>
 __device__ __forceinline__ void group_overflow(const GroupArgs& A, LDS& L,
-                                               const Meta& M) {
+                                               const Meta& M, int slot = 0) {
     uint32_t nn[2] = {0, 0};
     uint64_t oo[2] = {0, 0};
     const uint32_t tid = otid();
+    const int nq = PAIR ? 1 : A.nrel;
 #pragma unroll
-    for (int r = 0; r < 2; r++) {
-        if (r >= A.nrel) break;
-        const uint32_t t0 = M.t0[r], nt = M.nt[r];
+    for (int q = 0; q < 2; q++) {
+        if (q >= nq) break;
+        const int r = PAIR ? slot : q;
+        const uint32_t t0 = r ? M.t0[1] : M.t0[0], nt = r ? M.nt[1] : M.nt[0];
+        const uint32_t g = PAIR && r ? M.g[1] : M.g[0];
         unsigned long long acc = 0;
         for (uint32_t t = tid; t < nt; t += GS_THREADS) {
             uint32_t lo, len;
-            Src::run(A.tt[r], A.nb2, t0 + t, M.g, lo, len);
+            Src::run(A.tt[r], A.nb2, t0 + t, g, lo, len);
             acc += ((unsigned long long)lo << 32) | len;
         }
         unsigned long long tot;
         (void)block_scan64(acc, L.scan64, &tot);
-        nn[r] = (uint32_t)tot;
-        oo[r] = tot >> 32;
+        nn[q] = (uint32_t)tot;
+        oo[q] = tot >> 32;
     }
     if (tid == 0) {
         const uint32_t k = atomicAdd(A.novf, 1u);
         if (k < A.ovf_cap) {
             OvfEntry e;
-            e.bucket = M.b;
-            e.d2 = M.g;
+            e.bucket = PAIR && slot ? M.b[1] : M.b[0];
+            e.d2 = PAIR && slot ? M.g[1] : M.g[0];
             e.nr[0] = nn[0];
             e.nr[1] = nn[1];
             e.off[0] = oo[0];
@@ -592,21 +637,22 @@ __device__ __forceinline__ void gather_group(const GroupArgs& A, GroupLDS<typena
 // as the elements sit in LDS (the registers are free): the persistent loop
 // issues the next group's gather there.  Returns false when the group must
 // take the skew path.
-template <class Lay, class Meta, typename Hook>
+template <class Lay, bool PAIR, class Meta, typename Hook>
 __device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS<typename Lay::W>& L,
                                            const Meta& C, const RangePlan& P,
                                            int r, uint32_t nr, uint32_t off,
                                            typename Lay::W (&v)[GS_ITEMS], bool& clamped,
                                            Hook&& after_place) {
     const uint32_t tid = otid(), wid = tid >> 6, lane = tid & 63;
-    const uint32_t d12 = (C.b << P.D2) | C.g;
+    const uint32_t cb = PAIR && r ? C.b[1] : C.b[0], cg = PAIR && r ? C.g[1] : C.g[0];
+    const uint32_t d12 = (cb << P.D2) | cg;
 #if SMJ_GS_ABL == 1
     {   // ablation (measurements only): no sort, gathered order written out
         Tup* dst = A.out[r] + C.ost[r] + off;
 #pragma unroll
         for (int k = 0; k < GS_ITEMS; k++) {
             const uint32_t j = k * GS_THREADS + tid;
-            if (j < nr) st_stream(dst + j, Lay::unpack(P, v[k], C.b));
+            if (j < nr) st_stream(dst + j, Lay::unpack(P, v[k], cb));
         }
         after_place();
         __syncthreads();
@@ -617,8 +663,8 @@ __device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS<typename
     // first and the last group of the plan can hold keys outside its range
     // (plan_rel clamps them there); every other group takes the 32-bit digit.
     uint32_t dg[GS_ITEMS];
-    const bool edge = (C.b == 0 && C.g == 0) ||
-                      (C.b == (1u << P.D1) - 1 && C.g == A.nb2 - 1);
+    const bool edge = (cb == 0 && cg == 0) ||
+                      (cb == (1u << P.D1) - 1 && cg == A.nb2 - 1);
     if (A.d3_fast && !edge) {
         const uint32_t base_lo = (uint32_t)P.base, mask = (1u << P.D3) - 1;
 #pragma unroll
@@ -632,7 +678,7 @@ __device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS<typename
         for (int k = 0; k < GS_ITEMS; k++) {
             const bool valid = k * GS_THREADS + tid < nr;
             clamped |= valid && Lay::clamped(P, v[k]);
-            dg[k] = plan_d3(P, Lay::rel(P, v[k], C.b), d12);
+            dg[k] = plan_d3(P, Lay::rel(P, v[k], cb), d12);
             if (valid) atomicAdd(&L.cnt[r][dg[k] >> 1], 1u << ((dg[k] & 1) * 16));
         }
     }
@@ -676,7 +722,7 @@ __device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS<typename
     }
     after_place();
     __syncthreads();
-    if (dup) {
+    if (dup && SMJ_GS_ABL != 2) {
         // ---- equal-digit runs.  The group is ordered by digit, so an
         // inversion can only sit inside such a run: one parallel pass finds
         // out whether any needs sorting (never for equal tuples of a hot key).
@@ -712,7 +758,7 @@ __device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS<typename
 #pragma unroll
     for (int k = 0; k < GS_ITEMS; k++) {
         const uint32_t j = k * GS_THREADS + tid;
-        if (j < nr) st_stream(dst + j, Lay::unpack(P, L.B[j], C.b));
+        if (j < nr && SMJ_GS_ABL != 3) st_stream(dst + j, Lay::unpack(P, L.B[j], cb));
     }
     return true;
 }
@@ -722,8 +768,10 @@ __device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS<typename
 // data is in registers, its R is gathered as soon as the current R sits in
 // LDS and its S as soon as the current S does, so both gathers fly under the
 // current sort, write-out and count; the tile runs of the group after next are
-// loaded one group further ahead.  Matches are added to `matches`.
-template <class Lay, int TPL, class Src>
+// loaded one group further ahead.  Matches are added to `matches`.  In pair
+// mode (one relation) an iteration takes two consecutive groups of the
+// sequence, one per slot, pipelined the same way.
+template <class Lay, int TPL, class Src, bool PAIR>
 __device__ __forceinline__ void group_loop(const GroupArgs& A, GroupLDS<typename Lay::W>& L,
                                            uint32_t g0, uint32_t stride, uint32_t cnt,
                                            unsigned long long& matches) {
@@ -731,64 +779,94 @@ __device__ __forceinline__ void group_loop(const GroupArgs& A, GroupLDS<typename
     const RangePlan& P = A.plan;
     const uint32_t tid = otid();
     const int nrel = A.nrel;
+    constexpr bool pair = PAIR;
+    const int nslot = group_slots<PAIR>(A);
     if (cnt == 0) return;
+    const uint32_t nit = pair ? (cnt + 1) / 2 : cnt;
+    // a slot's group fits in LDS; without pair mode a group fits when both
+    // of its relations do
+    auto fits = [&](const uint32_t (&n)[2], bool f[2]) {
+        f[0] = n[0] <= GS_CAP;
+        f[1] = n[1] <= GS_CAP;
+        if (!pair) f[0] = f[1] = f[0] && f[1];
+    };
 
     for (uint32_t i = tid; i < GS_NB3; i += GS_THREADS) (&L.cnt[0][0])[i] = 0u;
     GroupMeta<TPL> M;
-    load_meta<Src>(A, g0, M, false);
-    build_tables(A, L, M);
+    load_meta<Src, PAIR>(A, g0, stride, cnt, 0, M, false);
+    build_tables<PAIR>(A, L, M);
     GroupMeta<TPL> C = M;
     uint32_t cn[2], co[2];
 #pragma unroll
     for (int r = 0; r < 2; r++) {
-        cn[r] = r < nrel ? __builtin_amdgcn_readfirstlane(L.n[r]) : 0;
-        co[r] = r < nrel ? __builtin_amdgcn_readfirstlane(L.off[r]) : 0;
+        cn[r] = r < nslot ? __builtin_amdgcn_readfirstlane(L.n[r]) : 0;
+        co[r] = r < nslot ? __builtin_amdgcn_readfirstlane(L.off[r]) : 0;
     }
-    bool cur_fits = cn[0] <= GS_CAP && cn[1] <= GS_CAP;
+    bool cf[2];
+    fits(cn, cf);
     W vr[GS_ITEMS], vs[GS_ITEMS];
-    if (cur_fits) {
-        gather_group<Lay, Src>(A, L, C, 0, cn[0], vr);
-        if (nrel > 1) gather_group<Lay, Src>(A, L, C, 1, cn[1], vs);
-    }
-    if (cnt > 1) load_meta<Src>(A, g0 + stride, M, true);
+    if (cf[0]) gather_group<Lay, Src>(A, L, C, 0, cn[0], vr);
+    if (cf[1] && nslot > 1) gather_group<Lay, Src>(A, L, C, 1, cn[1], vs);
+    if (nit > 1) load_meta<Src, PAIR>(A, g0, stride, cnt, 1, M, true);
 
-    for (uint32_t j = 0; j < cnt; j++) {
-        const bool has_next = j + 1 < cnt;
+    for (uint32_t j = 0; j < nit; j++) {
+        const bool has_next = j + 1 < nit;
         // every lane's gather of group gi has read the tables: rebuild them
         __syncthreads();
         const GroupMeta<TPL> N = M;
         uint32_t nn[2] = {0, 0}, no[2] = {0, 0};
         if (has_next) {
-            build_tables(A, L, N);
+            build_tables<PAIR>(A, L, N);
 #pragma unroll
             for (int r = 0; r < 2; r++) {
-                nn[r] = r < nrel ? __builtin_amdgcn_readfirstlane(L.n[r]) : 0;
-                no[r] = r < nrel ? __builtin_amdgcn_readfirstlane(L.off[r]) : 0;
+                nn[r] = r < nslot ? __builtin_amdgcn_readfirstlane(L.n[r]) : 0;
+                no[r] = r < nslot ? __builtin_amdgcn_readfirstlane(L.off[r]) : 0;
             }
         }
-        if (j + 2 < cnt) load_meta<Src>(A, g0 + (j + 2) * stride, M, true);
-        const bool next_fits = has_next && nn[0] <= GS_CAP && nn[1] <= GS_CAP;
+        if (j + 2 < nit) load_meta<Src, PAIR>(A, g0, stride, cnt, j + 2, M, true);
+        bool nf[2];
+        fits(nn, nf);
+        nf[0] &= has_next;
+        nf[1] &= has_next;
         auto gather_next_r = [&]() {
-            if (next_fits) gather_group<Lay, Src>(A, L, N, 0, nn[0], vr);
+            if (nf[0]) gather_group<Lay, Src>(A, L, N, 0, nn[0], vr);
         };
         auto gather_next_s = [&]() {
-            if (next_fits && nrel > 1) gather_group<Lay, Src>(A, L, N, 1, nn[1], vs);
+            if (nf[1] && nslot > 1) gather_group<Lay, Src>(A, L, N, 1, nn[1], vs);
         };
-        if (!cur_fits) {
-            group_overflow<Src>(A, L, C);
+        if (pair) {
+            // ---- two groups of one relation, independently: a group that
+            // does not fit or fails is queued for the skew path on its own
+            bool clamped = false;
+            bool ok = cf[0] && sort_group<Lay, PAIR>(A, L, C, P, 0, cn[0], co[0], vr, clamped,
+                                               gather_next_r);
+            if (!cf[0]) gather_next_r();
+            if (!ok) {
+                __syncthreads();
+                group_overflow<Src, PAIR>(A, L, C, 0);
+            }
+            ok = cf[1] && sort_group<Lay, PAIR>(A, L, C, P, 1, cn[1], co[1], vs, clamped,
+                                          gather_next_s);
+            if (!cf[1]) gather_next_s();
+            if (!ok) {
+                __syncthreads();
+                group_overflow<Src, PAIR>(A, L, C, 1);
+            }
+        } else if (!cf[0]) {
+            group_overflow<Src, PAIR>(A, L, C);
             gather_next_r();
             gather_next_s();
         } else {
             bool clamped = false;
-            bool ok = sort_group<Lay>(A, L, C, P, 0, cn[0], co[0], vr, clamped, gather_next_r);
+            bool ok = sort_group<Lay, PAIR>(A, L, C, P, 0, cn[0], co[0], vr, clamped, gather_next_r);
             bool s_issued = false;
             if (ok && nrel > 1) {
-                ok = sort_group<Lay>(A, L, C, P, 1, cn[1], co[1], vs, clamped, gather_next_s);
+                ok = sort_group<Lay, PAIR>(A, L, C, P, 1, cn[1], co[1], vs, clamped, gather_next_s);
                 s_issued = true;
             }
             if (!ok) {
                 __syncthreads();
-                group_overflow<Src>(A, L, C);
+                group_overflow<Src, PAIR>(A, L, C);
                 if (!s_issued) gather_next_s();
             } else if (nrel == 2) {
                 // ---- merge-join count of the two groups
@@ -808,10 +886,10 @@ __device__ __forceinline__ void group_loop(const GroupArgs& A, GroupLDS<typename
                     const Tup* Rs = A.out[0] + C.ost[0] + co[0];
                     const uint32_t nR = cn[0], nS = cn[1];
                     for (uint32_t i = tid; i < nS; i += GS_THREADS) {
-                        const int64_t k = tup_key(Lay::unpack(P, L.B[i], C.b));
-                        if (i > 0 && tup_key(Lay::unpack(P, L.B[i - 1], C.b)) == k) continue;
+                        const int64_t k = tup_key(Lay::unpack(P, L.B[i], C.b[0]));
+                        if (i > 0 && tup_key(Lay::unpack(P, L.B[i - 1], C.b[0])) == k) continue;
                         uint32_t e = i + 1;
-                        while (e < nS && tup_key(Lay::unpack(P, L.B[e], C.b)) == k) e++;
+                        while (e < nS && tup_key(Lay::unpack(P, L.B[e], C.b[0])) == k) e++;
                         uint32_t lo = 0, hi = nR;
                         while (lo < hi) {
                             const uint32_t m = (lo + hi) >> 1;
@@ -835,7 +913,8 @@ __device__ __forceinline__ void group_loop(const GroupArgs& A, GroupLDS<typename
         cn[1] = nn[1];
         co[0] = no[0];
         co[1] = no[1];
-        cur_fits = next_fits;
+        cf[0] = nf[0];
+        cf[1] = nf[1];
     }
 }
 
@@ -847,7 +926,7 @@ __device__ __forceinline__ void group_loop(const GroupArgs& A, GroupLDS<typename
 // the 128-byte line that two neighbouring groups' runs share in a tile is
 // fetched into that L2 once instead of once per XCD.  The grid is a multiple
 // of 8 (launch_groupsort).
-template <class Lay, int TPL>
+template <class Lay, int TPL, bool PAIR>
 __global__ void __launch_bounds__(GS_THREADS, gs_wg_per_cu<typename Lay::W>() * GS_THREADS / 256)
 k_groupsort(GroupArgs A) {
     typedef typename Lay::W W;
@@ -866,7 +945,7 @@ k_groupsort(GroupArgs A) {
 #endif
     unsigned long long matches = 0;
     if (cnt == 0) return;
-    group_loop<Lay, TPL, SrcPlain>(A, L, g0, stride, cnt, matches);
+    group_loop<Lay, TPL, SrcPlain, PAIR>(A, L, g0, stride, cnt, matches);
     if (A.nrel == 2) {
         matches = wave_sum(matches);
         if ((otid() & 63) == 0 && matches) atomicAdd(A.count_dev, matches);
@@ -1588,12 +1667,13 @@ static void set_pass_attrs() {
     SMJ_CHECK(hipFuncSetAttribute((const void*)k_tilepass<Lay>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     // several workgroups per CU (launch bounds): ask for what one needs
-    SMJ_CHECK(hipFuncSetAttribute((const void*)k_groupsort<Lay, 2>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)sizeof(GroupLDS<typename Lay::W>)));
-    SMJ_CHECK(hipFuncSetAttribute((const void*)k_groupsort<Lay, 4>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)sizeof(GroupLDS<typename Lay::W>)));
+    const void* gs[4] = {(const void*)k_groupsort<Lay, 2, false>,
+                         (const void*)k_groupsort<Lay, 4, false>,
+                         (const void*)k_groupsort<Lay, 2, true>,
+                         (const void*)k_groupsort<Lay, 4, true>};
+    for (const void* f : gs)
+        SMJ_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)sizeof(GroupLDS<typename Lay::W>)));
     done = true;
 }
 
@@ -1619,12 +1699,18 @@ static uint32_t groupsort_grid(uint32_t ngroups, uint32_t maxwg, uint32_t& per) 
 
 template <class Lay>
 static void launch_groupsort(int tpl, uint32_t nwg, hipStream_t st, const GroupArgs& G) {
-    if (tpl == 4)
-        hipLaunchKernelGGL((k_groupsort<Lay, 4>), dim3(nwg), dim3(GS_THREADS),
-                           sizeof(GroupLDS<typename Lay::W>), st, G);
-    else
-        hipLaunchKernelGGL((k_groupsort<Lay, 2>), dim3(nwg), dim3(GS_THREADS),
-                           sizeof(GroupLDS<typename Lay::W>), st, G);
+    const size_t lds = sizeof(GroupLDS<typename Lay::W>);
+    if (G.pair) {
+        if (tpl == 4)
+            hipLaunchKernelGGL((k_groupsort<Lay, 4, true>), dim3(nwg), dim3(GS_THREADS), lds, st, G);
+        else
+            hipLaunchKernelGGL((k_groupsort<Lay, 2, true>), dim3(nwg), dim3(GS_THREADS), lds, st, G);
+    } else {
+        if (tpl == 4)
+            hipLaunchKernelGGL((k_groupsort<Lay, 4, false>), dim3(nwg), dim3(GS_THREADS), lds, st, G);
+        else
+            hipLaunchKernelGGL((k_groupsort<Lay, 2, false>), dim3(nwg), dim3(GS_THREADS), lds, st, G);
+    }
 }
 
 // Bucket pass without a host synchronisation before the kernels (sampled
@@ -1706,6 +1792,7 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
     G.pack_bad = a.pack_bad;
     G.d3_fast = a.digit_fast && Lay::fast_ok(T.plan, T.plan.s3, T.plan.D3);
     G.nrel = nrel;
+    G.pair = SMJ_GS_PAIR && nrel == 1;
     G.plan = *a.host_plan;
     G.count_dev = a.count_dev;
     G.nb2 = nb2;
@@ -1749,7 +1836,7 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
         if (a.pack_bad)
             SMJ_CHECK(hipMemcpyAsync(h + 1, a.pack_bad, 4, hipMemcpyDeviceToHost, st));
     }
-    SMJ_CHECK(hipStreamSynchronize(st));
+    ws->wait_stream(st);
     if (a.status_out) {
         a.status_out[0] = h[0];
         a.status_out[1] = h[1];
@@ -1890,6 +1977,7 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
     G.pack_bad = nullptr;
     G.d3_fast = a.digit_fast && LayTup::fast_ok(*hplan, hplan->s3, hplan->D3);
     G.nrel = nrel;
+    G.pair = SMJ_GS_PAIR && nrel == 1;
     G.plan = *hplan;
     G.count_dev = a.count_dev;
     G.nb2 = nb2;
@@ -1932,7 +2020,7 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
     // ---- overflow path (synchronises once)
     uint32_t* h_novf = (uint32_t*)ws->host_pinned("bs_h_novf", 4);
     SMJ_CHECK(hipMemcpyAsync(h_novf, novf, 4, hipMemcpyDeviceToHost, st));
-    SMJ_CHECK(hipStreamSynchronize(st));
+    ws->wait_stream(st);
     const uint32_t no = *h_novf;
     if (no == 0) return true;
     if (no > ovf_cap) {

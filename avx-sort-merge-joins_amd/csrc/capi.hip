@@ -1794,6 +1794,10 @@ void smj_trace_enable(smj_workspace* wsp, int on) {
 
 void smj_trace_reset(smj_workspace* wsp) { ((Workspace*)wsp)->trace_n = 0; }
 
+void smj_trace_only(smj_workspace* wsp, const char* name) {
+    ((Workspace*)wsp)->trace_only = name ? name : "";
+}
+
 // Aggregate the traced kernels by name: returns the number of names written;
 // names are '\n'-separated in `names` (capacity `cap` bytes).
 int smj_trace_read(smj_workspace* wsp, char* names, int cap, float* ms_sum,

@@ -765,7 +765,7 @@ static bool multiway_merge_buckets(Workspace* ws, const Tup* const* runs, const 
                       D, mm, off, dflag, out);
     }
     SMJ_CHECK(hipGetLastError());
-    SMJ_CHECK(hipStreamSynchronize(st));
+    ws->wait_stream(st);
     return hflag[0] == 0 && hflag[1] == 0;
 }
 

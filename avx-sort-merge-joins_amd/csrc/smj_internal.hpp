@@ -58,6 +58,9 @@ struct PlanDigit1 {
 
 // Grow-only named device scratch.  Reallocation frees the old buffer with
 // hipFree (which synchronises), so it only happens on warm-up calls.
+#ifndef SMJ_SPIN_WAIT
+#define SMJ_SPIN_WAIT 1  // Workspace::wait_stream polls an event (0: a lab build's stream sync)
+#endif
 struct Workspace {
     std::map<std::string, std::pair<void*, size_t>> bufs;
     std::map<std::string, std::pair<void*, size_t>> pinned;
@@ -125,6 +128,23 @@ struct Workspace {
         SMJ_CHECK(hipEventRecord(s.ev, st));
         s.used = true;
     }
+    // The host's wait for a stream (the per-call synchronisation that reads
+    // the status flags): an event behind the stream's work, polled with
+    // hipEventQuery (busy wait) instead of hipStreamSynchronize's blocking
+    // wait, which wakes the thread several microseconds after the work ends.
+    hipEvent_t wait_ev = nullptr;
+    void wait_stream(hipStream_t st) {
+#if SMJ_SPIN_WAIT
+        if (!wait_ev) SMJ_CHECK(hipEventCreateWithFlags(&wait_ev, hipEventDisableTiming));
+        SMJ_CHECK(hipEventRecord(wait_ev, st));
+        hipError_t e;
+        while ((e = hipEventQuery(wait_ev)) == hipErrorNotReady) {
+        }
+        SMJ_CHECK(e);
+#else
+        SMJ_CHECK(hipStreamSynchronize(st));
+#endif
+    }
     void events() {
         if (!ev_init) {
             for (auto& e : ev) SMJ_CHECK(hipEventCreate(&e));
@@ -139,10 +159,14 @@ struct Workspace {
         hipEvent_t a, b;
     };
     bool trace_on = false;
+    std::string trace_only;  // non-empty: trace this kernel name alone
     std::vector<TraceRec> trace;
     size_t trace_n = 0;
+    bool traced(const char* name) const {
+        return trace_on && (trace_only.empty() || trace_only == name);
+    }
     int trace_begin(const char* name, hipStream_t st) {
-        if (!trace_on) return -1;
+        if (!traced(name)) return -1;
         if (trace_n == trace.size()) {
             TraceRec r;
             SMJ_CHECK(hipEventCreate(&r.a));
@@ -159,7 +183,7 @@ struct Workspace {
     // a trace record whose events the runtime stamps at the kernel's own start
     // and end (hipExtLaunchKernelGGL): no event-record gap around short kernels
     bool trace_ext(const char* name, hipEvent_t* a, hipEvent_t* b) {
-        if (!trace_on) return false;
+        if (!traced(name)) return false;
         if (trace_n == trace.size()) {
             TraceRec r;
             SMJ_CHECK(hipEventCreate(&r.a));

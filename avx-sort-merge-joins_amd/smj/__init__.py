@@ -57,7 +57,7 @@ DEVICE_SYMBOLS = [
     "smj_dev_merge2", "smj_dev_multiway_merge_host", "smj_dev_merge_join_count",
     "smj_dev_join", "smj_join_phase_ms", "smj_dev_gen_pk", "smj_dev_gen_fk",
     "smj_dev_gen_zipf", "smj_dev_synchronize", "smj_dev_partition_range",
-    "smj_trace_enable", "smj_trace_reset", "smj_trace_read", "smj_dev_join_segmented",
+    "smj_trace_enable", "smj_trace_reset", "smj_trace_only", "smj_trace_read", "smj_dev_join_segmented",
     "smj_dev_partition_range_packed", "smj_dev_materialize", "smj_selfcheck_lds_order",
     "smj_set_materialize", "smj_dev_join_segmented_tables", "smj_dev_partition_range_sampled",
     "smj_sampled_capacity", "smj_sampled_shards", "smj_context_workspace",
@@ -192,6 +192,7 @@ class Library:
                                      _P]),
             "smj_trace_enable": (None, [_P, C.c_int]),
             "smj_trace_reset": (None, [_P]),
+            "smj_trace_only": (None, [_P, C.c_char_p]),
             "smj_trace_read": (C.c_int, [_P, C.c_char_p, C.c_int, _P, _P, C.c_int]),
         }
         for name, (res, args) in sig.items():
@@ -518,8 +519,11 @@ class Library:
         """Violations of lane-ordered LDS atomic returns (0 expected)."""
         return int(self.lib.smj_selfcheck_lds_order(self.ws, self.stream_ptr()))
 
-    def trace(self, on: bool):
+    def trace(self, on: bool, only: str | None = None):
+        """Start (reset) or stop the per-kernel event trace; `only` names the
+        one kernel to trace."""
         self.lib.smj_trace_enable(self.ws, int(on))
+        self.lib.smj_trace_only(self.ws, only.encode() if only else None)
         self.lib.smj_trace_reset(self.ws)
 
     def trace_read(self):

@@ -66,6 +66,9 @@ def parse():
     p.add_argument("--cpu-n", type=int, default=128_000_000,
                    help="tuples per relation of the bounded CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-trace", action="store_true",
+                   help="lab: no per-kernel HIP events in the timed loop (measures what "
+                        "the trace costs; the line then has no roofline)")
     p.add_argument("--check", action="store_true",
                    help="also verify sortedness/multiset of the sorted outputs")
     p.add_argument("--exchange-path", action="store_true",
@@ -307,7 +310,7 @@ def main():
         if exchange:
             dj.stats_reset()
 
-    elapsed, kern = timed_loop(a, tracer, dist, step, reset)
+    elapsed, kern, brk = timed_loop(a, tracer, dist, step, reset)
     if a.api and not exchange:
         count.fill_(api_count[0])
 
@@ -380,7 +383,8 @@ def main():
             "S_tuples_per_s_M": round(total / (elapsed / a.steps) / 1e6, 2),
             "pipeline_alg_GBps_5w": round(pipeline_gbs, 1),
             "pipeline_frac": round(pipeline_gbs / HBM_PEAK_GBS, 4),
-            "kernels_ms_per_step": {k: round(v[0] / a.steps, 4) for k, v in kern.items()},
+            # untimed steps, every kernel traced (timed_loop)
+            "kernels_ms_per_step": {k: round(v, 4) for k, v in brk.items()},
             "device": lib.lib.smj_device_name().decode(),
             "exchange": xchg,
         },
@@ -397,8 +401,9 @@ class _WsTracer:
     def __init__(self, lib, ws):
         self.lib, self.ws = lib, ws
 
-    def trace(self, on):
+    def trace(self, on, only=None):
         self.lib.lib.smj_trace_enable(self.ws, int(on))
+        self.lib.lib.smj_trace_only(self.ws, only.encode() if only else None)
         self.lib.lib.smj_trace_reset(self.ws)
 
     def trace_read(self):
@@ -410,16 +415,28 @@ class _WsTracer:
 
 
 def timed_loop(a, lib, dist, step, reset=None):
-    """W untimed warm-up steps, then exactly K steps between a barrier +
-    synchronize on both sides; returns (max-over-ranks seconds, kernel trace)."""
+    """W untimed warm-up steps and a few untimed steps with every kernel
+    traced (the per-kernel breakdown, which also names the dominant kernel),
+    then exactly K steps between a barrier + synchronize on both sides with
+    only the dominant kernel traced (one HIP event pair per launch: the other
+    kernels' events would perturb the step).  Returns (max-over-ranks
+    seconds, {dominant kernel: (ms, launches)} over the timed steps,
+    {kernel: ms per step} of the untimed breakdown)."""
     for _ in range(a.warmup):
         step()
+    nb = min(a.steps, 3)
+    lib.trace(not a.no_trace)
+    for _ in range(nb):
+        step()
     torch.cuda.synchronize()
+    brk = {k: v[0] / nb for k, v in lib.trace_read().items()}
+    dom = max(brk, key=brk.get) if brk else None
+    lib.trace(False)
     if dist:
         dist.barrier()
     if reset:
         reset()
-    lib.trace(True)
+    lib.trace(dom is not None, only=dom)
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
@@ -427,13 +444,13 @@ def timed_loop(a, lib, dist, step, reset=None):
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern = lib.trace_read()
+    kern = lib.trace_read() if dom else {}
     lib.trace(False)
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    return elapsed, kern
+    return elapsed, kern, brk
 
 
 def dominant_roofline(kern, bytes_of, cfg_key):
@@ -493,12 +510,12 @@ def run_exchange(a, json_out, N, rank, local):
         dj._rows(xb, cap, cs, sl, rl, gmax).wait()
 
     class _NoTrace:
-        def trace(self, on):
+        def trace(self, on, only=None):
             pass
 
         def trace_read(self):
             return {}
-    elapsed, _ = timed_loop(a, _NoTrace(), dist if N > 1 else None, step)
+    elapsed, _, _ = timed_loop(a, _NoTrace(), dist if N > 1 else None, step)
     t = elapsed / a.steps
     sent = row * (sum(sl) - sl[rank])  # this rank's bytes to other ranks per step
     recv = row * (sum(rl) - rl[rank])
@@ -583,7 +600,7 @@ def run_op(a, lib, json_out, dist, N, rank):
         def step():
             lib.dev_partition(R, out, a.bits, a.shift, True, hist, off)
     torch.cuda.synchronize()
-    elapsed, kern = timed_loop(a, lib, dist, step)
+    elapsed, kern, brk = timed_loop(a, lib, dist, step)
     if a.op in ("sort", "merge"):
         keys = out[:, 1]
         ok = bool((keys[1:] >= keys[:-1]).all().item()) if n > 1 else True
@@ -634,7 +651,8 @@ def run_op(a, lib, json_out, dist, N, rank):
         "detail": {
             "alg_GBps_2Nw": round(alg / (elapsed / a.steps) / 1e9, 1),
             "alg_frac_2Nw": round(alg / (elapsed / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
-            "kernels_ms_per_step": {k: round(v[0] / a.steps, 4) for k, v in kern.items()},
+            # untimed steps, every kernel traced (timed_loop)
+            "kernels_ms_per_step": {k: round(v, 4) for k, v in brk.items()},
             "device": lib.lib.smj_device_name().decode(),
         },
     }

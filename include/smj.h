@@ -584,6 +584,9 @@ smj_workspace * smj_context_workspace(void);
 /* Per-kernel HIP-event trace of the join pipeline (bench.py roofline). */
 void smj_trace_enable(smj_workspace * ws, int on);
 void smj_trace_reset(smj_workspace * ws);
+/* Trace only the kernel `name` (NULL or "": every kernel): one event pair per
+ * step instead of one per kernel in bench.py's timed loop. */
+void smj_trace_only(smj_workspace * ws, const char * name);
 int smj_trace_read(smj_workspace * ws, char * names, int cap, float * ms_sum,
                    int * launches, int max);
 
