@@ -979,6 +979,9 @@ constexpr int SK_THREADS = SMJ_SK_THREADS;
 constexpr int SK_ITEMS = 8;
 constexpr int SK_CHUNK = SK_THREADS * SK_ITEMS;
 constexpr uint32_t kSkewSmall = 16384;  // tuples per relation, one workgroup
+#ifndef SMJ_SKEW_ITEM
+#define SMJ_SKEW_ITEM 8192  // tuples per work item of a large skew group (2048 measured slower)
+#endif
 constexpr int SK_TM = 256;              // tile runs in LDS tables (small groups)
 
 struct SkewArgs {
@@ -1003,25 +1006,24 @@ __device__ __forceinline__ const typename Lay::W* skew_run(const GroupArgs& G, i
     return static_cast<const typename Lay::W*>(G.tmp[r]) + tt.off[t0 + t] + lo;
 }
 
+constexpr uint32_t SK_WIN = kSkewSmall / 64;  // 64-position windows of a small group
+static_assert(SK_WIN == SK_THREADS, "one window per thread when the run tables are built");
+
 struct SkewSmallLDS {
     uint32_t h[2][GS_NB3];
     unsigned long long first[GS_NB3];  // pass 2: an element seen per digit
-    uint32_t runoff[2][SK_TM + 1];
-    uint64_t runsrc[2][SK_TM];
+    // one relation's non-empty tile runs in position order (the group pass's
+    // tables, build_tables; rebuilt per relation and pass, so that four
+    // workgroups fit a CU): group position j of run k is tmp[j + base[k]]
+    // (mod 2^64); window w: bit i of m = a run starts at 64 w + i, wk = runs
+    // starting before the window, minus one
+    uint64_t base[SK_TM];
+    struct Win {
+        unsigned long long m;
+        uint32_t wk, pad;
+    } win[SK_WIN];
     unsigned long long scr[SK_THREADS / 64 + 1];
 };
-
-// element j of relation r's group (run tables in LDS) -> its source tuple
-template <class W>
-__device__ __forceinline__ const W* skew_elem(const SkewSmallLDS& L, int r, const W* tmp,
-                                              uint32_t nt, uint32_t j) {
-    uint32_t lo = 0, hi = nt;  // last run with runoff <= j
-    while (hi - lo > 1) {
-        const uint32_t m = (lo + hi) >> 1;
-        if (L.runoff[r][m] <= j) lo = m; else hi = m;
-    }
-    return tmp + L.runsrc[r][lo] + (j - L.runoff[r][lo]);
-}
 
 // apply f(x) to every tuple of relation r's group, SK_ITEMS loads in flight
 // per thread (groups of more than SK_TM runs: run by run)
@@ -1031,13 +1033,27 @@ __device__ __forceinline__ void skew_for_each(const GroupArgs& G, const SkewSmal
                                               F&& f) {
     typedef typename Lay::W W;
     if (nt <= SK_TM) {
+        const W* tmp = static_cast<const W*>(G.tmp[r]);
+        const uint32_t lane = lane_id();
+        const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         for (uint32_t c = 0; c < n; c += SK_CHUNK) {
             W v[SK_ITEMS];
 #pragma unroll
             for (int k = 0; k < SK_ITEMS; k++) {
-                // unconditional (clamped) loads: a conditional one waits alone
-                const uint32_t j = min(c + k * SK_THREADS + threadIdx.x, n - 1);
-                v[k] = *skew_elem(L, r, static_cast<const W*>(G.tmp[r]), nt, j);
+                // a wave's 64 positions are one window (broadcast read): the
+                // run of the lane's position is the window's earlier runs plus
+                // the starts below the lane (mbcnt) and at it; positions past
+                // the end re-read position 0 (unconditional loads: a
+                // conditional one waits alone)
+                const uint32_t w = (c + k * SK_THREADS) / 64 + wid;  // uniform
+                const uint32_t j = w * 64 + lane;
+                const bool ok = j < n;
+                const auto win = L.win[ok ? w : 0u];
+                const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+                    (uint32_t)(win.m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)win.m, 0u));
+                const uint32_t at = (uint32_t)(win.m >> lane) & 1u;
+                const uint32_t q = ok ? win.wk + below + at : 0u;
+                v[k] = tmp[(uint64_t)(ok ? j : 0u) + L.base[q]];
             }
 #pragma unroll
             for (int k = 0; k < SK_ITEMS; k++) f(v[k], c + k * SK_THREADS + threadIdx.x < n);
@@ -1085,35 +1101,51 @@ k_skew_small(SkewArgs K) {
     const uint32_t tid = threadIdx.x;
     uint32_t t0[2] = {0, 0}, nt[2] = {0, 0};
     for (uint32_t i = tid; i < 2 * GS_NB3; i += SK_THREADS) (&L.h[0][0])[i] = 0;
-    // ---- run tables
+    __syncthreads();
     for (int r = 0; r < G.nrel; r++) {
         t0[r] = G.tt[r].btile0[e.bucket];
         nt[r] = G.tt[r].btile0[e.bucket + 1] - t0[r];
-        if (nt[r] > SK_TM) continue;
-        unsigned long long acc = 0;
+    }
+    // ---- run tables of relation r: one scan gives every tile run its start
+    // in the group (low half) and its index among the non-empty runs (high
+    // half).  Uniform control flow (barriers inside).
+    auto tables = [&](int r) {
+        if (nt[r] > SK_TM) return;  // run by run (skew_for_each)
+        __syncthreads();            // the previous tables are no longer read
+        L.win[tid].m = 0ull;        // SK_WIN == SK_THREADS
+        uint32_t len = 0;
         uint64_t src = 0;
         if (tid < nt[r]) {
             const TileTable& tt = G.tt[r];
             const uint16_t* pf = tt.prefT + (uint64_t)e.d2 * tt.tstride + t0[r] + tid;
-            acc = (uint32_t)(pf[tt.tstride] - pf[0]);
+            len = (uint32_t)(pf[tt.tstride] - pf[0]);
             src = tt.off[t0[r] + tid] + pf[0];
         }
+        const unsigned long long acc = ((unsigned long long)(len ? 1u : 0u) << 32) | len;
         unsigned long long tot;
-        const unsigned long long ex = block_scan64(acc, L.scr, &tot);
-        if (tid < nt[r]) {
-            L.runoff[r][tid] = (uint32_t)ex;
-            L.runsrc[r][tid] = src;
+        const unsigned long long ex = block_scan64(acc, L.scr, &tot);  // barriers: m is zero
+        const uint32_t st = (uint32_t)ex, k = (uint32_t)(ex >> 32);
+        if (len) {
+            L.base[k] = src - st;
+            atomicOr(&L.win[st >> 6].m, 1ull << (st & 63));
         }
-        if (tid == 0) L.runoff[r][nt[r]] = (uint32_t)tot;
-    }
-    __syncthreads();
+        __syncthreads();
+        // window prefix counts (one window per thread)
+        const uint32_t cw = (uint32_t)__popcll(L.win[tid].m);
+        unsigned long long wt;
+        const uint32_t wex = (uint32_t)block_scan64(cw, L.scr, &wt);  // ends with a barrier
+        L.win[tid].wk = wex - 1u;
+        __syncthreads();
+    };
     // ---- pass 1: d3 histograms
     bool clamped = false;
-    for (int r = 0; r < G.nrel; r++)
+    for (int r = 0; r < G.nrel; r++) {
+        tables(r);
         skew_for_each<Lay>(G, L, r, e.d2, t0[r], nt[r], e.nr[r], [&](const W& x, bool ok) {
             clamped |= ok && Lay::clamped(P, x);
             if (ok) atomicAdd(&L.h[r][plan_d3(P, Lay::rel(P, x, e.bucket), d12)], 1u);
         });
+    }
     const bool exact = P.s3 == 0 && !__syncthreads_or(clamped);
     if (!exact) {
         // inexact digits: copy the runs unsorted to the group's place
@@ -1160,6 +1192,7 @@ k_skew_small(SkewArgs K) {
         }
         __syncthreads();
         for (uint32_t d = tid; d < GS_NB3; d += SK_THREADS) L.first[d] = ~0ull;
+        tables(r);  // (barriers inside; without tables one barrier)
         __syncthreads();
         // ---- pass 2: place; and note whether some key holds differing
         // elements (the first element seen per digit is kept: ~0 is the
@@ -1382,8 +1415,10 @@ static void skew_path(Workspace* ws, const GroupArgs& G, OvfEntry* ovf, uint32_t
         large.push_back(i);
         lslot.push_back(sl);
         for (int r = 0; r < nrel; r++) {
-            // about 8K tuples per item (runs are strided over the items)
-            const uint32_t ts = std::min<uint32_t>(std::max<uint32_t>(he[i].nr[r] / 8192, 1), 256);
+            // about SMJ_SKEW_ITEM tuples per item (runs are strided over the
+            // items; an item past the bucket's runs exits)
+            const uint32_t ts =
+                std::min<uint32_t>(std::max<uint32_t>(he[i].nr[r] / SMJ_SKEW_ITEM, 1), 256);
             for (uint32_t s = 0; s < ts; s++)
                 items.push_back(make_uint4(i, sl, ((uint32_t)r << 16) | s, ts));
         }

@@ -144,6 +144,22 @@ def test_sort_zipf_skew(libs, oracles, width):
     assert np.array_equal(got, orc.sort(t))
 
 
+@pytest.mark.parametrize("copies", [40, 100, 700])
+def test_sort_long_equal_key_runs(libs, oracles, width, copies):
+    """One relation, groups that fit in LDS but hold equal-key runs longer than
+    the group pass fixes in place, payloads shuffled: the slot of the pair
+    mode (two groups per iteration) that fails is queued for the skew path on
+    its own while the other slot's group is written."""
+    orc, lib = oracles[width], libs[width]
+    rng = np.random.default_rng(copies)
+    n = (1 << 20) + 37
+    t = rand_tuples(width, n, 2)
+    t["key"] = 1 + (rng.permutation(n) // copies)
+    t["payload"] = rng.integers(0, 1 << 30, n)
+    got = lib.avxsort_tuples(t)
+    assert np.array_equal(got, orc.sort(t))
+
+
 def non_nan_words(rng, n):
     """int64 patterns that are neither NaN nor -0 as IEEE doubles."""
     v = rng.integers(-(1 << 63), (1 << 63) - 1, 2 * n, dtype=np.int64)
