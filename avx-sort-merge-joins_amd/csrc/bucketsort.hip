@@ -712,12 +712,15 @@ __device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS<typename
         ex += c[2 * q + 1];
     }
     __syncthreads();
-    // ---- place (lanes past the end drop their element in the dump slot)
+    // ---- place (lanes past the end drop their element in the dump slot).
+    // Every digit at most once (no equal-digit run: a PK relation's groups):
+    // the bin's start is the element's place, read without an atomic.
 #pragma unroll
     for (int k = 0; k < GS_ITEMS; k++) {
         const bool valid = k * GS_THREADS + tid < nr;
         const uint32_t sh = (dg[k] & 1) * 16;
-        const uint32_t old = atomicAdd(&L.cur[dg[k] >> 1], valid ? 1u << sh : 0u);
+        const uint32_t old = dup ? atomicAdd(&L.cur[dg[k] >> 1], valid ? 1u << sh : 0u)
+                                 : L.cur[valid ? dg[k] >> 1 : 0u];
         L.B[valid ? (old >> sh) & 0xffffu : GS_CAP] = v[k];
     }
     after_place();
