@@ -424,7 +424,7 @@ def timed_loop(a, lib, dist, step, reset=None):
     {kernel: ms per step} of the untimed breakdown)."""
     for _ in range(a.warmup):
         step()
-    nb = min(a.steps, 3)
+    nb = max(1, min(a.steps, 3))
     lib.trace(not a.no_trace)
     for _ in range(nb):
         step()
