@@ -1,0 +1,83 @@
+"""bench.py's timed loop on CPU (no GPU calls): warm-up, an untimed breakdown
+with every kernel traced, then exactly K timed steps with only the dominant
+kernel traced, and the roofline taken from that kernel."""
+import types
+
+import pytest
+
+import bench
+
+
+class FakeTraceLib:
+    """Stands in for smj.Library's trace_* (the kernel times of one step are
+    fixed: two scatter launches of 0.6 ms, one group pass of 1.3 ms)."""
+
+    STEP = {"k_scatter": (1.2, 2), "k_groupsort": (1.3, 1), "k_sample": (0.02, 1)}
+
+    def __init__(self):
+        self.on, self.only, self.steps, self.calls = False, None, 0, []
+
+    def trace(self, on, only=None):
+        self.on, self.only, self.steps = on, only, 0
+        self.calls.append((on, only))
+
+    def step(self):
+        if self.on:
+            self.steps += 1
+
+    def trace_read(self):
+        # like smj_trace_read: nothing recorded -> no names
+        if not self.steps:
+            return {}
+        out = {}
+        for k, (ms, n) in self.STEP.items():
+            if self.only in (None, k):
+                out[k] = (ms * self.steps, n * self.steps)
+        return out
+
+
+@pytest.fixture
+def no_cuda_sync(monkeypatch):
+    monkeypatch.setattr(bench.torch.cuda, "synchronize", lambda *a, **k: None)
+
+
+def run(lib, steps=7, warmup=2, no_trace=False):
+    a = types.SimpleNamespace(steps=steps, warmup=warmup, no_trace=no_trace)
+    n = [0]
+
+    def step():
+        n[0] += 1
+        lib.step()
+
+    elapsed, kern, brk = bench.timed_loop(a, lib, None, step)
+    return n[0], elapsed, kern, brk
+
+
+def test_dominant_kernel_alone_in_timed_steps(no_cuda_sync):
+    lib = FakeTraceLib()
+    n, elapsed, kern, brk = run(lib)
+    assert n == 2 + 3 + 7  # warm-up, untimed breakdown, timed
+    assert elapsed >= 0
+    assert brk == pytest.approx({k: v[0] for k, v in FakeTraceLib.STEP.items()})
+    # the timed steps trace the kernel with the largest summed time only
+    assert (True, "k_groupsort") in lib.calls
+    assert kern == {"k_groupsort": pytest.approx((1.3 * 7, 7))}
+    assert lib.calls[-1] == (False, None)
+
+
+def test_roofline_from_the_timed_kernel(no_cuda_sync):
+    lib = FakeTraceLib()
+    _, _, kern, _ = run(lib)
+    roof = bench.dominant_roofline(kern, lambda name: 8.192e9 if name == "k_groupsort" else None,
+                                   "none")
+    assert roof["kernel"] == "k_groupsort"
+    assert roof["avg_launch_ms"] == pytest.approx(1.3)
+    assert roof["frac"] == pytest.approx(8.192e9 / 1.3e-3 / 1e9 / bench.HBM_PEAK_GBS, rel=1e-3)
+
+
+def test_no_trace_lab_switch(no_cuda_sync):
+    lib = FakeTraceLib()
+    n, _, kern, brk = run(lib, steps=1, warmup=0, no_trace=True)
+    assert n == 1 + 1  # one untimed step (at least one), one timed
+    assert kern == {} and brk == {}
+    assert bench.dominant_roofline(kern, lambda name: 1.0, "none") is None
