@@ -1738,6 +1738,15 @@ static uint32_t groupsort_grid(uint32_t ngroups, uint32_t maxwg, uint32_t& per) 
 template <class Lay>
 static void launch_groupsort(int tpl, uint32_t nwg, hipStream_t st, const GroupArgs& G) {
     const size_t lds = sizeof(GroupLDS<typename Lay::W>);
+#if SMJ_GS_XCD
+    // k_groupsort's XCD-aware order splits the groups into 8 ranges of
+    // gridDim.x / 8 blocks each: any other grid would sort some groups twice
+    // (counting their matches twice) and leave others unsorted
+    if (nwg % 8 != 0) {
+        fprintf(stderr, "[ERROR] smj: group pass grid %u is not a multiple of 8\n", nwg);
+        abort();
+    }
+#endif
     if (G.pair) {
         if (tpl == 4)
             hipLaunchKernelGGL((k_groupsort<Lay, 4, true>), dim3(nwg), dim3(GS_THREADS), lds, st, G);

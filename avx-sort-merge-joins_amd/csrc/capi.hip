@@ -33,6 +33,20 @@ k_join_begin(smj::RangePlan* p, smj::RangePlan v, int set_plan, unsigned long lo
     for (uint32_t i = threadIdx.x; i < nzero; i += 256) zero[i] = 0;
 }
 
+// is_sorted_helper's scan (joincommon.c:397-500) in parallel: the first
+// position whose key is below its predecessor's (the predecessor of item 0 is
+// the key 0 the reference starts from) and the first whose key equals it
+__global__ void __launch_bounds__(256)
+k_sorted_scan(const smj::Tup* __restrict__ t, uint64_t n, unsigned long long* first) {
+    const uint64_t G = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += G) {
+        const int64_t k = smj::tup_key(smj::ld_g(t + i));
+        const int64_t prev = i ? smj::tup_key(smj::ld_g(t + i - 1)) : 0;
+        if (k < prev) atomicMin(&first[0], (unsigned long long)i);
+        else if (k == prev) atomicMin(&first[1], (unsigned long long)i);
+    }
+}
+
 namespace smj {
 void gen_pk_nopayload(Tup* out, uint64_t n, uint64_t first, uint64_t total,
                       uint64_t seed, hipStream_t st);
@@ -525,6 +539,52 @@ void histogram_memcpy_bench(relation_t** partitions, relation_t* input,
     sync();
 }
 
+// partition.c:93-149 (declared partition.h:38-43): the naive stable radix
+// cluster on bits [R, R + D) of key - 1 (partition.c:29), partitions back to
+// back, no padding.  The reference INCREMENTS the caller's int32 hist
+// (:111-113) and places partition i at the prefix sum of that hist (:116-122),
+// so counts already in hist shift the starts; this keeps that: a zero hist
+// (every reference caller) scatters straight into outRel, a non-zero one
+// scatters into scratch and moves each partition to its shifted start.
+void radix_cluster(relation_t* outRel, relation_t* inRel, int32_t* hist, int R, int D) {
+    Ctx& c = ctx();
+    const uint64_t n = inRel->num_tuples;
+    const uint32_t fan = 1u << D;
+    const uint32_t mask = (uint32_t)((((1ull << D) - 1) << R) & 0xffffffffull);
+    DevBuf in = dev_in(inRel->tuples, n, "api_in", true);
+    bool zero = true;
+    for (uint32_t i = 0; i < fan; i++) zero = zero && hist[i] == 0;
+    int64_t* dh = (int64_t*)c.ws.scratch("api_hist", fan * 8);
+    int64_t* doff = (int64_t*)c.ws.scratch("api_off", fan * 8);
+    const Digit32 dig{mask, (uint32_t)R};
+    std::vector<int64_t> hh(fan), ho(fan);
+    if (zero) {
+        DevBuf out = dev_in(outRel->tuples, n, "api_out", false);
+        stable_partition(&c.ws, in.d, n, out.d, dig, (uint32_t)D, 0, dh, doff, c.st);
+        SMJ_CHECK(hipMemcpyAsync(hh.data(), dh, fan * 8, hipMemcpyDeviceToHost, c.st));
+        dev_out(out, n);
+        sync();
+    } else {
+        Tup* tmp = (Tup*)c.ws.scratch("api_rc", (n ? n : 1) * sizeof(Tup));
+        stable_partition(&c.ws, in.d, n, tmp, dig, (uint32_t)D, 0, dh, doff, c.st);
+        SMJ_CHECK(hipMemcpyAsync(hh.data(), dh, fan * 8, hipMemcpyDeviceToHost, c.st));
+        SMJ_CHECK(hipMemcpyAsync(ho.data(), doff, fan * 8, hipMemcpyDeviceToHost, c.st));
+        sync();
+        const bool dev = is_device_ptr(outRel->tuples);
+        uint32_t dst = 0;  // partition.c:116-122, offsets from the incremented hist
+        for (uint32_t i = 0; i < fan; i++) {
+            if (hh[i])
+                SMJ_CHECK(hipMemcpyAsync(outRel->tuples + dst, tmp + ho[i],
+                                         (size_t)hh[i] * sizeof(Tup),
+                                         dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
+                                         c.st));
+            dst += (uint32_t)(hist[i] + (int32_t)hh[i]);
+        }
+        sync();
+    }
+    for (uint32_t i = 0; i < fan; i++) hist[i] += (int32_t)hh[i];
+}
+
 // ---------------------------------------------------------------------------
 // sorting (reference src/avxsort/avxsort.c:212-250, avxsort_multiway.c,
 // src/scalarsort/scalarsort.c)
@@ -1010,6 +1070,58 @@ uint64_t merge_join_interpolation(tuple_t* rtuples, tuple_t* stuples,
     return merge_join(rtuples, stuples, numR, numS, output);
 }
 
+// joincommon.c:397-500 (declared joincommon.h:99-100): 1 when the keys of the
+// `nitems` tuples at `items` never decrease, starting from key 0.  The 8-byte
+// build (no KEY_8B) prints the reference's warning at the first equal key
+// before any decrease and its error line at the first decrease; the KEY_8B
+// build prints nothing.  The scan runs on the device (k_sorted_scan).
+int is_sorted_helper(int64_t* items, uint64_t nitems) {
+    if (nitems == 0) return 1;
+    Ctx& c = ctx();
+    DevBuf t = dev_in(items, nitems, "api_chk", true);
+    unsigned long long* first = (unsigned long long*)c.ws.scratch("api_chk_first", 16);
+    const unsigned long long init[2] = {~0ull, ~0ull};
+    unsigned long long* h = (unsigned long long*)c.ws.host_pinned("api_chk_h", 16);
+    memcpy(h, init, 16);
+    SMJ_CHECK(hipMemcpyAsync(first, h, 16, hipMemcpyHostToDevice, c.st));
+    uint64_t g = (nitems + 255) / 256;
+    if (g > 2048) g = 2048;
+    hipLaunchKernelGGL(k_sorted_scan, dim3((uint32_t)g), dim3(256), 0, c.st, t.d, nitems, first);
+    SMJ_CHECK(hipGetLastError());
+    SMJ_CHECK(hipMemcpyAsync(h, first, 16, hipMemcpyDeviceToHost, c.st));
+    sync();
+    const unsigned long long bad = h[0], eq = h[1];
+#ifndef KEY_8B
+    // the key at position i and its predecessor's (0 before item 0)
+    auto key_at = [&](unsigned long long i) -> int32_t {
+        Tup v;
+        SMJ_CHECK(hipMemcpy(&v, t.d + i, sizeof(Tup), hipMemcpyDeviceToHost));
+        return (int32_t)tup_key(v);
+    };
+    if (eq != ~0ull && eq < bad)
+        printf("[WARN ] Equal items, still ok... item[%d].key=%d is equal to item[%d].key=%d\n",
+               (int)eq, key_at(eq), (int)(eq - 1), key_at(eq));
+    if (bad != ~0ull)
+        printf("[ERROR] item[%d].key=%d is less than item[%d].key=%d\n", (int)bad, key_at(bad),
+               (int)(bad - 1), bad ? key_at(bad - 1) : 0);
+    fflush(stdout);
+#endif
+    return bad == ~0ull ? 1 : 0;
+}
+
+// joincommon.c:503-515 (declared joincommon.h:101-103)
+void check_sorted(int64_t* R, int64_t* S, uint64_t nR, uint64_t nS, int my_tid) {
+    if (is_sorted_helper(R, nR))
+        printf("%d-thread -> R is sorted, size = %d\n", my_tid, (int)nR);
+    else
+        printf("%d-thread -> R is NOT sorted, size = %d\n", my_tid, (int)nR);
+    if (is_sorted_helper(S, nS))
+        printf("%d-thread -> S is sorted, size = %d\n", my_tid, (int)nS);
+    else
+        printf("%d-thread -> S is NOT sorted, size = %d\n", my_tid, (int)nS);
+    fflush(stdout);
+}
+
 // joincommon.c:29-212.  The orchestration of the reference's T join threads,
 // kept for drivers that bring their own join thread (tputbench.c:124-144).
 // The CPU mapping (src/util/cpu_mapping.c) is the driver's: when the driver
@@ -1145,8 +1257,10 @@ result_t* sortmergejoin_initrun(relation_t* relR, relation_t* relS,
     return res;
 }
 
+// mat: the materialisation of this call (1 / 0), or -1 for the process
+// default (smj_set_materialize / SMJ_MATERIALIZE)
 static result_t* join_api(relation_t* relR, relation_t* relS,
-                          joinconfig_t* joincfg, const char* name) {
+                          joinconfig_t* joincfg, const char* name, int mat = -1) {
     if ((joincfg->NTHREADS & (joincfg->NTHREADS - 1)) != 0) {
         fprintf(stdout, "[ERROR] %s sort-merge join runs with a power of 2 "
                         "#threads.\n", name);
@@ -1184,7 +1298,7 @@ static result_t* join_api(relation_t* relR, relation_t* relS,
         (threadresult_t*)calloc(joincfg->NTHREADS > 0 ? joincfg->NTHREADS : 1,
                                 sizeof(threadresult_t));
     res->resultlist[0].nresults = (int64_t)h;
-    if (materialize_on()) {
+    if (mat < 0 ? materialize_on() : mat > 0) {
         chainedtuplebuffer_t* cb = chainedtuplebuffer_init();
         materialize_append(sR, nR, sS, nS, cb);
         res->resultlist[0].results = cb;
@@ -1251,8 +1365,8 @@ void print_timing(uint64_t numtuples, struct timeval* start, struct timeval* end
 //       counts summed.
 // Unlike m-way (one multi-way merge, fused here into the bucket sort) every
 // merge pass reads and writes both relations once more.
-result_t* sortmergejoin_multipass(relation_t* relR, relation_t* relS,
-                                  joinconfig_t* joincfg) {
+static result_t* multipass_api(relation_t* relR, relation_t* relS, joinconfig_t* joincfg,
+                               int mat) {
     if ((joincfg->NTHREADS & (joincfg->NTHREADS - 1)) != 0) {
         fprintf(stdout, "[ERROR] m-pass sort-merge join runs with a power of 2 "
                         "#threads.\n");
@@ -1298,9 +1412,11 @@ result_t* sortmergejoin_multipass(relation_t* relR, relation_t* relS,
             const uint64_t rchunk = t + 1 == T ? nR - (uint64_t)t * (nR / T) : nR / T;
             const int64_t sh = rchunk ? (int64_t)ceil(log2((double)(rchunk * T))) - (int64_t)bits - 1
                                       : 0;
-            const uint32_t shift = sh > 0 ? (uint32_t)sh : 0u;
-            const uint32_t mask = shift + bits <= 32
-                ? (uint32_t)(((1ull << bits) - 1) << shift) : 0xffffffffu;
+            // the reference's uint32_t mask (partition.c:100): the digit bits
+            // above bit 31 drop out, so the digit stays below F for any shift
+            const uint32_t shift = sh > 0 ? (uint32_t)(sh < 63 ? sh : 63) : 0u;
+            const uint32_t mask =
+                shift < 32 ? (uint32_t)((((1ull << bits) - 1) << shift) & 0xffffffffull) : 0u;
             const Digit32 dig{mask, shift};
             stable_partition(&c.ws, rels[q]->d + c0[t], cl[t], part + c0[t], dig, bits, 0,
                              hist + (size_t)t * F, off + (size_t)t * F, c.st);
@@ -1360,7 +1476,7 @@ result_t* sortmergejoin_multipass(relation_t* relR, relation_t* relS,
         res->totalresults += (int64_t)h[t];
         res->resultlist[t].nresults = (int64_t)h[t];
         res->resultlist[t].threadid = t;
-        if (materialize_on()) {
+        if (mat < 0 ? materialize_on() : mat > 0) {
             // the thread's own sorted relations (its partitions), R-major
             chainedtuplebuffer_t* cb = chainedtuplebuffer_init();
             materialize_append(sR + toff[0][t], tlen[0][t], sS + toff[1][t], tlen[1][t], cb);
@@ -1374,6 +1490,24 @@ result_t* sortmergejoin_multipass(relation_t* relR, relation_t* relS,
         fflush(stderr);
     }
     return res;
+}
+
+result_t* sortmergejoin_multipass(relation_t* relR, relation_t* relS,
+                                  joinconfig_t* joincfg) {
+    return multipass_api(relR, relS, joincfg, -1);
+}
+
+result_t* smj_join(relation_t* relR, relation_t* relS, joinconfig_t* joincfg, int algo,
+                   int materialize) {
+    const int mat = materialize < 0 ? -1 : (materialize ? 1 : 0);
+    switch (algo) {
+        case 0: return join_api(relR, relS, joincfg, "m-way", mat);
+        case 1: return multipass_api(relR, relS, joincfg, mat);
+        case 2: return join_api(relR, relS, joincfg, "mpsm", mat);
+        default:
+            fprintf(stderr, "[ERROR] smj_join: unknown algorithm %d\n", algo);
+            return 0;
+    }
 }
 
 // ---------------------------------------------------------------------------

@@ -1,5 +1,8 @@
 // smj_internal.hpp -- host-side internal interfaces between the .hip units.
 #pragma once
+#include <sched.h>
+
+#include <chrono>
 #include <map>
 #include <mutex>
 #include <string>
@@ -137,8 +140,18 @@ struct Workspace {
 #if SMJ_SPIN_WAIT
         if (!wait_ev) SMJ_CHECK(hipEventCreateWithFlags(&wait_ev, hipEventDisableTiming));
         SMJ_CHECK(hipEventRecord(wait_ev, st));
+        // spin for a bounded time (the short waits of a join step end in a
+        // few microseconds); past it, yield the core and then block, so long
+        // sorts and merges do not hold a host core at 100 %
         hipError_t e;
+        const auto t0 = std::chrono::steady_clock::now();
         while ((e = hipEventQuery(wait_ev)) == hipErrorNotReady) {
+            const auto dt = std::chrono::steady_clock::now() - t0;
+            if (dt > std::chrono::microseconds(200)) {
+                e = hipEventSynchronize(wait_ev);
+                break;
+            }
+            if (dt > std::chrono::microseconds(50)) sched_yield();
         }
         SMJ_CHECK(e);
 #else

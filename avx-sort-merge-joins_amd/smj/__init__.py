@@ -49,7 +49,8 @@ REFERENCE_SYMBOLS = [
     "merge_join", "merge_join_interpolation", "print_timing", "sortmergejoin_multiway",
     "sortmergejoin_multipass", "sortmergejoin_mpsm", "sortmergejoin_initrun",
     "chainedtuplebuffer_init", "chainedtuplebuffer_free", "chainedtuplebuffer_tuples",
-    "cb_next_writepos", "write_result_relation",
+    "cb_next_writepos", "write_result_relation", "radix_cluster", "is_sorted_helper",
+    "check_sorted",
 ]
 DEVICE_SYMBOLS = [
     "smj_tuple_bytes", "smj_device_name", "smj_workspace_create",
@@ -62,7 +63,7 @@ DEVICE_SYMBOLS = [
     "smj_set_materialize", "smj_dev_join_segmented_tables", "smj_dev_partition_range_sampled",
     "smj_sampled_capacity", "smj_sampled_shards", "smj_context_workspace",
     "smj_dev_gen_nonunique", "smj_dev_gen_zipf_ref", "smj_glibc_rand",
-    "smj_dev_xsend", "smj_dev_xrecv",
+    "smj_dev_xsend", "smj_dev_xrecv", "smj_join",
 ]
 
 
@@ -153,6 +154,10 @@ class Library:
             "cb_next_writepos": (_P, [_P]),
             "write_result_relation": (None, [_P, C.c_char_p]),
             "smj_set_materialize": (None, [C.c_int]),
+            "smj_join": (C.POINTER(Result), [_P, _P, _P, C.c_int, C.c_int]),
+            "radix_cluster": (None, [_P, _P, _P, C.c_int, C.c_int]),
+            "is_sorted_helper": (C.c_int, [_P, _U64]),
+            "check_sorted": (None, [_P, _P, _U64, _U64, C.c_int]),
             "smj_tuple_bytes": (C.c_int, []),
             "smj_device_name": (C.c_char_p, []),
             "smj_workspace_create": (_P, []),
@@ -228,6 +233,22 @@ class Library:
         cnt = np.array([rels[i].num_tuples for i in range(fan)], np.int64)
         off = np.array([(rels[i].tuples - base) // self.width for i in range(fan)], np.int64)
         return out, cnt, off
+
+    def radix_cluster(self, t: np.ndarray, shift: int, bits: int, hist=None):
+        """radix_cluster (partition.c:93-149): returns (output, updated int32
+        hist).  `hist` (int32, 2^bits) is the caller's histogram the
+        reference adds to; zeros by default."""
+        t = np.ascontiguousarray(t, dtype=self.dtype)
+        h = np.zeros(1 << bits, np.int32) if hist is None else \
+            np.ascontiguousarray(hist, dtype=np.int32).copy()
+        out = np.zeros(len(t) + int(h.sum()), self.dtype)
+        rin, rout = self._rel(t), self._rel(out)
+        self.lib.radix_cluster(C.byref(rout), C.byref(rin), _ptr(h), shift, bits)
+        return out, h
+
+    def is_sorted_helper(self, t: np.ndarray) -> int:
+        t = np.ascontiguousarray(t, dtype=self.dtype)
+        return int(self.lib.is_sorted_helper(_ptr(t) if len(t) else None, len(t)))
 
     def avxsort_tuples(self, t: np.ndarray, fn: str = "avxsort_tuples") -> np.ndarray:
         a = np.ascontiguousarray(t, dtype=self.dtype).copy()
@@ -318,16 +339,11 @@ class Library:
                          20 << 20, 2)
         rr, rs = self._rel(R), self._rel(S)
         algo = algo or ("mpsm" if mpsm else "m-way")
-        fn = {"m-way": self.lib.sortmergejoin_multiway,
-              "m-pass": self.lib.sortmergejoin_multipass,
-              "mpsm": self.lib.sortmergejoin_mpsm}[algo]
-        if materialize or persist:
-            self.lib.smj_set_materialize(1)
-        try:
-            res = fn(C.byref(rr), C.byref(rs), C.byref(cfg))
-        finally:
-            if materialize or persist:
-                self.lib.smj_set_materialize(0)
+        code = {"m-way": 0, "m-pass": 1, "mpsm": 2}[algo]
+        # the materialisation is this call's own (smj_join), not the process
+        # switch the reference-named functions read
+        res = self.lib.smj_join(C.byref(rr), C.byref(rs), C.byref(cfg), code,
+                                1 if (materialize or persist) else 0)
         if not res:
             return None
         total = int(res.contents.totalresults)

@@ -56,10 +56,14 @@ def parse():
     p.add_argument("--shift", type=int, default=0, help="partition: shift bits")
     p.add_argument("--dist", default="uniform", choices=("uniform", "zipf"))
     p.add_argument("--theta", type=float, default=0.75)
-    p.add_argument("--zipf-gen", default="reference", choices=("reference", "fast"),
+    p.add_argument("--zipf-gen", default="auto", choices=("auto", "reference", "fast"),
                    help="zipf S: the reference's own create_relation_zipf after "
-                        "srand(54321), bit-exact (refgen.hip; the alphabet and CDF table "
-                        "are built on the host), or the fast rejection-inversion sampler")
+                        "srand(54321), bit-exact (refgen.hip), or the fast "
+                        "rejection-inversion sampler.  The reference stream needs the "
+                        "alphabet permutation and CDF table over 1..|R| built on the host "
+                        "(a serial shuffle) and held on the device: 12 bytes per key, "
+                        "~13 GB on every rank at N = 8 x 128M.  auto: the reference "
+                        "stream up to 2^28 keys, the fast sampler above")
     p.add_argument("--fanout-bits", type=int, default=8,
                    help="level-1 partitions (2^bits) of the join; the library raises it "
                         "as the relation size needs")
@@ -69,8 +73,11 @@ def parse():
     p.add_argument("--no-trace", action="store_true",
                    help="lab: no per-kernel HIP events in the timed loop (measures what "
                         "the trace costs; the line then has no roofline)")
-    p.add_argument("--check", action="store_true",
-                   help="also verify sortedness/multiset of the sorted outputs")
+    p.add_argument("--no-check", action="store_true",
+                   help="skip the output check after the timed loop (default: the sorted "
+                        "outputs are checked on the device for (key, payload) order and "
+                        "against the inputs' order-independent checksum; result_ok "
+                        "carries it)")
     p.add_argument("--exchange-path", action="store_true",
                    help="run the multi-GPU code path (range partition, all-to-all, "
                         "segmented local join) even at N=1 (a one-rank RCCL group)")
@@ -110,11 +117,23 @@ def _ref_exe(name):
 
 
 def host_cores():
-    """(threads this job may use, cores lscpu reports for the whole host)."""
-    share = os.cpu_count() or 1
-    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    if cap:
-        share = min(share, cap)
+    """(threads for the CPU baseline, facts about the host).
+
+    BASELINE.md §3 asks for T = the largest power of two within the host's
+    cores.  The cores this job may use are the process's affinity mask,
+    further limited by a cgroup CPU quota and by OMP_NUM_THREADS, which the
+    GPU pool sets to the job's CPU share (16 per GPU); lscpu reports the
+    machine.  All of them go into the line."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:  # cgroup v2: "max 100000" or "<quota> <period>"
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except Exception:
+        pass
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or None
+    share = min(x for x in (aff, quota, omp) if x)
     lscpu = None
     try:
         out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=30).stdout
@@ -124,7 +143,8 @@ def host_cores():
             lscpu = int(per.group(1)) * int(sock.group(1))
     except Exception:  # pragma: no cover
         pass
-    return share, lscpu
+    return share, {"affinity_cpus": aff, "cgroup_cpu_quota": quota, "omp_num_threads": omp,
+                   "host_cores_lscpu": lscpu}
 
 
 def _join_once(exe, n, threads, skew=0.0):
@@ -141,30 +161,32 @@ def _join_once(exe, n, threads, skew=0.0):
     return t, d["count"] == n
 
 
-def cpu_baseline(width, n, skew=0.0):
+def cpu_baseline(width, n, skew=0.0, t1=True):
     """The reference m-way join (oracle/_ref/cpu_baseline*: compiled from the
     reference's sources) on this host: T = the largest power of two within
-    the job's CPU share, and T = 1.  16-byte tuples take the
-    reference's scalar path, 8-byte tuples its AVX path.  skew > 0: S is the
-    reference driver's --skew input (create_relation_zipf, srand(54321)), the
-    relation the GPU line joins with --dist zipf."""
+    the job's CPU share (host_cores), and T = 1 on the same 128M x 128M
+    (BASELINE.md §3).  16-byte tuples take the reference's scalar path,
+    8-byte tuples its AVX path.  skew > 0: S is the reference driver's --skew
+    input (create_relation_zipf, srand(54321)), the relation the GPU line
+    joins with --dist zipf."""
     exe = _ref_exe(f"cpu_baseline{width}")
-    share, lscpu = host_cores()
+    share, facts = host_cores()
     threads = 1
     while threads * 2 <= share and threads * 2 <= 1024:
         threads *= 2
     t, ok = _join_once(exe, n, threads, skew)
-    # T = 1 on a quarter of the sample (a 128M single-thread run alone takes
-    # about 40 s with its generation)
-    n1 = max(n // 4, 1)
-    t1, ok1 = _join_once(exe, n1, 1, skew)
+    t1v, ok1 = None, True
+    if t1:
+        ts, ok1 = _join_once(exe, n, 1, skew)
+        t1v = round(2 * n / ts / 1e6, 3)
     path = "scalar" if width == 16 else "AVX"
     return {"value": round(2 * n / t / 1e6, 3), "unit": "Mtuples/s",
-            "cores": threads, "kind": "reference",
-            "host_cores_lscpu": lscpu,
-            "t1_value": round(2 * n1 / t1 / 1e6, 3),
+            "cores": threads, "kind": "reference", **facts,
+            "t1_value": t1v,
             "sample": f"sortmergejoin_multiway {n}x{n} {width}B tuples, {threads} threads "
-                      f"(t1_value: 1 thread on {n1}x{n1}), "
+                      f"(the job's CPU share: affinity {facts['affinity_cpus']}, cgroup quota "
+                      f"{facts['cgroup_cpu_quota']}, OMP_NUM_THREADS {facts['omp_num_threads']}; "
+                      f"t1_value: 1 thread on the same {n}x{n}), "
                       f"{f'PK / Zipf {skew} FK (create_relation_zipf)' if skew > 0 else 'PK/FK uniform'}, "
                       f"{path} path, "
                       f"count {'ok' if ok and ok1 else 'MISMATCH'}"}
@@ -181,7 +203,7 @@ def cpu_baseline_op(op, width, n, bits, shift, fanin=64):
     if not m:
         raise RuntimeError(f"{exe} printed no result (rc {r.returncode}): {r.stderr[-400:]}")
     d = json.loads(m.group(1))
-    _, lscpu = host_cores()
+    _, facts = host_cores()
     what = {"partition": f"partition_relation_optimized {n} tuples, {bits} bits, shift {shift}",
             "sort": f"{'avxsort_tuples' if width == 8 else 'scalarsort_tuples'} {n} tuples",
             "merge": f"{'avx' if width == 8 else 'scalar'}_multiway_merge of {fanin} runs "
@@ -189,24 +211,88 @@ def cpu_baseline_op(op, width, n, bits, shift, fanin=64):
     if op == "merge":
         n = n * fanin
     return {"value": round(n / d["seconds"] / 1e6, 3), "unit": "Mtuples/s", "cores": 1,
-            "kind": "reference", "host_cores_lscpu": lscpu,
+            "kind": "reference", **facts,
             "sample": f"{what}, {width}B tuples, create_relation_pk seed 12345, "
                       f"single core (as the reference bench), "
                       f"{'ok' if d['ok'] else 'FAILED'}"}
+
+
+def _pmc(cfg_key):
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get(cfg_key, {})
+    except Exception:
+        return {}
 
 
 def load_traffic(kernel, cfg_key):
     """HBM bytes per launch of `kernel` (FETCH_SIZE*2 + WRITE_SIZE, separate
     rocprofv3 --pmc passes of this same bench command; tools/make_traffic.py
     wrote profiles/pmc_traffic.json).  None when not profiled."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    try:
-        with open(path) as f:
-            d = json.load(f)
-        e = d.get(cfg_key, {}).get(kernel)
-        return int(e["bytes"]) if e else None
-    except Exception:
+    e = _pmc(cfg_key).get(kernel)
+    return int(e["bytes"]) if e else None
+
+
+def step_traffic(kernel, launches_per_step, cfg_key):
+    """PMC bytes of one whole step: every library kernel of the profiled run
+    (data generators excluded), its per-launch bytes times its launches, over
+    the profiled run's step count (the dominant kernel's launches there over
+    its launches per step).  None when the config was not profiled."""
+    d = _pmc(cfg_key)
+    if kernel not in d or not launches_per_step:
         return None
+    steps = d[kernel]["launches"] / launches_per_step
+    tot = sum(e["bytes"] * e["launches"] for k, e in d.items()
+              if k.startswith("k_") and not k.startswith("k_gen"))
+    return int(tot / steps)
+
+
+def _checksum(t):
+    """Order-independent checksum of (n, 2) rows (payload, key) as a wrapping
+    int64 tensor: sums of the keys, the payloads and of two 64-bit avalanche
+    hashes of each row (a lost row and a duplicated one cancel only if their
+    hashes collide, ~2^-64).  Sums over disjoint parts add up (mod 2^64)."""
+    k = t[:, 1].to(torch.int64)
+    p = t[:, 0].to(torch.int64)
+    z = (k * 0x2545F4914F6CDD1D) ^ (p + 0x632BE59BD9B4E019)
+    z = (z ^ (z >> 31)) * 0x1B873593CA5A7E35
+    z = (z ^ (z >> 29)) * 0x3C79AC492BA7B653
+    z = z ^ (z >> 32)
+    return torch.stack([k.sum(), p.sum(), z.sum(), (z * (z | 1)).sum()])
+
+
+def _is_sorted(t, w):
+    """Rows in the library's order: (key, payload) ascending; 8-byte tuples
+    compare as the signed 64-bit word key << 32 | unsigned payload."""
+    if t.shape[0] < 2:
+        return True
+    k = t[:, 1].to(torch.int64)
+    p = t[:, 0].to(torch.int64)
+    if w == 8:
+        p = p & 0xFFFFFFFF
+    ok = (k[1:] > k[:-1]) | ((k[1:] == k[:-1]) & (p[1:] >= p[:-1]))
+    return bool(ok.all().item())
+
+
+def output_check(pairs, w, dist=None):
+    """[(input rows, sorted output rows), ...] -> dict: every output sorted and
+    a permutation of its input (checksums; over a process group the sums of
+    all ranks are compared, as each rank sorts its key range of everyone's
+    rows)."""
+    res = {"sorted": True, "checksum_equal": True}
+    for src, out in pairs:
+        res["sorted"] = res["sorted"] and _is_sorted(out, w)
+        a, b = _checksum(src), _checksum(out)
+        if dist is not None:
+            dist.all_reduce(a)
+            dist.all_reduce(b)
+        res["checksum_equal"] = res["checksum_equal"] and bool(torch.equal(a, b))
+    if dist is not None:
+        f = torch.tensor([0 if res["sorted"] else 1], device="cuda")
+        dist.all_reduce(f)
+        res["sorted"] = int(f.item()) == 0
+    return res
 
 
 # --------------------------------------------------------------------------
@@ -263,6 +349,8 @@ def main():
     R = lib.empty(n)
     S = lib.empty(n)
     lib.dev_gen_pk(R, first, total, 12345)
+    if a.zipf_gen == "auto":
+        a.zipf_gen = "reference" if total <= (1 << 28) else "fast"
     if a.dist == "uniform":
         lib.dev_gen_fk(S, first, total, total, 54321)
     elif a.zipf_gen == "reference":
@@ -302,9 +390,10 @@ def main():
     else:
         from smj.dist import DeviceOps, DistributedJoin
         dj = DistributedJoin(DeviceOps(lib), a.fanout_bits, 1, total)
+        last = [None, None]
 
         def step():
-            dj.step(R, S, count)
+            last[0], last[1] = dj.step(R, S, count)
 
     def reset():
         if exchange:
@@ -333,6 +422,14 @@ def main():
     got = int(count.item())
     expect = total  # every S key exists once in R (PK/FK and Zipf over 1..|R|)
     ok = got == expect
+    # the last timed step's sorted relations, checked on the device (order and
+    # checksums against the inputs); the reference-named entry point keeps its
+    # sorted relations internal, so --api checks the count only
+    chk = None
+    if not a.no_check and not (a.api and not exchange):
+        outs = (sR, sS) if not exchange else tuple(last)
+        chk = output_check([(R, outs[0]), (S, outs[1])], w, dist if exchange and N > 1 else None)
+        ok = ok and chk["sorted"] and chk["checksum_equal"]
     ms_step = elapsed / a.steps * 1e3
     value = 2 * total / (elapsed / a.steps) / 1e6
 
@@ -341,8 +438,8 @@ def main():
             dist.destroy_process_group()
         return
 
-    roof = dominant_roofline(kern, lambda name: alg_bytes_per_launch(name, n, n, n, w),
-                             f"n{n}_w{w}_{a.dist}")
+    cfg_key = f"n{n}_w{w}_{a.dist}"
+    roof = dominant_roofline(kern, lambda name: alg_bytes_per_launch(name, n, n, n, w), cfg_key)
     pipeline_gbs = 5 * 2 * total * w / (elapsed / a.steps) / 1e9
 
     cpu = None
@@ -379,12 +476,16 @@ def main():
         "cpu_baseline": cpu,
         "result_ok": ok,
         "matches": got,
+        "output_check": chk if chk is not None else
+        ("count only (--api: the entry point keeps its sorted relations internal)"
+         if a.api else "skipped (--no-check)"),
         "detail": {
             "S_tuples_per_s_M": round(total / (elapsed / a.steps) / 1e6, 2),
             "pipeline_alg_GBps_5w": round(pipeline_gbs, 1),
             "pipeline_frac": round(pipeline_gbs / HBM_PEAK_GBS, 4),
+            **step_phys(roof, brk, ms_step, cfg_key),
             # untimed steps, every kernel traced (timed_loop)
-            "kernels_ms_per_step": {k: round(v, 4) for k, v in brk.items()},
+            "kernels_ms_per_step": {k: round(v[0], 4) for k, v in brk.items()},
             "device": lib.lib.smj_device_name().decode(),
             "exchange": xchg,
         },
@@ -429,7 +530,8 @@ def timed_loop(a, lib, dist, step, reset=None):
     for _ in range(nb):
         step()
     torch.cuda.synchronize()
-    brk = {k: v[0] / nb for k, v in lib.trace_read().items()}
+    brk_l = {k: (v[0] / nb, v[1] / nb) for k, v in lib.trace_read().items()}
+    brk = {k: v[0] for k, v in brk_l.items()}
     dom = max(brk, key=brk.get) if brk else None
     lib.trace(False)
     if dist:
@@ -450,7 +552,7 @@ def timed_loop(a, lib, dist, step, reset=None):
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    return elapsed, kern, brk
+    return elapsed, kern, brk_l
 
 
 def dominant_roofline(kern, bytes_of, cfg_key):
@@ -468,10 +570,30 @@ def dominant_roofline(kern, bytes_of, cfg_key):
         return None
     name, ms, launches, b = best
     ach = b / (ms / launches / 1e3) / 1e9
+    traffic = load_traffic(name, cfg_key)
+    # phys: the PMC bytes of one launch over its measured average duration --
+    # HBM utilisation, where frac is the algorithmic credit (16-byte tuples
+    # move as packed 8-byte words, so their credit exceeds their bytes)
+    phys = traffic / (ms / launches / 1e3) / 1e9 if traffic else None
     return {"bound": "hbm", "kernel": name, "achieved": round(ach, 1),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-            "traffic": load_traffic(name, cfg_key), "alg_bytes_per_launch": b,
-            "avg_launch_ms": round(ms / launches, 4)}
+            "traffic": traffic, "alg_bytes_per_launch": b,
+            "avg_launch_ms": round(ms / launches, 4),
+            "phys_achieved": round(phys, 1) if phys else None,
+            "phys_frac": round(phys / HBM_PEAK_GBS, 4) if phys else None}
+
+
+def step_phys(roof, brk_l, ms_step, cfg_key):
+    """The whole step's PMC bytes (step_traffic) over the measured step time."""
+    if not roof:
+        return {}
+    k = roof["kernel"]
+    b = step_traffic(k, brk_l.get(k, (0, 0))[1], cfg_key)
+    if not b:
+        return {"step_pmc_bytes": None}
+    g = b / (ms_step / 1e3) / 1e9
+    return {"step_pmc_bytes": b, "step_phys_GBps": round(g, 1),
+            "step_phys_frac": round(g / HBM_PEAK_GBS, 4)}
 
 
 def run_exchange(a, json_out, N, rank, local):
@@ -551,6 +673,26 @@ def run_exchange(a, json_out, N, rank, local):
     dist.destroy_process_group()
 
 
+def partition_check(R, out, hist, off, bits, shift, w):
+    """partition_relation_optimized's output on the device: counts sum to n,
+    every partition starts on a 64-byte boundary, every tuple of partition p
+    has digit p (((key - 1) & mask) >> shift, partition.c:29), and the
+    partitions together are a permutation of the input (checksums)."""
+    n = R.shape[0]
+    fan = 1 << bits
+    res = {"counts_sum": int(hist.sum().item()) == n,
+           "aligned_64B": bool(((off * w) % 64 == 0).all().item())}
+    pid = torch.repeat_interleave(torch.arange(fan, device="cuda"), hist)
+    base = torch.cumsum(hist, 0) - hist
+    pos = off[pid] + torch.arange(n, device="cuda") - base[pid]
+    rows = out[pos]
+    mask = ((1 << bits) - 1) << shift
+    dig = ((rows[:, 1].to(torch.int64) - 1) & mask) >> shift
+    res["digits"] = bool((dig == pid).all().item())
+    res["checksum_equal"] = bool(torch.equal(_checksum(R), _checksum(rows)))
+    return res
+
+
 def run_op(a, lib, json_out, dist, N, rank):
     """bench_sort / bench_partitioning on the device (BASELINE configs 2 and
     3): one step = one smj_dev_sort (avxsort_tuples' device form) or one
@@ -601,19 +743,26 @@ def run_op(a, lib, json_out, dist, N, rank):
             lib.dev_partition(R, out, a.bits, a.shift, True, hist, off)
     torch.cuda.synchronize()
     elapsed, kern, brk = timed_loop(a, lib, dist, step)
-    if a.op in ("sort", "merge"):
-        keys = out[:, 1]
-        ok = bool((keys[1:] >= keys[:-1]).all().item()) if n > 1 else True
+    chk = None
+    if a.no_check:
+        ok = True
+    elif a.op == "sort":
+        chk = output_check([(R, out)], w)
+    elif a.op == "merge":
+        chk = output_check([(torch.cat(runs), out)], w)
     else:
-        ok = int(hist.sum().item()) == n
+        chk = partition_check(R, out, hist, off, a.bits, a.shift, w)
+    if chk is not None:
+        ok = all(v for v in chk.values() if isinstance(v, bool))
     if rank != 0:
         if dist:
             dist.destroy_process_group()
         return
     ms_step = elapsed / a.steps * 1e3
     value = N * n / (elapsed / a.steps) / 1e6
+    cfg_key = f"{a.op}_n{n}_w{w}"
     roof = dominant_roofline(kern, lambda name: alg_bytes_per_launch(name, n, n, 0, w, a.op),
-                             f"{a.op}_n{n}_w{w}")
+                             cfg_key)
     alg = 2 * n * w  # 2·N·w for bench_sort and bench_partitioning
     cpu = None
     if N == 1 and not a.no_cpu_baseline:
@@ -648,11 +797,13 @@ def run_op(a, lib, json_out, dist, N, rank):
         "roofline": roof,
         "cpu_baseline": cpu,
         "result_ok": ok,
+        "output_check": chk if chk is not None else "skipped (--no-check)",
         "detail": {
             "alg_GBps_2Nw": round(alg / (elapsed / a.steps) / 1e9, 1),
             "alg_frac_2Nw": round(alg / (elapsed / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
+            **step_phys(roof, brk, ms_step, cfg_key),
             # untimed steps, every kernel traced (timed_loop)
-            "kernels_ms_per_step": {k: round(v, 4) for k, v in brk.items()},
+            "kernels_ms_per_step": {k: round(v[0], 4) for k, v in brk.items()},
             "device": lib.lib.smj_device_name().decode(),
         },
     }

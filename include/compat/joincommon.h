@@ -2,7 +2,8 @@
  * joincommon.h -- drop-in for the reference header src/joins/joincommon.h
  * (sdecoder/AVX-sort-merge-joins): merge_join (:78-80),
  * merge_join_interpolation (:92-95), sortmergejoin_initrun (:59-61),
- * print_timing (:64-66), and the thread scaffolding arg_t / relationpair_t
+ * print_timing (:64-66),
+ * is_sorted_helper / check_sorted (:99-103), and the thread scaffolding arg_t / relationpair_t
  * (:105-155), all declared in ../smj.h.  DEBUGMSG keeps the reference's
  * macro (:46-54) for drivers that use it.
  */

@@ -165,6 +165,14 @@ void partition_relation_optimized_V2(relation_t ** partitions,
 void histogram_memcpy_bench(relation_t ** partitions, relation_t * input,
                             relation_t * output, uint32_t nbits);
 
+/* partition.h:38-43 (defined partition.c:93-149) -- the naive stable radix
+ * cluster on bits [R, R + D) of key - 1 into outRel->tuples, partitions back
+ * to back (no padding).  Like the reference it ADDS each partition's count to
+ * hist[0 .. 2^D) and starts partition i at the prefix sum of the updated hist,
+ * so the caller zeroes hist first for the usual layout. */
+void radix_cluster(relation_t * outRel, relation_t * inRel, int32_t * hist,
+                   int R, int D);
+
 /* ------------------------------------------------------------------------ */
 /* Sorting (reference src/avxsort/avxsort.h:35-57,                           */
 /* src/avxsort/avxsort_multiway.h:35-55, src/scalarsort/scalarsort.h).       */
@@ -264,10 +272,19 @@ uint64_t merge_join(tuple_t * rtuples, tuple_t * stuples, const uint64_t numR,
  * (the other threads' lists stay NULL; m-pass fills one list per thread, as
  * its threads own disjoint partitions).  Default: the environment variable
  * SMJ_MATERIALIZE (unset = off).  The switch is process-wide, like the
- * compile-time flag it stands for: every join in the process sees the last
- * value set (an atomic; concurrent joins that need different modes cannot
- * share a process). */
+ * compile-time flag it stands for: every reference-named join in the
+ * process sees the last value set (an atomic).  Callers that need a mode per
+ * call use smj_join below instead. */
 void smj_set_materialize(int on);
+
+/* The reference's three join algorithms with the materialisation chosen per
+ * call (library extension; the reference fixes it per build): algo 0 =
+ * sortmergejoin_multiway, 1 = sortmergejoin_multipass, 2 =
+ * sortmergejoin_mpsm; materialize 1 / 0 overrides the process switch for this
+ * call only, -1 follows it.  Returns what the named function returns (NULL
+ * for an unknown algo). */
+result_t * smj_join(relation_t * relR, relation_t * relS, joinconfig_t * joincfg,
+                    int algo, int materialize);
 
 /* main.c:609-614 (PERSIST_RELATIONS + JOIN_MATERIALIZE): append the
  * materialised result to `filename` in the text format of write_relation
@@ -285,6 +302,18 @@ void write_result_relation(result_t * result, const char * filename);
 void print_timing(uint64_t numtuples, struct timeval * start,
                   struct timeval * end, FILE * out);
 #endif
+
+/* joincommon.h:99-100 (defined joincommon.c:397-500): 1 when the keys of
+ * the `nitems` tuples at `items` (a tuple_t array passed as int64_t*) never
+ * decrease, starting from key 0, else 0.  Without KEY_8B it prints the
+ * reference's "[WARN ] Equal items" line at the first repeated key before any
+ * decrease and its "[ERROR]" line at the first decrease; with KEY_8B it
+ * prints nothing.  The scan runs on the device. */
+int is_sorted_helper(int64_t * items, uint64_t nitems);
+
+/* joincommon.h:101-103 (defined joincommon.c:503-515): prints whether R and
+ * S are sorted ("%d-thread -> R is sorted, size = %d"). */
+void check_sorted(int64_t * R, int64_t * S, uint64_t nR, uint64_t nS, int my_tid);
 
 /* joincommon.c (not in joincommon.h's prose): merge_join with an
  * interpolation search for the start; same count as merge_join. */

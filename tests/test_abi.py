@@ -87,3 +87,19 @@ def test_glibc_rand_jump_ahead(smj_mod, width):
         x = libc.rand()
         if k in (65535, 65536, 999_999):
             assert L.glibc_rand(4242, k) == x, k
+
+
+@pytest.mark.parametrize("width", [8, 16])
+def test_c_caller_links(smj_mod, width, tmp_path):
+    """tests/compat_check/abi_extras.c (radix_cluster, is_sorted_helper,
+    check_sorted through the compat headers) compiles and links against the
+    library like a reference driver; tests/test_gpu_abi.py runs it."""
+    import subprocess
+    src = os.path.join(ROOT, "tests", "compat_check", "abi_extras.c")
+    lib = os.path.dirname(smj_mod.lib_path(width))
+    name = "smj_hip" if width == 8 else "smj_hip_k8"
+    exe = tmp_path / "abi_extras"
+    cmd = ["gcc", "-O1", "-std=gnu99", "-I", os.path.join(ROOT, "include", "compat"), src,
+           f"-L{lib}", f"-l{name}", "-o", str(exe)] + (["-DKEY_8B"] if width == 16 else [])
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]

@@ -58,7 +58,10 @@ def test_dominant_kernel_alone_in_timed_steps(no_cuda_sync):
     n, elapsed, kern, brk = run(lib)
     assert n == 2 + 3 + 7  # warm-up, untimed breakdown, timed
     assert elapsed >= 0
-    assert brk == pytest.approx({k: v[0] for k, v in FakeTraceLib.STEP.items()})
+    assert {k: v[0] for k, v in brk.items()} == pytest.approx(
+        {k: v[0] for k, v in FakeTraceLib.STEP.items()})
+    assert {k: v[1] for k, v in brk.items()} == pytest.approx(
+        {k: v[1] for k, v in FakeTraceLib.STEP.items()})
     # the timed steps trace the kernel with the largest summed time only
     assert (True, "k_groupsort") in lib.calls
     assert kern == {"k_groupsort": pytest.approx((1.3 * 7, 7))}
@@ -81,3 +84,51 @@ def test_no_trace_lab_switch(no_cuda_sync):
     assert n == 1 + 1  # one untimed step (at least one), one timed
     assert kern == {} and brk == {}
     assert bench.dominant_roofline(kern, lambda name: 1.0, "none") is None
+
+
+def test_phys_fields(monkeypatch):
+    """roofline.phys_frac = PMC bytes per launch / average launch time / peak
+    beside the credited frac; the step's PMC bytes from every library kernel
+    of the profiled run over its step count."""
+    pmc = {"k_groupsort": {"bytes": 6.3e9, "launches": 15},
+           "k_scatter": {"bytes": 3.2e9, "launches": 30},
+           "k_tilepass": {"bytes": 4.1e9, "launches": 15},
+           "k_gen_perm": {"bytes": 2e9, "launches": 2}}
+    monkeypatch.setattr(bench, "_pmc", lambda key: pmc)
+    kern = {"k_groupsort": (1.28 * 10, 10)}
+    roof = bench.dominant_roofline(kern, lambda name: 8.192e9, "cfg")
+    assert roof["traffic"] == int(6.3e9)
+    assert roof["phys_frac"] == pytest.approx(6.3e9 / 1.28e-3 / 1e9 / bench.HBM_PEAK_GBS,
+                                              rel=1e-3)
+    assert roof["frac"] > roof["phys_frac"]
+    sp = bench.step_phys(roof, {"k_groupsort": (1.28, 1.0), "k_scatter": (1.2, 2.0)}, 3.4,
+                         "cfg")
+    step_bytes = 6.3e9 + 2 * 3.2e9 + 4.1e9  # the generator is not part of a step
+    assert sp["step_pmc_bytes"] == pytest.approx(step_bytes, rel=1e-6)
+    assert sp["step_phys_frac"] == pytest.approx(step_bytes / 3.4e-3 / 1e9 / bench.HBM_PEAK_GBS,
+                                                 rel=1e-3)
+
+
+@pytest.mark.parametrize("w", [8, 16])
+def test_output_check_on_cpu_tensors(w):
+    """bench.py's output check (sortedness in the library's order, checksums
+    against the input) on CPU tensors of the bench's (n, 2) layout."""
+    import torch
+    dt = torch.int32 if w == 8 else torch.int64
+    g = torch.Generator().manual_seed(5)
+    keys = torch.randint(1, 1000, (5000,), generator=g)
+    pay = torch.randint(-(1 << 30), 1 << 30, (5000,), generator=g)
+    src = torch.stack([pay, keys], 1).to(dt)
+    # the library's order: (key, payload), payload unsigned for 8-byte tuples
+    p64 = src[:, 0].to(torch.int64)
+    pk = p64 & 0xFFFFFFFF if w == 8 else p64
+    order = sorted(range(5000), key=lambda i: (int(src[i, 1]), int(pk[i])))
+    out = src[torch.tensor(order)]
+    assert bench.output_check([(src, out)], w) == {"sorted": True, "checksum_equal": True}
+    bad = out.clone()
+    bad[10], bad[11] = out[11].clone(), out[10].clone()
+    if not torch.equal(bad, out):
+        assert bench.output_check([(src, bad)], w)["sorted"] is False
+    lost = out.clone()
+    lost[7] = lost[8]
+    assert bench.output_check([(src, lost)], w)["checksum_equal"] is False

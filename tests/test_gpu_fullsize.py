@@ -76,10 +76,16 @@ def test_bench_partition_full(libs, oracles, width, bits, shift):
     np.testing.assert_array_equal(got[:len(want)][mask], want[mask])
 
 
-@pytest.mark.parametrize("dist_", ["uniform", "zipf"])
-def test_headline_join_full_bitexact(libs, oracles, width, dist_):
+@pytest.mark.parametrize("dist_,fanout_bits", [
+    ("uniform", 8),     # bench.py's plan: D1 = 8, D2 = 8, packed words at s1 = 19
+    ("zipf_ref", 8),    # the Zipf line's S: create_relation_zipf after srand(54321)
+    ("uniform", 9),
+    ("zipf", 9),        # the fast rejection-inversion sampler (N1024 tests' S)
+])
+def test_headline_join_full_bitexact(libs, oracles, width, dist_, fanout_bits):
     """BASELINE configs[3] (R = S = 128M): the device join's sorted R, sorted S
-    and count against the oracle's sortmergejoin on the same inputs."""
+    and count against the oracle's sortmergejoin on the same inputs, at the
+    exact plan bench.py times (fanout_bits 8) and at 9."""
     import torch
     lib, orc = libs[width], oracles[width]
     n = 128_000_000
@@ -87,11 +93,13 @@ def test_headline_join_full_bitexact(libs, oracles, width, dist_):
     lib.dev_gen_pk(R, 0, n, 12345)
     if dist_ == "uniform":
         lib.dev_gen_fk(S, 0, n, n, 54321)
+    elif dist_ == "zipf_ref":
+        lib.dev_gen_zipf_ref(S, 0, n, 0.75, 54321)
     else:
         lib.dev_gen_zipf(S, 0, n, 0.75, 54321)
     sR, sS = lib.empty(n), lib.empty(n)
     cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
-    lib.dev_join(R, S, sR, sS, cnt, 9, 1, n)
+    lib.dev_join(R, S, sR, sS, cnt, fanout_bits, 1, n)
     torch.cuda.synchronize()
     count = int(cnt.item())
     hR, hS = lib.to_host(R), lib.to_host(S)
