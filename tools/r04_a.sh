@@ -13,3 +13,5 @@ timeout -k 10 400 python bench.py > $O/join16.json 2> $O/join16.err || { tail -2
 cat $O/join16.json
 timeout -k 10 200 python bench.py --op sort --width 8 --no-cpu-baseline > $O/sort8.json 2> $O/sort8.err || { tail -20 $O/sort8.err; exit 1; }
 cat $O/sort8.json
+timeout -k 10 300 build_lab/scatterlab 27 > $O/scatterlab.txt 2>&1 || { tail -5 $O/scatterlab.txt; exit 1; }
+cat $O/scatterlab.txt
