@@ -54,6 +54,9 @@ constexpr int TP_THREADS = SMJ_TP_THREADS;
 #ifndef SMJ_GS_PAIR
 #define SMJ_GS_PAIR 1  // one relation: two groups per group-pass iteration (0: a lab build's one)
 #endif
+#ifndef SMJ_GS_TWO
+#define SMJ_GS_TWO 1  // both slots of a group-pass iteration in one barrier chain (sort_two)
+#endif
 #ifndef SMJ_GS_ABL
 #define SMJ_GS_ABL 0  // ablations for measurements only (1: no in-group sort; 2: no
                       // equal-digit run fixing; 3: no write-out)
@@ -333,7 +336,8 @@ struct GroupLDS {
         unsigned long long m;
         uint32_t wk, pad;
     } win[2][GS_WIN];
-    uint32_t wtot[GS_THREADS / 64];
+    uint32_t wtot[2][GS_THREADS / 64];
+    uint32_t flags;  // sort_two's block vote: any repeated d3 digit (slot 0, 1), a clamped key
     unsigned long long scan64[GS_THREADS / 64 + 1];
     uint32_t n[2];
     uint32_t off[2];
@@ -564,7 +568,8 @@ __device__ __forceinline__ void build_tables(const GroupArgs& A, LDS& L,
 // 0 of its entry); otherwise both relations of the group are.
 template <class Src, bool PAIR, class LDS, class Meta>
 __device__ __forceinline__ void group_overflow(const GroupArgs& A, LDS& L,
-                                               const Meta& M, int slot = 0) {
+                                               const Meta& M, int slot = 0,
+                                               uint32_t counted = 0) {
     uint32_t nn[2] = {0, 0};
     uint64_t oo[2] = {0, 0};
     const uint32_t tid = otid();
@@ -596,7 +601,7 @@ __device__ __forceinline__ void group_overflow(const GroupArgs& A, LDS& L,
             e.nr[1] = nn[1];
             e.off[0] = oo[0];
             e.off[1] = oo[1];
-            e.counted = 0;
+            e.counted = counted;
             e.pad = 0;
             A.ovf[k] = e;
         }
@@ -697,12 +702,12 @@ __device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS<typename
         mx = max(mx, max(c[2 * q], c[2 * q + 1]));
     }
     const uint32_t incl = wave_incl_scan32(loc);
-    if (lane == 63) L.wtot[wid] = incl;
+    if (lane == 63) L.wtot[0][wid] = incl;
     const bool dup = __syncthreads_or(mx > 1);
     uint32_t ex = incl - loc;
 #pragma unroll
     for (uint32_t w = 0; w < GS_THREADS / 64; w++)
-        if (w < wid) ex += L.wtot[w];
+        if (w < wid) ex += L.wtot[0][w];
     const uint32_t first = ex;
 #pragma unroll
     for (int q = 0; q < GS_BPT / 2; q++) {
@@ -766,6 +771,270 @@ __device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS<typename
     return true;
 }
 
+// Hide a value from the optimiser (an empty asm that "changes" its words):
+// the value is recomputed from it instead of being kept alive.
+template <class T>
+__device__ __forceinline__ void launder(T& x) {
+    static_assert(sizeof(T) % 4 == 0, "word-sized");
+    uint32_t* w = reinterpret_cast<uint32_t*>(&x);
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 4); i++) asm volatile("" : "+v"(w[i]));
+}
+
+// Equal-digit runs of one sorted slot in B (see sort_group): false when a
+// long run is out of order (the skew path).  c / first: the calling thread's
+// bins' counts and the start of its first bin.
+template <class Lay>
+__device__ __forceinline__ bool fix_runs(GroupLDS<typename Lay::W>& L, uint32_t nr,
+                                         const uint32_t (&c)[GS_BPT], uint32_t first) {
+    const uint32_t tid = otid();
+    bool ok = true;
+    for (uint32_t i = tid + 1; i < nr; i += GS_THREADS) ok &= !Lay::less(L.B[i], L.B[i - 1]);
+    if (!__syncthreads_or(!ok)) return true;
+    uint32_t e = first;
+    bool has_long = false;
+#pragma unroll
+    for (int q = 0; q < GS_BPT; q++) {
+        const uint32_t b0 = e;
+        e += c[q];
+        if (c[q] > 1) {
+            if (c[q] <= GS_RUNMAX)
+                insertion_sort<Lay>(L.B + b0, c[q]);
+            else
+                has_long = true;
+        }
+    }
+    if (__syncthreads_or(has_long)) {
+        ok = true;
+        for (uint32_t i = tid + 1; i < nr; i += GS_THREADS) ok &= !Lay::less(L.B[i], L.B[i - 1]);
+        if (__syncthreads_or(!ok)) return false;
+    }
+    return true;
+}
+
+// Both slots' groups (R and S of one group, or pair mode's two groups of one
+// relation) through ONE chain of barriers (round 4): the two d3 histograms,
+// their scans and cursors are built together, then slot 0 is placed, fixed
+// and written, then slot 1.  sort_group ran the whole chain once per slot
+// (hist | scan | cursors | place | write, twice: 8 block barriers per join
+// group); here it is 6.  LDS is unchanged: slot 1's cursors overwrite its
+// counts in L.cnt[1] (the owning thread keeps the counts in registers, and
+// computes the exact-key match count from them during the scan), and every
+// thread zeroes its own bins at the end, so no barrier clears the histograms.
+// Only called when both slots' groups fit.  join: nrel == 2 (a failed slot 0
+// skips slot 1, the caller queues both, as sort_group's callers do).
+// Returns bit r set = slot r must take the skew path; `exact` reports whether
+// `matches` got the exact-key count (otherwise the caller counts by search).
+template <class Lay, bool PAIR, class Meta, typename Hook0, typename Hook1>
+__device__ __forceinline__ uint32_t sort_two(const GroupArgs& A, GroupLDS<typename Lay::W>& L,
+                                             const Meta& C, const RangePlan& P,
+                                             const uint32_t (&nr)[2], const uint32_t (&off)[2],
+                                             typename Lay::W (&v0)[GS_ITEMS],
+                                             typename Lay::W (&v1)[GS_ITEMS], bool join,
+                                             unsigned long long& matches, bool& exact,
+                                             Hook0&& after0, Hook1&& after1) {
+    typedef typename Lay::W W;
+    const uint32_t tid = otid(), wid = tid >> 6, lane = tid & 63;
+    // the d3 digit of slot r's elements: the fast form unless the group is
+    // an edge group of the plan (the branch is uniform: taken outside the
+    // loops, as in sort_group).  Recomputed where needed (two digit arrays
+    // held over the scans would push the kernel past 128 VGPRs).
+    auto fast = [&](int r) {
+        const uint32_t cb = PAIR && r ? C.b[1] : C.b[0], cg = PAIR && r ? C.g[1] : C.g[0];
+        const bool edge = (cb == 0 && cg == 0) || (cb == (1u << P.D1) - 1 && cg == A.nb2 - 1);
+        return A.d3_fast && !edge;
+    };
+    auto slow_digit = [&](int r, const W& x) -> uint32_t {
+        const uint32_t cb = PAIR && r ? C.b[1] : C.b[0], cg = PAIR && r ? C.g[1] : C.g[0];
+        return plan_d3(P, Lay::rel(P, x, cb), (cb << P.D2) | cg);
+    };
+    const uint32_t base_lo = (uint32_t)P.base, mask3 = (1u << P.D3) - 1;
+    bool clamped = false;
+    auto hist = [&](int r, const W(&v)[GS_ITEMS]) {
+        if (fast(r)) {
+#pragma unroll
+            for (int k = 0; k < GS_ITEMS; k++) {
+                const uint32_t d = Lay::digit_fast(v[k], base_lo, P.s1, P.s3, mask3);
+                if (k * GS_THREADS + tid < nr[r])
+                    atomicAdd(&L.cnt[r][d >> 1], 1u << ((d & 1) * 16));
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < GS_ITEMS; k++) {
+                const bool valid = k * GS_THREADS + tid < nr[r];
+                clamped |= valid && Lay::clamped(P, v[k]);
+                const uint32_t d = slow_digit(r, v[k]);
+                if (valid) atomicAdd(&L.cnt[r][d >> 1], 1u << ((d & 1) * 16));
+            }
+        }
+    };
+    hist(0, v0);
+    hist(1, v1);
+    __syncthreads();
+    // ---- both scans
+    uint32_t w0[GS_BPT / 2], w1[GS_BPT / 2];
+    uint32_t loc0 = 0, loc1 = 0, mx0 = 0, mx1 = 0;
+#pragma unroll
+    for (int q = 0; q < GS_BPT / 2; q++) {
+        w0[q] = L.cnt[0][tid * (GS_BPT / 2) + q];
+        w1[q] = L.cnt[1][tid * (GS_BPT / 2) + q];
+        const uint32_t a0 = w0[q] & 0xffffu, a1 = w0[q] >> 16;
+        const uint32_t b0 = w1[q] & 0xffffu, b1 = w1[q] >> 16;
+        loc0 += a0 + a1;
+        loc1 += b0 + b1;
+        mx0 = max(mx0, max(a0, a1));
+        mx1 = max(mx1, max(b0, b1));
+    }
+    const uint32_t incl0 = wave_incl_scan32(loc0), incl1 = wave_incl_scan32(loc1);
+    if (lane == 63) {
+        L.wtot[0][wid] = incl0;
+        L.wtot[1][wid] = incl1;
+    }
+    const uint32_t vote = (mx0 > 1 ? 1u : 0u) | (mx1 > 1 ? 2u : 0u) | (clamped ? 4u : 0u);
+    if (vote) atomicOr(&L.flags, vote);
+    __syncthreads();
+    const uint32_t fl = __builtin_amdgcn_readfirstlane(L.flags);
+    exact = join && P.s3 == 0 && !(fl & 4);
+    if (exact) {
+        // the level-3 digit is the exact key: sum_k |R_k| * |S_k| over the
+        // owned bins (taken back by the caller if a slot fails)
+#pragma unroll
+        for (int q = 0; q < GS_BPT / 2; q++)
+            matches += (unsigned long long)(w0[q] & 0xffffu) * (w1[q] & 0xffffu) +
+                       (unsigned long long)(w0[q] >> 16) * (w1[q] >> 16);
+    }
+    uint32_t ex0 = incl0 - loc0, ex1 = incl1 - loc1;
+#pragma unroll
+    for (uint32_t w = 0; w < GS_THREADS / 64; w++)
+        if (w < wid) {
+            ex0 += L.wtot[0][w];
+            ex1 += L.wtot[1][w];
+        }
+#pragma unroll
+    for (int q = 0; q < GS_BPT / 2; q++) {
+        uint32_t lo16 = ex0;
+        ex0 += w0[q] & 0xffffu;
+        L.cur[tid * (GS_BPT / 2) + q] = lo16 | (ex0 << 16);
+        ex0 += w0[q] >> 16;
+        lo16 = ex1;
+        ex1 += w1[q] & 0xffffu;
+        L.cnt[1][tid * (GS_BPT / 2) + q] = lo16 | (ex1 << 16);
+        ex1 += w1[q] >> 16;
+    }
+    __syncthreads();
+    // the vote has been read by every thread (before the barrier above)
+    if (tid == 0) L.flags = 0;
+    auto place1 = [&](uint32_t* cur, bool dup, bool valid, uint32_t d, const W& x) {
+        const uint32_t sh = (d & 1) * 16;
+        const uint32_t old = dup ? atomicAdd(&cur[d >> 1], valid ? 1u << sh : 0u)
+                                 : cur[valid ? d >> 1 : 0u];
+        L.B[valid ? (old >> sh) & 0xffffu : GS_CAP] = x;
+    };
+    auto place = [&](int r, uint32_t* cur, bool dup, const W(&v)[GS_ITEMS]) {
+        // an opaque copy of each element: otherwise the compiler keeps the
+        // histogram's digits alive over the scans instead of recomputing them
+        if (fast(r)) {
+#pragma unroll
+            for (int k = 0; k < GS_ITEMS; k++) {
+                W x = v[k];
+                launder(x);
+                place1(cur, dup, k * GS_THREADS + tid < nr[r],
+                       Lay::digit_fast(x, base_lo, P.s1, P.s3, mask3), v[k]);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < GS_ITEMS; k++) {
+                W x = v[k];
+                launder(x);
+                place1(cur, dup, k * GS_THREADS + tid < nr[r], slow_digit(r, x), v[k]);
+            }
+        }
+    };
+    // after a placement by atomics every cursor word holds its two bins'
+    // ends: the owned bins' counts come back from them and the thread's
+    // first start (no count registers held over the placement)
+    auto fix = [&](int r, const uint32_t* cur) {
+        uint32_t c[GS_BPT];
+        // the first owned bin starts where the previous thread's last ends
+        const uint32_t first = tid ? cur[tid * (GS_BPT / 2) - 1] >> 16 : 0u;
+        uint32_t prev = first;
+#pragma unroll
+        for (int q = 0; q < GS_BPT / 2; q++) {
+            const uint32_t e = cur[tid * (GS_BPT / 2) + q];
+            c[2 * q] = (e & 0xffffu) - prev;
+            c[2 * q + 1] = (e >> 16) - (e & 0xffffu);
+            prev = e >> 16;
+        }
+        return fix_runs<Lay>(L, nr[r], c, first);
+    };
+    auto write = [&](int r) {
+        const uint32_t cb = PAIR && r ? C.b[1] : C.b[0];
+        Tup* dst = A.out[r] + C.ost[r] + off[r];
+#pragma unroll
+        for (int k = 0; k < GS_ITEMS; k++) {
+            const uint32_t j = k * GS_THREADS + tid;
+            if (j < nr[r] && SMJ_GS_ABL != 3) st_stream(dst + j, Lay::unpack(P, L.B[j], cb));
+        }
+    };
+    uint32_t failed = 0;
+    // ---- slot 0
+    place(0, L.cur, fl & 1, v0);
+    after0();
+    __syncthreads();
+    if ((fl & 1) && SMJ_GS_ABL != 2 && !fix(0, L.cur)) failed |= 1;
+    if (!failed) write(0);
+    // ---- slot 1 (a join whose R failed leaves S to the skew path too)
+    if (!(join && failed)) {
+        __syncthreads();  // B is free again
+        place(1, L.cnt[1], fl & 2, v1);
+        after1();
+        __syncthreads();
+        if ((fl & 2) && SMJ_GS_ABL != 2 && !fix(1, L.cnt[1])) failed |= 2;
+        if (!(failed & 2)) write(1);
+    } else {
+        after1();
+        __syncthreads();  // slot 1's cursors are read no more
+    }
+    // the owned bins: zero for the next group (cursors and counts read no more)
+#pragma unroll
+    for (int q = 0; q < GS_BPT / 2; q++) {
+        L.cnt[0][tid * (GS_BPT / 2) + q] = 0u;
+        L.cnt[1][tid * (GS_BPT / 2) + q] = 0u;
+    }
+    return failed;
+}
+
+// Merge-join count of a group whose last digit is not the exact key: S's
+// sorted group is still in B, R's is in out (written by this workgroup before
+// a barrier, so visible); every S key run binary-searches R.
+template <class Lay, class Meta>
+__device__ __forceinline__ void count_by_search(const GroupArgs& A, GroupLDS<typename Lay::W>& L,
+                                                const Meta& C, const RangePlan& P,
+                                                const uint32_t (&cn)[2], const uint32_t (&co)[2],
+                                                unsigned long long& matches) {
+    const uint32_t tid = otid();
+    const Tup* Rs = A.out[0] + C.ost[0] + co[0];
+    const uint32_t nR = cn[0], nS = cn[1];
+    for (uint32_t i = tid; i < nS; i += GS_THREADS) {
+        const int64_t k = tup_key(Lay::unpack(P, L.B[i], C.b[0]));
+        if (i > 0 && tup_key(Lay::unpack(P, L.B[i - 1], C.b[0])) == k) continue;
+        uint32_t e = i + 1;
+        while (e < nS && tup_key(Lay::unpack(P, L.B[e], C.b[0])) == k) e++;
+        uint32_t lo = 0, hi = nR;
+        while (lo < hi) {
+            const uint32_t m = (lo + hi) >> 1;
+            if (tup_key(Rs[m]) < k) lo = m + 1; else hi = m;
+        }
+        const uint32_t lb = lo;
+        hi = nR;
+        while (lo < hi) {
+            const uint32_t m = (lo + hi) >> 1;
+            if (tup_key(Rs[m]) <= k) lo = m + 1; else hi = m;
+        }
+        matches += (unsigned long long)(lo - lb) * (e - i);
+    }
+}
+
 // Groups g0, g0 + stride, ... (cnt of them) in order, software-pipelined
 // across groups: the next group's tables are built while the current one's
 // data is in registers, its R is gathered as soon as the current R sits in
@@ -795,6 +1064,7 @@ __device__ __forceinline__ void group_loop(const GroupArgs& A, GroupLDS<typename
     };
 
     for (uint32_t i = tid; i < GS_NB3; i += GS_THREADS) (&L.cnt[0][0])[i] = 0u;
+    if (tid == 0) L.flags = 0u;
     GroupMeta<TPL> M;
     load_meta<Src, PAIR>(A, g0, stride, cnt, 0, M, false);
     build_tables<PAIR>(A, L, M);
@@ -837,7 +1107,33 @@ __device__ __forceinline__ void group_loop(const GroupArgs& A, GroupLDS<typename
         auto gather_next_s = [&]() {
             if (nf[1] && nslot > 1) gather_group<Lay, Src>(A, L, N, 1, nn[1], vs);
         };
-        if (pair) {
+        bool cleared = false;  // sort_two zeroed the histograms itself
+        if (SMJ_GS_TWO && nslot == 2 && (pair || (cf[0] && cf[1]))) {
+            // ---- both slots in one barrier chain (sort_two).  Pair mode: a
+            // slot whose group does not fit goes in empty and is queued below
+            const bool join = !pair;
+            bool exact = false;
+            const uint32_t nr2[2] = {cf[0] ? cn[0] : 0u, cf[1] ? cn[1] : 0u};
+            const uint32_t failed = sort_two<Lay, PAIR>(A, L, C, P, nr2, co, vr, vs, join, matches,
+                                                         exact, gather_next_r, gather_next_s);
+            cleared = true;
+            if (join) {
+                if (failed) {
+                    // an exact count is already in `matches`: the skew path
+                    // only sorts the group
+                    __syncthreads();
+                    group_overflow<Src, PAIR>(A, L, C, 0, exact ? 1u : 0u);
+                } else if (!exact) {
+                    count_by_search<Lay>(A, L, C, P, cn, co, matches);
+                }
+            } else {
+                for (int q = 0; q < 2; q++)
+                    if (!cf[q] || (failed & (1u << q))) {
+                        __syncthreads();
+                        group_overflow<Src, PAIR>(A, L, C, q);
+                    }
+            }
+        } else if (pair && !SMJ_GS_TWO) {
             // ---- two groups of one relation, independently: a group that
             // does not fit or fails is queued for the skew path on its own
             bool clamped = false;
@@ -855,7 +1151,11 @@ __device__ __forceinline__ void group_loop(const GroupArgs& A, GroupLDS<typename
                 __syncthreads();
                 group_overflow<Src, PAIR>(A, L, C, 1);
             }
-        } else if (!cf[0]) {
+        } else if (!cf[0] || (SMJ_GS_TWO && SMJ_GS_PAIR)) {
+            // With sort_two and pair mode, a non-pair kernel only runs joins
+            // (nrel 2), whose groups reach here only when they do not fit:
+            // the per-slot path below is then compiled out (kept in, it
+            // pushes the join kernel past 128 VGPRs into scratch)
             group_overflow<Src, PAIR>(A, L, C);
             gather_next_r();
             gather_next_s();
@@ -884,33 +1184,14 @@ __device__ __forceinline__ void group_loop(const GroupArgs& A, GroupLDS<typename
                                    (unsigned long long)(a0 >> 16) * (a1 >> 16);
                     }
                 } else {
-                    // S is still in B; R's sorted group is in out (written above
-                    // by this workgroup: visible after the barrier)
-                    const Tup* Rs = A.out[0] + C.ost[0] + co[0];
-                    const uint32_t nR = cn[0], nS = cn[1];
-                    for (uint32_t i = tid; i < nS; i += GS_THREADS) {
-                        const int64_t k = tup_key(Lay::unpack(P, L.B[i], C.b[0]));
-                        if (i > 0 && tup_key(Lay::unpack(P, L.B[i - 1], C.b[0])) == k) continue;
-                        uint32_t e = i + 1;
-                        while (e < nS && tup_key(Lay::unpack(P, L.B[e], C.b[0])) == k) e++;
-                        uint32_t lo = 0, hi = nR;
-                        while (lo < hi) {
-                            const uint32_t m = (lo + hi) >> 1;
-                            if (tup_key(Rs[m]) < k) lo = m + 1; else hi = m;
-                        }
-                        const uint32_t lb = lo;
-                        hi = nR;
-                        while (lo < hi) {
-                            const uint32_t m = (lo + hi) >> 1;
-                            if (tup_key(Rs[m]) <= k) lo = m + 1; else hi = m;
-                        }
-                        matches += (unsigned long long)(lo - lb) * (e - i);
-                    }
+                    count_by_search<Lay>(A, L, C, P, cn, co, matches);
                 }
             }
         }
-        __syncthreads();  // histograms and B are reused by the next group
-        for (uint32_t i = tid; i < GS_NB3; i += GS_THREADS) (&L.cnt[0][0])[i] = 0u;
+        if (!cleared) {
+            __syncthreads();  // histograms and B are reused by the next group
+            for (uint32_t i = tid; i < GS_NB3; i += GS_THREADS) (&L.cnt[0][0])[i] = 0u;
+        }
         C = N;
         cn[0] = nn[0];
         cn[1] = nn[1];
