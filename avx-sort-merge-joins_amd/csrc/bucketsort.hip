@@ -568,8 +568,7 @@ __device__ __forceinline__ void build_tables(const GroupArgs& A, LDS& L,
 // 0 of its entry); otherwise both relations of the group are.
 template <class Src, bool PAIR, class LDS, class Meta>
 __device__ __forceinline__ void group_overflow(const GroupArgs& A, LDS& L,
-                                               const Meta& M, int slot = 0,
-                                               uint32_t counted = 0) {
+                                               const Meta& M, int slot = 0) {
     uint32_t nn[2] = {0, 0};
     uint64_t oo[2] = {0, 0};
     const uint32_t tid = otid();
@@ -601,7 +600,7 @@ __device__ __forceinline__ void group_overflow(const GroupArgs& A, LDS& L,
             e.nr[1] = nn[1];
             e.off[0] = oo[0];
             e.off[1] = oo[1];
-            e.counted = counted;
+            e.counted = 0;
             e.pad = 0;
             A.ovf[k] = e;
         }
@@ -895,13 +894,15 @@ __device__ __forceinline__ uint32_t sort_two(const GroupArgs& A, GroupLDS<typena
     __syncthreads();
     const uint32_t fl = __builtin_amdgcn_readfirstlane(L.flags);
     exact = join && P.s3 == 0 && !(fl & 4);
+    // the level-3 digit is the exact key: sum_k |R_k| * |S_k| over the owned
+    // bins, added once both slots are sorted (the skew path counts a queued
+    // group itself)
+    unsigned long long m = 0;
     if (exact) {
-        // the level-3 digit is the exact key: sum_k |R_k| * |S_k| over the
-        // owned bins (taken back by the caller if a slot fails)
 #pragma unroll
         for (int q = 0; q < GS_BPT / 2; q++)
-            matches += (unsigned long long)(w0[q] & 0xffffu) * (w1[q] & 0xffffu) +
-                       (unsigned long long)(w0[q] >> 16) * (w1[q] >> 16);
+            m += (unsigned long long)(w0[q] & 0xffffu) * (w1[q] & 0xffffu) +
+                 (unsigned long long)(w0[q] >> 16) * (w1[q] >> 16);
     }
     uint32_t ex0 = incl0 - loc0, ex1 = incl1 - loc1;
 #pragma unroll
@@ -1001,6 +1002,7 @@ __device__ __forceinline__ uint32_t sort_two(const GroupArgs& A, GroupLDS<typena
         L.cnt[0][tid * (GS_BPT / 2) + q] = 0u;
         L.cnt[1][tid * (GS_BPT / 2) + q] = 0u;
     }
+    if (!failed) matches += m;
     return failed;
 }
 
@@ -1119,10 +1121,8 @@ __device__ __forceinline__ void group_loop(const GroupArgs& A, GroupLDS<typename
             cleared = true;
             if (join) {
                 if (failed) {
-                    // an exact count is already in `matches`: the skew path
-                    // only sorts the group
                     __syncthreads();
-                    group_overflow<Src, PAIR>(A, L, C, 0, exact ? 1u : 0u);
+                    group_overflow<Src, PAIR>(A, L, C);
                 } else if (!exact) {
                     count_by_search<Lay>(A, L, C, P, cn, co, matches);
                 }
@@ -2074,21 +2074,25 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
         ntiles[r] = (uint32_t*)ws->scratch(names[r][6], 4);
     }
     if (nrel == 1) tt[1] = tt[0];
-    {
-        // tile numbering of both relations: two launches
+    // the relations whose tile stage this call runs, as launch slots 0..ns-1
+    int sel[2] = {0, 0}, ns = 0;
+    for (int r = 0; r < nrel; r++)
+        if (a.stage & (1u << r)) sel[ns++] = r;
+    if (ns) {
+        // tile numbering of the selected relations: two launches
         SegRel S;
-        for (int r = 0; r < 2; r++) {
-            const int rr = r < nrel ? r : 0;
-            S.seg_cnt[r] = a.seg_cnt[rr];
-            S.bcount[r] = a.bcount[rr];
-            S.bstart[r] = a.bstart[rr];
-            S.seg_start[r] = a.seg_start[rr];
-            S.ntiles[r] = ntiles[rr];
-            S.ostart[r] = ostart[rr];
-            S.tt[r] = tt[rr];
+        for (int i = 0; i < 2; i++) {
+            const int rr = sel[i < ns ? i : 0];
+            S.seg_cnt[i] = a.seg_cnt[rr];
+            S.bcount[i] = a.bcount[rr];
+            S.bstart[i] = a.bstart[rr];
+            S.seg_start[i] = a.seg_start[rr];
+            S.ntiles[i] = ntiles[rr];
+            S.ostart[i] = ostart[rr];
+            S.tt[i] = tt[rr];
         }
-        hipLaunchKernelGGL(k_seg_scan, dim3(nrel), dim3(256), 0, st, S, nb, a.nseg, tsz);
-        hipLaunchKernelGGL(k_tiles2, dim3(nb, nrel), dim3(64), 0, st, S, a.nseg, tsz);
+        hipLaunchKernelGGL(k_seg_scan, dim3(ns), dim3(256), 0, st, S, nb, a.nseg, tsz);
+        hipLaunchKernelGGL(k_tiles2, dim3(nb, ns), dim3(64), 0, st, S, a.nseg, tsz);
     }
     if (a.ev_tile) SMJ_CHECK(hipEventRecord(a.ev_tile, st));
 
@@ -2096,17 +2100,20 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
     const uint32_t ovf_cap = ngroups;
     OvfEntry* ovf = (OvfEntry*)ws->scratch("bs_ovf", (size_t)ovf_cap * sizeof(OvfEntry));
     uint32_t* novf = a.status ? a.status + 2 : (uint32_t*)ws->scratch("bs_novf", 4);
-    if (!a.status) SMJ_CHECK(hipMemsetAsync(novf, 0, 4, st));
+    if (!a.status && (a.stage & 4)) SMJ_CHECK(hipMemsetAsync(novf, 0, 4, st));
     TilePassArgs T;
     GroupArgs G;
+    for (int i = 0; i < 2; i++) {
+        const int rr = sel[i < ns ? i : 0];
+        T.part[i] = a.part[rr];
+        T.tmp[i] = a.tmp[rr];
+        T.tt[i] = tt[rr];
+        T.t0[i] = 0;
+        T.nt[i] = i < ns ? ub[rr] : 0;
+        T.ntiles[i] = ntiles[rr];
+    }
     for (int r = 0; r < 2; r++) {
         const int rr = r < nrel ? r : 0;
-        T.part[r] = a.part[rr];
-        T.tmp[r] = a.tmp[rr];
-        T.tt[r] = tt[rr];
-        T.t0[r] = 0;
-        T.nt[r] = r < nrel ? ub[r] : 0;
-        T.ntiles[r] = ntiles[rr];
         G.tmp[r] = a.tmp[rr];
         G.out[r] = a.out[rr];
         G.bstart[r] = a.bstart[rr];
@@ -2129,13 +2136,21 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
     G.ovf_cap = ovf_cap;
     G.g_begin = 0;
     G.g_end = ngroups;
-    {
-        TraceScope ts(ws, "k_tilepass", st);
-        const size_t tp_lds = TILE2 * sizeof(W) + nb2 * 4 + 64;
-        hipLaunchKernelGGL(k_tilepass<Lay>, dim3(T.nt[0] + T.nt[1]), dim3(TP_THREADS),
-                           tp_lds, st, T);
+    if (ns) {
+        {
+            TraceScope ts(ws, "k_tilepass", st);
+            const size_t tp_lds = TILE2 * sizeof(W) + nb2 * 4 + 64;
+            hipLaunchKernelGGL(k_tilepass<Lay>, dim3(T.nt[0] + T.nt[1]), dim3(TP_THREADS),
+                               tp_lds, st, T);
+        }
+        const uint32_t ubs[2] = {T.nt[0], T.nt[1]};
+        uint32_t* nts[2] = {ntiles[sel[0]], ntiles[sel[ns > 1 ? 1 : 0]]};
+        launch_preft(T.tt, ns, ubs, nts, nb2, st);
     }
-    launch_preft(tt, nrel, ub, ntiles, nb2, st);
+    if (!(a.stage & 4)) {
+        SMJ_CHECK(hipGetLastError());
+        return true;  // the group pass comes with a later call
+    }
 #ifdef SMJ_LAB_FLUSH
     {   // lab build only: evict the Infinity Cache between the tile and the
         // group pass (1 GiB of stores), to measure what its residency buys
@@ -2205,8 +2220,8 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
 #endif
         return bucket_sort_nosync<LayTup>(ws, a, st);
     }
-    if (a.packed) {
-        fprintf(stderr, "[ERROR] smj: packed bucket sort needs the host plan\n");
+    if (a.packed || a.stage != 7) {
+        fprintf(stderr, "[ERROR] smj: packed or staged bucket sorts need the host plan\n");
         abort();
     }
 

@@ -1644,7 +1644,8 @@ static void join_segmented_core(Workspace* ws, void* R, uint64_t nR, void* S, ui
                                 uint32_t bucket_bits, int64_t key_lo, int64_t key_hi,
                                 uint32_t flags, tuple_t* sortedR, tuple_t* sortedS,
                                 unsigned long long* count_dev, hipStream_t st) {
-    SMJ_CHECK(hipMemsetAsync(count_dev, 0, sizeof(unsigned long long), st));
+    if (!(flags & SMJ_SEG_STAGE_R))  // the count belongs to the group pass's call
+        SMJ_CHECK(hipMemsetAsync(count_dev, 0, sizeof(unsigned long long), st));
     uint32_t D1, D2, D2cap;
     choose_levels(nR > nS ? nR : nS, bucket_bits, &D1, &D2, &D2cap);
     // the buckets are the exchanged partitions: level 1 is fixed
@@ -1705,6 +1706,13 @@ static void join_segmented_core(Workspace* ws, void* R, uint64_t nR, void* S, ui
     a.host_plan = &hplan;
     a.packed = packed;  // checked packable before the exchange: no pack_bad here
     a.digit_fast = packed;  // packed words never lie outside the plan
+    if ((flags & SMJ_SEG_STAGE_R) && (flags & SMJ_SEG_STAGE_REST)) {
+        fprintf(stderr, "[ERROR] smj_dev_join_segmented: SMJ_SEG_STAGE_R and _REST are two "
+                "calls\n");
+        abort();
+    }
+    if (flags & SMJ_SEG_STAGE_R) a.stage = 1;          // R's tile stage only
+    else if (flags & SMJ_SEG_STAGE_REST) a.stage = 6;  // S's tile stage + group pass
     if (!bucket_sort(ws, a, st)) {
         fprintf(stderr, "[ERROR] smj_dev_join_segmented: unexpected partition flag\n");
         abort();

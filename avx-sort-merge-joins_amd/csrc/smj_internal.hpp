@@ -338,6 +338,12 @@ struct BucketSortArgs {
     // join turns it off for tuples (a caller's key outside its range could sit
     // in the last non-empty bucket instead)
     bool digit_fast = true;
+    // which stages run (bucket_sort_nosync; segmented joins): bit r = the
+    // tile stage (tile numbering, tile pass, prefix table) of relation r,
+    // bit 2 = the group pass and the one synchronisation.  A later call runs
+    // the stages an earlier one left out, with the same arguments: the
+    // multi-GPU join sorts R's tiles while S's rows are still in flight.
+    uint32_t stage = 7;
     hipEvent_t ev_tile = nullptr;   // optional phase markers
     hipEvent_t ev_bucket = nullptr;
     hipEvent_t ev_ovf = nullptr;

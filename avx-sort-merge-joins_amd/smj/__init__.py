@@ -490,17 +490,21 @@ class Library:
             self.stream_ptr())
 
     def dev_join_segmented_tables(self, R, nR, startR, cntR, S, nS, startS, cntS, bucket_bits,
-                                  key_lo, key_hi, sortedR, sortedS, count, packed=False):
+                                  key_lo, key_hi, sortedR, sortedS, count, packed=False,
+                                  stage=None):
         """smj_dev_join_segmented from explicit segment tables: start/cnt are
         int64 (2^bucket_bits, nseg) device tensors (element offsets into R /
-        S and counts); nR / nS count the elements inside the segments."""
+        S and counts); nR / nS count the elements inside the segments.
+        stage: None (the whole join), "R" (R's tile stage only) or "REST" (the
+        rest, after a "R" call with the same arguments)."""
         for t in (startR, cntR, startS, cntS):
             assert t.is_contiguous() and t.shape == startR.shape
         assert startR.shape[0] == 1 << bucket_bits
+        flags = (1 if packed else 0) | {None: 0, "R": 2, "REST": 4}[stage]
         self.lib.smj_dev_join_segmented_tables(
             self.ws, R.data_ptr(), nR, startR.data_ptr(), cntR.data_ptr(), S.data_ptr(), nS,
             startS.data_ptr(), cntS.data_ptr(), startR.shape[1], bucket_bits, key_lo, key_hi,
-            1 if packed else 0, sortedR.data_ptr(), sortedS.data_ptr(), count.data_ptr(),
+            flags, sortedR.data_ptr(), sortedS.data_ptr(), count.data_ptr(),
             self.stream_ptr())
 
     def sampled_capacity(self, n, nbits):

@@ -233,10 +233,10 @@ class DeviceOps:
                                                     seg_start, seg_cnt, flags)
 
     def join_segmented_tables(self, R, nR, startR, cntR, S, nS, startS, cntS, bucket_bits,
-                              key_lo, key_hi, sR, sS, count, packed=False):
+                              key_lo, key_hi, sR, sS, count, packed=False, stage=None):
         self.lib.dev_join_segmented_tables(R, nR, startR, cntR, S, nS, startS, cntS,
                                            bucket_bits, key_lo, key_hi, sR, sS, count,
-                                           packed=packed)
+                                           packed=packed, stage=stage)
 
     def xsend(self, start, cnt, flags, world, msg, chunk):
         self.lib.dev_xsend(start, cnt, flags, world, msg, chunk)
@@ -275,6 +275,14 @@ class DistributedJoin:
         # partition takes
         self.shards = ops.shards() if hasattr(ops, "shards") else 1
         self.buf = {}
+        # the local join in two calls overlapping S's rows (SMJ_XSTAGED=0: one)
+        self.staged = os.environ.get("SMJ_XSTAGED", "1") != "0"
+        # the rows travel on a communicator of their own: its stream is not
+        # ordered behind the table exchange of S (queued behind S's partition)
+        self.row_group = None
+        if self.world > 1:
+            ranks = [self._global(g) for g in range(self.world)]
+            self.row_group = dist.new_group(ranks=ranks)
         self.recv_hint = {}  # remote rows received per relation and layout (sticky)
         self.last_recv = {}
         self.last_rows = {}
@@ -439,15 +447,29 @@ class DistributedJoin:
         remote = sum(rl) - rl[me]
         self.recv_hint[xkey] = max(remote, self.recv_hint.get(xkey, 0))
         xb = self._xbuf(xkey, cap + remote, st["packed"], keep=cap)
+        grown = xb is not st["xb"]
         row = 8 if st["packed"] else xb.element_size() * (xb.shape[1] if xb.dim() > 1 else 1)
         self.stats["sent_B"] += row * (sum(sl) - sl[me])
         self.stats["recv_B"] += row * remote
         self.stats["gap_B"] += row * (sum(rl) - sum(ru))
         ev = None
-        if key == "S" and xb.is_cuda:
-            ev = torch.cuda.Event(enable_timing=True)
-            ev.record()
-        work = self._rows(xb, cap, cs, sl, rl, gmax)
+        if xb.is_cuda:
+            # the rows are issued from a stream that waits only for this
+            # attempt (partition, tables, summary), not for work queued after
+            # it (the other relation's partition); a grown buffer's copy of
+            # the partition is on the current stream
+            rs = self._row_stream()
+            if grown:
+                rs.wait_stream(torch.cuda.current_stream())
+            else:
+                rs.wait_event(st["ev"])
+            with torch.cuda.stream(rs):
+                if key == "S":
+                    ev = torch.cuda.Event(enable_timing=True)
+                    ev.record()
+                work = self._rows(xb, cap, cs, sl, rl, gmax)
+        else:
+            work = self._rows(xb, cap, cs, sl, rl, gmax)
         self.last_recv[key] = (sl, rl)
         self.last_rows[key] = (xb, cap, cs, sl, rl, gmax)  # bench.py --op exchange repeats it
         self._ev_issue = ev
@@ -479,7 +501,7 @@ class DistributedJoin:
         for g in range(G):
             roff.append(ro)
             ro += 0 if g == me else rl[g]
-        if xb.is_cuda and dist.get_backend(self.group) == "nccl":
+        if xb.is_cuda and dist.get_backend(self._rgroup()) == "nccl":
             if gmax is None:
                 raise ValueError("the RCCL row exchange needs the global message maximum")
             rounds = -(-gmax // step)
@@ -493,7 +515,7 @@ class DistributedJoin:
                     return xb[start + lo:start + min(lo + step, n)]
                 ins = [piece(cs[g], sl[g], g) for g in range(G)]
                 outs = [piece(roff[g], rl[g], g) for g in range(G)]
-                works.append(dist.all_to_all(outs, ins, group=self.group, async_op=True))
+                works.append(dist.all_to_all(outs, ins, group=self._rgroup(), async_op=True))
             return _Works(works)
         ops = []
         for g in range(G):
@@ -502,57 +524,88 @@ class DistributedJoin:
             peer = self._global(g)
             for k in range(0, sl[g], step):
                 ops.append(dist.P2POp(dist.isend, xb[cs[g] + k:cs[g] + min(k + step, sl[g])],
-                                      peer, group=self.group))
+                                      peer, group=self._rgroup()))
             for k in range(0, rl[g], step):
                 ops.append(dist.P2POp(dist.irecv, xb[roff[g] + k:roff[g] + min(k + step, rl[g])],
-                                      peer, group=self.group))
+                                      peer, group=self._rgroup()))
         return _Works(dist.batch_isend_irecv(ops) if ops else [])
 
     def _global(self, g):
         return g if self.group is None else dist.get_global_rank(self.group, g)
 
+    def _rgroup(self):
+        return self.row_group if self.row_group is not None else self.group
+
+    def _row_stream(self):
+        s = self.buf.get("_rows")
+        if s is None:
+            s = self.buf["_rows"] = torch.cuda.Stream()
+        return s
+
     def step(self, R, S, count):
-        if self.world > 1:
-            # the row exchange of R overlaps the partition of S
-            rR, tR, cR, nR, wR, pR = self._exchange(R, "R")
-            rS, tS, cS, nS, wS, pS = self._exchange(S, "S")
-        else:
-            # one rank: no rows travel, so both partitions are queued before
-            # the one wait for their summaries
-            packed = bool(getattr(self.ops, "can_pack", False))
-            aR = self._attempt(R, "R", packed, self.sampled)
-            aS = self._attempt(S, "S", packed, self.sampled)
-            if aR is None:
-                aR = self._attempt(R, "R", False, self.sampled)
-            if aS is None:
-                aS = self._attempt(S, "S", False, self.sampled)
-            rR, tR, cR, nR, wR, pR = self._finish(R, aR)
-            rS, tS, cS, nS, wS, pS = self._finish(S, aS)
+        """One join step.  Both relations' attempts (partition, table
+        exchange, summary copy) are queued before the first host wait, so the
+        device partitions S while the host reads R's summary; R's rows then
+        leave at once (their own stream and communicator, ordered only after
+        R's attempt, so they overlap S's partition), S's rows after S's
+        summary.  The local join runs in two calls: R's tile stage as soon as
+        R's rows are in (overlapping S's rows in flight), then S's tile stage,
+        the group pass and the count (smj_dev_join_segmented_tables,
+        SMJ_SEG_STAGE_R / _REST).  One rank: no rows travel, one call."""
+        packed = bool(getattr(self.ops, "can_pack", False))
+        aR = self._attempt(R, "R", packed, self.sampled)
+        if aR is None:
+            aR = self._attempt(R, "R", False, self.sampled)
+        aS = self._attempt(S, "S", packed, self.sampled)
+        if aS is None:
+            aS = self._attempt(S, "S", False, self.sampled)
+        rR, tR, cR, nR, wR, pR = self._finish(R, aR)
+        rS, tS, cS, nS, wS, pS = self._finish(S, aS)
         eS = self._ev_issue
-        wR.wait()
-        wS.wait()
-        if eS is not None:
-            e1 = torch.cuda.Event(enable_timing=True)
-            e1.record()
-            self._ev.append((eS, e1))
-        self.stats["steps"] += 1
         # both relations must reach the local join in one layout: the one
         # that went out packed is exchanged again as tuples
         if pR and not pS:
-            rR, tR, cR, nR, wR, pR = self._exchange(R, "R", allow_pack=False)
             wR.wait()
+            rR, tR, cR, nR, wR, pR = self._exchange(R, "R", allow_pack=False)
         elif pS and not pR:
-            rS, tS, cS, nS, wS, pS = self._exchange(S, "S", allow_pack=False)
             wS.wait()
+            rS, tS, cS, nS, wS, pS = self._exchange(S, "S", allow_pack=False)
+            eS = self._ev_issue
         assert pR == pS
         self.last_packed = pR
+        if eS is not None:
+            # S's row exchange alone: its completion on a stream of its own
+            # (the compute stream runs R's tile stage meanwhile)
+            side = self._side_stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                wS.wait()
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record()
+            self._ev.append((eS, e1))
+        self.stats["steps"] += 1
         sR = self._grow("sortR", nR)
         sS = self._grow("sortS", nS)
-        self.ops.join_segmented_tables(rR, nR, tR, cR, rS, nS, tS, cS, self.lbits,
-                                       self.key_lo, self.key_hi, sR, sS, count, packed=pR)
+        args = (rR, nR, tR, cR, rS, nS, tS, cS, self.lbits, self.key_lo, self.key_hi, sR, sS,
+                count)
+        if self.world > 1 and self.staged:
+            wR.wait()
+            self.ops.join_segmented_tables(*args, packed=pR, stage="R")
+            wS.wait()
+            self.ops.join_segmented_tables(*args, packed=pR, stage="REST")
+        else:
+            wR.wait()
+            wS.wait()
+            self.ops.join_segmented_tables(*args, packed=pR)
         if self.world > 1:
             dist.all_reduce(count, group=self.group)
         return sR, sS
+
+    def _side_stream(self):
+        s = self.buf.get("_side")
+        if s is None:
+            s = self.buf["_side"] = torch.cuda.Stream()
+        return s
 
     def stats_read(self):
         """The statistics with S's exchange time summed (synchronises)."""

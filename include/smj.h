@@ -537,6 +537,14 @@ int smj_dev_partition_range_packed(smj_workspace * ws, const tuple_t * in, uint6
  * scratch (overwritten).  sortedR/sortedS receive the sorted relations as
  * tuples, count_dev the number of matching pairs. */
 #define SMJ_SEG_PACKED 1u
+/* Stages of one local join split over two calls with the same arguments
+ * (the multi-GPU join overlaps them with the row exchange): a call with
+ * SMJ_SEG_STAGE_R sorts only R's tiles (its tile pass: R must be complete,
+ * S need not have arrived); the next call with SMJ_SEG_STAGE_REST sorts S's
+ * tiles and runs the group pass and the count.  Neither flag: the whole join
+ * in one call. */
+#define SMJ_SEG_STAGE_R 2u
+#define SMJ_SEG_STAGE_REST 4u
 void smj_dev_join_segmented(smj_workspace * ws, void * R, uint64_t nR,
                             const int64_t * segR, void * S, uint64_t nS,
                             const int64_t * segS, uint32_t nseg,

@@ -78,9 +78,20 @@ class HostOps:
         return True
 
     def join_segmented_tables(self, R, nR, startR, cntR, S, nS, startS, cntS, bucket_bits,
-                              key_lo, key_hi, sR, sS, count, packed=False):
+                              key_lo, key_hi, sR, sS, count, packed=False, stage=None):
         """Gather every bucket's segments (bucket-major) and join the dense
-        relations with the checks of join_segmented."""
+        relations with the checks of join_segmented.  The staged form (the
+        device sorts R's tiles first): a "R" call must precede the "REST" call
+        of the same step, with the same tables; the join happens at "REST"."""
+        if stage == "R":
+            self.staged_r = (R.data_ptr(), startR.data_ptr(), nR)
+            self.stage_calls = getattr(self, "stage_calls", 0) + 1
+            return
+        if stage == "REST":
+            assert getattr(self, "staged_r", None) == (R.data_ptr(), startR.data_ptr(), nR)
+            self.staged_r = None
+        else:
+            self.whole_calls = getattr(self, "whole_calls", 0) + 1
         dense = []
         for X, n, st, ct in ((R, nR, startR, cntR), (S, nS, startS, cntS)):
             assert st.shape == ct.shape and st.shape[0] == 1 << bucket_bits
@@ -210,6 +221,13 @@ def _worker(rank, world, port, n, q, s_payload="negative", mode="sampled"):
             sR, sS = dj.step(rows(R), rows(S), count)
             assert int(count.item()) == expect
             assert dj.last_packed == (s_payload == "rowid")
+        # the local join: two calls per step (R's tile stage while S's rows
+        # fly, then the rest) across ranks unless SMJ_XSTAGED=0, one call on
+        # one rank
+        if world > 1 and os.environ.get("SMJ_XSTAGED", "1") != "0":
+            assert getattr(ops, "stage_calls", 0) == 2 and getattr(ops, "whole_calls", 0) == 0
+        else:
+            assert getattr(ops, "whole_calls", 0) == 2 and getattr(ops, "stage_calls", 0) == 0
         # every key this rank sorted is in its contiguous share of the range
         own = owners(dj.fanout, world)
         for got in (sR, sS):
@@ -257,7 +275,8 @@ def _free_port():
     (2, None, "r_negative", "sampled"), (3, None, "r_negative", "sampled"),
     (2, None, "rowid", "exact"), (3, None, "negative", "exact"),
     (3, None, "rowid", "mixed"), (2, None, "negative", "mixed"),
-    (3, None, "rowid", "overflow")])
+    (3, None, "rowid", "overflow"), (2, None, "rowid", "sampled-onecall"),
+    (3, None, "negative", "exact-onecall")])
 def test_distributed_join_gloo(world, chunk_mb, s_payload, mode, oracles, monkeypatch):
     """chunk_mb 0: every row message over the chunk limit, so the exchange
     takes the chunked isend/irecv path (the one RCCL needs for >1 GiB).
@@ -268,6 +287,9 @@ def test_distributed_join_gloo(world, chunk_mb, s_payload, mode, oracles, monkey
     R cannot be packed but S can (S goes again, as tuples)."""
     if chunk_mb is not None:
         monkeypatch.setenv("SMJ_A2A_CHUNK_MB", str(chunk_mb))
+    if mode.endswith("-onecall"):  # the local join in one call (no staging)
+        monkeypatch.setenv("SMJ_XSTAGED", "0")
+        mode = mode[:-len("-onecall")]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

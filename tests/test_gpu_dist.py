@@ -38,6 +38,8 @@ def test_segmented_join_simulated_exchange(libs, oracles, width, world, kind, pa
     orc, lib = oracles[width], libs[width]
     if packed and width != 16:
         pytest.skip("packed words are the 16-byte layout")
+    if staged and world == 1:
+        pytest.skip("one rank: nothing in flight, the join is one call")
     n = 600_000
     R, S = _inputs(orc, kind, n)
     total, _, _ = orc.sortmergejoin(R, S)
@@ -101,17 +103,23 @@ def test_segmented_join_simulated_exchange(libs, oracles, width, world, kind, pa
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
 @pytest.mark.parametrize("kind", ["pk_fk", "zipf"])
 @pytest.mark.parametrize("packed", [False, True])
-def test_sampled_exchange_simulated(libs, oracles, width, world, kind, packed):
+@pytest.mark.parametrize("staged", [False, True], ids=["onecall", "staged"])
+def test_sampled_exchange_simulated(libs, oracles, width, world, kind, packed, staged):
     """The sampled exchange partition (smj_dev_partition_range_sampled: K shard
     regions per partition, slack between them) simulated on one GPU: rank g
     receives from every source the chunk [start of its first owned region,
     start of the next rank's first region) -- gaps included -- and joins it
-    through smj_dev_join_segmented_tables with the sources' region tables."""
+    through smj_dev_join_segmented_tables with the sources' region tables.
+    staged: the join in two calls (SMJ_SEG_STAGE_R, then _REST), S's receive
+    buffer holding garbage during the first (the multi-GPU join runs R's tile
+    stage while S's rows are still in flight)."""
     import torch
     from smj.dist import ceil_log2, owned, plan_shift
     orc, lib = oracles[width], libs[width]
     if packed and width != 16:
         pytest.skip("packed words are the 16-byte layout")
+    if staged and world == 1:
+        pytest.skip("one rank: nothing in flight, the join is one call")
     n = 600_000
     R, S = _inputs(orc, kind, n)
     total, _, _ = orc.sortmergejoin(R, S)
@@ -167,9 +175,17 @@ def test_sampled_exchange_simulated(libs, oracles, width, world, kind, packed):
             used[key] = nused
         sR, sS = lib.empty(used["R"]), lib.empty(used["S"])
         cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
-        lib.dev_join_segmented_tables(recv["R"], used["R"], *tabs["R"], recv["S"], used["S"],
-                                      *tabs["S"], lbits, key_lo, key_hi, sR, sS, cnt,
-                                      packed=packed)
+        args = (recv["R"], used["R"], *tabs["R"], recv["S"], used["S"], *tabs["S"], lbits,
+                key_lo, key_hi, sR, sS, cnt)
+        if staged:
+            s_rows = recv["S"].clone()
+            recv["S"].fill_(-3)  # S has not arrived yet
+            lib.dev_join_segmented_tables(*args, packed=packed, stage="R")
+            torch.cuda.synchronize()
+            recv["S"].copy_(s_rows)
+            lib.dev_join_segmented_tables(*args, packed=packed, stage="REST")
+        else:
+            lib.dev_join_segmented_tables(*args, packed=packed)
         torch.cuda.synchronize()
         lo_k, hi_k = 1 + (p_lo << s1), 1 + (p_hi << s1)
         mR = R[(R["key"] >= lo_k) & (R["key"] < hi_k)] if g < world - 1 else R[R["key"] >= lo_k]
