@@ -38,8 +38,6 @@ def test_segmented_join_simulated_exchange(libs, oracles, width, world, kind, pa
     orc, lib = oracles[width], libs[width]
     if packed and width != 16:
         pytest.skip("packed words are the 16-byte layout")
-    if staged and world == 1:
-        pytest.skip("one rank: nothing in flight, the join is one call")
     n = 600_000
     R, S = _inputs(orc, kind, n)
     total, _, _ = orc.sortmergejoin(R, S)
