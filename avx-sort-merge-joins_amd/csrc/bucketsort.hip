@@ -166,6 +166,7 @@ struct TilePassArgs {
     uint32_t nb2;
     const unsigned int* pack_bad;  // set: the packed partition is void, exit
     uint32_t d2_fast;              // Lay::fast_ok for the level-2 digit (host)
+    uint64_t pstride[2] = {0, 0};  // plane stride of part/tmp (LayP48)
 };
 
 template <class Lay>
@@ -184,8 +185,8 @@ k_tilepass(TilePassArgs A) {
     const uint32_t t = A.t0[r] + (r ? blockIdx.x - A.nt[0] : blockIdx.x);
     if (A.ntiles[r] && t >= *A.ntiles[r]) return;
     const TileTable& tt = A.tt[r];
-    const W* __restrict__ part = static_cast<const W*>(A.part[r]);
-    W* __restrict__ tmp = static_cast<W*>(A.tmp[r]);
+    const typename Lay::CView part = Lay::cview(A.part[r], A.pstride[r]);
+    const typename Lay::View tmp = Lay::view(A.tmp[r], A.pstride[r]);
     const uint64_t off = tt.off[t];
     const uint32_t len = tt.len[t];
     const uint32_t b = tt.bucket[t];
@@ -307,6 +308,7 @@ struct GroupArgs {
     uint32_t ovf_cap;
     const unsigned int* pack_bad;  // set: the packed partition is void, exit
     uint32_t d3_fast;              // Lay::fast_ok for the level-3 digit (host)
+    uint64_t pstride[2] = {0, 0};  // plane stride of tmp (LayP48)
     // one relation (nrel == 1): two groups per loop iteration, one in each
     // relation slot (the slots' tables alias relation 0), so that a group's
     // gather flies under the other slot's sort as in the join
@@ -355,8 +357,8 @@ struct SrcPlain {
         lo = pf[0];
         len = (uint32_t)(pf[tt.tstride] - pf[0]);
     }
-    template <class W>
-    __device__ static __forceinline__ W load(const W* p) { return *p; }
+    template <class V>
+    __device__ static __forceinline__ auto load(const V& p) { return p[0]; }
 };
 
 // A group and, for the calling thread, its tile run: wave r < nslot owns
@@ -618,7 +620,7 @@ __device__ __forceinline__ void gather_group(const GroupArgs& A, GroupLDS<typena
                                              const Meta& C, int r, uint32_t n,
                                              typename Lay::W (&v)[GS_ITEMS]) {
     if (n == 0) return;
-    const typename Lay::W* tp = static_cast<const typename Lay::W*>(A.tmp[r]) + C.bst[r];
+    const typename Lay::CView tp = Lay::cview(A.tmp[r], A.pstride[r]) + C.bst[r];
     const uint32_t lane = lane_id();
     const uint32_t wid = __builtin_amdgcn_readfirstlane(otid() >> 6);
 #pragma unroll
@@ -1281,13 +1283,13 @@ struct SkewArgs {
 
 // tile t of group (b, g) in relation r: run [src, src + len)
 template <class Lay>
-__device__ __forceinline__ const typename Lay::W* skew_run(const GroupArgs& G, int r, uint32_t g,
-                                                         uint32_t t0, uint32_t t, uint32_t& len) {
+__device__ __forceinline__ typename Lay::CView skew_run(const GroupArgs& G, int r, uint32_t g,
+                                                      uint32_t t0, uint32_t t, uint32_t& len) {
     const TileTable& tt = G.tt[r];
     const uint16_t* pf = tt.prefT + (uint64_t)g * tt.tstride + t0 + t;
     const uint32_t lo = pf[0];
     len = (uint32_t)(pf[tt.tstride] - lo);
-    return static_cast<const typename Lay::W*>(G.tmp[r]) + tt.off[t0 + t] + lo;
+    return Lay::cview(G.tmp[r], G.pstride[r]) + (tt.off[t0 + t] + lo);
 }
 
 constexpr uint32_t SK_WIN = kSkewSmall / 64;  // 64-position windows of a small group
@@ -1317,7 +1319,7 @@ __device__ __forceinline__ void skew_for_each(const GroupArgs& G, const SkewSmal
                                               F&& f) {
     typedef typename Lay::W W;
     if (nt <= SK_TM) {
-        const W* tmp = static_cast<const W*>(G.tmp[r]);
+        const typename Lay::CView tmp = Lay::cview(G.tmp[r], G.pstride[r]);
         const uint32_t lane = lane_id();
         const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         for (uint32_t c = 0; c < n; c += SK_CHUNK) {
@@ -1345,7 +1347,7 @@ __device__ __forceinline__ void skew_for_each(const GroupArgs& G, const SkewSmal
     } else {
         for (uint32_t t = 0; t < nt; t++) {
             uint32_t len;
-            const W* src = skew_run<Lay>(G, r, g, t0, t, len);
+            const typename Lay::CView src = skew_run<Lay>(G, r, g, t0, t, len);
             for (uint32_t i0 = 0; i0 < len; i0 += SK_THREADS) {
                 const uint32_t i = i0 + threadIdx.x;
                 f(src[i < len ? i : len - 1], i < len);
@@ -1438,7 +1440,7 @@ k_skew_small(SkewArgs K) {
             uint32_t pos = 0;
             for (uint32_t t = 0; t < nt[r]; t++) {
                 uint32_t len;
-                const W* src = skew_run<Lay>(G, r, e.d2, t0[r], t, len);
+                const typename Lay::CView src = skew_run<Lay>(G, r, e.d2, t0[r], t, len);
                 for (uint32_t i = tid; i < len; i += SK_THREADS)
                     dst[pos + i] = Lay::unpack(P, src[i], e.bucket);
                 pos += len;
@@ -1518,7 +1520,7 @@ k_skew_hist(SkewArgs K) {
     bool clamped = false;
     for (uint32_t t = s; t < nt; t += ts) {
         uint32_t len;
-        const W* src = skew_run<Lay>(G, (int)r, e.d2, t0, t, len);
+        const typename Lay::CView src = skew_run<Lay>(G, (int)r, e.d2, t0, t, len);
         for (uint32_t c = 0; c < len; c += SK_CHUNK) {
             W v[SK_ITEMS];
 #pragma unroll
@@ -1606,7 +1608,7 @@ k_skew_place(SkewArgs K) {
             unsigned long long pos;
             (void)block_scan64(acc, scr, &pos);
             uint32_t len;
-            const W* src = skew_run<Lay>(G, (int)r, e.d2, t0, t, len);
+            const typename Lay::CView src = skew_run<Lay>(G, (int)r, e.d2, t0, t, len);
             for (uint32_t i = threadIdx.x; i < len; i += SK_THREADS)
                 dst[pos + i] = Lay::unpack(P, src[i], e.bucket);
         }
@@ -1616,7 +1618,7 @@ k_skew_place(SkewArgs K) {
     uint32_t* gcur = K.ghist + ((size_t)sl * 2 + r) * GS_NB3;
     for (uint32_t t = s; t < nt; t += ts) {
         uint32_t len;
-        const W* src = skew_run<Lay>(G, (int)r, e.d2, t0, t, len);
+        const typename Lay::CView src = skew_run<Lay>(G, (int)r, e.d2, t0, t, len);
         for (uint32_t c = 0; c < len; c += SK_CHUNK) {
             for (uint32_t d = threadIdx.x; d < GS_NB3; d += SK_THREADS) h[d] = 0;
             W v[SK_ITEMS];
@@ -2107,6 +2109,7 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
         const int rr = sel[i < ns ? i : 0];
         T.part[i] = a.part[rr];
         T.tmp[i] = a.tmp[rr];
+        T.pstride[i] = a.pstride[rr];
         T.tt[i] = tt[rr];
         T.t0[i] = 0;
         T.nt[i] = i < ns ? ub[rr] : 0;
@@ -2115,6 +2118,7 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
     for (int r = 0; r < 2; r++) {
         const int rr = r < nrel ? r : 0;
         G.tmp[r] = a.tmp[rr];
+        G.pstride[r] = a.pstride[rr];
         G.out[r] = a.out[rr];
         G.bstart[r] = a.bstart[rr];
         G.ostart[r] = ostart[rr];
@@ -2216,6 +2220,7 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
     set_pass_attrs<LayTup>();
     if (a.host_plan && a.seg_start[0] && a.part_flag) {
 #ifdef KEY_8B
+        if (a.p48) return bucket_sort_nosync<LayP48>(ws, a, st);
         if (a.packed) return bucket_sort_nosync<LayPacked>(ws, a, st);
 #endif
         return bucket_sort_nosync<LayTup>(ws, a, st);

@@ -304,6 +304,17 @@ static bool use_packing() {
     return v != 0;
 }
 
+// ... and 48-bit words in two planes first (LayP48) when every payload fits
+// 48 - s1 bits; SMJ_P48=0 starts from 64-bit words
+static bool use_p48() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("SMJ_P48");
+        v = e ? atoi(e) : 1;
+    }
+    return v != 0;
+}
+
 // Sort of one relation (nrel 1) or sort + merge-join count of two (nrel 2):
 // range plan -> sampled level-1 partition -> tile pass -> group pass.  The
 // plan must be known on the host (no mid-pipeline synchronisation, and 16-byte
@@ -369,24 +380,56 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
     unsigned int* sample = (unsigned int*)ws->scratch("sp_sample", (size_t)nrel * nb * 4);
     unsigned long long* cnt = count_dev
         ? count_dev : (unsigned long long*)ws->scratch("sort_cnt", 8);
-    // attempts: sampled + packed words, sampled tuples, exact tuples; a later
-    // one runs only when the one before reported a region overflow or an
-    // unpackable tuple (its tile and group passes then did nothing or are
-    // discarded: the count restarts from 0).  A guessed plan that a key falls
-    // outside of is replaced by the exact one and the attempts restart.
-    int mode = can_pack ? 0 : (sampled ? 1 : 2);
+    // attempts: sampled + 48-bit words (-1), sampled + packed words (0),
+    // sampled tuples (1), exact tuples (2); a later one runs only when the one
+    // before reported a region overflow or an unpackable tuple (its tile and
+    // group passes then did nothing or are discarded: the count restarts from
+    // 0).  A payload too wide for 48 bits but not for 64 goes from -1 to 0.  A
+    // guessed plan that a key falls outside of is replaced by the exact one
+    // and the attempts restart.  The 48-bit scatter's carries (128 bytes a
+    // partition) fit LDS up to 512 partitions.
+    auto first_mode = [&]() {
+#ifdef KEY_8B
+        if (can_pack && use_p48() && nb <= 512) return -1;
+#endif
+        return can_pack ? 0 : (sampled ? 1 : 2);
+    };
+    int mode = first_mode();
     while (mode <= 2) {
-        const bool packed = mode == 0;
+        const bool p48 = mode == -1;
+        const bool packed = mode <= 0;
         // the status word the tile and group passes exit on (sampled modes)
         const bool check = packed || (guessed && mode == 1);
         hipLaunchKernelGGL(k_join_begin, dim3(1), dim3(256), 0, st, plan, hplan,
                            plan_on_host ? 1 : 0, cnt, status, sample,
                            mode < 2 ? (uint32_t)nrel * nb : 0u);
+        // LayP48's plane stride: the partition buffer's capacity in elements,
+        // rounded to 32 (the hi plane starts 16-byte aligned); the buffer
+        // holds 16 bytes an element, the planes take 6
+        uint64_t pstride[2] = {0, 0};
+        for (int r = 0; r < nrel && p48; r++)
+            pstride[r] = (sampled_capacity(ns[r], D1) + 31) & ~31ull;
         if (mode < 2) {
             void* outs_v[2] = {part[0], part[nrel > 1 ? 1 : 0]};
-            sampled_partition(ws, nrel, rels, ns, outs_v, plan, D1, sample, bst, bh, sgs, sgc,
-                              status, st, plan_on_host ? &hplan : nullptr, packed,
-                              check ? status + 1 : nullptr);
+            if (p48 && nrel > 1 && pstride[0] != pstride[1]) {
+                // one stride per launch: the two relations take turns
+                for (int r = 0; r < nrel; r++) {
+                    const Tup* rr1[1] = {rels[r]};
+                    const uint64_t nn1[1] = {ns[r]};
+                    void* oo1[1] = {part[r]};
+                    uint64_t* bs1[1] = {bst[r]};
+                    int64_t* bh1[1] = {bh[r]};
+                    uint64_t* sgs1[1] = {sgs[r]};
+                    int64_t* sgc1[1] = {sgc[r]};
+                    sampled_partition(ws, 1, rr1, nn1, oo1, plan, D1, sample + (size_t)r * nb,
+                                      bs1, bh1, sgs1, sgc1, status, st, &hplan, true,
+                                      status + 1, pstride[r]);
+                }
+            } else {
+                sampled_partition(ws, nrel, rels, ns, outs_v, plan, D1, sample, bst, bh, sgs,
+                                  sgc, status, st, plan_on_host ? &hplan : nullptr, packed,
+                                  check ? status + 1 : nullptr, pstride[0]);
+            }
         } else {
             for (int r = 0; r < nrel; r++)
                 plan_partition(ws, rels[r], ns[r], part[r], plan, D1, bst[r], bh[r], st);
@@ -414,12 +457,21 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
         a.ev_ovf = ws->ev[3];
         a.host_plan = plan_on_host ? &hplan : nullptr;
         a.packed = packed;
+        a.p48 = p48;
+        a.pstride[0] = pstride[0];
+        a.pstride[1] = pstride[1];
         a.pack_bad = check ? status + 1 : nullptr;
         a.status = status;
         if (mode < 2) a.part_flag = status;
         uint32_t why[2] = {0, 0};
         a.status_out = why;
         if (bucket_sort(ws, a, st)) break;
+        if (mode == -1 && !(guessed && (why[1] & kBadRange))) {
+            // payloads too wide for 48 bits only: 64-bit words; anything else
+            // (overflow, unpackable) as from 64-bit words
+            mode = (why[1] & kBadPayload48) && !(why[1] & kBadPayload) && !why[0] ? 0 : 1;
+            continue;
+        }
         if (guessed && (why[1] & kBadRange)) {
             // a key outside 1..size_guess: the exact plan, attempts from the top
             guessed = false;
@@ -431,7 +483,7 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
 #ifdef KEY_8B
             can_pack = sampled && plan_on_host && use_packing() && LayPacked::usable(hplan);
 #endif
-            mode = can_pack ? 0 : (sampled ? 1 : 2);
+            mode = first_mode();
             continue;
         }
         mode++;

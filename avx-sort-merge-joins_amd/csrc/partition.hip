@@ -1326,9 +1326,11 @@ k_regions_done(RegionRel R, uint32_t nbins, unsigned int* __restrict__ flag) {
 
 // lanes of the scatter write whole 64-byte segments: the complete segments
 // of a tile are numbered, segown[s] = the partition of segment s
-template <int THREADS, int ITEMS, class OutT>
+// (SB: bytes an element takes in the output's first plane: the segment is
+// kSegBytes of that plane; one plane for every layout but LayP48)
+template <int THREADS, int ITEMS, class OutT, uint32_t SB = sizeof(OutT)>
 struct ScatterGeom {
-    static constexpr uint32_t SEG = kSegBytes / sizeof(OutT);  // elements per segment
+    static constexpr uint32_t SEG = kSegBytes / SB;  // elements per segment
     static constexpr uint32_t TILE = THREADS * ITEMS;
     static __host__ __device__ constexpr uint32_t max_segs(uint32_t nbins) {
         return (TILE + nbins * (SEG - 1)) / SEG;
@@ -1336,7 +1338,7 @@ struct ScatterGeom {
     // stage OutT[TILE] | carry OutT[nbins * SEG] | pos u64[nbins] |
     // tstart, tfill, kc, segpre u32[nbins] | segown u16[max_segs] | scan scratch
     static __host__ __device__ constexpr size_t lds_bytes(uint32_t nbins) {
-        return (size_t)TILE * sizeof(OutT) + (size_t)nbins * kSegBytes +
+        return (size_t)TILE * sizeof(OutT) + (size_t)nbins * SEG * sizeof(OutT) +
                (size_t)nbins * (8 + 4 * 4) + ((size_t)max_segs(nbins) * 2 + 15) / 16 * 16 +
                (THREADS / 64 + 1) * 4;
     }
@@ -1350,10 +1352,10 @@ __global__ void __launch_bounds__(THREADS)
 k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_arg,
               uint32_t nbins, unsigned long long* __restrict__ cursor_all,
               const uint64_t* __restrict__ cap_end_all,
-              typename Pack::OutT* __restrict__ out, Pack pk,
+              void* __restrict__ out, uint64_t ostride, Pack pk,
               unsigned int* __restrict__ bad_flag) {
     typedef typename Pack::OutT OutT;
-    typedef ScatterGeom<THREADS, ITEMS, OutT> Geo;
+    typedef ScatterGeom<THREADS, ITEMS, OutT, Pack::kStoreBytes> Geo;
     constexpr uint32_t SEG = Geo::SEG;
     constexpr int TILE = (int)Geo::TILE;
     uint32_t bad = 0;
@@ -1485,7 +1487,7 @@ k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
             const uint32_t k = kc[d];
             const uint64_t p = pos[d];
             const OutT x = e < k ? carry[d * SEG + e] : stage[tstart[d] + e - k];
-            if (p != ~0ull) out[p + e] = x;
+            if (p != ~0ull) Pack::store(out, ostride, p + e, x);
         }
         __syncthreads();
         // ---- leftovers (< SEG) become the partition's carry
@@ -1515,7 +1517,7 @@ k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
     __syncthreads();
     for (uint32_t q = threadIdx.x; q < nbins * SEG; q += THREADS) {
         const uint32_t d = q / SEG, j = q % SEG;
-        if (j < kc[d] && pos[d] != ~0ull) out[pos[d] + j] = carry[q];
+        if (j < kc[d] && pos[d] != ~0ull) Pack::store(out, ostride, pos[d] + j, carry[q]);
     }
     if (bad_flag && bad) atomicOr(bad_flag, bad);
 }
@@ -1930,19 +1932,20 @@ static constexpr uint64_t kRegionSlack = 1024;  // per shard
 //     sum <= (n + 4*stride) * 9/8 + 2^dbits * kShards * (slack + ALIGN - 1),
 // ALIGN = kRegionAlign in elements (the capacities' rounding).
 uint64_t sampled_capacity(uint64_t n, uint32_t dbits) {
-    const uint64_t ALIGN = kRegionAlign / 8;
+    const uint64_t ALIGN = kRegionAlign / 4;  // the finest: LayP48's 4-byte plane
     return n + n / 8 + 5 * kSampleStride + 1 +
            ((uint64_t)1 << dbits) * kShards * (kRegionSlack + ALIGN);
 }
 
 template <int ITEMS, class Pack>
 static bool sampled_scatter_t(Workspace* ws, const Tup* in, uint64_t n, void* out,
-                              const PlanDigit1& dig, uint32_t nbins,
+                              uint64_t ostride, const PlanDigit1& dig, uint32_t nbins,
                               unsigned long long* cursor, const uint64_t* cap_end,
                               const Pack& pk, unsigned int* bad_flag, hipStream_t st) {
     constexpr int THREADS = SMJ_SC_THREADS;
     constexpr int TILE = THREADS * ITEMS;
-    const size_t lds = ScatterGeom<THREADS, ITEMS, typename Pack::OutT>::lds_bytes(nbins);
+    const size_t lds = ScatterGeom<THREADS, ITEMS, typename Pack::OutT,
+                                   Pack::kStoreBytes>::lds_bytes(nbins);
     if (lds > 160 * 1024) return false;
     uint64_t ntiles = (n + TILE - 1) / TILE;
     const uint32_t maxwg = 256 * SMJ_SC_WG_PER_CU;
@@ -1969,12 +1972,12 @@ static bool sampled_scatter_t(Workspace* ws, const Tup* in, uint64_t n, void* ou
         if (vec)
             hipLaunchKernelGGL((k_scatter_res<THREADS, ITEMS, PlanDigit1, Pack, true>), dim3(nwg),
                                dim3(THREADS), lds, st, in, n, chunk, dig, nbins, cursor,
-                               cap_end, (typename Pack::OutT*)out, pk, bad_flag);
+                               cap_end, out, ostride, pk, bad_flag);
     }
     if (!vec)
         hipLaunchKernelGGL((k_scatter_res<THREADS, ITEMS, PlanDigit1, Pack, false>), dim3(nwg),
                            dim3(THREADS), lds, st, in, n, chunk, dig, nbins, cursor,
-                           cap_end, (typename Pack::OutT*)out, pk, bad_flag);
+                           cap_end, out, ostride, pk, bad_flag);
     return true;
 }
 
@@ -1983,7 +1986,7 @@ static bool sampled_scatter_t(Workspace* ws, const Tup* in, uint64_t n, void* ou
 // 1024; packed words 8 / 4 x 1024; 16-byte tuples 4 x 1024), measured best.
 template <class Pack>
 static void sampled_scatter(Workspace* ws, const Tup* in, uint64_t n, void* out,
-                            const PlanDigit1& dig, uint32_t nbins,
+                            uint64_t ostride, const PlanDigit1& dig, uint32_t nbins,
                             unsigned long long* cursor, const uint64_t* cap_end,
                             const Pack& pk, unsigned int* bad_flag, hipStream_t st) {
     constexpr int THREADS = SMJ_SC_THREADS;
@@ -1995,9 +1998,11 @@ static void sampled_scatter(Workspace* ws, const Tup* in, uint64_t n, void* out,
         ? (sizeof(typename Pack::OutT) == 8 ? SMJ_SC_ITEMS16P : SMJ_SC_ITEMS16)
         : SMJ_SC_ITEMS8;
     constexpr int SMALL = sizeof(Tup) == 16 ? 4 : 8;
-    if (sampled_scatter_t<BIG>(ws, in, n, out, dig, nbins, cursor, cap_end, pk, bad_flag, st))
+    if (sampled_scatter_t<BIG>(ws, in, n, out, ostride, dig, nbins, cursor, cap_end, pk,
+                               bad_flag, st))
         return;
-    if (sampled_scatter_t<SMALL>(ws, in, n, out, dig, nbins, cursor, cap_end, pk, bad_flag, st))
+    if (sampled_scatter_t<SMALL>(ws, in, n, out, ostride, dig, nbins, cursor, cap_end, pk,
+                                 bad_flag, st))
         return;
     fprintf(stderr, "[ERROR] smj: sampled scatter LDS exceeds 160 KiB (%u partitions)\n", nbins);
     abort();
@@ -2008,12 +2013,19 @@ void sampled_partition(Workspace* ws, int nrel, const Tup* const* in, const uint
                        unsigned int* sample, uint64_t* const* starts_dev,
                        int64_t* const* hist_out, uint64_t* const* seg_start,
                        int64_t* const* seg_cnt, unsigned int* flag_dev, hipStream_t st,
-                       const RangePlan* host_plan, bool packed, unsigned int* bad) {
+                       const RangePlan* host_plan, bool packed, unsigned int* bad,
+                       uint64_t p48_stride) {
     PlanDigit1 dig{plan_dev};
     const uint32_t nbins = 1u << dbits;
 #ifndef KEY_8B
     packed = false;
+    p48_stride = 0;
 #endif
+    // p48_stride > 0: 48-bit words in two planes of that many elements (LayP48)
+    if (p48_stride && !packed) {
+        fprintf(stderr, "[ERROR] smj: the 48-bit layout is a packed layout\n");
+        abort();
+    }
     if (packed && !host_plan) {
         fprintf(stderr, "[ERROR] smj: packed partition needs the host plan\n");
         abort();
@@ -2055,19 +2067,30 @@ void sampled_partition(Workspace* ws, int nrel, const Tup* const* in, const uint
         if (g == 0) g = 1;
         hipLaunchKernelGGL((k_sample_hist<PlanDigit1>), dim3(g, nrel), dim3(256),
                            nbins * sizeof(unsigned int), st, S, kSampleStride, dig, nbins);
+        // regions aligned to 128 bytes of the first plane (LayP48: 32
+        // elements, so the hi plane's regions start on 64 bytes)
         hipLaunchKernelGGL(k_regions, dim3(nrel), dim3(256), 0, st, R, nbins, kSampleStride,
-                           kRegionSlack, packed ? 8u : (uint32_t)sizeof(Tup));
+                           kRegionSlack, p48_stride ? 4u : packed ? 8u : (uint32_t)sizeof(Tup));
     }
     for (int r = 0; r < nrel; r++) {
         if (!n[r]) continue;
 #ifdef KEY_8B
+        if (p48_stride) {
+            LayP48::Pack pk;
+            pk.bu = key_u(host_plan->base);
+            pk.span = host_plan->span;
+            pk.s1 = host_plan->s1;
+            sampled_scatter(ws, in[r], n[r], out[r], p48_stride, dig, nbins, R.cursor[r],
+                            R.cap_end[r], pk, bad, st);
+            continue;
+        }
         if (packed) {
             LayPacked::Pack pk;
             pk.bu = key_u(host_plan->base);
             pk.span = host_plan->span;
             pk.s1 = host_plan->s1;
-            sampled_scatter(ws, in[r], n[r], out[r], dig, nbins, R.cursor[r], R.cap_end[r], pk,
-                            bad, st);
+            sampled_scatter(ws, in[r], n[r], out[r], 0, dig, nbins, R.cursor[r], R.cap_end[r],
+                            pk, bad, st);
             continue;
         }
 #endif
@@ -2077,7 +2100,7 @@ void sampled_partition(Workspace* ws, int nrel, const Tup* const* in, const uint
             pk.bu = key_u(host_plan->base);
             pk.span = host_plan->span;
         }
-        sampled_scatter(ws, in[r], n[r], out[r], dig, nbins, R.cursor[r], R.cap_end[r], pk,
+        sampled_scatter(ws, in[r], n[r], out[r], 0, dig, nbins, R.cursor[r], R.cap_end[r], pk,
                         bad && host_plan ? bad : (unsigned int*)nullptr, st);
     }
     hipLaunchKernelGGL(k_regions_done, dim3(nrel), dim3(256), 0, st, R, nbins, flag_dev);

@@ -212,6 +212,7 @@ struct RefDigit {
 // bits of a partition's "bad tuple" flag (status word 1 of a join)
 constexpr uint32_t kBadPayload = 1;  // a payload does not fit a packed word
 constexpr uint32_t kBadRange = 2;    // a key lies outside the plan range
+constexpr uint32_t kBadPayload48 = 4;  // ... fits a 64-bit word, not a 48-bit one
 
 struct RangePlan {
     int64_t base;     // smallest key of the range
@@ -252,6 +253,14 @@ __host__ __device__ __forceinline__ uint32_t plan_d1(const RangePlan& p,
 struct LayTup {
     typedef Tup W;
     static constexpr bool packed = false;
+    // element views of an intermediate buffer (base, plane stride): plain
+    // pointers for the one-array layouts
+    typedef const W* CView;
+    typedef W* View;
+    __device__ static __forceinline__ CView cview(const void* b, uint64_t) {
+        return static_cast<const W*>(b);
+    }
+    __device__ static __forceinline__ View view(void* b, uint64_t) { return static_cast<W*>(b); }
     __device__ static __forceinline__ uint64_t rel(const RangePlan& P, const W& w, uint32_t) {
         return plan_rel(P, tup_key(w));
     }
@@ -288,6 +297,12 @@ struct LayTup {
 struct LayPacked {
     typedef uint64_t W;
     static constexpr bool packed = true;
+    typedef const W* CView;
+    typedef W* View;
+    __device__ static __forceinline__ CView cview(const void* b, uint64_t) {
+        return static_cast<const W*>(b);
+    }
+    __device__ static __forceinline__ View view(void* b, uint64_t) { return static_cast<W*>(b); }
     __device__ static __forceinline__ uint64_t rel(const RangePlan& P, const W& w, uint32_t b) {
         return ((uint64_t)b << P.s1) | (w >> (64 - P.s1));
     }
@@ -323,8 +338,121 @@ struct LayPacked {
             bad |= ((uint64_t)t.payload >> pb) != 0 ? kBadPayload : 0u;
             return ((r & ((1ull << s1) - 1)) << pb) | (uint64_t)t.payload;
         }
+        static constexpr uint32_t kStoreBytes = 8;  // bytes of one element in a plane
+        __device__ static __forceinline__ void store(void* out, uint64_t, uint64_t i,
+                                                     uint64_t x) {
+            static_cast<uint64_t*>(out)[i] = x;
+        }
     };
     // packing applies to plans whose level-1 buckets span 2^1 .. 2^32 keys
+    __host__ static bool usable(const RangePlan& P) { return P.s1 >= 1 && P.s1 <= 32; }
+};
+
+// ---------------------------------------------------------------------------
+// LayP48 (16-byte tuples, round 4): the packed word of LayPacked cut to 48
+// bits,
+//     w = (rel mod 2^s1) << (48 - s1)  |  payload          (payload < 2^(48-s1))
+// and stored as two planes of one buffer: lo = w mod 2^32 (uint32[stride])
+// then hi = w >> 32 (uint16[stride]), element i at lo[i] and hi[i].  6 bytes
+// an element instead of 8: the level-1 scatter writes, the tile pass reads and
+// writes and the group pass reads a quarter fewer bytes.  In registers and in
+// LDS an element is still a uint64_t, ordered like the (key, payload) order.
+// The partition flags kBadPayload48 when a payload needs more than 48 - s1
+// bits; the join then reruns with 64-bit words (LayPacked).
+// ---------------------------------------------------------------------------
+typedef const __attribute__((address_space(1))) uint32_t* G32c;
+typedef const __attribute__((address_space(1))) uint16_t* G16c;
+typedef __attribute__((address_space(1))) uint32_t* G32;
+typedef __attribute__((address_space(1))) uint16_t* G16;
+
+struct P48CView {
+    G32c lo;
+    G16c hi;
+    __device__ __forceinline__ uint64_t operator[](uint64_t i) const {
+        return (uint64_t)lo[i] | ((uint64_t)hi[i] << 32);
+    }
+    __device__ __forceinline__ P48CView operator+(uint64_t k) const {
+        return P48CView{lo + k, hi + k};
+    }
+};
+
+struct P48View {
+    G32 lo;
+    G16 hi;
+    __device__ __forceinline__ uint64_t operator[](uint64_t i) const {
+        return (uint64_t)lo[i] | ((uint64_t)hi[i] << 32);
+    }
+    __device__ __forceinline__ P48View operator+(uint64_t k) const {
+        return P48View{lo + k, hi + k};
+    }
+};
+
+// streaming store of element 0 of a view (the plane counterpart of st_w)
+__device__ __forceinline__ void st_w(const P48View& p, uint64_t v) {
+#if SMJ_NT_STORES
+    __builtin_nontemporal_store((uint32_t)v, p.lo);
+    __builtin_nontemporal_store((uint16_t)(v >> 32), p.hi);
+#else
+    p.lo[0] = (uint32_t)v;
+    p.hi[0] = (uint16_t)(v >> 32);
+#endif
+}
+
+struct LayP48 {
+    typedef uint64_t W;
+    static constexpr bool packed = true;
+    typedef P48CView CView;
+    typedef P48View View;
+    __device__ static __forceinline__ CView cview(const void* b, uint64_t stride) {
+        const uint32_t* lo = static_cast<const uint32_t*>(b);
+        return CView{(G32c)lo, (G16c)(const uint16_t*)(lo + stride)};
+    }
+    __device__ static __forceinline__ View view(void* b, uint64_t stride) {
+        uint32_t* lo = static_cast<uint32_t*>(b);
+        return View{(G32)lo, (G16)(uint16_t*)(lo + stride)};
+    }
+    __device__ static __forceinline__ uint64_t rel(const RangePlan& P, const W& w, uint32_t b) {
+        return ((uint64_t)b << P.s1) | (w >> (48 - P.s1));
+    }
+    __device__ static __forceinline__ bool clamped(const RangePlan&, const W&) { return false; }
+    __device__ static __forceinline__ bool less(const W& a, const W& b) { return a < b; }
+    __device__ static __forceinline__ uint64_t same_key_id(const W& w) { return w; }
+    __device__ static __forceinline__ uint32_t digit_fast(const W& w, uint32_t, uint32_t s1,
+                                                          uint32_t sh, uint32_t mask) {
+        return (uint32_t)(w >> (48 - s1 + sh)) & mask;
+    }
+    __host__ static bool fast_ok(const RangePlan& P, uint32_t sh, uint32_t width) {
+        return sh + width <= P.s1;
+    }
+    __device__ static __forceinline__ Tup unpack(const RangePlan& P, const W& w, uint32_t b) {
+        Tup t;
+        t.payload = (int64_t)(w & (~0ull >> (16 + P.s1)));
+        t.key = (int64_t)((key_u(P.base) + rel(P, w, b)) ^ 0x8000000000000000ull);
+        return t;
+    }
+    struct Pack {
+        typedef uint64_t OutT;
+        uint64_t bu, span;
+        uint32_t s1;
+        __device__ __forceinline__ uint64_t operator()(const Tup& t, uint32_t& bad) const {
+            const uint64_t ku = key_u(t.key);
+            const uint64_t r = ku - bu;
+            const uint32_t pb = 48 - s1;
+            const uint64_t pay = (uint64_t)t.payload;
+            bad |= (ku < bu || r > span) ? kBadRange : 0u;
+            bad |= (pay >> (64 - s1)) != 0 ? kBadPayload : 0u;
+            bad |= (pay >> pb) != 0 ? kBadPayload48 : 0u;
+            return ((r & ((1ull << s1) - 1)) << pb) | (pay & ((1ull << pb) - 1));
+        }
+        // the lo plane sets the segment: 16 elements = 64 bytes (hi: 32 bytes)
+        static constexpr uint32_t kStoreBytes = 4;
+        __device__ static __forceinline__ void store(void* out, uint64_t stride, uint64_t i,
+                                                     uint64_t x) {
+            uint32_t* lo = static_cast<uint32_t*>(out);
+            ((G32)lo)[i] = (uint32_t)x;
+            ((G16)(uint16_t*)(lo + stride))[i] = (uint16_t)(x >> 32);
+        }
+    };
     __host__ static bool usable(const RangePlan& P) { return P.s1 >= 1 && P.s1 <= 32; }
 };
 #endif
@@ -333,6 +461,10 @@ struct LayPacked {
 struct PackNone {
     typedef Tup OutT;
     __device__ __forceinline__ Tup operator()(const Tup& t, uint32_t&) const { return t; }
+    static constexpr uint32_t kStoreBytes = sizeof(Tup);
+    __device__ static __forceinline__ void store(void* out, uint64_t, uint64_t i, const Tup& x) {
+        static_cast<Tup*>(out)[i] = x;
+    }
 };
 
 // the plain layout with a range check: kBadRange when the key lies outside
@@ -346,6 +478,10 @@ struct PackRange {
         const uint64_t ku = key_u(tup_key(t));
         bad |= (ku < bu || ku - bu > span) ? kBadRange : 0u;
         return t;
+    }
+    static constexpr uint32_t kStoreBytes = sizeof(Tup);
+    __device__ static __forceinline__ void store(void* out, uint64_t, uint64_t i, const Tup& x) {
+        static_cast<Tup*>(out)[i] = x;
     }
 };
 

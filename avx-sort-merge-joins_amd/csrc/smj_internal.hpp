@@ -293,7 +293,7 @@ void sampled_partition(Workspace* ws, int nrel, const Tup* const* in, const uint
                        int64_t* const* hist_out, uint64_t* const* seg_start,
                        int64_t* const* seg_cnt, unsigned int* flag_dev, hipStream_t st,
                        const RangePlan* host_plan = nullptr, bool packed = false,
-                       unsigned int* bad = nullptr);
+                       unsigned int* bad = nullptr, uint64_t p48_stride = 0);
 void hist_memcpy(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
                  uint32_t dbits, hipStream_t st);
 // lane order of LDS atomic returns (k_scatter_swp's ranks): violations, 0 expected
@@ -326,6 +326,10 @@ struct BucketSortArgs {
     // partition the bucket pass then runs without a mid-pipeline host sync
     const RangePlan* host_plan = nullptr;
     bool packed = false;            // part/tmp hold LayPacked words (host_plan's)
+    // part/tmp hold LayP48 words (packed too): two planes of pstride[r]
+    // elements each (lo uint32, then hi uint16)
+    bool p48 = false;
+    uint64_t pstride[2] = {0, 0};
     // optional 4-word block zeroed by the caller: [0] = part_flag, [1] =
     // pack_bad, [2] = the skew queue length (read back in one copy)
     unsigned int* status = nullptr;

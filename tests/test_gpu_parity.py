@@ -463,13 +463,34 @@ def test_device_join_keys_outside_hint(libs, oracles, width):
     assert np.array_equal(lib.to_host(sS), eS)
 
 
-@pytest.mark.parametrize("payload", ["rowid", "negative", "wide"])
+@pytest.mark.parametrize("payload", ["rowid", "negative", "wide", "wide48", "p48off"])
 def test_device_join_packed_words(libs, oracles, width, payload):
     """With a key-range hint the 16-byte join carries packed words (key offset
-    in the bucket + payload in one 64-bit word) through the intermediate
-    passes.  Payloads that do not fit (negative, or wider than 64 - s1 bits)
-    make the partition flag the attempt and the join rerun on tuples; the
-    result is the same either way."""
+    in the bucket + payload) through the intermediate passes: 48-bit words in
+    two planes first (LayP48), 64-bit words when a payload needs more than
+    48 - s1 bits ("wide48": 2^44 here, s1 = 11), tuples when it needs more
+    than 64 - s1 or is negative.  "p48off": SMJ_P48=0 (64-bit words from the
+    start).  The result is the same on every path."""
+    if payload == "p48off":
+        if width != 16:
+            pytest.skip("packed words are the 16-byte layout")
+        # the switch is read once per process: a child process runs the case
+        import subprocess
+        import sys
+        from conftest import PKG, ROOT
+        here = os.path.dirname(os.path.abspath(__file__))
+        env = dict(os.environ, SMJ_P48="0",
+                   PYTHONPATH=os.pathsep.join([here, ROOT, PKG, os.environ.get("PYTHONPATH", "")]))
+        code = ("import test_gpu_parity as t, oracle, smj; "
+                "t._packed_join_case({16: smj.Library(16)}, {16: oracle.Oracle(16)}, 16, 'rowid')")
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                           timeout=240, cwd=here, env=env)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+        return
+    _packed_join_case(libs, oracles, width, payload)
+
+
+def _packed_join_case(libs, oracles, width, payload):
     import torch
     orc, lib = oracles[width], libs[width]
     n = 500_000
@@ -478,6 +499,8 @@ def test_device_join_packed_words(libs, oracles, width, payload):
         S["payload"][n // 3] = -5
     elif payload == "wide" and width == 16:
         R["payload"][7] = np.int64(1) << 60
+    elif payload == "wide48" and width == 16:
+        R["payload"][7] = np.int64(1) << 44
     exp, eR, eS = orc.sortmergejoin(R, S)
     dR, dS = lib.to_device(R), lib.to_device(S)
     sR, sS = lib.empty(n), lib.empty(n)
