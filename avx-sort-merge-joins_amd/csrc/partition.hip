@@ -1479,15 +1479,30 @@ k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
         }
         __syncthreads();
         // ---- whole segments: SEG consecutive lanes per segment, element e of
-        // a partition = carry (e < kc) or its staged tuples
-        for (uint32_t q = threadIdx.x; q < nseg * SEG; q += THREADS) {
-            const uint32_t sg = q / SEG;
-            const uint32_t d = segown[sg];
-            const uint32_t e = (sg - segpre[d]) * SEG + q % SEG;
-            const uint32_t k = kc[d];
-            const uint64_t p = pos[d];
-            const OutT x = e < k ? carry[d * SEG + e] : stage[tstart[d] + e - k];
-            if (p != ~0ull) Pack::store(out, ostride, p + e, x);
+        // a partition = carry (e < kc) or its staged tuples (pair stores:
+        // SEG / 2 lanes, two adjacent elements each)
+        if constexpr (Pack::kPairs) {
+            constexpr uint32_t PS = SEG / 2;
+            for (uint32_t q = threadIdx.x; q < nseg * PS; q += THREADS) {
+                const uint32_t sg = q / PS;
+                const uint32_t d = segown[sg];
+                const uint32_t e = (sg - segpre[d]) * SEG + 2 * (q % PS);
+                const uint32_t k = kc[d];
+                const uint64_t p = pos[d];
+                const OutT x0 = e < k ? carry[d * SEG + e] : stage[tstart[d] + e - k];
+                const OutT x1 = e + 1 < k ? carry[d * SEG + e + 1] : stage[tstart[d] + e + 1 - k];
+                if (p != ~0ull) Pack::store2(out, ostride, p + e, x0, x1);
+            }
+        } else {
+            for (uint32_t q = threadIdx.x; q < nseg * SEG; q += THREADS) {
+                const uint32_t sg = q / SEG;
+                const uint32_t d = segown[sg];
+                const uint32_t e = (sg - segpre[d]) * SEG + q % SEG;
+                const uint32_t k = kc[d];
+                const uint64_t p = pos[d];
+                const OutT x = e < k ? carry[d * SEG + e] : stage[tstart[d] + e - k];
+                if (p != ~0ull) Pack::store(out, ostride, p + e, x);
+            }
         }
         __syncthreads();
         // ---- leftovers (< SEG) become the partition's carry

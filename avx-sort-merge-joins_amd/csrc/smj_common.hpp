@@ -343,6 +343,10 @@ struct LayPacked {
                                                      uint64_t x) {
             static_cast<uint64_t*>(out)[i] = x;
         }
+        static constexpr bool kPairs = false;  // store2: LayP48's two-plane pairs only
+        template <class X>
+        __device__ static __forceinline__ void store2(void*, uint64_t, uint64_t, const X&,
+                                                      const X&) {}
     };
     // packing applies to plans whose level-1 buckets span 2^1 .. 2^32 keys
     __host__ static bool usable(const RangePlan& P) { return P.s1 >= 1 && P.s1 <= 32; }
@@ -452,6 +456,19 @@ struct LayP48 {
             ((G32)lo)[i] = (uint32_t)x;
             ((G16)(uint16_t*)(lo + stride))[i] = (uint16_t)(x >> 32);
         }
+        // elements i and i + 1 (i even) with one store per plane: 8 + 4
+        // bytes a lane instead of 4 + 2 (half the store instructions)
+        static constexpr bool kPairs = true;
+        __device__ static __forceinline__ void store2(void* out, uint64_t stride, uint64_t i,
+                                                      uint64_t x0, uint64_t x1) {
+            typedef uint32_t U2 __attribute__((ext_vector_type(2)));
+            typedef uint16_t H2 __attribute__((ext_vector_type(2)));
+            uint32_t* lo = static_cast<uint32_t*>(out);
+            const U2 l = {(uint32_t)x0, (uint32_t)x1};
+            const H2 h = {(uint16_t)(x0 >> 32), (uint16_t)(x1 >> 32)};
+            *(__attribute__((address_space(1))) U2*)(lo + i) = l;
+            *(__attribute__((address_space(1))) H2*)((uint16_t*)(lo + stride) + i) = h;
+        }
     };
     __host__ static bool usable(const RangePlan& P) { return P.s1 >= 1 && P.s1 <= 32; }
 };
@@ -465,6 +482,10 @@ struct PackNone {
     __device__ static __forceinline__ void store(void* out, uint64_t, uint64_t i, const Tup& x) {
         static_cast<Tup*>(out)[i] = x;
     }
+    static constexpr bool kPairs = false;  // store2: LayP48's two-plane pairs only
+    template <class X>
+    __device__ static __forceinline__ void store2(void*, uint64_t, uint64_t, const X&,
+                              const X&) {}
 };
 
 // the plain layout with a range check: kBadRange when the key lies outside
@@ -483,6 +504,10 @@ struct PackRange {
     __device__ static __forceinline__ void store(void* out, uint64_t, uint64_t i, const Tup& x) {
         static_cast<Tup*>(out)[i] = x;
     }
+    static constexpr bool kPairs = false;  // store2: LayP48's two-plane pairs only
+    template <class X>
+    __device__ static __forceinline__ void store2(void*, uint64_t, uint64_t, const X&,
+                              const X&) {}
 };
 
 __host__ __device__ __forceinline__ uint32_t plan_d2(const RangePlan& p,
