@@ -2219,8 +2219,8 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
     }
     set_pass_attrs<LayTup>();
     if (a.host_plan && a.seg_start[0] && a.part_flag) {
-#ifdef KEY_8B
         if (a.p48) return bucket_sort_nosync<LayP48>(ws, a, st);
+#ifdef KEY_8B
         if (a.packed) return bucket_sort_nosync<LayPacked>(ws, a, st);
 #endif
         return bucket_sort_nosync<LayTup>(ws, a, st);

@@ -388,9 +388,15 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
     // guessed plan that a key falls outside of is replaced by the exact one
     // and the attempts restart.  The 48-bit scatter's carries (128 bytes a
     // partition) fit LDS up to 512 partitions.
+    // (8-byte tuples have no 64-bit packed words: the 48-bit ones, else
+    // tuples; the same conditions as packing, checked here)
     auto first_mode = [&]() {
 #ifdef KEY_8B
         if (can_pack && use_p48() && nb <= 512) return -1;
+#else
+        if (sampled && plan_on_host && use_packing() && use_p48() &&
+            LayP48::usable(hplan) && nb <= 512)
+            return -1;
 #endif
         return can_pack ? 0 : (sampled ? 1 : 2);
     };
@@ -469,7 +475,8 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
         if (mode == -1 && !(guessed && (why[1] & kBadRange))) {
             // payloads too wide for 48 bits only: 64-bit words; anything else
             // (overflow, unpackable) as from 64-bit words
-            mode = (why[1] & kBadPayload48) && !(why[1] & kBadPayload) && !why[0] ? 0 : 1;
+            mode = (why[1] & kBadPayload48) && !(why[1] & kBadPayload) && !why[0] && can_pack
+                ? 0 : 1;
             continue;
         }
         if (guessed && (why[1] & kBadRange)) {

@@ -2033,8 +2033,8 @@ void sampled_partition(Workspace* ws, int nrel, const Tup* const* in, const uint
     PlanDigit1 dig{plan_dev};
     const uint32_t nbins = 1u << dbits;
 #ifndef KEY_8B
-    packed = false;
-    p48_stride = 0;
+    // 8-byte tuples: no 64-bit packed words, but 48-bit ones (LayP48)
+    packed = p48_stride != 0;
 #endif
     // p48_stride > 0: 48-bit words in two planes of that many elements (LayP48)
     if (p48_stride && !packed) {
@@ -2089,7 +2089,6 @@ void sampled_partition(Workspace* ws, int nrel, const Tup* const* in, const uint
     }
     for (int r = 0; r < nrel; r++) {
         if (!n[r]) continue;
-#ifdef KEY_8B
         if (p48_stride) {
             LayP48::Pack pk;
             pk.bu = key_u(host_plan->base);
@@ -2099,6 +2098,7 @@ void sampled_partition(Workspace* ws, int nrel, const Tup* const* in, const uint
                             R.cap_end[r], pk, bad, st);
             continue;
         }
+#ifdef KEY_8B
         if (packed) {
             LayPacked::Pack pk;
             pk.bu = key_u(host_plan->base);

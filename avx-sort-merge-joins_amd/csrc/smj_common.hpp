@@ -351,11 +351,13 @@ struct LayPacked {
     // packing applies to plans whose level-1 buckets span 2^1 .. 2^32 keys
     __host__ static bool usable(const RangePlan& P) { return P.s1 >= 1 && P.s1 <= 32; }
 };
+#endif
 
 // ---------------------------------------------------------------------------
-// LayP48 (16-byte tuples, round 4): the packed word of LayPacked cut to 48
-// bits,
+// LayP48 (round 4, both tuple widths): the packed word of LayPacked cut to
+// 48 bits,
 //     w = (rel mod 2^s1) << (48 - s1)  |  payload          (payload < 2^(48-s1))
+// (8-byte tuples: the payload as the unsigned 32-bit value their order uses)
 // and stored as two planes of one buffer: lo = w mod 2^32 (uint32[stride])
 // then hi = w >> 32 (uint16[stride]), element i at lo[i] and hi[i].  6 bytes
 // an element instead of 8: the level-1 scatter writes, the tile pass reads and
@@ -429,20 +431,30 @@ struct LayP48 {
         return sh + width <= P.s1;
     }
     __device__ static __forceinline__ Tup unpack(const RangePlan& P, const W& w, uint32_t b) {
+        const uint64_t pay = w & (~0ull >> (16 + P.s1));
+        const int64_t key = (int64_t)((key_u(P.base) + rel(P, w, b)) ^ 0x8000000000000000ull);
+#ifdef KEY_8B
         Tup t;
-        t.payload = (int64_t)(w & (~0ull >> (16 + P.s1)));
-        t.key = (int64_t)((key_u(P.base) + rel(P, w, b)) ^ 0x8000000000000000ull);
+        t.payload = (int64_t)pay;
+        t.key = key;
         return t;
+#else
+        return ((uint64_t)(uint32_t)key << 32) | pay;
+#endif
     }
     struct Pack {
         typedef uint64_t OutT;
         uint64_t bu, span;
         uint32_t s1;
         __device__ __forceinline__ uint64_t operator()(const Tup& t, uint32_t& bad) const {
-            const uint64_t ku = key_u(t.key);
+            const uint64_t ku = key_u(tup_key(t));
             const uint64_t r = ku - bu;
             const uint32_t pb = 48 - s1;
+#ifdef KEY_8B
             const uint64_t pay = (uint64_t)t.payload;
+#else
+            const uint64_t pay = (uint32_t)t;  // unsigned, as the 8-byte order takes it
+#endif
             bad |= (ku < bu || r > span) ? kBadRange : 0u;
             bad |= (pay >> (64 - s1)) != 0 ? kBadPayload : 0u;
             bad |= (pay >> pb) != 0 ? kBadPayload48 : 0u;
@@ -472,7 +484,6 @@ struct LayP48 {
     };
     __host__ static bool usable(const RangePlan& P) { return P.s1 >= 1 && P.s1 <= 32; }
 };
-#endif
 
 // identity "packing" of the plain layout
 struct PackNone {

@@ -9,14 +9,16 @@ mkdir -p $O
 [ -n "${NOSUITE:-}" ] || tail -1 $O/pytest_gpu.txt
 [ -n "${NOSUITE:-}" ] || timeout -k 10 120 build_lab/planelab > $O/planelab.txt 2>&1 || { cat $O/planelab.txt; exit 1; }
 [ -n "${NOSUITE:-}" ] || cat $O/planelab.txt
+DEFAULT_ARGS=$'--steps 10\n--dist zipf --steps 10\n--op sort --width 16 --steps 10'
 for rep in 1 2; do
-  for args in "--steps 10" "--dist zipf --steps 10" "--op sort --width 16 --steps 10"; do
+  while IFS= read -r args; do
+    [ -z "$args" ] && continue
     tag=$(echo "$args" | tr -c 'a-z0-9' '_')
     for side in p48 p64; do
       if [ $side = p64 ]; then export SMJ_P48=0; else unset SMJ_P48; fi
-      timeout -k 10 200 python3 bench.py $args --no-cpu-baseline > $O/${tag}_${side}_$rep.json 2> $O/${tag}_${side}_$rep.err || { echo "FAIL $side $args"; tail -5 $O/${tag}_${side}_$rep.err; exit 1; }
-      python3 -c "import json,sys;d=json.load(open(sys.argv[1]));print(sys.argv[2], sys.argv[3], sys.argv[4], d['ms_per_step'], d['result_ok'], d['detail']['kernels_ms_per_step'])" $O/${tag}_${side}_$rep.json "$rep" "$side" "$args"
+      timeout -k 10 200 python3 bench.py $args --no-cpu-baseline > $O/${tag}_${side}_$rep.json 2> $O/${tag}_${side}_$rep.err < /dev/null || { echo "FAIL $side $args"; tail -5 $O/${tag}_${side}_$rep.err; exit 1; }
+      python3 -c "import json,sys;d=json.load(open(sys.argv[1]));print(sys.argv[2], sys.argv[3], sys.argv[4], d['ms_per_step'], d['result_ok'], d['detail']['kernels_ms_per_step'])" $O/${tag}_${side}_$rep.json "$rep" "$side" "$args" < /dev/null
     done
-  done
+  done <<< "${ARGS:-$DEFAULT_ARGS}"
 done
 unset SMJ_P48
