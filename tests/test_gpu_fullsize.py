@@ -49,6 +49,32 @@ def test_bench_sort_full(libs, oracles, width, payload):
     np.testing.assert_array_equal(got, want)
 
 
+@pytest.mark.parametrize("payload", ["fits48", "wide48"])
+def test_sort_p48_fallback(libs, oracles, width, payload):
+    """The 48-bit layout (LayP48) and its fallbacks at a size where the plan's
+    s1 is 17 (2^25 keys over 256 partitions): payloads below 2^(48 - 17) go as
+    48-bit words; a payload of 2^31 and above (8-byte tuples: any negative
+    int32, as the unsigned value their order uses; 16-byte: 2^40) sends the
+    sort to tuples (8 B) or 64-bit words (16 B).  Bit-exact against the
+    oracle either way."""
+    import torch
+    lib, orc = libs[width], oracles[width]
+    n = 1 << 25
+    R = lib.empty(n)
+    lib.dev_gen_pk(R, 0, n, 777, with_payload=True)
+    if payload == "wide48":
+        big = -(1 << 30) if width == 8 else (1 << 40)
+        R[::4096, 0] = big
+    out = lib.empty(n)
+    lib.dev_sort(R, out)
+    torch.cuda.synchronize()
+    host_in = lib.to_host(R)
+    got = lib.to_host(out)
+    del R, out
+    _free(torch)
+    np.testing.assert_array_equal(got, orc.sort_radix(host_in))
+
+
 @pytest.mark.parametrize("bits,shift", [(10, 0), (10, 7)])
 def test_bench_partition_full(libs, oracles, width, bits, shift):
     import torch
