@@ -21,4 +21,6 @@ else
   O2=gpurun_out/r04_fin2
   bash tools/r03_lines.sh $O2 "sort8:--op sort --width 8 --steps 10 --warmup 2" "part8:--op partition --width 8 --steps 10 --warmup 2" "merge8:--op merge --steps 20 --warmup 3" || exit 1
   NO_PMC=1 CPU_ARGS=--no-cpu-baseline bash tools/r03_lines.sh $O2/nopmc "api16:--api --steps 10 --warmup 2" "xpath16:--exchange-path --steps 10 --warmup 2" "join16:--steps 10 --warmup 2" || exit 1
+  # SQ counters of the 8-byte join (the group pass's wait share)
+  O=$O2/sq bash tools/r03_sqprobe.sh --width 8 > $O2/sq_join8.txt 2>&1 || { tail -5 $O2/sq_join8.txt; exit 1; }
 fi
