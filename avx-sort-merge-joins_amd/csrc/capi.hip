@@ -1702,7 +1702,8 @@ static void join_segmented_core(Workspace* ws, void* R, uint64_t nR, void* S, ui
                                 uint64_t* const* ss, int64_t* const* sc, uint32_t nseg,
                                 uint32_t bucket_bits, int64_t key_lo, int64_t key_hi,
                                 uint32_t flags, tuple_t* sortedR, tuple_t* sortedS,
-                                unsigned long long* count_dev, hipStream_t st) {
+                                unsigned long long* count_dev, hipStream_t st,
+                                const uint64_t* pstride = nullptr) {
     if (!(flags & SMJ_SEG_STAGE_R))  // the count belongs to the group pass's call
         SMJ_CHECK(hipMemsetAsync(count_dev, 0, sizeof(unsigned long long), st));
     uint32_t D1, D2, D2cap;
@@ -1714,15 +1715,21 @@ static void join_segmented_core(Workspace* ws, void* R, uint64_t nR, void* S, ui
     if (D2 > kMaxD2) D2 = kMaxD2;
     D2cap = D2 + 2 < kMaxD2 ? D2 + 2 : (D2 > kMaxD2 ? D2 : kMaxD2);
     RangePlan hplan = make_plan(key_lo, key_hi, D1, D2, D2cap, kGroupD3Max);
-    const bool packed = (flags & SMJ_SEG_PACKED) != 0;
+    const bool p48 = pstride != nullptr;  // 48-bit words in two planes (LayP48)
+    const bool packed = (flags & SMJ_SEG_PACKED) != 0 || p48;
+    if (p48 && !LayP48::usable(hplan)) {
+        fprintf(stderr, "[ERROR] smj_dev_join_segmented_planes: 48-bit words need "
+                "1 <= s1 <= 32 (s1 = %u)\n", hplan.s1);
+        abort();
+    }
 #ifdef KEY_8B
-    if (packed && !LayPacked::usable(hplan)) {
+    if (packed && !p48 && !LayPacked::usable(hplan)) {
         fprintf(stderr, "[ERROR] smj_dev_join_segmented: packed words need 1 <= s1 <= 32 "
                 "(s1 = %u)\n", hplan.s1);
         abort();
     }
 #else
-    if (packed) {
+    if (packed && !p48) {
         fprintf(stderr, "[ERROR] smj_dev_join_segmented: packed words are a 16-byte-tuple "
                 "layout\n");
         abort();
@@ -1765,6 +1772,8 @@ static void join_segmented_core(Workspace* ws, void* R, uint64_t nR, void* S, ui
     a.host_plan = &hplan;
     a.packed = packed;  // checked packable before the exchange: no pack_bad here
     a.digit_fast = packed;  // packed words never lie outside the plan
+    a.p48 = p48;
+    for (int r = 0; r < 2 && p48; r++) a.pstride[r] = pstride[r];
     if ((flags & SMJ_SEG_STAGE_R) && (flags & SMJ_SEG_STAGE_REST)) {
         fprintf(stderr, "[ERROR] smj_dev_join_segmented: SMJ_SEG_STAGE_R and _REST are two "
                 "calls\n");
@@ -1827,6 +1836,29 @@ void smj_dev_join_segmented_tables(smj_workspace* wsp, void* R, uint64_t nR,
     int64_t* sc[2] = {(int64_t*)cntR, (int64_t*)cntS};
     join_segmented_core((Workspace*)wsp, R, nR, S, nS, ss, sc, nseg, bucket_bits, key_lo,
                         key_hi, flags, sortedR, sortedS, count_dev, (hipStream_t)stream);
+}
+
+void smj_dev_join_segmented_planes(smj_workspace* wsp, void* R, uint64_t strideR, uint64_t nR,
+                                   const int64_t* startR, const int64_t* cntR, void* S,
+                                   uint64_t strideS, uint64_t nS, const int64_t* startS,
+                                   const int64_t* cntS, uint32_t nseg, uint32_t bucket_bits,
+                                   int64_t key_lo, int64_t key_hi, uint32_t flags,
+                                   tuple_t* sortedR, tuple_t* sortedS,
+                                   unsigned long long* count_dev, smj_stream_t stream) {
+    check_segmented("smj_dev_join_segmented_planes", nseg, bucket_bits, nR, nS);
+    if ((flags & SMJ_SEG_PACKED) || strideR % 32 || strideS % 32 || strideR < nR ||
+        strideS < nS) {
+        fprintf(stderr, "[ERROR] smj_dev_join_segmented_planes: flags %u (stages only), "
+                "strides %llu / %llu (multiples of 32, >= nR %llu / nS %llu)\n", flags,
+                (unsigned long long)strideR, (unsigned long long)strideS,
+                (unsigned long long)nR, (unsigned long long)nS);
+        abort();
+    }
+    uint64_t* ss[2] = {(uint64_t*)startR, (uint64_t*)startS};
+    int64_t* sc[2] = {(int64_t*)cntR, (int64_t*)cntS};
+    const uint64_t pst[2] = {strideR, strideS};
+    join_segmented_core((Workspace*)wsp, R, nR, S, nS, ss, sc, nseg, bucket_bits, key_lo,
+                        key_hi, flags, sortedR, sortedS, count_dev, (hipStream_t)stream, pst);
 }
 
 void smj_join_phase_ms(smj_workspace* wsp, float* ms5) {
@@ -1980,6 +2012,44 @@ int smj_dev_partition_range_sampled(smj_workspace* wsp, const tuple_t* in, uint6
     int64_t* sc[1] = {seg_cnt_out};
     sampled_partition(ws, 1, rels, ns, outs, plan, nbits, sample, st_, h_, ss, sc, flags, st,
                       &h, packed != 0, packed ? flags + 1 : nullptr);
+    return 1;
+}
+
+int smj_dev_partition_range_planes(smj_workspace* wsp, const tuple_t* in, uint64_t n,
+                                   void* out, uint64_t stride, uint32_t nbits,
+                                   int64_t key_min, int64_t key_max, int64_t* seg_start_out,
+                                   int64_t* seg_cnt_out, unsigned int* flags,
+                                   smj_stream_t stream) {
+    Workspace* ws = (Workspace*)wsp;
+    hipStream_t st = (hipStream_t)stream;
+    // the scatter's LDS carries hold 2^9 partitions of 48-bit words (the
+    // 1-GPU join's limit for this layout too)
+    if (nbits > 9 || n >= (1ull << 32)) return 0;
+    RangePlan h = make_plan(key_min, key_max, nbits, 0, 0, 0);
+    if (!LayP48::usable(h)) return 0;
+    if (stride % 32 || stride < sampled_capacity(n, nbits)) {
+        fprintf(stderr, "[ERROR] smj_dev_partition_range_planes: stride %llu (a multiple of "
+                "32, >= smj_sampled_capacity = %llu)\n", (unsigned long long)stride,
+                (unsigned long long)sampled_capacity(n, nbits));
+        abort();
+    }
+    const uint32_t nbins = 1u << nbits;
+    RangePlan* plan = (RangePlan*)ws->scratch("xp_plan", sizeof(RangePlan));
+    hipLaunchKernelGGL(k_setplan, dim3(1), dim3(1), 0, st, plan, h);
+    unsigned int* sample = (unsigned int*)ws->scratch("xp_sample", (size_t)nbins * 4);
+    SMJ_CHECK(hipMemsetAsync(sample, 0, (size_t)nbins * 4, st));
+    SMJ_CHECK(hipMemsetAsync(flags, 0, 8, st));
+    uint64_t* starts = (uint64_t*)ws->scratch("xp_starts", (size_t)nbins * 8);
+    int64_t* hist = (int64_t*)ws->scratch("xp_hist", (size_t)nbins * 8);
+    const Tup* rels[1] = {(const Tup*)in};
+    const uint64_t ns[1] = {n};
+    void* outs[1] = {out};
+    uint64_t* st_[1] = {starts};
+    int64_t* h_[1] = {hist};
+    uint64_t* ss[1] = {(uint64_t*)seg_start_out};
+    int64_t* sc[1] = {seg_cnt_out};
+    sampled_partition(ws, 1, rels, ns, outs, plan, nbits, sample, st_, h_, ss, sc, flags, st,
+                      &h, true, flags + 1, stride);
     return 1;
 }
 

@@ -63,7 +63,8 @@ DEVICE_SYMBOLS = [
     "smj_set_materialize", "smj_dev_join_segmented_tables", "smj_dev_partition_range_sampled",
     "smj_sampled_capacity", "smj_sampled_shards", "smj_context_workspace",
     "smj_dev_gen_nonunique", "smj_dev_gen_zipf_ref", "smj_glibc_rand",
-    "smj_dev_xsend", "smj_dev_xrecv", "smj_join",
+    "smj_dev_xsend", "smj_dev_xrecv", "smj_join", "smj_dev_partition_range_planes",
+    "smj_dev_join_segmented_planes",
 ]
 
 
@@ -183,6 +184,11 @@ class Library:
                                                      _P, _P]),
             "smj_dev_partition_range_sampled": (C.c_int, [_P, _P, _U64, _P, _U32, _I64, _I64,
                                                           C.c_int, _P, _P, _P, _P]),
+            "smj_dev_partition_range_planes": (C.c_int, [_P, _P, _U64, _P, _U64, _U32, _I64,
+                                                         _I64, _P, _P, _P, _P]),
+            "smj_dev_join_segmented_planes": (None, [_P, _P, _U64, _U64, _P, _P, _P, _U64,
+                                                     _U64, _P, _P, _U32, _U32, _I64, _I64,
+                                                     _U32, _P, _P, _P, _P]),
             "smj_sampled_capacity": (_U64, [_U64, _U32]),
             "smj_sampled_shards": (_U32, []),
             "smj_dev_materialize": (_U64, [_P, _P, _U64, _P, _U64, _P, _U64, _P]),
@@ -506,6 +512,34 @@ class Library:
             startS.data_ptr(), cntS.data_ptr(), startR.shape[1], bucket_bits, key_lo, key_hi,
             flags, sortedR.data_ptr(), sortedS.data_ptr(), count.data_ptr(),
             self.stream_ptr())
+
+    def dev_join_segmented_planes(self, R, strideR, nR, startR, cntR, S, strideS, nS, startS,
+                                  cntS, bucket_bits, key_lo, key_hi, sortedR, sortedS, count,
+                                  stage=None):
+        """smj_dev_join_segmented_tables on 48-bit words in two planes (R / S:
+        device buffers of 6 * stride bytes, smj_dev_partition_range_planes'
+        layout)."""
+        for t in (startR, cntR, startS, cntS):
+            assert t.is_contiguous() and t.shape == startR.shape
+        assert startR.shape[0] == 1 << bucket_bits
+        for X, st in ((R, strideR), (S, strideS)):
+            assert X.numel() * X.element_size() >= 6 * st and st % 32 == 0
+        flags = {None: 0, "R": 2, "REST": 4}[stage]
+        self.lib.smj_dev_join_segmented_planes(
+            self.ws, R.data_ptr(), strideR, nR, startR.data_ptr(), cntR.data_ptr(),
+            S.data_ptr(), strideS, nS, startS.data_ptr(), cntS.data_ptr(), startR.shape[1],
+            bucket_bits, key_lo, key_hi, flags, sortedR.data_ptr(), sortedS.data_ptr(),
+            count.data_ptr(), self.stream_ptr())
+
+    def dev_partition_range_planes(self, inp, out, stride, nbits, key_min, key_max, seg_start,
+                                   seg_cnt, flags):
+        """smj_dev_partition_range_planes: `out` a device buffer of 6 * stride
+        bytes; False when the form does not apply (nothing launched)."""
+        assert out.numel() * out.element_size() >= 6 * stride
+        return bool(self.lib.smj_dev_partition_range_planes(
+            self.ws, inp.data_ptr(), inp.shape[0], out.data_ptr(), stride, nbits, key_min,
+            key_max, seg_start.data_ptr(), seg_cnt.data_ptr(), flags.data_ptr(),
+            self.stream_ptr()))
 
     def sampled_capacity(self, n, nbits):
         return int(self.lib.smj_sampled_capacity(n, nbits))

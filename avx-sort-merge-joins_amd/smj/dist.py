@@ -52,6 +52,58 @@ INT64_MAX = (1 << 63) - 1
 # (profiles/r02_a2a_bisect.txt).  Larger exchanges go as chunked
 # point-to-point sends in one group.
 CHUNK_BYTES = int(os.environ.get("SMJ_A2A_CHUNK_MB", "512")) << 20
+# The exchange layouts, narrowest last: tuples, 64-bit packed words (16-byte
+# tuples only), 48-bit words in two planes (LayP48, both widths; the sampled
+# partition's LDS carries hold at most 2^9 partitions of them).  Both
+# relations of a step reach the local join in one layout.
+LAYOUTS = ("tuples", "words", "planes")
+PLANE_MAX_BITS = 9
+# a local bucket the tile pass / group pass take in stride: <= 192 tiles of
+# 8192 elements (choose_levels' bucket_cap in the library)
+LOCAL_BUCKET_CAP = 192 * 8192
+# the partition's not-packable bits (smj_common.hpp kBad*): 1 payload wider
+# than a 64-bit word holds, 2 key outside the plan, 4 payload wider than a
+# 48-bit word holds -- also what a rank where the planes form does not apply
+# reports (every rank then takes packed words)
+BAD_PAYLOAD, BAD_RANGE, BAD_PAYLOAD48 = 1, 2, 4
+
+
+class Planes:
+    """An exchange buffer of 48-bit words in two planes of one int32 buffer
+    (smj_dev_partition_range_planes): lo = int32[stride], then hi =
+    int16[stride]; element i is lo[i] | hi[i] << 32 (unsigned).  6 bytes an
+    element on the wire and in HBM instead of 8 (words) or 16 (tuples)."""
+
+    def __init__(self, stride: int, device=None):
+        assert stride % 32 == 0
+        self.stride = stride
+        self.buf = torch.empty(stride * 3 // 2, dtype=torch.int32, device=device)
+        self.lo = self.buf[:stride]
+        self.hi = self.buf[stride:].view(torch.int16)
+        self.planes = (self.lo, self.hi)
+
+    @property
+    def is_cuda(self):
+        return self.buf.is_cuda
+
+    @property
+    def device(self):
+        return self.buf.device
+
+    def data_ptr(self):
+        return self.buf.data_ptr()
+
+
+def _wire(t):
+    """A row piece as RCCL carries it (it has no 16-bit integer type: the hi
+    plane goes as bytes)."""
+    return t.view(torch.uint8) if t.dtype == torch.int16 else t
+
+
+def row_bytes(xb) -> int:
+    """Bytes one element of an exchange buffer takes (all planes)."""
+    planes = xb.planes if isinstance(xb, Planes) else (xb,)
+    return sum(p.element_size() * (p[0].numel() if p.dim() > 1 else 1) for p in planes)
 
 
 class _Works:
@@ -89,6 +141,21 @@ def range_digit(keys: torch.Tensor, key_min: int, key_max: int, bits: int) -> to
     L = max(key_max - key_min, 0).bit_length()
     rel = (keys.to(torch.int64) - key_min).clamp(0, (1 << L) - 1)
     return rel >> plan_shift(key_min, key_max, bits)
+
+
+def partition_bits(bucket_bits: int, world: int, planes: bool, n_hint=None) -> int:
+    """Exchange partition width: bucket_bits per rank (2^min(bucket_bits +
+    log2 G, 10) partitions), unless the 48-bit planes are offered and one bit
+    less keeps them: 2^9 partitions, when every rank's share (n_hint elements
+    per relation, balanced) still splits into local buckets of at most
+    LOCAL_BUCKET_CAP elements -- at 128M per rank, G = 2 and 4 (256 / 128
+    buckets, the 1-GPU join's own fanout-8 shape at G = 2), not 8."""
+    pbits = min(bucket_bits + ceil_log2(world), MAX_PARTITION_BITS)
+    if planes and pbits > PLANE_MAX_BITS and n_hint is not None:
+        lbits = PLANE_MAX_BITS - ceil_log2(world)
+        if lbits >= 6 and -(-n_hint // (1 << lbits)) <= LOCAL_BUCKET_CAP:
+            pbits = PLANE_MAX_BITS
+    return pbits
 
 
 def ceil_log2(x: int) -> int:
@@ -191,6 +258,10 @@ class DeviceOps:
     def __init__(self, lib):
         self.lib = lib
         self.can_pack = lib.width == 16 and os.environ.get("SMJ_PACK", "1") != "0"
+        # 48-bit words in two planes, as the 1-GPU join (SMJ_P48=0: off); a
+        # sampled form only, so SMJ_XSAMPLED=0 turns them off too
+        self.can_planes = (os.environ.get("SMJ_P48", "1") != "0"
+                           and os.environ.get("SMJ_XSAMPLED") != "0")
 
     def empty(self, n):
         return self.lib.empty(n)
@@ -232,8 +303,18 @@ class DeviceOps:
         return self.lib.dev_partition_range_sampled(inp, out, nbits, key_min, key_max, packed,
                                                     seg_start, seg_cnt, flags)
 
+    def partition_range_planes(self, inp, out, nbits, key_min, key_max, seg_start, seg_cnt,
+                               flags):
+        return self.lib.dev_partition_range_planes(inp, out.buf, out.stride, nbits, key_min,
+                                                   key_max, seg_start, seg_cnt, flags)
+
     def join_segmented_tables(self, R, nR, startR, cntR, S, nS, startS, cntS, bucket_bits,
                               key_lo, key_hi, sR, sS, count, packed=False, stage=None):
+        if isinstance(R, Planes):
+            self.lib.dev_join_segmented_planes(R.buf, R.stride, nR, startR, cntR, S.buf,
+                                               S.stride, nS, startS, cntS, bucket_bits,
+                                               key_lo, key_hi, sR, sS, count, stage=stage)
+            return
         self.lib.dev_join_segmented_tables(R, nR, startR, cntR, S, nS, startS, cntS,
                                            bucket_bits, key_lo, key_hi, sR, sS, count,
                                            packed=packed, stage=stage)
@@ -249,15 +330,20 @@ class DistributedJoin:
     """One process per device; `step` joins the local slices of R and S
     against the slices on all other ranks and leaves the GLOBAL match count in
     `count` on every rank.  `bucket_bits`: level-1 buckets per rank (2^9 =
-    512, what the 1-GPU join uses)."""
+    512, what the 1-GPU join uses); `n_hint`: elements per rank and relation,
+    identical on every rank (lets the 48-bit planes take 2^9 partitions
+    across ranks, partition_bits)."""
 
     def __init__(self, ops, bucket_bits: int, key_min: int, key_max: int,
-                 group=None):
+                 group=None, n_hint=None):
         self.ops = ops
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
-        self.pbits = min(bucket_bits + ceil_log2(self.world), MAX_PARTITION_BITS)
+        offers_planes = (bool(getattr(ops, "can_planes", False))
+                         and hasattr(ops, "partition_range_planes"))
+        # n_hint: elements per rank and relation (the same on every rank)
+        self.pbits = partition_bits(bucket_bits, self.world, offers_planes, n_hint)
         if os.environ.get("SMJ_XBITS"):  # rehearse the G-GPU partition width on fewer
             self.pbits = int(os.environ["SMJ_XBITS"])
         self.fanout = 1 << self.pbits
@@ -271,6 +357,10 @@ class DistributedJoin:
         self.p_lo, self.p_hi = owned(F, G, self.rank)
         cs = getattr(ops, "can_sample", False)
         self.sampled = bool(cs(self.world) if callable(cs) else cs)
+        # the first layout tried each step: the narrowest the ops offer
+        self.can_pack = bool(getattr(ops, "can_pack", False))
+        self.can_planes = offers_planes and self.pbits <= PLANE_MAX_BITS
+        self.layout = "planes" if self.can_planes else "words" if self.can_pack else "tuples"
         # segment-table width: the same on every rank whichever form a rank's
         # partition takes
         self.shards = ops.shards() if hasattr(ops, "shards") else 1
@@ -286,7 +376,8 @@ class DistributedJoin:
         self.recv_hint = {}  # remote rows received per relation and layout (sticky)
         self.last_recv = {}
         self.last_rows = {}
-        self.last_packed = False  # the layout of the last step's exchange
+        self.last_layout = "tuples"  # the layout of the last step's exchange
+        self.last_packed = False  # ... not tuples
         self.stats_reset()
 
     def stats_reset(self):
@@ -303,14 +394,22 @@ class DistributedJoin:
             self.buf[key] = b
         return b[:n]
 
-    def _xbuf(self, key, need, words, keep=0):
+    def _xbuf(self, key, need, lay, keep=0, dev=None):
         """The exchange buffer of one relation: the rank's own partition (its
         first `cap` elements) followed by the rows received from the other
         ranks, so the local join reads the rank's own rows in place.  Grows
         (sticky across steps) to `need` elements, keeping the first `keep`."""
         b = self.buf.get(key)
+        if lay == "planes":
+            if b is None or b.stride < need:
+                nb = Planes(-(-max(need, 1) // 32) * 32, device=dev)
+                if b is not None and keep:
+                    for p, q in zip(nb.planes, b.planes):
+                        p[:keep].copy_(q[:keep])
+                self.buf[key] = b = nb
+            return b
         if b is None or b.shape[0] < need:
-            nb = (self.ops.empty_words if words else self.ops.empty)(max(need, 1))
+            nb = (self.ops.empty_words if lay == "words" else self.ops.empty)(max(need, 1))
             if b is not None and keep:
                 nb[:keep].copy_(b[:keep])
             self.buf[key] = b = nb
@@ -360,30 +459,53 @@ class DistributedJoin:
             return None
         return ss.view(F, K), sc.view(F, K), flags
 
-    def _attempt(self, rel, key, packed, sampled):
+    def _planes(self, rel, xb, key):
+        """Sampled range partition of `rel` into the planes `xb` (48-bit
+        words); where the form does not apply on this rank, empty tables
+        flagged BAD_PAYLOAD48, so that every rank drops the layout together."""
+        dev = rel.device
+        F, K = self.fanout, self.shards
+        ss = self._small("ss" + key, (F * K,), dev=dev)
+        sc = self._small("sc" + key, (F * K,), dev=dev)
+        flags = self._small("fl" + key, (2,), torch.int32, dev)
+        if not self.ops.partition_range_planes(rel, xb, self.pbits, self.key_min,
+                                               self.key_max, ss, sc, flags):
+            ss.zero_()
+            sc.zero_()
+            flags[0] = 0
+            flags[1] = BAD_PAYLOAD48
+        return ss.view(F, K), sc.view(F, K), flags
+
+    def _attempt(self, rel, key, lay, sampled):
         """Enqueue one exchange attempt of `rel`: its range partition (sampled
-        or exact, packed words or tuples), the table messages (device), their
-        all-to-all and the receive tables, and an asynchronous copy of the
-        small summary the host needs.  Returns the attempt's state (nothing
-        has been waited for), or None when packed words do not apply at all."""
+        or exact; tuples, packed words, or 48-bit planes -- always sampled),
+        the table messages (device), their all-to-all and the receive tables,
+        and an asynchronous copy of the small summary the host needs.
+        Returns the attempt's state (nothing has been waited for), or None
+        when packed words do not apply at all."""
         G, me = self.world, self.rank
         dev = rel.device
         F, K = self.fanout, self.shards
         n = rel.shape[0]
         mine = self.p_hi - self.p_lo
         nb = 1 << self.lbits
-        xkey = ("xw" if packed else "xt") + key
+        sampled = sampled or lay == "planes"
+        xkey = {"tuples": "xt", "words": "xw", "planes": "xp"}[lay] + key
         cap = self.ops.sampled_capacity(n, self.pbits) if sampled else n
         # room for the remote rows: last step's, else an even share + 1/8
         extra = self.recv_hint.get(xkey, (cap * (G - 1)) // G + cap // 8 if G > 1 else 0)
-        xb = self._xbuf(xkey, cap + extra, packed)
-        part = xb[:cap]
-        res = self._sampled(rel, part, packed, key) if sampled else None
-        if res is None:  # exact partition (the receivers read either form)
-            cap = n if sampled else cap
-            res = self._partition(rel, part[:n], packed)
-            if res is None:
-                return None
+        xb = self._xbuf(xkey, cap + extra, lay, dev=dev)
+        if lay == "planes":
+            res = self._planes(rel, xb, key)
+        else:
+            packed = lay == "words"
+            part = xb[:cap]
+            res = self._sampled(rel, part, packed, key) if sampled else None
+            if res is None:  # exact partition (the receivers read either form)
+                cap = n if sampled else cap
+                res = self._partition(rel, part[:n], packed)
+                if res is None:
+                    return None
         start, cnt, fl = res
         xsend = getattr(self.ops, "xsend", xsend_torch)
         xrecv = getattr(self.ops, "xrecv", xrecv_torch)
@@ -417,16 +539,30 @@ class DistributedJoin:
             ev.record()
         else:
             hs, ev = summary, None
-        return dict(key=key, xkey=xkey, xb=xb, cap=cap, packed=packed, sampled=sampled,
-                    tstart=tstart, tcnt=tcnt, host=hs, ev=ev)
+        return dict(key=key, xkey=xkey, xb=xb, cap=cap, lay=lay, sampled=sampled,
+                    tstart=tstart, tcnt=tcnt, host=hs, ev=ev, dev=dev)
 
-    def _finish(self, rel, st, allow_pack=True):
+    def _next_layout(self, lay, sampled, bad, ovf):
+        """The layout and form an invalid attempt repeats with, on every rank
+        alike (bad and ovf are maxima over the ranks): a region overflow ->
+        exact partitions (planes have no exact form: words, else tuples);
+        a payload too wide for 48 bits -> words; anything else unpackable ->
+        tuples."""
+        if lay == "planes":
+            wide_only = bad and not bad & (BAD_PAYLOAD | BAD_RANGE)
+            lay = "words" if self.can_pack and (wide_only or not bad) else "tuples"
+            return lay, self.sampled and not ovf
+        if lay == "words" and bad:
+            lay = "tuples"
+        return lay, sampled and not ovf
+
+    def _finish(self, rel, st):
         """Wait for an attempt's summary; repeat the attempt until every rank
         agrees it is valid (a sampled region overflow anywhere -> every rank
-        partitions exactly; an unpackable tuple anywhere -> every rank sends
-        tuples), then start its row exchange.  Returns (exchange buffer, start
-        and count tables (2^lbits, world * K) for the local join, elements
-        inside the segments, async work, packed?)."""
+        partitions exactly; an unpackable tuple anywhere -> every rank takes
+        a wider layout), then start its row exchange.  Returns (exchange
+        buffer, start and count tables (2^lbits, world * K) for the local
+        join, elements inside the segments, async work, layout)."""
         G, me = self.world, self.rank
         key = st["key"] if st is not None else None
         while True:
@@ -436,19 +572,18 @@ class DistributedJoin:
                 host = st["host"].tolist()
                 cs, sl, rl, ru = host[:G], host[G:2 * G], host[2 * G:3 * G], host[3 * G:4 * G]
                 bad, ovf, gmax = host[4 * G:]
-                if not ovf and not (st["packed"] and bad):
+                if not ovf and not (st["lay"] != "tuples" and bad):
                     break
-                packed = st["packed"] and not bad
-                sampled = st["sampled"] and not ovf
+                lay, sampled = self._next_layout(st["lay"], st["sampled"], bad, ovf)
             else:  # packed words did not apply at all: tuples, on every rank
-                packed, sampled = False, self.sampled
-            st = self._attempt(rel, key, packed, sampled)
+                lay, sampled = "tuples", self.sampled
+            st = self._attempt(rel, key, lay, sampled)
         xkey, cap = st["xkey"], st["cap"]
         remote = sum(rl) - rl[me]
         self.recv_hint[xkey] = max(remote, self.recv_hint.get(xkey, 0))
-        xb = self._xbuf(xkey, cap + remote, st["packed"], keep=cap)
+        xb = self._xbuf(xkey, cap + remote, st["lay"], keep=cap, dev=st["dev"])
         grown = xb is not st["xb"]
-        row = 8 if st["packed"] else xb.element_size() * (xb.shape[1] if xb.dim() > 1 else 1)
+        row = row_bytes(xb)
         self.stats["sent_B"] += row * (sum(sl) - sl[me])
         self.stats["recv_B"] += row * remote
         self.stats["gap_B"] += row * (sum(rl) - sum(ru))
@@ -473,14 +608,14 @@ class DistributedJoin:
         self.last_recv[key] = (sl, rl)
         self.last_rows[key] = (xb, cap, cs, sl, rl, gmax)  # bench.py --op exchange repeats it
         self._ev_issue = ev
-        return xb, st["tstart"], st["tcnt"], sum(ru), work, st["packed"]
+        return xb, st["tstart"], st["tcnt"], sum(ru), work, st["lay"]
 
-    def _exchange(self, rel, key, allow_pack=True):
-        """One relation's exchange: attempt, wait, start the rows."""
-        packed = allow_pack and bool(getattr(self.ops, "can_pack", False))
-        st = self._attempt(rel, key, packed, self.sampled)
+    def _exchange(self, rel, key, lay=None):
+        """One relation's exchange in `lay` (default: the first layout) or a
+        wider one: attempt, wait, start the rows."""
+        st = self._attempt(rel, key, lay or self.layout, self.sampled)
         if st is None:
-            st = self._attempt(rel, key, False, self.sampled)
+            st = self._attempt(rel, key, "tuples", self.sampled)
         return self._finish(rel, st)
 
     def _rows(self, xb, cap, cs, sl, rl, gmax=None):
@@ -495,7 +630,9 @@ class DistributedJoin:
         me, G = self.rank, self.world
         if G == 1:
             return _Works([])
-        row = xb.element_size() * (xb[0].numel() if xb.dim() > 1 else 1)
+        # planes: the same element ranges of each plane, one transfer each
+        planes = xb.planes if isinstance(xb, Planes) else (xb,)
+        row = max(row_bytes(p) for p in planes)
         step = max(CHUNK_BYTES // row, 1)
         ro, roff = cap, []
         for g in range(G):
@@ -508,26 +645,29 @@ class DistributedJoin:
             works = []
             for k in range(max(rounds, 1)):
                 lo = k * step
-
-                def piece(start, n, g):
-                    if g == me or lo >= n:
-                        return xb[:0]
-                    return xb[start + lo:start + min(lo + step, n)]
-                ins = [piece(cs[g], sl[g], g) for g in range(G)]
-                outs = [piece(roff[g], rl[g], g) for g in range(G)]
-                works.append(dist.all_to_all(outs, ins, group=self._rgroup(), async_op=True))
+                for p in planes:
+                    def piece(start, n, g):
+                        if g == me or lo >= n:
+                            return _wire(p[:0])
+                        return _wire(p[start + lo:start + min(lo + step, n)])
+                    ins = [piece(cs[g], sl[g], g) for g in range(G)]
+                    outs = [piece(roff[g], rl[g], g) for g in range(G)]
+                    works.append(dist.all_to_all(outs, ins, group=self._rgroup(),
+                                                 async_op=True))
             return _Works(works)
         ops = []
         for g in range(G):
             if g == me:
                 continue
             peer = self._global(g)
-            for k in range(0, sl[g], step):
-                ops.append(dist.P2POp(dist.isend, xb[cs[g] + k:cs[g] + min(k + step, sl[g])],
-                                      peer, group=self._rgroup()))
-            for k in range(0, rl[g], step):
-                ops.append(dist.P2POp(dist.irecv, xb[roff[g] + k:roff[g] + min(k + step, rl[g])],
-                                      peer, group=self._rgroup()))
+            for p in planes:
+                for k in range(0, sl[g], step):
+                    ops.append(dist.P2POp(dist.isend, p[cs[g] + k:cs[g] + min(k + step, sl[g])],
+                                          peer, group=self._rgroup()))
+                for k in range(0, rl[g], step):
+                    ops.append(dist.P2POp(dist.irecv,
+                                          p[roff[g] + k:roff[g] + min(k + step, rl[g])],
+                                          peer, group=self._rgroup()))
         return _Works(dist.batch_isend_irecv(ops) if ops else [])
 
     def _global(self, g):
@@ -552,27 +692,27 @@ class DistributedJoin:
         R's rows are in (overlapping S's rows in flight), then S's tile stage,
         the group pass and the count (smj_dev_join_segmented_tables,
         SMJ_SEG_STAGE_R / _REST).  One rank: no rows travel, one call."""
-        packed = bool(getattr(self.ops, "can_pack", False))
-        aR = self._attempt(R, "R", packed, self.sampled)
+        aR = self._attempt(R, "R", self.layout, self.sampled)
         if aR is None:
-            aR = self._attempt(R, "R", False, self.sampled)
-        aS = self._attempt(S, "S", packed, self.sampled)
+            aR = self._attempt(R, "R", "tuples", self.sampled)
+        aS = self._attempt(S, "S", self.layout, self.sampled)
         if aS is None:
-            aS = self._attempt(S, "S", False, self.sampled)
+            aS = self._attempt(S, "S", "tuples", self.sampled)
         rR, tR, cR, nR, wR, pR = self._finish(R, aR)
         rS, tS, cS, nS, wS, pS = self._finish(S, aS)
         eS = self._ev_issue
         # both relations must reach the local join in one layout: the one
-        # that went out packed is exchanged again as tuples
-        if pR and not pS:
-            wR.wait()
-            rR, tR, cR, nR, wR, pR = self._exchange(R, "R", allow_pack=False)
-        elif pS and not pR:
-            wS.wait()
-            rS, tS, cS, nS, wS, pS = self._exchange(S, "S", allow_pack=False)
-            eS = self._ev_issue
-        assert pR == pS
-        self.last_packed = pR
+        # that went out narrower is exchanged again in the other's
+        while pR != pS:
+            if LAYOUTS.index(pR) > LAYOUTS.index(pS):
+                wR.wait()
+                rR, tR, cR, nR, wR, pR = self._exchange(R, "R", pS)
+            else:
+                wS.wait()
+                rS, tS, cS, nS, wS, pS = self._exchange(S, "S", pR)
+                eS = self._ev_issue
+        self.last_layout = pR
+        self.last_packed = pR != "tuples"
         if eS is not None:
             # S's row exchange alone: its completion on a stream of its own
             # (the compute stream runs R's tile stage meanwhile)
@@ -590,13 +730,13 @@ class DistributedJoin:
                 count)
         if self.world > 1 and self.staged:
             wR.wait()
-            self.ops.join_segmented_tables(*args, packed=pR, stage="R")
+            self.ops.join_segmented_tables(*args, packed=pR == "words", stage="R")
             wS.wait()
-            self.ops.join_segmented_tables(*args, packed=pR, stage="REST")
+            self.ops.join_segmented_tables(*args, packed=pR == "words", stage="REST")
         else:
             wR.wait()
             wS.wait()
-            self.ops.join_segmented_tables(*args, packed=pR)
+            self.ops.join_segmented_tables(*args, packed=pR == "words")
         if self.world > 1:
             dist.all_reduce(count, group=self.group)
         return sR, sS

@@ -418,7 +418,9 @@ def main():
             lib.dev_join(R, S, sR, sS, count, a.fanout_bits, 1, total)
     else:
         from smj.dist import DeviceOps, DistributedJoin
-        dj = DistributedJoin(DeviceOps(lib), a.fanout_bits, 1, total)
+        # n_hint: the same on every rank (the largest share)
+        dj = DistributedJoin(DeviceOps(lib), a.fanout_bits, 1, total,
+                             n_hint=total - total // N * (N - 1))
         last = [None, None]
 
         def step():
@@ -444,6 +446,7 @@ def main():
                 # with the rows (own rows included)
                 "slack_bytes_recv_per_gpu": st.get("gap_B", 0) // k,
                 "packed_words": bool(dj.last_packed),
+                "exchange_layout": dj.last_layout,
                 "exchange_S_ms": round(st["xS_ms"] / k, 3),
                 "exchange_S_GBps": round(st["sent_B"] / 2 / k / (st["xS_ms"] / k * 1e-3) / 1e9, 1)
                 if st["xS_ms"] > 0 and st["sent_B"] > 0 else None,
@@ -629,14 +632,15 @@ def run_exchange(a, json_out, N, rank, local):
     """The multi-GPU join's row exchange alone (numabench's memory bandwidth
     study, tputbench.c:665-1171, as xGMI bandwidth): S (--n tuples per GPU,
     default 128M, the join's slice) is range-partitioned once by
-    DistributedJoin (packed words for 16-byte tuples); one step repeats that
+    DistributedJoin (its first layout: 48-bit planes where the partition
+    width allows, else packed words for 16-byte tuples); one step repeats that
     exchange's row transfer -- DistributedJoin._rows, the join's own code
     path: list all-to-alls on the RCCL communicator in rounds of at most
     512 MB per peer, the own chunk read in place.  value = bytes that crossed to OTHER ranks, per
     GPU per second (N = 1: no row leaves the rank, nothing to time)."""
     import torch.distributed as dist
     import smj
-    from smj.dist import DeviceOps, DistributedJoin
+    from smj.dist import DeviceOps, DistributedJoin, row_bytes
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29533")
     os.environ.setdefault("RANK", "0")
@@ -650,12 +654,12 @@ def run_exchange(a, json_out, N, rank, local):
     lib.dev_gen_pk(R, n * rank, total, 12345)
     S = lib.empty(n)
     lib.dev_gen_fk(S, n * rank, total, total, 54321)
-    dj = DistributedJoin(DeviceOps(lib), a.fanout_bits, 1, total)
-    _, _, _, _, work, packed = dj._exchange(S, "S")
+    dj = DistributedJoin(DeviceOps(lib), a.fanout_bits, 1, total, n_hint=n)
+    _, _, _, _, work, lay = dj._exchange(S, "S")
     work.wait()
     torch.cuda.synchronize()
     xb, cap, cs, sl, rl, gmax = dj.last_rows["S"]
-    row = 8 if packed else 2 * xb.element_size()
+    row = row_bytes(xb)
 
     def step():
         dj._rows(xb, cap, cs, sl, rl, gmax).wait()
@@ -681,10 +685,11 @@ def run_exchange(a, json_out, N, rank, local):
             "value": round(per_gpu, 1) if per_gpu is not None else 0.0,
             "unit": "GB/s", "n_gpus": N, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(t * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "int64" if packed else ("int64" if w == 16 else "int32"),
+            "vs_baseline": None,
+            "dtype": {"words": "int64", "planes": "u48"}.get(lay, "int64" if w == 16 else "int32"),
             "data": "synthetic",
             "config": {"workload": f"row exchange of S (FK, {n} {w}-byte tuples per GPU"
-                                   f"{', as packed 8-byte words' if packed else ''}) "
+                                   f"{', as ' + lay if lay != 'tuples' else ''}, {row} B a row) "
                                    f"range-partitioned over {N} rank(s)",
                        "tuples_per_gpu": n, "parallelism": f"range-partition x{N}"},
             "roofline": ({"bound": "xgmi", "achieved": round(per_gpu, 1), "peak": xgmi_peak,

@@ -565,6 +565,20 @@ void smj_dev_join_segmented_tables(smj_workspace * ws, void * R, uint64_t nR,
                                    uint32_t flags, tuple_t * sortedR, tuple_t * sortedS,
                                    unsigned long long * count_dev, smj_stream_t stream);
 
+/* smj_dev_join_segmented_tables on 48-bit words in two planes (the layout
+ * smj_dev_partition_range_planes writes): X's element i is
+ * lo[i] | hi[i] << 32 with lo = (uint32_t *)X and hi = (uint16_t *)(lo +
+ * strideX); strideX a multiple of 32 elements.  flags: the stage bits only.
+ * Both tuple widths. */
+void smj_dev_join_segmented_planes(smj_workspace * ws, void * R, uint64_t strideR,
+                                   uint64_t nR, const int64_t * startR,
+                                   const int64_t * cntR, void * S, uint64_t strideS,
+                                   uint64_t nS, const int64_t * startS,
+                                   const int64_t * cntS, uint32_t nseg,
+                                   uint32_t bucket_bits, int64_t key_lo, int64_t key_hi,
+                                   uint32_t flags, tuple_t * sortedR, tuple_t * sortedS,
+                                   unsigned long long * count_dev, smj_stream_t stream);
+
 /* Range partition of smj_dev_partition_range by the 1-GPU join's sampled
  * scatter (no histogram pass; packed words when `packed`).  Partition p is
  * smj_sampled_shards() consecutive regions, p's before p + 1's; region
@@ -580,6 +594,20 @@ int smj_dev_partition_range_sampled(smj_workspace * ws, const tuple_t * in, uint
                                     int64_t key_max, int packed, int64_t * seg_start,
                                     int64_t * seg_cnt, unsigned int * flags,
                                     smj_stream_t stream);
+/* smj_dev_partition_range_sampled writing 48-bit words (both tuple widths,
+ * the 1-GPU join's LayP48): w = (key - base) mod 2^s1 << (48 - s1) | payload,
+ * s1 the partition width's bit count, payload as unsigned (8-byte tuples:
+ * its 32 bits), stored as two planes of `out`: lo = w mod 2^32 at
+ * (uint32_t *)out, hi = w >> 32 at (uint16_t *)((uint32_t *)out + stride);
+ * stride >= smj_sampled_capacity(n, nbits), a multiple of 32.  flags[1]
+ * gets 1 (payload wider than 64 - s1 bits), 2 (key outside the range) or 4
+ * (payload wider than 48 - s1 bits), or-ed.  Returns 0 (nothing launched)
+ * when the form does not apply: nbits > 9, n >= 2^32, or s1 outside 1..32. */
+int smj_dev_partition_range_planes(smj_workspace * ws, const tuple_t * in, uint64_t n,
+                                   void * out, uint64_t stride, uint32_t nbits,
+                                   int64_t key_min, int64_t key_max, int64_t * seg_start,
+                                   int64_t * seg_cnt, unsigned int * flags,
+                                   smj_stream_t stream);
 uint64_t smj_sampled_capacity(uint64_t n, uint32_t nbits);
 uint32_t smj_sampled_shards(void);
 

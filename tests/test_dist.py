@@ -20,14 +20,16 @@ from conftest import PKG, ROOT
 
 class HostOps:
     """Host stand-ins for DeviceOps (16-byte tuples as (n, 2) int64 rows; the
-    packed exchange as int64 words, like smj_dev_partition_range_packed)."""
+    packed exchange as int64 words, like smj_dev_partition_range_packed; 48-bit
+    words in two planes, like smj_dev_partition_range_planes)."""
 
     can_pack = True
     K = 3  # shards of the sampled layout (the device uses smj_sampled_shards())
 
-    def __init__(self, orc, sampled=True, overflow=False, not_applicable=False):
+    def __init__(self, orc, sampled=True, overflow=False, not_applicable=False, planes=True):
         self.orc = orc
         self.can_sample = sampled
+        self.can_planes = planes and sampled
         self.overflow = overflow  # report a region overflow from the sampled form
         self.not_applicable = not_applicable  # the sampled form returns False
 
@@ -46,6 +48,7 @@ class HostOps:
         F, K, n = 1 << nbits, self.K, inp.shape[0]
         if self.not_applicable:
             return False
+        flags.zero_()
         if packed:
             words = torch.empty(n, dtype=torch.int64)
             hist = torch.zeros(F, dtype=torch.int64)
@@ -59,6 +62,17 @@ class HostOps:
             vals[torch.argsort(d, stable=True)] = words
         else:
             vals = inp
+        pos, order = self._place(inp, nbits, key_min, key_max, seg_start, seg_cnt, flags)
+        out.fill_(-7)  # the slack must never be read
+        out[pos] = vals[order]
+        return True
+
+    def _place(self, inp, nbits, key_min, key_max, seg_start, seg_cnt, flags):
+        """The sampled layout's element positions: partition p is K
+        consecutive shard regions (shard = position / n * K), each followed by
+        slack; returns (positions, input order) and fills the tables."""
+        from smj.dist import range_digit
+        F, K, n = 1 << nbits, self.K, inp.shape[0]
         d = range_digit(inp[:, 1], key_min, key_max, nbits)
         q = torch.arange(n) * K // max(n, 1)
         idx = d * K + q
@@ -69,13 +83,58 @@ class HostOps:
         first = torch.cumsum(cnt, 0) - cnt
         si = idx[order]
         pos = start[si] + torch.arange(n) - first[si]
-        out.fill_(-7)  # the slack must never be read
-        out[pos] = vals[order]
         seg_start.copy_(start)
         seg_cnt.copy_(cnt)
         if self.overflow:
             flags[0] = 1
+        return pos, order
+
+    def partition_range_planes(self, inp, out, nbits, key_min, key_max, seg_start, seg_cnt,
+                               flags):
+        """smj_dev_partition_range_planes: the sampled layout of 48-bit words
+        w = (key - base) mod 2^s1 << (48 - s1) | payload, lo 32 bits in
+        out.lo, hi 16 in out.hi; flags[1] or-s 1 / 2 / 4 (payload over 64 -
+        s1 bits / key outside the range / payload over 48 - s1 bits)."""
+        if self.not_applicable or nbits > 9:
+            return False
+        s1 = self._s1(key_min, key_max, nbits)
+        if not 1 <= s1 <= 32:
+            return False
+        n = inp.shape[0]
+        assert out.stride >= self.sampled_capacity(n, nbits) and out.stride % 32 == 0
+        flags.zero_()
+        L = max(key_max - key_min, 0).bit_length()
+        k = inp[:, 1].numpy().astype(np.int64)
+        pu = inp[:, 0].numpy().astype(np.int64).view(np.uint64)
+        rel = (k - key_min).astype(np.uint64)
+        bad = 0
+        if ((k < key_min) | (rel > np.uint64((1 << L) - 1))).any():
+            bad |= 2
+        if (pu >> np.uint64(64 - s1)).any():
+            bad |= 1
+        if (pu >> np.uint64(48 - s1)).any():
+            bad |= 4
+        w = ((rel & np.uint64((1 << s1) - 1)) << np.uint64(48 - s1)) | \
+            (pu & np.uint64((1 << (48 - s1)) - 1))
+        pos, order = self._place(inp, nbits, key_min, key_max, seg_start, seg_cnt, flags)
+        flags[1] = bad
+        lo = torch.from_numpy((w & np.uint64(0xFFFFFFFF)).astype(np.uint32).view(np.int32))
+        hi = torch.from_numpy((w >> np.uint64(32)).astype(np.uint16).view(np.int16))
+        out.lo.fill_(-7)  # the slack must never be read
+        out.hi.fill_(-7)
+        out.lo[pos] = lo[order]
+        out.hi[pos] = hi[order]
         return True
+
+    @staticmethod
+    def _take(X, a, c):
+        """Elements [a, a + c) of an exchange buffer (planes: as int64 words)."""
+        from smj.dist import Planes
+        if isinstance(X, Planes):
+            lo = X.lo[a:a + c].numpy().view(np.uint32).astype(np.uint64)
+            hi = X.hi[a:a + c].numpy().view(np.uint16).astype(np.uint64)
+            return torch.from_numpy((lo | (hi << np.uint64(32))).view(np.int64))
+        return X[a:a + c]
 
     def join_segmented_tables(self, R, nR, startR, cntR, S, nS, startS, cntS, bucket_bits,
                               key_lo, key_hi, sR, sS, count, packed=False, stage=None):
@@ -92,6 +151,9 @@ class HostOps:
             self.staged_r = None
         else:
             self.whole_calls = getattr(self, "whole_calls", 0) + 1
+        from smj.dist import Planes
+        planes = isinstance(R, Planes)
+        assert planes == isinstance(S, Planes) and not (planes and packed)
         dense = []
         for X, n, st, ct in ((R, nR, startR, cntR), (S, nS, startS, cntS)):
             assert st.shape == ct.shape and st.shape[0] == 1 << bucket_bits
@@ -100,16 +162,16 @@ class HostOps:
                 for j in range(st.shape[1]):
                     a, c = int(st[b, j]), int(ct[b, j])
                     if c:
-                        rows.append(X[a:a + c])
+                        rows.append(self._take(X, a, c))
                         seg[0, b] += c
-            Xd = torch.cat(rows) if rows else X[:0]
+            Xd = torch.cat(rows) if rows else self._take(X, 0, 0)
             assert Xd.shape[0] == n
-            if not packed:
+            if not packed and not planes:
                 assert bool((Xd[:, 1] != -7).all()), "a gap was read"  # keys are >= 1
             dense.append((Xd, seg))
         (Rd, segR), (Sd, segS) = dense
         self.join_segmented(Rd, segR, Sd, segS, bucket_bits, key_lo, key_hi, sR, sS, count,
-                            packed=packed)
+                            packed=packed, bits=48 if planes else 64)
 
     def empty(self, n):
         return torch.empty((n, 2), dtype=torch.int64)
@@ -141,15 +203,15 @@ class HostOps:
         hist.copy_(torch.bincount(d, minlength=1 << nbits))
         return True
 
-    def _unpack(self, words, seg, key_lo, key_hi, bucket_bits):
+    def _unpack(self, words, seg, key_lo, key_hi, bucket_bits, bits=64):
         s1 = self._s1(key_lo, key_hi, bucket_bits)
         b = torch.repeat_interleave(torch.arange(seg.shape[1]).repeat(seg.shape[0]),
                                     seg.reshape(-1)).numpy().astype(np.uint64)
         w = words.numpy().view(np.uint64)
-        rel = (b << np.uint64(s1)) | (w >> np.uint64(64 - s1))
+        rel = (b << np.uint64(s1)) | (w >> np.uint64(bits - s1))
         rows = np.empty((len(w), 2), np.int64)
         rows[:, 1] = key_lo + rel.astype(np.int64)
-        rows[:, 0] = (w & np.uint64((1 << (64 - s1)) - 1)).astype(np.int64)
+        rows[:, 0] = (w & np.uint64((1 << (bits - s1)) - 1)).astype(np.int64)
         return torch.from_numpy(rows)
 
     def partition_range(self, inp, out, nbits, key_min, key_max, hist):
@@ -160,11 +222,11 @@ class HostOps:
         hist.copy_(torch.bincount(d, minlength=1 << nbits))
 
     def join_segmented(self, R, segR, S, segS, bucket_bits, key_lo, key_hi, sR, sS, count,
-                       packed=False):
+                       packed=False, bits=64):
         from smj.dist import range_digit
-        if packed:
-            R = self._unpack(R, segR, key_lo, key_hi, bucket_bits)
-            S = self._unpack(S, segS, key_lo, key_hi, bucket_bits)
+        if packed or bits == 48:
+            R = self._unpack(R, segR, key_lo, key_hi, bucket_bits, bits)
+            S = self._unpack(S, segS, key_lo, key_hi, bucket_bits, bits)
         # the receive layout the device join relies on: source by source,
         # local bucket b holds exactly the keys of local digit b
         for rows, seg in ((R, segR), (S, segS)):
@@ -182,12 +244,13 @@ class HostOps:
         count.fill_(c)
 
 
-def _worker(rank, world, port, n, q, s_payload="negative", mode="sampled"):
+def _worker(rank, world, port, n, q, s_payload="negative", mode="sampled", planes=True,
+            wide=False):
     import sys
     for p in (ROOT, PKG):
         sys.path.insert(0, p)
     import oracle
-    from smj.dist import DistributedJoin, owners, range_digit
+    from smj.dist import DistributedJoin, Planes, owners, range_digit
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}",
                             rank=rank, world_size=world)
@@ -205,6 +268,8 @@ def _worker(rank, world, port, n, q, s_payload="negative", mode="sampled"):
         S["payload"] = -np.arange(total) if s_payload == "negative" else np.arange(total)
         if s_payload == "r_negative":  # R cannot be packed, S can
             R["payload"] = -np.arange(total)
+        if s_payload == "wide48":  # 64-bit words hold S's payloads, 48-bit ones do not
+            S["payload"] = (1 << 45) + np.arange(total)
         expect = orc.merge_join(np.sort(R, order="key"), np.sort(S, order="key"))
 
         def rows(t):
@@ -214,13 +279,28 @@ def _worker(rank, world, port, n, q, s_payload="negative", mode="sampled"):
         # others sampled: receivers read either form), "overflow" (rank 1's
         # sampled regions overflow: every rank repeats exactly)
         ops = HostOps(orc, sampled=mode != "exact", overflow=mode == "overflow" and rank == 1,
-                      not_applicable=mode == "mixed" and rank == 0)
-        dj = DistributedJoin(ops, 6, 1, total)
+                      not_applicable=mode == "mixed" and rank == 0, planes=planes)
+        if wide:  # 2^9 buckets per rank: planes take 2^9 partitions across ranks
+            dj = DistributedJoin(ops, 9, 1, total, n_hint=n)
+            assert dj.pbits == (9 if ops.can_planes else 9 + (world > 1))
+        else:
+            dj = DistributedJoin(ops, 6, 1, total)
+        # the layout both relations reach the local join in: planes when the
+        # payloads fit 48-bit words on every rank (a rank where the planes do
+        # not apply, or a sampled overflow, sends every rank to words)
+        if s_payload in ("negative", "r_negative"):
+            want = "tuples"
+        elif s_payload == "wide48" or not ops.can_planes or mode in ("mixed", "overflow"):
+            want = "words"
+        else:
+            want = "planes"
+        assert dj.layout == ("planes" if ops.can_planes else "words")
         count = torch.zeros(1, dtype=torch.int64)
         for _ in range(2):  # second step reuses the grown buffers
             sR, sS = dj.step(rows(R), rows(S), count)
             assert int(count.item()) == expect
-            assert dj.last_packed == (s_payload == "rowid")
+            assert dj.last_layout == want, (dj.last_layout, want)
+            assert dj.last_packed == (want != "tuples")
         # the local join: two calls per step (R's tile stage while S's rows
         # fly, then the rest) across ranks unless SMJ_XSTAGED=0, one call on
         # one rank
@@ -239,15 +319,18 @@ def _worker(rank, world, port, n, q, s_payload="negative", mode="sampled"):
         # step's transfer again lands the same rows in the same places, and the
         # own chunk is never copied
         xb, cap, cs, sl, rl, gmax = dj.last_rows["S"]
+        assert isinstance(xb, Planes) == (want == "planes")
         remote = sum(rl) - rl[rank]
-        before = xb[:cap + remote].clone()
-        xb[cap:cap + remote] = -9
+        planes_ = xb.planes if isinstance(xb, Planes) else (xb,)
+        before = [p[:cap + remote].clone() for p in planes_]
+        for p in planes_:
+            p[cap:cap + remote] = -9
         dj._rows(xb, cap, cs, sl, rl, gmax).wait()
         # every rank agrees on the largest message (the RCCL rounds)
         t = torch.tensor([gmax])
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         assert int(t) == gmax >= max(sl + rl)
-        assert torch.equal(xb[:cap + remote], before)
+        assert all(torch.equal(p[:cap + remote], b) for p, b in zip(planes_, before))
         # no row lost or duplicated
         sizes = torch.tensor([sR.shape[0], sS.shape[0]])
         dist.all_reduce(sizes)
@@ -276,24 +359,35 @@ def _free_port():
     (2, None, "rowid", "exact"), (3, None, "negative", "exact"),
     (3, None, "rowid", "mixed"), (2, None, "negative", "mixed"),
     (3, None, "rowid", "overflow"), (2, None, "rowid", "sampled-onecall"),
-    (3, None, "negative", "exact-onecall")])
+    (3, None, "negative", "exact-onecall"),
+    (1, None, "wide48", "sampled"), (2, None, "wide48", "sampled"),
+    (2, 0, "rowid", "sampled-noplanes"), (3, None, "rowid", "sampled-noplanes"),
+    (1, None, "rowid", "sampled-noplanes"), (2, None, "rowid", "sampled-wide"),
+    (2, None, "rowid", "sampled-noplanes-wide")])
 def test_distributed_join_gloo(world, chunk_mb, s_payload, mode, oracles, monkeypatch):
     """chunk_mb 0: every row message over the chunk limit, so the exchange
     takes the chunked isend/irecv path (the one RCCL needs for >1 GiB).
     mode: the exchange partition's form (sampled with gaps, exact, a mix of
     the two, or a sampled overflow that sends every rank back to exact).
-    s_payload "rowid": both relations exchanged as packed words; "negative":
-    S cannot be packed, every rank falls back to tuples for both; "r_negative":
-    R cannot be packed but S can (S goes again, as tuples)."""
+    s_payload "rowid": both relations exchanged as 48-bit planes (packed
+    words with "-noplanes" ops, a rank where the planes do not apply, or an
+    overflow); "negative": S cannot be packed, every rank falls back to tuples
+    for both; "r_negative": R cannot be packed but S can (S goes again, as
+    tuples); "wide48": S's payloads need 64-bit words (both go as words)."""
     if chunk_mb is not None:
         monkeypatch.setenv("SMJ_A2A_CHUNK_MB", str(chunk_mb))
     if mode.endswith("-onecall"):  # the local join in one call (no staging)
         monkeypatch.setenv("SMJ_XSTAGED", "0")
         mode = mode[:-len("-onecall")]
+    planes = not mode.endswith("-noplanes")  # ops without the 48-bit planes
+    mode = mode.replace("-noplanes", "")
+    wide = mode.endswith("-wide")  # 2^9 buckets per rank and an n hint
+    mode = mode.replace("-wide", "")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, 5000, q, s_payload, mode))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, 5000, q, s_payload, mode,
+                                               planes, wide))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -349,3 +443,22 @@ def test_local_range_int64_edges():
                     assert klo == b + (p_lo << gs1)
                 assert (1 << lbits) >= p_hi - p_lo
             assert kmax - base < (1 << max(kmax - kmin, 0).bit_length())
+
+
+def test_partition_bits():
+    """The exchange's partition width: bucket_bits + log2 G up to 2^10, or
+    2^9 where the 48-bit planes then fit and every rank's local buckets stay
+    within LOCAL_BUCKET_CAP (128M per rank: G = 2, 4; not 8)."""
+    import sys
+    sys.path.insert(0, PKG)
+    from smj.dist import partition_bits
+    n = 128_000_000
+    assert partition_bits(9, 1, True, n) == 9
+    assert partition_bits(9, 2, False, n) == 10
+    assert partition_bits(9, 2, True, None) == 10  # no hint: the default width
+    assert partition_bits(9, 2, True, n) == 9
+    assert partition_bits(9, 4, True, n) == 9
+    assert partition_bits(9, 8, True, n) == 10  # 2^6 buckets of 2M > the cap
+    assert partition_bits(9, 8, True, n // 2) == 9
+    assert partition_bits(6, 3, True, n) == 8
+    assert partition_bits(9, 16, True, 1000) == 10  # fewer than 2^6 local buckets

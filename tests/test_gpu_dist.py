@@ -100,9 +100,9 @@ def test_segmented_join_simulated_exchange(libs, oracles, width, world, kind, pa
 
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
 @pytest.mark.parametrize("kind", ["pk_fk", "zipf"])
-@pytest.mark.parametrize("packed", [False, True])
+@pytest.mark.parametrize("layout", ["tuples", "words", "planes"])
 @pytest.mark.parametrize("staged", [False, True], ids=["onecall", "staged"])
-def test_sampled_exchange_simulated(libs, oracles, width, world, kind, packed, staged):
+def test_sampled_exchange_simulated(libs, oracles, width, world, kind, layout, staged):
     """The sampled exchange partition (smj_dev_partition_range_sampled: K shard
     regions per partition, slack between them) simulated on one GPU: rank g
     receives from every source the chunk [start of its first owned region,
@@ -110,10 +110,13 @@ def test_sampled_exchange_simulated(libs, oracles, width, world, kind, packed, s
     through smj_dev_join_segmented_tables with the sources' region tables.
     staged: the join in two calls (SMJ_SEG_STAGE_R, then _REST), S's receive
     buffer holding garbage during the first (the multi-GPU join runs R's tile
-    stage while S's rows are still in flight)."""
+    stage while S's rows are still in flight).  layout "planes": 48-bit words
+    in two planes (smj_dev_partition_range_planes and
+    smj_dev_join_segmented_planes), both widths."""
     import torch
-    from smj.dist import ceil_log2, owned, plan_shift
+    from smj.dist import Planes, ceil_log2, owned, plan_shift
     orc, lib = oracles[width], libs[width]
+    packed = layout == "words"
     if packed and width != 16:
         pytest.skip("packed words are the 16-byte layout")
     if staged and world == 1:
@@ -131,12 +134,19 @@ def test_sampled_exchange_simulated(libs, oracles, width, world, kind, packed, s
             sl = rel[s * n // world:(s + 1) * n // world]
             d_in = lib.to_device(sl)
             cap = lib.sampled_capacity(len(sl), pbits)
-            out = (torch.full((cap,), -7, dtype=torch.int64, device="cuda") if packed
-                   else lib.empty(cap))
             ss = torch.empty(F * K, dtype=torch.int64, device="cuda")
             sc = torch.empty(F * K, dtype=torch.int64, device="cuda")
             fl = torch.ones(2, dtype=torch.int32, device="cuda")
-            assert lib.dev_partition_range_sampled(d_in, out, pbits, 1, n, packed, ss, sc, fl)
+            if layout == "planes":
+                out = Planes(-(-cap // 32) * 32, device="cuda")
+                out.buf.fill_(-7)
+                assert lib.dev_partition_range_planes(d_in, out.buf, out.stride, pbits, 1, n,
+                                                      ss, sc, fl)
+            else:
+                out = (torch.full((cap,), -7, dtype=torch.int64, device="cuda") if packed
+                       else lib.empty(cap))
+                assert lib.dev_partition_range_sampled(d_in, out, pbits, 1, n, packed, ss, sc,
+                                                       fl)
             torch.cuda.synchronize()
             assert fl.tolist() == [0, 0]
             assert int(sc.sum()) == len(sl)
@@ -159,12 +169,19 @@ def test_sampled_exchange_simulated(libs, oracles, width, world, kind, packed, s
                 out, ss, sc = parts[key, s]
                 c0 = int(ss[p_lo, 0])
                 c1 = int(ss[p_hi, 0]) if p_hi < F else int((ss + sc).max())
-                rows.append(out[c0:c1])
+                rows.append([p[c0:c1] for p in out.planes] if layout == "planes"
+                            else out[c0:c1])
                 tst.append(ss[p_lo:p_hi] - c0 + base)
                 tct.append(sc[p_lo:p_hi])
                 base += c1 - c0
                 nused += int(sc[p_lo:p_hi].sum())
-            recv[key] = torch.cat(rows).contiguous()
+            if layout == "planes":  # the chunks back to back in both planes
+                rb = Planes(-(-max(base, 1) // 32) * 32, device="cuda")
+                for i in range(2):
+                    rb.planes[i][:base].copy_(torch.cat([r[i] for r in rows]))
+                recv[key] = rb
+            else:
+                recv[key] = torch.cat(rows).contiguous()
             st_ = torch.zeros(1 << lbits, world * K, dtype=torch.int64, device="cuda")
             ct_ = torch.zeros_like(st_)
             st_[:mine] = torch.stack(tst, 1).reshape(mine, world * K)
@@ -173,17 +190,28 @@ def test_sampled_exchange_simulated(libs, oracles, width, world, kind, packed, s
             used[key] = nused
         sR, sS = lib.empty(used["R"]), lib.empty(used["S"])
         cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
-        args = (recv["R"], used["R"], *tabs["R"], recv["S"], used["S"], *tabs["S"], lbits,
-                key_lo, key_hi, sR, sS, cnt)
-        if staged:
-            s_rows = recv["S"].clone()
-            recv["S"].fill_(-3)  # S has not arrived yet
-            lib.dev_join_segmented_tables(*args, packed=packed, stage="R")
-            torch.cuda.synchronize()
-            recv["S"].copy_(s_rows)
-            lib.dev_join_segmented_tables(*args, packed=packed, stage="REST")
+        if layout == "planes":
+            rR, rS = recv["R"], recv["S"]
+            args = (rR.buf, rR.stride, used["R"], *tabs["R"], rS.buf, rS.stride, used["S"],
+                    *tabs["S"], lbits, key_lo, key_hi, sR, sS, cnt)
+            join = lib.dev_join_segmented_planes
+            s_buf = rS.buf
         else:
-            lib.dev_join_segmented_tables(*args, packed=packed)
+            args = (recv["R"], used["R"], *tabs["R"], recv["S"], used["S"], *tabs["S"],
+                    lbits, key_lo, key_hi, sR, sS, cnt)
+
+            def join(*a, stage=None):
+                lib.dev_join_segmented_tables(*a, packed=packed, stage=stage)
+            s_buf = recv["S"]
+        if staged:
+            s_rows = s_buf.clone()
+            s_buf.fill_(-3)  # S has not arrived yet
+            join(*args, stage="R")
+            torch.cuda.synchronize()
+            s_buf.copy_(s_rows)
+            join(*args, stage="REST")
+        else:
+            join(*args)
         torch.cuda.synchronize()
         lo_k, hi_k = 1 + (p_lo << s1), 1 + (p_hi << s1)
         mR = R[(R["key"] >= lo_k) & (R["key"] < hi_k)] if g < world - 1 else R[R["key"] >= lo_k]
@@ -226,7 +254,10 @@ def test_distributed_join_one_rank_rccl(libs, width, xsampled, monkeypatch):
             sR, sS = dj.step(R, S, count)
             torch.cuda.synchronize()
             assert int(count.item()) == n
-            assert dj.last_packed == (width == 16)
+            # one rank: 48-bit planes unless the exact partition is forced
+            # (planes are a sampled form); else packed words at 16 bytes
+            want = "planes" if xsampled == "1" else "words" if width == 16 else "tuples"
+            assert dj.last_layout == want
         ref = torch.sort(S[:, 1].to(torch.int64)).values
         assert torch.equal(sS[:, 1].to(torch.int64), ref)
         assert torch.equal(sR[:, 1].to(torch.int64), torch.arange(1, n + 1, device="cuda"))
