@@ -148,8 +148,9 @@ def partition_bits(bucket_bits: int, world: int, planes: bool, n_hint=None) -> i
     log2 G, 10) partitions), unless the 48-bit planes are offered and one bit
     less keeps them: 2^9 partitions, when every rank's share (n_hint elements
     per relation, balanced) still splits into local buckets of at most
-    LOCAL_BUCKET_CAP elements -- at 128M per rank, G = 2 and 4 (256 / 128
-    buckets, the 1-GPU join's own fanout-8 shape at G = 2), not 8."""
+    LOCAL_BUCKET_CAP elements -- at 128M per rank and bucket_bits 9, G = 2
+    and 4 (256 / 128 local buckets; 256 is the 1-GPU join's own fan-out-8
+    shape), not 8; at bucket_bits 8 (bench.py's default) G = 4."""
     pbits = min(bucket_bits + ceil_log2(world), MAX_PARTITION_BITS)
     if planes and pbits > PLANE_MAX_BITS and n_hint is not None:
         lbits = PLANE_MAX_BITS - ceil_log2(world)
