@@ -476,11 +476,14 @@ k_scatter_swc(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
 // for the first form of this scatter, against 1.46 / 1.51 ms for
 // k_scatter_swc (ballot ranks) and 0.84 ms for the same atomic ranks without
 // the carry (34 % extra write bytes, 41 % partial write requests).
+#ifndef SMJ_SWP_SEG
+#define SMJ_SWP_SEG 64  // bytes a segment of the stable scatter
+#endif
 template <int THREADS, int ITEMS>
 struct SwaGeom {
     static constexpr int W = THREADS / 64;
     static constexpr int TILE = THREADS * ITEMS;
-    static constexpr uint32_t SEG = 64 / sizeof(Tup);
+    static constexpr uint32_t SEG = SMJ_SWP_SEG / sizeof(Tup);
     static constexpr uint32_t CW = SEG - 1;
     // stage Tup[TILE] | carry Tup[B][CW] | counters u32[W][B/2] | info u32x4[B] |
     // segown u16[TILE/SEG + 2B] | scan scratch

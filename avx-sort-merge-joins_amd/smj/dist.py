@@ -526,9 +526,10 @@ class DistributedJoin:
             dist.all_to_all_single(msg, inp, [HEAD + 2 * mine * K] * G, per_in,
                                    group=self.group)
         xrecv(msg, chunk, G, me, mine, K, tstart, tcnt, cap, summary)
-        # every rank must run the same number of row all-to-all rounds
-        summary[4 * G + 2:] = summary[G:3 * G].max()
+        # every rank must run the same number of row all-to-all rounds (one
+        # rank: no rows travel, the entry stays unread)
         if G > 1:
+            summary[4 * G + 2:] = summary[G:3 * G].max()
             dist.all_reduce(summary[4 * G + 2:], op=dist.ReduceOp.MAX, group=self.group)
         if summary.is_cuda:
             hs = self.buf.get("xhost" + key)
@@ -573,6 +574,8 @@ class DistributedJoin:
                 host = st["host"].tolist()
                 cs, sl, rl, ru = host[:G], host[G:2 * G], host[2 * G:3 * G], host[3 * G:4 * G]
                 bad, ovf, gmax = host[4 * G:]
+                if G == 1:  # not computed on one rank (no rows travel)
+                    gmax = max(sl[0], rl[0])
                 if not ovf and not (st["lay"] != "tuples" and bad):
                     break
                 lay, sampled = self._next_layout(st["lay"], st["sampled"], bad, ovf)
@@ -699,6 +702,10 @@ class DistributedJoin:
         aS = self._attempt(S, "S", self.layout, self.sampled)
         if aS is None:
             aS = self._attempt(S, "S", "tuples", self.sampled)
+        if self.world == 1:
+            done = self._one_rank(aR, aS, count)
+            if done is not None:
+                return done
         rR, tR, cR, nR, wR, pR = self._finish(R, aR)
         rS, tS, cS, nS, wS, pS = self._finish(S, aS)
         eS = self._ev_issue
@@ -740,6 +747,39 @@ class DistributedJoin:
             self.ops.join_segmented_tables(*args, packed=pR == "words")
         if self.world > 1:
             dist.all_reduce(count, group=self.group)
+        return sR, sS
+
+    def _one_rank(self, aR, aS, count):
+        """One rank, both attempts valid in one layout (the usual case): no
+        rows travel, so the local join is issued right after the summaries
+        arrive, without the row streams and events of the general path.
+        Returns None (nothing issued) otherwise."""
+        hs = []
+        for st in (aR, aS):
+            if st["ev"] is not None:
+                st["ev"].synchronize()
+            h = st["host"].tolist()
+            bad, ovf = h[4], h[5]
+            if ovf or (st["lay"] != "tuples" and bad):
+                return None
+            hs.append(h)
+        if aR["lay"] != aS["lay"]:
+            return None
+        lay = aR["lay"]
+        nR, nS = hs[0][3], hs[1][3]  # elements inside the segments
+        sR = self._grow("sortR", nR)
+        sS = self._grow("sortS", nS)
+        self.ops.join_segmented_tables(aR["xb"], nR, aR["tstart"], aR["tcnt"], aS["xb"], nS,
+                                       aS["tstart"], aS["tcnt"], self.lbits, self.key_lo,
+                                       self.key_hi, sR, sS, count, packed=lay == "words")
+        self.last_layout = lay
+        self.last_packed = lay != "tuples"
+        for st, h in zip((aR, aS), hs):
+            self.last_recv[st["key"]] = ([h[1]], [h[2]])
+            self.last_rows[st["key"]] = (st["xb"], st["cap"], [h[0]], [h[1]], [h[2]],
+                                         max(h[1], h[2]))
+            self.stats["gap_B"] += row_bytes(st["xb"]) * (h[2] - h[3])
+        self.stats["steps"] += 1
         return sR, sS
 
     def _side_stream(self):
