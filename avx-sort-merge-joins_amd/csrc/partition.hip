@@ -1233,10 +1233,18 @@ k_sample_hist(SampleRel S, uint32_t stride, Digit dig_arg, uint32_t nbins) {
 // workgroups, blockIdx % kShards), so that the reservation atomics of a
 // partition are spread over kShards cursors (kShards: smj_internal.hpp).
 
-// Write unit of the sampled scatter: every store writes whole segments of
-// this many bytes (128 = one L2 line: no partially written lines).
+// Write unit of the sampled scatter: a partition's run of a tile is written
+// in whole segments of this many bytes (of the first plane), the rest waits in
+// the partition's LDS carry for the next tile.  Round 4, with the 48-bit
+// layout (tools/r04_sclab.sh, two interleaved rounds on one box,
+// profiles/r04_lab/sclab_b.txt, sclab_c.txt): 64 -> 16 bytes took the 16-byte
+// join 3.34 / 3.30 -> 3.14 / 3.15 ms, the 8-byte join 2.77 / 2.76 -> 2.68 /
+// 2.68, the 8-byte sort 1.50 / 1.53 -> 1.45 / 1.48 (k_scatter -0.06 to -0.1
+// ms): the runs are as long either way (one per partition and tile), the
+// carries and their per-tile copies shrink.  8 bytes: the scatter no faster,
+// the 16-byte join's group pass 0.1 ms slower; 32 between 64 and 16.
 #ifndef SMJ_SC_SEG
-#define SMJ_SC_SEG 64
+#define SMJ_SC_SEG 16
 #endif
 constexpr uint32_t kSegBytes = SMJ_SC_SEG;
 constexpr uint32_t kRegionAlign = 128;  // bytes; a multiple of kSegBytes
@@ -1333,7 +1341,7 @@ k_regions_done(RegionRel R, uint32_t nbins, unsigned int* __restrict__ flag) {
 // kSegBytes of that plane; one plane for every layout but LayP48)
 template <int THREADS, int ITEMS, class OutT, uint32_t SB = sizeof(OutT)>
 struct ScatterGeom {
-    static constexpr uint32_t SEG = kSegBytes / SB;  // elements per segment
+    static constexpr uint32_t SEG = kSegBytes >= SB ? kSegBytes / SB : 1;  // elements per segment
     static constexpr uint32_t TILE = THREADS * ITEMS;
     static __host__ __device__ constexpr uint32_t max_segs(uint32_t nbins) {
         return (TILE + nbins * (SEG - 1)) / SEG;

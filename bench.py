@@ -719,7 +719,11 @@ def partition_check(R, out, hist, off, bits, shift, w):
     pid = torch.repeat_interleave(torch.arange(fan, device="cuda"), hist)
     base = torch.cumsum(hist, 0) - hist
     pos = off[pid] + torch.arange(n, device="cuda") - base[pid]
-    rows = out[pos]
+    # gathered in chunks: one 2^27-row gather of 16-byte rows exceeds the
+    # launch configuration torch's index kernel accepts on this part
+    rows = torch.empty((n,) + tuple(out.shape[1:]), dtype=out.dtype, device=out.device)
+    for i in range(0, n, 1 << 24):
+        rows[i:i + (1 << 24)] = out.index_select(0, pos[i:i + (1 << 24)])
     mask = ((1 << bits) - 1) << shift
     dig = ((rows[:, 1].to(torch.int64) - 1) & mask) >> shift
     res["digits"] = bool((dig == pid).all().item())

@@ -10,7 +10,7 @@
 # that PART=1 left in profiles/ (tools/r03_collect.sh).
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
-O=gpurun_out/r04_fin
+O=${O:-gpurun_out/r04_fin}
 mkdir -p $O
 if [ "${PART:-1}" = 1 ]; then
   if [ -z "${SKIP_SUITE:-}" ]; then
@@ -20,7 +20,7 @@ if [ "${PART:-1}" = 1 ]; then
   timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.txt 2>&1 || { cat $O/smoke.txt; exit 1; }
   bash tools/r03_lines.sh $O "join16:--steps 10 --warmup 2" "join8:--width 8 --steps 10 --warmup 2" "zipf16:--dist zipf --steps 10 --warmup 2" || exit 1
 else
-  O2=gpurun_out/r04_fin2
+  O2=${O2:-gpurun_out/r04_fin2}
   bash tools/r03_lines.sh $O2 "sort8:--op sort --width 8 --steps 10 --warmup 2" "part8:--op partition --width 8 --steps 10 --warmup 2" "merge8:--op merge --steps 20 --warmup 3" || exit 1
   NO_PMC=1 CPU_ARGS=--no-cpu-baseline bash tools/r03_lines.sh $O2/nopmc "api16:--api --steps 10 --warmup 2" "xpath16:--exchange-path --steps 10 --warmup 2" "join16:--steps 10 --warmup 2" || exit 1
   # SQ counters of the 8-byte join (the group pass's wait share)

@@ -8,12 +8,17 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=${OUT:-gpurun_out/r04_sclab}; mkdir -p $O
 for rep in ${REPS:-1 2}; do
-  for b in "--steps 10" "--width 8 --steps 10" "--op sort --width 8 --steps 10"; do
+  # LINES: bench arguments, one line per config (default: the 16 B and 8 B
+  # joins and the 8 B sort)
+  while IFS= read -r b; do
+    [ -z "$b" ] && continue
     for v in base ${VARIANTS:-s2 s3 s4}; do
       if [ $v = base ]; then unset SMJ_LIB_DIR; else export SMJ_LIB_DIR=avx-sort-merge-joins_amd/lib_$v; fi
-      timeout -k 10 200 python3 bench.py $b --no-cpu-baseline > $O/b.json 2> $O/b.err || { echo "FAIL $v $b"; tail -5 $O/b.err; exit 1; }
+      timeout -k 10 200 python3 bench.py $b --no-cpu-baseline < /dev/null > $O/b.json 2> $O/b.err || { echo "FAIL $v $b"; tail -5 $O/b.err; exit 1; }
       python3 -c "import json; d=json.load(open('$O/b.json')); print('$rep', '$v', '$b', '|', d['ms_per_step'], 'ms', 'ok' if d.get('result_ok') else 'BAD', {k: v for k, v in d['detail']['kernels_ms_per_step'].items()})"
     done
-  done
+  done <<< "${LINES:-"--steps 10
+--width 8 --steps 10
+--op sort --width 8 --steps 10"}"
 done
 unset SMJ_LIB_DIR
