@@ -6,7 +6,8 @@
 // After the level-1 radix partition (partition.hip) every bucket b holds the
 // tuples whose key falls in one contiguous key range of the RangePlan.
 //
-//   k_tilepass  : every bucket is cut into tiles of TILE2 tuples.  A tile is
+//   k_tilepass  : every bucket is cut into tiles (tile_elems: 16384 8-byte
+//                 elements, 8192 16-byte tuples).  A tile is
 //                 loaded into registers, counted by its level-2 digit d2 (the
 //                 "group") in an LDS histogram, staged in LDS grouped by d2 and
 //                 written back linearly (fully coalesced), together with the
@@ -37,8 +38,15 @@
 
 namespace smj {
 
+// tile-pass workgroup: TP_THREADS threads, tp_items<W>() elements each
+// (tile_elems below: 16384 8-byte elements, 8192 16-byte ones).  Round 4 with
+// the 48-bit layout (tools/r04_sclab.sh, profiles/r04_lab/tilelab.txt, two
+// interleaved rounds on one box): 16384-element tiles against 8192 took the
+// 16-byte join 3.29 -> 3.22 ms, the 8-byte join 2.69 -> 2.64, the 8-byte sort
+// 1.48 -> 1.46 (the group pass gathers runs twice as long: -0.03 to -0.08 ms;
+// the tile pass +0.02).  Round 3, with 64-bit words, had measured the reverse.
 #ifndef SMJ_TP_THREADS
-#define SMJ_TP_THREADS 512
+#define SMJ_TP_THREADS 1024
 #endif
 constexpr int TP_THREADS = SMJ_TP_THREADS;
 // group pass: digit-major prefix table (k_preft) and non-temporal gathers
@@ -61,9 +69,20 @@ constexpr int TP_THREADS = SMJ_TP_THREADS;
 #define SMJ_GS_ABL 0  // ablations for measurements only (1: no in-group sort; 2: no
                       // equal-digit run fixing; 3: no write-out)
 #endif
-constexpr int TP_ITEMS = 16;
-constexpr int TILE2 = TP_THREADS * TP_ITEMS;  // tuples per tile
-const uint32_t kTileTuples = TILE2;
+// elements a tile-pass thread holds: the stage of a tile is 128 KB of LDS
+// (16-byte elements: 16-byte tuples in their own layout take half the tile)
+template <class W>
+constexpr int tp_items() {
+    return (int)(128 * 1024 / sizeof(W)) / TP_THREADS;
+}
+template <class W>
+constexpr uint32_t tile_elems() {
+    return (uint32_t)(TP_THREADS * tp_items<W>());
+}
+static_assert(tile_elems<uint64_t>() <= 65535 + 1, "u16 prefix rows");
+// the bucket-size unit of the plan (choose_levels): 8192 elements, fixed
+// when the tiles grew (round 4) so that the plans stay as measured
+const uint32_t kTileTuples = 8192;
 
 #ifndef SMJ_GS_THREADS
 #define SMJ_GS_THREADS 256
@@ -82,7 +101,8 @@ constexpr int gs_wg_per_cu() {
     return sizeof(W) == 16 ? SMJ_GS_WG_PER_CU : SMJ_GS_WG_PER_CU8;
 }
 // 2560 elements per relation: the plan's groups average 2048, so a group's
-// run in an 8192-element tile is ~64 words (512 B) and the gathers waste less
+// run in an 8192-element tile was ~64 words (512 B; 16384-element tiles since
+// round 4: ~128) and the gathers waste less
 // of the partial 128-byte lines at run ends than with 1280 (1024 on average,
 // 256 B runs): 128M x 128M join, group pass 16 B 1.50 -> 1.39 ms, 8 B 1.29 ->
 // 1.16 ms; 3072 loses (3 workgroups per CU)
@@ -127,23 +147,23 @@ struct OvfEntry {
 
 // ---------------------------------------------------------------------------
 // tile table: block b writes the tiles of bucket b, numbered from btile0[b]
-// (uploaded by the host): consecutive TILE2 chunks of each of its segments
+// (uploaded by the host): consecutive tsz-element chunks of each of its segments
 // (one segment = the whole bucket, or kShards of a sampled partition).
 __global__ void __launch_bounds__(64)
 k_tiles(const uint64_t* __restrict__ bstart, const int64_t* __restrict__ bcount,
         const uint64_t* __restrict__ seg_start, const int64_t* __restrict__ seg_cnt,
-        uint32_t nseg, TileTable tt) {
+        uint32_t nseg, TileTable tt, uint32_t tsz) {
     const uint32_t b = blockIdx.x;
     uint32_t t0 = tt.btile0[b];
     for (uint32_t q = 0; q < nseg; q++) {
         const uint64_t s0 = seg_start ? seg_start[(size_t)b * nseg + q] : bstart[b];
         const int64_t cnt = seg_cnt ? seg_cnt[(size_t)b * nseg + q] : bcount[b];
-        const uint32_t nt = (uint32_t)((cnt + TILE2 - 1) / TILE2);
+        const uint32_t nt = (uint32_t)((cnt + tsz - 1) / tsz);
         for (uint32_t i = threadIdx.x; i < nt; i += 64) {
-            const uint64_t o = (uint64_t)i * TILE2;
+            const uint64_t o = (uint64_t)i * tsz;
             const int64_t rem = cnt - (int64_t)o;
             tt.off[t0 + i] = s0 + o;
-            tt.len[t0 + i] = (uint32_t)(rem < TILE2 ? rem : TILE2);
+            tt.len[t0 + i] = (uint32_t)(rem < (int64_t)tsz ? rem : tsz);
             tt.bucket[t0 + i] = b;
         }
         t0 += nt;
@@ -173,12 +193,13 @@ template <class Lay>
 __global__ void __launch_bounds__(TP_THREADS)
 k_tilepass(TilePassArgs A) {
     typedef typename Lay::W W;
+    constexpr int TP_ITEMS = tp_items<W>();
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     if (A.pack_bad && *A.pack_bad) return;
     const RangePlan& P = A.plan;
     const uint32_t nb2 = A.nb2;
     W* stage = reinterpret_cast<W*>(lds_raw);
-    uint32_t* hist = reinterpret_cast<uint32_t*>(lds_raw + TILE2 * sizeof(W));
+    uint32_t* hist = reinterpret_cast<uint32_t*>(lds_raw + tile_elems<W>() * sizeof(W));
     uint32_t* scr = hist + nb2;
 
     const int r = blockIdx.x < A.nt[0] ? 0 : 1;
@@ -2005,7 +2026,7 @@ static uint64_t expected_tiles(uint64_t nmax, uint32_t nb, uint32_t nseg, uint32
     const uint64_t per = nmax / (nb ? nb : 1);
     return (per + per / 4) / tsz + nseg + 1;
 }
-static int group_tpl(uint64_t nmax, uint32_t nb, uint32_t nseg, uint32_t tsz = TILE2) {
+static int group_tpl(uint64_t nmax, uint32_t nb, uint32_t nseg, uint32_t tsz) {
     return expected_tiles(nmax, nb, nseg, tsz) <= 128 ? 2 : 4;
 }
 
@@ -2055,7 +2076,7 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
     const int nrel = a.nrel;
     const uint32_t nb2 = 1u << a.host_plan->D2;
     const uint64_t nmax = nrel > 1 && a.n[1] > a.n[0] ? a.n[1] : a.n[0];
-    const uint32_t tsz = TILE2;
+    const uint32_t tsz = tile_elems<W>();
     TileTable tt[2];
     static const char* names[2][8] = {
         {"bs_off0", "bs_len0", "bs_bkt0", "bs_bt00", "bs_pref0", "bs_ost0", "bs_nt0", "bs_preft0"},
@@ -2143,7 +2164,7 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
     if (ns) {
         {
             TraceScope ts(ws, "k_tilepass", st);
-            const size_t tp_lds = TILE2 * sizeof(W) + nb2 * 4 + 64;
+            const size_t tp_lds = (size_t)tsz * sizeof(W) + nb2 * 4 + 64;
             hipLaunchKernelGGL(k_tilepass<Lay>, dim3(T.nt[0] + T.nt[1]), dim3(TP_THREADS),
                                tp_lds, st, T);
         }
@@ -2232,6 +2253,7 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
 
     // ---- host view of the plan and the bucket counts (one synchronisation):
     // launch sizes and the tile numbering are derived from them
+    const uint32_t tsz = tile_elems<Tup>();
     uint64_t* hcnt = (uint64_t*)ws->host_pinned("bs_hcnt", (size_t)2 * nb * 8);
     RangePlan* hplan = (RangePlan*)ws->host_pinned("bs_hplan", sizeof(RangePlan));
     const bool segs = a.seg_start[0] != nullptr;
@@ -2272,9 +2294,9 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
             bt0[b] = acc;
             if (segs) {
                 for (uint32_t q = 0; q < nseg; q++)
-                    acc += (uint32_t)((hseg[((size_t)r * nb + b) * nseg + q] + TILE2 - 1) / TILE2);
+                    acc += (uint32_t)((hseg[((size_t)r * nb + b) * nseg + q] + tsz - 1) / tsz);
             } else {
-                acc += (uint32_t)((hcnt[r * nb + b] + TILE2 - 1) / TILE2);
+                acc += (uint32_t)((hcnt[r * nb + b] + tsz - 1) / tsz);
             }
         }
         bt0[nb] = acc;
@@ -2292,7 +2314,7 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
         SMJ_CHECK(hipMemcpyAsync(ostart[r], hdst + r * nb, (size_t)nb * 8,
                                  hipMemcpyHostToDevice, st));
         hipLaunchKernelGGL(k_tiles, dim3(nb), dim3(64), 0, st, a.bstart[r],
-                           a.bcount[r], a.seg_start[r], a.seg_cnt[r], nseg, tt[r]);
+                           a.bcount[r], a.seg_start[r], a.seg_cnt[r], nseg, tt[r], tsz);
     }
     if (nrel == 1) tt[1] = tt[0];
     if (a.ev_tile) SMJ_CHECK(hipEventRecord(a.ev_tile, st));
@@ -2302,7 +2324,7 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
     OvfEntry* ovf = (OvfEntry*)ws->scratch("bs_ovf", (size_t)ovf_cap * sizeof(OvfEntry));
     uint32_t* novf = (uint32_t*)ws->scratch("bs_novf", 4);
     SMJ_CHECK(hipMemsetAsync(novf, 0, 4, st));
-    const size_t tp_lds = TILE2 * sizeof(Tup) + nb2 * 4 + 64;
+    const size_t tp_lds = (size_t)tsz * sizeof(Tup) + nb2 * 4 + 64;
 
     TilePassArgs T;
     GroupArgs G;
@@ -2360,7 +2382,7 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
         const uint32_t nwg = groupsort_grid(ng, maxwg, G.per);
         TraceScope ts(ws, "k_groupsort", st);
         const uint64_t nmax = nrel > 1 && a.n[1] > a.n[0] ? a.n[1] : a.n[0];
-        launch_groupsort<LayTup>(group_tpl(nmax, nb, nseg), nwg, st, G);
+        launch_groupsort<LayTup>(group_tpl(nmax, nb, nseg, tsz), nwg, st, G);
     }
     SMJ_CHECK(hipGetLastError());
     if (a.ev_ovf) SMJ_CHECK(hipEventRecord(a.ev_ovf, st));

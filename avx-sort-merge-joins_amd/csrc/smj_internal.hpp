@@ -301,7 +301,7 @@ uint64_t lds_order_selfcheck(Workspace* ws, hipStream_t st);
 
 // ---- bucketsort.hip : MSD bucket sort (+ fused merge-join count)
 extern const uint32_t kGroupTarget;  // expected tuples per group of the plan
-extern const uint32_t kTileTuples;   // tile of the tile pass
+extern const uint32_t kTileTuples;   // bucket-size unit of the plan (8192)
 extern const uint32_t kGroupD3Max;   // widest level-3 digit of the group pass
 struct BucketSortArgs {
     // level-1 partitioned relation(s): bucket b occupies

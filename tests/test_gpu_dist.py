@@ -330,5 +330,75 @@ def test_rccl_list_all_to_all_views(libs, monkeypatch):
         e = buf[:0]
         dist.all_to_all([e], [e], async_op=True).wait()
         torch.cuda.synchronize()
+        # the 48-bit planes' pieces as _rows sends them: the lo plane as
+        # int32, the hi plane's int16 as bytes (RCCL has no 16-bit integer)
+        from smj.dist import Planes, _wire
+        a, b = Planes(1024, device="cuda"), Planes(1024, device="cuda")
+        a.buf.copy_(torch.arange(a.buf.numel(), dtype=torch.int32, device="cuda") * 7919)
+        b.buf.fill_(-1)
+        for lo, hi in ((0, 300), (300, 300), (300, 1000)):
+            for pa, pb in zip(a.planes, b.planes):
+                dist.all_to_all([_wire(pb[lo:hi])], [_wire(pa[lo:hi])], async_op=True).wait()
+        torch.cuda.synchronize()
+        for pa, pb in zip(a.planes, b.planes):
+            assert torch.equal(pa[:1000], pb[:1000])
     finally:
         dist.destroy_process_group()
+
+
+def test_partition_range_planes_flags(libs, width):
+    """smj_dev_partition_range_planes' not-packable flags and its limits: a
+    payload wider than 48 - s1 bits sets 4 (and 1 past 64 - s1 bits), a key
+    outside the range 2; more than 2^9 partitions: not applicable (False,
+    nothing launched).  Clean input: every element comes back unpacked from
+    its region (the words restated here)."""
+    import torch
+    from smj.dist import Planes, plan_shift
+    lib = libs[width]
+    n, nbits, kmax = 100_000, 8, 1 << 30  # s1 = 22: payloads up to 2^26
+    K = lib.sampled_shards()
+    F = 1 << nbits
+    s1 = plan_shift(1, kmax, nbits)
+    g = torch.Generator().manual_seed(7)
+    keys = torch.randint(1, kmax + 1, (n,), generator=g)
+    pays = torch.randint(0, 1 << 20, (n,), generator=g)
+
+    def run(k, p, bits=nbits):
+        h = np.zeros(n, dtype=lib.dtype)
+        h["key"], h["payload"] = k.numpy(), p.numpy()
+        d = lib.to_device(h)
+        cap = lib.sampled_capacity(n, bits)
+        out = Planes(-(-cap // 32) * 32, device="cuda")
+        ss = torch.empty((1 << bits) * K, dtype=torch.int64, device="cuda")
+        sc = torch.empty_like(ss)
+        fl = torch.full((2,), 9, dtype=torch.int32, device="cuda")
+        ok = lib.dev_partition_range_planes(d, out.buf, out.stride, bits, 1, kmax, ss, sc, fl)
+        torch.cuda.synchronize()
+        return ok, out, ss, sc, fl.tolist()
+
+    ok, out, ss, sc, fl = run(keys, pays)
+    assert ok and fl == [0, 0] and int(sc.sum()) == n
+    lo = out.lo.cpu().numpy().view(np.uint32).astype(np.uint64)
+    hi = out.hi.cpu().numpy().view(np.uint16).astype(np.uint64)
+    w = lo | (hi << np.uint64(32))
+    got = []
+    for i, (a, c) in enumerate(zip(ss.cpu().tolist(), sc.cpu().tolist())):
+        x = w[a:a + c]
+        rel = (np.uint64(i // K) << np.uint64(s1)) | (x >> np.uint64(48 - s1))
+        got.append(np.stack([(rel + np.uint64(1)).astype(np.int64),
+                             (x & np.uint64((1 << (48 - s1)) - 1)).astype(np.int64)], 1))
+    got = np.concatenate(got)
+    want = np.stack([keys.numpy(), pays.numpy()], 1)
+    assert np.array_equal(got[np.lexsort((got[:, 1], got[:, 0]))],
+                          want[np.lexsort((want[:, 1], want[:, 0]))])
+    wide = pays.clone()
+    wide[5] = 1 << (48 - s1)  # fits 64 - s1 bits, not 48 - s1
+    assert run(keys, wide)[4][1] == 4
+    if width == 16:  # 8-byte tuples carry 32-bit payloads: never past 64 - s1
+        wider = pays.clone()
+        wider[9] = 1 << (64 - s1)
+        assert run(keys, wider)[4][1] == 5
+    out_of_range = keys.clone()
+    out_of_range[3] = kmax + 5
+    assert run(out_of_range, pays)[4][1] & 2
+    assert not run(keys, pays, bits=10)[0]
