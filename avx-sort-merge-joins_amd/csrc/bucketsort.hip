@@ -65,6 +65,20 @@ constexpr int TP_THREADS = SMJ_TP_THREADS;
 #ifndef SMJ_GS_TWO
 #define SMJ_GS_TWO 1  // both slots of a group-pass iteration in one barrier chain (sort_two)
 #endif
+// Group-pass metadata one iteration ahead, loaded at the top of the
+// iteration (1: two ahead, prefetched while the current group sorts).  The
+// prefetch kept a third metadata copy live in scalar registers; without it
+// the join kernel spills 79 instead of 154 SGPRs to VGPR lanes and the group
+// pass runs 0.003-0.035 ms faster (round 4, profiles/r04_lab/metalab.txt).
+#ifndef SMJ_GS_META_PREFETCH
+#define SMJ_GS_META_PREFETCH 0
+#endif
+// lab: the group pass reads its GroupArgs from device memory through a
+// pointer laundered every iteration (scalar reloads instead of values held
+// in scalar registers across the persistent loop)
+#ifndef SMJ_GS_ARGS_MEM
+#define SMJ_GS_ARGS_MEM 0
+#endif
 #ifndef SMJ_GS_ABL
 #define SMJ_GS_ABL 0  // ablations for measurements only (1: no in-group sort; 2: no
                       // equal-digit run fixing; 3: no write-out)
@@ -1069,10 +1083,11 @@ __device__ __forceinline__ void count_by_search(const GroupArgs& A, GroupLDS<typ
 // mode (one relation) an iteration takes two consecutive groups of the
 // sequence, one per slot, pipelined the same way.
 template <class Lay, int TPL, class Src, bool PAIR>
-__device__ __forceinline__ void group_loop(const GroupArgs& A, GroupLDS<typename Lay::W>& L,
+__device__ __forceinline__ void group_loop(const GroupArgs& A0, GroupLDS<typename Lay::W>& L,
                                            uint32_t g0, uint32_t stride, uint32_t cnt,
                                            unsigned long long& matches) {
     typedef typename Lay::W W;
+    const GroupArgs& A = A0;
     const RangePlan& P = A.plan;
     const uint32_t tid = otid();
     const int nrel = A.nrel;
@@ -1105,10 +1120,19 @@ __device__ __forceinline__ void group_loop(const GroupArgs& A, GroupLDS<typename
     W vr[GS_ITEMS], vs[GS_ITEMS];
     if (cf[0]) gather_group<Lay, Src>(A, L, C, 0, cn[0], vr);
     if (cf[1] && nslot > 1) gather_group<Lay, Src>(A, L, C, 1, cn[1], vs);
-    if (nit > 1) load_meta<Src, PAIR>(A, g0, stride, cnt, 1, M, true);
+    if (nit > 1 && SMJ_GS_META_PREFETCH) load_meta<Src, PAIR>(A, g0, stride, cnt, 1, M, true);
 
     for (uint32_t j = 0; j < nit; j++) {
+#if SMJ_GS_ARGS_MEM
+        // the arguments again, from memory (opaque pointer: not hoisted)
+        typedef const __attribute__((address_space(4))) GroupArgs* ConstArgs;
+        ConstArgs Aj = (ConstArgs)&A0;  // constant memory: scalar loads
+        asm volatile("" : "+s"(Aj));
+        const GroupArgs& A = *(const GroupArgs*)Aj;
+        const RangePlan& P = A.plan;
+#endif
         const bool has_next = j + 1 < nit;
+        if (!SMJ_GS_META_PREFETCH && has_next) load_meta<Src, PAIR>(A, g0, stride, cnt, j + 1, M, true);
         // every lane's gather of group gi has read the tables: rebuild them
         __syncthreads();
         const GroupMeta<TPL> N = M;
@@ -1121,7 +1145,8 @@ __device__ __forceinline__ void group_loop(const GroupArgs& A, GroupLDS<typename
                 no[r] = r < nslot ? __builtin_amdgcn_readfirstlane(L.off[r]) : 0;
             }
         }
-        if (j + 2 < nit) load_meta<Src, PAIR>(A, g0, stride, cnt, j + 2, M, true);
+        if (SMJ_GS_META_PREFETCH && j + 2 < nit)
+            load_meta<Src, PAIR>(A, g0, stride, cnt, j + 2, M, true);
         bool nf[2];
         fits(nn, nf);
         nf[0] &= has_next;
@@ -1233,10 +1258,21 @@ __device__ __forceinline__ void group_loop(const GroupArgs& A, GroupLDS<typename
 // the 128-byte line that two neighbouring groups' runs share in a tile is
 // fetched into that L2 once instead of once per XCD.  The grid is a multiple
 // of 8 (launch_groupsort).
+#if SMJ_GS_ARGS_MEM
+typedef const GroupArgs* __restrict__ GroupArgsParam;
+#define SMJ_GS_ARGS_REF(p) (*(p))
+#else
+typedef GroupArgs GroupArgsParam;
+#define SMJ_GS_ARGS_REF(p) (p)
+#endif
+
+__global__ void k_put_args(GroupArgs G, GroupArgs* dst) { *dst = G; }
+
 template <class Lay, int TPL, bool PAIR>
 __global__ void __launch_bounds__(GS_THREADS, gs_wg_per_cu<typename Lay::W>() * GS_THREADS / 256)
-k_groupsort(GroupArgs A) {
+k_groupsort(GroupArgsParam Ap) {
     typedef typename Lay::W W;
+    const GroupArgs& A = SMJ_GS_ARGS_REF(Ap);
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     if (A.pack_bad && *A.pack_bad) return;
     GroupLDS<W>& L = *reinterpret_cast<GroupLDS<W>*>(lds_raw);
@@ -2040,8 +2076,15 @@ static uint32_t groupsort_grid(uint32_t ngroups, uint32_t maxwg, uint32_t& per) 
 }
 
 template <class Lay>
-static void launch_groupsort(int tpl, uint32_t nwg, hipStream_t st, const GroupArgs& G) {
+static void launch_groupsort(Workspace* ws, int tpl, uint32_t nwg, hipStream_t st,
+                             const GroupArgs& G0) {
     const size_t lds = sizeof(GroupLDS<typename Lay::W>);
+#if SMJ_GS_ARGS_MEM
+    GroupArgs* G = (GroupArgs*)ws->scratch("gs_args", sizeof(GroupArgs));
+    hipLaunchKernelGGL(k_put_args, dim3(1), dim3(1), 0, st, G0, G);
+#else
+    const GroupArgs& G = G0;
+#endif
 #if SMJ_GS_XCD
     // k_groupsort's XCD-aware order splits the groups into 8 ranges of
     // gridDim.x / 8 blocks each: any other grid would sort some groups twice
@@ -2051,7 +2094,7 @@ static void launch_groupsort(int tpl, uint32_t nwg, hipStream_t st, const GroupA
         abort();
     }
 #endif
-    if (G.pair) {
+    if (G0.pair) {
         if (tpl == 4)
             hipLaunchKernelGGL((k_groupsort<Lay, 4, true>), dim3(nwg), dim3(GS_THREADS), lds, st, G);
         else
@@ -2188,7 +2231,7 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
         const uint32_t maxwg = gs_wg_per_cu<W>() * 256;
         const uint32_t nwg = groupsort_grid(ngroups, maxwg, G.per);
         TraceScope ts(ws, "k_groupsort", st);
-        launch_groupsort<Lay>(group_tpl(nmax, nb, a.nseg, tsz), nwg, st, G);
+        launch_groupsort<Lay>(ws, group_tpl(nmax, nb, a.nseg, tsz), nwg, st, G);
     }
     SMJ_CHECK(hipGetLastError());
     if (a.ev_ovf) SMJ_CHECK(hipEventRecord(a.ev_ovf, st));
@@ -2382,7 +2425,7 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
         const uint32_t nwg = groupsort_grid(ng, maxwg, G.per);
         TraceScope ts(ws, "k_groupsort", st);
         const uint64_t nmax = nrel > 1 && a.n[1] > a.n[0] ? a.n[1] : a.n[0];
-        launch_groupsort<LayTup>(group_tpl(nmax, nb, nseg, tsz), nwg, st, G);
+        launch_groupsort<LayTup>(ws, group_tpl(nmax, nb, nseg, tsz), nwg, st, G);
     }
     SMJ_CHECK(hipGetLastError());
     if (a.ev_ovf) SMJ_CHECK(hipEventRecord(a.ev_ovf, st));
