@@ -73,11 +73,15 @@ constexpr int TP_THREADS = SMJ_TP_THREADS;
 #ifndef SMJ_GS_META_PREFETCH
 #define SMJ_GS_META_PREFETCH 0
 #endif
-// lab: the group pass reads its GroupArgs from device memory through a
-// pointer laundered every iteration (scalar reloads instead of values held
-// in scalar registers across the persistent loop)
+// The group pass reads its GroupArgs from device memory (written by a
+// one-thread kernel before the launch) through a constant-address pointer
+// laundered every iteration: the arguments are reloaded with scalar loads
+// instead of held in scalar registers across the persistent loop.  The join
+// kernel then spills 13 SGPRs instead of 79; the 16-byte join's group pass
+// 1.30-1.32 -> 1.26-1.28 ms, the 8-byte join's 1.03 -> 1.01-1.03 (round 4,
+// interleaved on one box, profiles/r04_lab/argslab.txt).
 #ifndef SMJ_GS_ARGS_MEM
-#define SMJ_GS_ARGS_MEM 0
+#define SMJ_GS_ARGS_MEM 1
 #endif
 #ifndef SMJ_GS_ABL
 #define SMJ_GS_ABL 0  // ablations for measurements only (1: no in-group sort; 2: no
