@@ -80,11 +80,6 @@ constexpr int TP_THREADS = SMJ_TP_THREADS;
 // kernel then spills 13 SGPRs instead of 79; the 16-byte join's group pass
 // 1.30-1.32 -> 1.26-1.28 ms, the 8-byte join's 1.03 -> 1.01-1.03 (round 4,
 // interleaved on one box, profiles/r04_lab/argslab.txt).
-// the tile pass as one persistent workgroup per CU with the next tile's loads
-// in flight (k_tilepass_p; 0: one workgroup per tile, k_tilepass)
-#ifndef SMJ_TP_PERSIST
-#define SMJ_TP_PERSIST 0
-#endif
 #ifndef SMJ_GS_ARGS_MEM
 #define SMJ_GS_ARGS_MEM 1
 #endif
@@ -150,16 +145,6 @@ typedef int64_t KeyT;
 typedef int32_t KeyT;
 #endif
 
-// an opaque copy: the compiler cannot reuse values computed from x before
-// (it recomputes them instead of keeping them live)
-template <class T>
-__device__ __forceinline__ void launder(T& x) {
-    static_assert(sizeof(T) % 4 == 0, "word-sized");
-    uint32_t* w = reinterpret_cast<uint32_t*>(&x);
-#pragma unroll
-    for (int i = 0; i < (int)(sizeof(T) / 4); i++) asm volatile("" : "+v"(w[i]));
-}
-
 struct TileTable {
     uint64_t* off;     // tile start in `part`
     uint32_t* len;     // tile length
@@ -222,41 +207,58 @@ struct TilePassArgs {
     uint64_t pstride[2] = {0, 0};  // plane stride of part/tmp (LayP48)
 };
 
-// One tile of the tile pass: v holds its elements (loaded by the caller),
-// grouped by d2 through LDS and written to tmp at the tile's offset, with its
-// prefix row.  Uniform control flow (block barriers inside).
-template <class Lay, bool TILE_DG = true>
-__device__ __forceinline__ void tile_body(const TilePassArgs& A, unsigned char* lds_raw, int r,
-                                          uint32_t t, uint64_t off, uint32_t len, uint32_t b,
-                                          const typename Lay::W (&v)[tp_items<typename Lay::W>()]) {
+template <class Lay>
+__global__ void __launch_bounds__(TP_THREADS)
+k_tilepass(TilePassArgs A) {
     typedef typename Lay::W W;
     constexpr int TP_ITEMS = tp_items<W>();
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    if (A.pack_bad && *A.pack_bad) return;
     const RangePlan& P = A.plan;
     const uint32_t nb2 = A.nb2;
     W* stage = reinterpret_cast<W*>(lds_raw);
     uint32_t* hist = reinterpret_cast<uint32_t*>(lds_raw + tile_elems<W>() * sizeof(W));
     uint32_t* scr = hist + nb2;
+
+    const int r = blockIdx.x < A.nt[0] ? 0 : 1;
+    const uint32_t t = A.t0[r] + (r ? blockIdx.x - A.nt[0] : blockIdx.x);
+    if (A.ntiles[r] && t >= *A.ntiles[r]) return;
     const TileTable& tt = A.tt[r];
+    const typename Lay::CView part = Lay::cview(A.part[r], A.pstride[r]);
     const typename Lay::View tmp = Lay::view(A.tmp[r], A.pstride[r]);
+    const uint64_t off = tt.off[t];
+    const uint32_t len = tt.len[t];
+    const uint32_t b = tt.bucket[t];
+
     for (uint32_t d = threadIdx.x; d < nb2; d += TP_THREADS) hist[d] = 0;
-    __syncthreads();
-    // keys outside the plan range (clamped by plan_rel) only sit in the first
-    // and the last bucket: every other tile takes the 32-bit digit.  The
-    // digits are computed again at placement (persistent form: no digit array
-    // held over the scan beside two register tiles)
-    const bool fast = A.d2_fast && b != 0 && b != (1u << P.D1) - 1;
-    const uint32_t base_lo = (uint32_t)P.base, mask = nb2 - 1;
-    auto digit = [&](const W& x) -> uint32_t {
-        return fast ? Lay::digit_fast(x, base_lo, P.s1, P.s2, mask) : plan_d2(P, Lay::rel(P, x, b), b);
-    };
-    uint32_t dg[TILE_DG ? TP_ITEMS : 1];
+    W v[TP_ITEMS];
+    uint32_t dg[TP_ITEMS];
 #pragma unroll
     for (int j = 0; j < TP_ITEMS; j++) {
         uint32_t i = j * TP_THREADS + threadIdx.x;
-        if (i < len) {
-            const uint32_t d = digit(v[j]);
-            if (TILE_DG) dg[TILE_DG ? j : 0] = d;
-            atomicAdd(&hist[d], 1u);
+        if (i < len) v[j] = part[off + i];
+    }
+    __syncthreads();
+    // keys outside the plan range (clamped by plan_rel) only sit in the first
+    // and the last bucket: every other tile takes the 32-bit digit
+    if (A.d2_fast && b != 0 && b != (1u << P.D1) - 1) {
+        const uint32_t base_lo = (uint32_t)P.base, mask = nb2 - 1;
+#pragma unroll
+        for (int j = 0; j < TP_ITEMS; j++) {
+            uint32_t i = j * TP_THREADS + threadIdx.x;
+            if (i < len) {
+                dg[j] = Lay::digit_fast(v[j], base_lo, P.s1, P.s2, mask);
+                atomicAdd(&hist[dg[j]], 1u);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < TP_ITEMS; j++) {
+            uint32_t i = j * TP_THREADS + threadIdx.x;
+            if (i < len) {
+                dg[j] = plan_d2(P, Lay::rel(P, v[j], b), b);
+                atomicAdd(&hist[dg[j]], 1u);
+            }
         }
     }
     __syncthreads();
@@ -286,15 +288,7 @@ __device__ __forceinline__ void tile_body(const TilePassArgs& A, unsigned char* 
     for (int j = 0; j < TP_ITEMS; j++) {
         uint32_t i = j * TP_THREADS + threadIdx.x;
         if (i < len) {
-            uint32_t d;
-            if (TILE_DG) {
-                d = dg[TILE_DG ? j : 0];
-            } else {
-                W x = v[j];
-                launder(x);
-                d = digit(x);
-            }
-            uint32_t pos = atomicAdd(&hist[d], 1u);
+            uint32_t pos = atomicAdd(&hist[dg[j]], 1u);
             stage[pos] = v[j];
         }
     }
@@ -303,117 +297,6 @@ __device__ __forceinline__ void tile_body(const TilePassArgs& A, unsigned char* 
     for (int j = 0; j < TP_ITEMS; j++) {
         uint32_t i = j * TP_THREADS + threadIdx.x;
         if (i < len) st_w(tmp + off + i, stage[i]);
-    }
-}
-
-template <class Lay>
-__device__ __forceinline__ void tile_load(const TilePassArgs& A, int r, uint64_t off, uint32_t len,
-                                          typename Lay::W (&v)[tp_items<typename Lay::W>()]) {
-    // unconditional loads (past the end: the last element again), so that a
-    // fixed count is in flight and no branch splits the wait bookkeeping
-    const typename Lay::CView part = Lay::cview(A.part[r], A.pstride[r]) + off;
-    const uint32_t last = len ? len - 1 : 0u;
-#pragma unroll
-    for (int j = 0; j < tp_items<typename Lay::W>(); j++) {
-        const uint32_t i = j * TP_THREADS + threadIdx.x;
-        v[j] = part[i < len ? i : last];
-    }
-}
-
-// one workgroup per tile
-template <class Lay>
-__global__ void __launch_bounds__(TP_THREADS)
-k_tilepass(TilePassArgs A) {
-    typedef typename Lay::W W;
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
-    if (A.pack_bad && *A.pack_bad) return;
-    const int r = blockIdx.x < A.nt[0] ? 0 : 1;
-    const uint32_t t = A.t0[r] + (r ? blockIdx.x - A.nt[0] : blockIdx.x);
-    if (A.ntiles[r] && t >= *A.ntiles[r]) return;
-    const TileTable& tt = A.tt[r];
-    const uint64_t off = tt.off[t];
-    const uint32_t len = tt.len[t];
-    const uint32_t b = tt.bucket[t];
-    W v[tp_items<W>()];
-    tile_load<Lay>(A, r, off, len, v);
-    tile_body<Lay>(A, lds_raw, r, t, off, len, b, v);
-}
-
-// Persistent form (round 4): a workgroup per CU walks the tiles q =
-// blockIdx.x, + gridDim.x, ... of both relations; the next tile's elements are
-// loaded while the current one is grouped (two register tiles), and the
-// metadata two tiles ahead.  One workgroup holds a CU (128 KB of LDS stage),
-// so the one-tile form paid every tile's load latency with the CU idle.
-struct TileRef {
-    int r;
-    uint32_t t, len, b;
-    uint64_t off;
-    bool ok;
-};
-
-// tile q's table entries, loaded but not yet made uniform: the loads are
-// waited for only where tile_fin reads them (after the current tile's work)
-__device__ __forceinline__ TileRef tile_raw(const TilePassArgs& A, uint32_t q, uint32_t n0,
-                                            uint32_t n) {
-    TileRef x;
-    x.ok = q < n;
-    x.r = q < n0 ? 0 : 1;
-    x.t = A.t0[x.r] + (x.r ? q - n0 : q);
-    const uint32_t tc = x.ok ? x.t : A.t0[0];  // a valid entry either way
-    const TileTable& tt = A.tt[x.ok ? x.r : 0];
-    x.off = tt.off[tc];
-    x.len = tt.len[tc];
-    x.b = tt.bucket[tc];
-    return x;
-}
-
-__device__ __forceinline__ TileRef tile_fin(TileRef x) {
-    x.off = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x.off >> 32)) << 32) |
-            __builtin_amdgcn_readfirstlane((uint32_t)x.off);
-    x.len = __builtin_amdgcn_readfirstlane(x.len);
-    x.b = __builtin_amdgcn_readfirstlane(x.b);
-    return x;
-}
-
-template <class Lay>
-__global__ void __launch_bounds__(TP_THREADS)
-k_tilepass_p(TilePassArgs A) {
-    typedef typename Lay::W W;
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
-    if (A.pack_bad && *A.pack_bad) return;
-    // the tiles that exist: relation r's first min(nt[r], its device count)
-    uint32_t m[2];
-    for (int r = 0; r < 2; r++) {
-        m[r] = A.nt[r];
-        if (A.ntiles[r] && A.nt[r]) {
-            const uint32_t c = *A.ntiles[r];
-            const uint32_t have = c > A.t0[r] ? c - A.t0[r] : 0u;
-            m[r] = have < m[r] ? have : m[r];
-        }
-    }
-    const uint32_t n0 = m[0], n = m[0] + m[1], g = gridDim.x;
-    uint32_t q = blockIdx.x;
-    if (q >= n) return;
-    TileRef cur = tile_fin(tile_raw(A, q, n0, n));
-    W v[tp_items<W>()], nv[tp_items<W>()];
-    tile_load<Lay>(A, cur.r, cur.off, cur.len, v);
-    TileRef nxt = tile_fin(tile_raw(A, q + g, n0, n));
-    for (;;) {
-        // the next tile's elements (past the last tile: this one again, so
-        // that the loads are unconditional), then the table entries of the
-        // one after: both land while this tile is grouped
-        tile_load<Lay>(A, nxt.ok ? nxt.r : cur.r, nxt.ok ? nxt.off : cur.off,
-                       nxt.ok ? nxt.len : cur.len, nv);
-        const TileRef raw = tile_raw(A, q + 2 * g, n0, n);
-        tile_body<Lay, false>(A, lds_raw, cur.r, cur.t, cur.off, cur.len, cur.b, v);
-        if (!nxt.ok) break;
-        const TileRef nn = tile_fin(raw);
-        __syncthreads();  // the stage and the histogram are reused
-#pragma unroll
-        for (int j = 0; j < tp_items<W>(); j++) v[j] = nv[j];
-        cur = nxt;
-        nxt = nn;
-        q += g;
     }
 }
 
@@ -930,6 +813,13 @@ __device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS<typename
 
 // Hide a value from the optimiser (an empty asm that "changes" its words):
 // the value is recomputed from it instead of being kept alive.
+template <class T>
+__device__ __forceinline__ void launder(T& x) {
+    static_assert(sizeof(T) % 4 == 0, "word-sized");
+    uint32_t* w = reinterpret_cast<uint32_t*>(&x);
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 4); i++) asm volatile("" : "+v"(w[i]));
+}
 
 // Equal-digit runs of one sorted slot in B (see sort_group): false when a
 // long run is out of order (the skew path).  c / first: the calling thread's
@@ -2158,8 +2048,6 @@ static void set_pass_attrs() {
     if (done) return;
     SMJ_CHECK(hipFuncSetAttribute((const void*)k_tilepass<Lay>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    SMJ_CHECK(hipFuncSetAttribute((const void*)k_tilepass_p<Lay>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     // several workgroups per CU (launch bounds): ask for what one needs
     const void* gs[4] = {(const void*)k_groupsort<Lay, 2, false>,
                          (const void*)k_groupsort<Lay, 4, false>,
@@ -2324,14 +2212,8 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
         {
             TraceScope ts(ws, "k_tilepass", st);
             const size_t tp_lds = (size_t)tsz * sizeof(W) + nb2 * 4 + 64;
-            if (SMJ_TP_PERSIST) {
-                const uint32_t tot = T.nt[0] + T.nt[1];
-                hipLaunchKernelGGL(k_tilepass_p<Lay>, dim3(tot < 256 ? tot : 256),
-                                   dim3(TP_THREADS), tp_lds, st, T);
-            } else {
-                hipLaunchKernelGGL(k_tilepass<Lay>, dim3(T.nt[0] + T.nt[1]), dim3(TP_THREADS),
-                                   tp_lds, st, T);
-            }
+            hipLaunchKernelGGL(k_tilepass<Lay>, dim3(T.nt[0] + T.nt[1]), dim3(TP_THREADS),
+                               tp_lds, st, T);
         }
         const uint32_t ubs[2] = {T.nt[0], T.nt[1]};
         uint32_t* nts[2] = {ntiles[sel[0]], ntiles[sel[ns > 1 ? 1 : 0]]};
