@@ -462,3 +462,32 @@ def test_partition_bits():
     assert partition_bits(9, 8, True, n // 2) == 9
     assert partition_bits(6, 3, True, n) == 8
     assert partition_bits(9, 16, True, 1000) == 10  # fewer than 2^6 local buckets
+
+
+def test_next_layout_ladder():
+    """DistributedJoin._next_layout: the layout and form an invalid attempt
+    repeats with (bad / ovf are maxima over the ranks): planes -> words when
+    only the 48-bit payload limit failed or a region overflowed (exact form),
+    -> tuples when a payload needs more than 64 - s1 bits or a key lies
+    outside the plan; words -> tuples on any bad bit; tuples stay."""
+    import sys
+    sys.path.insert(0, PKG)
+    from smj.dist import (BAD_PAYLOAD, BAD_PAYLOAD48, BAD_RANGE, DistributedJoin)
+
+    class J:
+        _next_layout = DistributedJoin._next_layout
+
+        def __init__(self, can_pack, sampled):
+            self.can_pack, self.sampled = can_pack, sampled
+    j = J(True, True)
+    assert j._next_layout("planes", True, BAD_PAYLOAD48, 0) == ("words", True)
+    assert j._next_layout("planes", True, BAD_PAYLOAD | BAD_PAYLOAD48, 0) == ("tuples", True)
+    assert j._next_layout("planes", True, BAD_RANGE, 0) == ("tuples", True)
+    assert j._next_layout("planes", True, 0, 1) == ("words", False)  # overflow: exact words
+    assert j._next_layout("words", True, BAD_PAYLOAD, 0) == ("tuples", True)
+    assert j._next_layout("words", True, 0, 1) == ("words", False)
+    assert j._next_layout("tuples", True, 0, 1) == ("tuples", False)
+    # 8-byte tuples (no 64-bit words) and an exact default form
+    k = J(False, False)
+    assert k._next_layout("planes", True, BAD_PAYLOAD48, 0) == ("tuples", False)
+    assert k._next_layout("planes", True, 0, 1) == ("tuples", False)
