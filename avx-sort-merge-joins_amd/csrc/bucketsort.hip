@@ -98,9 +98,19 @@ constexpr uint32_t tile_elems() {
     return (uint32_t)(TP_THREADS * tp_items<W>());
 }
 static_assert(tile_elems<uint64_t>() <= 65535 + 1, "u16 prefix rows");
-// the bucket-size unit of the plan (choose_levels): 8192 elements, fixed
-// when the tiles grew (round 4) so that the plans stay as measured
-const uint32_t kTileTuples = 8192;
+// the bucket-size unit of the plan (choose_levels): a level-1 bucket stays
+// within 192 of these (the group pass takes up to 256 tiles of a bucket).
+// 16384, the tile of 8-byte elements: the 1024M x 1024M join then plans 2^9
+// level-1 partitions instead of 2^10 and its scatter takes 10.4 instead of
+// 14.5 ms (31.0 -> 27.3 ms; Zipf 34.4 -> 31.6; 128M unchanged: round 4,
+// profiles/r04_lab/kt_lines.txt).  16-byte tuples in their own layout keep
+// 8192-element tiles: a bucket of up to 3.1M of them is 384 tiles, past the
+// group pass's 256, and takes the skew path (that layout is the fallback for
+// unpackable keys only).
+#ifndef SMJ_PLAN_TILE
+#define SMJ_PLAN_TILE 16384
+#endif
+const uint32_t kTileTuples = SMJ_PLAN_TILE;
 
 #ifndef SMJ_GS_THREADS
 #define SMJ_GS_THREADS 256

@@ -390,12 +390,18 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
     // partition) fit LDS up to 512 partitions.
     // (8-byte tuples have no 64-bit packed words: the 48-bit ones, else
     // tuples; the same conditions as packing, checked here)
+    // A 48-bit word keeps 48 - s1 payload bits.  Payloads are taken to lie
+    // within the key span (the row ids of a PK relation, as in the
+    // benchmark): where they would not, the 48-bit attempt would fail on them
+    // and partition a second time, so the join starts with 64-bit words (the
+    // 1024M x 1024M join: 2^9 partitions leave 27 payload bits).
+    const bool p48_fits = hplan.s1 >= 1 && hplan.s1 <= 32 && hplan.span < (1ull << (48 - hplan.s1));
     auto first_mode = [&]() {
 #ifdef KEY_8B
-        if (can_pack && use_p48() && nb <= 512) return -1;
+        if (can_pack && use_p48() && p48_fits && nb <= 512) return -1;
 #else
         if (sampled && plan_on_host && use_packing() && use_p48() &&
-            LayP48::usable(hplan) && nb <= 512)
+            LayP48::usable(hplan) && p48_fits && nb <= 512)
             return -1;
 #endif
         return can_pack ? 0 : (sampled ? 1 : 2);

@@ -59,8 +59,8 @@ CHUNK_BYTES = int(os.environ.get("SMJ_A2A_CHUNK_MB", "512")) << 20
 LAYOUTS = ("tuples", "words", "planes")
 PLANE_MAX_BITS = 9
 # a local bucket the tile pass / group pass take in stride: <= 192 tiles of
-# 8192 elements (choose_levels' bucket_cap in the library)
-LOCAL_BUCKET_CAP = 192 * 8192
+# 16384 elements (choose_levels' bucket_cap in the library)
+LOCAL_BUCKET_CAP = 192 * 16384
 # the partition's not-packable bits (smj_common.hpp kBad*): 1 payload wider
 # than a 64-bit word holds, 2 key outside the plan, 4 payload wider than a
 # 48-bit word holds -- also what a rank where the planes form does not apply
@@ -143,18 +143,32 @@ def range_digit(keys: torch.Tensor, key_min: int, key_max: int, bits: int) -> to
     return rel >> plan_shift(key_min, key_max, bits)
 
 
-def partition_bits(bucket_bits: int, world: int, planes: bool, n_hint=None) -> int:
+def planes_hold(key_min: int, key_max: int, pbits: int) -> bool:
+    """Whether 48-bit words are worth trying at 2^pbits exchange partitions:
+    a word holds the key's s1 low bits and a payload below 2^(48 - s1), and
+    payloads are taken to lie within the key span (the row ids of a PK
+    relation, as in the benchmark).  Where they would not, every step would
+    partition twice (planes, then 64-bit words once a rank reports a payload
+    too wide), so the exchange starts with words: 128M per rank at G = 4 is
+    such a case (keys 1..512M, 2^9 partitions: s1 = 20, payloads below 2^28)."""
+    s1 = plan_shift(key_min, key_max, pbits)
+    return 1 <= s1 <= 32 and key_max - key_min < (1 << (48 - s1))
+
+
+def partition_bits(bucket_bits: int, world: int, planes: bool, n_hint=None,
+                   key_range=None) -> int:
     """Exchange partition width: bucket_bits per rank (2^min(bucket_bits +
     log2 G, 10) partitions), unless the 48-bit planes are offered and one bit
     less keeps them: 2^9 partitions, when every rank's share (n_hint elements
     per relation, balanced) still splits into local buckets of at most
-    LOCAL_BUCKET_CAP elements -- at 128M per rank and bucket_bits 9, G = 2
-    and 4 (256 / 128 local buckets; 256 is the 1-GPU join's own fan-out-8
-    shape), not 8; at bucket_bits 8 (bench.py's default) G = 4."""
+    LOCAL_BUCKET_CAP elements (at 128M per rank up to G = 8: 2^6 local
+    buckets of 2M) and, given key_range, the words hold the payloads
+    (planes_hold: with the benchmark's row-id payloads only G <= 2)."""
     pbits = min(bucket_bits + ceil_log2(world), MAX_PARTITION_BITS)
     if planes and pbits > PLANE_MAX_BITS and n_hint is not None:
         lbits = PLANE_MAX_BITS - ceil_log2(world)
-        if lbits >= 6 and -(-n_hint // (1 << lbits)) <= LOCAL_BUCKET_CAP:
+        fits = key_range is None or planes_hold(key_range[0], key_range[1], PLANE_MAX_BITS)
+        if fits and lbits >= 6 and -(-n_hint // (1 << lbits)) <= LOCAL_BUCKET_CAP:
             pbits = PLANE_MAX_BITS
     return pbits
 
@@ -344,7 +358,8 @@ class DistributedJoin:
         offers_planes = (bool(getattr(ops, "can_planes", False))
                          and hasattr(ops, "partition_range_planes"))
         # n_hint: elements per rank and relation (the same on every rank)
-        self.pbits = partition_bits(bucket_bits, self.world, offers_planes, n_hint)
+        self.pbits = partition_bits(bucket_bits, self.world, offers_planes, n_hint,
+                                    (key_min, key_max))
         if os.environ.get("SMJ_XBITS"):  # rehearse the G-GPU partition width on fewer
             self.pbits = int(os.environ["SMJ_XBITS"])
         self.fanout = 1 << self.pbits
@@ -360,7 +375,8 @@ class DistributedJoin:
         self.sampled = bool(cs(self.world) if callable(cs) else cs)
         # the first layout tried each step: the narrowest the ops offer
         self.can_pack = bool(getattr(ops, "can_pack", False))
-        self.can_planes = offers_planes and self.pbits <= PLANE_MAX_BITS
+        self.can_planes = (offers_planes and self.pbits <= PLANE_MAX_BITS
+                           and planes_hold(self.key_min, self.key_max, self.pbits))
         self.layout = "planes" if self.can_planes else "words" if self.can_pack else "tuples"
         # segment-table width: the same on every rank whichever form a rank's
         # partition takes

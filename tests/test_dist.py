@@ -448,7 +448,8 @@ def test_local_range_int64_edges():
 def test_partition_bits():
     """The exchange's partition width: bucket_bits + log2 G up to 2^10, or
     2^9 where the 48-bit planes then fit and every rank's local buckets stay
-    within LOCAL_BUCKET_CAP (128M per rank: G = 2, 4; not 8)."""
+    within LOCAL_BUCKET_CAP (128M per rank: up to G = 8) and, given the key
+    range, 48-bit words hold payloads as wide as the key span."""
     import sys
     sys.path.insert(0, PKG)
     from smj.dist import partition_bits
@@ -458,10 +459,19 @@ def test_partition_bits():
     assert partition_bits(9, 2, True, None) == 10  # no hint: the default width
     assert partition_bits(9, 2, True, n) == 9
     assert partition_bits(9, 4, True, n) == 9
-    assert partition_bits(9, 8, True, n) == 10  # 2^6 buckets of 2M > the cap
-    assert partition_bits(9, 8, True, n // 2) == 9
+    assert partition_bits(9, 8, True, n) == 9  # 2^6 buckets of 2M, within the cap
+    assert partition_bits(9, 8, True, 2 * n) == 10  # 4M a bucket: past it
+    assert partition_bits(9, 8, True, n, (1, 8 * n)) == 10  # 27 payload bits
     assert partition_bits(6, 3, True, n) == 8
     assert partition_bits(9, 16, True, 1000) == 10  # fewer than 2^6 local buckets
+    # payloads taken to lie within the key span (row ids): keys 1..512M at
+    # 2^9 partitions leave 28 payload bits, too few -> 64-bit words, 2^10
+    from smj.dist import planes_hold
+    assert partition_bits(8, 4, True, n, (1, 4 * n)) == 10
+    assert partition_bits(8, 2, True, n, (1, 2 * n)) == 9  # 2^9 natively
+    assert partition_bits(9, 2, True, n, (1, 2 * n)) == 9  # 29 payload bits hold 256M
+    assert planes_hold(1, n, 8) and planes_hold(1, 2 * n, 9)
+    assert not planes_hold(1, 4 * n, 9) and not planes_hold(1, 8 * n, 9)
 
 
 def test_next_layout_ladder():
