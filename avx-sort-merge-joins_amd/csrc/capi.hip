@@ -50,6 +50,9 @@ k_sorted_scan(const smj::Tup* __restrict__ t, uint64_t n, unsigned long long* fi
 namespace smj {
 void gen_pk_nopayload(Tup* out, uint64_t n, uint64_t first, uint64_t total,
                       uint64_t seed, hipStream_t st);
+// mgpu.hip: the multi-GPU join behind sortmergejoin_mpsm (mat: -1 = the
+// process switch, else this call's materialisation)
+result_t* mpsm_api(relation_t* relR, relation_t* relS, joinconfig_t* joincfg, int mat);
 }
 
 using namespace smj;
@@ -272,8 +275,9 @@ k_keyrange(const Tup* __restrict__ r0, uint64_t n0, const Tup* __restrict__ r1, 
     }
 }
 
-static bool key_range(Workspace* ws, const Tup* const* rels, const uint64_t* ns, int nrel,
-                      int64_t* lo, int64_t* hi, hipStream_t st) {
+namespace smj {
+bool key_range(Workspace* ws, const Tup* const* rels, const uint64_t* ns, int nrel,
+               int64_t* lo, int64_t* hi, hipStream_t st) {
     unsigned long long* mm = (unsigned long long*)ws->scratch("keyrange", 16);
     unsigned long long* h = (unsigned long long*)ws->host_pinned("keyrange_h", 16);
     const unsigned long long init[2] = {~0ull, 0ull};
@@ -292,6 +296,7 @@ static bool key_range(Workspace* ws, const Tup* const* rels, const uint64_t* ns,
     *hi = (int64_t)(h[1] ^ 0x8000000000000000ull);
     return true;
 }
+}  // namespace smj
 
 // 16-byte sorts and joins carry packed words through the intermediate passes
 // when the plan allows it (LayPacked); SMJ_PACK=0 keeps tuples
@@ -1026,25 +1031,34 @@ tuple_t* cb_next_writepos(chainedtuplebuffer_t* cb) { return cb_reserve(cb, 1); 
 
 // the matches of sorted device runs R and S, appended to cb (two device
 // passes: the count sizes the device buffer, the second writes it)
-static uint64_t materialize_append(const Tup* r, uint64_t nR, const Tup* s, uint64_t nS,
-                                   chainedtuplebuffer_t* cb) {
-    Ctx& c = ctx();
-    smj_workspace* ws = (smj_workspace*)&c.ws;
+}  // extern "C"
+namespace smj {
+uint64_t materialize_append_on(Workspace* wsp, hipStream_t st, const Tup* r, uint64_t nR,
+                               const Tup* s, uint64_t nS, chainedtuplebuffer_t* cb) {
+    smj_workspace* ws = (smj_workspace*)wsp;
     const uint64_t total = smj_dev_materialize(ws, (const tuple_t*)r, nR, (const tuple_t*)s,
-                                               nS, nullptr, 0, c.st);
+                                               nS, nullptr, 0, st);
     if (total == 0) return 0;
-    Tup* o = (Tup*)c.ws.scratch("api_mat", total * sizeof(Tup));
+    Tup* o = (Tup*)wsp->scratch("api_mat", total * sizeof(Tup));
     const uint64_t got = smj_dev_materialize(ws, (const tuple_t*)r, nR, (const tuple_t*)s, nS,
-                                             (tuple_t*)o, total, c.st);
+                                             (tuple_t*)o, total, st);
     if (got != total) {
         fprintf(stderr, "[ERROR] smj: materialisation count changed (%llu, %llu)\n",
                 (unsigned long long)total, (unsigned long long)got);
         abort();
     }
     tuple_t* dst = cb_reserve(cb, total);
-    SMJ_CHECK(hipMemcpyAsync(dst, o, total * sizeof(Tup), hipMemcpyDeviceToHost, c.st));
-    sync();
+    SMJ_CHECK(hipMemcpyAsync(dst, o, total * sizeof(Tup), hipMemcpyDeviceToHost, st));
+    SMJ_CHECK(hipStreamSynchronize(st));
     return total;
+}
+}  // namespace smj
+extern "C" {
+
+static uint64_t materialize_append(const Tup* r, uint64_t nR, const Tup* s, uint64_t nS,
+                                   chainedtuplebuffer_t* cb) {
+    Ctx& c = ctx();
+    return materialize_append_on(&c.ws, c.st, r, nR, s, nS, cb);
 }
 
 // Process-wide, like the reference's compile-time -DJOIN_MATERIALIZE that it
@@ -1055,7 +1069,9 @@ static std::atomic<int> g_materialize{-1};
 
 void smj_set_materialize(int on) { g_materialize.store(on ? 1 : 0); }
 
-static bool materialize_on() {
+}  // extern "C"
+namespace smj {
+bool materialize_on() {
     int v = g_materialize.load();
     if (v < 0) {
         const char* e = getenv("SMJ_MATERIALIZE");
@@ -1065,6 +1081,8 @@ static bool materialize_on() {
     }
     return v > 0;
 }
+}  // namespace smj
+extern "C" {
 
 // decimal of a signed 32-bit value into p; returns the end
 static char* put_i32(char* p, int32_t v) {
@@ -1395,9 +1413,12 @@ result_t* sortmergejoin_multiway(relation_t* relR, relation_t* relS,
     return join_api(relR, relS, joincfg, "m-way");
 }
 
+// sortmergejoin_mpsm.c:38-45 is a stub in the reference; SURVEY.md §2 row 9
+// and BASELINE configs[4] make it the multi-GPU join: NTHREADS ranks, one per
+// visible GPU (mgpu.hip)
 result_t* sortmergejoin_mpsm(relation_t* relR, relation_t* relS,
                              joinconfig_t* joincfg) {
-    return join_api(relR, relS, joincfg, "mpsm");
+    return mpsm_api(relR, relS, joincfg, -1);
 }
 
 void print_timing(uint64_t numtuples, struct timeval* start, struct timeval* end,
@@ -1568,7 +1589,7 @@ result_t* smj_join(relation_t* relR, relation_t* relS, joinconfig_t* joincfg, in
     switch (algo) {
         case 0: return join_api(relR, relS, joincfg, "m-way", mat);
         case 1: return multipass_api(relR, relS, joincfg, mat);
-        case 2: return join_api(relR, relS, joincfg, "mpsm", mat);
+        case 2: return mpsm_api(relR, relS, joincfg, mat);
         default:
             fprintf(stderr, "[ERROR] smj_join: unknown algorithm %d\n", algo);
             return 0;

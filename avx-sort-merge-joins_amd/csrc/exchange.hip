@@ -143,6 +143,38 @@ k_xrecv(const int64_t* __restrict__ msg, const int64_t* __restrict__ chunk, uint
     }
 }
 
+// The tables of an exact range partition (partitions back to back, hist[p]
+// elements each) in the sampled partition's shape: shard 0 of partition p
+// starts at the exclusive prefix sum of hist, the other K - 1 shards are
+// empty.  One workgroup of 1024 threads, F <= 1024.
+__global__ void __launch_bounds__(1024)
+k_hist_tables(const int64_t* __restrict__ hist, uint32_t F, uint32_t K,
+              int64_t* __restrict__ start, int64_t* __restrict__ cnt) {
+    __shared__ int64_t sc[2][1024];
+    const uint32_t p = threadIdx.x;
+    const int64_t h = p < F ? hist[p] : 0;
+    int cur = 0;
+    sc[0][p] = h;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele scan
+        sc[cur ^ 1][p] = sc[cur][p] + (p >= o ? sc[cur][p - o] : 0);
+        cur ^= 1;
+        __syncthreads();
+    }
+    if (p < F) {
+        for (uint32_t q = 0; q < K; q++) {
+            start[(size_t)p * K + q] = q == 0 ? sc[cur][p] - h : 0;
+            cnt[(size_t)p * K + q] = q == 0 ? h : 0;
+        }
+    }
+}
+
+void hist_tables(const int64_t* hist, uint32_t F, uint32_t K, int64_t* start, int64_t* cnt,
+                 hipStream_t st) {
+    hipLaunchKernelGGL(k_hist_tables, dim3(1), dim3(1024), 0, st, hist, F, K, start, cnt);
+    SMJ_CHECK(hipGetLastError());
+}
+
 void xsend(const int64_t* start, const int64_t* cnt, const unsigned int* flags, uint32_t F,
            uint32_t K, uint32_t G, int64_t* msg, int64_t* chunk, hipStream_t st) {
     hipLaunchKernelGGL(k_xsend, dim3(1), dim3(256), 0, st, start, cnt, flags, F, K, G, msg,

@@ -1,0 +1,526 @@
+// mgpu.hip -- the multi-GPU join on the device: sortmergejoin_mpsm and
+// smj_mgpu_join (include/smj.h).
+//
+// One process drives G GPUs: rank g is a host thread with device g, two HIP
+// streams (kMain: partitions, tables, the local join; kRows: the row
+// exchange) and two RCCL communicators over the same devices, one per stream
+// (ncclCommInitAll), so that R's rows travel while S is partitioned and S's
+// rows while R's tiles are sorted.  The orchestration is mgpu_orch.hpp
+// (shared with the CPU tests' host stand-ins); this file gives it
+//   DevOps   -- the library's kernels on one rank's device and streams
+//               (smj_dev_partition_range_{planes,sampled,...}, the exchange
+//               tables, smj_dev_join_segmented_{tables,planes});
+//   DevColl  -- grouped ncclSend/ncclRecv (peers in NEXT order) and
+//               ncclAllReduce, or, when several ranks share one device (the
+//               single-GPU tests of the G-rank protocol), device copies
+//               between the ranks' buffers (mg::CopyColl).
+// Reference structure: the T join threads of joincommon.c:118-165 on their
+// chunks (:127-139), the co-partition exchange of
+// sortmergejoin_multiway.c:463-556, NEXT peer order numa_shuffle.c:83.
+#include <string.h>
+#include <sys/time.h>
+
+#include <map>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include <rccl/rccl.h>
+
+#include "../../include/smj.h"
+#include "mgpu_orch.hpp"
+#include "smj_common.hpp"
+#include "smj_internal.hpp"
+
+namespace smj {
+bool key_range(Workspace* ws, const Tup* const* rels, const uint64_t* ns, int nrel,
+               int64_t* lo, int64_t* hi, hipStream_t st);
+uint64_t materialize_append_on(Workspace* ws, hipStream_t st, const Tup* r, uint64_t nR,
+                               const Tup* s, uint64_t nS, chainedtuplebuffer_t* cb);
+bool materialize_on();
+}  // namespace smj
+
+using namespace smj;
+
+#define SMJ_NCCL(call)                                                              \
+    do {                                                                            \
+        ncclResult_t r_ = (call);                                                   \
+        if (r_ != ncclSuccess) {                                                    \
+            fprintf(stderr, "[ERROR] smj mpsm: RCCL %s at %s:%d: %s\n", #call,     \
+                    __FILE__, __LINE__, ncclGetErrorString(r_));                    \
+            abort();                                                                \
+        }                                                                           \
+    } while (0)
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// the device work of one rank
+// ---------------------------------------------------------------------------
+struct DevOps {
+    static constexpr int kTupleBytes = (int)sizeof(Tup);
+    int device = 0;
+    hipStream_t st[2] = {nullptr, nullptr};
+    hipEvent_t ev[mg::kNumEvents] = {};
+    Workspace* ws = nullptr;
+
+    smj_workspace* w() const { return (smj_workspace*)ws; }
+    bool can_pack() const { return sizeof(Tup) == 16; }
+    void* alloc(size_t b) {
+        void* p = nullptr;
+        SMJ_CHECK(hipMalloc(&p, b ? b : 16));
+        return p;
+    }
+    void release(void* p) { SMJ_CHECK(hipFree(p)); }
+    void* host_alloc(size_t b) {
+        void* p = nullptr;
+        SMJ_CHECK(hipHostMalloc(&p, b ? b : 16, hipHostMallocDefault));
+        return p;
+    }
+    void host_release(void* p) { SMJ_CHECK(hipHostFree(p)); }
+    void copy(void* d, const void* s, size_t b, int sid) {
+        if (b) SMJ_CHECK(hipMemcpyAsync(d, s, b, hipMemcpyDefault, st[sid]));
+    }
+    void to_host(void* h, const void* d, size_t b, int sid) {
+        if (b) SMJ_CHECK(hipMemcpyAsync(h, d, b, hipMemcpyDeviceToHost, st[sid]));
+    }
+    void to_dev(void* d, const void* h, size_t b, int sid) {
+        if (b) SMJ_CHECK(hipMemcpyAsync(d, h, b, hipMemcpyHostToDevice, st[sid]));
+    }
+    void fill_u32(void* p, uint32_t v, size_t count, int sid) {
+        if (count) SMJ_CHECK(hipMemsetD32Async((hipDeviceptr_t)p, (int)v, count, st[sid]));
+    }
+    void record(int e, int sid) { SMJ_CHECK(hipEventRecord(ev[e], st[sid])); }
+    void wait(int sid, int e) { SMJ_CHECK(hipStreamWaitEvent(st[sid], ev[e], 0)); }
+    void host_wait(int e) { SMJ_CHECK(hipEventSynchronize(ev[e])); }
+    void sync(int sid) { SMJ_CHECK(hipStreamSynchronize(st[sid])); }
+    uint32_t shards() { return smj_sampled_shards(); }
+    uint64_t sampled_capacity(uint64_t n, uint32_t nbits) { return smj_sampled_capacity(n, nbits); }
+    int part_planes(const void* in, uint64_t n, void* out, uint64_t stride, uint32_t nbits,
+                    int64_t kmin, int64_t kmax, int64_t* ss, int64_t* sc, uint32_t* flags) {
+        return smj_dev_partition_range_planes(w(), (const tuple_t*)in, n, out, stride, nbits,
+                                              kmin, kmax, ss, sc, flags, st[0]);
+    }
+    int part_sampled(const void* in, uint64_t n, void* out, uint32_t nbits, int64_t kmin,
+                     int64_t kmax, int packed, int64_t* ss, int64_t* sc, uint32_t* flags) {
+        return smj_dev_partition_range_sampled(w(), (const tuple_t*)in, n, out, nbits, kmin,
+                                               kmax, packed, ss, sc, flags, st[0]);
+    }
+    void part_exact(const void* in, uint64_t n, void* out, uint32_t nbits, int64_t kmin,
+                    int64_t kmax, int64_t* hist) {
+        smj_dev_partition_range(w(), (const tuple_t*)in, n, (tuple_t*)out, nbits, kmin, kmax,
+                                hist, st[0]);
+    }
+    int part_exact_packed(const void* in, uint64_t n, void* out, uint32_t nbits, int64_t kmin,
+                          int64_t kmax, int64_t* hist, uint32_t* bad) {
+        return smj_dev_partition_range_packed(w(), (const tuple_t*)in, n, (uint64_t*)out, nbits,
+                                              kmin, kmax, hist, bad, st[0]);
+    }
+    void hist_tables(const int64_t* hist, uint32_t F, uint32_t K, int64_t* ss, int64_t* sc) {
+        smj::hist_tables(hist, F, K, ss, sc, st[0]);
+    }
+    void xsend(const int64_t* ss, const int64_t* sc, const uint32_t* flags, uint32_t F,
+               uint32_t K, uint32_t G, int64_t* msg, int64_t* chunk) {
+        smj::xsend(ss, sc, flags, F, K, G, msg, chunk, st[0]);
+    }
+    void xrecv(const int64_t* msg, const int64_t* chunk, uint32_t G, uint32_t rank,
+               uint32_t mine, uint32_t K, uint32_t nb, uint64_t cap, int64_t* ts, int64_t* tc,
+               int64_t* summary) {
+        smj::xrecv(msg, chunk, G, rank, mine, K, nb, cap, ts, tc, summary, st[0]);
+    }
+    void join(int lay, void* R, uint64_t strideR, uint64_t nR, const int64_t* tsR,
+              const int64_t* tcR, void* S, uint64_t strideS, uint64_t nS, const int64_t* tsS,
+              const int64_t* tcS, uint32_t nseg, uint32_t lbits, int64_t klo, int64_t khi,
+              int stage, void* sortedR, void* sortedS, unsigned long long* count) {
+        const uint32_t sf = stage == 1 ? SMJ_SEG_STAGE_R : stage == 2 ? SMJ_SEG_STAGE_REST : 0u;
+        if (lay == mg::kPlanes)
+            smj_dev_join_segmented_planes(w(), R, strideR, nR, tsR, tcR, S, strideS, nS, tsS,
+                                          tcS, nseg, lbits, klo, khi, sf, (tuple_t*)sortedR,
+                                          (tuple_t*)sortedS, count, st[0]);
+        else
+            smj_dev_join_segmented_tables(w(), R, nR, tsR, tcR, S, nS, tsS, tcS, nseg, lbits,
+                                          klo, khi, sf | (lay == mg::kWords ? SMJ_SEG_PACKED : 0u),
+                                          (tuple_t*)sortedR, (tuple_t*)sortedS, count, st[0]);
+    }
+    bool key_range(const void* R, uint64_t nR, const void* S, uint64_t nS, int64_t* lo,
+                   int64_t* hi) {
+        const Tup* rels[2] = {(const Tup*)R, (const Tup*)S};
+        const uint64_t ns[2] = {nR, nS};
+        return smj::key_range(ws, rels, ns, 2, lo, hi, st[0]);
+    }
+};
+
+// ---------------------------------------------------------------------------
+// collectives: RCCL, one communicator per stream; or device copies
+// ---------------------------------------------------------------------------
+struct DevColl {
+    bool rccl = true;
+    ncclComm_t comm[2] = {nullptr, nullptr};
+    DevOps* ops = nullptr;
+    int me = 0;
+    mg::CopyColl<DevOps> copy;
+
+    void exchange(int sid, const std::vector<mg::Piece>& sends,
+                  const std::vector<mg::Piece>& recvs) {
+        if (!rccl) {
+            copy.exchange(sid, sends, recvs);
+            return;
+        }
+        // a rank's pieces to itself are a device copy (the k-th sent with the
+        // k-th received); the others one group of sends and receives, issued
+        // per peer in NEXT order as the pieces come
+        std::vector<const mg::Piece*> self_s, self_r;
+        SMJ_NCCL(ncclGroupStart());
+        for (const mg::Piece& p : sends) {
+            if (p.peer == me) self_s.push_back(&p);
+            else if (p.bytes)
+                SMJ_NCCL(ncclSend(p.ptr, p.bytes, ncclUint8, p.peer, comm[sid], ops->st[sid]));
+        }
+        for (const mg::Piece& p : recvs) {
+            if (p.peer == me) self_r.push_back(&p);
+            else if (p.bytes)
+                SMJ_NCCL(ncclRecv(p.ptr, p.bytes, ncclUint8, p.peer, comm[sid], ops->st[sid]));
+        }
+        SMJ_NCCL(ncclGroupEnd());
+        if (self_s.size() != self_r.size()) {
+            fprintf(stderr, "[ERROR] smj mpsm: %zu pieces to self, %zu from self\n",
+                    self_s.size(), self_r.size());
+            abort();
+        }
+        for (size_t k = 0; k < self_s.size(); k++)
+            ops->copy(self_r[k]->ptr, self_s[k]->ptr, self_s[k]->bytes, sid);
+    }
+    void allreduce_sum_u64(int sid, unsigned long long* p) {
+        if (!rccl) {
+            copy.allreduce_sum_u64(sid, p);
+            return;
+        }
+        SMJ_NCCL(ncclAllReduce(p, p, 1, ncclUint64, ncclSum, comm[sid], ops->st[sid]));
+    }
+};
+
+typedef mg::Rank<DevOps, DevColl> DevRank;
+
+// One rank's device state, kept across calls (streams, events, workspace and
+// the rank's sticky exchange buffers).
+struct RankCtx {
+    DevOps ops;
+    DevColl coll;
+    DevRank rank;
+    Workspace ws;
+    void* inbuf[2] = {nullptr, nullptr};  // staged input slices
+    size_t inbytes[2] = {0, 0};
+    int device = 0;
+
+    explicit RankCtx(int dev) : device(dev) {
+        SMJ_CHECK(hipSetDevice(dev));
+        for (int s = 0; s < 2; s++)
+            SMJ_CHECK(hipStreamCreateWithFlags(&ops.st[s], hipStreamNonBlocking));
+        for (auto& e : ops.ev) SMJ_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        ops.device = dev;
+        ops.ws = &ws;
+        coll.ops = &ops;
+        rank.ops = &ops;
+        rank.coll = &coll;
+    }
+    ~RankCtx() {
+        (void)hipSetDevice(device);
+        rank.release_all();
+        for (int r = 0; r < 2; r++)
+            if (inbuf[r]) (void)hipFree(inbuf[r]);
+        for (auto& e : ops.ev) (void)hipEventDestroy(e);
+        for (int s = 0; s < 2; s++) (void)hipStreamDestroy(ops.st[s]);
+    }
+};
+
+// The process's ranks for one configuration (G ranks, RCCL or copies); a
+// call with another configuration releases them first.  Calls are
+// serialised: every call uses all of the configuration's devices.
+struct Group {
+    int G = 0;
+    bool rccl = true;
+    std::vector<std::unique_ptr<RankCtx>> ranks;
+    std::vector<ncclComm_t> comms[2];
+    std::unique_ptr<mg::HostGroup> host;
+
+    ~Group() {
+        for (auto& c : comms)
+            for (ncclComm_t x : c)
+                if (x) (void)ncclCommDestroy(x);
+        ranks.clear();
+    }
+};
+
+std::mutex g_mu;
+std::unique_ptr<Group> g_group;
+
+Group& group_for(int G, bool rccl) {
+    if (g_group && g_group->G == G && g_group->rccl == rccl) return *g_group;
+    g_group.reset();
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        fprintf(stderr, "[ERROR] smj: no HIP device visible; the MI355X library has no CPU "
+                        "fallback.\n");
+        abort();
+    }
+    if (rccl && G > ndev) {
+        fprintf(stderr, "[ERROR] smj mpsm: %d RCCL ranks need %d devices (%d visible); "
+                        "SMJ_MG_COPY runs ranks on shared devices\n", G, G, ndev);
+        abort();
+    }
+    std::unique_ptr<Group> g(new Group());
+    g->G = G;
+    g->rccl = rccl;
+    g->host.reset(new mg::HostGroup(G));
+    for (int r = 0; r < G; r++) g->ranks.emplace_back(new RankCtx(r % ndev));
+    if (rccl) {
+        std::vector<int> devs((size_t)G);
+        for (int r = 0; r < G; r++) devs[r] = r;
+        for (int c = 0; c < 2; c++) {
+            g->comms[c].assign((size_t)G, nullptr);
+            SMJ_NCCL(ncclCommInitAll(g->comms[c].data(), G, devs.data()));
+        }
+    }
+    for (int r = 0; r < G; r++) {
+        RankCtx& rc = *g->ranks[r];
+        rc.rank.grp = g->host.get();
+        rc.rank.me = r;
+        rc.rank.G = G;
+        rc.coll.rccl = rccl;
+        rc.coll.me = r;
+        if (rccl)
+            for (int c = 0; c < 2; c++) rc.coll.comm[c] = g->comms[c][r];
+        rc.coll.copy.grp = g->host.get();
+        rc.coll.copy.ops = &rc.ops;
+        rc.coll.copy.me = r;
+    }
+    g_group = std::move(g);
+    return *g_group;
+}
+
+// device of a pointer (-1: host memory)
+int ptr_device(const void* p) {
+    if (!p) return -1;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged) return a.device;
+    return -1;
+}
+
+// Rank r's slice [off, off + n) of a caller relation on the rank's device: in
+// place when it already lies there, else copied (host -> device, or peer).
+const void* stage_slice(RankCtx& rc, int rel, const Tup* base, uint64_t off, uint64_t n) {
+    const Tup* p = base + off;
+    if (n == 0) return p;
+    if (ptr_device(base) == rc.device) return p;
+    const size_t b = n * sizeof(Tup);
+    if (rc.inbytes[rel] < b) {
+        if (rc.inbuf[rel]) SMJ_CHECK(hipFree(rc.inbuf[rel]));
+        SMJ_CHECK(hipMalloc(&rc.inbuf[rel], b));
+        rc.inbytes[rel] = b;
+    }
+    SMJ_CHECK(hipMemcpyAsync(rc.inbuf[rel], p, b, hipMemcpyDefault, rc.ops.st[0]));
+    return rc.inbuf[rel];
+}
+
+struct CallArgs {
+    const Tup* R;
+    uint64_t nR;
+    const Tup* S;
+    uint64_t nS;
+    mg::Options opt;
+    Tup* sortedR = nullptr;  // host or device destinations of the sorted shares
+    Tup* sortedS = nullptr;
+    int mat = 0;             // materialise into per-rank buffers
+    result_t* res = nullptr;
+};
+
+struct CallOut {
+    uint64_t total = 0;
+    std::vector<uint64_t> nR, nS, local;
+    mg::Stats stats;
+    double ms = 0;
+};
+
+void run_call(Group& grp, const CallArgs& a, CallOut& out) {
+    const int G = grp.G;
+    out.nR.assign((size_t)G, 0);
+    out.nS.assign((size_t)G, 0);
+    out.local.assign((size_t)G, 0);
+    std::vector<uint64_t> total((size_t)G, 0);
+    // joincommon.c:127-139: thread i takes [i n / T, (i + 1) n / T), the last
+    // one the rest
+    const uint64_t perR = a.nR / G, perS = a.nS / G;
+    struct timeval t0, t1;
+    gettimeofday(&t0, NULL);
+    mg::run_ranks(G, [&](int r) {
+        RankCtx& rc = *grp.ranks[r];
+        SMJ_CHECK(hipSetDevice(rc.device));
+        const uint64_t nr = r == G - 1 ? a.nR - perR * r : perR;
+        const uint64_t ns = r == G - 1 ? a.nS - perS * r : perS;
+        const void* R = stage_slice(rc, 0, a.R, perR * r, nr);
+        const void* S = stage_slice(rc, 1, a.S, perS * r, ns);
+        uint64_t onR = 0, onS = 0, loc = 0;
+        total[r] = rc.rank.run(R, nr, S, ns, a.opt, &onR, &onS, &loc);
+        out.nR[r] = onR;
+        out.nS[r] = onS;
+        out.local[r] = loc;
+        // the sorted shares, concatenated in rank order (one contiguous key
+        // range per rank, ascending)
+        if (a.sortedR || a.sortedS) {
+            grp.host->barrier();
+            uint64_t oR = 0, oS = 0;
+            for (int g = 0; g < r; g++) {
+                oR += out.nR[g];
+                oS += out.nS[g];
+            }
+            if (a.sortedR) rc.ops.copy(a.sortedR + oR, rc.rank.sorted[0], onR * sizeof(Tup), 0);
+            if (a.sortedS) rc.ops.copy(a.sortedS + oS, rc.rank.sorted[1], onS * sizeof(Tup), 0);
+            rc.ops.sync(0);
+        }
+        if (a.mat && a.res) {
+            chainedtuplebuffer_t* cb = chainedtuplebuffer_init();
+            materialize_append_on(&rc.ws, rc.ops.st[0], (const Tup*)rc.rank.sorted[0], onR,
+                                  (const Tup*)rc.rank.sorted[1], onS, cb);
+            a.res->resultlist[r].results = cb;
+        }
+    });
+    gettimeofday(&t1, NULL);
+    for (int r = 1; r < G; r++)
+        if (total[r] != total[0]) {
+            fprintf(stderr, "[ERROR] smj mpsm: ranks disagree on the count (%llu, %llu)\n",
+                    (unsigned long long)total[0], (unsigned long long)total[r]);
+            abort();
+        }
+    out.total = total[0];
+    out.stats = grp.ranks[0]->rank.stats;
+    out.ms = (t1.tv_sec - t0.tv_sec) * 1e3 + (t1.tv_usec - t0.tv_usec) * 1e-3;
+}
+
+}  // namespace
+
+namespace smj {
+
+// sortmergejoin_mpsm: NTHREADS ranks, at most one per visible GPU (the
+// reference's T threads become T GPUs; a 1-GPU host runs one rank), RCCL
+// collectives; the key range guessed as 1..|R| like sortmergejoin_multiway
+// (the reference's radix shift assumes it, sortmergejoin_multiway.c:372-376)
+// and verified by the exchange partition.
+result_t* mpsm_api(relation_t* relR, relation_t* relS, joinconfig_t* joincfg, int mat) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        fprintf(stderr, "[ERROR] smj: no HIP device visible; the MI355X library has no CPU "
+                        "fallback.\n");
+        abort();
+    }
+    const int T = joincfg->NTHREADS > 0 ? joincfg->NTHREADS : 1;
+    const int G = T < ndev ? T : ndev;
+    std::lock_guard<std::mutex> lk(g_mu);
+    int dev0 = 0;
+    SMJ_CHECK(hipGetDevice(&dev0));
+    Group& grp = group_for(G, true);
+    CallArgs a;
+    a.R = (const Tup*)relR->tuples;
+    a.nR = relR->num_tuples;
+    a.S = (const Tup*)relS->tuples;
+    a.nS = relS->num_tuples;
+    a.opt.guess_max = a.nR;
+    a.mat = (mat < 0 ? materialize_on() : mat > 0) ? 1 : 0;
+    result_t* res = (result_t*)malloc(sizeof(result_t));
+    res->nthreads = T;
+    res->resultlist = (threadresult_t*)calloc((size_t)T, sizeof(threadresult_t));
+    a.res = res;
+    CallOut o;
+    run_call(grp, a, o);
+    SMJ_CHECK(hipSetDevice(dev0));
+    res->totalresults = (int64_t)o.total;
+    for (int r = 0; r < G; r++) {
+        res->resultlist[r].nresults = (int64_t)o.local[r];
+        res->resultlist[r].threadid = (uint32_t)r;
+    }
+    if (!getenv("SMJ_QUIET")) {
+        // the reference's stats lines (joincommon.c:176-196); host microseconds
+        const unsigned long long us = (unsigned long long)(o.ms * 1e3);
+        fprintf(stdout, "Total, Partitioning, Sort, First-Merge, Merge, Join\n");
+        fprintf(stdout, "%llu, 0, 0, 0, 0, %llu\n", us, us);
+        fprintf(stdout, "[INFO ] mpsm: %d GPU%s, exchange in %s, 2^%u partitions, %d "
+                        "attempts\n", G, G > 1 ? "s" : "", mg::layout_name(o.stats.layout),
+                o.stats.pbits, o.stats.attempts);
+        fprintf(stderr, "NUM-TUPLES = %lld TOTAL-TIME-USECS = %.4lf ", (long long)a.nS,
+                o.ms * 1e3);
+        fprintf(stderr, "TUPLES-PER-SECOND = %.4lf ", a.nS / (o.ms * 1e-3));
+        fflush(stdout);
+        fflush(stderr);
+    }
+    return res;
+}
+
+}  // namespace smj
+
+extern "C" {
+
+int64_t smj_mgpu_join(const tuple_t* R, uint64_t nR, const tuple_t* S, uint64_t nS, int nranks,
+                      uint32_t flags, int64_t key_min, int64_t key_max, tuple_t* sortedR,
+                      tuple_t* sortedS, uint64_t* rank_counts, smj_mgpu_stats* stats) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        fprintf(stderr, "[ERROR] smj: no HIP device visible; the MI355X library has no CPU "
+                        "fallback.\n");
+        abort();
+    }
+    const int G = nranks > 0 ? nranks : ndev;
+    if (G > 64) {
+        fprintf(stderr, "[ERROR] smj_mgpu_join: %d ranks (at most 64)\n", G);
+        abort();
+    }
+    std::lock_guard<std::mutex> lk(g_mu);
+    int dev0 = 0;
+    SMJ_CHECK(hipGetDevice(&dev0));
+    Group& grp = group_for(G, !(flags & SMJ_MG_COPY));
+    CallArgs a;
+    a.R = (const Tup*)R;
+    a.nR = nR;
+    a.S = (const Tup*)S;
+    a.nS = nS;
+    if (key_min <= key_max) {
+        a.opt.kmin = key_min;
+        a.opt.kmax = key_max;
+    } else {
+        a.opt.guess_max = nR;
+    }
+    a.opt.planes = !(flags & SMJ_MG_NOPLANES);
+    a.opt.staged = !(flags & SMJ_MG_ONECALL);
+    a.opt.sampled = (flags & SMJ_MG_SAMPLED) ? 1 : (flags & SMJ_MG_EXACT) ? 0 : -1;
+    a.sortedR = (Tup*)sortedR;
+    a.sortedS = (Tup*)sortedS;
+    CallOut o;
+    run_call(grp, a, o);
+    SMJ_CHECK(hipSetDevice(dev0));
+    if (rank_counts)
+        for (int r = 0; r < G; r++) {
+            rank_counts[2 * r] = o.nR[r];
+            rank_counts[2 * r + 1] = o.nS[r];
+        }
+    if (stats) {
+        stats->layout = o.stats.layout;
+        stats->pbits = o.stats.pbits;
+        stats->attempts = o.stats.attempts;
+        stats->replans = o.stats.replans;
+        stats->sent_bytes = o.stats.sent_B;
+        stats->recv_bytes = o.stats.recv_B;
+        stats->key_min = o.stats.kmin;
+        stats->key_max = o.stats.kmax;
+        stats->ms = o.ms;
+    }
+    return (int64_t)o.total;
+}
+
+void smj_mgpu_release(void) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_group.reset();
+}
+
+}  // extern "C"

@@ -259,6 +259,9 @@ void xsend(const int64_t* start, const int64_t* cnt, const unsigned int* flags, 
 void xrecv(const int64_t* msg, const int64_t* chunk, uint32_t G, uint32_t rank, uint32_t mine,
            uint32_t K, uint32_t nb, uint64_t cap, int64_t* tstart, int64_t* tcnt,
            int64_t* summary, hipStream_t st);
+// exact partition (hist) -> start/cnt tables of K shards, shard 0 used (F <= 1024)
+void hist_tables(const int64_t* hist, uint32_t F, uint32_t K, int64_t* start, int64_t* cnt,
+                 hipStream_t st);
 
 // ---- partition.hip
 void stable_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,

@@ -64,7 +64,7 @@ DEVICE_SYMBOLS = [
     "smj_sampled_capacity", "smj_sampled_shards", "smj_context_workspace",
     "smj_dev_gen_nonunique", "smj_dev_gen_zipf_ref", "smj_glibc_rand",
     "smj_dev_xsend", "smj_dev_xrecv", "smj_join", "smj_dev_partition_range_planes",
-    "smj_dev_join_segmented_planes",
+    "smj_dev_join_segmented_planes", "smj_mgpu_join", "smj_mgpu_release",
 ]
 
 
@@ -96,6 +96,18 @@ class ThreadResult(C.Structure):
 class Result(C.Structure):
     _fields_ = [("totalresults", C.c_int64),
                 ("resultlist", C.POINTER(ThreadResult)), ("nthreads", C.c_int)]
+
+
+class MgpuStats(C.Structure):
+    """include/smj.h smj_mgpu_stats."""
+    _fields_ = [("layout", C.c_int), ("pbits", C.c_uint32), ("attempts", C.c_int),
+                ("replans", C.c_int), ("sent_bytes", C.c_uint64), ("recv_bytes", C.c_uint64),
+                ("key_min", C.c_int64), ("key_max", C.c_int64), ("ms", C.c_double)]
+
+
+# smj_mgpu_join flags (include/smj.h)
+MG_COPY, MG_NOPLANES, MG_ONECALL, MG_SAMPLED, MG_EXACT = 1, 2, 4, 8, 16
+MG_LAYOUTS = ("tuples", "words", "planes")
 
 
 class ChainedTupleBuffer(C.Structure):
@@ -201,6 +213,9 @@ class Library:
             "smj_dev_xsend": (None, [_P, _P, _P, _U32, _U32, _U32, _P, _P, _P]),
             "smj_dev_xrecv": (None, [_P, _P, _U32, _U32, _U32, _U32, _U32, _U64, _P, _P, _P,
                                      _P]),
+            "smj_mgpu_join": (_I64, [_P, _U64, _P, _U64, C.c_int, _U32, _I64, _I64, _P, _P,
+                                     _P, _P]),
+            "smj_mgpu_release": (None, []),
             "smj_trace_enable": (None, [_P, C.c_int]),
             "smj_trace_reset": (None, [_P]),
             "smj_trace_only": (None, [_P, C.c_char_p]),
@@ -331,6 +346,43 @@ class Library:
             return n, self._take_buffer(cb)
         finally:
             self.lib.chainedtuplebuffer_free(cb)
+
+    def mgpu_join(self, R, S, nranks=0, flags=0, key_range=None, sorted_out=True):
+        """smj_mgpu_join: the multi-GPU join of sortmergejoin_mpsm over
+        `nranks` ranks (0: one per visible GPU; MG_COPY: ranks may share a
+        GPU).  R and S are host numpy arrays or device torch tensors (shape
+        (n, 2)).  Returns (count, sorted R, sorted S, per-rank (nR, nS),
+        stats dict); the sorted relations are the ranks' shares in rank order
+        (None unless sorted_out)."""
+        dev = not isinstance(R, np.ndarray)
+        if dev:
+            nR, nS = R.shape[0], S.shape[0]
+            pR, pS = R.data_ptr(), S.data_ptr()
+            sR = R.new_empty(R.shape) if sorted_out else None
+            sS = S.new_empty(S.shape) if sorted_out else None
+            qR = sR.data_ptr() if sorted_out else None
+            qS = sS.data_ptr() if sorted_out else None
+        else:
+            R = np.ascontiguousarray(R, dtype=self.dtype)
+            S = np.ascontiguousarray(S, dtype=self.dtype)
+            nR, nS = len(R), len(S)
+            pR, pS = (_ptr(R) if nR else None), (_ptr(S) if nS else None)
+            sR = np.zeros(nR, self.dtype) if sorted_out else None
+            sS = np.zeros(nS, self.dtype) if sorted_out else None
+            qR = _ptr(sR) if sorted_out and nR else None
+            qS = _ptr(sS) if sorted_out and nS else None
+        G = nranks
+        if G <= 0:
+            import torch as _t
+            G = _t.cuda.device_count()
+        counts = np.zeros(2 * G, np.uint64)
+        st = MgpuStats()
+        kmin, kmax = key_range if key_range is not None else (1, 0)
+        c = self.lib.smj_mgpu_join(pR, nR, pS, nS, G, flags, kmin, kmax, qR, qS,
+                                   _ptr(counts), C.byref(st))
+        stats = {f: getattr(st, f) for f, _ in MgpuStats._fields_}
+        stats["layout"] = MG_LAYOUTS[stats["layout"]]
+        return int(c), sR, sS, counts.reshape(G, 2), stats
 
     def sortmergejoin_multiway(self, R, S, nthreads=1, fanout=128, mpsm=False,
                                algo=None, materialize=False, persist=None):

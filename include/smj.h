@@ -383,11 +383,57 @@ result_t * sortmergejoin_multiway(relation_t * relR, relation_t * relS,
 result_t * sortmergejoin_multipass(relation_t * relR, relation_t * relS,
                                    joinconfig_t * joincfg);
 
-/* sortmergejoin_mpsm.c is a stub that exits in the reference; here it is the
- * same device pipeline (one process drives one GPU; multi-GPU runs shard
- * with smj_dev_* + an RCCL all-to-all). */
+/* sortmergejoin_mpsm.c:38-45 is a stub that exits in the reference; SURVEY.md
+ * §2 row 9 and BASELINE configs[4] make it the multi-GPU join, and here it is
+ * that: G = min(NTHREADS, visible GPUs) ranks in this process, one host thread
+ * and one GPU each (the reference's T threads, joincommon.c:118-165, on
+ * contiguous chunks of R and S, :127-139).  Every rank range-partitions its
+ * chunks on its GPU, the partitions go to their owner GPUs over RCCL (grouped
+ * ncclSend/ncclRecv, peers in NEXT order, numa_shuffle.c:83; the co-partition
+ * exchange of sortmergejoin_multiway.c:463-556), each GPU sorts and joins the
+ * contiguous key range it owns, and the counts are all-reduced
+ * (ncclAllReduce).  totalresults = the global count; resultlist[g].nresults
+ * = rank g's; with materialisation resultlist[g].results holds rank g's
+ * matches (ranks in key order).  Keys are planned as 1..|R| like the m-way
+ * join and verified (a key outside -> the measured range). */
 result_t * sortmergejoin_mpsm(relation_t * relR, relation_t * relS,
                               joinconfig_t * joincfg);
+
+/* The multi-GPU join of sortmergejoin_mpsm with its outputs (library
+ * extension).  nranks ranks (0 = one per visible GPU); R and S in host memory
+ * or in device memory any rank's GPU can read; rank g takes the g-th chunk of
+ * each (the last one the rest).  key_min <= key_max: the key range (keys
+ * outside it are legal but unbalance the ranks); otherwise 1..nR, verified.
+ * sortedR / sortedS (optional, nR / nS tuples, host or device): the sorted
+ * relations, the ranks' shares concatenated in rank order -- each rank owns
+ * one contiguous key range, so this is the globally sorted relation.
+ * rank_counts (optional, 2 * nranks): the tuples of R and of S each rank
+ * sorted.  Returns the number of matching pairs. */
+#define SMJ_MG_COPY     1u  /* collectives by device copies instead of RCCL:
+                               ranks may share a GPU (rank g on device g mod
+                               the visible count); every exchange synchronises */
+#define SMJ_MG_NOPLANES 2u  /* no 48-bit planes: 64-bit words or tuples */
+#define SMJ_MG_ONECALL  4u  /* the local join in one call (not staged) */
+#define SMJ_MG_SAMPLED  8u  /* sampled exchange partitions (default: one rank) */
+#define SMJ_MG_EXACT   16u  /* exact exchange partitions (default: > 1 rank) */
+typedef struct smj_mgpu_stats {
+    int      layout;      /* of the exchange: 0 tuples, 1 64-bit words, 2 48-bit planes */
+    uint32_t pbits;       /* exchange partitions = 2^pbits */
+    int      attempts;    /* exchange attempts of rank 0 (2 = none repeated) */
+    int      replans;     /* the guessed key range replaced by the measured one */
+    uint64_t sent_bytes;  /* rows rank 0 sent to other ranks */
+    uint64_t recv_bytes;  /* ... and received */
+    int64_t  key_min;     /* the global plan's range */
+    int64_t  key_max;
+    double   ms;          /* host wall time of the call */
+} smj_mgpu_stats;
+int64_t smj_mgpu_join(const tuple_t * R, uint64_t nR, const tuple_t * S, uint64_t nS,
+                      int nranks, uint32_t flags, int64_t key_min, int64_t key_max,
+                      tuple_t * sortedR, tuple_t * sortedS, uint64_t * rank_counts,
+                      smj_mgpu_stats * stats);
+/* Frees the ranks' devices buffers, streams and communicators (kept across
+ * calls of one configuration). */
+void smj_mgpu_release(void);
 
 /* ------------------------------------------------------------------------ */
 /* Device-resident asynchronous API (no reference counterpart: this is the   */
