@@ -345,8 +345,18 @@ struct CallOut {
     double ms = 0;
 };
 
-void run_call(Group& grp, const CallArgs& a, CallOut& out) {
+// level-1 buckets per rank: 2^8 (the 1-GPU join's fan-out), more while a
+// bucket would exceed the tile pass's kLocalBucketCap (the 1024M-per-rank
+// join of BASELINE configs[4] on one GPU: 2^9)
+uint32_t bucket_bits_for(uint64_t n_per_rank) {
+    uint32_t b = 8;
+    while (b < mg::kMaxPartBits && (n_per_rank >> b) > mg::kLocalBucketCap) b++;
+    return b;
+}
+
+void run_call(Group& grp, CallArgs a, CallOut& out) {
     const int G = grp.G;
+    a.opt.bucket_bits = bucket_bits_for(std::max(a.nR, a.nS) / (uint64_t)G);
     out.nR.assign((size_t)G, 0);
     out.nS.assign((size_t)G, 0);
     out.local.assign((size_t)G, 0);

@@ -1502,7 +1502,17 @@ k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
                 const uint64_t p = pos[d];
                 const OutT x0 = e < k ? carry[d * SEG + e] : stage[tstart[d] + e - k];
                 const OutT x1 = e + 1 < k ? carry[d * SEG + e + 1] : stage[tstart[d] + e + 1 - k];
-                if (p != ~0ull) Pack::store2(out, ostride, p + e, x0, x1);
+                // p is odd after a workgroup sharing this shard cursor flushed
+                // an odd carry (the flush below): the pair store needs p + e
+                // even (e is), else two element stores
+                if (p != ~0ull) {
+                    if ((p & 1) == 0) {
+                        Pack::store2(out, ostride, p + e, x0, x1);
+                    } else {
+                        Pack::store(out, ostride, p + e, x0);
+                        Pack::store(out, ostride, p + e + 1, x1);
+                    }
+                }
             }
         } else {
             for (uint32_t q = threadIdx.x; q < nseg * SEG; q += THREADS) {

@@ -37,6 +37,8 @@
 #include <thread>
 #include <vector>
 
+#include <sys/mman.h>
+
 #include "smj_common.hpp"
 #include "smj_internal.hpp"
 
@@ -277,19 +279,56 @@ static void zipf_tables(Workspace* ws, uint32_t seed, uint64_t skip, uint32_t si
         // gen_alphabet (genzipf.c:28-53): values 1..size, then for i = size-1
         // down to 1 swap with k = i * rand() / RAND_MAX, the rand() calls
         // skip, skip + 1, ... of the stream
-        std::vector<uint32_t> ha(size);
-        for (uint32_t i = 0; i < size; i++) ha[i] = i + 1;
+        // The swaps are serial through the array, but the draws, and so the
+        // swap targets k, are known ahead: the target PD swaps ahead is
+        // prefetched, so ~PD cache misses are in flight instead of one (the
+        // 1024M alphabet of BASELINE configs[4] is 4 GB of random swaps).
+        // Huge pages keep the TLB walks off the misses.
+        const size_t abytes = ((size_t)size * 4 + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
+        uint32_t* ha = (uint32_t*)aligned_alloc(2u << 20, abytes);
+        if (!ha) {
+            perror("[ERROR] smj: zipf alphabet");
+            abort();
+        }
+        madvise(ha, abytes, MADV_HUGEPAGE);
+        {
+            unsigned nt = std::thread::hardware_concurrency();
+            nt = nt < 1 ? 1 : (nt > 16 ? 16 : nt);
+            std::vector<std::thread> th;
+            for (unsigned q = 0; q < nt; q++)
+                th.emplace_back([&, q] {
+                    const uint64_t lo = (uint64_t)size * q / nt, hi = (uint64_t)size * (q + 1) / nt;
+                    for (uint64_t i = lo; i < hi; i++) ha[i] = (uint32_t)(i + 1);
+                });
+            for (auto& t : th) t.join();
+        }
         if (size > 1) {
             uint32_t w[kLag], o[kLag];
             window_for_output(seed, skip, w);
             int used = kLag;
-            for (uint32_t i = size - 1; i > 0; i--) {
+            auto draw_k = [&](uint32_t i) {
                 if (used == kLag) {
                     turn(w, o);
                     used = 0;
                 }
-                const uint32_t rnd = o[used++];
-                const uint32_t k = (uint32_t)((unsigned long)i * rnd / 2147483647ul);
+                return (uint32_t)((unsigned long)i * o[used++] / 2147483647ul);
+            };
+            constexpr uint32_t PD = 64;  // swaps in flight
+            uint32_t ring[PD];
+            uint32_t gi = size - 1;      // next i whose k is drawn
+            for (uint32_t d = 0; d < PD && gi > 0; d++, gi--) {
+                ring[d] = draw_k(gi);
+                __builtin_prefetch(&ha[ring[d]], 1);
+            }
+            uint32_t slot = 0;
+            for (uint32_t i = size - 1; i > 0; i--) {
+                const uint32_t k = ring[slot];
+                if (gi > 0) {
+                    const uint32_t nk = draw_k(gi--);
+                    ring[slot] = nk;
+                    __builtin_prefetch(&ha[nk], 1);
+                }
+                slot = slot + 1 == PD ? 0 : slot + 1;
                 const uint32_t tmp = ha[i];
                 ha[i] = ha[k];
                 ha[k] = tmp;
@@ -316,10 +355,17 @@ static void zipf_tables(Workspace* ws, uint32_t seed, uint64_t skip, uint32_t si
             hl[i] = sum;
         }
         const double scale = sum;
-        for (uint32_t i = 0; i < size; i++) hl[i] = hl[i] / scale;
-        SMJ_CHECK(hipMemcpyAsync(a, ha.data(), (size_t)size * 4, hipMemcpyHostToDevice, st));
+        std::vector<std::thread> th2;
+        for (unsigned q = 0; q < nt; q++)
+            th2.emplace_back([&, q] {
+                const uint64_t lo = (uint64_t)size * q / nt, hi = (uint64_t)size * (q + 1) / nt;
+                for (uint64_t i = lo; i < hi; i++) hl[i] = hl[i] / scale;
+            });
+        for (auto& t : th2) t.join();
+        SMJ_CHECK(hipMemcpyAsync(a, ha, (size_t)size * 4, hipMemcpyHostToDevice, st));
         SMJ_CHECK(hipMemcpyAsync(l, hl.data(), (size_t)size * 8, hipMemcpyHostToDevice, st));
-        SMJ_CHECK(hipStreamSynchronize(st));  // the host vectors go out of scope
+        SMJ_CHECK(hipStreamSynchronize(st));  // the host arrays go out of scope
+        free(ha);
         cache.seed = seed;
         cache.skip = skip;
         cache.size = size;

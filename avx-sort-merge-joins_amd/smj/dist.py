@@ -341,16 +341,42 @@ class DeviceOps:
         self.lib.dev_xrecv(msg, chunk, world, rank, mine, K, tstart, tcnt, cap, summary)
 
 
+# The row exchange's own communicator per process group (a second RCCL
+# communicator over the same ranks, so R's rows are not queued behind S's
+# table exchange): created once per group and shared by every DistributedJoin
+# on it.  new_group with use_local_synchronization involves only the group's
+# members, so a join built on a sub-group does not need the ranks outside it.
+_ROW_GROUPS = {}
+
+
+def _row_group(group, ranks):
+    key = (id(group) if group is not None else None, tuple(ranks))
+    g = _ROW_GROUPS.get(key)
+    if g is None:
+        g = dist.new_group(ranks=ranks, use_local_synchronization=True)
+        _ROW_GROUPS[key] = g
+    return g
+
+
+def release_row_groups():
+    """Destroy the cached row communicators (before destroy_process_group,
+    or when the groups they mirror go away)."""
+    for g in _ROW_GROUPS.values():
+        dist.destroy_process_group(g)
+    _ROW_GROUPS.clear()
+
+
 class DistributedJoin:
     """One process per device; `step` joins the local slices of R and S
     against the slices on all other ranks and leaves the GLOBAL match count in
     `count` on every rank.  `bucket_bits`: level-1 buckets per rank (2^9 =
     512, what the 1-GPU join uses); `n_hint`: elements per rank and relation,
     identical on every rank (lets the 48-bit planes take 2^9 partitions
-    across ranks, partition_bits)."""
+    across ranks, partition_bits); `row_group`: the communicator the rows
+    travel on (default: one per `group`, cached, see _row_group)."""
 
     def __init__(self, ops, bucket_bits: int, key_min: int, key_max: int,
-                 group=None, n_hint=None):
+                 group=None, n_hint=None, row_group=None):
         self.ops = ops
         self.group = group
         self.world = dist.get_world_size(group)
@@ -386,10 +412,9 @@ class DistributedJoin:
         self.staged = os.environ.get("SMJ_XSTAGED", "1") != "0"
         # the rows travel on a communicator of their own: its stream is not
         # ordered behind the table exchange of S (queued behind S's partition)
-        self.row_group = None
-        if self.world > 1:
-            ranks = [self._global(g) for g in range(self.world)]
-            self.row_group = dist.new_group(ranks=ranks)
+        self.row_group = row_group
+        if self.world > 1 and row_group is None:
+            self.row_group = _row_group(group, [self._global(g) for g in range(self.world)])
         self.recv_hint = {}  # remote rows received per relation and layout (sticky)
         self.last_recv = {}
         self.last_rows = {}

@@ -30,6 +30,14 @@ import torch  # noqa: E402  (owns the HIP runtime before the library loads)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
+def _close(dist):
+    """Destroy the process group (and the join's cached row communicators)."""
+    mod = sys.modules.get("smj.dist")
+    if mod is not None:
+        mod.release_row_groups()
+    dist.destroy_process_group()
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -467,7 +475,7 @@ def main():
 
     if rank != 0:
         if dist:
-            dist.destroy_process_group()
+            _close(dist)
         return
 
     cfg_key = f"n{n}_w{w}_{a.dist}"
@@ -524,7 +532,7 @@ def main():
     }
     print(json.dumps(out), file=json_out, flush=True)
     if dist:
-        dist.destroy_process_group()
+        _close(dist)
 
 
 class _WsTracer:
@@ -704,7 +712,7 @@ def run_exchange(a, json_out, N, rank, local):
                        "own chunk in place; no bytes cross xGMI"},
         }
         print(json.dumps(out), file=json_out, flush=True)
-    dist.destroy_process_group()
+    _close(dist)
 
 
 def partition_check(R, out, hist, off, bits, shift, w):
@@ -794,7 +802,7 @@ def run_op(a, lib, json_out, dist, N, rank):
         ok = all(v for v in chk.values() if isinstance(v, bool))
     if rank != 0:
         if dist:
-            dist.destroy_process_group()
+            _close(dist)
         return
     ms_step = elapsed / a.steps * 1e3
     value = N * n / (elapsed / a.steps) / 1e6
@@ -847,7 +855,7 @@ def run_op(a, lib, json_out, dist, N, rank):
     }
     print(json.dumps(out_line), file=json_out, flush=True)
     if dist:
-        dist.destroy_process_group()
+        _close(dist)
 
 
 if __name__ == "__main__":

@@ -340,7 +340,69 @@ def _worker(rank, world, port, n, q, s_payload="negative", mode="sampled", plane
         q.put((rank, repr(e)))
         raise
     finally:
+        from smj.dist import release_row_groups
+        release_row_groups()
         dist.destroy_process_group()
+
+
+def _sub_worker(rank, world, port, n, q):
+    """A DistributedJoin on the sub-group {0, 1} of a world of 3: rank 2
+    takes no part in it (the row communicator is created with
+    use_local_synchronization, only by the members), and two joins on the
+    same group share one cached row communicator."""
+    import sys
+    for p in (ROOT, PKG):
+        sys.path.insert(0, p)
+    import oracle
+    from smj import dist as sd
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}",
+                            rank=rank, world_size=world)
+    try:
+        if rank < 2:
+            sub = dist.new_group(ranks=[0, 1], use_local_synchronization=True)
+            orc = oracle.Oracle(16)
+            total = 2 * n
+            orc.seed(12345)
+            R = orc.create_relation_pk(total)
+            R["payload"] = np.arange(total)
+            orc.seed(54321)
+            S = orc.create_relation_fk(total, total)
+            S["payload"] = np.arange(total)
+            expect = orc.merge_join(np.sort(R, order="key"), np.sort(S, order="key"))
+
+            def rows(t):
+                return torch.from_numpy(
+                    t[rank * n:(rank + 1) * n].view(np.int64).reshape(-1, 2).copy())
+            joins = [sd.DistributedJoin(HostOps(orc), 6, 1, total, group=sub) for _ in range(2)]
+            assert joins[0].row_group is joins[1].row_group and len(sd._ROW_GROUPS) == 1
+            count = torch.zeros(1, dtype=torch.int64)
+            for dj in joins:
+                dj.step(rows(R), rows(S), count)
+                assert int(count.item()) == expect
+            sd.release_row_groups()
+            assert not sd._ROW_GROUPS
+        q.put((rank, "ok"))
+    except BaseException as e:
+        q.put((rank, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_distributed_join_subgroup():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sub_worker, args=(r, 3, port, 4000, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+    res = dict(q.get(timeout=5) for _ in range(3))
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert res == {r: "ok" for r in range(3)}, res
 
 
 def _free_port():

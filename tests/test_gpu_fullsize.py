@@ -15,6 +15,7 @@ the qsort restatement in tests/test_oracle.py); the join's two run on two host
 threads (ctypes drops the GIL).
 """
 import os
+import time
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
@@ -172,7 +173,12 @@ def test_n1024_join_properties(libs, dist_):
     if dist_ == "uniform":
         lib.dev_gen_fk(S, 0, n, n, 54321)
     else:
-        lib.dev_gen_zipf(S, 0, n, 0.75, 54321)
+        # the reference's own create_relation_zipf stream (genzipf.c:97-159,
+        # bit-exact, refgen.hip), the relation configs[4] names
+        t0 = time.time()
+        lib.dev_gen_zipf_ref(S, 0, n, 0.75, 54321)
+        torch.cuda.synchronize()
+        print(f"[n1024] create_relation_zipf stream generated in {time.time() - t0:.1f} s")
     sR, sS = lib.empty(n), lib.empty(n)
     cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
     lib.dev_join(R, S, sR, sS, cnt, 9, 1, n)
@@ -213,7 +219,7 @@ def test_distributed_join_n1024_one_rank():
         n = 1_024_000_000
         R, S = lib.empty(n), lib.empty(n)
         lib.dev_gen_pk(R, 0, n, 12345)
-        lib.dev_gen_zipf(S, 0, n, 0.75, 54321)
+        lib.dev_gen_zipf_ref(S, 0, n, 0.75, 54321)  # create_relation_zipf's stream
         dj = DistributedJoin(DeviceOps(lib), 9, 1, n)
         count = torch.zeros(1, dtype=torch.int64, device="cuda")
         for _ in range(2):
@@ -229,3 +235,30 @@ def test_distributed_join_n1024_one_rank():
     finally:
         dist.destroy_process_group()
     _free(torch)
+
+
+def test_mpsm_n1024_zipf_ref(libs):
+    """BASELINE configs[4] through the C API's multi-GPU join
+    (smj_mgpu_join, the sortmergejoin_mpsm path: one RCCL rank per visible
+    GPU): R = S = 1024M 16-byte tuples, S the reference's create_relation_zipf
+    stream (theta 0.75, seed 54321).  Count = |S|, both outputs sorted and
+    permutations of their inputs (checksums)."""
+    import torch
+    lib = libs[16]
+    n = 1_024_000_000
+    R, S = lib.empty(n), lib.empty(n)
+    lib.dev_gen_pk(R, 0, n, 12345)
+    lib.dev_gen_zipf_ref(S, 0, n, 0.75, 54321)
+    torch.cuda.synchronize()
+    try:
+        c, sR, sS, counts, st = lib.mgpu_join(R, S, 0)
+        assert c == n and st["replans"] == 0
+        for src, out in ((R, sR), (S, sS)):
+            k = out[:, 1]
+            assert bool((k[1:] >= k[:-1]).all())
+            assert _checksum(torch, src) == _checksum(torch, out)
+        del sR, sS
+    finally:
+        lib.lib.smj_mgpu_release()
+        del R, S
+        _free(torch)
