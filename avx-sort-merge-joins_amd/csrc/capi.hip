@@ -759,6 +759,44 @@ static uint32_t grid_n(uint64_t n) {
     return (uint32_t)(b < 4096 ? (b ? b : 1) : 4096);
 }
 
+// inregister_sort_keyval32 (src/avxsort/avxsort_core.h:1213-1274): one
+// lane per column of a 16-item block, {x[j], x[j+4], x[j+8], x[j+12]} through
+// the reference's 4x4 odd-even network of VMINPD / VMAXPD, written as row j
+// (the network's output after its 4x4 transpose).  VMINPD(a, b) = a < b ? a
+// : b and VMAXPD(a, b) = a > b ? a : b as IEEE doubles -- an unordered pair (a
+// NaN) or two zeros give the second operand -- compared on the bit patterns
+// in integer arithmetic (sign-magnitude), so denormals and NaNs behave
+// exactly as on the AVX unit.
+__device__ __forceinline__ bool fp64_lt_bits(uint64_t a, uint64_t b) {
+    const uint64_t ma = a & 0x7fffffffffffffffull, mb = b & 0x7fffffffffffffffull;
+    if (ma > 0x7ff0000000000000ull || mb > 0x7ff0000000000000ull) return false;
+    if ((ma | mb) == 0) return false;
+    const int64_t ka = (int64_t)a < 0 ? -(int64_t)ma : (int64_t)ma;
+    const int64_t kb = (int64_t)b < 0 ? -(int64_t)mb : (int64_t)mb;
+    return ka < kb;
+}
+
+__global__ void __launch_bounds__(256)
+k_inreg4x4(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uint64_t nblocks) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= nblocks * 4) return;
+    const uint64_t b = i >> 2;
+    const uint32_t j = (uint32_t)(i & 3);
+    const uint64_t* x = in + 16 * b;
+    auto mn = [](uint64_t p, uint64_t q) { return fp64_lt_bits(p, q) ? p : q; };
+    auto mx = [](uint64_t p, uint64_t q) { return fp64_lt_bits(q, p) ? p : q; };
+    const uint64_t a = x[j], bb = x[4 + j], c = x[8 + j], d = x[12 + j];
+    const uint64_t a1 = mn(a, bb), b1 = mx(a, bb), c1 = mn(c, d), d1 = mx(c, d);
+    const uint64_t b2 = mn(b1, d1), d2 = mx(b1, d1);
+    const uint64_t a2 = mn(a1, c1), c2 = mx(a1, c1);
+    const uint64_t b3 = mn(b2, c2), c3 = mx(b2, c2);
+    uint64_t* o = out + 16 * b + 4 * j;
+    o[0] = a2;
+    o[1] = b3;
+    o[2] = c3;
+    o[3] = d2;
+}
+
 static void sort_int64_into(const int64_t* inp, int64_t* outp, uint64_t n, bool fp64) {
     if (n == 0) return;
     Ctx& c = ctx();
@@ -823,6 +861,20 @@ static void sort_int32_into(const int32_t* inp, int32_t* outp, uint64_t n) {
 }
 
 extern "C" {
+
+void smj_inregister_sort_keyval32(const int64_t* items, int64_t* output, uint64_t nblocks) {
+    if (nblocks == 0) return;
+    Ctx& c = ctx();
+    const uint64_t ntup = nblocks * 128 / sizeof(Tup);
+    DevBuf in = dev_in(items, ntup, "api_ir_in", true);
+    DevBuf out = dev_in(output, ntup, "api_ir_out", false);
+    const uint64_t lanes = nblocks * 4;
+    hipLaunchKernelGGL(k_inreg4x4, dim3((uint32_t)((lanes + 255) / 256)), dim3(256), 0, c.st,
+                       (const uint64_t*)in.d, (uint64_t*)out.d, nblocks);
+    SMJ_CHECK(hipGetLastError());
+    dev_out(out, ntup);
+    sync();
+}
 
 void avxsort_int64(int64_t** inputptr, int64_t** outputptr, uint64_t nitems) {
     sort_int64_into(*inputptr, *outputptr, nitems, true);

@@ -65,6 +65,7 @@ DEVICE_SYMBOLS = [
     "smj_dev_gen_nonunique", "smj_dev_gen_zipf_ref", "smj_glibc_rand",
     "smj_dev_xsend", "smj_dev_xrecv", "smj_join", "smj_dev_partition_range_planes",
     "smj_dev_join_segmented_planes", "smj_mgpu_join", "smj_mgpu_release",
+    "smj_inregister_sort_keyval32",
 ]
 
 
@@ -216,6 +217,7 @@ class Library:
             "smj_mgpu_join": (_I64, [_P, _U64, _P, _U64, C.c_int, _U32, _I64, _I64, _P, _P,
                                      _P, _P]),
             "smj_mgpu_release": (None, []),
+            "smj_inregister_sort_keyval32": (None, [_P, _P, _U64]),
             "smj_trace_enable": (None, [_P, C.c_int]),
             "smj_trace_reset": (None, [_P]),
             "smj_trace_only": (None, [_P, C.c_char_p]),
@@ -286,6 +288,13 @@ class Library:
         pa, pb = C.c_void_p(a.ctypes.data), C.c_void_p(b.ctypes.data)
         getattr(self.lib, fn)(C.byref(pa), C.byref(pb), len(a))
         return (b if pb.value == b.ctypes.data else a).copy()
+
+    def inregister_sort_keyval32(self, items: np.ndarray) -> np.ndarray:
+        """smj_inregister_sort_keyval32 on len(items) / 16 blocks."""
+        a = np.ascontiguousarray(items, dtype=np.int64)
+        out = np.zeros_like(a)
+        self.lib.smj_inregister_sort_keyval32(_ptr(a), _ptr(out), len(a) // 16)
+        return out
 
     def merge_int64(self, a, b, fn="avx_merge_int64") -> np.ndarray:
         a = np.ascontiguousarray(a, dtype=np.int64)

@@ -5,10 +5,14 @@
  * merge networks merge{4,8,16}_{eqlen,varlen}[_aligned] (avxsort_core.h:76-1100,
  * 1601-1750), the 4x4 in-register sort inregister_sort_keyval32
  * (avxsort_core.h:1213-1290, 1538-1600) and keycmp (avxsort_core.h:1400-1412).
- * On MI355X there are no host register kernels: each one is the library's
- * device merge / sort of the same int64 items in the same FP64 order
- * (avx_merge_int64, avxsort_int64), so the reference's kernel tests check the
- * device path with their own data.  The reference header has no include
+ * On MI355X there are no host register kernels: each one is a library call on
+ * the device.  inregister_sort_keyval32 is the reference's network itself
+ * (smj_inregister_sort_keyval32, byte-identical).  The merges are the
+ * library's device merge of the same int64 items in the same FP64 order
+ * (avx_merge_int64): the same output; unlike the reference's _varlen
+ * kernels they never write into their inputs (the reference flushes its last
+ * register into consumed input slots, avxsort_core.h:461-475; INTEGRATION.md
+ * documents the difference).  The reference header has no include
  * guard; this one has.  Host wrappers only; the declarations live in ../smj.h.
  */
 #ifndef SMJ_COMPAT_AVXSORT_CORE_H
@@ -57,15 +61,12 @@ SMJ_COMPAT_MERGE_VARLEN(merge8_varlen_aligned)
 SMJ_COMPAT_MERGE_VARLEN(merge16_varlen_aligned)
 #undef SMJ_COMPAT_MERGE_VARLEN
 
-/* 16 items -> output in four sorted rows of four (here: all 16 sorted, which
- * is a stronger order than the reference's transposed 4x4 network leaves) */
+/* 16 items -> four rows of four: row j = column j of the 4x4 input through
+ * the reference's odd-even network (avxsort_core.h:1213-1274), byte-identical
+ * (the device kernel behind smj_inregister_sort_keyval32) */
 static inline void inregister_sort_keyval32(int64_t * items, int64_t * output)
 {
-    int64_t a[16], b[16];
-    int64_t * in = a, * o = b;
-    memcpy(a, items, sizeof(a));
-    avxsort_int64(&in, &o, 16);
-    memcpy(output, o, sizeof(a));
+    smj_inregister_sort_keyval32(items, output, 1);
 }
 
 static inline void inregister_sort_keyval32_aligned(int64_t * items, int64_t * output)

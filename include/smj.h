@@ -196,6 +196,16 @@ void scalarsort_int64(int64_t ** inputptr, int64_t ** outputptr,
 void scalarsort_int32(int32_t ** inputptr, int32_t ** outputptr,
                       uint64_t nitems);
 
+/* The reference's in-register kernel inregister_sort_keyval32
+ * (src/avxsort/avxsort_core.h:1213-1274, the compat header
+ * include/compat/avxsort_core.h maps that name here), on nblocks consecutive
+ * blocks of 16 int64 items: output row j of a block (items 4j..4j+3) is the
+ * column {x[j], x[j+4], x[j+8], x[j+12]} after the reference's 4x4 odd-even
+ * network of VMINPD/VMAXPD on the items as IEEE doubles, byte-identical to
+ * the AVX kernel (NaNs and signed zeros included).  Runs on the device. */
+void smj_inregister_sort_keyval32(const int64_t * items, int64_t * output,
+                                  uint64_t nblocks);
+
 /* ------------------------------------------------------------------------ */
 /* Merging (reference src/merge/merge.h:35-97, avx_multiwaymerge.h:33-38,    */
 /* scalar_multiwaymerge.h:31-78). Return value = tuples written.             */

@@ -144,6 +144,13 @@ class Oracle(_Lib):
         self.fn("sort_int64_fp64", None, _P, _I64)(_ptr(b), len(b))
         return b
 
+    def inregister_sort_keyval32(self, items: np.ndarray) -> np.ndarray:
+        """avxsort_core.h:1213-1274 on len(items) / 16 blocks (restated)."""
+        a = np.ascontiguousarray(items, dtype=np.int64)
+        out = np.zeros_like(a)
+        self.fn("inregister_sort_keyval32", None, _P, _P, _I64)(_ptr(a), _ptr(out), len(a) // 16)
+        return out
+
     def merge_int64_fp64(self, a: np.ndarray, b: np.ndarray) -> np.ndarray:
         a = np.ascontiguousarray(a, dtype=np.int64)
         b = np.ascontiguousarray(b, dtype=np.int64)
@@ -260,6 +267,25 @@ class Reference(_Lib):
         self.fn("avx_merge_int64", _U64, _P, _P, _P, _U64, _U64)(
             _ptr(A), _ptr(B), _ptr(out), len(a), len(b))
         return np.array(out)
+
+    def inregister_sort_keyval32(self, items):
+        """avxsort_core.h:1213-1274 on len(items) / 16 blocks (the AVX kernel)."""
+        a = np.ascontiguousarray(items, dtype=np.int64)
+        out = np.zeros_like(a)
+        self.fn("inregister_sort_keyval32", None, _P, _P, _I64)(_ptr(a), _ptr(out), len(a) // 16)
+        return out
+
+    def merge16_varlen(self, a, b):
+        """avxsort_core.h:388-500: (output, A and B as the kernel leaves them --
+        its last register is flushed into consumed input slots, :461-475)."""
+        A = np.zeros(len(a) + 32, np.int64)
+        A[: len(a)] = a
+        B = np.zeros(len(b) + 32, np.int64)
+        B[: len(b)] = b
+        out = np.zeros(len(a) + len(b) + 32, np.int64)
+        self.fn("merge16_varlen", None, _P, _P, _P, C.c_uint32, C.c_uint32)(
+            _ptr(A), _ptr(B), _ptr(out), len(a), len(b))
+        return out[: len(a) + len(b)].copy(), A[: len(a)].copy(), B[: len(b)].copy()
 
     def merge(self, a, b, fn="avx_merge_tuples"):
         A = self._aligned(len(a))

@@ -44,7 +44,10 @@ for w in 8 16; do
         objs="$objs $o"
     done
     $CXX -O2 -fPIC $def $INC -c "$HERE/ref_shim.cpp" -o "$objdir/ref_shim.o" -w
-    $CXX -shared -Wl,-Bsymbolic $objs "$objdir/ref_shim.o" -o "$HERE/_ref/libref$w.so" -lpthread -lm
+    # the AVX register kernels are inline in avxsort_core.h: a shim built -mavx
+    $CXX $FLAGS $def $INC -c "$HERE/ref_shim_avx.cpp" -o "$objdir/ref_shim_avx.o"
+    $CXX -shared -Wl,-Bsymbolic $objs "$objdir/ref_shim.o" "$objdir/ref_shim_avx.o" \
+        -o "$HERE/_ref/libref$w.so" -lpthread -lm
     $CXX -O2 $def $INC -c "$HERE/cpu_baseline.cpp" -o "$objdir/cpu_baseline.o" -w
     $CXX $objs "$objdir/cpu_baseline.o" -o "$HERE/_ref/cpu_baseline$w" -lpthread -lm
     $CXX -O2 $def $INC -c "$HERE/cpu_baseline_ops.cpp" -o "$objdir/cpu_baseline_ops.o" -w

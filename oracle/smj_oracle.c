@@ -294,6 +294,40 @@ static int i64_fp_cmp(const void *a, const void *b) {
     return x < y ? -1 : (x > y);
 }
 void orc_sort_int64_fp64(int64_t *a, int64_t n) { qsort(a, (size_t)n, 8, i64_fp_cmp); }
+
+/* inregister_sort_keyval32 (src/avxsort/avxsort_core.h:1213-1274) on nblocks
+ * blocks of 16 items: the 4x4 odd-even network of _mm256_min_pd/_max_pd over
+ * the four columns {x[j], x[j+4], x[j+8], x[j+12]}, then the 4x4 transpose,
+ * so output row j (items 4j..4j+3) is column j's network result.  VMINPD
+ * (a, b) = a < b ? a : b and VMAXPD(a, b) = a > b ? a : b as IEEE doubles: an
+ * unordered compare (a NaN) or two zeros return the second operand. */
+static int fp64_lt(int64_t a, int64_t b) {
+    const uint64_t ma = (uint64_t)a & 0x7fffffffffffffffull, mb = (uint64_t)b & 0x7fffffffffffffffull;
+    if (ma > 0x7ff0000000000000ull || mb > 0x7ff0000000000000ull) return 0;  /* NaN */
+    if (ma == 0 && mb == 0) return 0;                                        /* +-0 */
+    const int64_t ka = a < 0 ? -(int64_t)ma : (int64_t)ma;
+    const int64_t kb = b < 0 ? -(int64_t)mb : (int64_t)mb;
+    return ka < kb;
+}
+static int64_t vmin(int64_t a, int64_t b) { return fp64_lt(a, b) ? a : b; }
+static int64_t vmax(int64_t a, int64_t b) { return fp64_lt(b, a) ? a : b; }
+void orc_inregister_sort_keyval32(const int64_t *items, int64_t *out, int64_t nblocks) {
+    for (int64_t k = 0; k < nblocks; k++) {
+        const int64_t *x = items + 16 * k;
+        int64_t *o = out + 16 * k;
+        for (int j = 0; j < 4; j++) {
+            const int64_t a = x[j], b = x[4 + j], c = x[8 + j], d = x[12 + j];
+            const int64_t a1 = vmin(a, b), b1 = vmax(a, b), c1 = vmin(c, d), d1 = vmax(c, d);
+            const int64_t b2 = vmin(b1, d1), d2 = vmax(b1, d1);
+            const int64_t a2 = vmin(a1, c1), c2 = vmax(a1, c1);
+            const int64_t b3 = vmin(b2, c2), c3 = vmax(b2, c2);
+            o[4 * j + 0] = a2;
+            o[4 * j + 1] = b3;
+            o[4 * j + 2] = c3;
+            o[4 * j + 3] = d2;
+        }
+    }
+}
 uint64_t orc_merge_int64_fp64(const int64_t *A, const int64_t *B, int64_t *out,
                               uint64_t la, uint64_t lb) {
     uint64_t i = 0, j = 0, k = 0;

@@ -10,6 +10,7 @@ them.  Nothing here runs on the GPU box.
 
     python tests/golden/make_golden.py           # golden_w8/w16.npz
     python tests/golden/make_golden.py --int64   # golden_int64.npz
+    python tests/golden/make_golden.py --avxcore # golden_avxcore.npz
     python tests/golden/make_golden.py --big     # golden_big.npz (digests)
 """
 import hashlib
@@ -249,11 +250,50 @@ def int64_fixtures():
     print(f"wrote {path} ({os.path.getsize(path) / 1e6:.2f} MB, {len(out)} arrays)")
 
 
+def special_words():
+    """Bit patterns the FP64 networks treat specially: NaNs (quiet, signalling,
+    negative), +-0, +-inf, denormals, the extremes of the int64 range."""
+    v = [0, -2 ** 63, 0x7FF0000000000000, -0x0010000000000000, 0x7FF8000000000000,
+         0x7FF0000000000001, -0x0008000000000000, 0x7FFFFFFFFFFFFFFF, 1, -2 ** 63 + 1,
+         0x000FFFFFFFFFFFFF, 0x0010000000000000, 2 ** 62, -(2 ** 62), 42, -42]
+    return np.array(v, dtype=np.int64)
+
+
+def avxcore_fixtures():
+    """The reference's AVX register kernels the compat header
+    include/compat/avxsort_core.h maps (check_merge.c calls them):
+    inregister_sort_keyval32 (avxsort_core.h:1213-1274) on 16-item blocks of
+    random, special and duplicate patterns, and merge16_varlen
+    (:388-500) with the inputs as it leaves them (its register flush into
+    consumed input slots, :461-475)."""
+    ref = oracle.Reference(8)
+    rng = np.random.default_rng(1213)
+    sp = special_words()
+    blocks = [carriers(rng, 16 * 200), non_nan_words(rng, 16 * 200),
+              rng.integers(-(1 << 63), (1 << 63) - 1, 16 * 300, dtype=np.int64),
+              rng.choice(sp, 16 * 300), rng.integers(-3, 4, 16 * 100).astype(np.int64),
+              np.tile(np.arange(16, dtype=np.int64), 10), np.tile(np.arange(16, 0, -1), 10)]
+    inp = np.concatenate(blocks).astype(np.int64)
+    out = {"inreg_in": inp, "inreg_out": ref.inregister_sort_keyval32(inp)}
+    for i, (la, lb) in enumerate(((100, 77), (1000, 1003), (16 * 40 + 3, 16 * 17 + 15),
+                                  (4096, 33), (33, 4096))):
+        a = ref.sort_int64(carriers(rng, la))
+        b = ref.sort_int64(carriers(rng, lb))
+        o, a2, b2 = ref.merge16_varlen(a, b)
+        out[f"varlen{i}_a"], out[f"varlen{i}_b"] = a, b
+        out[f"varlen{i}_out"], out[f"varlen{i}_a_after"], out[f"varlen{i}_b_after"] = o, a2, b2
+    path = os.path.join(HERE, "golden_avxcore.npz")
+    np.savez_compressed(path, **out)
+    print(f"wrote {path} ({os.path.getsize(path) / 1e6:.2f} MB, {len(out)} arrays)")
+
+
 if __name__ == "__main__":
     if len(sys.argv) == 5 and sys.argv[1] == "--join-case":
         join_case(*map(int, sys.argv[2:]))
     elif len(sys.argv) == 2 and sys.argv[1] == "--int64":
         int64_fixtures()
+    elif len(sys.argv) == 2 and sys.argv[1] == "--avxcore":
+        avxcore_fixtures()
     elif len(sys.argv) == 2 and sys.argv[1] == "--big":
         big_fixtures()
     else:

@@ -198,3 +198,28 @@ def test_reference_generators_on_device(gcase):
     lib.dev_gen_zipf_ref(z, 0, 500, 0.75, 777)
     torch.cuda.synchronize()
     assert np.array_equal(lib.to_host(z), exp)
+
+
+def test_golden_inregister_network(libs):
+    """The compat kernel inregister_sort_keyval32 (include/compat/
+    avxsort_core.h -> smj_inregister_sort_keyval32, on the device) byte-
+    identical to the reference's AVX kernel (avxsort_core.h:1213-1274) on
+    random, special (NaN, +-0, +-inf, denormal) and duplicate blocks."""
+    g = np.load(os.path.join(ROOT, "tests", "golden", "golden_avxcore.npz"))
+    for w in (8, 16):
+        got = libs[w].inregister_sort_keyval32(g["inreg_in"])
+        assert np.array_equal(got, g["inreg_out"])
+
+
+@pytest.mark.parametrize("case", range(5))
+def test_golden_varlen_merge(libs, case):
+    """merge16_varlen (avxsort_core.h:388-500) as the compat header maps it
+    (avx_merge_int64): the reference's output exactly.  The reference also
+    flushes its last register into consumed slots of one input (:461-475,
+    seen in the fixture); the library leaves its inputs untouched
+    (INTEGRATION.md)."""
+    g = np.load(os.path.join(ROOT, "tests", "golden", "golden_avxcore.npz"))
+    a, b = g[f"varlen{case}_a"].copy(), g[f"varlen{case}_b"].copy()
+    got = libs[8].merge_int64(a, b)
+    assert np.array_equal(got, g[f"varlen{case}_out"])
+    assert np.array_equal(a, g[f"varlen{case}_a"]) and np.array_equal(b, g[f"varlen{case}_b"])

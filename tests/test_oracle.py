@@ -269,3 +269,13 @@ def test_big_multiway(w, k, maxlen, oracles):
     out = orc.multiway_merge(runs)
     assert len(out) == int(g[f"w{w}_mw{k}_n"][0])
     check_big(w, out, g, f"w{w}_mw{k}")
+
+
+def test_inregister_network_restatement_vs_golden():
+    """orc_inregister_sort_keyval32 against the reference's AVX kernel
+    (avxsort_core.h:1213-1274, tests/golden/golden_avxcore.npz): NaNs, signed
+    zeros, infinities, denormals and duplicates included."""
+    import oracle
+    g = np.load(os.path.join(ROOT, "tests", "golden", "golden_avxcore.npz"))
+    got = oracle.Oracle(8).inregister_sort_keyval32(g["inreg_in"])
+    assert np.array_equal(got, g["inreg_out"])
