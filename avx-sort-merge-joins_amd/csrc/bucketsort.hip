@@ -83,6 +83,10 @@ constexpr int TP_THREADS = SMJ_TP_THREADS;
 #ifndef SMJ_GS_ARGS_MEM
 #define SMJ_GS_ARGS_MEM 1
 #endif
+// the skew path's statistics on stderr (lab builds: make EXTRA=-DSMJ_LAB_DIAG=1)
+#ifndef SMJ_LAB_DIAG
+#define SMJ_LAB_DIAG 0
+#endif
 #ifndef SMJ_GS_ABL
 #define SMJ_GS_ABL 0  // ablations for measurements only (1: no in-group sort; 2: no
                       // equal-digit run fixing; 3: no write-out)
@@ -1781,7 +1785,7 @@ static void skew_path(Workspace* ws, const GroupArgs& G, OvfEntry* ovf, uint32_t
         }
     }
     const size_t nl = large.size();
-    if (getenv("SMJ_SKEW_STATS")) {  // measurements only
+    if (SMJ_LAB_DIAG) {  // lab builds only (make EXTRA=-DSMJ_LAB_DIAG=1)
         uint64_t ts = 0, tl = 0;
         for (uint32_t i : small) ts += he[i].nr[0] + (nrel > 1 ? he[i].nr[1] : 0);
         for (uint32_t i : large) tl += he[i].nr[0] + (nrel > 1 ? he[i].nr[1] : 0);
@@ -1843,7 +1847,7 @@ static void skew_path(Workspace* ws, const GroupArgs& G, OvfEntry* ovf, uint32_t
     std::vector<uint32_t> rest;
     for (uint32_t i = 0; i < no; i++)
         if (flags[i] != 0 || G.plan.s3 != 0) rest.push_back(i);
-    if (getenv("SMJ_DEBUG_OVF"))
+    if (SMJ_LAB_DIAG)
         fprintf(stderr, "[smj] skew: %u queued groups (%zu small, %zu large, %zu items), "
                 "%zu left to the merge sort\n", no, small.size(), nl, items.size(), rest.size());
     if (rest.empty()) return;

@@ -167,15 +167,8 @@ static void choose_levels(uint64_t n, uint32_t want_d1, uint32_t* D1,
 }
 
 // level-1 partition of sorts and joins: sampled regions (no histogram pass)
-// unless SMJ_SAMPLED=0
-static bool use_sampled() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("SMJ_SAMPLED");
-        v = e ? atoi(e) : 1;
-    }
-    return v != 0;
-}
+// unless the workspace's layout policy turns them off (smj_workspace_set_layouts)
+static bool use_sampled(const Workspace* ws) { return !(ws->layouts_off & SMJ_LAYOUT_NO_SAMPLED); }
 
 // exact key range [min, max] of the relations (one read pass); min > max
 // when they are empty.  16-byte non-temporal loads over one contiguous chunk
@@ -299,26 +292,12 @@ bool key_range(Workspace* ws, const Tup* const* rels, const uint64_t* ns, int nr
 }  // namespace smj
 
 // 16-byte sorts and joins carry packed words through the intermediate passes
-// when the plan allows it (LayPacked); SMJ_PACK=0 keeps tuples
-static bool use_packing() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("SMJ_PACK");
-        v = e ? atoi(e) : 1;
-    }
-    return v != 0;
-}
+// when the plan allows it (LayPacked) ...
+static bool use_packing(const Workspace* ws) { return !(ws->layouts_off & SMJ_LAYOUT_NO_PACKED); }
 
 // ... and 48-bit words in two planes first (LayP48) when every payload fits
-// 48 - s1 bits; SMJ_P48=0 starts from 64-bit words
-static bool use_p48() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("SMJ_P48");
-        v = e ? atoi(e) : 1;
-    }
-    return v != 0;
-}
+// 48 - s1 bits
+static bool use_p48(const Workspace* ws) { return !(ws->layouts_off & SMJ_LAYOUT_NO_P48); }
 
 // Sort of one relation (nrel 1) or sort + merge-join count of two (nrel 2):
 // range plan -> sampled level-1 partition -> tile pass -> group pass.  The
@@ -345,22 +324,23 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
     choose_levels(nmax, fanout_bits, &D1, &D2, &D2cap);
     RangePlan* plan = (RangePlan*)ws->scratch("plan", sizeof(RangePlan));
     const uint32_t nb = 1u << D1;
-    const bool sampled = use_sampled() && D1 <= 10;  // LDS carries up to 1024
+    const bool sampled = use_sampled(ws) && D1 <= 10;  // LDS carries up to 1024
     bool plan_on_host = hint_min <= hint_max;
     // a guessed plan is verified by the sampled scatter only
     bool guessed = false;
-    if (!plan_on_host && size_guess > 0 && sampled && !getenv("SMJ_SAMPLED_PLAN")) {
+    const bool sample_plan = (ws->layouts_off & SMJ_LAYOUT_SAMPLE_PLAN) != 0;
+    if (!plan_on_host && size_guess > 0 && sampled && !sample_plan) {
         hint_min = 1;
         hint_max = (int64_t)(size_guess < (uint64_t)INT64_MAX ? size_guess : INT64_MAX);
         plan_on_host = guessed = true;
     }
-    if (!plan_on_host && !getenv("SMJ_SAMPLED_PLAN"))
+    if (!plan_on_host && !sample_plan)
         plan_on_host = key_range(ws, rels, ns, nrel, &hint_min, &hint_max, st);
     RangePlan hplan = make_plan(hint_min, hint_max, D1, D2, D2cap, kGroupD3Max);
     if (!plan_on_host)
         plan_from_sample(ws, rels, ns, nrel, D1, D2, D2cap, hint_min, hint_max, plan, st);
 #ifdef KEY_8B
-    bool can_pack = sampled && plan_on_host && use_packing() && LayPacked::usable(hplan);
+    bool can_pack = sampled && plan_on_host && use_packing(ws) && LayPacked::usable(hplan);
 #else
     const bool can_pack = false;
 #endif
@@ -403,9 +383,9 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
     const bool p48_fits = hplan.s1 >= 1 && hplan.s1 <= 32 && hplan.span < (1ull << (48 - hplan.s1));
     auto first_mode = [&]() {
 #ifdef KEY_8B
-        if (can_pack && use_p48() && p48_fits && nb <= 512) return -1;
+        if (can_pack && use_p48(ws) && p48_fits && nb <= 512) return -1;
 #else
-        if (sampled && plan_on_host && use_packing() && use_p48() &&
+        if (sampled && plan_on_host && use_packing(ws) && use_p48(ws) &&
             LayP48::usable(hplan) && p48_fits && nb <= 512)
             return -1;
 #endif
@@ -499,7 +479,7 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
                 plan_from_sample(ws, rels, ns, nrel, D1, D2, D2cap, hint_min, hint_max, plan,
                                  st);
 #ifdef KEY_8B
-            can_pack = sampled && plan_on_host && use_packing() && LayPacked::usable(hplan);
+            can_pack = sampled && plan_on_host && use_packing(ws) && LayPacked::usable(hplan);
 #endif
             mode = first_mode();
             continue;
@@ -1669,6 +1649,10 @@ smj_workspace* smj_workspace_create(void) {
     return (smj_workspace*)new Workspace();
 }
 void smj_workspace_destroy(smj_workspace* ws) { delete (Workspace*)ws; }
+
+void smj_workspace_set_layouts(smj_workspace* ws, uint32_t off) {
+    ((Workspace*)(ws ? ws : smj_context_workspace()))->layouts_off = off;
+}
 
 void smj_dev_partition(smj_workspace* ws, const tuple_t* in, uint64_t n,
                        tuple_t* out, uint32_t nbits, uint32_t shiftbits,

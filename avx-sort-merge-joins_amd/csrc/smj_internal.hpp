@@ -65,6 +65,9 @@ struct PlanDigit1 {
 #define SMJ_SPIN_WAIT 1  // Workspace::wait_stream polls an event (0: a lab build's stream sync)
 #endif
 struct Workspace {
+    // layouts this workspace's sorts and joins may not use
+    // (smj_workspace_set_layouts, SMJ_LAYOUT_* in smj.h)
+    uint32_t layouts_off = 0;
     std::map<std::string, std::pair<void*, size_t>> bufs;
     std::map<std::string, std::pair<void*, size_t>> pinned;
     // the k-way merge's run table as last uploaded, and where (a repeated

@@ -65,7 +65,7 @@ DEVICE_SYMBOLS = [
     "smj_dev_gen_nonunique", "smj_dev_gen_zipf_ref", "smj_glibc_rand",
     "smj_dev_xsend", "smj_dev_xrecv", "smj_join", "smj_dev_partition_range_planes",
     "smj_dev_join_segmented_planes", "smj_mgpu_join", "smj_mgpu_release",
-    "smj_inregister_sort_keyval32",
+    "smj_inregister_sort_keyval32", "smj_workspace_set_layouts",
 ]
 
 
@@ -106,6 +106,8 @@ class MgpuStats(C.Structure):
                 ("key_min", C.c_int64), ("key_max", C.c_int64), ("ms", C.c_double)]
 
 
+# smj_workspace_set_layouts bits (include/smj.h)
+LAYOUT_NO_P48, LAYOUT_NO_PACKED, LAYOUT_NO_SAMPLED, LAYOUT_SAMPLE_PLAN = 1, 2, 4, 8
 # smj_mgpu_join flags (include/smj.h)
 MG_COPY, MG_NOPLANES, MG_ONECALL, MG_SAMPLED, MG_EXACT = 1, 2, 4, 8, 16
 MG_LAYOUTS = ("tuples", "words", "planes")
@@ -218,6 +220,7 @@ class Library:
                                      _P, _P]),
             "smj_mgpu_release": (None, []),
             "smj_inregister_sort_keyval32": (None, [_P, _P, _U64]),
+            "smj_workspace_set_layouts": (None, [_P, _U32]),
             "smj_trace_enable": (None, [_P, C.c_int]),
             "smj_trace_reset": (None, [_P]),
             "smj_trace_only": (None, [_P, C.c_char_p]),
@@ -436,6 +439,11 @@ class Library:
         if self._ws is None:
             self._ws = self.lib.smj_workspace_create()
         return self._ws
+
+    def set_layouts(self, off: int = 0):
+        """smj_workspace_set_layouts on this Library's workspace (LAYOUT_*
+        bits: layouts its device sorts and joins may not use; 0 = all)."""
+        self.lib.smj_workspace_set_layouts(self.ws, off)
 
     @staticmethod
     def stream_ptr():

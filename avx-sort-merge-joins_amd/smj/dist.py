@@ -29,7 +29,6 @@ stand-ins for the device ops that live in tests/).
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.distributed as dist
@@ -50,8 +49,9 @@ INT64_MAX = (1 << 63) - 1
 # exactly half the message every time, from 1100 MiB up (1024 MiB is exact),
 # so the limit is a byte count inside RCCL, not an element count of ours
 # (profiles/r02_a2a_bisect.txt).  Larger exchanges go as chunked
-# point-to-point sends in one group.
-CHUNK_BYTES = int(os.environ.get("SMJ_A2A_CHUNK_MB", "512")) << 20
+# point-to-point sends in one group.  (A module attribute: tests lower it to
+# exercise the chunked path.)
+CHUNK_BYTES = 512 << 20
 # The exchange layouts, narrowest last: tuples, 64-bit packed words (16-byte
 # tuples only), 48-bit words in two planes (LayP48, both widths; the sampled
 # partition's LDS carries hold at most 2^9 partitions of them).  Both
@@ -267,16 +267,16 @@ def xrecv_torch(msg, chunk, world, rank, mine, K, tstart, tcnt, cap, summary):
 
 class DeviceOps:
     """The device implementation of the ops interface (libsmj_hip*.so).
-    16-byte tuples travel as packed 64-bit words (smj_dev_partition_range_packed)
-    unless SMJ_PACK=0."""
+    pack: 16-byte tuples may travel as packed 64-bit words
+    (smj_dev_partition_range_packed); planes: both widths as 48-bit words in
+    two planes (a sampled form only); sampled: the exchange partition's form,
+    None = sampled on one rank, exact across ranks (see can_sample)."""
 
-    def __init__(self, lib):
+    def __init__(self, lib, pack=True, planes=True, sampled=None):
         self.lib = lib
-        self.can_pack = lib.width == 16 and os.environ.get("SMJ_PACK", "1") != "0"
-        # 48-bit words in two planes, as the 1-GPU join (SMJ_P48=0: off); a
-        # sampled form only, so SMJ_XSAMPLED=0 turns them off too
-        self.can_planes = (os.environ.get("SMJ_P48", "1") != "0"
-                           and os.environ.get("SMJ_XSAMPLED") != "0")
+        self.can_pack = lib.width == 16 and pack
+        self.can_planes = planes and sampled is not False
+        self._sampled = sampled
 
     def empty(self, n):
         return self.lib.empty(n)
@@ -302,10 +302,9 @@ class DeviceOps:
     # the rows.  On one rank nothing travels and it is the faster form (5.98
     # -> 5.17 ms at N=1, round 2); across ranks the slack is ~14-19 % more
     # xGMI bytes against one HBM read saved, so there the exact partition is
-    # the default.  SMJ_XSAMPLED=1/0 forces either.
+    # the default.  DeviceOps(sampled=True/False) forces either.
     def can_sample(self, world=1):
-        v = os.environ.get("SMJ_XSAMPLED")
-        return world == 1 if v is None else v != "0"
+        return world == 1 if self._sampled is None else bool(self._sampled)
 
     def shards(self):
         return self.lib.sampled_shards()
@@ -373,10 +372,12 @@ class DistributedJoin:
     512, what the 1-GPU join uses); `n_hint`: elements per rank and relation,
     identical on every rank (lets the 48-bit planes take 2^9 partitions
     across ranks, partition_bits); `row_group`: the communicator the rows
-    travel on (default: one per `group`, cached, see _row_group)."""
+    travel on (default: one per `group`, cached, see _row_group); `staged`:
+    the local join in two calls overlapping S's rows (False: one call);
+    `pbits`: force the exchange partition width."""
 
     def __init__(self, ops, bucket_bits: int, key_min: int, key_max: int,
-                 group=None, n_hint=None, row_group=None):
+                 group=None, n_hint=None, row_group=None, staged=True, pbits=None):
         self.ops = ops
         self.group = group
         self.world = dist.get_world_size(group)
@@ -386,8 +387,8 @@ class DistributedJoin:
         # n_hint: elements per rank and relation (the same on every rank)
         self.pbits = partition_bits(bucket_bits, self.world, offers_planes, n_hint,
                                     (key_min, key_max))
-        if os.environ.get("SMJ_XBITS"):  # rehearse the G-GPU partition width on fewer
-            self.pbits = int(os.environ["SMJ_XBITS"])
+        if pbits is not None:  # rehearse the G-GPU partition width on fewer ranks
+            self.pbits = pbits
         self.fanout = 1 << self.pbits
         if self.fanout < self.world:
             raise ValueError(f"fanout 2^{self.pbits} < world size {self.world}")
@@ -408,8 +409,8 @@ class DistributedJoin:
         # partition takes
         self.shards = ops.shards() if hasattr(ops, "shards") else 1
         self.buf = {}
-        # the local join in two calls overlapping S's rows (SMJ_XSTAGED=0: one)
-        self.staged = os.environ.get("SMJ_XSTAGED", "1") != "0"
+        # the local join in two calls overlapping S's rows (staged=False: one)
+        self.staged = staged
         # the rows travel on a communicator of their own: its stream is not
         # ordered behind the table exchange of S (queued behind S's partition)
         self.row_group = row_group

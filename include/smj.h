@@ -462,6 +462,17 @@ typedef struct smj_workspace smj_workspace;
 smj_workspace * smj_workspace_create(void);
 void smj_workspace_destroy(smj_workspace * ws);
 
+/* Layouts the sorts and joins on `ws` may not use (NULL: the calling thread's
+ * workspace behind the reference-named entry points).  Default 0: every
+ * layout allowed, each taken where it applies; the results
+ * are the same whichever layout runs.  For A/B measurements and tests. */
+#define SMJ_LAYOUT_NO_P48      1u  /* no 48-bit words in two planes */
+#define SMJ_LAYOUT_NO_PACKED   2u  /* no 64-bit packed words (16-byte tuples) */
+#define SMJ_LAYOUT_NO_SAMPLED  4u  /* exact histogram + scatter level-1 partition */
+#define SMJ_LAYOUT_SAMPLE_PLAN 8u  /* without a key-range hint: plan from a device
+                                      sample instead of from the relation size */
+void smj_workspace_set_layouts(smj_workspace * ws, uint32_t off);
+
 /* Stable radix partition, the device form of partition_relation*.
  * padded != 0 -> partition_relation_optimized layout.
  * hist_out / off_out (device, int64[1<<nbits]) receive per-partition counts

@@ -245,12 +245,15 @@ class HostOps:
 
 
 def _worker(rank, world, port, n, q, s_payload="negative", mode="sampled", planes=True,
-            wide=False):
+            wide=False, chunk_mb=None, staged=True):
     import sys
     for p in (ROOT, PKG):
         sys.path.insert(0, p)
     import oracle
+    import smj.dist as sd
     from smj.dist import DistributedJoin, Planes, owners, range_digit
+    if chunk_mb is not None:  # every row message over the limit: chunked
+        sd.CHUNK_BYTES = chunk_mb << 20
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}",
                             rank=rank, world_size=world)
@@ -281,10 +284,10 @@ def _worker(rank, world, port, n, q, s_payload="negative", mode="sampled", plane
         ops = HostOps(orc, sampled=mode != "exact", overflow=mode == "overflow" and rank == 1,
                       not_applicable=mode == "mixed" and rank == 0, planes=planes)
         if wide:  # 2^9 buckets per rank: planes take 2^9 partitions across ranks
-            dj = DistributedJoin(ops, 9, 1, total, n_hint=n)
+            dj = DistributedJoin(ops, 9, 1, total, n_hint=n, staged=staged)
             assert dj.pbits == (9 if ops.can_planes else 9 + (world > 1))
         else:
-            dj = DistributedJoin(ops, 6, 1, total)
+            dj = DistributedJoin(ops, 6, 1, total, staged=staged)
         # the layout both relations reach the local join in: planes when the
         # payloads fit 48-bit words on every rank (a rank where the planes do
         # not apply, or a sampled overflow, sends every rank to words)
@@ -302,9 +305,9 @@ def _worker(rank, world, port, n, q, s_payload="negative", mode="sampled", plane
             assert dj.last_layout == want, (dj.last_layout, want)
             assert dj.last_packed == (want != "tuples")
         # the local join: two calls per step (R's tile stage while S's rows
-        # fly, then the rest) across ranks unless SMJ_XSTAGED=0, one call on
+        # fly, then the rest) across ranks unless staged=False, one call on
         # one rank
-        if world > 1 and os.environ.get("SMJ_XSTAGED", "1") != "0":
+        if world > 1 and staged:
             assert getattr(ops, "stage_calls", 0) == 2 and getattr(ops, "whole_calls", 0) == 0
         else:
             assert getattr(ops, "whole_calls", 0) == 2 and getattr(ops, "stage_calls", 0) == 0
@@ -436,10 +439,9 @@ def test_distributed_join_gloo(world, chunk_mb, s_payload, mode, oracles, monkey
     overflow); "negative": S cannot be packed, every rank falls back to tuples
     for both; "r_negative": R cannot be packed but S can (S goes again, as
     tuples); "wide48": S's payloads need 64-bit words (both go as words)."""
-    if chunk_mb is not None:
-        monkeypatch.setenv("SMJ_A2A_CHUNK_MB", str(chunk_mb))
+    staged = True
     if mode.endswith("-onecall"):  # the local join in one call (no staging)
-        monkeypatch.setenv("SMJ_XSTAGED", "0")
+        staged = False
         mode = mode[:-len("-onecall")]
     planes = not mode.endswith("-noplanes")  # ops without the 48-bit planes
     mode = mode.replace("-noplanes", "")
@@ -449,7 +451,7 @@ def test_distributed_join_gloo(world, chunk_mb, s_payload, mode, oracles, monkey
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, 5000, q, s_payload, mode,
-                                               planes, wide))
+                                               planes, wide, chunk_mb, staged))
              for r in range(world)]
     for p in procs:
         p.start()

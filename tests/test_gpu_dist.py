@@ -237,7 +237,6 @@ def test_distributed_join_one_rank_rccl(libs, width, xsampled, monkeypatch):
     import torch
     import torch.distributed as dist
     from smj.dist import DeviceOps, DistributedJoin
-    monkeypatch.setenv("SMJ_XSAMPLED", xsampled)
     lib = libs[width]
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ["MASTER_PORT"] = str(_free_port())
@@ -248,7 +247,7 @@ def test_distributed_join_one_rank_rccl(libs, width, xsampled, monkeypatch):
         R, S = lib.empty(n), lib.empty(n)
         lib.dev_gen_pk(R, 0, n, 12345)
         lib.dev_gen_fk(S, 0, n, n, 54321)
-        dj = DistributedJoin(DeviceOps(lib), 9, 1, n)
+        dj = DistributedJoin(DeviceOps(lib, sampled=xsampled == "1"), 9, 1, n)
         count = torch.zeros(1, dtype=torch.int64, device="cuda")
         for _ in range(2):
             sR, sS = dj.step(R, S, count)

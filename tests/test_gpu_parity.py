@@ -469,23 +469,18 @@ def test_device_join_packed_words(libs, oracles, width, payload):
     in the bucket + payload) through the intermediate passes: 48-bit words in
     two planes first (LayP48), 64-bit words when a payload needs more than
     48 - s1 bits ("wide48": 2^44 here, s1 = 11), tuples when it needs more
-    than 64 - s1 or is negative.  "p48off": SMJ_P48=0 (64-bit words from the
+    than 64 - s1 or is negative.  "p48off": the workspace's layouts without
+    the 48-bit planes (smj_workspace_set_layouts: 64-bit words from the
     start).  The result is the same on every path."""
     if payload == "p48off":
         if width != 16:
             pytest.skip("packed words are the 16-byte layout")
-        # the switch is read once per process: a child process runs the case
-        import subprocess
-        import sys
-        from conftest import PKG, ROOT
-        here = os.path.dirname(os.path.abspath(__file__))
-        env = dict(os.environ, SMJ_P48="0",
-                   PYTHONPATH=os.pathsep.join([here, ROOT, PKG, os.environ.get("PYTHONPATH", "")]))
-        code = ("import test_gpu_parity as t, oracle, smj; "
-                "t._packed_join_case({16: smj.Library(16)}, {16: oracle.Oracle(16)}, 16, 'rowid')")
-        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
-                           timeout=240, cwd=here, env=env)
-        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+        import smj
+        libs[16].set_layouts(smj.LAYOUT_NO_P48)
+        try:
+            _packed_join_case(libs, oracles, width, "rowid")
+        finally:
+            libs[16].set_layouts(0)
         return
     _packed_join_case(libs, oracles, width, payload)
 

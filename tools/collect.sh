@@ -1,0 +1,30 @@
+#!/usr/bin/env bash
+# Copy a closing run's artifacts (tools/closing_run.sh -> gpurun_out/<round>_fin)
+# into profiles/ under the round's prefix: per config the unprofiled line, the
+# line printed under rocprofv3 and that run's kernel stats; the roofline
+# checks, the PMC traffic table, the GPU suite log and the smoke log.
+# usage: tools/collect.sh ROUND [INDIR]     (ROUND e.g. r05)
+set -e
+cd "$(dirname "$0")/.."
+R=${1:?round prefix, e.g. r05}
+I=${2:-gpurun_out/${R}_fin}
+P=profiles
+stats() { find "$1" -name '*kernel_stats.csv' | head -1; }
+for d in "$I" "$I/nopmc"; do
+  [ -d "$d" ] || continue
+  for f in "$d"/*_noprof.json; do
+    [ -f "$f" ] || continue
+    n=$(basename "$f" _noprof.json)
+    t=$n
+    [ "$d" = "$I/nopmc" ] && [ -f "$I/${n}_noprof.json" ] && t=${n}b  # a second line of a config
+    cp "$f" "$P/${R}_${t}_noprof.json"
+    [ -f "$d/$n.json" ] && cp "$d/$n.json" "$P/${R}_$t.json"
+    s=$(stats "$d/trace_$n"); [ -n "$s" ] && cp "$s" "$P/${R}_${t}_kernel_stats.csv"
+  done
+done
+[ -f "$I/roofcheck.json" ] && cp "$I/roofcheck.json" "$P/${R}_roofcheck.json"
+[ -f "$I/nopmc/roofcheck.json" ] && cp "$I/nopmc/roofcheck.json" "$P/${R}_roofcheck_nopmc.json"
+[ -f "$I/pmc_traffic.json" ] && cp "$I/pmc_traffic.json" "$P/pmc_traffic.json"
+[ -f "$I/pytest_gpu.txt" ] && cp "$I/pytest_gpu.txt" "$P/${R}_pytest_gpu.txt"
+[ -f "$I/smoke.txt" ] && cp "$I/smoke.txt" "$P/${R}_smoke.txt"
+ls -la "$P" | grep -c "${R}_"

@@ -1,11 +1,11 @@
 #!/usr/bin/env bash
-# Round-3 roofline artifacts: per config, in ONE command on one box,
+# Roofline artifacts: per config, in ONE command on one box,
 #   NAME_noprof.json   the bench line without the profiler (CPU baseline on)
 #   NAME.json          the line printed by rocprofv3 --kernel-trace --stats
 #   trace_NAME/        that run's kernel stats / trace CSV
 #   fetch_/write_NAME  FETCH_SIZE and WRITE_SIZE passes -> pmc_traffic.json
 # then tools/roofcheck.py compares each line's frac with the rocprof average.
-# usage: tools/r03_lines.sh OUTDIR NAME:args [NAME:args ...]
+# usage: tools/lines.sh OUTDIR NAME:args [NAME:args ...]
 # The first failure ends the script (no GPU step after a failed one).
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"

@@ -1,10 +1,10 @@
 #!/usr/bin/env bash
 # SQ counters of the join's three passes (issue, wait and LDS behaviour), one
 # rocprofv3 --pmc pass per counter set (at most 8 SQ counters a pass), then a
-# per-launch table.  usage: tools/r03_sqprobe.sh [bench args]
+# per-launch table.  usage: tools/sqprobe.sh [bench args]
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
-O=${O:-gpurun_out/r03_sq}; mkdir -p $O
+O=${O:-gpurun_out/sq}; mkdir -p $O
 ARGS=${*:---width 8}
 P1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_VALU"
 P2="SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"
