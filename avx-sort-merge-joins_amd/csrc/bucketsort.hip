@@ -2098,6 +2098,9 @@ static void launch_groupsort(Workspace* ws, int tpl, uint32_t nwg, hipStream_t s
                              const GroupArgs& G0) {
     const size_t lds = sizeof(GroupLDS<typename Lay::W>);
 #if SMJ_GS_ARGS_MEM
+    // one argument slot per workspace: a workspace serves one stream at a
+    // time (smj.h: one per stream/thread), so the group pass of the previous
+    // call on it has read its arguments before k_put_args rewrites them
     GroupArgs* G = (GroupArgs*)ws->scratch("gs_args", sizeof(GroupArgs));
     hipLaunchKernelGGL(k_put_args, dim3(1), dim3(1), 0, st, G0, G);
 #else

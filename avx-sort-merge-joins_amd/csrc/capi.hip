@@ -143,8 +143,11 @@ static uint32_t ceil_log2(uint64_t x) {
 // bucket) so that the expected group is kGroupTarget tuples (3/4 of what the
 // group pass holds in LDS); the plan may widen D2 up to D2cap to make the last
 // digit the exact key
+// `tile`: the elements of a tile-pass tile of the layout the buckets will
+// hold (kTileTuples for 8-byte elements: words, 48-bit words, 8-byte tuples;
+// half of it for 16-byte tuples in their own layout)
 static void choose_levels(uint64_t n, uint32_t want_d1, uint32_t* D1,
-                          uint32_t* D2, uint32_t* D2cap) {
+                          uint32_t* D2, uint32_t* D2cap, uint32_t tile = kTileTuples) {
     const uint64_t target = kGroupTarget;
     uint32_t B = n > target ? ceil_log2((n + target - 1) / target) : 0;
     // level 1: 256 partitions by default, more when a bucket would exceed
@@ -154,7 +157,7 @@ static void choose_levels(uint64_t n, uint32_t want_d1, uint32_t* D1,
     // partitions 3.57 / 3.09 ms (16 / 8 B) against 3.63 / 3.16 ms with 512 --
     // longer scatter streams and tile-pass runs, a slightly slower group pass
     uint32_t d1 = want_d1 ? want_d1 : 8;
-    const uint64_t bucket_cap = 192ull * kTileTuples;
+    const uint64_t bucket_cap = 192ull * tile;
     while (d1 < kNarrowDigitBits && (n >> d1) > bucket_cap) d1++;
     if (d1 > B) d1 = B;
     if (d1 > kNarrowDigitBits) d1 = kNarrowDigitBits;
@@ -323,7 +326,7 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
     uint32_t D1, D2, D2cap;
     choose_levels(nmax, fanout_bits, &D1, &D2, &D2cap);
     RangePlan* plan = (RangePlan*)ws->scratch("plan", sizeof(RangePlan));
-    const uint32_t nb = 1u << D1;
+    uint32_t nb = 1u << D1;
     const bool sampled = use_sampled(ws) && D1 <= 10;  // LDS carries up to 1024
     bool plan_on_host = hint_min <= hint_max;
     // a guessed plan is verified by the sampled scatter only
@@ -349,20 +352,43 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
     int64_t* bh[2] = {nullptr, nullptr};
     uint64_t* sgs[2] = {nullptr, nullptr};
     int64_t* sgc[2] = {nullptr, nullptr};
-    for (int r = 0; r < nrel; r++) {
-        const uint64_t cap = sampled ? sampled_capacity(ns[r], D1) : (ns[r] ? ns[r] : 1);
-        part[r] = (Tup*)ws->scratch(nm[r][0], cap * sizeof(Tup));
-        bst[r] = (uint64_t*)ws->scratch(nm[r][1], nb * 8);
-        bh[r] = (int64_t*)ws->scratch(nm[r][2], nb * 8);
-        sgs[r] = (uint64_t*)ws->scratch(nm[r][3], (size_t)nb * kShards * 8);
-        sgc[r] = (int64_t*)ws->scratch(nm[r][4], (size_t)nb * kShards * 8);
-    }
+    unsigned int* sample = nullptr;
+    auto alloc = [&]() {
+        for (int r = 0; r < nrel; r++) {
+            const uint64_t cap = sampled ? sampled_capacity(ns[r], D1) : (ns[r] ? ns[r] : 1);
+            part[r] = (Tup*)ws->scratch(nm[r][0], cap * sizeof(Tup));
+            bst[r] = (uint64_t*)ws->scratch(nm[r][1], nb * 8);
+            bh[r] = (int64_t*)ws->scratch(nm[r][2], nb * 8);
+            sgs[r] = (uint64_t*)ws->scratch(nm[r][3], (size_t)nb * kShards * 8);
+            sgc[r] = (int64_t*)ws->scratch(nm[r][4], (size_t)nb * kShards * 8);
+        }
+        // the sampled partition's counters: zeroed by k_join_begin on every
+        // attempt (never assumed zero from an earlier call)
+        sample = (unsigned int*)ws->scratch("sp_sample", (size_t)nrel * nb * 4);
+    };
+    alloc();
     // [0] region overflow, [1] bad tuple (kBadPayload | kBadRange), [2] skew
     // queue length
     unsigned int* status = (unsigned int*)ws->scratch("join_status", 16);
-    // the sampled partition's counters: zeroed by k_join_begin on every
-    // attempt (never assumed zero from an earlier call)
-    unsigned int* sample = (unsigned int*)ws->scratch("sp_sample", (size_t)nrel * nb * 4);
+    // 16-byte tuples in their own layout hold tiles of kTileTuples / 2: when
+    // an attempt falls back to them, the level widths are chosen again for
+    // that tile (a bucket within the group pass's 256 tiles)
+    bool tuple_levels = sizeof(Tup) != 16;
+    auto tuple_plan = [&]() {
+        if (tuple_levels) return;
+        tuple_levels = true;
+        uint32_t d1, d2, d2c;
+        choose_levels(nmax, fanout_bits, &d1, &d2, &d2c, kTileTuples / 2);
+        if (d1 == D1 || (sampled && d1 > 10)) return;  // the sampled scatter's carries
+        D1 = d1;
+        D2 = d2;
+        D2cap = d2c;
+        nb = 1u << D1;
+        hplan = make_plan(hint_min, hint_max, D1, D2, D2cap, kGroupD3Max);
+        if (!plan_on_host)
+            plan_from_sample(ws, rels, ns, nrel, D1, D2, D2cap, hint_min, hint_max, plan, st);
+        alloc();
+    };
     unsigned long long* cnt = count_dev
         ? count_dev : (unsigned long long*)ws->scratch("sort_cnt", 8);
     // attempts: sampled + 48-bit words (-1), sampled + packed words (0),
@@ -393,6 +419,7 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
     };
     int mode = first_mode();
     while (mode <= 2) {
+        if (mode >= 1) tuple_plan();
         const bool p48 = mode == -1;
         const bool packed = mode <= 0;
         // the status word the tile and group passes exit on (sampled modes)
@@ -409,7 +436,9 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
         if (mode < 2) {
             void* outs_v[2] = {part[0], part[nrel > 1 ? 1 : 0]};
             if (p48 && nrel > 1 && pstride[0] != pstride[1]) {
-                // one stride per launch: the two relations take turns
+                // one stride per launch: the two relations take turns.  Both
+                // calls use relation 0's region scratch (cursor, cap_end):
+                // correct because they run in order on the one stream `st`
                 for (int r = 0; r < nrel; r++) {
                     const Tup* rr1[1] = {rels[r]};
                     const uint64_t nn1[1] = {ns[r]};

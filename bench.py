@@ -30,6 +30,24 @@ import torch  # noqa: E402  (owns the HIP runtime before the library loads)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
+def set_payloads(R, S, kind, first):
+    """--payload: rewrite the payload column of both relations in HBM (before
+    the timed region).  wide48: 2^40 + global row id -- more than the 48 - s1
+    bits a 48-bit word keeps at the headline plan, within the 64 - s1 of a
+    packed 64-bit word; full64: a 64-bit avalanche hash of the global row id,
+    negative for half the rows -- unpackable, the join keeps 16-byte tuples."""
+    if kind == "rowid" or R.dtype != torch.int64:
+        return
+    for t, salt in ((R, 0), (S, 1 << 62)):
+        i = torch.arange(first, first + t.shape[0], dtype=torch.int64, device=t.device)
+        if kind == "wide48":
+            t[:, 0] = i + (1 << 40)
+        else:
+            z = (i + salt) * -7046029254386353131  # 0x9E3779B97F4A7C15
+            z = (z ^ (z >> 31)) * 0x1B873593CA5A7E35
+            t[:, 0] = z ^ (z >> 29)
+
+
 def _close(dist):
     """Destroy the process group (and the join's cached row communicators)."""
     mod = sys.modules.get("smj.dist")
@@ -72,6 +90,12 @@ def parse():
                         "(a serial shuffle) and held on the device: 12 bytes per key, "
                         "~13 GB on every rank at N = 8 x 128M.  auto: the reference "
                         "stream up to 2^28 keys, the fast sampler above")
+    p.add_argument("--payload", default="rowid", choices=("rowid", "wide48", "full64"),
+                   help="join payloads: rowid = the generators' row ids (R: 5 + i; they "
+                        "fit 48-bit words: the intermediates move 6 bytes an element); "
+                        "wide48 = 2^40 + row id (64-bit packed words, 8 bytes); full64 = "
+                        "random 64-bit values, negative ones included (the 16-byte "
+                        "tuples themselves)")
     p.add_argument("--fanout-bits", type=int, default=8,
                    help="level-1 partitions (2^bits) of the join; the library raises it "
                         "as the relation size needs")
@@ -394,6 +418,7 @@ def main():
         lib.dev_gen_zipf_ref(S, first, total, a.theta, 54321)
     else:
         lib.dev_gen_zipf(S, first, total, a.theta, 54321)
+    set_payloads(R, S, a.payload, first)
     torch.cuda.synchronize()
 
     count = torch.zeros(1, dtype=torch.int64, device="cuda")
@@ -478,7 +503,7 @@ def main():
             _close(dist)
         return
 
-    cfg_key = f"n{n}_w{w}_{a.dist}"
+    cfg_key = f"n{n}_w{w}_{a.dist}" + ("" if a.payload == "rowid" else f"_{a.payload}")
     roof = dominant_roofline(kern, lambda name: alg_bytes_per_launch(name, n, n, n, w), cfg_key)
     pipeline_gbs = 5 * 2 * total * w / (elapsed / a.steps) / 1e9
 
@@ -508,9 +533,14 @@ def main():
                                   "no key-range hint)" if a.api else "")
                                + (f" theta={a.theta} ({'create_relation_zipf, srand(54321)' if a.zipf_gen == 'reference' else 'rejection-inversion sampler'})"
                                   if a.dist == "zipf" else "")
-                               + ", PK/FK keys 1..|R|",
+                               + ", PK/FK keys 1..|R|"
+                               + {"rowid": ", row-id payloads (48-bit intermediates)",
+                                  "wide48": ", payloads 2^40 + row id (64-bit packed "
+                                            "intermediates)",
+                                  "full64": ", random 64-bit payloads (16-byte tuple "
+                                            "intermediates)"}[a.payload if w == 16 else "rowid"],
                    "tuples_per_relation_per_gpu": n, "tuples_per_relation_total": total,
-                   "tuple_bytes": w,
+                   "tuple_bytes": w, "payload": a.payload if w == 16 else "rowid",
                    "distribution": a.dist, "parallelism": f"range-partition x{N}"},
         "roofline": roof,
         "cpu_baseline": cpu,

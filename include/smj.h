@@ -457,7 +457,9 @@ int smj_tuple_bytes(void);
 /* Name of the device the library initialised, for logs. */
 const char * smj_device_name(void);
 
-/* Opaque reusable scratch (device memory).  One per stream/thread. */
+/* Opaque reusable scratch (device memory).  One per stream/thread: calls on
+ * one workspace must be ordered on one stream (they share its scratch and
+ * the group pass's argument slot). */
 typedef struct smj_workspace smj_workspace;
 smj_workspace * smj_workspace_create(void);
 void smj_workspace_destroy(smj_workspace * ws);

@@ -23,7 +23,8 @@ def get(f, d):
 op = get("--op", "join")
 if op == "join":
     n = get("--n", "128000000"); w = get("--width", "16"); dist = get("--dist", "uniform")
-    print(f"n{n}_w{w}_{dist}")
+    pay = get("--payload", "rowid")
+    print(f"n{n}_w{w}_{dist}" + ("" if pay == "rowid" else f"_{pay}"))
 else:
     w = get("--width", "8")
     n = int(get("--n", str(65536 if op == "merge" else 1 << 27)))
