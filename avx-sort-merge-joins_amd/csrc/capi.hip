@@ -417,7 +417,26 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
 #endif
         return can_pack ? 0 : (sampled ? 1 : 2);
     };
-    int mode = first_mode();
+    // The layout hint of the workspace: when the last call of the same shape
+    // had to leave the narrower layouts because of its payloads (too wide for
+    // 48-bit words, or for packed words at all), start at the layout it
+    // reached -- its partition would only be repeated -- and re-probe from the
+    // top every 16th call.  Data-dependent like the fallback it skips; the
+    // results are the same in every layout.
+    const uint64_t shape = ((uint64_t)nrel << 62) ^ ns[0] ^ (nrel > 1 ? ns[1] << 31 : 0);
+    bool hinted = false;
+    auto hinted_mode = [&](int m) {
+        hinted = false;
+        if (ws->mode_hint <= m || ws->hint_shape != shape || ++ws->hint_calls % 16 == 0)
+            return m;
+        const int h = ws->mode_hint == 0 ? (can_pack ? 0 : (sampled ? 1 : 2))
+                                         : (sampled ? 1 : 2);
+        hinted = h > m;
+        return h > m ? h : m;
+    };
+    int mode = hinted_mode(first_mode());
+    const bool started_hinted = hinted;
+    int payload_fb = -2;  // the mode a payload flag sent this call to
     while (mode <= 2) {
         if (mode >= 1) tuple_plan();
         const bool p48 = mode == -1;
@@ -497,6 +516,8 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
             // (overflow, unpackable) as from 64-bit words
             mode = (why[1] & kBadPayload48) && !(why[1] & kBadPayload) && !why[0] && can_pack
                 ? 0 : 1;
+            if (!why[0] && (why[1] & (kBadPayload | kBadPayload48)) && !(why[1] & kBadRange))
+                payload_fb = mode;
             continue;
         }
         if (guessed && (why[1] & kBadRange)) {
@@ -510,10 +531,18 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
 #ifdef KEY_8B
             can_pack = sampled && plan_on_host && use_packing(ws) && LayPacked::usable(hplan);
 #endif
-            mode = first_mode();
+            mode = hinted_mode(first_mode());
             continue;
         }
+        if (mode == 0 && !why[0] && (why[1] & kBadPayload) && !(why[1] & kBadRange))
+            payload_fb = 1;
         mode++;
+    }
+    if (payload_fb >= 0) {
+        ws->mode_hint = payload_fb;
+        ws->hint_shape = shape;
+    } else if (!started_hinted) {
+        ws->mode_hint = -2;  // the narrow layouts held (or failed for other reasons)
     }
     SMJ_CHECK(hipEventRecord(ws->ev[4], st));
 }

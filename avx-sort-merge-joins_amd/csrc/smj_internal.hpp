@@ -68,6 +68,12 @@ struct Workspace {
     // layouts this workspace's sorts and joins may not use
     // (smj_workspace_set_layouts, SMJ_LAYOUT_* in smj.h)
     uint32_t layouts_off = 0;
+    // the layout the last join or sort of shape hint_shape reached after
+    // leaving the narrower ones for its payloads (-2: none; capi.hip
+    // device_bucket), and the calls since (a re-probe every 16th)
+    int mode_hint = -2;
+    uint64_t hint_shape = 0;
+    uint32_t hint_calls = 0;
     std::map<std::string, std::pair<void*, size_t>> bufs;
     std::map<std::string, std::pair<void*, size_t>> pinned;
     // the k-way merge's run table as last uploaded, and where (a repeated
