@@ -655,3 +655,34 @@ def test_reference_generators_vs_oracle(libs, oracles, width, kind, n, maxid, sk
         lib.dev_gen_zipf_ref(t, first, maxid, 0.75, 4242, skip)
     torch.cuda.synchronize()
     assert np.array_equal(lib.to_host(t), exp[first:first + n])
+
+
+def test_layout_hint_alternating_payloads(libs, oracles):
+    """The workspace's layout hint (capi.hip device_bucket): joins of one
+    shape whose payloads alternate between 48-bit, 64-bit-word and unpackable
+    values.  A call after a payload fallback starts at the layout the last one
+    reached (every 16th re-probes from the top); every call must still give
+    the oracle's count and sorted relations, whichever layout it runs in."""
+    import torch
+    orc, lib = oracles[16], libs[16]
+    n = 300_000
+    R, S = make_join_inputs(orc, 16, "pk_fk", n, n)
+    cases = {}
+    for kind in ("rowid", "wide48", "negative"):
+        r, s = R.copy(), S.copy()
+        if kind == "wide48":
+            r["payload"] += np.int64(1) << 44
+        elif kind == "negative":
+            s["payload"] = -1 - s["payload"]
+        exp, eR, eS = orc.sortmergejoin(r, s)
+        cases[kind] = (lib.to_device(r), lib.to_device(s), exp, eR, eS)
+    sR, sS = lib.empty(n), lib.empty(n)
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    seq = ["wide48", "wide48", "rowid", "negative", "negative", "rowid", "wide48"] * 3
+    for kind in seq:
+        dR, dS, exp, eR, eS = cases[kind]
+        lib.dev_join(dR, dS, sR, sS, cnt, 9, 1, n)
+        torch.cuda.synchronize()
+        assert int(cnt.item()) == exp, kind
+        assert np.array_equal(lib.to_host(sR), eR), kind
+        assert np.array_equal(lib.to_host(sS), eS), kind
