@@ -31,6 +31,7 @@
 // finished by the segmented merge sort (mergesort.hip) and the merge-join
 // count kernel.
 #include <algorithm>
+#include <type_traits>
 #include <vector>
 
 #include "smj_common.hpp"
@@ -387,7 +388,7 @@ struct GroupLDS {
     uint32_t run[2][GS_TMAX];
     // per 64-position window w: bit i of m: a run starts at position 64 w + i;
     // wk: runs starting before the window, minus one (one 16-byte LDS read)
-    struct Win {
+    struct alignas(16) Win {  // one 16-byte LDS read
         unsigned long long m;
         uint32_t wk, pad;
     } win[2][GS_WIN];
@@ -667,7 +668,10 @@ __device__ __forceinline__ void group_overflow(const GroupArgs& A, LDS& L,
 // flight at once).  Position j = k * GS_THREADS + thread: a wave's 64
 // positions are one bitmap window (broadcast read), so the run of the lane's
 // position is the window's earlier runs plus the run starts below the lane
-// (mbcnt) and at it.  Lanes past the end re-read position 0.
+// (mbcnt) and at it.  Branch-free (the compiler may then keep several
+// elements' LDS reads in flight): a position past the end has every run start
+// below it, so its run is the last one, and it re-reads the group's last
+// element (p = n - 1).
 template <class Lay, class Src, class Meta>
 __device__ __forceinline__ void gather_group(const GroupArgs& A, GroupLDS<typename Lay::W>& L,
                                              const Meta& C, int r, uint32_t n,
@@ -676,18 +680,15 @@ __device__ __forceinline__ void gather_group(const GroupArgs& A, GroupLDS<typena
     const typename Lay::CView tp = Lay::cview(A.tmp[r], A.pstride[r]) + C.bst[r];
     const uint32_t lane = lane_id();
     const uint32_t wid = __builtin_amdgcn_readfirstlane(otid() >> 6);
+    typedef uint32_t U4 __attribute__((ext_vector_type(4)));
 #pragma unroll
     for (int k = 0; k < GS_ITEMS; k++) {
         const uint32_t w = k * (GS_THREADS / 64) + wid;  // uniform
+        const U4 win = *reinterpret_cast<const U4*>(&L.win[r][w]);
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi(win.y, __builtin_amdgcn_mbcnt_lo(win.x, 0u));
+        const uint32_t at = (uint32_t)((((uint64_t)win.y << 32) | win.x) >> lane) & 1u;
         const uint32_t j = w * 64 + lane;
-        const auto win = L.win[r][w];
-        const uint32_t below = __builtin_amdgcn_mbcnt_hi(
-            (uint32_t)(win.m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)win.m, 0u));
-        const uint32_t at = (uint32_t)(win.m >> lane) & 1u;
-        const bool ok = j < n;
-        const uint32_t q = ok ? win.wk + below + at : 0u;
-        const uint32_t p = ok ? j : 0u;
-        v[k] = Src::load(tp + (uint32_t)(p + L.run[r][q]));
+        v[k] = Src::load(tp + (min(j, n - 1) + L.run[r][win.z + below + at]));
     }
 }
 
@@ -906,9 +907,10 @@ __device__ __forceinline__ uint32_t sort_two(const GroupArgs& A, GroupLDS<typena
     bool clamped = false;
     auto hist = [&](int r, const W(&v)[GS_ITEMS]) {
         if (fast(r)) {
+            const typename Lay::FastDigit fd(P, P.s3, P.D3);
 #pragma unroll
             for (int k = 0; k < GS_ITEMS; k++) {
-                const uint32_t d = Lay::digit_fast(v[k], base_lo, P.s1, P.s3, mask3);
+                const uint32_t d = fd(v[k]);
                 if (k * GS_THREADS + tid < nr[r])
                     atomicAdd(&L.cnt[r][d >> 1], 1u << ((d & 1) * 16));
             }
@@ -986,24 +988,32 @@ __device__ __forceinline__ uint32_t sort_two(const GroupArgs& A, GroupLDS<typena
                                  : cur[valid ? d >> 1 : 0u];
         L.B[valid ? (old >> sh) & 0xffffu : GS_CAP] = x;
     };
+    // one loop per (digit form, placement form): `dup` is uniform, and
+    // tested inside the element loop it made every element wait for the LDS
+    // queue before and after its cursor read; unswitched, the plain reads of
+    // the no-repeat form are in flight together
+    auto place_loop = [&](int r, uint32_t* cur, const W(&v)[GS_ITEMS], auto&& digit,
+                          auto dupc) {
+#pragma unroll
+        for (int k = 0; k < GS_ITEMS; k++) {
+            // an opaque copy of each element: otherwise the compiler keeps the
+            // histogram's digits alive over the scans instead of recomputing
+            W x = v[k];
+            launder(x);
+            place1(cur, decltype(dupc)::value, k * GS_THREADS + tid < nr[r], digit(x), v[k]);
+        }
+    };
     auto place = [&](int r, uint32_t* cur, bool dup, const W(&v)[GS_ITEMS]) {
-        // an opaque copy of each element: otherwise the compiler keeps the
-        // histogram's digits alive over the scans instead of recomputing them
+        typedef std::integral_constant<bool, true> Dup;
+        typedef std::integral_constant<bool, false> NoDup;
         if (fast(r)) {
-#pragma unroll
-            for (int k = 0; k < GS_ITEMS; k++) {
-                W x = v[k];
-                launder(x);
-                place1(cur, dup, k * GS_THREADS + tid < nr[r],
-                       Lay::digit_fast(x, base_lo, P.s1, P.s3, mask3), v[k]);
-            }
+            const typename Lay::FastDigit fd(P, P.s3, P.D3);
+            if (dup) place_loop(r, cur, v, fd, Dup());
+            else place_loop(r, cur, v, fd, NoDup());
         } else {
-#pragma unroll
-            for (int k = 0; k < GS_ITEMS; k++) {
-                W x = v[k];
-                launder(x);
-                place1(cur, dup, k * GS_THREADS + tid < nr[r], slow_digit(r, x), v[k]);
-            }
+            auto sd = [&](const W& x) { return slow_digit(r, x); };
+            if (dup) place_loop(r, cur, v, sd, Dup());
+            else place_loop(r, cur, v, sd, NoDup());
         }
     };
     // after a placement by atomics every cursor word holds its two bins'
@@ -1026,10 +1036,11 @@ __device__ __forceinline__ uint32_t sort_two(const GroupArgs& A, GroupLDS<typena
     auto write = [&](int r) {
         const uint32_t cb = PAIR && r ? C.b[1] : C.b[0];
         Tup* dst = A.out[r] + C.ost[r] + off[r];
+        const typename Lay::Unpack up(P, cb);
 #pragma unroll
         for (int k = 0; k < GS_ITEMS; k++) {
             const uint32_t j = k * GS_THREADS + tid;
-            if (j < nr[r] && SMJ_GS_ABL != 3) st_stream(dst + j, Lay::unpack(P, L.B[j], cb));
+            if (j < nr[r] && SMJ_GS_ABL != 3) st_stream(dst + j, up(L.B[j]));
         }
     };
     uint32_t failed = 0;

@@ -283,6 +283,21 @@ struct LayTup {
     __host__ static bool fast_ok(const RangePlan& P, uint32_t sh, uint32_t width) {
         return sh + width <= 32;
     }
+    // digit_fast and unpack with their plan values read once (per group) into
+    // registers: the group pass's per-element code then reads no argument
+    // memory (bucketsort.hip sort_two)
+    struct FastDigit {
+        uint32_t base_lo, sh, mask;
+        __device__ FastDigit(const RangePlan& P, uint32_t s, uint32_t width)
+            : base_lo((uint32_t)P.base), sh(s), mask((1u << width) - 1) {}
+        __device__ __forceinline__ uint32_t operator()(const W& w) const {
+            return (((uint32_t)tup_key(w) - base_lo) >> sh) & mask;
+        }
+    };
+    struct Unpack {
+        __device__ Unpack(const RangePlan&, uint32_t) {}
+        __device__ __forceinline__ Tup operator()(const W& w) const { return w; }
+    };
     // equal keys: the elements are identical iff these values are
     __device__ static __forceinline__ uint64_t same_key_id(const W& w) {
 #ifdef KEY_8B
@@ -323,6 +338,26 @@ struct LayPacked {
         t.key = (int64_t)((key_u(P.base) + rel(P, w, b)) ^ 0x8000000000000000ull);
         return t;
     }
+    struct FastDigit {  // digit_fast with the plan read once (LayTup::FastDigit)
+        uint32_t tsh, mask;
+        __device__ FastDigit(const RangePlan& P, uint32_t s, uint32_t width)
+            : tsh(64 - P.s1 + s), mask((1u << width) - 1) {}
+        __device__ __forceinline__ uint32_t operator()(const W& w) const {
+            return (uint32_t)(w >> tsh) & mask;
+        }
+    };
+    struct Unpack {  // unpack of bucket b's words, the plan read once
+        uint64_t kbu, pmask;
+        uint32_t sh;
+        __device__ Unpack(const RangePlan& P, uint32_t b)
+            : kbu(key_u(P.base) + ((uint64_t)b << P.s1)), pmask(~0ull >> P.s1), sh(64 - P.s1) {}
+        __device__ __forceinline__ Tup operator()(const W& w) const {
+            Tup t;
+            t.payload = (int64_t)(w & pmask);
+            t.key = (int64_t)((kbu + (w >> sh)) ^ 0x8000000000000000ull);
+            return t;
+        }
+    };
     // the level-1 partition's packing of tuple t into bucket rel >> s1;
     // `bad` gets kBadPayload when the payload lies outside [0, 2^pb) and
     // kBadRange when the key lies outside the plan (t cannot be packed)
@@ -442,6 +477,35 @@ struct LayP48 {
         return ((uint64_t)(uint32_t)key << 32) | pay;
 #endif
     }
+    struct FastDigit {  // digit_fast with the plan read once (LayTup::FastDigit)
+        uint32_t tsh, mask;
+        __device__ FastDigit(const RangePlan& P, uint32_t s, uint32_t width)
+            : tsh(48 - P.s1 + s), mask((1u << width) - 1) {}
+        __device__ __forceinline__ uint32_t operator()(const W& w) const {
+            return (uint32_t)(w >> tsh) & mask;
+        }
+    };
+    // unpack of bucket b's words, the plan read once: key = base + b 2^s1 +
+    // (w >> (48 - s1)) (the low s1 bits of the offset and the bucket's bits
+    // do not overlap, so + is |); 8-byte tuples need the low 32 bits only
+    struct Unpack {
+        uint64_t kbu, pmask;
+        uint32_t sh;
+        __device__ Unpack(const RangePlan& P, uint32_t b)
+            : kbu(key_u(P.base) + ((uint64_t)b << P.s1)), pmask(~0ull >> (16 + P.s1)),
+              sh(48 - P.s1) {}
+        __device__ __forceinline__ Tup operator()(const W& w) const {
+#ifdef KEY_8B
+            Tup t;
+            t.payload = (int64_t)(w & pmask);
+            t.key = (int64_t)((kbu + (w >> sh)) ^ 0x8000000000000000ull);
+            return t;
+#else
+            const uint32_t key = (uint32_t)kbu + (uint32_t)(w >> sh);
+            return ((uint64_t)key << 32) | (uint32_t)(w & pmask);
+#endif
+        }
+    };
     struct Pack {
         typedef uint64_t OutT;
         uint64_t bu, span;
