@@ -197,6 +197,30 @@ struct DevColl {
         }
         SMJ_NCCL(ncclAllReduce(p, p, 1, ncclUint64, ncclSum, comm[sid], ops->st[sid]));
     }
+    // a host value over the ranks (0 sum, 1 min, 2 max): in one process
+    // through the host group, across processes one 8-byte ncclAllReduce
+    int64_t* red_dev = nullptr;
+    int64_t* red_host = nullptr;
+    int64_t reduce(int64_t v, int op) {
+        if (!rccl) return copy.reduce(v, op);
+        if (!red_dev) {
+            red_dev = (int64_t*)ops->alloc(8);
+            red_host = (int64_t*)ops->host_alloc(8);
+        }
+        *red_host = v;
+        ops->to_dev(red_dev, red_host, 8, mg::kMain);
+        SMJ_NCCL(ncclAllReduce(red_dev, red_dev, 1, ncclInt64,
+                               op == 1 ? ncclMin : op == 2 ? ncclMax : ncclSum, comm[mg::kMain],
+                               ops->st[mg::kMain]));
+        ops->to_host(red_host, red_dev, 8, mg::kMain);
+        ops->sync(mg::kMain);
+        return *red_host;
+    }
+    void release() {
+        if (red_dev) ops->release(red_dev);
+        if (red_host) ops->host_release(red_host);
+        red_dev = red_host = nullptr;
+    }
 };
 
 typedef mg::Rank<DevOps, DevColl> DevRank;
@@ -226,6 +250,7 @@ struct RankCtx {
     ~RankCtx() {
         (void)hipSetDevice(device);
         rank.release_all();
+        coll.release();
         for (int r = 0; r < 2; r++)
             if (inbuf[r]) (void)hipFree(inbuf[r]);
         for (auto& e : ops.ev) (void)hipEventDestroy(e);
@@ -283,7 +308,6 @@ Group& group_for(int G, bool rccl) {
     }
     for (int r = 0; r < G; r++) {
         RankCtx& rc = *g->ranks[r];
-        rc.rank.grp = g->host.get();
         rc.rank.me = r;
         rc.rank.G = G;
         rc.coll.rccl = rccl;
@@ -531,6 +555,116 @@ int64_t smj_mgpu_join(const tuple_t* R, uint64_t nR, const tuple_t* S, uint64_t 
 void smj_mgpu_release(void) {
     std::lock_guard<std::mutex> lk(g_mu);
     g_group.reset();
+}
+
+// ---- one rank of a multi-process group (one process per GPU: bench.py
+// --gpus N under torch.distributed.run).  The two communicators come from one
+// id: ncclCommInitRank, then ncclCommSplit for the row exchange's own.
+struct smj_mgpu_comm {
+    RankCtx* rc;
+    ncclComm_t comm[2];
+};
+
+int smj_mgpu_unique_id(void* out, int cap) {
+    if (cap < (int)sizeof(ncclUniqueId)) return -(int)sizeof(ncclUniqueId);
+    ncclUniqueId id;
+    SMJ_NCCL(ncclGetUniqueId(&id));
+    memcpy(out, &id, sizeof(id));
+    return (int)sizeof(id);
+}
+
+smj_mgpu_comm* smj_mgpu_comm_init(const void* id, int nranks, int rank) {
+    if (nranks < 1 || rank < 0 || rank >= nranks) {
+        fprintf(stderr, "[ERROR] smj_mgpu_comm_init: rank %d of %d\n", rank, nranks);
+        abort();
+    }
+    int dev = 0;
+    SMJ_CHECK(hipGetDevice(&dev));
+    smj_mgpu_comm* c = new smj_mgpu_comm();
+    c->rc = new RankCtx(dev);
+    ncclUniqueId uid;
+    memcpy(&uid, id, sizeof(uid));
+    SMJ_NCCL(ncclCommInitRank(&c->comm[0], nranks, uid, rank));
+    SMJ_NCCL(ncclCommSplit(c->comm[0], 0, rank, &c->comm[1], NULL));
+    RankCtx& rc = *c->rc;
+    rc.rank.me = rank;
+    rc.rank.G = nranks;
+    rc.coll.rccl = true;
+    rc.coll.me = rank;
+    rc.coll.comm[0] = c->comm[0];
+    rc.coll.comm[1] = c->comm[1];
+    return c;
+}
+
+int64_t smj_mgpu_rank_join(smj_mgpu_comm* c, const tuple_t* R, uint64_t nR, const tuple_t* S,
+                           uint64_t nS, uint32_t flags, int64_t key_min, int64_t key_max,
+                           uint64_t guess_max, tuple_t** sortedR, uint64_t* nR_out,
+                           tuple_t** sortedS, uint64_t* nS_out, smj_mgpu_stats* stats) {
+    RankCtx& rc = *c->rc;
+    int dev0 = 0;
+    SMJ_CHECK(hipGetDevice(&dev0));
+    SMJ_CHECK(hipSetDevice(rc.device));
+    mg::Options o;
+    if (key_min <= key_max) {
+        o.kmin = key_min;
+        o.kmax = key_max;
+    } else {
+        o.guess_max = guess_max;
+    }
+    o.planes = !(flags & SMJ_MG_NOPLANES);
+    o.staged = !(flags & SMJ_MG_ONECALL);
+    o.sampled = (flags & SMJ_MG_SAMPLED) ? 1 : (flags & SMJ_MG_EXACT) ? 0 : -1;
+    // every rank must take the same level-1 width: from the largest share
+    // (an 8-byte all-reduce)
+    const uint64_t nmax = (uint64_t)rc.coll.reduce((int64_t)(nR > nS ? nR : nS), 2);
+    o.bucket_bits = bucket_bits_for(nmax);
+    struct timeval t0, t1;
+    gettimeofday(&t0, NULL);
+    const void* r = stage_slice(rc, 0, (const Tup*)R, 0, nR);
+    const void* s = stage_slice(rc, 1, (const Tup*)S, 0, nS);
+    uint64_t onR = 0, onS = 0, loc = 0;
+    const uint64_t total = rc.rank.run(r, nR, s, nS, o, &onR, &onS, &loc);
+    gettimeofday(&t1, NULL);
+    if (sortedR) *sortedR = (tuple_t*)rc.rank.sorted[0];
+    if (sortedS) *sortedS = (tuple_t*)rc.rank.sorted[1];
+    if (nR_out) *nR_out = onR;
+    if (nS_out) *nS_out = onS;
+    if (stats) {
+        const mg::Stats& x = rc.rank.stats;
+        stats->layout = x.layout;
+        stats->pbits = x.pbits;
+        stats->attempts = x.attempts;
+        stats->replans = x.replans;
+        stats->sent_bytes = x.sent_B;
+        stats->recv_bytes = x.recv_B;
+        stats->key_min = x.kmin;
+        stats->key_max = x.kmax;
+        stats->ms = (t1.tv_sec - t0.tv_sec) * 1e3 + (t1.tv_usec - t0.tv_usec) * 1e-3;
+    }
+    SMJ_CHECK(hipSetDevice(dev0));
+    return (int64_t)total;
+}
+
+void smj_mgpu_rank_sorted(smj_mgpu_comm* c, tuple_t* outR, tuple_t* outS) {
+    RankCtx& rc = *c->rc;
+    int dev0 = 0;
+    SMJ_CHECK(hipGetDevice(&dev0));
+    SMJ_CHECK(hipSetDevice(rc.device));
+    uint64_t n[2] = {0, 0};
+    rc.rank.sorted_sizes(&n[0], &n[1]);
+    if (outR) rc.ops.copy(outR, rc.rank.sorted[0], n[0] * sizeof(Tup), mg::kMain);
+    if (outS) rc.ops.copy(outS, rc.rank.sorted[1], n[1] * sizeof(Tup), mg::kMain);
+    rc.ops.sync(mg::kMain);
+    SMJ_CHECK(hipSetDevice(dev0));
+}
+
+smj_workspace* smj_mgpu_comm_workspace(smj_mgpu_comm* c) { return c->rc->ops.w(); }
+
+void smj_mgpu_comm_destroy(smj_mgpu_comm* c) {
+    if (!c) return;
+    delete c->rc;
+    for (int i = 1; i >= 0; i--) (void)ncclCommDestroy(c->comm[i]);
+    delete c;
 }
 
 }  // extern "C"

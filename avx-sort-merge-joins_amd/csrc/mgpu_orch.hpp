@@ -57,6 +57,8 @@
 //   void exchange(int stream, const std::vector<Piece>& sends,
 //                 const std::vector<Piece>& recvs);
 //   void allreduce_sum_u64(int stream, unsigned long long* dev);
+//   int64_t reduce(int64_t v, int op);   host value over the ranks (0 sum,
+//                                        1 min, 2 max), every rank gets it
 #pragma once
 #include <stdint.h>
 #include <stdio.h>
@@ -259,6 +261,7 @@ struct CopyColl {
         ops->to_dev(dev, &v, 8, stream);
         ops->sync(stream);
     }
+    int64_t reduce(int64_t v, int op) { return grp->reduce(me, v, op); }
 };
 
 // ---------------------------------------------------------------------------
@@ -289,7 +292,6 @@ template <class Ops, class Coll>
 struct Rank {
     Ops* ops;
     Coll* coll;
-    HostGroup* grp;
     int me = 0, G = 1;
 
     // buffers kept across calls (sticky sizes, like dist.py's)
@@ -619,8 +621,8 @@ struct Rank {
             l = a;
             h = b;
         }
-        *lo = grp->reduce(me, l, 1);
-        *hi = grp->reduce(me, h, 2);
+        *lo = coll->reduce(l, 1);
+        *hi = coll->reduce(h, 2);
     }
 
     // One join of this rank's slices R[0, nR) and S[0, nS).  Returns the
@@ -726,10 +728,15 @@ struct Rank {
         coll->allreduce_sum_u64(kMain, count + 1);
         ops->to_host(count_h, count, 16, kMain);
         ops->sync(kMain);
-        *nR_out = v[0].nused;
-        *nS_out = v[1].nused;
+        *nR_out = last_n[0] = v[0].nused;
+        *nS_out = last_n[1] = v[1].nused;
         *local = count_h[0];
         return count_h[1];
+    }
+    uint64_t last_n[2] = {0, 0};
+    void sorted_sizes(uint64_t* nr, uint64_t* ns) const {
+        *nr = last_n[0];
+        *ns = last_n[1];
     }
 
     void release_all() {

@@ -65,7 +65,9 @@ DEVICE_SYMBOLS = [
     "smj_dev_gen_nonunique", "smj_dev_gen_zipf_ref", "smj_glibc_rand",
     "smj_dev_xsend", "smj_dev_xrecv", "smj_join", "smj_dev_partition_range_planes",
     "smj_dev_join_segmented_planes", "smj_mgpu_join", "smj_mgpu_release",
-    "smj_inregister_sort_keyval32", "smj_workspace_set_layouts",
+    "smj_inregister_sort_keyval32", "smj_workspace_set_layouts", "smj_mgpu_unique_id",
+    "smj_mgpu_comm_init", "smj_mgpu_rank_join", "smj_mgpu_comm_destroy", "smj_mgpu_rank_sorted",
+    "smj_mgpu_comm_workspace",
 ]
 
 
@@ -111,6 +113,44 @@ LAYOUT_NO_P48, LAYOUT_NO_PACKED, LAYOUT_NO_SAMPLED, LAYOUT_SAMPLE_PLAN = 1, 2, 4
 # smj_mgpu_join flags (include/smj.h)
 MG_COPY, MG_NOPLANES, MG_ONECALL, MG_SAMPLED, MG_EXACT = 1, 2, 4, 8, 16
 MG_LAYOUTS = ("tuples", "words", "planes")
+
+
+class MgpuComm:
+    """One rank of a multi-process smj_mgpu_comm (Library.mgpu_comm)."""
+
+    def __init__(self, lib, handle):
+        self.lib, self.h = lib, handle
+
+    def join(self, R, S, flags=0, key_range=None, guess_max=0):
+        """smj_mgpu_rank_join on this rank's device slices (torch tensors of
+        shape (n, 2)): (global count, tuples of the rank's sorted R share and
+        S share, stats); sorted() copies the shares out."""
+        L = self.lib
+        nR, nS = C.c_uint64(), C.c_uint64()
+        st = MgpuStats()
+        kmin, kmax = key_range if key_range is not None else (1, 0)
+        # the library's streams read R and S: torch's writes must be done
+        torch.cuda.current_stream(R.device).synchronize()
+        c = L.lib.smj_mgpu_rank_join(self.h, R.data_ptr(), R.shape[0], S.data_ptr(),
+                                     S.shape[0], flags, kmin, kmax, guess_max, None,
+                                     C.byref(nR), None, C.byref(nS), C.byref(st))
+        stats = {f: getattr(st, f) for f, _ in MgpuStats._fields_}
+        stats["layout"] = MG_LAYOUTS[stats["layout"]]
+        self.n = (nR.value, nS.value)
+        return int(c), nR.value, nS.value, stats
+
+    def sorted(self):
+        """The rank's sorted shares of the last join, copied into new device
+        tensors."""
+        sR, sS = self.lib.empty(self.n[0]), self.lib.empty(self.n[1])
+        self.lib.lib.smj_mgpu_rank_sorted(self.h, sR.data_ptr() if self.n[0] else None,
+                                          sS.data_ptr() if self.n[1] else None)
+        return sR, sS
+
+    def close(self):
+        if self.h:
+            self.lib.lib.smj_mgpu_comm_destroy(self.h)
+            self.h = None
 
 
 class ChainedTupleBuffer(C.Structure):
@@ -219,6 +259,13 @@ class Library:
             "smj_mgpu_join": (_I64, [_P, _U64, _P, _U64, C.c_int, _U32, _I64, _I64, _P, _P,
                                      _P, _P]),
             "smj_mgpu_release": (None, []),
+            "smj_mgpu_unique_id": (C.c_int, [_P, C.c_int]),
+            "smj_mgpu_comm_init": (_P, [_P, C.c_int, C.c_int]),
+            "smj_mgpu_rank_join": (_I64, [_P, _P, _U64, _P, _U64, _U32, _I64, _I64, _U64,
+                                          _P, _P, _P, _P, _P]),
+            "smj_mgpu_comm_destroy": (None, [_P]),
+            "smj_mgpu_rank_sorted": (None, [_P, _P, _P]),
+            "smj_mgpu_comm_workspace": (_P, [_P]),
             "smj_inregister_sort_keyval32": (None, [_P, _P, _U64]),
             "smj_workspace_set_layouts": (None, [_P, _U32]),
             "smj_trace_enable": (None, [_P, C.c_int]),
@@ -395,6 +442,24 @@ class Library:
         stats = {f: getattr(st, f) for f, _ in MgpuStats._fields_}
         stats["layout"] = MG_LAYOUTS[stats["layout"]]
         return int(c), sR, sS, counts.reshape(G, 2), stats
+
+    def mgpu_comm(self, nranks, rank, group=None):
+        """smj_mgpu_comm_init for this process's rank of a torch.distributed
+        group (one process per GPU): rank 0's id is broadcast over `group`."""
+        import torch.distributed as dist
+        idb = np.zeros(128, np.uint8)
+        if rank == 0:
+            n = self.lib.smj_mgpu_unique_id(_ptr(idb), len(idb))
+            assert n == 128, n
+        if nranks > 1:
+            t = torch.from_numpy(idb.astype(np.int64))
+            if dist.get_backend(group) == "nccl":
+                t = t.cuda()
+            dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0,
+                           group=group)
+            idb = t.cpu().numpy().astype(np.uint8)
+        c = self.lib.smj_mgpu_comm_init(_ptr(idb), nranks, rank)
+        return MgpuComm(self, c)
 
     def sortmergejoin_multiway(self, R, S, nthreads=1, fanout=128, mpsm=False,
                                algo=None, materialize=False, persist=None):

@@ -113,6 +113,10 @@ def parse():
     p.add_argument("--exchange-path", action="store_true",
                    help="run the multi-GPU code path (range partition, all-to-all, "
                         "segmented local join) even at N=1 (a one-rank RCCL group)")
+    p.add_argument("--impl", default="python", choices=("python", "c"),
+                   help="multi-GPU join: the torch.distributed orchestration (smj.dist) or "
+                        "the C entry smj_mgpu_rank_join (mgpu_orch.hpp, its own RCCL "
+                        "communicator per rank)")
     p.add_argument("--api", action="store_true",
                    help="join: time the reference-named entry point sortmergejoin_multiway "
                         "(relation_t over device-resident tuples, no key-range hint: the "
@@ -449,6 +453,18 @@ def main():
 
         def step():
             lib.dev_join(R, S, sR, sS, count, a.fanout_bits, 1, total)
+    elif a.impl == "c":
+        comm = lib.mgpu_comm(N, rank)
+        mg_st = {"steps": 0, "sent_B": 0, "recv_B": 0, "layout": None}
+
+        def step():
+            c, _, _, st = comm.join(R, S, key_range=(1, total))
+            count.fill_(c)
+            mg_st["steps"] += 1
+            mg_st["sent_B"] += st["sent_bytes"]
+            mg_st["recv_B"] += st["recv_bytes"]
+            mg_st["layout"] = st["layout"]
+        tracer = _WsTracer(lib, lib.lib.smj_mgpu_comm_workspace(comm.h))
     else:
         from smj.dist import DeviceOps, DistributedJoin
         # n_hint: the same on every rank (the largest share)
@@ -460,7 +476,9 @@ def main():
             last[0], last[1] = dj.step(R, S, count)
 
     def reset():
-        if exchange:
+        if exchange and a.impl == "c":
+            mg_st.update(steps=0, sent_B=0, recv_B=0)
+        elif exchange:
             dj.stats_reset()
 
     elapsed, kern, brk = timed_loop(a, tracer, dist, step, reset)
@@ -468,7 +486,13 @@ def main():
         count.fill_(api_count[0])
 
     xchg = None
-    if exchange:
+    if exchange and a.impl == "c":
+        k = max(mg_st["steps"], 1)
+        xchg = {"impl": "c (smj_mgpu_rank_join)",
+                "xgmi_bytes_sent_per_gpu": mg_st["sent_B"] // k,
+                "xgmi_bytes_recv_per_gpu": mg_st["recv_B"] // k,
+                "exchange_layout": mg_st["layout"], "xgmi_peak_GBps": 7 * 153}
+    elif exchange:
         st = dj.stats_read()
         k = max(st["steps"], 1)
         # xGMI bytes per GPU per step and S's row all-to-all rate (SURVEY.md
@@ -492,12 +516,16 @@ def main():
     # sorted relations internal, so --api checks the count only
     chk = None
     if not a.no_check and not (a.api and not exchange):
+        if exchange and a.impl == "c":
+            last = list(comm.sorted())
         outs = (sR, sS) if not exchange else tuple(last)
         chk = output_check([(R, outs[0]), (S, outs[1])], w, dist if exchange and N > 1 else None)
         ok = ok and chk["sorted"] and chk["checksum_equal"]
     ms_step = elapsed / a.steps * 1e3
     value = 2 * total / (elapsed / a.steps) / 1e6
 
+    if exchange and a.impl == "c":
+        comm.close()
     if rank != 0:
         if dist:
             _close(dist)
@@ -541,7 +569,8 @@ def main():
                                             "intermediates)"}[a.payload if w == 16 else "rowid"],
                    "tuples_per_relation_per_gpu": n, "tuples_per_relation_total": total,
                    "tuple_bytes": w, "payload": a.payload if w == 16 else "rowid",
-                   "distribution": a.dist, "parallelism": f"range-partition x{N}"},
+                   "distribution": a.dist, "parallelism": f"range-partition x{N}"
+                   + (" (C orchestration)" if exchange and a.impl == "c" else "")},
         "roofline": roof,
         "cpu_baseline": cpu,
         "result_ok": ok,

@@ -445,6 +445,32 @@ int64_t smj_mgpu_join(const tuple_t * R, uint64_t nR, const tuple_t * S, uint64_
  * calls of one configuration). */
 void smj_mgpu_release(void);
 
+/* The same join with one rank per PROCESS (one process per GPU, e.g. under
+ * torch.distributed.run): rank 0 gets an id (smj_mgpu_unique_id: writes up to
+ * `cap` bytes, returns their count, 128), every process passes it to
+ * smj_mgpu_comm_init on its current device, then every rank calls
+ * smj_mgpu_rank_join with its own slices of R and S (host, or device memory
+ * of its GPU).  key_min <= key_max: the global key range, the same on every
+ * rank; otherwise keys 1..guess_max (the global |R|), verified.  *sortedR /
+ * *sortedS receive device pointers to the rank's sorted share (*nR_out /
+ * *nS_out tuples, one contiguous key range, ranks in order), valid until the
+ * next call on the communicator.  Returns the global match count on every
+ * rank.  flags: SMJ_MG_NOPLANES / _ONECALL / _SAMPLED / _EXACT. */
+typedef struct smj_mgpu_comm smj_mgpu_comm;
+int smj_mgpu_unique_id(void * out, int cap);
+smj_mgpu_comm * smj_mgpu_comm_init(const void * id, int nranks, int rank);
+int64_t smj_mgpu_rank_join(smj_mgpu_comm * comm, const tuple_t * R, uint64_t nR,
+                           const tuple_t * S, uint64_t nS, uint32_t flags,
+                           int64_t key_min, int64_t key_max, uint64_t guess_max,
+                           tuple_t ** sortedR, uint64_t * nR_out, tuple_t ** sortedS,
+                           uint64_t * nS_out, smj_mgpu_stats * stats);
+/* copies the rank's sorted shares of the last smj_mgpu_rank_join (host or
+ * device destinations; NULL skips one) */
+void smj_mgpu_rank_sorted(smj_mgpu_comm * comm, tuple_t * outR, tuple_t * outS);
+/* the rank's workspace (its kernel trace: smj_trace_*) */
+struct smj_workspace * smj_mgpu_comm_workspace(smj_mgpu_comm * comm);
+void smj_mgpu_comm_destroy(smj_mgpu_comm * comm);
+
 /* ------------------------------------------------------------------------ */
 /* Device-resident asynchronous API (no reference counterpart: this is the   */
 /* form a GPU-aware caller binds).  All pointers are device pointers,        */

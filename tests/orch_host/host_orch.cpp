@@ -437,7 +437,6 @@ extern "C" int64_t host_mpsm_join(const void* R, uint64_t nR, const void* S, uin
         coll[g].me = g;
         ranks[g].ops = &ops[g];
         ranks[g].coll = &coll[g];
-        ranks[g].grp = &grp;
         ranks[g].me = g;
         ranks[g].G = G;
     }

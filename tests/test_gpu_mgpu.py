@@ -142,3 +142,29 @@ def test_mgpu_configurations_alternate(libs, oracles):
         assert lib.mgpu_join(R, S, G, flags, sorted_out=False)[0] == want
         assert lib.sortmergejoin_multiway(R, S, nthreads=4, algo="mpsm") == want
     lib.lib.smj_mgpu_release()
+
+
+@pytest.mark.parametrize("kind", ["uniform", "zipf", "outside"])
+def test_mgpu_rank_comm_world1(libs, oracles, width, kind):
+    """The multi-process entry (smj_mgpu_comm_init over ncclCommInitRank +
+    ncclCommSplit, smj_mgpu_rank_join, smj_mgpu_rank_sorted) as one rank of a
+    world of one: device slices in, count and sorted shares as the oracle's;
+    a second call on the same communicator reuses its buffers."""
+    import torch
+    orc, lib = oracles[width], libs[width]
+    R, S = relations(orc, width, 300007, kind, seed=2024)
+    want, eR, eS = orc.sortmergejoin(R, S)
+    it = np.int64 if width == 16 else np.int32
+    tR = torch.from_numpy(R.view(it).reshape(-1, 2).copy()).cuda()
+    tS = torch.from_numpy(S.view(it).reshape(-1, 2).copy()).cuda()
+    comm = lib.mgpu_comm(1, 0)
+    try:
+        for _ in range(2):
+            c, nR, nS, st = comm.join(tR, tS, guess_max=len(R))
+            assert c == want and (nR, nS) == (len(R), len(S))
+            assert st["replans"] == (1 if kind == "outside" else 0)
+            sR, sS = comm.sorted()
+            assert np.array_equal(sR.cpu().numpy().reshape(-1).view(R.dtype), eR)
+            assert np.array_equal(sS.cpu().numpy().reshape(-1).view(S.dtype), eS)
+    finally:
+        comm.close()
