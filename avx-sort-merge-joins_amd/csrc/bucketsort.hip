@@ -90,7 +90,7 @@ constexpr int TP_THREADS = SMJ_TP_THREADS;
 #endif
 #ifndef SMJ_GS_ABL
 #define SMJ_GS_ABL 0  // ablations for measurements only (1: no in-group sort; 2: no
-                      // equal-digit run fixing; 3: no write-out)
+                      // equal-digit run fixing; 3: no write-out; profiles/r05_lab/abl.txt)
 #endif
 // elements a tile-pass thread holds: the stage of a tile is 128 KB of LDS
 // (16-byte elements: 16-byte tuples in their own layout take half the tile)
@@ -889,6 +889,27 @@ __device__ __forceinline__ uint32_t sort_two(const GroupArgs& A, GroupLDS<typena
                                              unsigned long long& matches, bool& exact,
                                              Hook0&& after0, Hook1&& after1) {
     typedef typename Lay::W W;
+#if SMJ_GS_ABL == 1
+    {   // ablation (timing only): no sort, each lane writes its elements to
+        // the group's place in gathered order (the output is not sorted, the
+        // count not taken)
+        const uint32_t t = otid();
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+            const W(&v)[GS_ITEMS] = r ? v1 : v0;
+            const uint32_t cb = PAIR && r ? C.b[1] : C.b[0];
+            Tup* dst = A.out[r] + C.ost[r] + off[r];
+            const typename Lay::Unpack up(P, cb);
+#pragma unroll
+            for (int k = 0; k < GS_ITEMS; k++)
+                if (k * GS_THREADS + t < nr[r]) st_stream(dst + k * GS_THREADS + t, up(v[k]));
+            if (r == 0) after0(); else after1();
+        }
+        __syncthreads();
+        exact = true;
+        return 0u;
+    }
+#endif
     const uint32_t tid = otid(), wid = tid >> 6, lane = tid & 63;
     // the d3 digit of slot r's elements: the fast form unless the group is
     // an edge group of the plan (the branch is uniform: taken outside the
