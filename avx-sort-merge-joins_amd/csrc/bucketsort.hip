@@ -129,9 +129,15 @@ constexpr int GS_THREADS = SMJ_GS_THREADS;      // one workgroup per group
 #ifndef SMJ_GS_WG_PER_CU8
 #define SMJ_GS_WG_PER_CU8 4
 #endif
-template <class W>
+// 32-bit words (LayP32) in pair mode (one relation: the sort): the kernel
+// needs ~85 VGPRs and 26 KB of LDS a workgroup, so more fit
+#ifndef SMJ_GS_WG_PER_CU4P
+#define SMJ_GS_WG_PER_CU4P 5  // 4: sort 2^27 group pass 0.474 ms, 5: 0.447, 6: 0.440 (r05_lab/p32_ab.txt)
+#endif
+template <class W, bool PAIR = false>
 constexpr int gs_wg_per_cu() {
-    return sizeof(W) == 16 ? SMJ_GS_WG_PER_CU : SMJ_GS_WG_PER_CU8;
+    return sizeof(W) == 16 ? SMJ_GS_WG_PER_CU
+         : (sizeof(W) == 4 && PAIR) ? SMJ_GS_WG_PER_CU4P : SMJ_GS_WG_PER_CU8;
 }
 // 2560 elements per relation: the plan's groups average 2048, so a group's
 // run in an 8192-element tile was ~64 words (512 B; 16384-element tiles since
@@ -1319,7 +1325,8 @@ typedef GroupArgs GroupArgsParam;
 __global__ void k_put_args(GroupArgs G, GroupArgs* dst) { *dst = G; }
 
 template <class Lay, int TPL, bool PAIR>
-__global__ void __launch_bounds__(GS_THREADS, gs_wg_per_cu<typename Lay::W>() * GS_THREADS / 256)
+__global__ void __launch_bounds__(GS_THREADS,
+                                  (gs_wg_per_cu<typename Lay::W, PAIR>() * GS_THREADS / 256))
 k_groupsort(GroupArgsParam Ap) {
     typedef typename Lay::W W;
     const GroupArgs& A = SMJ_GS_ARGS_REF(Ap);
@@ -2281,7 +2288,8 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
 #endif
     if (a.ev_bucket) SMJ_CHECK(hipEventRecord(a.ev_bucket, st));
     {
-        const uint32_t maxwg = gs_wg_per_cu<W>() * 256;
+        const uint32_t maxwg =
+            (G.pair ? gs_wg_per_cu<W, true>() : gs_wg_per_cu<W, false>()) * 256;
         const uint32_t nwg = groupsort_grid(ngroups, maxwg, G.per);
         TraceScope ts(ws, "k_groupsort", st);
         launch_groupsort<Lay>(ws, group_tpl(nmax, nb, a.nseg, tsz), nwg, st, G);
@@ -2336,6 +2344,7 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
     }
     set_pass_attrs<LayTup>();
     if (a.host_plan && a.seg_start[0] && a.part_flag) {
+        if (a.p32) return bucket_sort_nosync<LayP32>(ws, a, st);
         if (a.p48) return bucket_sort_nosync<LayP48>(ws, a, st);
 #ifdef KEY_8B
         if (a.packed) return bucket_sort_nosync<LayPacked>(ws, a, st);

@@ -302,6 +302,9 @@ static bool use_packing(const Workspace* ws) { return !(ws->layouts_off & SMJ_LA
 // 48 - s1 bits
 static bool use_p48(const Workspace* ws) { return !(ws->layouts_off & SMJ_LAYOUT_NO_P48); }
 
+// ... and 32-bit words before those (LayP32) where the payloads are tiny
+static bool use_p32(const Workspace* ws) { return !(ws->layouts_off & SMJ_LAYOUT_NO_P32); }
+
 // Sort of one relation (nrel 1) or sort + merge-join count of two (nrel 2):
 // range plan -> sampled level-1 partition -> tile pass -> group pass.  The
 // plan must be known on the host (no mid-pipeline synchronisation, and 16-byte
@@ -407,14 +410,24 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
     // and partition a second time, so the join starts with 64-bit words (the
     // 1024M x 1024M join: 2^9 partitions leave 27 payload bits).
     const bool p48_fits = hplan.s1 >= 1 && hplan.s1 <= 32 && hplan.span < (1ull << (48 - hplan.s1));
-    auto first_mode = [&]() {
+    const uint64_t shape = ((uint64_t)nrel << 62) ^ ns[0] ^ (nrel > 1 ? ns[1] << 31 : 0);
+    // 48-bit words, whatever their payloads
+    auto p48_ok = [&]() {
 #ifdef KEY_8B
-        if (can_pack && use_p48(ws) && p48_fits && nb <= 512) return -1;
+        return can_pack && use_p48(ws) && nb <= 512;
 #else
-        if (sampled && plan_on_host && use_packing(ws) && use_p48(ws) &&
-            LayP48::usable(hplan) && p48_fits && nb <= 512)
-            return -1;
+        return sampled && plan_on_host && use_packing(ws) && use_p48(ws) &&
+               LayP48::usable(hplan) && nb <= 512;
 #endif
+    };
+    // 32-bit words (mode -2) are tried first: nothing tells the payloads'
+    // width beforehand, and a shape whose payloads did not fit does not try
+    // them again (p32_fail_shape)
+    auto first_mode = [&]() {
+        if (sampled && plan_on_host && use_packing(ws) && use_p32(ws) &&
+            LayP32::usable(hplan) && ws->p32_fail_shape != shape)
+            return -2;
+        if (p48_ok() && p48_fits) return -1;
         return can_pack ? 0 : (sampled ? 1 : 2);
     };
     // The layout hint of the workspace: when the last call of the same shape
@@ -423,7 +436,6 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
     // reached -- its partition would only be repeated -- and re-probe from the
     // top every 16th call.  Data-dependent like the fallback it skips; the
     // results are the same in every layout.
-    const uint64_t shape = ((uint64_t)nrel << 62) ^ ns[0] ^ (nrel > 1 ? ns[1] << 31 : 0);
     bool hinted = false;
     auto hinted_mode = [&](int m) {
         hinted = false;
@@ -439,6 +451,7 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
     int payload_fb = -2;  // the mode a payload flag sent this call to
     while (mode <= 2) {
         if (mode >= 1) tuple_plan();
+        const bool p32 = mode == -2;
         const bool p48 = mode == -1;
         const bool packed = mode <= 0;
         // the status word the tile and group passes exit on (sampled modes)
@@ -473,7 +486,7 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
             } else {
                 sampled_partition(ws, nrel, rels, ns, outs_v, plan, D1, sample, bst, bh, sgs,
                                   sgc, status, st, plan_on_host ? &hplan : nullptr, packed,
-                                  check ? status + 1 : nullptr, pstride[0]);
+                                  check ? status + 1 : nullptr, pstride[0], p32);
             }
         } else {
             for (int r = 0; r < nrel; r++)
@@ -503,6 +516,7 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
         a.host_plan = plan_on_host ? &hplan : nullptr;
         a.packed = packed;
         a.p48 = p48;
+        a.p32 = p32;
         a.pstride[0] = pstride[0];
         a.pstride[1] = pstride[1];
         a.pack_bad = check ? status + 1 : nullptr;
@@ -511,6 +525,21 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
         uint32_t why[2] = {0, 0};
         a.status_out = why;
         if (bucket_sort(ws, a, st)) break;
+        if (mode == -2 && !(guessed && (why[1] & kBadRange))) {
+            // payloads too wide for 32 bits: the narrowest wider words that
+            // hold them; anything else (overflow, a key outside the plan) as
+            // from 64-bit words
+            const bool pay = !why[0] && !(why[1] & kBadRange);
+            if (pay && (why[1] & (kBadPayload | kBadPayload48 | kBadPayload32)))
+                ws->p32_fail_shape = shape;
+            if (pay && !(why[1] & (kBadPayload | kBadPayload48)) && p48_ok())
+                mode = -1;
+            else if (pay && !(why[1] & kBadPayload) && can_pack)
+                mode = 0;
+            else
+                mode = 1;
+            continue;
+        }
         if (mode == -1 && !(guessed && (why[1] & kBadRange))) {
             // payloads too wide for 48 bits only: 64-bit words; anything else
             // (overflow, unpackable) as from 64-bit words
@@ -538,6 +567,8 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
             payload_fb = 1;
         mode++;
     }
+    ws->last_layout = mode == -2 ? SMJ_LAYOUT_USED_P32 : mode == -1 ? SMJ_LAYOUT_USED_P48
+                    : mode == 0 ? SMJ_LAYOUT_USED_WORDS : SMJ_LAYOUT_USED_TUPLES;
     if (payload_fb >= 0) {
         ws->mode_hint = payload_fb;
         ws->hint_shape = shape;
@@ -1710,6 +1741,10 @@ void smj_workspace_destroy(smj_workspace* ws) { delete (Workspace*)ws; }
 
 void smj_workspace_set_layouts(smj_workspace* ws, uint32_t off) {
     ((Workspace*)(ws ? ws : smj_context_workspace()))->layouts_off = off;
+}
+
+int smj_workspace_last_layout(smj_workspace* ws) {
+    return ((Workspace*)(ws ? ws : smj_context_workspace()))->last_layout;
 }
 
 void smj_dev_partition(smj_workspace* ws, const tuple_t* in, uint64_t n,

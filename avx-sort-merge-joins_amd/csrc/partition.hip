@@ -1355,6 +1355,17 @@ struct ScatterGeom {
     }
 };
 
+// whether a Pack stores whole 16-byte segments with one store (store4)
+template <class P, class = void>
+struct requires_quads : std::false_type {};
+template <class P>
+struct requires_quads<P, std::void_t<decltype(P::kQuads)>> : std::true_type {};
+template <class Pack>
+constexpr bool pack_quads() {
+    if constexpr (requires_quads<Pack>::value) return Pack::kQuads;
+    else return false;
+}
+
 // VEC (8-byte tuples, ITEMS even): item pair (2p, 2p+1) of a thread is one
 // 16-byte load of two adjacent tuples -- the order inside a partition is free
 // here, so the pairing needs no transpose
@@ -1492,7 +1503,27 @@ k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
         // ---- whole segments: SEG consecutive lanes per segment, element e of
         // a partition = carry (e < kc) or its staged tuples (pair stores:
         // SEG / 2 lanes, two adjacent elements each)
-        if constexpr (Pack::kPairs) {
+        if constexpr (pack_quads<Pack>() && SEG == 4) {
+            // a whole segment a lane: one 16-byte store (LayP32)
+            for (uint32_t sg = threadIdx.x; sg < nseg; sg += THREADS) {
+                const uint32_t d = segown[sg];
+                const uint32_t e = (sg - segpre[d]) * SEG;
+                const uint32_t k = kc[d];
+                const uint64_t p = pos[d];
+                OutT x[4];
+#pragma unroll
+                for (uint32_t i = 0; i < 4; i++)
+                    x[i] = e + i < k ? carry[d * SEG + e + i] : stage[tstart[d] + e + i - k];
+                if (p != ~0ull) {
+                    if ((p & 3) == 0) {
+                        Pack::store4(out, ostride, p + e, x);
+                    } else {  // after an odd flush of a workgroup sharing the cursor
+#pragma unroll
+                        for (uint32_t i = 0; i < 4; i++) Pack::store(out, ostride, p + e + i, x[i]);
+                    }
+                }
+            }
+        } else if constexpr (Pack::kPairs) {
             constexpr uint32_t PS = SEG / 2;
             for (uint32_t q = threadIdx.x; q < nseg * PS; q += THREADS) {
                 const uint32_t sg = q / PS;
@@ -2031,7 +2062,7 @@ static void sampled_scatter(Workspace* ws, const Tup* in, uint64_t n, void* out,
         abort();
     }
     constexpr int BIG = sizeof(Tup) == 16
-        ? (sizeof(typename Pack::OutT) == 8 ? SMJ_SC_ITEMS16P : SMJ_SC_ITEMS16)
+        ? (sizeof(typename Pack::OutT) <= 8 ? SMJ_SC_ITEMS16P : SMJ_SC_ITEMS16)
         : SMJ_SC_ITEMS8;
     constexpr int SMALL = sizeof(Tup) == 16 ? 4 : 8;
     if (sampled_scatter_t<BIG>(ws, in, n, out, ostride, dig, nbins, cursor, cap_end, pk,
@@ -2050,13 +2081,17 @@ void sampled_partition(Workspace* ws, int nrel, const Tup* const* in, const uint
                        int64_t* const* hist_out, uint64_t* const* seg_start,
                        int64_t* const* seg_cnt, unsigned int* flag_dev, hipStream_t st,
                        const RangePlan* host_plan, bool packed, unsigned int* bad,
-                       uint64_t p48_stride) {
+                       uint64_t p48_stride, bool p32) {
     PlanDigit1 dig{plan_dev};
     const uint32_t nbins = 1u << dbits;
 #ifndef KEY_8B
-    // 8-byte tuples: no 64-bit packed words, but 48-bit ones (LayP48)
-    packed = p48_stride != 0;
+    // 8-byte tuples: no 64-bit packed words, but 48- and 32-bit ones
+    packed = p48_stride != 0 || p32;
 #endif
+    if (p32 && (p48_stride || !packed)) {
+        fprintf(stderr, "[ERROR] smj: the 32-bit layout is a packed one-plane layout\n");
+        abort();
+    }
     // p48_stride > 0: 48-bit words in two planes of that many elements (LayP48)
     if (p48_stride && !packed) {
         fprintf(stderr, "[ERROR] smj: the 48-bit layout is a packed layout\n");
@@ -2106,10 +2141,20 @@ void sampled_partition(Workspace* ws, int nrel, const Tup* const* in, const uint
         // regions aligned to 128 bytes of the first plane (LayP48: 32
         // elements, so the hi plane's regions start on 64 bytes)
         hipLaunchKernelGGL(k_regions, dim3(nrel), dim3(256), 0, st, R, nbins, kSampleStride,
-                           kRegionSlack, p48_stride ? 4u : packed ? 8u : (uint32_t)sizeof(Tup));
+                           kRegionSlack,
+                           p48_stride || p32 ? 4u : packed ? 8u : (uint32_t)sizeof(Tup));
     }
     for (int r = 0; r < nrel; r++) {
         if (!n[r]) continue;
+        if (p32) {
+            LayP32::Pack pk;
+            pk.bu = key_u(host_plan->base);
+            pk.span = host_plan->span;
+            pk.s1 = host_plan->s1;
+            sampled_scatter(ws, in[r], n[r], out[r], 0, dig, nbins, R.cursor[r], R.cap_end[r],
+                            pk, bad, st);
+            continue;
+        }
         if (p48_stride) {
             LayP48::Pack pk;
             pk.bu = key_u(host_plan->base);

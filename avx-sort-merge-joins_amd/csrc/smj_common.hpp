@@ -213,6 +213,7 @@ struct RefDigit {
 constexpr uint32_t kBadPayload = 1;  // a payload does not fit a packed word
 constexpr uint32_t kBadRange = 2;    // a key lies outside the plan range
 constexpr uint32_t kBadPayload48 = 4;  // ... fits a 64-bit word, not a 48-bit one
+constexpr uint32_t kBadPayload32 = 8;  // ... fits a 48-bit word, not a 32-bit one
 
 struct RangePlan {
     int64_t base;     // smallest key of the range
@@ -547,6 +548,159 @@ struct LayP48 {
         }
     };
     __host__ static bool usable(const RangePlan& P) { return P.s1 >= 1 && P.s1 <= 32; }
+};
+
+// LayP32 (round 5, both tuple widths): the packed word cut to 32 bits, one
+// plane, W = uint32_t in registers and LDS as well:
+//     w = (rel mod 2^s1) << (32 - s1)  |  payload        (payload < 2^(32 - s1))
+// It holds where the payloads are tiny -- the sort benchmark's relation
+// (create_relation_pk: keys 1..N, payload 0, BASELINE configs[1]) -- and
+// moves 4 bytes an element through the intermediate passes instead of 6; its
+// tiles hold 32768 elements.  The partition flags kBadPayload32 when a
+// payload needs more bits (with kBadPayload48 / kBadPayload as for the wider
+// words), and the call reruns in the next wider layout.
+// views of a LayP32 buffer: global pointers (loads through them stay
+// global_load), elements read by value
+struct P32CView {
+    G32c p;
+    __device__ __forceinline__ uint32_t operator[](uint64_t i) const { return p[i]; }
+    __device__ __forceinline__ P32CView operator+(uint64_t k) const { return P32CView{p + k}; }
+};
+struct P32View {
+    G32 p;
+    __device__ __forceinline__ uint32_t operator[](uint64_t i) const { return p[i]; }
+    __device__ __forceinline__ P32View operator+(uint64_t k) const { return P32View{p + k}; }
+};
+__device__ __forceinline__ void st_w(const P32View& v, uint32_t x) {
+#if SMJ_NT_STORES
+    __builtin_nontemporal_store(x, v.p);
+#else
+    v.p[0] = x;
+#endif
+}
+
+struct LayP32 {
+    typedef uint32_t W;
+    static constexpr bool packed = true;
+    typedef P32CView CView;
+    typedef P32View View;
+    __device__ static __forceinline__ CView cview(const void* b, uint64_t) {
+        return CView{(G32c) static_cast<const uint32_t*>(b)};
+    }
+    __device__ static __forceinline__ View view(void* b, uint64_t) {
+        return View{(G32) static_cast<uint32_t*>(b)};
+    }
+    __device__ static __forceinline__ uint64_t rel(const RangePlan& P, const W& w, uint32_t b) {
+        return ((uint64_t)b << P.s1) | (uint64_t)(w >> (32 - P.s1));
+    }
+    __device__ static __forceinline__ bool clamped(const RangePlan&, const W&) { return false; }
+    __device__ static __forceinline__ bool less(const W& a, const W& b) { return a < b; }
+    __device__ static __forceinline__ uint64_t same_key_id(const W& w) { return w; }
+    __device__ static __forceinline__ uint32_t digit_fast(const W& w, uint32_t, uint32_t s1,
+                                                          uint32_t sh, uint32_t mask) {
+        return (w >> (32 - s1 + sh)) & mask;
+    }
+    __host__ static bool fast_ok(const RangePlan& P, uint32_t sh, uint32_t width) {
+        return sh + width <= P.s1;
+    }
+    __device__ static __forceinline__ Tup unpack(const RangePlan& P, const W& w, uint32_t b) {
+        const uint32_t pay = w & (0xffffffffu >> P.s1);
+        const int64_t key = (int64_t)((key_u(P.base) + rel(P, w, b)) ^ 0x8000000000000000ull);
+#ifdef KEY_8B
+        Tup t;
+        t.payload = (int64_t)pay;
+        t.key = key;
+        return t;
+#else
+        return ((uint64_t)(uint32_t)key << 32) | pay;
+#endif
+    }
+    struct FastDigit {
+        uint32_t tsh, mask;
+        __device__ FastDigit(const RangePlan& P, uint32_t s, uint32_t width)
+            : tsh(32 - P.s1 + s), mask((1u << width) - 1) {}
+        __device__ __forceinline__ uint32_t operator()(const W& w) const {
+            return (w >> tsh) & mask;
+        }
+    };
+    struct Unpack {
+        uint64_t kbu;
+        uint32_t pmask, sh;
+        __device__ Unpack(const RangePlan& P, uint32_t b)
+            : kbu(key_u(P.base) + ((uint64_t)b << P.s1)), pmask(0xffffffffu >> P.s1),
+              sh(32 - P.s1) {}
+        __device__ __forceinline__ Tup operator()(const W& w) const {
+#ifdef KEY_8B
+            Tup t;
+            t.payload = (int64_t)(w & pmask);
+            t.key = (int64_t)((kbu + (w >> sh)) ^ 0x8000000000000000ull);
+            return t;
+#else
+            const uint32_t key = (uint32_t)kbu + (w >> sh);
+            return ((uint64_t)key << 32) | (w & pmask);
+#endif
+        }
+    };
+    struct Pack {
+        typedef uint32_t OutT;
+        uint64_t bu, span;
+        uint32_t s1;
+        __device__ __forceinline__ uint32_t operator()(const Tup& t, uint32_t& bad) const {
+            const uint64_t ku = key_u(tup_key(t));
+            const uint64_t r = ku - bu;
+#ifdef KEY_8B
+            const uint64_t pay = (uint64_t)t.payload;
+#else
+            const uint64_t pay = (uint32_t)t;  // unsigned, as the 8-byte order takes it
+#endif
+            bad |= (ku < bu || r > span) ? kBadRange : 0u;
+            bad |= (pay >> (64 - s1)) != 0 ? kBadPayload : 0u;
+            bad |= (pay >> (48 - s1)) != 0 ? kBadPayload48 : 0u;
+            bad |= (pay >> (32 - s1)) != 0 ? kBadPayload32 : 0u;
+            return ((uint32_t)r << (32 - s1)) | ((uint32_t)pay & (0xffffffffu >> s1));
+        }
+        static constexpr uint32_t kStoreBytes = 4;
+        __device__ static __forceinline__ void store(void* out, uint64_t, uint64_t i, uint32_t x) {
+#if SMJ_NT_STORES
+            __builtin_nontemporal_store(x, (G32) static_cast<uint32_t*>(out) + i);
+#else
+            ((G32) static_cast<uint32_t*>(out))[i] = x;
+#endif
+        }
+        // a whole 16-byte segment (i a multiple of 4) with one store
+#ifndef SMJ_P32_QUADS
+#define SMJ_P32_QUADS 1
+#endif
+        static constexpr bool kQuads = SMJ_P32_QUADS;
+        __device__ static __forceinline__ void store4(void* out, uint64_t, uint64_t i,
+                                                      const uint32_t (&x)[4]) {
+            typedef uint32_t U4 __attribute__((ext_vector_type(4)));
+            const U4 v = {x[0], x[1], x[2], x[3]};
+            __attribute__((address_space(1))) U4* p =
+                (__attribute__((address_space(1))) U4*)(static_cast<uint32_t*>(out) + i);
+#if SMJ_NT_STORES
+            __builtin_nontemporal_store(v, p);
+#else
+            *p = v;
+#endif
+        }
+        // elements i and i + 1 (i even) with one 8-byte store
+        static constexpr bool kPairs = true;
+        __device__ static __forceinline__ void store2(void* out, uint64_t, uint64_t i, uint32_t x0,
+                                                      uint32_t x1) {
+            typedef uint32_t U2 __attribute__((ext_vector_type(2)));
+            const U2 v = {x0, x1};
+            __attribute__((address_space(1))) U2* p =
+                (__attribute__((address_space(1))) U2*)(static_cast<uint32_t*>(out) + i);
+#if SMJ_NT_STORES
+            __builtin_nontemporal_store(v, p);
+#else
+            *p = v;
+#endif
+        }
+    };
+    // s1 key bits and at least one payload bit
+    __host__ static bool usable(const RangePlan& P) { return P.s1 >= 1 && P.s1 <= 31; }
 };
 
 // identity "packing" of the plain layout

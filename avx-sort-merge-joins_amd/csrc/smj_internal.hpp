@@ -74,6 +74,11 @@ struct Workspace {
     int mode_hint = -2;
     uint64_t hint_shape = 0;
     uint32_t hint_calls = 0;
+    // the shape of the last call whose payloads did not fit 32-bit words: the
+    // next calls of that shape start at the wider layouts (no re-probe; the
+    // 32-bit words are for relations with tiny payloads, e.g. the sort's)
+    uint64_t p32_fail_shape = ~0ull;
+    int last_layout = -1;  // smj_workspace_last_layout (SMJ_LAYOUT_USED_*)
     std::map<std::string, std::pair<void*, size_t>> bufs;
     std::map<std::string, std::pair<void*, size_t>> pinned;
     // the k-way merge's run table as last uploaded, and where (a repeated
@@ -305,7 +310,8 @@ void sampled_partition(Workspace* ws, int nrel, const Tup* const* in, const uint
                        int64_t* const* hist_out, uint64_t* const* seg_start,
                        int64_t* const* seg_cnt, unsigned int* flag_dev, hipStream_t st,
                        const RangePlan* host_plan = nullptr, bool packed = false,
-                       unsigned int* bad = nullptr, uint64_t p48_stride = 0);
+                       unsigned int* bad = nullptr, uint64_t p48_stride = 0,
+                       bool p32 = false);
 void hist_memcpy(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
                  uint32_t dbits, hipStream_t st);
 // lane order of LDS atomic returns (k_scatter_swp's ranks): violations, 0 expected
@@ -342,6 +348,7 @@ struct BucketSortArgs {
     // elements each (lo uint32, then hi uint16)
     bool p48 = false;
     uint64_t pstride[2] = {0, 0};
+    bool p32 = false;  // part/tmp hold LayP32 words (packed too, one plane)
     // optional 4-word block zeroed by the caller: [0] = part_flag, [1] =
     // pack_bad, [2] = the skew queue length (read back in one copy)
     unsigned int* status = nullptr;

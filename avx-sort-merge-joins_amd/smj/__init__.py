@@ -67,7 +67,7 @@ DEVICE_SYMBOLS = [
     "smj_dev_join_segmented_planes", "smj_mgpu_join", "smj_mgpu_release",
     "smj_inregister_sort_keyval32", "smj_workspace_set_layouts", "smj_mgpu_unique_id",
     "smj_mgpu_comm_init", "smj_mgpu_rank_join", "smj_mgpu_comm_destroy", "smj_mgpu_rank_sorted",
-    "smj_mgpu_comm_workspace",
+    "smj_mgpu_comm_workspace", "smj_workspace_last_layout",
 ]
 
 
@@ -110,6 +110,9 @@ class MgpuStats(C.Structure):
 
 # smj_workspace_set_layouts bits (include/smj.h)
 LAYOUT_NO_P48, LAYOUT_NO_PACKED, LAYOUT_NO_SAMPLED, LAYOUT_SAMPLE_PLAN = 1, 2, 4, 8
+LAYOUT_NO_P32 = 16
+# smj_workspace_last_layout values
+LAYOUTS_USED = ("tuples", "words", "p48", "p32")
 # smj_mgpu_join flags (include/smj.h)
 MG_COPY, MG_NOPLANES, MG_ONECALL, MG_SAMPLED, MG_EXACT = 1, 2, 4, 8, 16
 MG_LAYOUTS = ("tuples", "words", "planes")
@@ -268,13 +271,21 @@ class Library:
             "smj_mgpu_comm_workspace": (_P, [_P]),
             "smj_inregister_sort_keyval32": (None, [_P, _P, _U64]),
             "smj_workspace_set_layouts": (None, [_P, _U32]),
+            "smj_workspace_last_layout": (C.c_int, [_P]),
             "smj_trace_enable": (None, [_P, C.c_int]),
             "smj_trace_reset": (None, [_P]),
             "smj_trace_only": (None, [_P, C.c_char_p]),
             "smj_trace_read": (C.c_int, [_P, C.c_char_p, C.c_int, _P, _P, C.c_int]),
         }
         for name, (res, args) in sig.items():
-            f = getattr(L, name)
+            try:
+                f = getattr(L, name)
+            except AttributeError:
+                # an older build loaded for an A/B (SMJ_LIB_DIR): its missing
+                # entry points stay unbound; the shipped library has them all
+                if os.environ.get("SMJ_LIB_DIR"):
+                    continue
+                raise
             f.restype = res
             f.argtypes = args
         got = L.smj_tuple_bytes()
@@ -509,6 +520,25 @@ class Library:
         """smj_workspace_set_layouts on this Library's workspace (LAYOUT_*
         bits: layouts its device sorts and joins may not use; 0 = all)."""
         self.lib.smj_workspace_set_layouts(self.ws, off)
+
+    def reset_workspace(self):
+        """Destroy this Library's workspace (its scratch and its remembered
+        layouts); the next device call creates a fresh one."""
+        if self._ws is not None:
+            import torch
+            torch.cuda.synchronize()
+            self.lib.smj_workspace_destroy(self._ws)
+            self._ws = None
+
+    def last_layout(self, api: bool = False) -> str:
+        """The intermediate layout the last device sort or join finished in
+        (smj_workspace_last_layout): on this Library's workspace, or (api)
+        on the calling thread's, which the reference-named entries use."""
+        f = getattr(self.lib, "smj_workspace_last_layout", None)
+        if f is None or f.restype is not C.c_int:  # an older A/B build
+            return "unknown"
+        k = f(None if api else self.ws)
+        return LAYOUTS_USED[k] if k >= 0 else "none"
 
     @staticmethod
     def stream_ptr():

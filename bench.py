@@ -482,6 +482,9 @@ def main():
             dj.stats_reset()
 
     elapsed, kern, brk = timed_loop(a, tracer, dist, step, reset)
+    # the intermediate layout the last step ran in (the 1-GPU join: p48 for
+    # row-id payloads, words or tuples for wider ones)
+    layout = None if exchange else lib.last_layout(api=a.api)
     if a.api and not exchange:
         count.fill_(api_count[0])
 
@@ -586,6 +589,7 @@ def main():
             # untimed steps, every kernel traced (timed_loop)
             "kernels_ms_per_step": {k: round(v[0], 4) for k, v in brk.items()},
             "device": lib.lib.smj_device_name().decode(),
+            "intermediate_layout": layout,
             "exchange": xchg,
         },
     }
@@ -848,6 +852,7 @@ def run_op(a, lib, json_out, dist, N, rank):
             lib.dev_partition(R, out, a.bits, a.shift, True, hist, off)
     torch.cuda.synchronize()
     elapsed, kern, brk = timed_loop(a, lib, dist, step)
+    layout = lib.last_layout() if a.op == "sort" else None
     chk = None
     if a.no_check:
         ok = True
@@ -910,6 +915,7 @@ def run_op(a, lib, json_out, dist, N, rank):
             # untimed steps, every kernel traced (timed_loop)
             "kernels_ms_per_step": {k: round(v[0], 4) for k, v in brk.items()},
             "device": lib.lib.smj_device_name().decode(),
+            "intermediate_layout": layout,
         },
     }
     print(json.dumps(out_line), file=json_out, flush=True)

@@ -686,3 +686,75 @@ def test_layout_hint_alternating_payloads(libs, oracles):
         assert int(cnt.item()) == exp, kind
         assert np.array_equal(lib.to_host(sR), eR), kind
         assert np.array_equal(lib.to_host(sS), eS), kind
+
+
+# ------------------------------------------------- 32-bit words (LayP32)
+@pytest.mark.parametrize("case", ["pk", "tiny", "wide", "negative"])
+def test_sort_p32_words(libs, oracles, width, case):
+    """Sorts whose payloads fit 32 - s1 bits (the sort benchmark's payload 0)
+    carry 32-bit words through the intermediate passes (LayP32); a wider
+    payload sends the call to the next layout that holds it (48-bit words,
+    or tuples for a negative 16-byte payload), and later calls of that shape
+    start there.  The result is the oracle's on every path."""
+    import torch
+    orc, lib = oracles[width], libs[width]
+    n = (1 << 20) + 77
+    orc.seed(4242)
+    t = orc.create_relation_pk(n)  # payload 0
+    rng = np.random.default_rng(7)
+    if case == "tiny":
+        t["payload"] = rng.integers(0, 16, n)
+    elif case == "wide":
+        t["payload"][n // 3] = 1 << 28
+    elif case == "negative":
+        t["payload"][5] = -1
+    want = {"pk": "p32", "tiny": "p32", "wide": "p48",
+            "negative": "p48" if width == 8 else "tuples"}[case]
+    exp = orc.sort(t)
+    lib.reset_workspace()  # no layout remembered
+    d = lib.to_device(t)
+    out = lib.empty(n)
+    for call in range(2):
+        lib.dev_sort(d, out)
+        torch.cuda.synchronize()
+        assert np.array_equal(lib.to_host(out), exp), (case, call)
+        assert lib.last_layout() == want, (case, call, lib.last_layout())
+    if case != "pk":
+        # the shape that failed 32-bit words does not try them again, a new
+        # shape does
+        t2 = t[:n - 1].copy()
+        t2["payload"] = 0
+        d2, o2 = lib.to_device(t2), lib.empty(n - 1)
+        lib.dev_sort(d2, o2)
+        torch.cuda.synchronize()
+        assert np.array_equal(lib.to_host(o2), orc.sort(t2))
+        assert lib.last_layout() == "p32"
+    import smj
+    lib.set_layouts(smj.LAYOUT_NO_P32)
+    lib.dev_sort(d, out)
+    torch.cuda.synchronize()
+    assert np.array_equal(lib.to_host(out), exp)
+    assert lib.last_layout() != "p32"
+    lib.set_layouts(0)
+
+
+@pytest.mark.parametrize("n", [300_000, 4_000_000])
+def test_join_p32_words(libs, oracles, width, n):
+    """A join whose row-id payloads fit 32 - s1 bits (300K tuples: s1 = 11
+    at 2^8 buckets) runs on 32-bit words; at 4M they do not and the join
+    takes the 48-bit words.  Count and sorted relations as the oracle's."""
+    import torch
+    orc, lib = oracles[width], libs[width]
+    R, S = make_join_inputs(orc, width, "pk_fk", n, n)
+    exp, eR, eS = orc.sortmergejoin(R, S)
+    lib.reset_workspace()
+    dR, dS = lib.to_device(R), lib.to_device(S)
+    sR, sS = lib.empty(n), lib.empty(n)
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    for call in range(2):
+        lib.dev_join(dR, dS, sR, sS, cnt, 8, 1, n)
+        torch.cuda.synchronize()
+        assert int(cnt.item()) == exp
+        assert np.array_equal(lib.to_host(sR), eR)
+        assert np.array_equal(lib.to_host(sS), eS)
+        assert lib.last_layout() == ("p32" if n < 1_000_000 else "p48"), (call, lib.last_layout())
