@@ -1798,10 +1798,11 @@ template <class Lay>
 static void skew_path(Workspace* ws, const GroupArgs& G, OvfEntry* ovf, uint32_t no,
                       const uint64_t* hdst, uint32_t nb, hipStream_t st) {
     const int nrel = G.nrel;
-    std::vector<OvfEntry> he(no);
-    SMJ_CHECK(hipMemcpyAsync(he.data(), ovf, no * sizeof(OvfEntry),
-                             hipMemcpyDeviceToHost, st));
-    SMJ_CHECK(hipStreamSynchronize(st));
+    // pinned host copies (a pageable destination makes each copy a staged,
+    // blocking transfer)
+    OvfEntry* he = (OvfEntry*)ws->host_pinned("sk_he", (size_t)no * sizeof(OvfEntry));
+    SMJ_CHECK(hipMemcpyAsync(he, ovf, no * sizeof(OvfEntry), hipMemcpyDeviceToHost, st));
+    ws->wait_stream(st);
     // small groups: one workgroup each; large ones: work items over their runs
     std::vector<uint32_t> small, large, lslot;
     std::vector<uint4> items;
@@ -1877,11 +1878,10 @@ static void skew_path(Workspace* ws, const GroupArgs& G, OvfEntry* ovf, uint32_t
         hipLaunchKernelGGL(k_skew_check, dim3(ni), dim3(SK_THREADS), 0, st, K);
     }
     SMJ_CHECK(hipGetLastError());
-    std::vector<uint32_t> flags(no, 0);
-    SMJ_CHECK(hipMemcpyAsync(flags.data(), gflag, (size_t)no * 4, hipMemcpyDeviceToHost, st));
-    SMJ_CHECK(hipMemcpyAsync(he.data(), ovf, no * sizeof(OvfEntry),
-                             hipMemcpyDeviceToHost, st));
-    SMJ_CHECK(hipStreamSynchronize(st));
+    uint32_t* flags = (uint32_t*)ws->host_pinned("sk_flags", (size_t)no * 4);
+    SMJ_CHECK(hipMemcpyAsync(flags, gflag, (size_t)no * 4, hipMemcpyDeviceToHost, st));
+    SMJ_CHECK(hipMemcpyAsync(he, ovf, no * sizeof(OvfEntry), hipMemcpyDeviceToHost, st));
+    ws->wait_stream(st);
     // what the device could not finish
     std::vector<uint32_t> rest;
     for (uint32_t i = 0; i < no; i++)
@@ -2323,11 +2323,11 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
         fprintf(stderr, "[ERROR] smj: overflow table too small\n");
         abort();
     }
-    std::vector<uint64_t> hdst((size_t)2 * nb);
+    uint64_t* hdst = (uint64_t*)ws->host_pinned("sk_hdst", (size_t)2 * nb * 8);
     for (int r = 0; r < nrel; r++)
-        SMJ_CHECK(hipMemcpyAsync(hdst.data() + (size_t)r * nb, ostart[r], (size_t)nb * 8,
+        SMJ_CHECK(hipMemcpyAsync(hdst + (size_t)r * nb, ostart[r], (size_t)nb * 8,
                                  hipMemcpyDeviceToHost, st));
-    skew_path<Lay>(ws, G, ovf, no, hdst.data(), nb, st);
+    skew_path<Lay>(ws, G, ovf, no, hdst, nb, st);
     SMJ_CHECK(hipGetLastError());
     return true;
 }
