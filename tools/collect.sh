@@ -16,7 +16,8 @@ for d in "$I" "$I/nopmc"; do
     [ -f "$f" ] || continue
     n=$(basename "$f" _noprof.json)
     t=$n
-    [ "$d" = "$I/nopmc" ] && [ -f "$I/${n}_noprof.json" ] && t=${n}b  # a second line of a config
+    # a second line of a config (the unprofiled pass of a later call): keep the first
+    [ "$d" = "$I/nopmc" ] && { [ -f "$I/${n}_noprof.json" ] || [ -f "$P/${R}_${n}_noprof.json" ]; } && t=${n}b
     cp "$f" "$P/${R}_${t}_noprof.json"
     [ -f "$d/$n.json" ] && cp "$d/$n.json" "$P/${R}_$t.json"
     s=$(stats "$d/trace_$n"); [ -n "$s" ] && cp "$s" "$P/${R}_${t}_kernel_stats.csv"
