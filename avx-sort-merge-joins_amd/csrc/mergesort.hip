@@ -428,7 +428,10 @@ void segmented_sort(Workspace* ws, Tup* data, const uint64_t* seg_off,
 //                 off[i][b] = first element of run i in bucket >= b (k x (B+1)
 //                 binary searches, no data pass; a streaming pass that wrote
 //                 the boundaries where consecutive buckets differ measured
-//                 slower: 0.76 against 0.57 ms for 64 runs of 2M);
+//                 slower: 0.76 against 0.57 ms for 64 runs of 2M; the two
+//                 searches of a slice done by the merge's own workgroups,
+//                 round 5, took the merge 0.026 -> 0.066 ms: each workgroup
+//                 waits for a chain of dependent loads);
 //   k_km_merge  : one workgroup per bucket sums its slice starts (= its place
 //                 in the output: no size / scan kernels), gathers its k slices with
 //                 coalesced loads (all in flight), counting-sorts them in LDS
@@ -436,9 +439,11 @@ void segmented_sort(Workspace* ws, Tup* data, const uint64_t* seg_off,
 //                 exact key when the bucket spans <= 4096 keys), fixes the
 //                 equal-digit runs on the full (key, payload) order and writes
 //                 the bucket to its place in the output in one stream.
-// Traffic: each tuple read once and written once (2w).  A bucket larger than
-// LDS (a hot key) or a long unsorted equal-digit run flags the merge, which
-// then runs as the merge-path tree.
+// Traffic: each tuple read once and written once (2w).  A long unsorted
+// equal-digit run is sorted in LDS (bitonic, on the full order); a bucket
+// larger than LDS (a hot key) is queued for k_km_over, which ranks its
+// elements by binary searches across the runs' slices (round 5: no host
+// decision, so the merge needs no host synchronisation).
 constexpr int KM_THREADS = 256;
 constexpr uint32_t KM_CAP = sizeof(Tup) == 8 ? 4096 : 2048;  // bucket capacity (32 KB)
 constexpr uint32_t KM_IPT = KM_CAP / KM_THREADS;
@@ -497,14 +502,14 @@ __device__ __forceinline__ uint32_t km_shift(uint64_t lo, uint64_t hi, uint32_t 
 // the key range for k_km_merge.
 __global__ void __launch_bounds__(KM_THREADS)
 k_km_bounds(const KmRun* __restrict__ runs, uint32_t k, uint32_t D,
-            unsigned long long* __restrict__ mm, uint32_t* __restrict__ off) {
+            unsigned long long* __restrict__ mm, uint32_t* __restrict__ off,
+            unsigned int* __restrict__ queue) {
     uint64_t minu, maxu;
     km_range(runs, k, minu, maxu);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         mm[0] = minu;
         mm[1] = maxu;
-        mm[2] = 0;  // k_km_merge's flags (it runs after this kernel)
-        mm[3] = 0;
+        queue[0] = 0;  // k_km_merge's overflow queue (it runs after this kernel)
     }
     const uint32_t B = 1u << D;
     const uint64_t idx = (uint64_t)blockIdx.x * KM_THREADS + threadIdx.x;
@@ -528,10 +533,47 @@ k_km_bounds(const KmRun* __restrict__ runs, uint32_t k, uint32_t D,
     off[idx] = (uint32_t)pos;
 }
 
+// sort buf[0, total) in LDS on the full order (bitonic over the next power of
+// two, the tail filled with the largest tuple): the rare bucket with a long
+// equal-digit run out of order
+__device__ __forceinline__ Tup km_max_tup() {
+#ifdef KEY_8B
+    Tup t;
+    t.key = INT64_MAX;
+    t.payload = INT64_MAX;
+    return t;
+#else
+    return (Tup)INT64_MAX;
+#endif
+}
+__device__ void km_bitonic(Tup* buf, uint32_t total) {
+    uint32_t n = 1;
+    while (n < total) n <<= 1;
+    for (uint32_t i = total + threadIdx.x; i < n; i += KM_THREADS) buf[i] = km_max_tup();
+    __syncthreads();
+    for (uint32_t k = 2; k <= n; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = threadIdx.x; i < n; i += KM_THREADS) {
+                const uint32_t l = i ^ j;
+                if (l > i) {
+                    const Tup a = buf[i], c = buf[l];
+                    const bool up = (i & k) == 0;
+                    if (up ? tup_less(c, a) : tup_less(a, c)) {
+                        buf[i] = c;
+                        buf[l] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
 __global__ void __launch_bounds__(KM_THREADS)
 k_km_merge(const KmRun* __restrict__ runs, uint32_t k, uint32_t D,
            const unsigned long long* __restrict__ mm, const uint32_t* __restrict__ off,
            unsigned int* __restrict__ flag, Tup* __restrict__ out) {
+    // flag: [0] queued buckets, [2 + q] the q-th (k_km_over)
     __shared__ __attribute__((aligned(16))) Tup buf[KM_CAP];
     __shared__ uint32_t cnt[KM_NB / 2];     // digit histogram, two u16 per word
     __shared__ uint32_t cur[KM_NB / 2];     // placement cursors
@@ -578,8 +620,11 @@ k_km_merge(const KmRun* __restrict__ runs, uint32_t k, uint32_t D,
     }
     const uint32_t total = tot2 & 0x1fffffu;
     if (total == 0) return;  // uniform: an empty bucket
-    if (total > KM_CAP) {    // a bucket larger than LDS: the caller merges another way
-        if (tid == 0) flag[0] = 1u;  // host-mapped: plain stores, every writer stores 1
+    if (total > KM_CAP) {    // a bucket larger than LDS: k_km_over merges it
+        if (tid == 0) {
+            const uint32_t q = atomicAdd(flag, 1u);
+            flag[2 + q] = b;  // the queue (room for every bucket)
+        }
         return;
     }
     if (len) {
@@ -703,18 +748,82 @@ k_km_merge(const KmRun* __restrict__ runs, uint32_t k, uint32_t D,
             ok = true;
             for (uint32_t i = tid + 1; i < total; i += KM_THREADS)
                 ok &= !tup_less(buf[i], buf[i - 1]);
-            if (__syncthreads_or(!ok)) {
-                if (tid == 0) flag[1] = 1u;
-                return;
-            }
+            if (__syncthreads_or(!ok)) km_bitonic(buf, total);  // a long run out of order
         }
     }
     // ---- the bucket, in order, to its place in the output
     for (uint32_t j = tid; j < total; j += KM_THREADS) out[o + j] = buf[j];
 }
 
-// true when the one-pass merge ran; false: a bucket overflowed (or k is
-// outside the one-pass range) and nothing was written
+// Buckets too large for LDS (queued by k_km_merge): every workgroup takes
+// its share of every queued bucket's elements (the queue's length is only
+// known on the device; a hot key can put most of the input in one bucket).
+// Element p of run i's slice goes to its rank among the bucket's elements:
+// its position in its slice plus, in every other slice j, the elements below
+// it (equal ones too when j < i) -- binary searches, no LDS; ties keep run
+// order, so the output is the merged order whatever the tie.
+__global__ void __launch_bounds__(KM_THREADS)
+k_km_over(const KmRun* __restrict__ runs, uint32_t k, uint32_t D,
+          const uint32_t* __restrict__ off, const unsigned int* __restrict__ flag,
+          Tup* __restrict__ out) {
+    __shared__ uint32_t slo[KM_KMAX], sln[KM_KMAX], sst[KM_KMAX];
+    __shared__ uint32_t scr[KM_THREADS / 64 + 1];
+    __shared__ unsigned long long wsum[KM_THREADS / 64];
+    const uint32_t nq = flag[0];
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t q = 0; q < nq; q++) {
+        const uint32_t b = flag[2 + q];
+        uint32_t lo = 0, len = 0;
+        if (tid < k) {
+            const uint32_t* orow = off + (uint64_t)tid * ((1u << D) + 1);
+            lo = orow[b];
+            len = orow[b + 1] - lo;
+        }
+        // the slices' starts in the bucket (block scan) and the bucket's
+        // place in the output: the sum of the slice starts
+        uint32_t total;
+        const uint32_t ex = block_exclusive_scan(len, scr, &total);
+        const unsigned long long ls = wave_sum((unsigned long long)lo);
+        if ((tid & 63) == 0) wsum[tid >> 6] = ls;
+        if (tid < k) {
+            slo[tid] = lo;
+            sln[tid] = len;
+            sst[tid] = ex;
+        }
+        __syncthreads();
+        uint64_t o = 0;
+#pragma unroll
+        for (int w = 0; w < KM_THREADS / 64; w++) o += wsum[w];
+        for (uint32_t e = blockIdx.x * KM_THREADS + tid; e < total; e += gridDim.x * KM_THREADS) {
+            // the slice of e: the last start <= e (binary search over k)
+            uint32_t a = 0, z = k - 1;
+            while (a < z) {
+                const uint32_t m = (a + z + 1) >> 1;
+                if (sst[m] <= e) a = m; else z = m - 1;
+            }
+            while (a + 1 < k && sln[a] == 0) a++;  // (an empty slice shares its start)
+            const uint32_t i = a, p = e - sst[i];
+            const Tup x = ld_g(runs[i].p + slo[i] + p);
+            uint64_t rank = p;
+            for (uint32_t j = 0; j < k; j++) {
+                if (j == i || sln[j] == 0) continue;
+                const Tup* sj = runs[j].p + slo[j];
+                uint32_t l = 0, h = sln[j];
+                while (l < h) {  // j < i: elements <= x; j > i: elements < x
+                    const uint32_t m = (l + h) >> 1;
+                    const Tup y = ld_g(sj + m);
+                    if (j < i ? !tup_less(x, y) : tup_less(y, x)) l = m + 1; else h = m;
+                }
+                rank += l;
+            }
+            out[o + rank] = x;
+        }
+        __syncthreads();
+    }
+}
+
+// true when the one-pass merge ran (queued buckets included); false: k is
+// outside the one-pass range and nothing was written
 static bool multiway_merge_buckets(Workspace* ws, const Tup* const* runs, const uint64_t* lens,
                                    uint32_t k, uint64_t total, Tup* out, hipStream_t st) {
     if (k < 3 || k > KM_KMAX) return false;
@@ -724,19 +833,23 @@ static bool multiway_merge_buckets(Workspace* ws, const Tup* const* runs, const 
     uint32_t D = 0;
     while (D < 24 && (total >> D) > KM_CAP / 2) D++;
     const uint32_t B = 1u << D;
-    // one pinned block, one copy: the key-range / flag words (written by
+    // one pinned block, one copy: the key-range words (written by
     // k_km_bounds), then the runs -- skipped when this workspace uploaded the
-    // same table to the same place last time
+    // same table to the same place last time.  No host synchronisation
+    // follows, so the staging block comes from a ring (its copy has finished
+    // before the block is written again).
     const size_t hdr = 32, bytes = hdr + (size_t)k * sizeof(KmRun);
     unsigned long long* mm = (unsigned long long*)ws->scratch("km_hdr", bytes);
-    unsigned int* flag = (unsigned int*)(mm + 2);
     const KmRun* dr = (const KmRun*)((char*)mm + hdr);
     uint32_t* off = (uint32_t*)ws->scratch("km_off", (size_t)(B + 1) * k * 4);
-    // the pinned block is free again after the synchronisation below
-    unsigned long long* h = (unsigned long long*)ws->host_pinned("km_hdr_h", bytes);
+    // the overflow queue: [0] length (zeroed by k_km_bounds), [2..] bucket
+    // numbers (k_km_merge)
+    unsigned int* q = (unsigned int*)ws->scratch("km_queue", ((size_t)B + 2) * 4);
+    uint32_t slot = 0;
+    unsigned long long* h = (unsigned long long*)ws->ring_acquire("km_hdr_h", bytes, &slot);
     h[0] = ~0ull;
     h[1] = 0;
-    h[2] = 0;  // flag[0]: a bucket overflows; flag[1]: a long unsorted equal-digit run
+    h[2] = 0;
     h[3] = 0;
     KmRun* hr = (KmRun*)((char*)h + hdr);
     for (uint32_t i = 0; i < k; i++) hr[i] = KmRun{runs[i], lens[i]};
@@ -744,6 +857,7 @@ static bool multiway_merge_buckets(Workspace* ws, const Tup* const* runs, const 
     if (ws->km_last_dev != (const void*)mm || ws->km_last.size() != rb ||
         memcmp(ws->km_last.data(), hr, rb) != 0) {
         SMJ_CHECK(hipMemcpyAsync(mm, h, bytes, hipMemcpyHostToDevice, st));
+        ws->ring_release("km_hdr_h", slot, st);
         ws->km_last.assign((const unsigned char*)hr, (const unsigned char*)hr + rb);
         ws->km_last_dev = mm;
     }
@@ -751,27 +865,22 @@ static bool multiway_merge_buckets(Workspace* ws, const Tup* const* runs, const 
     {
         traced_launch(ws, "k_km_bounds", k_km_bounds,
                       dim3((uint32_t)((nb + KM_THREADS - 1) / KM_THREADS)), dim3(KM_THREADS), 0,
-                      st, dr, k, D, mm, off);
+                      st, dr, k, D, mm, off, q);
     }
-    // the flags live in pinned host memory the kernel writes directly, so
-    // the synchronisation needs no copy behind the kernels
-    volatile unsigned int* hflag = (volatile unsigned int*)ws->host_pinned("km_flag", 16);
-    hflag[0] = 0;
-    hflag[1] = 0;
-    unsigned int* dflag = nullptr;
-    SMJ_CHECK(hipHostGetDevicePointer((void**)&dflag, (void*)hflag, 0));
     {
         traced_launch(ws, "k_km_merge", k_km_merge, dim3(B), dim3(KM_THREADS), 0, st, dr, k,
-                      D, mm, off, dflag, out);
+                      D, mm, off, q, out);
     }
+    // the queued buckets (usually none: every workgroup exits at once)
+    hipLaunchKernelGGL(k_km_over, dim3(B < 64 ? B : 64), dim3(KM_THREADS), 0, st, dr, k, D, off,
+                       q, out);
     SMJ_CHECK(hipGetLastError());
-    ws->wait_stream(st);
-    return hflag[0] == 0 && hflag[1] == 0;
+    return true;
 }
 
-// k-way merge: one pass by value buckets (above); otherwise (k > 256, one
-// run, two runs, or a bucket too big for LDS) a tree of 2-way merge-path
-// passes.
+// k-way merge: one pass by value buckets (above; buckets too big for LDS
+// finished by k_km_over); otherwise (k > 256, one run, two runs) a tree of
+// 2-way merge-path passes.
 void multiway_merge(Workspace* ws, const Tup* const* runs, const uint64_t* lens,
                     uint32_t k, Tup* out, hipStream_t st) {
     uint64_t total = 0;

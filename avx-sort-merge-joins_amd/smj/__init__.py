@@ -624,7 +624,7 @@ class Library:
     def dev_multiway_merge(self, runs, out):
         """k-way merge of sorted device runs (list of (n_i, 2) tensors, or a
         run_table of them) into `out` (smj_dev_multiway_merge_host;
-        synchronises the stream)."""
+        stream-ordered, no host synchronisation for 3..256 runs)."""
         ptrs, lens, k, _keep = runs if isinstance(runs, tuple) else self.run_table(runs)
         self.lib.smj_dev_multiway_merge_host(self.ws, ptrs, lens, k, out.data_ptr(),
                                              self.stream_ptr())

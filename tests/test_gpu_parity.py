@@ -244,8 +244,8 @@ def test_multiway_merge(libs, oracles, width, k):
 
 
 def test_multiway_merge_skew_and_large(libs, oracles, width):
-    """One hot key over every run (a value bucket larger than LDS: the merge
-    takes the merge-path tree), keys spanning the whole signed range, empty
+    """One hot key over every run (a value bucket larger than LDS: k_km_over
+    ranks its elements by binary searches), keys spanning the whole signed range, empty
     runs between full ones, and the bench_multiwaymerge shape 64 x 65536."""
     orc, lib = oracles[width], libs[width]
     rng = np.random.default_rng(77)
@@ -262,6 +262,47 @@ def test_multiway_merge_skew_and_large(libs, oracles, width):
         out, n, consumed = lib.avx_multiway_merge(runs)
         assert n == len(exp) and consumed
         assert np.array_equal(out, exp)
+
+
+def test_multiway_merge_long_equal_runs(libs, oracles, width):
+    """A value bucket within LDS whose equal-key run (480 copies of one key
+    across 4 runs, payloads interleaved) is longer than the serial fix
+    handles: the one-pass merge sorts that bucket in LDS (bitonic)."""
+    orc, lib = oracles[width], libs[width]
+    runs = []
+    for i in range(4):
+        t = rand_tuples(width, 3000, 900 + i, 0, 100000)
+        t["key"][:120] = 50000
+        runs.append(orc.sort(t))
+    exp = orc.multiway_merge(runs)
+    out, n, consumed = lib.avx_multiway_merge(runs)
+    assert n == len(exp) and consumed
+    assert np.array_equal(out, exp)
+
+
+def test_dev_multiway_merge_back_to_back(libs, oracles, width):
+    """The device k-way merge does not wait for the stream: merges of
+    different run tables issued back to back (a hot-key bucket past LDS in
+    every other one) all land, each in its own output."""
+    import torch
+    orc, lib = oracles[width], libs[width]
+    cases = []
+    for c in range(6):
+        rng = np.random.default_rng(1000 + c)
+        k = int(rng.integers(3, 80))
+        runs = []
+        for i in range(k):
+            hi = 9 if c % 2 else 1 << 20
+            runs.append(orc.sort(rand_tuples(width, int(rng.integers(0, 2000)), 50 * c + i, 7, hi)))
+        exp = orc.multiway_merge(runs)
+        druns = [lib.to_device(r) for r in runs]
+        out = lib.empty(max(len(exp), 1))
+        cases.append((druns, out, exp))
+    for druns, out, _ in cases:
+        lib.dev_multiway_merge(druns, out)
+    torch.cuda.synchronize()
+    for druns, out, exp in cases:
+        assert np.array_equal(lib.to_host(out)[:len(exp)], exp)
 
 
 # -------------------------------------------------------------------- joins
