@@ -527,7 +527,9 @@ void smj_dev_sort(smj_workspace * ws, const tuple_t * in, uint64_t n,
 void smj_dev_merge2(const tuple_t * a, uint64_t na, const tuple_t * b,
                     uint64_t nb, tuple_t * out, smj_stream_t stream);
 
-/* k-way merge of sorted device runs whose pointers/lengths are host arrays. */
+/* k-way merge of sorted device runs whose pointers/lengths are host arrays.
+ * Stream-ordered: for 3..256 runs no host synchronisation (round 5; the
+ * host arrays may be reused as soon as the call returns). */
 void smj_dev_multiway_merge_host(smj_workspace * ws,
                                  const tuple_t * const * runs,
                                  const uint64_t * lens, uint32_t k,
