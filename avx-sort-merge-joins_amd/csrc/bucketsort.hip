@@ -50,13 +50,6 @@ namespace smj {
 #define SMJ_TP_THREADS 1024
 #endif
 constexpr int TP_THREADS = SMJ_TP_THREADS;
-// group pass: digit-major prefix table (k_preft) and non-temporal gathers
-#ifndef SMJ_PREFT
-#define SMJ_PREFT 1
-#endif
-#ifndef SMJ_GATHER_NT
-#define SMJ_GATHER_NT 0
-#endif
 #ifndef SMJ_GS_XCD
 #define SMJ_GS_XCD 1  // XCD-aware group order in k_groupsort (0: a lab build's contiguous chunks)
 #endif
