@@ -219,12 +219,16 @@ struct TilePassArgs {
     const unsigned int* pack_bad;  // set: the packed partition is void, exit
     uint32_t d2_fast;              // Lay::fast_ok for the level-2 digit (host)
     uint64_t pstride[2] = {0, 0};  // plane stride of part/tmp (LayP48)
+    uint64_t ostride[2] = {0, 0};  // of tmp when it is written in another layout (LayP40)
 };
 
-template <class Lay>
+// Lay: the partition's layout; LayO: the layout the grouped tiles are written
+// in (LayP40 after LayP48: the group's digit is not stored)
+template <class Lay, class LayO = Lay>
 __global__ void __launch_bounds__(TP_THREADS)
 k_tilepass(TilePassArgs A) {
     typedef typename Lay::W W;
+    static_assert(std::is_same<W, typename LayO::W>::value, "one element type");
     constexpr int TP_ITEMS = tp_items<W>();
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     if (A.pack_bad && *A.pack_bad) return;
@@ -239,7 +243,8 @@ k_tilepass(TilePassArgs A) {
     if (A.ntiles[r] && t >= *A.ntiles[r]) return;
     const TileTable& tt = A.tt[r];
     const typename Lay::CView part = Lay::cview(A.part[r], A.pstride[r]);
-    const typename Lay::View tmp = Lay::view(A.tmp[r], A.pstride[r]);
+    const typename LayO::View tmp =
+        LayO::view(A.tmp[r], std::is_same<Lay, LayO>::value ? A.pstride[r] : A.ostride[r]);
     const uint64_t off = tt.off[t];
     const uint32_t len = tt.len[t];
     const uint32_t b = tt.bucket[t];
@@ -673,10 +678,11 @@ __device__ __forceinline__ void group_overflow(const GroupArgs& A, LDS& L,
 // element (p = n - 1).
 template <class Lay, class Src, class Meta>
 __device__ __forceinline__ void gather_group(const GroupArgs& A, GroupLDS<typename Lay::W>& L,
-                                             const Meta& C, int r, uint32_t n,
+                                             const Meta& C, int r, uint32_t grp, uint32_t n,
                                              typename Lay::W (&v)[GS_ITEMS]) {
     if (n == 0) return;
-    const typename Lay::CView tp = Lay::cview(A.tmp[r], A.pstride[r]) + C.bst[r];
+    const typename Lay::CView tp =
+        with_group(Lay::cview(A.tmp[r], A.pstride[r]), grp, A.plan) + C.bst[r];
     const uint32_t lane = lane_id();
     const uint32_t wid = __builtin_amdgcn_readfirstlane(otid() >> 6);
     typedef uint32_t U4 __attribute__((ext_vector_type(4)));
@@ -1167,8 +1173,10 @@ __device__ __forceinline__ void group_loop(const GroupArgs& A0, GroupLDS<typenam
     bool cf[2];
     fits(cn, cf);
     W vr[GS_ITEMS], vs[GS_ITEMS];
-    if (cf[0]) gather_group<Lay, Src>(A, L, C, 0, cn[0], vr);
-    if (cf[1] && nslot > 1) gather_group<Lay, Src>(A, L, C, 1, cn[1], vs);
+    // slot r's group digit (both slots hold one group in a join)
+    auto slot_g = [&](const GroupMeta<TPL>& X, int r) { return PAIR && r ? X.g[1] : X.g[0]; };
+    if (cf[0]) gather_group<Lay, Src>(A, L, C, 0, slot_g(C, 0), cn[0], vr);
+    if (cf[1] && nslot > 1) gather_group<Lay, Src>(A, L, C, 1, slot_g(C, 1), cn[1], vs);
     if (nit > 1 && SMJ_GS_META_PREFETCH) load_meta<Src, PAIR>(A, g0, stride, cnt, 1, M, true);
 
     for (uint32_t j = 0; j < nit; j++) {
@@ -1201,10 +1209,10 @@ __device__ __forceinline__ void group_loop(const GroupArgs& A0, GroupLDS<typenam
         nf[0] &= has_next;
         nf[1] &= has_next;
         auto gather_next_r = [&]() {
-            if (nf[0]) gather_group<Lay, Src>(A, L, N, 0, nn[0], vr);
+            if (nf[0]) gather_group<Lay, Src>(A, L, N, 0, slot_g(N, 0), nn[0], vr);
         };
         auto gather_next_s = [&]() {
-            if (nf[1] && nslot > 1) gather_group<Lay, Src>(A, L, N, 1, nn[1], vs);
+            if (nf[1] && nslot > 1) gather_group<Lay, Src>(A, L, N, 1, slot_g(N, 1), nn[1], vs);
         };
         bool cleared = false;  // sort_two zeroed the histograms itself
         if (SMJ_GS_TWO && nslot == 2 && (pair || (cf[0] && cf[1]))) {
@@ -1396,7 +1404,7 @@ __device__ __forceinline__ typename Lay::CView skew_run(const GroupArgs& G, int 
     const uint16_t* pf = tt.prefT + (uint64_t)g * tt.tstride + t0 + t;
     const uint32_t lo = pf[0];
     len = (uint32_t)(pf[tt.tstride] - lo);
-    return Lay::cview(G.tmp[r], G.pstride[r]) + (tt.off[t0 + t] + lo);
+    return with_group(Lay::cview(G.tmp[r], G.pstride[r]), g, G.plan) + (tt.off[t0 + t] + lo);
 }
 
 constexpr uint32_t SK_WIN = kSkewSmall / 64;  // 64-position windows of a small group
@@ -1426,7 +1434,7 @@ __device__ __forceinline__ void skew_for_each(const GroupArgs& G, const SkewSmal
                                               F&& f) {
     typedef typename Lay::W W;
     if (nt <= SK_TM) {
-        const typename Lay::CView tmp = Lay::cview(G.tmp[r], G.pstride[r]);
+        const typename Lay::CView tmp = with_group(Lay::cview(G.tmp[r], G.pstride[r]), g, G.plan);
         const uint32_t lane = lane_id();
         const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         for (uint32_t c = 0; c < n; c += SK_CHUNK) {
@@ -2164,10 +2172,26 @@ static void launch_groupsort(Workspace* ws, int tpl, uint32_t nwg, hipStream_t s
 // partition + host-known plan): launch sizes are upper bounds, the tile
 // numbering is computed on the device.  One synchronisation at the end (skew
 // queue and the partition's overflow flag).
-template <class Lay>
+#ifndef SMJ_P40
+#define SMJ_P40 1  // the tile pass writes 48-bit words without their group digit
+#endif
+// Lay: the level-1 partition's layout; LayG: the layout the tile pass
+// writes and the group pass reads (LayP40 after LayP48)
+template <class Lay, class LayG = Lay>
 static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
     typedef typename Lay::W W;
     set_pass_attrs<Lay>();
+    set_pass_attrs<LayG>();
+    constexpr bool p40 = !std::is_same<Lay, LayG>::value;
+    if (p40) {
+        static bool done = false;
+        if (!done) {
+            SMJ_CHECK(hipFuncSetAttribute((const void*)k_tilepass<Lay, LayG>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          160 * 1024));
+            done = true;
+        }
+    }
     const uint32_t nb = a.nbuckets;
     const int nrel = a.nrel;
     const uint32_t nb2 = 1u << a.host_plan->D2;
@@ -2232,10 +2256,22 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
         T.nt[i] = i < ns ? ub[rr] : 0;
         T.ntiles[i] = ntiles[rr];
     }
+    // LayP40: the grouped tiles' byte plane, a buffer of the workspace per
+    // relation (kept across the calls of a staged join); its offset from the
+    // lo plane is the layout's "stride"
+    uint64_t hoff[2] = {0, 0};
+    if (p40) {
+        static const char* hn[2] = {"p40_hi0", "p40_hi1"};
+        for (int r = 0; r < nrel; r++) {
+            const uint8_t* hb = (const uint8_t*)ws->scratch(hn[r], a.pstride[r] ? a.pstride[r] : 1);
+            hoff[r] = (uint64_t)((uintptr_t)hb - (uintptr_t)a.tmp[r]);
+        }
+        for (int i = 0; i < 2; i++) T.ostride[i] = hoff[sel[i < ns ? i : 0]];
+    }
     for (int r = 0; r < 2; r++) {
         const int rr = r < nrel ? r : 0;
         G.tmp[r] = a.tmp[rr];
-        G.pstride[r] = a.pstride[rr];
+        G.pstride[r] = p40 ? hoff[rr] : a.pstride[rr];
         G.out[r] = a.out[rr];
         G.bstart[r] = a.bstart[rr];
         G.ostart[r] = ostart[rr];
@@ -2261,8 +2297,8 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
         {
             TraceScope ts(ws, "k_tilepass", st);
             const size_t tp_lds = (size_t)tsz * sizeof(W) + nb2 * 4 + 64;
-            hipLaunchKernelGGL(k_tilepass<Lay>, dim3(T.nt[0] + T.nt[1]), dim3(TP_THREADS),
-                               tp_lds, st, T);
+            hipLaunchKernelGGL((k_tilepass<Lay, LayG>), dim3(T.nt[0] + T.nt[1]),
+                               dim3(TP_THREADS), tp_lds, st, T);
         }
         const uint32_t ubs[2] = {T.nt[0], T.nt[1]};
         uint32_t* nts[2] = {ntiles[sel[0]], ntiles[sel[ns > 1 ? 1 : 0]]};
@@ -2285,7 +2321,7 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
             (G.pair ? gs_wg_per_cu<W, true>() : gs_wg_per_cu<W, false>()) * 256;
         const uint32_t nwg = groupsort_grid(ngroups, maxwg, G.per);
         TraceScope ts(ws, "k_groupsort", st);
-        launch_groupsort<Lay>(ws, group_tpl(nmax, nb, a.nseg, tsz), nwg, st, G);
+        launch_groupsort<LayG>(ws, group_tpl(nmax, nb, a.nseg, tsz), nwg, st, G);
     }
     SMJ_CHECK(hipGetLastError());
     if (a.ev_ovf) SMJ_CHECK(hipEventRecord(a.ev_ovf, st));
@@ -2320,7 +2356,7 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
     for (int r = 0; r < nrel; r++)
         SMJ_CHECK(hipMemcpyAsync(hdst + (size_t)r * nb, ostart[r], (size_t)nb * 8,
                                  hipMemcpyDeviceToHost, st));
-    skew_path<Lay>(ws, G, ovf, no, hdst, nb, st);
+    skew_path<LayG>(ws, G, ovf, no, hdst, nb, st);
     SMJ_CHECK(hipGetLastError());
     return true;
 }
@@ -2338,7 +2374,10 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
     set_pass_attrs<LayTup>();
     if (a.host_plan && a.seg_start[0] && a.part_flag) {
         if (a.p32) return bucket_sort_nosync<LayP32>(ws, a, st);
-        if (a.p48) return bucket_sort_nosync<LayP48>(ws, a, st);
+        if (a.p48)
+            return SMJ_P40 && LayP40::holds(*a.host_plan)
+                ? bucket_sort_nosync<LayP48, LayP40>(ws, a, st)
+                : bucket_sort_nosync<LayP48>(ws, a, st);
 #ifdef KEY_8B
         if (a.packed) return bucket_sort_nosync<LayPacked>(ws, a, st);
 #endif

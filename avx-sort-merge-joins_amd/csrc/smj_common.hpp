@@ -703,6 +703,64 @@ struct LayP32 {
     __host__ static bool usable(const RangePlan& P) { return P.s1 >= 1 && P.s1 <= 31; }
 };
 
+// LayP40 (round 5): the tile pass's output of 48-bit words.  Inside one
+// group (bucket b, level-2 digit g) the word's top D2 bits are g, so the tile
+// pass stores only the low 48 - D2 <= 40 bits: the lo plane in place, bits
+// 32..39 in a byte plane of their own (the 16-bit plane of the input is still
+// being read by other tiles), 5 bytes an element instead of 6.  A view made
+// for one group (with_group) ORs g back in on every load, so the group pass
+// and the skew kernels see LayP48's words and use LayP48's arithmetic.  The
+// plane "stride" of this layout is the byte offset from the lo plane to the
+// byte plane (any buffer; the offset wraps modulo 2^64).  Applies when D2 >= 8.
+typedef const __attribute__((address_space(1))) uint8_t* G8c;
+typedef __attribute__((address_space(1))) uint8_t* G8;
+struct P40CView {
+    G32c lo;
+    G8c hi;
+    uint64_t gbits;  // the group's digit, in place (0 before with_group)
+    __device__ __forceinline__ uint64_t operator[](uint64_t i) const {
+        return (uint64_t)lo[i] | ((uint64_t)hi[i] << 32) | gbits;
+    }
+    __device__ __forceinline__ P40CView operator+(uint64_t k) const {
+        return P40CView{lo + k, hi + k, gbits};
+    }
+};
+struct P40View {
+    G32 lo;
+    G8 hi;
+    __device__ __forceinline__ P40View operator+(uint64_t k) const { return P40View{lo + k, hi + k}; }
+};
+__device__ __forceinline__ void st_w(const P40View& p, uint64_t v) {
+#if SMJ_NT_STORES
+    __builtin_nontemporal_store((uint32_t)v, p.lo);
+    __builtin_nontemporal_store((uint8_t)(v >> 32), p.hi);
+#else
+    p.lo[0] = (uint32_t)v;
+    p.hi[0] = (uint8_t)(v >> 32);
+#endif
+}
+struct LayP40 : LayP48 {
+    typedef P40CView CView;
+    typedef P40View View;
+    __device__ static __forceinline__ CView cview(const void* b, uint64_t hoff) {
+        return CView{(G32c) static_cast<const uint32_t*>(b),
+                     (G8c)(static_cast<const uint8_t*>(b) + hoff), 0ull};
+    }
+    __device__ static __forceinline__ View view(void* b, uint64_t hoff) {
+        return View{(G32) static_cast<uint32_t*>(b), (G8)(static_cast<uint8_t*>(b) + hoff)};
+    }
+    __host__ static bool holds(const RangePlan& P) { return P.D2 >= 8; }
+};
+// a view of group g's elements: LayP40 restores the digit; the other layouts'
+// views are complete already
+template <class V>
+__device__ __forceinline__ V with_group(const V& v, uint32_t, const RangePlan&) {
+    return v;
+}
+__device__ __forceinline__ P40CView with_group(const P40CView& v, uint32_t g, const RangePlan& P) {
+    return P40CView{v.lo, v.hi, (uint64_t)g << (48 - P.D2)};
+}
+
 // identity "packing" of the plain layout
 struct PackNone {
     typedef Tup OutT;
