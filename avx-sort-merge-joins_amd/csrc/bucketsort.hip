@@ -50,6 +50,9 @@ namespace smj {
 #define SMJ_TP_THREADS 1024
 #endif
 constexpr int TP_THREADS = SMJ_TP_THREADS;
+#ifndef SMJ_TP_PERSIST
+#define SMJ_TP_PERSIST 1  // persistent tile pass, next tile's loads in flight (0: one tile a workgroup)
+#endif
 #ifndef SMJ_GS_XCD
 #define SMJ_GS_XCD 1  // XCD-aware group order in k_groupsort (0: a lab build's contiguous chunks)
 #endif
@@ -316,6 +319,170 @@ k_tilepass(TilePassArgs A) {
     for (int j = 0; j < TP_ITEMS; j++) {
         uint32_t i = j * TP_THREADS + threadIdx.x;
         if (i < len) st_w(tmp + off + i, stage[i]);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// The tile pass as a persistent kernel (round 5): one workgroup per CU walks
+// the tiles idx = blockIdx.x + k * gridDim.x of both relations, and the next
+// tile's loads are issued before the current tile's LDS phases, so they fly
+// under its ranking, staging and stores.  (One tile per workgroup, as in
+// k_tilepass, holds 128 KB of LDS: a CU runs one workgroup at a time and every
+// tile's loads start only when the previous workgroup has gone.)  Two
+// register tiles alternate (the loop is unrolled by two: no register copy
+// waits for loads).  LDS phases per tile: digits + histogram | scan + prefix
+// row | ranks + stage | histogram cleared, stage -> HBM.
+template <class Lay, class LayO>
+struct TilePassP {
+    typedef typename Lay::W W;
+    static constexpr int ITEMS = tp_items<W>();
+    // element j of a thread
+    __device__ static __forceinline__ uint32_t elem(int j) {
+        return (uint32_t)j * TP_THREADS + threadIdx.x;
+    }
+    const TilePassArgs& A;
+    W* stage;
+    uint32_t* hist;
+    uint32_t* scr;
+    uint32_t n0, total;
+
+    struct Meta {
+        uint64_t off;
+        uint32_t len, b, t;
+        int r;
+    };
+    // tile idx's place; past the last tile, the last tile's place with no
+    // elements (its loads then read one valid element, discarded)
+    __device__ __forceinline__ Meta meta(uint32_t idx) const {
+        const bool none = idx >= total;
+        if (none) idx = total - 1;
+        Meta m;
+        m.r = idx < n0 ? 0 : 1;
+        m.t = A.t0[m.r] + (m.r ? idx - n0 : idx);
+        // the tile table is read-only here: scalar loads through the constant
+        // address space (a vector load's wait would drain the previous tile's
+        // stores before the next tile's loads are issued)
+        const TileTable& tt = A.tt[m.r];
+        typedef const __attribute__((address_space(4))) uint64_t* C64;
+        typedef const __attribute__((address_space(4))) uint32_t* C32;
+        m.off = ((C64)tt.off)[m.t];
+        m.len = none ? 0u : ((C32)tt.len)[m.t];
+        m.b = ((C32)tt.bucket)[m.t];
+        return m;
+    }
+    // unconditional loads (clamped to the tile): a fixed count in flight, no
+    // branches around them
+    __device__ __forceinline__ void load(W (&v)[ITEMS], const Meta& m) const {
+        const typename Lay::CView part = Lay::cview(A.part[m.r], A.pstride[m.r]) + m.off;
+        const uint32_t lim = m.len ? m.len - 1 : 0u;
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint32_t i = elem(j);
+            v[j] = part[i < lim ? i : lim];
+        }
+    }
+    // the level-2 digits of the tile's elements, hist[d] += 1 (RANK false)
+    // or the element staged at hist[d]++ (RANK true); recomputed in both
+    // phases instead of held (the two register tiles leave no room)
+    template <bool RANK>
+    __device__ __forceinline__ void digits(const W (&v)[ITEMS], const Meta& m) const {
+        const RangePlan& P = A.plan;
+        if (A.d2_fast && m.b != 0 && m.b != (1u << P.D1) - 1) {
+            const uint32_t base_lo = (uint32_t)P.base, mask = A.nb2 - 1;
+#pragma unroll
+            for (int j = 0; j < ITEMS; j++) {
+                const uint32_t i = elem(j);
+                if (i < m.len) {
+                    const uint32_t d = Lay::digit_fast(v[j], base_lo, P.s1, P.s2, mask);
+                    if (RANK)
+                        stage[atomicAdd(&hist[d], 1u)] = v[j];
+                    else
+                        atomicAdd(&hist[d], 1u);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < ITEMS; j++) {
+                const uint32_t i = elem(j);
+                if (i < m.len) {
+                    const uint32_t d = plan_d2(P, Lay::rel(P, v[j], m.b), m.b);
+                    if (RANK)
+                        stage[atomicAdd(&hist[d], 1u)] = v[j];
+                    else
+                        atomicAdd(&hist[d], 1u);
+                }
+            }
+        }
+    }
+    __device__ __forceinline__ void tile(const W (&v)[ITEMS], const Meta& m) const {
+        const uint32_t nb2 = A.nb2;
+        __syncthreads();  // the histogram is clear, the previous stage read out
+        digits<false>(v, m);
+        __syncthreads();
+        const uint32_t per = (nb2 + TP_THREADS - 1) / TP_THREADS;
+        const uint32_t d0 = threadIdx.x * per;
+        uint32_t loc = 0;
+        for (uint32_t k = 0; k < per; k++)
+            if (d0 + k < nb2) loc += hist[d0 + k];
+        uint32_t tot;
+        uint32_t ex = block_exclusive_scan(loc, scr, &tot);
+        uint16_t* pref = A.tt[m.r].pref + (uint64_t)m.t * (nb2 + 1);
+        for (uint32_t k = 0; k < per; k++) {
+            const uint32_t d = d0 + k;
+            if (d < nb2) {
+                const uint32_t c = hist[d];
+                hist[d] = ex;
+                pref[d] = (uint16_t)ex;
+                ex += c;
+            }
+        }
+        if (threadIdx.x == 0) pref[nb2] = (uint16_t)m.len;
+        __syncthreads();
+        digits<true>(v, m);
+        __syncthreads();
+        for (uint32_t d = threadIdx.x; d < nb2; d += TP_THREADS) hist[d] = 0;
+        const typename LayO::View tmp = LayO::view(
+            A.tmp[m.r], std::is_same<Lay, LayO>::value ? A.pstride[m.r] : A.ostride[m.r]) + m.off;
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint32_t i = elem(j);
+            if (i < m.len) st_w(tmp + i, stage[i]);
+        }
+    }
+};
+
+template <class Lay, class LayO = Lay>
+__global__ void __launch_bounds__(TP_THREADS)
+k_tilepass_p(TilePassArgs A) {
+    typedef TilePassP<Lay, LayO> TP;
+    typedef typename TP::W W;
+    static_assert(std::is_same<W, typename LayO::W>::value, "one element type");
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    if (A.pack_bad && *A.pack_bad) return;
+    TP s{A};
+    s.stage = reinterpret_cast<W*>(lds_raw);
+    s.hist = reinterpret_cast<uint32_t*>(lds_raw + tile_elems<W>() * sizeof(W));
+    s.scr = s.hist + A.nb2;
+    uint32_t n[2];
+    for (int r = 0; r < 2; r++)
+        n[r] = A.nt[r] == 0 ? 0u : A.ntiles[r] ? min(*A.ntiles[r], A.nt[r]) : A.nt[r];
+    s.n0 = n[0];
+    s.total = n[0] + n[1];
+    uint32_t idx = blockIdx.x;
+    if (idx >= s.total) return;
+    for (uint32_t d = threadIdx.x; d < A.nb2; d += TP_THREADS) s.hist[d] = 0;
+    W a[TP::ITEMS], b[TP::ITEMS];
+    typename TP::Meta ma = s.meta(idx), mb;
+    s.load(a, ma);
+    for (;;) {
+        mb = s.meta(idx + gridDim.x);
+        s.load(b, mb);
+        s.tile(a, ma);
+        if ((idx += gridDim.x) >= s.total) break;
+        ma = s.meta(idx + gridDim.x);
+        s.load(a, ma);
+        s.tile(b, mb);
+        if ((idx += gridDim.x) >= s.total) break;
     }
 }
 
@@ -2095,12 +2262,32 @@ static void launch_preft_range(const TilePassArgs& T, int nrel, uint32_t nb2,
     launch_preft(tt, nrel, ub, nt, nb2, st);
 }
 
+// the tile pass over the tiles [0, nt[r]) of both relations (device counts:
+// at most ntiles[r]); persistent, one workgroup per CU (SMJ_TP_PERSIST) for
+// 16-byte tuples
+template <class Lay, class LayO>
+static void launch_tilepass(const TilePassArgs& T, size_t lds, hipStream_t st) {
+    const uint32_t nblk = T.nt[0] + T.nt[1];
+    // measured (profiles/r05_lab/tp_ab.txt): 16-byte tuples 1.63 -> 1.52 ms;
+    // words (8-byte elements, two loads and two stores each for the 48-bit
+    // planes) 0.65 -> 0.68-0.71 ms, the prefetch and the stores together
+    // saturating the 63 outstanding memory operations; 32-bit words spill
+    if (SMJ_TP_PERSIST && sizeof(typename Lay::W) == 16) {
+        hipLaunchKernelGGL((k_tilepass_p<Lay, LayO>), dim3(nblk < 256 ? nblk : 256),
+                           dim3(TP_THREADS), lds, st, T);
+    } else {
+        hipLaunchKernelGGL((k_tilepass<Lay, LayO>), dim3(nblk), dim3(TP_THREADS), lds, st, T);
+    }
+}
+
 // dynamic LDS limits of the tile and group passes (per layout)
 template <class Lay>
 static void set_pass_attrs() {
     static bool done = false;
     if (done) return;
     SMJ_CHECK(hipFuncSetAttribute((const void*)k_tilepass<Lay>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    SMJ_CHECK(hipFuncSetAttribute((const void*)k_tilepass_p<Lay>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     // several workgroups per CU (launch bounds): ask for what one needs
     const void* gs[4] = {(const void*)k_groupsort<Lay, 2, false>,
@@ -2187,6 +2374,9 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
         static bool done = false;
         if (!done) {
             SMJ_CHECK(hipFuncSetAttribute((const void*)k_tilepass<Lay, LayG>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          160 * 1024));
+            SMJ_CHECK(hipFuncSetAttribute((const void*)k_tilepass_p<Lay, LayG>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize,
                                           160 * 1024));
             done = true;
@@ -2297,8 +2487,7 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
         {
             TraceScope ts(ws, "k_tilepass", st);
             const size_t tp_lds = (size_t)tsz * sizeof(W) + nb2 * 4 + 64;
-            hipLaunchKernelGGL((k_tilepass<Lay, LayG>), dim3(T.nt[0] + T.nt[1]),
-                               dim3(TP_THREADS), tp_lds, st, T);
+            launch_tilepass<Lay, LayG>(T, tp_lds, st);
         }
         const uint32_t ubs[2] = {T.nt[0], T.nt[1]};
         uint32_t* nts[2] = {ntiles[sel[0]], ntiles[sel[ns > 1 ? 1 : 0]]};
@@ -2505,7 +2694,7 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
     if (ntiles) {
         {
             TraceScope ts(ws, "k_tilepass", st);
-            hipLaunchKernelGGL(k_tilepass<LayTup>, dim3(ntiles), dim3(TP_THREADS), tp_lds, st, T);
+            launch_tilepass<LayTup, LayTup>(T, tp_lds, st);
         }
         launch_preft_range(T, nrel, nb2, st);
     }
