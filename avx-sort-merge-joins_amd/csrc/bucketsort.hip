@@ -2563,8 +2563,12 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
     set_pass_attrs<LayTup>();
     if (a.host_plan && a.seg_start[0] && a.part_flag) {
         if (a.p32) return bucket_sort_nosync<LayP32>(ws, a, st);
+        // 16-byte tuples only: with 8-byte tuples the group pass gained
+        // less than the byte plane cost it (the join 2.542-2.551 ms either
+        // way, the group pass 0.911-0.921 -> 0.930 ms, its SQ wait share
+        // 0.49 -> 0.56; profiles/r05_lab/p40_ab.txt, r05_sq_join8*)
         if (a.p48)
-            return SMJ_P40 && LayP40::holds(*a.host_plan)
+            return SMJ_P40 && sizeof(Tup) == 16 && LayP40::holds(*a.host_plan)
                 ? bucket_sort_nosync<LayP48, LayP40>(ws, a, st)
                 : bucket_sort_nosync<LayP48>(ws, a, st);
 #ifdef KEY_8B
