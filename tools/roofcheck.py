@@ -27,13 +27,18 @@ def stats(d):
     files = glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True)
     if not files:
         return {}
-    out = {}
+    out, main = {}, {}
     for r in csv.DictReader(open(files[0])):
         k = short(r["Name"])
         calls, tot = int(r["Calls"]), float(r["TotalDurationNs"])
         c0, t0 = out.get(k, (0, 0.0))
         out[k] = (c0 + calls, t0 + tot)
-    return {k: (c, t / c) for k, (c, t) in out.items()}
+        # the instantiation with the most time (a layout probe that stops at
+        # its first check, e.g. a 32-bit-word try whose payloads do not fit,
+        # is another instantiation of a few microseconds)
+        if tot > main.get(k, ("", 0, 0.0))[2]:
+            main[k] = (r["Name"], calls, tot)
+    return {k: (c, t / c, main[k]) for k, (c, t) in out.items()}
 
 
 def load(p):
@@ -57,11 +62,18 @@ def main():
             e.update(kernel=k, line_frac=rf["frac"], line_avg_ms=rf["avg_launch_ms"],
                      alg_bytes_per_launch=rf["alg_bytes_per_launch"])
             if k in st:
-                calls, avg_ns = st[k]
+                calls, avg_ns, (mname, mcalls, mtot) = st[k]
                 fr = rf["alg_bytes_per_launch"] / avg_ns / PEAK
                 e.update(rocprof_calls=calls, rocprof_avg_ms=round(avg_ns / 1e6, 4),
-                         rocprof_frac=round(fr, 4),
-                         rel_gap=round(abs(fr - rf["frac"]) / rf["frac"], 4),
+                         rocprof_frac=round(fr, 4))
+                # the gap is taken on the main instantiation when others ran
+                if mcalls != calls:
+                    avg_ns = mtot / mcalls
+                    fr = rf["alg_bytes_per_launch"] / avg_ns / PEAK
+                    e.update(rocprof_main=mname, rocprof_main_calls=mcalls,
+                             rocprof_main_avg_ms=round(avg_ns / 1e6, 4),
+                             rocprof_main_frac=round(fr, 4))
+                e.update(rel_gap=round(abs(fr - rf["frac"]) / rf["frac"], 4),
                          within_5pct=abs(fr - rf["frac"]) <= 0.05 * rf["frac"])
             e["ms_per_step"] = line.get("ms_per_step")
         nop = load(os.path.join(d, nm + "_noprof.json"))
