@@ -2283,21 +2283,14 @@ static void launch_tilepass(const TilePassArgs& T, size_t lds, hipStream_t st) {
 // dynamic LDS limits of the tile and group passes (per layout)
 template <class Lay>
 static void set_pass_attrs() {
-    static bool done = false;
-    if (done) return;
-    SMJ_CHECK(hipFuncSetAttribute((const void*)k_tilepass<Lay>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    SMJ_CHECK(hipFuncSetAttribute((const void*)k_tilepass_p<Lay>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    set_lds_attr((const void*)k_tilepass<Lay>, 160 * 1024);
+    set_lds_attr((const void*)k_tilepass_p<Lay>, 160 * 1024);
     // several workgroups per CU (launch bounds): ask for what one needs
     const void* gs[4] = {(const void*)k_groupsort<Lay, 2, false>,
                          (const void*)k_groupsort<Lay, 4, false>,
                          (const void*)k_groupsort<Lay, 2, true>,
                          (const void*)k_groupsort<Lay, 4, true>};
-    for (const void* f : gs)
-        SMJ_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)sizeof(GroupLDS<typename Lay::W>)));
-    done = true;
+    for (const void* f : gs) set_lds_attr(f, (int)sizeof(GroupLDS<typename Lay::W>));
 }
 
 // Tile runs per lane of the group pass: 2 (128 tiles per bucket) unless the
@@ -2371,16 +2364,8 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
     set_pass_attrs<LayG>();
     constexpr bool p40 = !std::is_same<Lay, LayG>::value;
     if (p40) {
-        static bool done = false;
-        if (!done) {
-            SMJ_CHECK(hipFuncSetAttribute((const void*)k_tilepass<Lay, LayG>,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize,
-                                          160 * 1024));
-            SMJ_CHECK(hipFuncSetAttribute((const void*)k_tilepass_p<Lay, LayG>,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize,
-                                          160 * 1024));
-            done = true;
-        }
+        set_lds_attr((const void*)k_tilepass<Lay, LayG>, 160 * 1024);
+        set_lds_attr((const void*)k_tilepass_p<Lay, LayG>, 160 * 1024);
     }
     const uint32_t nb = a.nbuckets;
     const int nrel = a.nrel;
@@ -2553,13 +2538,7 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
 bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
     const uint32_t nb = a.nbuckets;
     const int nrel = a.nrel;
-    static bool attr = false;
-    if (!attr) {
-        SMJ_CHECK(hipFuncSetAttribute((const void*)k_preft,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      PT_TILES * ((1 << kMaxD2) + 1) * 2));
-        attr = true;
-    }
+    set_lds_attr((const void*)k_preft, PT_TILES * ((1 << kMaxD2) + 1) * 2);
     set_pass_attrs<LayTup>();
     if (a.host_plan && a.seg_start[0] && a.part_flag) {
         if (a.p32) return bucket_sort_nosync<LayP32>(ws, a, st);

@@ -15,7 +15,7 @@
 //          rank's own chunk read in place inside its partition buffer and the
 //          other ranks' rows after it, and a small summary the host reads in
 //          one copy (chunk starts and sizes, receive sizes, used elements,
-//          the flags' maximum over ranks).
+//          the flags OR-ed over the ranks).
 // They replace two dozen small framework ops (and their host round trips) per
 // relation and step.
 #include "smj_common.hpp"
@@ -101,7 +101,7 @@ k_xsend(const int64_t* __restrict__ start, const int64_t* __restrict__ cnt,
 // msg: G rows of (head + 2 * mine * K), row s from rank s.  tstart/tcnt:
 // (2^lbits) x (G * K), bucket b = owned partition b, segment (s, q).
 // summary: [chunk start (G) | chunk size = send (G) | receive (G) | used
-// received (G) | max flag0 | max flag1]
+// received (G) | flag0 | flag1, each OR-ed over the ranks]
 __global__ void __launch_bounds__(256)
 k_xrecv(const int64_t* __restrict__ msg, const int64_t* __restrict__ chunk, uint32_t G,
         uint32_t rank, uint32_t mine, uint32_t K, uint32_t nb, uint64_t cap,
@@ -118,8 +118,8 @@ k_xrecv(const int64_t* __restrict__ msg, const int64_t* __restrict__ chunk, uint
             if (s != rank) ro += rl;
             summary[2 * G + s] = rl;
             summary[3 * G + s] = msg[(size_t)s * row + 1];
-            f0 = max(f0, msg[(size_t)s * row + 2]);
-            f1 = max(f1, msg[(size_t)s * row + 3]);
+            f0 |= msg[(size_t)s * row + 2];  // bit masks: every rank's reasons
+            f1 |= msg[(size_t)s * row + 3];
         }
         summary[4 * G] = f0;
         summary[4 * G + 1] = f1;

@@ -62,6 +62,8 @@ struct DevOps {
     int device = 0;
     hipStream_t st[2] = {nullptr, nullptr};
     hipEvent_t ev[mg::kNumEvents] = {};
+    hipEvent_t tev[mg::kNumTMarks] = {};  // timing marks (the phases of mg::Stats)
+    uint32_t tset = 0;                    // marks recorded since the rank was made
     Workspace* ws = nullptr;
 
     smj_workspace* w() const { return (smj_workspace*)ws; }
@@ -94,6 +96,16 @@ struct DevOps {
     void wait(int sid, int e) { SMJ_CHECK(hipStreamWaitEvent(st[sid], ev[e], 0)); }
     void host_wait(int e) { SMJ_CHECK(hipEventSynchronize(ev[e])); }
     void sync(int sid) { SMJ_CHECK(hipStreamSynchronize(st[sid])); }
+    void tmark(int m, int sid) {
+        SMJ_CHECK(hipEventRecord(tev[m], st[sid]));
+        tset |= 1u << m;
+    }
+    double tspan(int a, int b) {
+        if (!((tset >> a) & 1) || !((tset >> b) & 1)) return 0.0;
+        float ms = 0.f;
+        SMJ_CHECK(hipEventElapsedTime(&ms, tev[a], tev[b]));
+        return ms;
+    }
     uint32_t shards() { return smj_sampled_shards(); }
     uint64_t sampled_capacity(uint64_t n, uint32_t nbits) { return smj_sampled_capacity(n, nbits); }
     int part_planes(const void* in, uint64_t n, void* out, uint64_t stride, uint32_t nbits,
@@ -241,6 +253,7 @@ struct RankCtx {
         for (int s = 0; s < 2; s++)
             SMJ_CHECK(hipStreamCreateWithFlags(&ops.st[s], hipStreamNonBlocking));
         for (auto& e : ops.ev) SMJ_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        for (auto& e : ops.tev) SMJ_CHECK(hipEventCreate(&e));
         ops.device = dev;
         ops.ws = &ws;
         coll.ops = &ops;
@@ -254,6 +267,7 @@ struct RankCtx {
         for (int r = 0; r < 2; r++)
             if (inbuf[r]) (void)hipFree(inbuf[r]);
         for (auto& e : ops.ev) (void)hipEventDestroy(e);
+        for (auto& e : ops.tev) (void)hipEventDestroy(e);
         for (int s = 0; s < 2; s++) (void)hipStreamDestroy(ops.st[s]);
     }
 };
@@ -355,6 +369,11 @@ struct CallArgs {
     uint64_t nR;
     const Tup* S;
     uint64_t nS;
+    // smj_mgpu_join_slices: rank g's slices (R and S above unused)
+    const Tup* const* Rs = nullptr;
+    const uint64_t* nRs = nullptr;
+    const Tup* const* Ss = nullptr;
+    const uint64_t* nSs = nullptr;
     mg::Options opt;
     Tup* sortedR = nullptr;  // host or device destinations of the sorted shares
     Tup* sortedS = nullptr;
@@ -365,9 +384,33 @@ struct CallArgs {
 struct CallOut {
     uint64_t total = 0;
     std::vector<uint64_t> nR, nS, local;
-    mg::Stats stats;
+    mg::Stats stats;               // rank 0's
+    std::vector<mg::Stats> ranks;  // every rank's
     double ms = 0;
 };
+
+// the last call's per-rank statistics (smj_mgpu_last_stats; under g_mu)
+std::vector<mg::Stats> g_last_stats;
+double g_last_ms = 0;
+
+void fill_stats(const mg::Stats& x, double ms, smj_mgpu_stats* o) {
+    o->layout = x.layout;
+    o->pbits = x.pbits;
+    o->attempts = x.attempts;
+    o->replans = x.replans;
+    o->sent_bytes = x.sent_B;
+    o->recv_bytes = x.recv_B;
+    o->key_min = x.kmin;
+    o->key_max = x.kmax;
+    o->ms = ms;
+    o->partition_ms = x.part_ms;
+    o->tables_ms = x.tables_ms;
+    o->wait_ms = x.wait_ms;
+    o->join_ms = x.join_ms;
+    o->reduce_ms = x.reduce_ms;
+    o->busy_ms = x.busy_ms;
+    o->rows_ms = x.rows_ms;
+}
 
 // level-1 buckets per rank: 2^8 (the 1-GPU join's fan-out), more while a
 // bucket would exceed the tile pass's kLocalBucketCap (the 1024M-per-rank
@@ -380,7 +423,10 @@ uint32_t bucket_bits_for(uint64_t n_per_rank) {
 
 void run_call(Group& grp, CallArgs a, CallOut& out) {
     const int G = grp.G;
-    a.opt.bucket_bits = bucket_bits_for(std::max(a.nR, a.nS) / (uint64_t)G);
+    uint64_t share = std::max(a.nR, a.nS) / (uint64_t)G;
+    if (a.Rs)
+        for (int r = 0; r < G; r++) share = std::max(share, std::max(a.nRs[r], a.nSs[r]));
+    a.opt.bucket_bits = bucket_bits_for(share);
     out.nR.assign((size_t)G, 0);
     out.nS.assign((size_t)G, 0);
     out.local.assign((size_t)G, 0);
@@ -393,10 +439,18 @@ void run_call(Group& grp, CallArgs a, CallOut& out) {
     mg::run_ranks(G, [&](int r) {
         RankCtx& rc = *grp.ranks[r];
         SMJ_CHECK(hipSetDevice(rc.device));
-        const uint64_t nr = r == G - 1 ? a.nR - perR * r : perR;
-        const uint64_t ns = r == G - 1 ? a.nS - perS * r : perS;
-        const void* R = stage_slice(rc, 0, a.R, perR * r, nr);
-        const void* S = stage_slice(rc, 1, a.S, perS * r, ns);
+        uint64_t nr = r == G - 1 ? a.nR - perR * r : perR;
+        uint64_t ns = r == G - 1 ? a.nS - perS * r : perS;
+        const void *R, *S;
+        if (a.Rs) {  // the rank's own slices (on its GPU: read in place)
+            nr = a.nRs[r];
+            ns = a.nSs[r];
+            R = stage_slice(rc, 0, a.Rs[r], 0, nr);
+            S = stage_slice(rc, 1, a.Ss[r], 0, ns);
+        } else {
+            R = stage_slice(rc, 0, a.R, perR * r, nr);
+            S = stage_slice(rc, 1, a.S, perS * r, ns);
+        }
         uint64_t onR = 0, onS = 0, loc = 0;
         total[r] = rc.rank.run(R, nr, S, ns, a.opt, &onR, &onS, &loc);
         out.nR[r] = onR;
@@ -431,7 +485,20 @@ void run_call(Group& grp, CallArgs a, CallOut& out) {
         }
     out.total = total[0];
     out.stats = grp.ranks[0]->rank.stats;
+    out.ranks.clear();
+    for (int r = 0; r < G; r++) out.ranks.push_back(grp.ranks[r]->rank.stats);
     out.ms = (t1.tv_sec - t0.tv_sec) * 1e3 + (t1.tv_usec - t0.tv_usec) * 1e-3;
+    g_last_stats = out.ranks;
+    g_last_ms = out.ms;
+}
+
+// the rank with the longest busy span (the reference prints thread 0's
+// phases after a barrier; here the slowest GPU sets the step)
+const mg::Stats& slowest(const CallOut& o) {
+    size_t k = 0;
+    for (size_t r = 1; r < o.ranks.size(); r++)
+        if (o.ranks[r].busy_ms > o.ranks[k].busy_ms) k = r;
+    return o.ranks[k];
 }
 
 }  // namespace
@@ -476,13 +543,25 @@ result_t* mpsm_api(relation_t* relR, relation_t* relS, joinconfig_t* joincfg, in
         res->resultlist[r].threadid = (uint32_t)r;
     }
     if (!getenv("SMJ_QUIET")) {
-        // the reference's stats lines (joincommon.c:176-196); host microseconds
-        const unsigned long long us = (unsigned long long)(o.ms * 1e3);
+        // the reference's stats lines (joincommon.c:176-196): cumulative
+        // phase ends of the slowest rank, device nanoseconds (the reference
+        // prints cycles): partitioning = the range partitions and their
+        // tables, then the exchange (the main stream's wait for the rows:
+        // sortmergejoin_multiway.c:463-556 gathers the co-partitions there),
+        // then the local join (sort + merge-join count), then the all-reduce
+        const mg::Stats& x = slowest(o);
+        const double p = x.part_ms + x.tables_ms, xw = p + x.wait_ms, j = xw + x.join_ms;
+        auto ns = [](double ms) { return (unsigned long long)(ms * 1e6); };
         fprintf(stdout, "Total, Partitioning, Sort, First-Merge, Merge, Join\n");
-        fprintf(stdout, "%llu, 0, 0, 0, 0, %llu\n", us, us);
+        fprintf(stdout, "%llu, %llu, %llu, %llu, %llu, %llu\n", ns(x.busy_ms), ns(p), ns(xw),
+                ns(xw), ns(j), ns(x.busy_ms));
         fprintf(stdout, "[INFO ] mpsm: %d GPU%s, exchange in %s, 2^%u partitions, %d "
                         "attempts\n", G, G > 1 ? "s" : "", mg::layout_name(o.stats.layout),
                 o.stats.pbits, o.stats.attempts);
+        fprintf(stdout, "[INFO ] mpsm phases (ms, slowest rank): partition %.3f, tables %.3f, "
+                        "exchange wait %.3f, local join %.3f, all-reduce %.3f, busy %.3f; "
+                        "rows stream %.3f\n", x.part_ms, x.tables_ms, x.wait_ms, x.join_ms,
+                x.reduce_ms, x.busy_ms, x.rows_ms);
         fprintf(stderr, "NUM-TUPLES = %lld TOTAL-TIME-USECS = %.4lf ", (long long)a.nS,
                 o.ms * 1e3);
         fprintf(stderr, "TUPLES-PER-SECOND = %.4lf ", a.nS / (o.ms * 1e-3));
@@ -538,23 +617,95 @@ int64_t smj_mgpu_join(const tuple_t* R, uint64_t nR, const tuple_t* S, uint64_t 
             rank_counts[2 * r] = o.nR[r];
             rank_counts[2 * r + 1] = o.nS[r];
         }
-    if (stats) {
-        stats->layout = o.stats.layout;
-        stats->pbits = o.stats.pbits;
-        stats->attempts = o.stats.attempts;
-        stats->replans = o.stats.replans;
-        stats->sent_bytes = o.stats.sent_B;
-        stats->recv_bytes = o.stats.recv_B;
-        stats->key_min = o.stats.kmin;
-        stats->key_max = o.stats.kmax;
-        stats->ms = o.ms;
-    }
+    if (stats) fill_stats(o.stats, o.ms, stats);
     return (int64_t)o.total;
+}
+
+int64_t smj_mgpu_join_slices(const tuple_t* const* R, const uint64_t* nR,
+                             const tuple_t* const* S, const uint64_t* nS, int nranks,
+                             uint32_t flags, int64_t key_min, int64_t key_max,
+                             uint64_t* rank_counts, smj_mgpu_stats* stats) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        fprintf(stderr, "[ERROR] smj: no HIP device visible; the MI355X library has no CPU "
+                        "fallback.\n");
+        abort();
+    }
+    if (nranks < 1 || nranks > 64 || !R || !S || !nR || !nS) {
+        fprintf(stderr, "[ERROR] smj_mgpu_join_slices: %d ranks (1..64) and four arrays\n",
+                nranks);
+        abort();
+    }
+    const int G = nranks;
+    std::lock_guard<std::mutex> lk(g_mu);
+    int dev0 = 0;
+    SMJ_CHECK(hipGetDevice(&dev0));
+    Group& grp = group_for(G, !(flags & SMJ_MG_COPY));
+    CallArgs a;
+    a.R = a.S = nullptr;
+    a.nR = a.nS = 0;
+    uint64_t totR = 0;
+    for (int r = 0; r < G; r++) {
+        a.nR += nR[r];
+        a.nS += nS[r];
+        totR += nR[r];
+    }
+    a.Rs = (const Tup* const*)R;
+    a.nRs = nR;
+    a.Ss = (const Tup* const*)S;
+    a.nSs = nS;
+    if (key_min <= key_max) {
+        a.opt.kmin = key_min;
+        a.opt.kmax = key_max;
+    } else {
+        a.opt.guess_max = totR;
+    }
+    a.opt.planes = !(flags & SMJ_MG_NOPLANES);
+    a.opt.staged = !(flags & SMJ_MG_ONECALL);
+    a.opt.sampled = (flags & SMJ_MG_SAMPLED) ? 1 : (flags & SMJ_MG_EXACT) ? 0 : -1;
+    CallOut o;
+    run_call(grp, a, o);
+    SMJ_CHECK(hipSetDevice(dev0));
+    if (rank_counts)
+        for (int r = 0; r < G; r++) {
+            rank_counts[2 * r] = o.nR[r];
+            rank_counts[2 * r + 1] = o.nS[r];
+        }
+    if (stats) fill_stats(o.stats, o.ms, stats);
+    return (int64_t)o.total;
+}
+
+smj_workspace* smj_mgpu_group_workspace(int rank) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_group || rank < 0 || rank >= g_group->G) return nullptr;
+    return g_group->ranks[rank]->ops.w();
+}
+
+int smj_mgpu_last_stats(int rank, smj_mgpu_stats* out) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (rank < 0 || rank >= (int)g_last_stats.size() || !out) return -1;
+    fill_stats(g_last_stats[rank], g_last_ms, out);
+    return 0;
+}
+
+int smj_mgpu_last_sorted(int rank, tuple_t** sortedR, uint64_t* nR, tuple_t** sortedS,
+                         uint64_t* nS) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_group || rank < 0 || rank >= g_group->G) return -1;
+    DevRank& k = g_group->ranks[rank]->rank;
+    uint64_t n[2] = {0, 0};
+    k.sorted_sizes(&n[0], &n[1]);
+    if (sortedR) *sortedR = (tuple_t*)k.sorted[0];
+    if (sortedS) *sortedS = (tuple_t*)k.sorted[1];
+    if (nR) *nR = n[0];
+    if (nS) *nS = n[1];
+    return 0;
 }
 
 void smj_mgpu_release(void) {
     std::lock_guard<std::mutex> lk(g_mu);
     g_group.reset();
+    g_last_stats.clear();
 }
 
 // ---- one rank of a multi-process group (one process per GPU: bench.py
@@ -629,18 +780,9 @@ int64_t smj_mgpu_rank_join(smj_mgpu_comm* c, const tuple_t* R, uint64_t nR, cons
     if (sortedS) *sortedS = (tuple_t*)rc.rank.sorted[1];
     if (nR_out) *nR_out = onR;
     if (nS_out) *nS_out = onS;
-    if (stats) {
-        const mg::Stats& x = rc.rank.stats;
-        stats->layout = x.layout;
-        stats->pbits = x.pbits;
-        stats->attempts = x.attempts;
-        stats->replans = x.replans;
-        stats->sent_bytes = x.sent_B;
-        stats->recv_bytes = x.recv_B;
-        stats->key_min = x.kmin;
-        stats->key_max = x.kmax;
-        stats->ms = (t1.tv_sec - t0.tv_sec) * 1e3 + (t1.tv_usec - t0.tv_usec) * 1e-3;
-    }
+    if (stats)
+        fill_stats(rc.rank.stats,
+                   (t1.tv_sec - t0.tv_sec) * 1e3 + (t1.tv_usec - t0.tv_usec) * 1e-3, stats);
     SMJ_CHECK(hipSetDevice(dev0));
     return (int64_t)total;
 }

@@ -15,7 +15,7 @@
 //      rank owner(p) = p * G / F, so every rank owns one contiguous key range;
 //   2. a table message (the owned regions' offsets and counts, two flags) to
 //      every rank over the collective, the receive tables built on the device,
-//      one small summary read by the host (every flag is a maximum over all
+//      one small summary read by the host (every flag is OR-ed over all
 //      ranks, so every rank takes the same decisions);
 //   3. the rows: grouped send/recv of each chunk to its owner, peers in NEXT
 //      order, pieces of at most 512 MB;
@@ -43,6 +43,8 @@
 //   void fill_u32(void* p, uint32_t v, size_t count, int stream);
 //   void record(int ev, int stream); void wait(int stream, int ev);
 //   void host_wait(int ev); void sync(int stream);
+//   void tmark(int mark, int stream);           a timing mark (TMark)
+//   double tspan(int a, int b);                 ms between two completed marks
 //   uint32_t shards(); uint64_t sampled_capacity(uint64_t n, uint32_t nbits);
 //   int  part_planes(in, n, out, stride, nbits, kmin, kmax, ss, sc, flags);
 //   int  part_sampled(in, n, out, nbits, kmin, kmax, packed, ss, sc, flags);
@@ -94,6 +96,13 @@ enum Stream : int { kMain = 0, kRows = 1 };
 // events of one rank (Ops::record / wait)
 enum Event : int { kEvAttemptR = 0, kEvAttemptS = 1, kEvRowsR = 2, kEvRowsS = 3, kEvMain = 4,
                    kNumEvents = 5 };
+// timing marks of one rank (Ops::tmark / tspan), the phases of Stats: the
+// start and end of the call on kMain; per relation r the start of its range
+// partition, its end, the end of its table messages (kTPart0 + 3 r + 0/1/2);
+// per relation its row exchange on kRows (kTRows0 + 2 r + 0/1); the local
+// join (one call: J0-J1; staged: J0-J1 and J2-J3)
+enum TMark : int { kTStart = 0, kTPart0 = 1, kTRows0 = 7, kTJoin0 = 11, kTJoin1 = 12,
+                   kTJoin2 = 13, kTJoin3 = 14, kTEnd = 15, kNumTMarks = 16 };
 
 typedef __int128 i128;
 
@@ -165,7 +174,7 @@ inline LocalRange local_range(int64_t kmin, int64_t kmax, uint32_t pbits, uint32
 }
 
 // the layout and form an invalid attempt repeats with, on every rank alike
-// (bad / ovf are maxima over the ranks; dist.py _next_layout)
+// (bad / ovf are OR-ed over the ranks; dist.py _next_layout)
 inline void next_layout(int& lay, bool& sampled, uint32_t bad, uint32_t ovf, bool can_pack,
                         bool default_sampled) {
     if (lay == kPlanes) {
@@ -286,6 +295,13 @@ struct Stats {
     int replans = 0;            // guessed range replaced by the measured one
     uint64_t sent_B = 0, recv_B = 0;
     int64_t kmin = 0, kmax = 0; // the global plan's range
+    // device phases of the call in ms (Ops::tspan).  On kMain they are
+    // consecutive, so part + tables + wait + join + reduce = busy: wait is
+    // kMain idle (host decisions, the key-range pass of a re-plan, and the
+    // part of the row exchange the local work did not hide).  rows is the
+    // row exchange on kRows, which overlaps the others.
+    double part_ms = 0, tables_ms = 0, wait_ms = 0, join_ms = 0, reduce_ms = 0, busy_ms = 0,
+           rows_ms = 0;
 };
 
 template <class Ops, class Coll>
@@ -437,6 +453,7 @@ struct Rank {
         void* xb = s.xb[lay];
         const size_t FK = (size_t)F * K;
         bool done = false;
+        ops->tmark(kTPart0 + 3 * r, kMain);
         if (nn == 0) {  // nothing to partition: empty tables
             ops->fill_u32(a.ss, 0, 2 * FK, kMain);
             ops->fill_u32(a.sc, 0, 2 * FK, kMain);
@@ -446,11 +463,13 @@ struct Rank {
             if (!ops->part_planes(in[r], nn, xb, s.xcap[lay], pbits, lr.base, kmax, a.ss, a.sc,
                                   a.flags)) {
                 // the form does not apply on this rank: empty tables flagged
-                // as too wide for 48 bits, so every rank drops the layout
+                // as too wide for 48 bits, so every rank drops the layout.  A
+                // guessed range was not checked then, so the flag also asks
+                // for the measured range (the other forms do not check it)
                 ops->fill_u32(a.ss, 0, 2 * FK, kMain);
                 ops->fill_u32(a.sc, 0, 2 * FK, kMain);
                 ops->fill_u32(a.flags, 0, 1, kMain);
-                ops->fill_u32(a.flags + 1, kBadPayload48, 1, kMain);
+                ops->fill_u32(a.flags + 1, kBadPayload48 | (guessed ? kBadRange : 0u), 1, kMain);
             }
             done = true;
         } else if (sampled) {
@@ -472,6 +491,7 @@ struct Rank {
             }
             ops->hist_tables(a.hist, F, K, a.ss, a.sc);
         }
+        ops->tmark(kTPart0 + 3 * r + 1, kMain);
         ops->xsend(a.ss, a.sc, a.flags, F, K, (uint32_t)G, a.msg_in, a.chunk);
         const uint64_t row = kHead + 2ull * K * mine;
         const int64_t* msg = a.msg_in;
@@ -490,6 +510,7 @@ struct Rank {
         ops->xrecv(msg, a.chunk, (uint32_t)G, (uint32_t)me, mine, K, 1u << lr.lbits, a.cap,
                    a.tstart, a.tcnt, a.summary);
         ops->to_host(s.host, a.summary, (4ull * G + 2) * 8, kMain);
+        ops->tmark(kTPart0 + 3 * r + 2, kMain);
         ops->record(kEvAttemptR + r, kMain);
         stats.attempts++;
     }
@@ -502,6 +523,8 @@ struct Rank {
         RelState& s = rel[r];
         for (;;) {
             ops->host_wait(kEvAttemptR + r);
+            stats.part_ms += ops->tspan(kTPart0 + 3 * r, kTPart0 + 3 * r + 1);
+            stats.tables_ms += ops->tspan(kTPart0 + 3 * r + 1, kTPart0 + 3 * r + 2);
             const int64_t* h = s.host;
             const uint32_t bad = (uint32_t)h[4 * G], ovf = (uint32_t)h[4 * G + 1];
             if (!ovf && !(a.lay != kTuples && bad)) break;
@@ -539,7 +562,11 @@ struct Rank {
             // after a grown buffer's copy on kMain
             if (moved) ops->record(kEvMain, kMain);
             ops->wait(kRows, moved ? kEvMain : kEvAttemptR + r);
+            rows_time(r);
+            ops->tmark(kTRows0 + 2 * r, kRows);
             rows(v, cs, sl, rl);
+            ops->tmark(kTRows0 + 2 * r + 1, kRows);
+            rows_marked[r] = true;
             ops->record(kEvRowsR + r, kRows);
         }
         return 1;
@@ -581,6 +608,16 @@ struct Rank {
             }
         }
         coll->exchange(kRows, sends, recvs);
+    }
+
+    // the row exchange of relation r timed so far (before its marks are
+    // recorded again, and at the end of the call)
+    bool rows_marked[2] = {false, false};
+    void rows_time(int r) {
+        if (!rows_marked[r]) return;
+        ops->sync(kRows);
+        stats.rows_ms += ops->tspan(kTRows0 + 2 * r, kTRows0 + 2 * r + 1);
+        rows_marked[r] = false;
     }
 
     void set_plan(int64_t kmin_, int64_t kmax_) {
@@ -637,6 +674,8 @@ struct Rank {
         n[1] = nS;
         opt = o;
         stats = Stats();
+        rows_marked[0] = rows_marked[1] = false;
+        ops->tmark(kTStart, kMain);
         K = ops->shards();
         default_sampled = o.sampled < 0 ? G == 1 : o.sampled != 0;
         if (!count) {
@@ -706,28 +745,47 @@ struct Rank {
                       v[1].stride, v[1].nused, v[1].tstart, v[1].tcnt, nseg, lr.lbits, lr.key_lo,
                       lr.key_hi, stage, sorted[0], sorted[1], count);
         };
+        bool two = false;
         if (v[0].nused == 0 && v[1].nused == 0) {
             if (G > 1) {
                 ops->wait(kMain, kEvRowsR);
                 ops->wait(kMain, kEvRowsS);
             }
+            ops->tmark(kTJoin0, kMain);
             ops->fill_u32(count, 0, 2, kMain);
+            ops->tmark(kTJoin1, kMain);
         } else if (G > 1 && opt.staged) {
             ops->wait(kMain, kEvRowsR);
+            ops->tmark(kTJoin0, kMain);
             join(1);
+            ops->tmark(kTJoin1, kMain);
             ops->wait(kMain, kEvRowsS);
+            ops->tmark(kTJoin2, kMain);
             join(2);
+            ops->tmark(kTJoin3, kMain);
+            two = true;
         } else {
             if (G > 1) {
                 ops->wait(kMain, kEvRowsR);
                 ops->wait(kMain, kEvRowsS);
             }
+            ops->tmark(kTJoin0, kMain);
             join(0);
+            ops->tmark(kTJoin1, kMain);
         }
         ops->copy(count + 1, count, 8, kMain);
         coll->allreduce_sum_u64(kMain, count + 1);
+        ops->tmark(kTEnd, kMain);
         ops->to_host(count_h, count, 16, kMain);
         ops->sync(kMain);
+        // the phases (every mark on kMain has completed; the rows' marks too:
+        // kMain waited for the rows)
+        stats.join_ms = ops->tspan(kTJoin0, kTJoin1) + (two ? ops->tspan(kTJoin2, kTJoin3) : 0.0);
+        stats.reduce_ms = ops->tspan(two ? kTJoin3 : kTJoin1, kTEnd);
+        stats.busy_ms = ops->tspan(kTStart, kTEnd);
+        stats.wait_ms = std::max(0.0, stats.busy_ms - stats.part_ms - stats.tables_ms -
+                                          stats.join_ms - stats.reduce_ms);
+        for (int r = 0; r < 2; r++) rows_time(r);
         *nR_out = last_n[0] = v[0].nused;
         *nS_out = last_n[1] = v[1].nused;
         *local = count_h[0];

@@ -1675,13 +1675,7 @@ static void partition_hist_scatter(Workspace* ws, const Tup* in, uint64_t n,
     if (n == 0) return;
     if constexpr (!STABLE) {
         const size_t ldsu = scatter_u_lds<THREADS, ITEMS>(nbins);
-        static bool attr_u = false;
-        if (!attr_u) {
-            SMJ_CHECK(hipFuncSetAttribute(
-                (const void*)k_scatter_u<THREADS, ITEMS, Digit, Pack>,
-                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-            attr_u = true;
-        }
+        set_lds_attr((const void*)k_scatter_u<THREADS, ITEMS, Digit, Pack>, 160 * 1024);
         if (ldsu > 160 * 1024) {
             fprintf(stderr, "[ERROR] smj: scatter LDS %zu > 160 KiB\n", ldsu);
             abort();
@@ -1697,13 +1691,7 @@ static void partition_hist_scatter(Workspace* ws, const Tup* in, uint64_t n,
         // histogram's chunking, so counts[d][wg] match)
         typedef SwcGeom<512, 8> SG;
         if (nbins <= 4 * 512 && SG::lds_bytes(nbins) <= 160 * 1024) {
-            static bool attr_w = false;
-            if (!attr_w) {
-                SMJ_CHECK(hipFuncSetAttribute(
-                    (const void*)k_scatter_swc<512, 8, Digit>,
-                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-                attr_w = true;
-            }
+            set_lds_attr((const void*)k_scatter_swc<512, 8, Digit>, 160 * 1024);
             TraceScope ts(ws, "k_scatter", st);
             hipLaunchKernelGGL((k_scatter_swc<512, 8, Digit>), dim3(nwg), dim3(512),
                                SG::lds_bytes(nbins), st, in, n, chunk, dig, nbins, dbits,
@@ -1712,13 +1700,7 @@ static void partition_hist_scatter(Workspace* ws, const Tup* in, uint64_t n,
             return;
         }
         const size_t lds = scatter_lds<THREADS, ITEMS>(nbins);
-        static bool attr_set = false;
-        if (!attr_set) {
-            SMJ_CHECK(hipFuncSetAttribute(
-                (const void*)k_scatter<THREADS, ITEMS, Digit>,
-                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-            attr_set = true;
-        }
+        set_lds_attr((const void*)k_scatter<THREADS, ITEMS, Digit>, 160 * 1024);
         if (lds > 160 * 1024) {
             fprintf(stderr, "[ERROR] smj: scatter LDS %zu > 160 KiB\n", lds);
             abort();
@@ -1792,12 +1774,7 @@ static void stable_partition_swp(Workspace* ws, const Tup* in, uint64_t n, Tup* 
                            starts_dev, hist_out, off_out);
     }
     if (n == 0) return;
-    static bool attr = false;
-    if (!attr) {
-        SMJ_CHECK(hipFuncSetAttribute((const void*)k_scatter_swp<THREADS, ITEMS, Digit, true>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        attr = true;
-    }
+    set_lds_attr((const void*)k_scatter_swp<THREADS, ITEMS, Digit, true>, 160 * 1024);
     TraceScope ts(ws, "k_scatter", st);
     hipLaunchKernelGGL((k_scatter_swp<THREADS, ITEMS, Digit, true>), dim3(nwg), dim3(THREADS),
                        G::lds_bytes(nbins), st, in, n, chunk, dig, nbins, counts, nwg,
@@ -1921,13 +1898,7 @@ void plan_partition(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
                            starts_dev, hist_out, (int64_t*)nullptr);
     }
     if (n == 0) return;
-    static bool attr = false;
-    if (!attr) {
-        SMJ_CHECK(hipFuncSetAttribute(
-            (const void*)k_scatter_wc<THREADS, ITEMS, PlanDigit1>,
-            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        attr = true;
-    }
+    set_lds_attr((const void*)k_scatter_wc<THREADS, ITEMS, PlanDigit1>, 160 * 1024);
     TraceScope ts(ws, "k_scatter", st);
     hipLaunchKernelGGL((k_scatter_wc<THREADS, ITEMS, PlanDigit1>), dim3(nwg),
                        dim3(THREADS), lds, st, in, n, chunk, dig, nbins, counts,
@@ -2020,18 +1991,11 @@ static bool sampled_scatter_t(Workspace* ws, const Tup* in, uint64_t n, void* ou
     const uint64_t tiles_per_wg = (ntiles + nwg - 1) / nwg;
     const uint64_t chunk = tiles_per_wg * TILE;
     nwg = (uint32_t)((ntiles + tiles_per_wg - 1) / tiles_per_wg);
-    static bool attr = false;
     constexpr bool VEC_OK = sizeof(Tup) == 8 && ITEMS % 2 == 0;
-    if (!attr) {
-        SMJ_CHECK(hipFuncSetAttribute(
-            (const void*)k_scatter_res<THREADS, ITEMS, PlanDigit1, Pack, false>,
-            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        if constexpr (VEC_OK)
-            SMJ_CHECK(hipFuncSetAttribute(
-                (const void*)k_scatter_res<THREADS, ITEMS, PlanDigit1, Pack, true>,
-                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        attr = true;
-    }
+    set_lds_attr((const void*)k_scatter_res<THREADS, ITEMS, PlanDigit1, Pack, false>, 160 * 1024);
+    if constexpr (VEC_OK)
+        set_lds_attr((const void*)k_scatter_res<THREADS, ITEMS, PlanDigit1, Pack, true>,
+                     160 * 1024);
     TraceScope ts(ws, "k_scatter", st);
     bool vec = false;
     if constexpr (VEC_OK) {

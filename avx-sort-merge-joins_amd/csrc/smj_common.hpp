@@ -26,7 +26,25 @@
         }                                                                      \
     } while (0)
 
+#include <mutex>
+#include <set>
+#include <utility>
+
 namespace smj {
+
+// hipFuncSetAttribute(kernel, MaxDynamicSharedMemorySize, bytes) once per
+// (device, kernel): the attribute is held per device, and the in-process
+// multi-GPU join (mgpu.hip) launches from one host thread per device at once.
+// The attribute is set under the lock, so no thread launches before it holds.
+inline void set_lds_attr(const void* kernel, int bytes) {
+    static std::mutex mu;
+    static std::set<std::pair<int, const void*>> done;
+    int dev = 0;
+    SMJ_CHECK(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(mu);
+    if (!done.insert({dev, kernel}).second) return;
+    SMJ_CHECK(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+}
 
 #ifdef KEY_8B
 struct __attribute__((aligned(16))) Tup {

@@ -67,7 +67,8 @@ DEVICE_SYMBOLS = [
     "smj_dev_join_segmented_planes", "smj_mgpu_join", "smj_mgpu_release",
     "smj_inregister_sort_keyval32", "smj_workspace_set_layouts", "smj_mgpu_unique_id",
     "smj_mgpu_comm_init", "smj_mgpu_rank_join", "smj_mgpu_comm_destroy", "smj_mgpu_rank_sorted",
-    "smj_mgpu_comm_workspace", "smj_workspace_last_layout",
+    "smj_mgpu_comm_workspace", "smj_workspace_last_layout", "smj_mgpu_join_slices",
+    "smj_mgpu_last_stats", "smj_mgpu_last_sorted", "smj_mgpu_group_workspace",
 ]
 
 
@@ -105,7 +106,16 @@ class MgpuStats(C.Structure):
     """include/smj.h smj_mgpu_stats."""
     _fields_ = [("layout", C.c_int), ("pbits", C.c_uint32), ("attempts", C.c_int),
                 ("replans", C.c_int), ("sent_bytes", C.c_uint64), ("recv_bytes", C.c_uint64),
-                ("key_min", C.c_int64), ("key_max", C.c_int64), ("ms", C.c_double)]
+                ("key_min", C.c_int64), ("key_max", C.c_int64), ("ms", C.c_double),
+                # device phases, ms (the five before busy_ms add up to it)
+                ("partition_ms", C.c_double), ("tables_ms", C.c_double),
+                ("wait_ms", C.c_double), ("join_ms", C.c_double), ("reduce_ms", C.c_double),
+                ("busy_ms", C.c_double), ("rows_ms", C.c_double)]
+
+    def as_dict(self):
+        d = {f: getattr(self, f) for f, _ in self._fields_}
+        d["layout"] = MG_LAYOUTS[d["layout"]]
+        return d
 
 
 # smj_workspace_set_layouts bits (include/smj.h)
@@ -137,8 +147,7 @@ class MgpuComm:
         c = L.lib.smj_mgpu_rank_join(self.h, R.data_ptr(), R.shape[0], S.data_ptr(),
                                      S.shape[0], flags, kmin, kmax, guess_max, None,
                                      C.byref(nR), None, C.byref(nS), C.byref(st))
-        stats = {f: getattr(st, f) for f, _ in MgpuStats._fields_}
-        stats["layout"] = MG_LAYOUTS[stats["layout"]]
+        stats = st.as_dict()
         self.n = (nR.value, nS.value)
         return int(c), nR.value, nS.value, stats
 
@@ -166,6 +175,22 @@ _P = C.c_void_p
 _U64 = C.c_uint64
 _I64 = C.c_int64
 _U32 = C.c_uint32
+
+
+_HIP = None
+
+
+def _hip_copy(dst: int, src: int, nbytes: int) -> None:
+    """hipMemcpy(dst, src, nbytes, hipMemcpyDefault) through the HIP runtime
+    torch has loaded (device pointers the library hands out)."""
+    global _HIP
+    if _HIP is None:
+        _HIP = C.CDLL("libamdhip64.so")
+        _HIP.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        _HIP.hipMemcpy.restype = C.c_int
+    rc = _HIP.hipMemcpy(dst, src, nbytes, 4)
+    if rc != 0:
+        raise RuntimeError(f"hipMemcpy failed: {rc}")
 
 
 def _ptr(a):
@@ -262,6 +287,10 @@ class Library:
             "smj_mgpu_join": (_I64, [_P, _U64, _P, _U64, C.c_int, _U32, _I64, _I64, _P, _P,
                                      _P, _P]),
             "smj_mgpu_release": (None, []),
+            "smj_mgpu_join_slices": (_I64, [_P, _P, _P, _P, C.c_int, _U32, _I64, _I64, _P, _P]),
+            "smj_mgpu_last_stats": (C.c_int, [C.c_int, _P]),
+            "smj_mgpu_group_workspace": (_P, [C.c_int]),
+            "smj_mgpu_last_sorted": (C.c_int, [C.c_int, _P, _P, _P, _P]),
             "smj_mgpu_unique_id": (C.c_int, [_P, C.c_int]),
             "smj_mgpu_comm_init": (_P, [_P, C.c_int, C.c_int]),
             "smj_mgpu_rank_join": (_I64, [_P, _P, _U64, _P, _U64, _U32, _I64, _I64, _U64,
@@ -426,6 +455,10 @@ class Library:
         (None unless sorted_out)."""
         dev = not isinstance(R, np.ndarray)
         if dev:
+            # the ranks read device inputs on their own streams, which do not
+            # wait for torch's: order the call after every pending write
+            for t in (R, S):
+                torch.cuda.current_stream(t.device).synchronize()
             nR, nS = R.shape[0], S.shape[0]
             pR, pS = R.data_ptr(), S.data_ptr()
             sR = R.new_empty(R.shape) if sorted_out else None
@@ -450,9 +483,54 @@ class Library:
         kmin, kmax = key_range if key_range is not None else (1, 0)
         c = self.lib.smj_mgpu_join(pR, nR, pS, nS, G, flags, kmin, kmax, qR, qS,
                                    _ptr(counts), C.byref(st))
-        stats = {f: getattr(st, f) for f, _ in MgpuStats._fields_}
-        stats["layout"] = MG_LAYOUTS[stats["layout"]]
-        return int(c), sR, sS, counts.reshape(G, 2), stats
+        return int(c), sR, sS, counts.reshape(G, 2), st.as_dict()
+
+    def mgpu_join_slices(self, Rs, Ss, flags=0, key_range=None):
+        """smj_mgpu_join_slices: rank g joins the slices Rs[g] and Ss[g]
+        (device tensors on GPU g, shape (n, 2); read in place) -- a relation
+        already sharded over the GPUs' HBM, one host thread per GPU inside
+        this process (the reference's T join threads, joincommon.c:118-165).
+        Returns (count, per-rank (nR, nS) sorted, [per-rank stats dicts]);
+        mgpu_last_sorted(g) copies rank g's sorted shares out."""
+        G = len(Rs)
+        assert G == len(Ss) and G >= 1
+        for t in list(Rs) + list(Ss):
+            torch.cuda.current_stream(t.device).synchronize()
+        P, U = C.c_void_p * G, C.c_uint64 * G
+        pR = P(*[t.data_ptr() if t.shape[0] else None for t in Rs])
+        pS = P(*[t.data_ptr() if t.shape[0] else None for t in Ss])
+        nR = U(*[t.shape[0] for t in Rs])
+        nS = U(*[t.shape[0] for t in Ss])
+        counts = np.zeros(2 * G, np.uint64)
+        st = MgpuStats()
+        kmin, kmax = key_range if key_range is not None else (1, 0)
+        c = self.lib.smj_mgpu_join_slices(pR, nR, pS, nS, G, flags, kmin, kmax, _ptr(counts),
+                                          C.byref(st))
+        return int(c), counts.reshape(G, 2), [self.mgpu_last_stats(g) for g in range(G)]
+
+    def mgpu_last_stats(self, rank):
+        """smj_mgpu_last_stats: rank `rank`'s stats of the last smj_mgpu_join /
+        _slices call (its device phases)."""
+        st = MgpuStats()
+        if self.lib.smj_mgpu_last_stats(rank, C.byref(st)) != 0:
+            raise IndexError(f"no rank {rank} in the last multi-GPU join")
+        return st.as_dict()
+
+    def mgpu_last_sorted(self, rank, device):
+        """Rank `rank`'s sorted shares of the last smj_mgpu_join / _slices
+        call, copied into new tensors on `device` (the rank's GPU)."""
+        pR, pS = C.c_void_p(), C.c_void_p()
+        nR, nS = C.c_uint64(), C.c_uint64()
+        if self.lib.smj_mgpu_last_sorted(rank, C.byref(pR), C.byref(nR), C.byref(pS),
+                                         C.byref(nS)) != 0:
+            raise IndexError(f"no rank {rank} in the last multi-GPU join")
+        out = []
+        for p, n in ((pR, nR.value), (pS, nS.value)):
+            t = self.empty(n, device=device)
+            if n:
+                _hip_copy(t.data_ptr(), p.value, n * self.width)
+            out.append(t)
+        return tuple(out)
 
     def mgpu_comm(self, nranks, rank, group=None):
         """smj_mgpu_comm_init for this process's rank of a torch.distributed

@@ -243,8 +243,8 @@ def xsend_torch(start, cnt, flags, world, msg, chunk):
 def xrecv_torch(msg, chunk, world, rank, mine, K, tstart, tcnt, cap, summary):
     """smj_dev_xrecv in framework ops: the local join's segment tables (own
     chunk in place, the other ranks' rows from `cap` on, rank order) and the
-    summary [chunk starts | sizes | receive sizes | used received | max
-    flags]."""
+    summary [chunk starts | sizes | receive sizes | used received | the
+    flags OR-ed over the ranks]."""
     G = world
     m = msg.view(G, HEAD + 2 * mine * K)
     rl = m[:, 0].tolist()
@@ -262,7 +262,11 @@ def xrecv_torch(msg, chunk, world, rank, mine, K, tstart, tcnt, cap, summary):
     summary[:2 * G] = chunk
     summary[2 * G:3 * G] = m[:, 0]
     summary[3 * G:4 * G] = m[:, 1]
-    summary[4 * G:4 * G + 2] = m[:, 2:HEAD].max(0).values
+    fl = m[:, 2:HEAD]  # bit masks: OR-ed over the ranks (every rank's reasons)
+    acc = fl[0].clone()
+    for g in range(1, G):
+        acc |= fl[g]
+    summary[4 * G:4 * G + 2] = acc
 
 
 class DeviceOps:
@@ -588,7 +592,7 @@ class DistributedJoin:
 
     def _next_layout(self, lay, sampled, bad, ovf):
         """The layout and form an invalid attempt repeats with, on every rank
-        alike (bad and ovf are maxima over the ranks): a region overflow ->
+        alike (bad and ovf are OR-ed over the ranks): a region overflow ->
         exact partitions (planes have no exact form: words, else tuples);
         a payload too wide for 48 bits -> words; anything else unpackable ->
         tuples."""

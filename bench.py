@@ -48,6 +48,38 @@ def set_payloads(R, S, kind, first):
             t[:, 0] = z ^ (z >> 29)
 
 
+def shares(a, N):
+    """(tuples per relation on each rank, first global row of each, total):
+    weak scaling gives every rank --n; --n-total splits a fixed total."""
+    if a.n_total is not None:
+        total = a.n_total
+        base = total // N
+        ns = [base] * (N - 1) + [total - base * (N - 1)]
+    else:
+        total = a.n * N
+        ns = [a.n] * N
+    return ns, [sum(ns[:g]) for g in range(N)], total
+
+
+def make_relations(lib, a, n, first, total, device="cuda"):
+    """This rank's slices of R (PK: keys first+1.. of a permutation of
+    1..total) and S (FK uniform, or Zipf) generated in HBM on `device`."""
+    R = lib.empty(n, device=device)
+    S = lib.empty(n, device=device)
+    lib.dev_gen_pk(R, first, total, 12345)
+    if a.zipf_gen == "auto":
+        a.zipf_gen = "reference" if total <= (1 << 28) else "fast"
+    if a.dist == "uniform":
+        lib.dev_gen_fk(S, first, total, total, 54321)
+    elif a.zipf_gen == "reference":
+        lib.dev_gen_zipf_ref(S, first, total, a.theta, 54321)
+    else:
+        lib.dev_gen_zipf(S, first, total, a.theta, 54321)
+    set_payloads(R, S, a.payload, first)
+    torch.cuda.synchronize()
+    return R, S
+
+
 def _close(dist):
     """Destroy the process group (and the join's cached row communicators)."""
     mod = sys.modules.get("smj.dist")
@@ -113,10 +145,18 @@ def parse():
     p.add_argument("--exchange-path", action="store_true",
                    help="run the multi-GPU code path (range partition, all-to-all, "
                         "segmented local join) even at N=1 (a one-rank RCCL group)")
-    p.add_argument("--impl", default="python", choices=("python", "c"),
-                   help="multi-GPU join: the torch.distributed orchestration (smj.dist) or "
-                        "the C entry smj_mgpu_rank_join (mgpu_orch.hpp, its own RCCL "
-                        "communicator per rank)")
+    p.add_argument("--impl", default="c", choices=("python", "c"),
+                   help="multi-GPU join under a launcher (one process per GPU): the C entry "
+                        "smj_mgpu_rank_join (mgpu_orch.hpp, its own RCCL communicators per "
+                        "rank; the line carries every rank's phases) or the torch.distributed "
+                        "orchestration (smj.dist)")
+    p.add_argument("--launch", default="auto", choices=("auto", "threads", "spawn"),
+                   help="--gpus N > 1 without a launcher (no WORLD_SIZE): threads = one "
+                        "process, one host thread per GPU through smj_mgpu_join_slices (the "
+                        "reference's T join threads, joincommon.c:118-165; the join only); "
+                        "spawn = start N processes under torch.distributed.run (the driver's "
+                        "form) and print rank 0's line; auto = threads for the join, spawn "
+                        "for the other ops")
     p.add_argument("--api", action="store_true",
                    help="join: time the reference-named entry point sortmergejoin_multiway "
                         "(relation_t over device-resident tuples, no key-range hint: the "
@@ -361,19 +401,66 @@ def output_check(pairs, w, dist=None):
 
 
 # --------------------------------------------------------------------------
+def _json_stdout():
+    """stdout carries exactly the one JSON line: native libraries (RCCL
+    prints a version banner at communicator setup) write to stderr instead.
+    Returns the file the line goes to."""
+    sys.stdout.flush()
+    out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    return out
+
+
+def standalone(a):
+    """--gpus N > 1 with no launcher (no WORLD_SIZE): N GPUs must be
+    visible, else exit 2 (a line for fewer GPUs than asked would be
+    mislabelled).  Then the join runs in this process with one host thread
+    per GPU (--launch threads), or N processes start under
+    torch.distributed.run (--launch spawn) and rank 0's line is relayed.
+    Returns the exit code.  Nothing here touches the GPU before the spawn
+    (device_count does not initialise it on this image)."""
+    vis = torch.cuda.device_count()
+    if vis < a.gpus:
+        print(f"[bench] ERROR: --gpus {a.gpus} but {vis} GPU(s) visible; no line is printed "
+              f"(run on a node with {a.gpus} GPUs, or under torch.distributed.run)",
+              file=sys.stderr)
+        return 2
+    launch = a.launch if a.launch != "auto" else ("threads" if a.op == "join" else "spawn")
+    if launch == "threads":
+        if a.op != "join" or a.exchange_path or a.api:
+            print("[bench] ERROR: --launch threads runs the join (smj_mgpu_join_slices) only",
+                  file=sys.stderr)
+            return 2
+        run_threads_join(a, _json_stdout())
+        return 0
+    import socket
+    with socket.socket() as sk:  # a free port for the rendezvous
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={a.gpus}", "--master-addr", "127.0.0.1", "--master-port",
+           str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"[bench] spawning: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, text=True)
+    sys.stdout.write(r.stdout)
+    sys.stdout.flush()
+    return r.returncode
+
+
 def main():
     a = parse()
-    # stdout carries exactly the one JSON line: native libraries (RCCL prints
-    # a version banner at communicator setup) write to stderr instead
-    sys.stdout.flush()
-    json_out = os.fdopen(os.dup(1), "w")
-    os.dup2(2, 1)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and (a.gpus > 1 or a.launch == "threads"):
+        sys.exit(standalone(a))
+    world = int(world_env or "1")
+    N = max(world, 1)
+    if a.gpus != N:
+        print(f"[bench] ERROR: --gpus {a.gpus} but the launcher started WORLD_SIZE={world} "
+              "rank(s); no line is printed", file=sys.stderr)
+        sys.exit(2)
+    json_out = _json_stdout()
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    N = max(world, 1)
-    if a.gpus != N and world > 1:
-        print(f"[bench] --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     torch.cuda.set_device(local)
     dist = None
     exchange = a.op == "join" and (N > 1 or a.exchange_path)
@@ -402,28 +489,9 @@ def main():
         run_op(a, lib, json_out, dist, N, rank)
         return
     w = a.width
-    if a.n_total is not None:  # strong scaling: the total is fixed
-        total = a.n_total
-        base = total // N
-        first = base * rank
-        n = base if rank < N - 1 else total - base * (N - 1)
-    else:  # weak scaling: n per GPU
-        n = a.n
-        total = n * N
-        first = n * rank
-    R = lib.empty(n)
-    S = lib.empty(n)
-    lib.dev_gen_pk(R, first, total, 12345)
-    if a.zipf_gen == "auto":
-        a.zipf_gen = "reference" if total <= (1 << 28) else "fast"
-    if a.dist == "uniform":
-        lib.dev_gen_fk(S, first, total, total, 54321)
-    elif a.zipf_gen == "reference":
-        lib.dev_gen_zipf_ref(S, first, total, a.theta, 54321)
-    else:
-        lib.dev_gen_zipf(S, first, total, a.theta, 54321)
-    set_payloads(R, S, a.payload, first)
-    torch.cuda.synchronize()
+    ns_, firsts, total = shares(a, N)
+    n, first = ns_[rank], firsts[rank]
+    R, S = make_relations(lib, a, n, first, total)
 
     count = torch.zeros(1, dtype=torch.int64, device="cuda")
     tracer = lib
@@ -455,7 +523,8 @@ def main():
             lib.dev_join(R, S, sR, sS, count, a.fanout_bits, 1, total)
     elif a.impl == "c":
         comm = lib.mgpu_comm(N, rank)
-        mg_st = {"steps": 0, "sent_B": 0, "recv_B": 0, "layout": None}
+        mg_st = {"steps": 0, "sent_B": 0, "recv_B": 0, "layout": None,
+                 "ph": dict.fromkeys(PHASES, 0.0)}
 
         def step():
             c, _, _, st = comm.join(R, S, key_range=(1, total))
@@ -464,6 +533,8 @@ def main():
             mg_st["sent_B"] += st["sent_bytes"]
             mg_st["recv_B"] += st["recv_bytes"]
             mg_st["layout"] = st["layout"]
+            for p in PHASES:
+                mg_st["ph"][p] += st[p]
         tracer = _WsTracer(lib, lib.lib.smj_mgpu_comm_workspace(comm.h))
     else:
         from smj.dist import DeviceOps, DistributedJoin
@@ -477,7 +548,7 @@ def main():
 
     def reset():
         if exchange and a.impl == "c":
-            mg_st.update(steps=0, sent_B=0, recv_B=0)
+            mg_st.update(steps=0, sent_B=0, recv_B=0, ph=dict.fromkeys(PHASES, 0.0))
         elif exchange:
             dj.stats_reset()
 
@@ -491,9 +562,16 @@ def main():
     xchg = None
     if exchange and a.impl == "c":
         k = max(mg_st["steps"], 1)
-        xchg = {"impl": "c (smj_mgpu_rank_join)",
-                "xgmi_bytes_sent_per_gpu": mg_st["sent_B"] // k,
-                "xgmi_bytes_recv_per_gpu": mg_st["recv_B"] // k,
+        # every rank's phases and bytes, averaged over the timed steps
+        mine = torch.tensor([mg_st["ph"][p] / k for p in PHASES]
+                            + [mg_st["sent_B"] / k, mg_st["recv_B"] / k],
+                            dtype=torch.float64, device="cuda")
+        rows = [mine]
+        if N > 1:
+            rows = [torch.empty_like(mine) for _ in range(N)]
+            dist.all_gather(rows, mine)
+        xchg = {"impl": "c (smj_mgpu_rank_join, one process per GPU)",
+                **rank_phases([r.tolist() for r in rows]),
                 "exchange_layout": mg_st["layout"], "xgmi_peak_GBps": 7 * 153}
     elif exchange:
         st = dj.stats_read()
@@ -596,6 +674,143 @@ def main():
     print(json.dumps(out), file=json_out, flush=True)
     if dist:
         _close(dist)
+
+
+PHASES = ("partition_ms", "tables_ms", "wait_ms", "join_ms", "reduce_ms", "busy_ms", "rows_ms")
+
+
+def rank_phases(rows):
+    """rows[g] = rank g's PHASES + (bytes sent, bytes received) per step ->
+    the line's multi-GPU detail: every rank's device phases (smj_mgpu_stats:
+    the five before busy_ms are consecutive on the rank's main stream and add
+    up to it; rows_ms, the row exchange on its own stream, overlaps them), the
+    slowest rank's, and the xGMI bytes per GPU (the most any rank sent)."""
+    per = [{p: round(v, 4) for p, v in zip(PHASES, r)} for r in rows]
+    slow = max(range(len(rows)), key=lambda g: rows[g][PHASES.index("busy_ms")])
+    return {"phases_ms_per_rank": per, "slowest_rank": slow,
+            "xgmi_bytes_sent_per_gpu": int(max(r[len(PHASES)] for r in rows)),
+            "xgmi_bytes_recv_per_gpu": int(max(r[len(PHASES) + 1] for r in rows))}
+
+
+def run_threads_join(a, json_out):
+    """--gpus N > 1 without a launcher: the multi-GPU join in THIS process,
+    one host thread per GPU (smj_mgpu_join_slices: the in-process group of
+    sortmergejoin_mpsm, ncclCommInitAll over the N GPUs, the reference's T join
+    threads of joincommon.c:118-165).  Rank g's slices of R and S are
+    generated on GPU g before the timed region and read in place.  One step =
+    one call (it returns when every rank's count is in); value = all tuples
+    / the call's host time, which is the slowest rank's by construction."""
+    import smj
+    N = a.gpus
+    w = a.width or 16
+    a.width = w
+    if a.n is None:
+        a.n = 128_000_000
+    ns_, firsts, total = shares(a, N)
+    libs, Rs, Ss = [], [], []
+    for g in range(N):
+        dev = torch.device("cuda", g)
+        with torch.cuda.device(dev):
+            L = smj.Library(w)  # a workspace of its own on this GPU
+            R, S = make_relations(L, a, ns_[g], firsts[g], total, device=dev)
+        libs.append(L)
+        Rs.append(R)
+        Ss.append(S)
+    lib = libs[0]
+    acc = {"steps": 0, "rows": [[0.0] * (len(PHASES) + 2) for _ in range(N)], "layout": None}
+    last = {"count": None}
+
+    def step():
+        c, _, sts = lib.mgpu_join_slices(Rs, Ss, 0, key_range=(1, total))
+        last["count"] = c
+        acc["steps"] += 1
+        acc["layout"] = sts[0]["layout"]
+        for g, st in enumerate(sts):
+            vals = [st[p] for p in PHASES] + [st["sent_bytes"], st["recv_bytes"]]
+            acc["rows"][g] = [x + y for x, y in zip(acc["rows"][g], vals)]
+
+    def reset():
+        acc["steps"] = 0
+        acc["rows"] = [[0.0] * (len(PHASES) + 2) for _ in range(N)]
+    step()  # the group's setup (communicators, buffers) stays out of the timing
+    tracer = _WsTracer(lib, lib.lib.smj_mgpu_group_workspace(0))
+    elapsed, kern, brk = timed_loop(a, tracer, None, step, reset)
+    k = max(acc["steps"], 1)
+    xchg = {"impl": "c (smj_mgpu_join_slices: one process, one host thread per GPU)",
+            **rank_phases([[v / k for v in r] for r in acc["rows"]]),
+            "exchange_layout": acc["layout"], "xgmi_peak_GBps": 7 * 153}
+    got = last["count"]
+    ok = got == total
+    chk = None
+    if not a.no_check:
+        # every rank's sorted shares: sorted, one key range per rank in rank
+        # order, and together a permutation of the inputs (checksums)
+        chk = {"sorted": True, "checksum_equal": True, "ranks_in_key_order": True}
+        sums = [torch.zeros(4, dtype=torch.int64) for _ in range(4)]
+        prev_hi = [None, None]
+        for g in range(N):
+            dev = torch.device("cuda", g)
+            with torch.cuda.device(dev):
+                outs = lib.mgpu_last_sorted(g, dev)
+                for r, (src, out) in enumerate(((Rs[g], outs[0]), (Ss[g], outs[1]))):
+                    chk["sorted"] = chk["sorted"] and _is_sorted(out, w)
+                    sums[2 * r] += _checksum(src).cpu()
+                    sums[2 * r + 1] += _checksum(out).cpu()
+                    if out.shape[0]:
+                        lo, hi = int(out[0, 1].item()), int(out[-1, 1].item())
+                        if prev_hi[r] is not None and lo < prev_hi[r]:
+                            chk["ranks_in_key_order"] = False
+                        prev_hi[r] = hi
+                del outs
+        chk["checksum_equal"] = bool(torch.equal(sums[0], sums[1]) and
+                                     torch.equal(sums[2], sums[3]))
+        ok = ok and all(chk.values())
+    ms_step = elapsed / a.steps * 1e3
+    value = 2 * total / (elapsed / a.steps) / 1e6
+    n0 = ns_[0]
+    cfg_key = f"n{n0}_w{w}_{a.dist}" + ("" if a.payload == "rowid" else f"_{a.payload}")
+    roof = dominant_roofline(kern, lambda name: alg_bytes_per_launch(name, n0, n0, n0, w),
+                             cfg_key)
+    strong = a.n_total is not None
+    out = {
+        "metric": "join throughput Mtuples/s (R⋈S) + achieved HBM GB/s, 128M⋈128M at 1/2/4/8 GPU",
+        "value": round(value, 2),
+        "unit": "Mtuples/s",
+        "n_gpus": N,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_step, 3),
+        "higher_is_better": True,
+        "scaling": "strong" if strong else "weak",
+        "vs_baseline": None,
+        "dtype": "int64" if w == 16 else "int32",
+        "data": "synthetic",
+        "config": {"workload": (f"sortmergejoin_mpsm R={total} S={total} over {N} GPUs"
+                                if strong else
+                                f"sortmergejoin_mpsm R={ns_[0]} S={ns_[0]} per GPU")
+                               + f", {w}-byte tuples, {a.dist}"
+                               + (f" theta={a.theta}" if a.dist == "zipf" else "")
+                               + ", PK/FK keys 1..|R|, payload " + a.payload,
+                   "tuples_per_relation_per_gpu": ns_[0], "tuples_per_relation_total": total,
+                   "tuple_bytes": w, "payload": a.payload, "distribution": a.dist,
+                   "parallelism": f"range-partition x{N}, one process, one host thread per GPU "
+                                  "(smj_mgpu_join_slices, RCCL)"},
+        "roofline": roof,
+        "cpu_baseline": None,
+        "result_ok": ok,
+        "matches": got,
+        "output_check": chk if chk is not None else "skipped (--no-check)",
+        "detail": {
+            "S_tuples_per_s_M": round(total / (elapsed / a.steps) / 1e6, 2),
+            "pipeline_alg_GBps_5w_per_gpu": round(5 * 2 * total * w / N / (elapsed / a.steps)
+                                                  / 1e9, 1),
+            "kernels_ms_per_step_rank0": {kk: round(v[0], 4) for kk, v in brk.items()},
+            "device": lib.lib.smj_device_name().decode(),
+            "exchange": xchg,
+        },
+    }
+    print(json.dumps(out), file=json_out, flush=True)
+    lib.lib.smj_mgpu_release()
 
 
 class _WsTracer:

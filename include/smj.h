@@ -418,7 +418,9 @@ result_t * sortmergejoin_mpsm(relation_t * relR, relation_t * relS,
  * relations, the ranks' shares concatenated in rank order -- each rank owns
  * one contiguous key range, so this is the globally sorted relation.
  * rank_counts (optional, 2 * nranks): the tuples of R and of S each rank
- * sorted.  Returns the number of matching pairs. */
+ * sorted.  Returns the number of matching pairs.  Device inputs are read on
+ * the ranks' own streams with no ordering against any caller stream: the
+ * caller finishes every write to R and S before the call. */
 #define SMJ_MG_COPY     1u  /* collectives by device copies instead of RCCL:
                                ranks may share a GPU (rank g on device g mod
                                the visible count); every exchange synchronises */
@@ -436,11 +438,49 @@ typedef struct smj_mgpu_stats {
     int64_t  key_min;     /* the global plan's range */
     int64_t  key_max;
     double   ms;          /* host wall time of the call */
+    /* device phases of the call on the rank's streams (HIP events), ms.  The
+     * first five are consecutive on the rank's main stream and add up to
+     * busy_ms: the range partitions of R and S (every attempt); their table
+     * messages (k_xsend, the table exchange, k_xrecv, the summary copy); the
+     * main stream waiting (host decisions and the row exchange the local work
+     * did not hide); the local join (tile pass, group pass and count, both
+     * stages); the count's all-reduce.  rows_ms: the row exchange on the
+     * rank's row stream, which overlaps them. */
+    double   partition_ms;
+    double   tables_ms;
+    double   wait_ms;
+    double   join_ms;
+    double   reduce_ms;
+    double   busy_ms;
+    double   rows_ms;
 } smj_mgpu_stats;
 int64_t smj_mgpu_join(const tuple_t * R, uint64_t nR, const tuple_t * S, uint64_t nS,
                       int nranks, uint32_t flags, int64_t key_min, int64_t key_max,
                       tuple_t * sortedR, tuple_t * sortedS, uint64_t * rank_counts,
                       smj_mgpu_stats * stats);
+/* The multi-GPU join over ranks whose slices already lie on their GPUs (the
+ * layout of a relation sharded over the node's HBM): rank g reads R[g]
+ * (nR[g] tuples) and S[g] (nS[g]), host memory or device memory of GPU g, and
+ * runs on GPU g (SMJ_MG_COPY: g mod the visible count).  Otherwise as
+ * smj_mgpu_join; the sorted shares stay on the ranks' GPUs
+ * (smj_mgpu_last_sorted).  key_min <= key_max: the global key range;
+ * otherwise keys 1..sum(nR), verified. */
+int64_t smj_mgpu_join_slices(const tuple_t * const * R, const uint64_t * nR,
+                             const tuple_t * const * S, const uint64_t * nS, int nranks,
+                             uint32_t flags, int64_t key_min, int64_t key_max,
+                             uint64_t * rank_counts, smj_mgpu_stats * stats);
+/* Rank `rank`'s statistics of the last smj_mgpu_join / _slices call (its
+ * phases; `ms` is the call's host time).  Returns 0, or -1 when there is no
+ * such rank. */
+int smj_mgpu_last_stats(int rank, smj_mgpu_stats * out);
+/* Device pointers to rank `rank`'s sorted shares of the last smj_mgpu_join /
+ * _slices call (on the rank's GPU, valid until the next call) and their
+ * sizes.  Returns 0, or -1 when there is no such rank. */
+int smj_mgpu_last_sorted(int rank, tuple_t ** sortedR, uint64_t * nR, tuple_t ** sortedS,
+                         uint64_t * nS);
+/* Rank `rank`'s workspace in the in-process group of the last smj_mgpu_join
+ * / _slices call (its kernel trace: smj_trace_*), NULL when there is none. */
+struct smj_workspace * smj_mgpu_group_workspace(int rank);
 /* Frees the ranks' devices buffers, streams and communicators (kept across
  * calls of one configuration). */
 void smj_mgpu_release(void);

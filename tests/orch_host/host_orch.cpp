@@ -122,6 +122,11 @@ struct HostOps {
     void wait(int, int) {}
     void host_wait(int) {}
     void sync(int) {}
+    // timing marks: a logical clock, so the phases' arithmetic is checked
+    // (every mark one unit after the previous one)
+    double clock = 0, mark_t[smj::mg::kNumTMarks] = {};
+    void tmark(int m, int) { mark_t[m] = (clock += 1.0); }
+    double tspan(int a, int b) { return mark_t[b] - mark_t[a]; }
     uint32_t shards() { return K; }
     uint64_t sampled_capacity(uint64_t n, uint32_t nbits) {
         return n + n / 8 + ((uint64_t)1 << nbits) * K * 5 + 16;
@@ -290,8 +295,8 @@ struct HostOps {
             if (s != me) ro += rl;
             summary[2 * G + s] = rl;
             summary[3 * G + s] = msg[s * row + 1];
-            f0 = std::max(f0, msg[s * row + 2]);
-            f1 = std::max(f1, msg[s * row + 3]);
+            f0 |= msg[s * row + 2];
+            f1 |= msg[s * row + 3];
         }
         summary[4 * G] = f0;
         summary[4 * G + 1] = f1;
@@ -417,7 +422,8 @@ typedef mg::Rank<HostOps, HostColl> HostRank;
 // flags: 1 no planes, 2 one-call join, 4 sampled, 8 exact
 // info (out, 8 + 2 G int64): layout, pbits, attempts (rank 0), replans,
 //   stage calls (all ranks), whole calls, errors, rank-0 bytes sent, then the
-//   per-rank sorted sizes of R and S
+//   per-rank sorted sizes of R and S, then rank 0's phases (mg::Stats: part,
+//   tables, wait, join, reduce, busy, rows) in HostOps::tmark clock units
 extern "C" int64_t host_mpsm_join(const void* R, uint64_t nR, const void* S, uint64_t nS, int G,
                                   uint32_t flags, uint32_t bucket_bits, int64_t kmin, int64_t kmax, int ovf_rank,
                                   int na_rank, int calls, void* sortedR, void* sortedS,
@@ -489,6 +495,11 @@ extern "C" int64_t host_mpsm_join(const void* R, uint64_t nR, const void* S, uin
         info[8 + 2 * g] = onR[g];
         info[9 + 2 * g] = onS[g];
     }
+    // rank 0's phases on the logical clock of HostOps::tmark (units)
+    const mg::Stats& st = ranks[0].stats;
+    const double ph[7] = {st.part_ms, st.tables_ms, st.wait_ms, st.join_ms, st.reduce_ms,
+                          st.busy_ms, st.rows_ms};
+    for (int i = 0; i < 7; i++) info[8 + 2 * G + i] = (int64_t)ph[i];
     if (err && errcap > 0) {
         snprintf(err, errcap, "%s", g_err.c_str());
     }

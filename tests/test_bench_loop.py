@@ -132,3 +132,44 @@ def test_output_check_on_cpu_tensors(w):
     lost = out.clone()
     lost[7] = lost[8]
     assert bench.output_check([(src, lost)], w)["checksum_equal"] is False
+
+
+# --gpus N: never a line for fewer GPUs than asked (this container has none)
+def _bench(args, env_extra):
+    import os
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra)
+    return subprocess.run([sys.executable, bench.__file__] + args, capture_output=True,
+                          text=True, env=env, timeout=300, cwd="/tmp")
+
+
+def test_gpus_more_than_visible_exits_nonzero():
+    import torch
+    n = max(2, torch.cuda.device_count() + 1)
+    r = _bench(["--gpus", str(n)], {})
+    assert r.returncode == 2, r.stderr[-500:]
+    assert r.stdout.strip() == ""  # no JSON line
+    assert "visible" in r.stderr
+
+
+@pytest.mark.parametrize("world,gpus", [("1", "2"), ("2", "8"), ("8", "1")])
+def test_gpus_must_match_the_launcher(world, gpus):
+    r = _bench(["--gpus", gpus], {"WORLD_SIZE": world, "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2, r.stderr[-500:]
+    assert r.stdout.strip() == ""
+    assert "WORLD_SIZE" in r.stderr
+
+
+def test_rank_phases_detail():
+    rows = [[0.2, 0.05, 0.1, 2.5, 0.01, 2.86, 0.7, 1e9, 1.1e9],
+            [0.2, 0.05, 0.3, 2.5, 0.01, 3.06, 0.8, 1.2e9, 0.9e9]]
+    d = bench.rank_phases(rows)
+    assert d["slowest_rank"] == 1
+    assert d["xgmi_bytes_sent_per_gpu"] == int(1.2e9)
+    assert d["xgmi_bytes_recv_per_gpu"] == int(1.1e9)
+    for r in d["phases_ms_per_rank"]:
+        parts = sum(r[p] for p in bench.PHASES[:5])
+        assert abs(parts - r["busy_ms"]) < 1e-6

@@ -142,6 +142,41 @@ def test_headline_join_full_bitexact(libs, oracles, width, dist_, fanout_bits):
     np.testing.assert_array_equal(gS, wS)
 
 
+@pytest.mark.parametrize("payload,layout", [("wide48", "words"), ("full64", "tuples")])
+def test_headline_join_full_payload_layouts(libs, oracles, payload, layout):
+    """The headline join (128M x 128M, 16-byte tuples, bench.py's plan) with
+    payloads the 48-bit words cannot hold: 2^40 + row id (64-bit packed
+    words) and random 64-bit values, negative ones included (the 16-byte
+    tuples themselves, the persistent tile pass k_tilepass_p).  bench.py
+    --payload sets the same payloads; sorted R, sorted S and the count
+    against the oracle's full (key, payload) radix sort."""
+    import torch
+    import bench
+    lib, orc = libs[16], oracles[16]
+    n = 128_000_000
+    R, S = lib.empty(n), lib.empty(n)
+    lib.dev_gen_pk(R, 0, n, 12345)
+    lib.dev_gen_fk(S, 0, n, n, 54321)
+    bench.set_payloads(R, S, payload, 0)
+    sR, sS = lib.empty(n), lib.empty(n)
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    lib.dev_join(R, S, sR, sS, cnt, 8, 1, n)
+    torch.cuda.synchronize()
+    assert lib.last_layout() == layout
+    count = int(cnt.item())
+    hR, hS = lib.to_host(R), lib.to_host(S)
+    gR, gS = lib.to_host(sR), lib.to_host(sS)
+    del R, S, sR, sS
+    _free(torch)
+    with ThreadPoolExecutor(2) as ex:
+        fR = ex.submit(orc.sort_radix, hR)
+        fS = ex.submit(orc.sort_radix, hS)
+        wR, wS = fR.result(), fS.result()
+    assert count == orc.merge_join(wR, wS) == n
+    np.testing.assert_array_equal(gR, wR)
+    np.testing.assert_array_equal(gS, wS)
+
+
 def _checksum(torch, t):
     """Order-independent checksum of (n, 2) rows: wrapping int64 sums of the
     keys, the payloads and of two 64-bit avalanche hashes of each row (a row
@@ -262,3 +297,36 @@ def test_mpsm_n1024_zipf_ref(libs):
         lib.lib.smj_mgpu_release()
         del R, S
         _free(torch)
+
+
+@pytest.mark.parametrize("width", [16, 8])
+def test_mgpu_copy8_zipf_32m(libs, oracles, width):
+    """The G = 8 rank protocol (smj_mgpu_join, ranks sharing the one GPU with
+    device-copy collectives, SMJ_MG_COPY) at 32M x 32M with the reference's
+    create_relation_zipf S (theta 0.75, seed 54321): count, and the ranks'
+    sorted shares in rank order, bit-exact against the oracle."""
+    import torch
+    from smj import MG_COPY
+    lib, orc = libs[width], oracles[width]
+    n = 32 << 20
+    R, S = lib.empty(n), lib.empty(n)
+    lib.dev_gen_pk(R, 0, n, 12345)
+    lib.dev_gen_zipf_ref(S, 0, n, 0.75, 54321)
+    torch.cuda.synchronize()
+    try:
+        c, sR, sS, counts, st = lib.mgpu_join(R, S, 8, MG_COPY)
+        assert counts[:, 0].sum() == n and counts[:, 1].sum() == n
+        assert (counts > 0).all()  # every rank owns a share of both
+        hR, hS = lib.to_host(R), lib.to_host(S)
+        gR, gS = lib.to_host(sR), lib.to_host(sS)
+    finally:
+        lib.lib.smj_mgpu_release()
+        del R, S
+        _free(torch)
+    with ThreadPoolExecutor(2) as ex:
+        fR = ex.submit(orc.sort_radix, hR)
+        fS = ex.submit(orc.sort_radix, hS)
+        wR, wS = fR.result(), fS.result()
+    assert c == orc.merge_join(wR, wS) == n
+    np.testing.assert_array_equal(gR, wR)
+    np.testing.assert_array_equal(gS, wS)

@@ -168,3 +168,77 @@ def test_mgpu_rank_comm_world1(libs, oracles, width, kind):
             assert np.array_equal(sS.cpu().numpy().reshape(-1).view(S.dtype), eS)
     finally:
         comm.close()
+
+
+def _phases_ok(st):
+    """smj_mgpu_stats phases: the five main-stream phases add up to busy_ms
+    (wait_ms is its remainder, never negative); the partition and the local
+    join took time on the device."""
+    five = (st["partition_ms"] + st["tables_ms"] + st["wait_ms"] + st["join_ms"]
+            + st["reduce_ms"])
+    assert abs(five - st["busy_ms"]) <= 1e-3 + 1e-6 * st["busy_ms"], st
+    assert st["partition_ms"] > 0 and st["join_ms"] > 0 and st["wait_ms"] >= 0, st
+    assert st["busy_ms"] <= st["ms"] * 1.05 + 0.05, st  # device span within the call
+
+
+@pytest.mark.parametrize("G,flags", [(1, 0), (3, MG_COPY), (8, MG_COPY)],
+                         ids=["rccl1", "copy3", "copy8"])
+@pytest.mark.parametrize("kind", ["uniform", "zipf", "wide48"])
+def test_mgpu_join_slices_vs_oracle(libs, oracles, width, G, flags, kind):
+    """smj_mgpu_join_slices: rank g's slices are separate device tensors
+    (ragged, one rank's S slice empty at G > 1), read in place; the ranks'
+    sorted shares (smj_mgpu_last_sorted) in rank order are the oracle's
+    sorted relations, and every rank reports its device phases
+    (smj_mgpu_last_stats)."""
+    import torch
+    orc, lib = oracles[width], libs[width]
+    n = (1 << 20) + 777
+    R, S = relations(orc, width, n, kind, seed=808)
+    want, eR, eS = orc.sortmergejoin(R, S)
+    it = np.int64 if width == 16 else np.int32
+    cutR = sorted({0, n} | {n * g // G + 13 * g for g in range(1, G)})
+    cutS = sorted({0, n} | {n * g // G - 7 * g for g in range(1, G)})
+    if G > 1:
+        cutS[1] = cutS[0]  # rank 0 gets no S
+    tR = torch.from_numpy(R.view(it).reshape(-1, 2).copy()).cuda()
+    tS = torch.from_numpy(S.view(it).reshape(-1, 2).copy()).cuda()
+    Rs = [tR[cutR[g]:cutR[g + 1]].clone() for g in range(G)]
+    Ss = [tS[cutS[g]:cutS[g + 1]].clone() for g in range(G)]
+    for _ in range(2):  # the second call reuses the group's buffers
+        c, counts, sts = lib.mgpu_join_slices(Rs, Ss, flags, key_range=None)
+        assert c == want
+        assert counts[:, 0].sum() == n and counts[:, 1].sum() == n
+        outR, outS = [], []
+        for g in range(G):
+            sR, sS = lib.mgpu_last_sorted(g, "cuda")
+            assert (sR.shape[0], sS.shape[0]) == tuple(counts[g])
+            outR.append(sR.cpu().numpy().reshape(-1).view(R.dtype))
+            outS.append(sS.cpu().numpy().reshape(-1).view(S.dtype))
+        assert np.array_equal(np.concatenate(outR), eR)
+        assert np.array_equal(np.concatenate(outS), eS)
+        for st in sts:
+            _phases_ok(st)
+        if G > 1:
+            assert all(st["rows_ms"] > 0 for st in sts)
+    assert lib.mgpu_last_stats(0)["layout"] == sts[0]["layout"]
+    with pytest.raises(IndexError):
+        lib.mgpu_last_stats(G)
+    lib.lib.smj_mgpu_release()
+
+
+def test_mgpu_rank_comm_phases(libs, oracles):
+    """The multi-process entry's stats carry the phases too (one rank)."""
+    import torch
+    orc, lib = oracles[16], libs[16]
+    R, S = relations(orc, 16, 500009, "uniform", seed=11)
+    tR = torch.from_numpy(R.view(np.int64).reshape(-1, 2).copy()).cuda()
+    tS = torch.from_numpy(S.view(np.int64).reshape(-1, 2).copy()).cuda()
+    comm = lib.mgpu_comm(1, 0)
+    try:
+        for _ in range(2):
+            c, _, _, st = comm.join(tR, tS, key_range=(1, len(R)))
+            assert c == orc.sortmergejoin(R, S)[0]
+            _phases_ok(st)
+            assert st["rows_ms"] == 0  # nothing travels on one rank
+    finally:
+        comm.close()

@@ -51,7 +51,7 @@ def run(f, R, S, G, flags=0, bucket_bits=4, key_range=None, ovf=-1, na=-1, calls
     dt = R.dtype
     sR = np.zeros(len(R), dt)
     sS = np.zeros(len(S), dt)
-    info = np.zeros(8 + 2 * G, np.int64)
+    info = np.zeros(8 + 2 * G + 7, np.int64)
     err = C.create_string_buffer(512)
     kmin, kmax = key_range if key_range else (1, 0)
     c = f(R.ctypes.data, len(R), S.ctypes.data, len(S), G, flags, bucket_bits, kmin, kmax,
@@ -117,6 +117,13 @@ def test_orchestration_vs_oracle(host_libs, oracles, width, G, kind):
     assert (info[4], info[5]) == ((2 * busy, 0) if G > 1 else (0, 2))
     # one contiguous share per rank, every tuple once
     assert info[8::2][:G].sum() == len(R) and info[9::2][:G].sum() == len(S)
+    # rank 0's phases (mg::Stats; a logical clock here, one unit per mark):
+    # consecutive on the main stream, so they add up to its busy span; the
+    # rows are timed on their own stream, only when something travels
+    part, tables, wait, join, reduce_, busy, rows = info[8 + 2 * G:]
+    assert part + tables + wait + join + reduce_ == busy
+    assert min(part, tables, join, reduce_) > 0 and wait >= 0
+    assert (rows > 0) == (G > 1)
 
 
 @pytest.mark.parametrize("G", [2, 3, 8])
