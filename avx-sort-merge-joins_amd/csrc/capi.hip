@@ -2115,14 +2115,15 @@ uint64_t smj_sampled_capacity(uint64_t n, uint32_t nbits) { return sampled_capac
 uint32_t smj_sampled_shards(void) { return kShards; }
 
 void smj_dev_xsend(const int64_t* start, const int64_t* cnt, const unsigned int* flags, uint32_t F,
-                   uint32_t K, uint32_t world, int64_t* msg, int64_t* chunk,
+                   uint32_t K, uint32_t world, uint32_t used, int64_t* msg, int64_t* chunk,
                    smj_stream_t stream) {
-    if (F > 1024 || world == 0 || world > 1024 || world > F) {
-        fprintf(stderr, "[ERROR] smj_dev_xsend: F %u, world %u (1 <= world <= F <= 1024)\n", F,
-                world);
+    if (used == 0) used = F;
+    if (F > 1024 || world == 0 || world > 1024 || world > F || used > F) {
+        fprintf(stderr, "[ERROR] smj_dev_xsend: F %u, world %u, used %u (1 <= world <= F <= "
+                        "1024, used <= F)\n", F, world, used);
         abort();
     }
-    xsend(start, cnt, flags, F, K, world, msg, chunk, (hipStream_t)stream);
+    xsend(start, cnt, flags, F, K, world, used, msg, chunk, (hipStream_t)stream);
 }
 
 void smj_dev_xrecv(const int64_t* msg, const int64_t* chunk, uint32_t world, uint32_t rank,

@@ -5,7 +5,10 @@
 //
 // After a rank range-partitions a relation into F partitions (K shard regions
 // each, exact partitions use shard 0 only), partition p belongs to rank
-// owner(p) = p * G / F (contiguous ranges, dist.py owners()).  Two one-
+// owner(p) = p * G / U, the last rank also owning [U, F) (contiguous ranges,
+// dist.py owners()).  U = the partitions the plan's key range reaches: F is a
+// power of two, the key span is not (keys 1..1024M at F = 2^10 reach 977
+// partitions), so splitting F would leave the last rank short.  Two one-
 // workgroup kernels turn the region tables into
 //   xsend: the message to every rank g -- [chunk size, used elements, the
 //          sender's two flags, the owned regions' offsets inside the chunk,
@@ -23,15 +26,19 @@
 
 namespace smj {
 
-__device__ __forceinline__ uint32_t owned_lo(uint32_t F, uint32_t G, uint32_t g) {
-    return (uint32_t)(((uint64_t)g * F + G - 1) / G);
+// the first partition of rank g (g = G: F); U = the partitions holding keys
+__device__ __forceinline__ uint32_t owned_lo(uint32_t F, uint32_t G, uint32_t U, uint32_t g) {
+    return g >= G ? F : (uint32_t)(((uint64_t)g * U + G - 1) / G);
+}
+__device__ __forceinline__ uint32_t owner_of(uint32_t G, uint32_t U, uint32_t p) {
+    return p < U ? (uint32_t)((uint64_t)p * G / U) : G - 1;
 }
 
 constexpr uint32_t kXHead = 4;  // chunk size, used, flag0 (not packable), flag1 (overflow)
 
 __global__ void __launch_bounds__(256)
 k_xsend(const int64_t* __restrict__ start, const int64_t* __restrict__ cnt,
-        const unsigned int* __restrict__ flags, uint32_t F, uint32_t K, uint32_t G,
+        const unsigned int* __restrict__ flags, uint32_t F, uint32_t K, uint32_t G, uint32_t U,
         int64_t* __restrict__ msg, int64_t* __restrict__ chunk) {
     __shared__ unsigned long long wend[4];
     __shared__ int64_t used[1024];
@@ -46,7 +53,7 @@ k_xsend(const int64_t* __restrict__ start, const int64_t* __restrict__ cnt,
     int64_t acc = 0;
     uint32_t cur = 0xffffffffu;
     for (uint32_t p = p0; p < p1; p++) {
-        const uint32_t g = (uint32_t)((uint64_t)p * G / F);
+        const uint32_t g = owner_of(G, U, p);
         if (g != cur) {
             if (acc) atomicAdd((unsigned long long*)&used[cur], (unsigned long long)acc);
             cur = g;
@@ -69,8 +76,8 @@ k_xsend(const int64_t* __restrict__ start, const int64_t* __restrict__ cnt,
     const int64_t cend = (int64_t)max(max(wend[0], wend[1]), max(wend[2], wend[3]));
     // chunk of g: from its first partition's first region to the next rank's
     for (uint32_t g = threadIdx.x; g < G; g += 256) {
-        const int64_t cs = start[(size_t)owned_lo(F, G, g) * K];
-        const int64_t ce = g + 1 < G ? start[(size_t)owned_lo(F, G, g + 1) * K] : cend;
+        const int64_t cs = start[(size_t)owned_lo(F, G, U, g) * K];
+        const int64_t ce = g + 1 < G ? start[(size_t)owned_lo(F, G, U, g + 1) * K] : cend;
         chunk[g] = cs;
         chunk[G + g] = ce - cs;
     }
@@ -78,8 +85,8 @@ k_xsend(const int64_t* __restrict__ start, const int64_t* __restrict__ cnt,
     // region entries of all ranks in one sweep, the heads by one thread each
     for (uint32_t i = threadIdx.x; i < F * K; i += 256) {
         const uint32_t p = i / K;
-        const uint32_t g = (uint32_t)((uint64_t)p * G / F);
-        const uint32_t lo = owned_lo(F, G, g), hi = owned_lo(F, G, g + 1);
+        const uint32_t g = owner_of(G, U, p);
+        const uint32_t lo = owned_lo(F, G, U, g), hi = owned_lo(F, G, U, g + 1);
         const uint64_t m0 = (uint64_t)g * kXHead + 2ull * K * lo;
         const uint32_t nreg = (hi - lo) * K, j = i - lo * K;
         const int64_t cs = start[(size_t)lo * K];
@@ -87,7 +94,7 @@ k_xsend(const int64_t* __restrict__ start, const int64_t* __restrict__ cnt,
         msg[m0 + kXHead + nreg + j] = cnt[i];
     }
     for (uint32_t g = threadIdx.x; g < G; g += 256) {
-        const uint32_t lo = owned_lo(F, G, g), hi = owned_lo(F, G, g + 1);
+        const uint32_t lo = owned_lo(F, G, U, g), hi = owned_lo(F, G, U, g + 1);
         const uint64_t m0 = (uint64_t)g * kXHead + 2ull * K * lo;
         const int64_t cs = start[(size_t)lo * K];
         const int64_t ce = g + 1 < G ? start[(size_t)hi * K] : cend;
@@ -176,8 +183,8 @@ void hist_tables(const int64_t* hist, uint32_t F, uint32_t K, int64_t* start, in
 }
 
 void xsend(const int64_t* start, const int64_t* cnt, const unsigned int* flags, uint32_t F,
-           uint32_t K, uint32_t G, int64_t* msg, int64_t* chunk, hipStream_t st) {
-    hipLaunchKernelGGL(k_xsend, dim3(1), dim3(256), 0, st, start, cnt, flags, F, K, G, msg,
+           uint32_t K, uint32_t G, uint32_t U, int64_t* msg, int64_t* chunk, hipStream_t st) {
+    hipLaunchKernelGGL(k_xsend, dim3(1), dim3(256), 0, st, start, cnt, flags, F, K, G, U, msg,
                        chunk);
     SMJ_CHECK(hipGetLastError());
 }

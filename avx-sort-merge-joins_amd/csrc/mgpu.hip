@@ -132,8 +132,8 @@ struct DevOps {
         smj::hist_tables(hist, F, K, ss, sc, st[0]);
     }
     void xsend(const int64_t* ss, const int64_t* sc, const uint32_t* flags, uint32_t F,
-               uint32_t K, uint32_t G, int64_t* msg, int64_t* chunk) {
-        smj::xsend(ss, sc, flags, F, K, G, msg, chunk, st[0]);
+               uint32_t K, uint32_t G, uint32_t U, int64_t* msg, int64_t* chunk) {
+        smj::xsend(ss, sc, flags, F, K, G, U, msg, chunk, st[0]);
     }
     void xrecv(const int64_t* msg, const int64_t* chunk, uint32_t G, uint32_t rank,
                uint32_t mine, uint32_t K, uint32_t nb, uint64_t cap, int64_t* ts, int64_t* tc,

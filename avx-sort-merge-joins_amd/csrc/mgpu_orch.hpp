@@ -11,8 +11,10 @@
 // (t + i) % T), merges and joins them, and the counts are summed.  Here a rank
 // plays a thread and its GPU plays the thread's NUMA region:
 //   1. range-partition the rank's slices of R and S on its GPU into
-//      F = 2^pbits partitions of the GLOBAL key range; partition p belongs to
-//      rank owner(p) = p * G / F, so every rank owns one contiguous key range;
+//      F = 2^pbits partitions of the GLOBAL key range; of the U partitions the
+//      key range reaches, partition p belongs to rank owner(p) = p * G / U
+//      (the ones above U to the last rank), so every rank owns one contiguous
+//      key range of about 1/G of the keys;
 //   2. a table message (the owned regions' offsets and counts, two flags) to
 //      every rank over the collective, the receive tables built on the device,
 //      one small summary read by the host (every flag is OR-ed over all
@@ -115,14 +117,31 @@ inline uint32_t ceil_log2(uint64_t x) { return x <= 1 ? 0 : bitlen(x - 1); }
 inline uint64_t span_of(int64_t kmin, int64_t kmax) {
     return kmax > kmin ? (uint64_t)kmax - (uint64_t)kmin : 0;
 }
-// [owned_lo(g), owned_lo(g + 1)) = the partitions of rank g (dist.py owned)
-inline uint32_t owned_lo(uint32_t F, uint32_t G, uint32_t g) {
-    return (uint32_t)(((uint64_t)g * F + G - 1) / G);
+// [owned_lo(g), owned_lo(g + 1)) = the partitions of rank g (dist.py owned):
+// the U partitions the key range reaches split evenly, the rest of the F to
+// the last rank (exchange.hip owner_of)
+inline uint32_t owned_lo(uint32_t F, uint32_t G, uint32_t U, uint32_t g) {
+    return g >= G ? F : (uint32_t)(((uint64_t)g * U + G - 1) / G);
 }
 // s1 of the range plan: partition p covers [kmin + p 2^s1, kmin + (p+1) 2^s1)
 inline uint32_t plan_shift(int64_t kmin, int64_t kmax, uint32_t bits) {
     const uint32_t L = bitlen(span_of(kmin, kmax));
     return L > bits ? L - bits : 0;
+}
+// the plan's base: kmin, moved down when base + 2^L - 1 would pass INT64_MAX
+inline int64_t plan_base(int64_t kmin, int64_t kmax) {
+    const uint32_t L = bitlen(span_of(kmin, kmax));
+    const i128 one = 1, i64max = (i128)INT64_MAX;
+    i128 base = kmin;
+    if (base + (one << L) - 1 > i64max) base = i64max - (one << L) + 1;
+    return (int64_t)base;
+}
+// the partitions [0, U) the key range reaches (dist.py used_parts)
+inline uint32_t used_parts(int64_t kmin, int64_t kmax, uint32_t pbits) {
+    const int64_t base = plan_base(kmin, kmax);
+    const uint32_t s1 = plan_shift(base, kmax, pbits);
+    const uint64_t u = (span_of(base, kmax) >> s1) + 1;
+    return (uint32_t)std::min<uint64_t>(u, 1ull << pbits);
 }
 // 48-bit words worth trying: s1 key bits plus payloads up to the key span
 inline bool planes_hold(int64_t kmin, int64_t kmax, uint32_t pbits) {
@@ -154,11 +173,10 @@ struct LocalRange {
 inline LocalRange local_range(int64_t kmin, int64_t kmax, uint32_t pbits, uint32_t G,
                               uint32_t rank) {
     const uint32_t L = bitlen(span_of(kmin, kmax));
-    const i128 one = 1, i64max = (i128)INT64_MAX;
-    i128 base = kmin;
-    if (base + (one << L) - 1 > i64max) base = i64max - (one << L) + 1;
-    const uint32_t F = 1u << pbits;
-    const uint32_t p_lo = owned_lo(F, G, rank), p_hi = owned_lo(F, G, rank + 1);
+    const i128 one = 1;
+    const i128 base = plan_base(kmin, kmax);
+    const uint32_t F = 1u << pbits, U = used_parts(kmin, kmax, pbits);
+    const uint32_t p_lo = owned_lo(F, G, U, rank), p_hi = owned_lo(F, G, U, rank + 1);
     LocalRange r;
     r.lbits = ceil_log2(std::max<uint32_t>(p_hi - p_lo, 1));
     const uint32_t s1 = plan_shift((int64_t)base, kmax, pbits);
@@ -330,7 +348,7 @@ struct Rank {
     uint64_t n[2] = {0, 0};
     Options opt;
     Stats stats;
-    uint32_t pbits = 0, F = 0, K = 1;
+    uint32_t pbits = 0, F = 0, U = 0, K = 1;  // U: the partitions the keys reach
     LocalRange lr{};
     int64_t kmax = 0;
     bool default_sampled = true, guessed = false;
@@ -492,7 +510,7 @@ struct Rank {
             ops->hist_tables(a.hist, F, K, a.ss, a.sc);
         }
         ops->tmark(kTPart0 + 3 * r + 1, kMain);
-        ops->xsend(a.ss, a.sc, a.flags, F, K, (uint32_t)G, a.msg_in, a.chunk);
+        ops->xsend(a.ss, a.sc, a.flags, F, K, (uint32_t)G, U, a.msg_in, a.chunk);
         const uint64_t row = kHead + 2ull * K * mine;
         const int64_t* msg = a.msg_in;
         if (G > 1) {
@@ -626,12 +644,13 @@ struct Rank {
         pbits = partition_bits(opt.bucket_bits, (uint32_t)G, offer, n_hint, true, kmin_, kmax_);
         if ((1u << pbits) < (uint32_t)G) pbits = ceil_log2((uint64_t)G);
         F = 1u << pbits;
+        U = used_parts(kmin_, kmax_, pbits);
         lr = local_range(kmin_, kmax_, pbits, (uint32_t)G, (uint32_t)me);
         kmax = kmax_;
         per_rank.assign((size_t)G, 0);
         for (int g = 0; g < G; g++)
-            per_rank[g] = owned_lo(F, (uint32_t)G, (uint32_t)g + 1) -
-                          owned_lo(F, (uint32_t)G, (uint32_t)g);
+            per_rank[g] = owned_lo(F, (uint32_t)G, U, (uint32_t)g + 1) -
+                          owned_lo(F, (uint32_t)G, U, (uint32_t)g);
         mine = per_rank[me];
         stats.pbits = pbits;
         stats.kmin = lr.base;

@@ -269,7 +269,7 @@ void gen_zipf_ref(Workspace* ws, Tup* out, uint64_t n, uint64_t first, uint64_t 
 
 // ---- exchange.hip : the multi-GPU exchange's tables
 void xsend(const int64_t* start, const int64_t* cnt, const unsigned int* flags, uint32_t F,
-           uint32_t K, uint32_t G, int64_t* msg, int64_t* chunk, hipStream_t st);
+           uint32_t K, uint32_t G, uint32_t U, int64_t* msg, int64_t* chunk, hipStream_t st);
 void xrecv(const int64_t* msg, const int64_t* chunk, uint32_t G, uint32_t rank, uint32_t mine,
            uint32_t K, uint32_t nb, uint64_t cap, int64_t* tstart, int64_t* tcnt,
            int64_t* summary, hipStream_t st);

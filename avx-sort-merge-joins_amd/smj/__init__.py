@@ -281,7 +281,7 @@ class Library:
             "smj_dev_gen_zipf_ref": (None, [_P, _P, _U64, _U64, _U64, C.c_double, _U32, _U64,
                                             _P]),
             "smj_glibc_rand": (_U32, [_U32, _U64]),
-            "smj_dev_xsend": (None, [_P, _P, _P, _U32, _U32, _U32, _P, _P, _P]),
+            "smj_dev_xsend": (None, [_P, _P, _P, _U32, _U32, _U32, _U32, _P, _P, _P]),
             "smj_dev_xrecv": (None, [_P, _P, _U32, _U32, _U32, _U32, _U32, _U64, _P, _P, _P,
                                      _P]),
             "smj_mgpu_join": (_I64, [_P, _U64, _P, _U64, C.c_int, _U32, _I64, _I64, _P, _P,
@@ -658,11 +658,12 @@ class Library:
         self.lib.smj_dev_gen_zipf_ref(self.ws, out.data_ptr(), out.shape[0], first, maxid,
                                       theta, seed, skip, self.stream_ptr())
 
-    def dev_xsend(self, start, cnt, flags, world, msg, chunk):
-        """smj_dev_xsend: start/cnt (F, K) int64, flags int64[2]."""
+    def dev_xsend(self, start, cnt, flags, world, msg, chunk, used=0):
+        """smj_dev_xsend: start/cnt (F, K) int64, flags int64[2]; `used`: the
+        partitions the key range reaches (0 = all)."""
         F, K = start.shape
         self.lib.smj_dev_xsend(start.data_ptr(), cnt.data_ptr(), flags.data_ptr(), F, K, world,
-                               msg.data_ptr(), chunk.data_ptr(), self.stream_ptr())
+                               used, msg.data_ptr(), chunk.data_ptr(), self.stream_ptr())
 
     def dev_xrecv(self, msg, chunk, world, rank, mine, K, tstart, tcnt, cap, summary):
         """smj_dev_xrecv: msg (world, 4 + 2 K mine), tstart/tcnt (nb, world K)."""

@@ -117,16 +117,35 @@ class _Works:
             w.wait()
 
 
-def owners(fanout: int, world: int) -> torch.Tensor:
-    """Owner rank of each of the `fanout` range partitions (contiguous)."""
-    return torch.arange(fanout, dtype=torch.int64) * world // fanout
+def owners(fanout: int, world: int, used: int | None = None) -> torch.Tensor:
+    """Owner rank of each of the `fanout` range partitions (contiguous): the
+    `used` partitions the key range reaches (used_parts; None = all) split
+    evenly, the ones above them to the last rank.  Splitting the power-of-two
+    partition space instead would leave the last rank short whenever the key
+    span is not a power of two (keys 1..1024M at 2^10 partitions reach 977:
+    ranks 0-6 would own 134M keys each and rank 7 85M)."""
+    u = fanout if used is None else used
+    p = torch.arange(fanout, dtype=torch.int64)
+    return torch.where(p < u, p * world // u, world - 1)
 
 
-def owned(fanout: int, world: int, rank: int) -> tuple[int, int]:
+def owned(fanout: int, world: int, rank: int, used: int | None = None) -> tuple[int, int]:
     """[first, last) partition owned by `rank` (the inverse of owners)."""
-    lo = -(-rank * fanout // world)
-    hi = -(-(rank + 1) * fanout // world)
-    return lo, hi
+    u = fanout if used is None else used
+
+    def first(g):
+        return fanout if g >= world else -(-g * u // world)
+    return first(rank), first(rank + 1)
+
+
+def used_parts(key_min: int, key_max: int, pbits: int) -> int:
+    """The exchange partitions the key range [key_min, key_max] reaches:
+    partition p starts at base + p 2^s1 (base = local_range's, key_min moved
+    down near INT64_MAX)."""
+    L = max(key_max - key_min, 0).bit_length()
+    base = min(key_min, INT64_MAX - (1 << L) + 1)
+    s1 = plan_shift(base, key_max, pbits)
+    return min(1 << pbits, ((max(key_max - base, 0)) >> s1) + 1)
 
 
 def plan_shift(key_min: int, key_max: int, bits: int) -> int:
@@ -187,11 +206,12 @@ def local_range(key_min: int, key_max: int, pbits: int, world: int, rank: int):
     level-1 buckets of its local plan, 2^lbits of them; [key_lo, key_hi] only
     fixes that plan's bit length s1 + lbits (make_plan), and the smallest such
     width keeps key_hi inside the global range, so inside int64."""
+    used = used_parts(key_min, key_max, pbits)
     L = max(key_max - key_min, 0).bit_length()
     if key_min + (1 << L) - 1 > INT64_MAX:
         key_min = INT64_MAX - (1 << L) + 1
     F = 1 << pbits
-    p_lo, p_hi = owned(F, world, rank)
+    p_lo, p_hi = owned(F, world, rank, used)
     lbits = ceil_log2(max(p_hi - p_lo, 1))
     s1 = plan_shift(key_min, key_max, pbits)
     key_lo = key_min + (p_lo << s1)
@@ -203,9 +223,9 @@ def local_range(key_min: int, key_max: int, pbits: int, world: int, rank: int):
     return key_min, key_lo, key_hi, lbits
 
 
-def send_counts(hist: torch.Tensor, world: int) -> torch.Tensor:
+def send_counts(hist: torch.Tensor, world: int, used: int | None = None) -> torch.Tensor:
     """Rows this rank sends to every rank: per-partition counts summed by owner."""
-    own = owners(hist.numel(), world).to(hist.device)
+    own = owners(hist.numel(), world, used).to(hist.device)
     out = torch.zeros(world, dtype=torch.int64, device=hist.device)
     return out.index_add_(0, own, hist.to(torch.int64))
 
@@ -213,7 +233,7 @@ def send_counts(hist: torch.Tensor, world: int) -> torch.Tensor:
 HEAD = 4  # message header: chunk size, used elements, flag0 (not packable), flag1 (overflow)
 
 
-def xsend_torch(start, cnt, flags, world, msg, chunk):
+def xsend_torch(start, cnt, flags, world, msg, chunk, used=0):
     """smj_dev_xsend in framework ops (the CPU stand-ins use it; the GPU test
     compares the kernel with it): the message to every rank, rank after rank,
     [chunk size, used, not packable, overflow, owned regions' offsets in the
@@ -221,9 +241,10 @@ def xsend_torch(start, cnt, flags, world, msg, chunk):
     [region overflow, not packable] as the sampled partition writes them."""
     F, K = start.shape
     G = world
+    u = used or F
     dev = start.device
-    own = owners(F, G).to(dev)
-    lo_of = torch.tensor([owned(F, G, g)[0] for g in range(G)], dtype=torch.int64, device=dev)
+    own = owners(F, G, u).to(dev)
+    lo_of = torch.tensor([owned(F, G, g, u)[0] for g in range(G)], dtype=torch.int64, device=dev)
     cstart = start[lo_of, 0]
     cend = (start + cnt).max()
     csize = torch.cat([cstart[1:], cend.view(1)]) - cstart
@@ -231,7 +252,7 @@ def xsend_torch(start, cnt, flags, world, msg, chunk):
     rel_start = torch.where(cnt > 0, start - cstart[own].view(F, 1), 0)
     parts = []
     for g in range(G):
-        lo, hi = owned(F, G, g)
+        lo, hi = owned(F, G, g, u)
         parts += [torch.stack([csize[g], used[g], flags[1].to(torch.int64),
                                flags[0].to(torch.int64)]),
                   rel_start[lo:hi].reshape(-1), cnt[lo:hi].reshape(-1)]
@@ -337,8 +358,8 @@ class DeviceOps:
                                            bucket_bits, key_lo, key_hi, sR, sS, count,
                                            packed=packed, stage=stage)
 
-    def xsend(self, start, cnt, flags, world, msg, chunk):
-        self.lib.dev_xsend(start, cnt, flags, world, msg, chunk)
+    def xsend(self, start, cnt, flags, world, msg, chunk, used=0):
+        self.lib.dev_xsend(start, cnt, flags, world, msg, chunk, used)
 
     def xrecv(self, msg, chunk, world, rank, mine, K, tstart, tcnt, cap, summary):
         self.lib.dev_xrecv(msg, chunk, world, rank, mine, K, tstart, tcnt, cap, summary)
@@ -400,8 +421,11 @@ class DistributedJoin:
             key_min, key_max, self.pbits, self.world, self.rank)
         self.key_max = key_max
         F, G = self.fanout, self.world
-        self.per_rank = [owned(F, G, g)[1] - owned(F, G, g)[0] for g in range(G)]
-        self.p_lo, self.p_hi = owned(F, G, self.rank)
+        # the partitions the key range reaches, split evenly (owners)
+        self.used = used_parts(key_min, key_max, self.pbits)
+        self.per_rank = [owned(F, G, g, self.used)[1] - owned(F, G, g, self.used)[0]
+                         for g in range(G)]
+        self.p_lo, self.p_hi = owned(F, G, self.rank, self.used)
         cs = getattr(ops, "can_sample", False)
         self.sampled = bool(cs(self.world) if callable(cs) else cs)
         # the first layout tried each step: the narrowest the ops offer
@@ -563,7 +587,7 @@ class DistributedJoin:
         tcnt = self._small("xtc" + key, (nb, G * K), dev=dev)
         # [4 G + 2]: the largest row message of any rank (all_to_all rounds)
         summary = self._small("xsm" + key, (4 * G + 3,), dev=dev)
-        xsend(start, cnt, fl, G, inp, chunk)
+        xsend(start, cnt, fl, G, inp, chunk, self.used)
         if G == 1:
             msg = inp
         else:

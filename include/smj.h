@@ -761,7 +761,10 @@ uint32_t smj_sampled_shards(void);
  * range partition into F partitions of K shard regions (start/cnt: F x K
  * int64, exact partitions use shard 0; flags: uint32[2] = region overflow,
  * not packable, as smj_dev_partition_range_sampled writes them) goes to
- * `world` ranks, partition p to rank p*world/F.
+ * `world` ranks: of the `used` partitions the plan's key range reaches
+ * (0 = all F), partition p goes to rank p*world/used, and the partitions
+ * from `used` on to the last rank (the ranks split the keys, not the
+ * power-of-two partition space).
  * smj_dev_xsend writes the message to every rank g, rank after rank
  * ([chunk size, used elements, flags[1], flags[0], the owned regions'
  * offsets inside the chunk, their counts]: 4 + 2 K n_g int64 for n_g owned
@@ -771,10 +774,11 @@ uint32_t smj_sampled_shards(void);
  * tcnt: nbuckets x world*K, bucket-major; the rank's own chunk in place at
  * its chunk start, the others from element `cap` on, rank order) and
  * summary[4 world + 2] = chunk starts, chunk sizes (sends), receive sizes,
- * used elements received, max not-packable flag, max overflow flag. */
+ * used elements received, the not-packable and overflow flags OR-ed over
+ * the ranks. */
 void smj_dev_xsend(const int64_t * start, const int64_t * cnt, const unsigned int * flags,
-                   uint32_t F, uint32_t K, uint32_t world, int64_t * msg, int64_t * chunk,
-                   smj_stream_t stream);
+                   uint32_t F, uint32_t K, uint32_t world, uint32_t used, int64_t * msg,
+                   int64_t * chunk, smj_stream_t stream);
 void smj_dev_xrecv(const int64_t * msg, const int64_t * chunk, uint32_t world, uint32_t rank,
                    uint32_t mine, uint32_t K, uint32_t nbuckets, uint64_t cap,
                    int64_t * tstart, int64_t * tcnt, int64_t * summary, smj_stream_t stream);

@@ -254,17 +254,17 @@ struct HostOps {
     }
     // exchange.hip k_xsend
     void xsend(const int64_t* start, const int64_t* cnt, const uint32_t* flags, uint32_t F,
-               uint32_t Kk, uint32_t G, int64_t* msg, int64_t* chunk) {
+               uint32_t Kk, uint32_t G, uint32_t U, int64_t* msg, int64_t* chunk) {
         int64_t cend = 0;
         std::vector<int64_t> used(G, 0);
         for (uint32_t p = 0; p < F; p++)
             for (uint32_t q = 0; q < Kk; q++) {
                 const size_t i = (size_t)p * Kk + q;
                 cend = std::max(cend, start[i] + cnt[i]);
-                used[(uint64_t)p * G / F] += cnt[i];
+                used[p < U ? (uint64_t)p * G / U : G - 1] += cnt[i];
             }
         for (uint32_t g = 0; g < G; g++) {
-            const uint32_t lo = mg::owned_lo(F, G, g), hi = mg::owned_lo(F, G, g + 1);
+            const uint32_t lo = mg::owned_lo(F, G, U, g), hi = mg::owned_lo(F, G, U, g + 1);
             const int64_t cs = start[(size_t)lo * Kk];
             const int64_t ce = g + 1 < G ? start[(size_t)hi * Kk] : cend;
             chunk[g] = cs;

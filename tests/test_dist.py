@@ -312,7 +312,7 @@ def _worker(rank, world, port, n, q, s_payload="negative", mode="sampled", plane
         else:
             assert getattr(ops, "whole_calls", 0) == 2 and getattr(ops, "stage_calls", 0) == 0
         # every key this rank sorted is in its contiguous share of the range
-        own = owners(dj.fanout, world)
+        own = owners(dj.fanout, world, dj.used)
         for got in (sR, sS):
             d = range_digit(got[:, 1], 1, total, dj.pbits)
             assert bool((own[d] == rank).all())
@@ -470,10 +470,14 @@ def test_owners_and_send_counts():
     from smj.dist import owned, owners, plan_shift, send_counts
     assert owners(8, 2).tolist() == [0, 0, 0, 0, 1, 1, 1, 1]
     assert owners(8, 3).tolist() == [0, 0, 0, 1, 1, 1, 2, 2]
-    for F, G in ((8, 3), (4096, 8), (2048, 3), (64, 5)):
-        own = owners(F, G)
+    # 5 of 8 partitions hold keys: those split, the empty top to the last rank
+    assert owners(8, 2, 5).tolist() == [0, 0, 0, 1, 1, 1, 1, 1]
+    assert owners(8, 3, 5).tolist() == [0, 0, 1, 1, 2, 2, 2, 2]
+    for F, G, U in ((8, 3, 8), (4096, 8, 4096), (2048, 3, 2048), (64, 5, 64), (1024, 8, 977),
+                    (1024, 3, 977), (16, 8, 3), (8, 8, 1)):
+        own = owners(F, G, U)
         for g in range(G):
-            lo, hi = owned(F, G, g)
+            lo, hi = owned(F, G, g, U)
             assert own[lo:hi].eq(g).all() and int(own.eq(g).sum()) == hi - lo
     # 1..2^30 in 4096 partitions of 2^18 keys (make_plan's s1)
     assert plan_shift(1, 1 << 30, 12) == 18
@@ -488,7 +492,7 @@ def test_local_range_int64_edges():
     ranges that reach INT64_MIN / INT64_MAX."""
     import sys
     sys.path.insert(0, PKG)
-    from smj.dist import INT64_MAX, local_range, owned, plan_shift
+    from smj.dist import INT64_MAX, local_range, owned, plan_shift, used_parts
     lo64 = -(1 << 63)
     cases = [(1, 128_000_000), (lo64, INT64_MAX), (1, (1 << 62) + 1), (lo64, 5),
              (INT64_MAX - 1000, INT64_MAX), (7, 7)]
@@ -502,7 +506,7 @@ def test_local_range_int64_edges():
                 assert b <= kmin and lo64 <= klo <= khi <= INT64_MAX
                 gs1 = plan_shift(b, kmax, pbits)
                 assert plan_shift(klo, khi, lbits) == gs1  # same partition width
-                p_lo, p_hi = owned(1 << pbits, world, rank)
+                p_lo, p_hi = owned(1 << pbits, world, rank, used_parts(kmin, kmax, pbits))
                 if (p_lo << gs1) < (1 << max(kmax - kmin, 0).bit_length()):
                     assert klo == b + (p_lo << gs1)
                 assert (1 << lbits) >= p_hi - p_lo
@@ -565,3 +569,34 @@ def test_next_layout_ladder():
     k = J(False, False)
     assert k._next_layout("planes", True, BAD_PAYLOAD48, 0) == ("tuples", False)
     assert k._next_layout("planes", True, 0, 1) == ("tuples", False)
+
+
+@pytest.mark.parametrize("G", [2, 3, 4, 8])
+@pytest.mark.parametrize("total", [None, 1_024_000_000, 128_000_000, 3_000_000])
+def test_rank_key_balance(G, total):
+    """Keys 1..total over G ranks (None: the weak-scaled benchmark, 128M per
+    rank): every rank owns one contiguous key range of whole partitions, at
+    most one partition more than its share of the partitions the keys reach,
+    and on the benchmark's shapes the largest holds at most 1 % more keys
+    than the mean (uniform keys: the rank loads).  The power-of-two partition
+    space split evenly would give ranks 0-6 134M keys each and rank 7 85M at
+    keys 1..1024M (1.048x the mean)."""
+    bench_shape = total is None
+    total = total or 128_000_000 * G
+    import sys
+    sys.path.insert(0, PKG)
+    from smj.dist import local_range, owned, partition_bits, used_parts
+    kmin, kmax = 1, total
+    pbits = partition_bits(8, G, True, total // G, (kmin, kmax))
+    F, U = 1 << pbits, used_parts(kmin, kmax, pbits)
+    base = local_range(kmin, kmax, pbits, G, 0)[0]
+    s1 = max((kmax - base).bit_length() - pbits, 0)
+    keys = []
+    for g in range(G):
+        lo, hi = owned(F, G, g, U)
+        a, b = max(base + (lo << s1), kmin), min(base + (hi << s1) - 1, kmax)
+        keys.append(max(b - a + 1, 0))
+    assert sum(keys) == total
+    assert max(keys) <= -(-U // G) << s1, keys
+    if bench_shape:
+        assert max(keys) / (total / G) <= 1.01, keys

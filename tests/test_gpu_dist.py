@@ -34,7 +34,7 @@ def _inputs(orc, kind, n):
 @pytest.mark.parametrize("packed", [False, True])
 def test_segmented_join_simulated_exchange(libs, oracles, width, world, kind, packed):
     import torch
-    from smj.dist import DistributedJoin, ceil_log2, owned, plan_shift
+    from smj.dist import DistributedJoin, ceil_log2, owned, plan_shift, used_parts
     orc, lib = oracles[width], libs[width]
     if packed and width != 16:
         pytest.skip("packed words are the 16-byte layout")
@@ -65,7 +65,7 @@ def test_segmented_join_simulated_exchange(libs, oracles, width, world, kind, pa
             parts[key, s] = (out, hist)
     got_total = 0
     for g in range(world):
-        p_lo, p_hi = owned(F, world, g)
+        p_lo, p_hi = owned(F, world, g, used_parts(1, n, pbits))
         lbits = ceil_log2(max(p_hi - p_lo, 1))
         key_lo = 1 + (p_lo << s1)
         key_hi = key_lo + (1 << (s1 + lbits)) - 1
@@ -114,7 +114,7 @@ def test_sampled_exchange_simulated(libs, oracles, width, world, kind, layout, s
     in two planes (smj_dev_partition_range_planes and
     smj_dev_join_segmented_planes), both widths."""
     import torch
-    from smj.dist import Planes, ceil_log2, owned, plan_shift
+    from smj.dist import Planes, ceil_log2, owned, plan_shift, used_parts
     orc, lib = oracles[width], libs[width]
     packed = layout == "words"
     if packed and width != 16:
@@ -157,7 +157,7 @@ def test_sampled_exchange_simulated(libs, oracles, width, world, kind, layout, s
             parts[key, s] = (out, ss, sc)
     got_total = 0
     for g in range(world):
-        p_lo, p_hi = owned(F, world, g)
+        p_lo, p_hi = owned(F, world, g, used_parts(1, n, pbits))
         mine = p_hi - p_lo
         lbits = ceil_log2(max(mine, 1))
         key_lo = 1 + (p_lo << s1)
@@ -264,11 +264,14 @@ def test_distributed_join_one_rank_rccl(libs, width, xsampled, monkeypatch):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("F,G", [(256, 1), (512, 2), (1024, 3), (1024, 8), (16, 16)])
-def test_exchange_table_kernels(libs, F, G):
+@pytest.mark.parametrize("F,G,U", [(256, 1, 256), (512, 2, 512), (1024, 3, 1024), (1024, 8, 1024),
+                                   (16, 16, 16), (1024, 8, 977), (1024, 3, 977), (512, 2, 489),
+                                   (16, 4, 3)])
+def test_exchange_table_kernels(libs, F, G, U):
     """smj_dev_xsend / smj_dev_xrecv (exchange.hip) against their framework-op
     statement in smj/dist.py (xsend_torch / xrecv_torch, which the gloo tests
-    run): random region tables with empty regions, every rank's view."""
+    run): random region tables with empty regions, every rank's view; U of
+    the F partitions reach the key range (the ranks split those)."""
     import torch
     from smj.dist import HEAD, owned, xrecv_torch, xsend_torch
     lib = libs[16]
@@ -280,14 +283,14 @@ def test_exchange_table_kernels(libs, F, G):
     size = cnt + slack
     start = (torch.cumsum(size.reshape(-1), 0) - size.reshape(-1)).view(F, K)
     flags = torch.tensor([0, 1], dtype=torch.int32)  # [overflow, not packable]
-    per = [owned(F, G, r)[1] - owned(F, G, r)[0] for r in range(G)]
+    per = [owned(F, G, r, U)[1] - owned(F, G, r, U)[0] for r in range(G)]
     mlen = sum(HEAD + 2 * K * m for m in per)
     want_msg, want_chunk = torch.empty(mlen, dtype=torch.int64), torch.empty(2 * G, dtype=torch.int64)
-    xsend_torch(start, cnt, flags, G, want_msg, want_chunk)
+    xsend_torch(start, cnt, flags, G, want_msg, want_chunk, U)
     d = {k: v.cuda() for k, v in dict(start=start, cnt=cnt, flags=flags).items()}
     msg = torch.full((mlen,), -5, dtype=torch.int64, device="cuda")
     chunk = torch.empty(2 * G, dtype=torch.int64, device="cuda")
-    lib.dev_xsend(d["start"], d["cnt"], d["flags"], G, msg, chunk)
+    lib.dev_xsend(d["start"], d["cnt"], d["flags"], G, msg, chunk, U)
     torch.cuda.synchronize()
     assert torch.equal(msg.cpu(), want_msg) and torch.equal(chunk.cpu(), want_chunk)
     # rank r receives, from every source, that source's message to r (here:

@@ -220,7 +220,7 @@ def test_plan_arithmetic_matches_dist_py():
     import tempfile
     from conftest import PKG
     sys.path.insert(0, PKG)
-    from smj.dist import local_range, partition_bits
+    from smj.dist import local_range, partition_bits, used_parts
     probe = r'''
 #include "%s"
 #include <stdio.h>
@@ -231,7 +231,8 @@ int main() {
     unsigned pb[][2] = {{9, 1}, {10, 2}, {11, 3}, {11, 8}, {4, 5}, {9, 8}};
     for (auto& c : cases) for (auto& p : pb) for (unsigned r = 0; r < p[1]; r++) {
         auto l = smj::mg::local_range(c[0], c[1], p[0], p[1], r);
-        printf("%%lld %%lld %%lld %%u\n", (long long)l.base, (long long)l.key_lo, (long long)l.key_hi, l.lbits);
+        printf("%%lld %%lld %%lld %%u %%u\n", (long long)l.base, (long long)l.key_lo, (long long)l.key_hi, l.lbits,
+               smj::mg::used_parts(c[0], c[1], p[0]));
     }
     unsigned long long ns[] = {0, 1000, 128000000, 256000000};
     for (unsigned bb = 6; bb <= 9; bb++) for (unsigned G = 1; G <= 16; G *= 2)
@@ -251,7 +252,7 @@ int main() {
         for pbits, world in ((9, 1), (10, 2), (11, 3), (11, 8), (4, 5), (9, 8)):
             for rank in range(world):
                 b, klo, khi, lb = local_range(kmin, kmax, pbits, world, rank)
-                want.append(f"{b} {klo} {khi} {lb}")
+                want.append(f"{b} {klo} {khi} {lb} {used_parts(kmin, kmax, pbits)}")
     for bb in range(6, 10):
         G = 1
         while G <= 16:
