@@ -80,14 +80,6 @@ constexpr int TP_THREADS = SMJ_TP_THREADS;
 #ifndef SMJ_GS_ARGS_MEM
 #define SMJ_GS_ARGS_MEM 1
 #endif
-// the skew path's statistics on stderr (lab builds: make EXTRA=-DSMJ_LAB_DIAG=1)
-#ifndef SMJ_LAB_DIAG
-#define SMJ_LAB_DIAG 0
-#endif
-#ifndef SMJ_GS_ABL
-#define SMJ_GS_ABL 0  // ablations for measurements only (1: no in-group sort; 2: no
-                      // equal-digit run fixing; 3: no write-out; profiles/r05_lab/abl.txt)
-#endif
 // elements a tile-pass thread holds: the stage of a tile is 128 KB of LDS
 // (16-byte elements: 16-byte tuples in their own layout take half the tile)
 template <class W>
@@ -878,19 +870,6 @@ __device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS<typename
     const uint32_t tid = otid(), wid = tid >> 6, lane = tid & 63;
     const uint32_t cb = PAIR && r ? C.b[1] : C.b[0], cg = PAIR && r ? C.g[1] : C.g[0];
     const uint32_t d12 = (cb << P.D2) | cg;
-#if SMJ_GS_ABL == 1
-    {   // ablation (measurements only): no sort, gathered order written out
-        Tup* dst = A.out[r] + C.ost[r] + off;
-#pragma unroll
-        for (int k = 0; k < GS_ITEMS; k++) {
-            const uint32_t j = k * GS_THREADS + tid;
-            if (j < nr) st_stream(dst + j, Lay::unpack(P, v[k], cb));
-        }
-        after_place();
-        __syncthreads();
-        return true;
-    }
-#endif
     // ---- level-3 digits, histogram (two u16 counters per word).  Only the
     // first and the last group of the plan can hold keys outside its range
     // (plan_rel clamps them there); every other group takes the 32-bit digit.
@@ -957,7 +936,7 @@ __device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS<typename
     }
     after_place();
     __syncthreads();
-    if (dup && SMJ_GS_ABL != 2) {
+    if (dup) {
         // ---- equal-digit runs.  The group is ordered by digit, so an
         // inversion can only sit inside such a run: one parallel pass finds
         // out whether any needs sorting (never for equal tuples of a hot key).
@@ -993,7 +972,7 @@ __device__ __forceinline__ bool sort_group(const GroupArgs& A, GroupLDS<typename
 #pragma unroll
     for (int k = 0; k < GS_ITEMS; k++) {
         const uint32_t j = k * GS_THREADS + tid;
-        if (j < nr && SMJ_GS_ABL != 3) st_stream(dst + j, Lay::unpack(P, L.B[j], cb));
+        if (j < nr) st_stream(dst + j, Lay::unpack(P, L.B[j], cb));
     }
     return true;
 }
@@ -1061,27 +1040,6 @@ __device__ __forceinline__ uint32_t sort_two(const GroupArgs& A, GroupLDS<typena
                                              unsigned long long& matches, bool& exact,
                                              Hook0&& after0, Hook1&& after1) {
     typedef typename Lay::W W;
-#if SMJ_GS_ABL == 1
-    {   // ablation (timing only): no sort, each lane writes its elements to
-        // the group's place in gathered order (the output is not sorted, the
-        // count not taken)
-        const uint32_t t = otid();
-#pragma unroll
-        for (int r = 0; r < 2; r++) {
-            const W(&v)[GS_ITEMS] = r ? v1 : v0;
-            const uint32_t cb = PAIR && r ? C.b[1] : C.b[0];
-            Tup* dst = A.out[r] + C.ost[r] + off[r];
-            const typename Lay::Unpack up(P, cb);
-#pragma unroll
-            for (int k = 0; k < GS_ITEMS; k++)
-                if (k * GS_THREADS + t < nr[r]) st_stream(dst + k * GS_THREADS + t, up(v[k]));
-            if (r == 0) after0(); else after1();
-        }
-        __syncthreads();
-        exact = true;
-        return 0u;
-    }
-#endif
     const uint32_t tid = otid(), wid = tid >> 6, lane = tid & 63;
     // the d3 digit of slot r's elements: the fast form unless the group is
     // an edge group of the plan (the branch is uniform: taken outside the
@@ -1233,7 +1191,7 @@ __device__ __forceinline__ uint32_t sort_two(const GroupArgs& A, GroupLDS<typena
 #pragma unroll
         for (int k = 0; k < GS_ITEMS; k++) {
             const uint32_t j = k * GS_THREADS + tid;
-            if (j < nr[r] && SMJ_GS_ABL != 3) st_stream(dst + j, up(L.B[j]));
+            if (j < nr[r]) st_stream(dst + j, up(L.B[j]));
         }
     };
     uint32_t failed = 0;
@@ -1241,7 +1199,7 @@ __device__ __forceinline__ uint32_t sort_two(const GroupArgs& A, GroupLDS<typena
     place(0, L.cur, fl & 1, v0);
     after0();
     __syncthreads();
-    if ((fl & 1) && SMJ_GS_ABL != 2 && !fix(0, L.cur)) failed |= 1;
+    if ((fl & 1) && !fix(0, L.cur)) failed |= 1;
     if (!failed) write(0);
     // ---- slot 1 (a join whose R failed leaves S to the skew path too)
     if (!(join && failed)) {
@@ -1249,7 +1207,7 @@ __device__ __forceinline__ uint32_t sort_two(const GroupArgs& A, GroupLDS<typena
         place(1, L.cnt[1], fl & 2, v1);
         after1();
         __syncthreads();
-        if ((fl & 2) && SMJ_GS_ABL != 2 && !fix(1, L.cnt[1])) failed |= 2;
+        if ((fl & 2) && !fix(1, L.cnt[1])) failed |= 2;
         if (!(failed & 2)) write(1);
     } else {
         after1();
@@ -1993,14 +1951,6 @@ static void skew_path(Workspace* ws, const GroupArgs& G, OvfEntry* ovf, uint32_t
         }
     }
     const size_t nl = large.size();
-    if (SMJ_LAB_DIAG) {  // lab builds only (make EXTRA=-DSMJ_LAB_DIAG=1)
-        uint64_t ts = 0, tl = 0;
-        for (uint32_t i : small) ts += he[i].nr[0] + (nrel > 1 ? he[i].nr[1] : 0);
-        for (uint32_t i : large) tl += he[i].nr[0] + (nrel > 1 ? he[i].nr[1] : 0);
-        fprintf(stderr, "[skew] %zu small groups (%llu tuples), %zu large (%llu tuples), "
-                "%zu items\n", small.size(), (unsigned long long)ts, nl,
-                (unsigned long long)tl, items.size());
-    }
     const size_t lbytes = (small.size() + 2 * nl) * 4;
     const size_t ibytes = items.size() * sizeof(uint4);
     unsigned char* hbuf = (unsigned char*)ws->host_pinned("sk_h", lbytes + ibytes + 16);
@@ -2054,9 +2004,6 @@ static void skew_path(Workspace* ws, const GroupArgs& G, OvfEntry* ovf, uint32_t
     std::vector<uint32_t> rest;
     for (uint32_t i = 0; i < no; i++)
         if (flags[i] != 0 || G.plan.s3 != 0) rest.push_back(i);
-    if (SMJ_LAB_DIAG)
-        fprintf(stderr, "[smj] skew: %u queued groups (%zu small, %zu large, %zu items), "
-                "%zu left to the merge sort\n", no, small.size(), nl, items.size(), rest.size());
     if (rest.empty()) return;
     for (int r = 0; r < nrel; r++) {
         std::vector<uint64_t> so, sl;
@@ -2482,13 +2429,6 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
         SMJ_CHECK(hipGetLastError());
         return true;  // the group pass comes with a later call
     }
-#ifdef SMJ_LAB_FLUSH
-    {   // lab build only: evict the Infinity Cache between the tile and the
-        // group pass (1 GiB of stores), to measure what its residency buys
-        void* fl = ws->scratch("lab_flush", (size_t)1 << 30);
-        SMJ_CHECK(hipMemsetAsync(fl, SMJ_LAB_FLUSH, (size_t)1 << 30, st));
-    }
-#endif
     if (a.ev_bucket) SMJ_CHECK(hipEventRecord(a.ev_bucket, st));
     {
         const uint32_t maxwg =

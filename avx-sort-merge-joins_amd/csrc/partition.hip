@@ -507,22 +507,6 @@ constexpr int vmcnt_imm(int n) { return (n & 15) | ((n >> 4) << 14) | 0x0f70; }
 // tile's stores.  The loads thus fly under a whole tile of LDS work instead of
 // the stage phase alone.  Loads are non-temporal (NT; the input is read
 // once), 8-byte tuples leave in 16-byte pair stores.
-#ifdef SMJ_SWP_PROF
-// lab build only: per-phase cycle counts of k_scatter_swp, summed over the
-// workgroups' thread 0 (read by smj_swp_prof)
-__device__ unsigned long long g_swp_prof[16];
-#define SWP_MARK(k)                                            \
-    do {                                                       \
-        const uint64_t t_ = __builtin_readcyclecounter();      \
-        prof[k] += t_ - tprev;                                 \
-        tprev = t_;                                            \
-    } while (0)
-#else
-#define SWP_MARK(k) \
-    do {            \
-    } while (0)
-#endif
-
 template <int THREADS, int ITEMS, class DigitL, bool NT>
 struct SwpTile {
     // info[d][3] = segment start (12 bits) | carry size (3) | emission + carry (17)
@@ -530,10 +514,6 @@ struct SwpTile {
                   "segment numbers fit 12 bits");
     static_assert(SwaGeom<THREADS, ITEMS>::CW <= 7, "carry size fits 3 bits");
     static_assert(SwaGeom<THREADS, ITEMS>::TILE + 8 < (1 << 17), "T fits 17 bits");
-#ifdef SMJ_SWP_PROF
-    uint64_t prof[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    uint64_t tprev = 0;
-#endif
     typedef SwaGeom<THREADS, ITEMS> G;
     static constexpr int W = G::W;
     static constexpr int TILE = G::TILE;
@@ -589,9 +569,6 @@ struct SwpTile {
 
     __device__ __forceinline__ void tile(const Tup (&v)[ITEMS], Tup (&pre)[ITEMS],
                                          uint64_t base) {
-#ifdef SMJ_SWP_PROF
-        tprev = __builtin_readcyclecounter();
-#endif
         const uint32_t tcount = (uint32_t)min((uint64_t)TILE, end - base);
         uint32_t dg[ITEMS], rk[ITEMS];
 #pragma unroll
@@ -604,9 +581,7 @@ struct SwpTile {
             if (valid) old = atomicAdd(&w32[wid * hb + (d >> 1)], 1u << sh);
             rk[j] = (old >> sh) & 0xffffu;
         }
-        SWP_MARK(0);
         __syncthreads();
-        SWP_MARK(1);
         uint32_t cw[W];
         uint32_t c[2] = {0, 0}, E[2] = {0, 0}, ns[2] = {0, 0};
         if (owner) {
@@ -652,11 +627,9 @@ struct SwpTile {
                 for (uint32_t k = 0; k < ns[h]; k++) segown[sp[h] + k] = (uint16_t)d;
             }
         }
-        SWP_MARK(2);
         // the next-but-one tile (its registers held the previous tile)
         load(pre, base + 2 * (uint64_t)TILE);
         __syncthreads();
-        SWP_MARK(3);
 #pragma unroll
         for (int j = 0; j < ITEMS; j++)
             if (dg[j] != 0xffffffffu) {
@@ -665,7 +638,6 @@ struct SwpTile {
                 stage[wo + rk[j]] = v[j];
             }
         __syncthreads();
-        SWP_MARK(4);
         if (owner) {
 #pragma unroll
             for (int w = 0; w < W; w++) w32[w * hb + t2] = 0;
@@ -673,7 +645,6 @@ struct SwpTile {
         // the next tile and the previous tile's stores have landed; the
         // next-but-one tile's ITEMS loads stay in flight
         __builtin_amdgcn_s_waitcnt(vmcnt_imm(ITEMS));
-        SWP_MARK(5);
 #ifndef KEY_8B
         // 8-byte tuples: a lane writes two adjacent tuples of a segment with
         // one 16-byte store (SEG / 2 lanes per segment); a pair cut by its
@@ -722,9 +693,7 @@ struct SwpTile {
                     out[addr] = x;
             }
         }
-        SWP_MARK(6);
         __syncthreads();
-        SWP_MARK(7);
         // ---- the owner's leftovers (< SEG) become the carry.  An emission
         // (E > 0) ends on a segment boundary past the old carry (E > kc), so
         // the new carry comes from the stage alone; without one the old carry
@@ -750,7 +719,6 @@ struct SwpTile {
                 kc[h] = T - E[h];
             }
         }
-        SWP_MARK(8);
     }
 };
 
@@ -815,20 +783,8 @@ k_scatter_swp(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
             for (uint32_t e = 0; e < s.kc[h]; e++) out[s.pos[h] + e] = s.carry[d * CW + e];
         }
     }
-#ifdef SMJ_SWP_PROF
-    if (threadIdx.x == 0)
-        for (int k = 0; k < 9; k++) atomicAdd(&g_swp_prof[k], (unsigned long long)s.prof[k]);
-#endif
 }
 
-#ifdef SMJ_SWP_PROF
-extern "C" void smj_swp_prof(unsigned long long* out) {
-    SMJ_CHECK(hipDeviceSynchronize());
-    SMJ_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_swp_prof), 16 * 8));
-    static const unsigned long long z[16] = {0};
-    SMJ_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_swp_prof), z, 16 * 8));
-}
-#endif
 
 // Histogram of the stable write-combining partition: counts[d][wg] of each
 // workgroup's chunk (the scatter's chunking), two register tiles alternating

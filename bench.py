@@ -170,12 +170,16 @@ def alg_bytes_per_launch(name, n_rel, nR, nS, w, op="join"):
     """Algorithmic HBM bytes of one launch: a materialising
     pass reads and writes every tuple once (2w), a histogram reads once (w).
     The join's tile and group passes take R and S in one launch; a sort's
-    take its one relation."""
+    take its one relation.  SURVEY.md §8(d) credits the join 5w a tuple:
+    the partition 2w (k_scatter), the sort 2w and the merge-join scan 1w.
+    The sort is two passes here, so the tile pass (an intermediate level,
+    in place) is credited 1w and the group pass, which writes the sorted
+    relation and counts, 2w: the per-kernel credits add up to 5w."""
     both = (nR + nS) if op == "join" else n_rel
     return {
         "k_hist": n_rel * w,                 # one relation per launch
         "k_scatter": 2 * n_rel * w,          # one relation per launch
-        "k_tilepass": 2 * both * w,
+        "k_tilepass": both * w,
         "k_groupsort": 2 * both * w,
         "k_km_merge": 2 * n_rel * w,         # every tuple of the runs, once
     }.get(name)
