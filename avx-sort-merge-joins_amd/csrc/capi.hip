@@ -411,6 +411,7 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
     // 1024M x 1024M join: 2^9 partitions leave 27 payload bits).
     const bool p48_fits = hplan.s1 >= 1 && hplan.s1 <= 32 && hplan.span < (1ull << (48 - hplan.s1));
     const uint64_t shape = ((uint64_t)nrel << 62) ^ ns[0] ^ (nrel > 1 ? ns[1] << 31 : 0);
+    Workspace::ShapeHint& H = ws->hint_for(shape);
     // 48-bit words, whatever their payloads
     auto p48_ok = [&]() {
 #ifdef KEY_8B
@@ -422,10 +423,10 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
     };
     // 32-bit words (mode -2) are tried first: nothing tells the payloads'
     // width beforehand, and a shape whose payloads did not fit does not try
-    // them again (p32_fail_shape)
+    // them again (Workspace::ShapeHint::p32_fail)
     auto first_mode = [&]() {
         if (sampled && plan_on_host && use_packing(ws) && use_p32(ws) &&
-            LayP32::usable(hplan) && ws->p32_fail_shape != shape)
+            LayP32::usable(hplan) && !H.p32_fail)
             return -2;
         if (p48_ok() && p48_fits) return -1;
         return can_pack ? 0 : (sampled ? 1 : 2);
@@ -439,9 +440,8 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
     bool hinted = false;
     auto hinted_mode = [&](int m) {
         hinted = false;
-        if (ws->mode_hint <= m || ws->hint_shape != shape || ++ws->hint_calls % 16 == 0)
-            return m;
-        const int h = ws->mode_hint == 0 ? (can_pack ? 0 : (sampled ? 1 : 2))
+        if (H.mode_hint <= m || ++H.calls % 16 == 0) return m;
+        const int h = H.mode_hint == 0 ? (can_pack ? 0 : (sampled ? 1 : 2))
                                          : (sampled ? 1 : 2);
         hinted = h > m;
         return h > m ? h : m;
@@ -531,7 +531,7 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
             // from 64-bit words
             const bool pay = !why[0] && !(why[1] & kBadRange);
             if (pay && (why[1] & (kBadPayload | kBadPayload48 | kBadPayload32)))
-                ws->p32_fail_shape = shape;
+                H.p32_fail = true;
             if (pay && !(why[1] & (kBadPayload | kBadPayload48)) && p48_ok())
                 mode = -1;
             else if (pay && !(why[1] & kBadPayload) && can_pack)
@@ -569,12 +569,10 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
     }
     ws->last_layout = mode == -2 ? SMJ_LAYOUT_USED_P32 : mode == -1 ? SMJ_LAYOUT_USED_P48
                     : mode == 0 ? SMJ_LAYOUT_USED_WORDS : SMJ_LAYOUT_USED_TUPLES;
-    if (payload_fb >= 0) {
-        ws->mode_hint = payload_fb;
-        ws->hint_shape = shape;
-    } else if (!started_hinted) {
-        ws->mode_hint = -2;  // the narrow layouts held (or failed for other reasons)
-    }
+    if (payload_fb >= 0)
+        H.mode_hint = payload_fb;
+    else if (!started_hinted)
+        H.mode_hint = -2;  // the narrow layouts held (or failed for other reasons)
     SMJ_CHECK(hipEventRecord(ws->ev[4], st));
 }
 

@@ -68,16 +68,39 @@ struct Workspace {
     // layouts this workspace's sorts and joins may not use
     // (smj_workspace_set_layouts, SMJ_LAYOUT_* in smj.h)
     uint32_t layouts_off = 0;
-    // the layout the last join or sort of shape hint_shape reached after
-    // leaving the narrower ones for its payloads (-2: none; capi.hip
-    // device_bucket), and the calls since (a re-probe every 16th)
-    int mode_hint = -2;
-    uint64_t hint_shape = 0;
-    uint32_t hint_calls = 0;
-    // the shape of the last call whose payloads did not fit 32-bit words: the
-    // next calls of that shape start at the wider layouts (no re-probe; the
-    // 32-bit words are for relations with tiny payloads, e.g. the sort's)
-    uint64_t p32_fail_shape = ~0ull;
+    // What the last joins and sorts of a few shapes (relation sizes) learnt
+    // about their payloads (capi.hip device_bucket), least recently used
+    // first out, so a caller alternating shapes on one workspace (sort R,
+    // sort S, join R and S) keeps every shape's:
+    //   mode_hint: the layout the last call reached after leaving the
+    //     narrower ones for its payloads (-2: none), with a re-probe every
+    //     16th call (calls);
+    //   p32_fail: its payloads did not fit 32-bit words, so its calls start at
+    //     the wider layouts (no re-probe: the 32-bit words are for relations
+    //     with tiny payloads, e.g. the sort's).
+    struct ShapeHint {
+        uint64_t shape = ~0ull;
+        int mode_hint = -2;
+        uint32_t calls = 0;
+        bool p32_fail = false;
+        uint64_t used = 0;  // LRU clock
+    };
+    ShapeHint hints[8];
+    uint64_t hint_clock = 0;
+    ShapeHint& hint_for(uint64_t shape) {
+        ShapeHint* victim = &hints[0];
+        for (ShapeHint& h : hints) {
+            if (h.shape == shape) {
+                h.used = ++hint_clock;
+                return h;
+            }
+            if (h.used < victim->used) victim = &h;
+        }
+        *victim = ShapeHint();
+        victim->shape = shape;
+        victim->used = ++hint_clock;
+        return *victim;
+    }
     int last_layout = -1;  // smj_workspace_last_layout (SMJ_LAYOUT_USED_*)
     std::map<std::string, std::pair<void*, size_t>> bufs;
     std::map<std::string, std::pair<void*, size_t>> pinned;

@@ -799,3 +799,37 @@ def test_join_p32_words(libs, oracles, width, n):
         assert np.array_equal(lib.to_host(sR), eR)
         assert np.array_equal(lib.to_host(sS), eS)
         assert lib.last_layout() == ("p32" if n < 1_000_000 else "p48"), (call, lib.last_layout())
+
+
+def test_layout_hints_per_shape(libs, oracles):
+    """A workspace alternating two join shapes whose payloads do not fit
+    32-bit words (row ids + 2^30) tries the 32-bit words once per shape, not
+    on every call: the workspace keeps each shape's hint (capi.hip
+    device_bucket, Workspace::ShapeHint).  A call that skips them partitions
+    each relation once (two k_scatter launches); every call gives the
+    oracle's count and sorted relations in the 48-bit words."""
+    import torch
+    orc, lib = oracles[16], libs[16]
+    cases = []
+    for nR, nS in ((300_007, 300_007), (200_003, 500_009)):
+        R, S = make_join_inputs(orc, 16, "pk_fk", nR, nS)
+        R["payload"] += np.int64(1) << 30
+        S["payload"] += np.int64(1) << 30
+        exp, eR, eS = orc.sortmergejoin(R, S)
+        cases.append((lib.to_device(R), lib.to_device(S), lib.empty(nR), lib.empty(nS),
+                      nR, exp, eR, eS))
+    lib.reset_workspace()
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    for call in range(6):
+        dR, dS, sR, sS, nR, exp, eR, eS = cases[call % 2]
+        lib.trace(True)
+        lib.dev_join(dR, dS, sR, sS, cnt, 8, 1, nR)
+        torch.cuda.synchronize()
+        launches = lib.trace_read().get("k_scatter", (0, 0))[1]
+        lib.trace(False)
+        assert int(cnt.item()) == exp, call
+        assert np.array_equal(lib.to_host(sR), eR), call
+        assert np.array_equal(lib.to_host(sS), eS), call
+        assert lib.last_layout() == "p48", (call, lib.last_layout())
+        if call >= 2:
+            assert launches == 2, (call, launches)
