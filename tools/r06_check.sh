@@ -8,7 +8,7 @@ T=${1:-r06a}
 O=gpurun_out/$T
 mkdir -p $O
 PY="python -u -m pytest -x -v --timeout 600 --timeout-method thread -m gpu"
-timeout -k 10 600 $PY tests/test_gpu_mgpu.py tests/test_gpu_dist.py > $O/pytest_mgpu.txt 2>&1 &&
+timeout -k 10 600 $PY tests/test_gpu_mgpu.py tests/test_gpu_dist.py tests/test_gpu_parity.py > $O/pytest_mgpu.txt 2>&1 &&
 timeout -k 10 900 $PY tests/test_gpu_fullsize.py -k "payload_layouts or copy8_zipf" > $O/pytest_full.txt 2>&1 &&
 timeout -k 10 300 python bench.py --no-cpu-baseline > $O/join16.json 2> $O/join16.err &&
 timeout -k 10 300 python bench.py --no-cpu-baseline --exchange-path --impl c > $O/xpathc16.json 2> $O/xpathc16.err &&
