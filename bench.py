@@ -128,6 +128,11 @@ def parse():
                         "wide48 = 2^40 + row id (64-bit packed words, 8 bytes); full64 = "
                         "random 64-bit values, negative ones included (the 16-byte "
                         "tuples themselves)")
+    p.add_argument("--sim-world", type=int, default=8,
+                   help="--op exchange on ONE GPU: time the exchange's device side as rank 0 "
+                        "of a world of this many GPUs would run it (its slice of the weak-scaled "
+                        "relation, the exact range partition into that world's partitions and "
+                        "layout, the table kernels; nothing crosses xGMI on one GPU)")
     p.add_argument("--fanout-bits", type=int, default=8,
                    help="level-1 partitions (2^bits) of the join; the library raises it "
                         "as the relation size needs")
@@ -939,6 +944,10 @@ def run_exchange(a, json_out, N, rank, local):
     w = a.width or 16
     lib = smj.load(w)
     n = a.n or 128_000_000
+    if N == 1 and a.sim_world > 1:
+        run_exchange_device_side(a, json_out, lib, n, w)
+        _close(dist)
+        return
     total = n * N
     R = lib.empty(n)
     lib.dev_gen_pk(R, n * rank, total, 12345)
@@ -995,6 +1004,75 @@ def run_exchange(a, json_out, N, rank, local):
         }
         print(json.dumps(out), file=json_out, flush=True)
     _close(dist)
+
+
+def run_exchange_device_side(a, json_out, lib, n, w):
+    """--op exchange on one GPU: what a rank of a --sim-world G world does on
+    its own GPU for the exchange, timed against HBM (the rows themselves
+    cross xGMI only with G GPUs).  S is rank 0's slice of the weak-scaled
+    relation (n tuples, FK keys over 1..G n); one step = DistributedJoin's
+    exchange attempt for S as rank 0 of G ranks runs it: the exact range
+    partition into G ranks' partitions (histogram + scatter, the layout the
+    plan allows: 64-bit words for 16-byte tuples at G = 8) and the table
+    kernels (k_xsend, k_xrecv) with the summary read.  The roofline is the
+    scatter's: it reads every tuple and writes its element once."""
+    from smj.dist import DeviceOps, DistributedJoin, owned, partition_bits, row_bytes, used_parts
+    G = a.sim_world
+    total = n * G
+    S = lib.empty(n)
+    lib.dev_gen_fk(S, 0, total, total, 54321)
+    torch.cuda.synchronize()
+    pbits = partition_bits(a.fanout_bits, G, True, n, (1, total))
+    dj = DistributedJoin(DeviceOps(lib, sampled=False), a.fanout_bits, 1, total, n_hint=n,
+                         pbits=pbits)
+    res = {}
+
+    def step():
+        res["x"] = dj._exchange(S, "S")
+    elapsed, kern, brk = timed_loop(a, lib, None, step)
+    xb = dj.last_rows["S"][0]
+    eb = row_bytes(xb)
+    lay = dj.last_layout
+    # rows rank 0 keeps: the partitions it owns among G ranks
+    F, U = 1 << pbits, used_parts(1, total, pbits)
+    lo, hi = owned(F, G, 0, U)
+    t = elapsed / a.steps
+    # the scatter: reads the tuple, writes its exchange element
+    sc_ms, sc_n = kern.get("k_scatter", (0.0, 0))
+    alg_sc = n * (w + eb)
+    roof = None
+    if sc_n:
+        ach = alg_sc / (sc_ms / sc_n / 1e3) / 1e9
+        roof = {"bound": "hbm", "kernel": "k_scatter (exact range partition)",
+                "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                "alg_bytes_per_launch": alg_sc, "avg_launch_ms": round(sc_ms / sc_n, 4)}
+    leave = n * (G - 1) / G * eb  # uniform keys: (G-1)/G of the rows leave the rank
+    xgmi_peak = 7 * 153.0
+    out = {
+        "metric": "exchange (the join's row exchange) GB/s per GPU over xGMI",
+        "value": 0.0, "unit": "GB/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(t * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": {"words": "int64", "planes": "u48"}.get(lay, "int64"),
+        "data": "synthetic",
+        "config": {"workload": f"the exchange's device side of S as rank 0 of {G} GPUs: {n} "
+                               f"{w}-byte FK tuples over keys 1..{total}, exact range partition "
+                               f"into 2^{pbits} partitions as {lay} ({eb} B a row) + table kernels",
+                   "tuples_per_gpu": n, "parallelism": f"one GPU, rank 0 of a simulated x{G}"},
+        "roofline": roof,
+        "cpu_baseline": None,
+        "result_ok": True,
+        "detail": {
+            "note": "one GPU: no row crosses xGMI, value 0; this line times the device work a "
+                    f"rank does for the exchange at {G} GPUs (HBM roofline of its partition)",
+            "kernels_ms_per_step": {k: round(v[0], 4) for k, v in brk.items()},
+            "exchange_layout": lay, "partition_bits": pbits, "owned_partitions_rank0": hi - lo,
+            "xgmi_bytes_leaving_rank_per_step": int(leave),
+            "xgmi_ms_at_link_peak": round(leave / (xgmi_peak * 1e9) * 1e3, 3),
+            "xgmi_peak_GBps": xgmi_peak,
+        },
+    }
+    print(json.dumps(out), file=json_out, flush=True)
 
 
 def partition_check(R, out, hist, off, bits, shift, w):
