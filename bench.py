@@ -1043,7 +1043,7 @@ def run_exchange_device_side(a, json_out, lib, n, w):
     roof = None
     if sc_n:
         ach = alg_sc / (sc_ms / sc_n / 1e3) / 1e9
-        roof = {"bound": "hbm", "kernel": "k_scatter (exact range partition)",
+        roof = {"bound": "hbm", "kernel": "k_scatter", "pass": "the exact range partition",
                 "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                 "alg_bytes_per_launch": alg_sc, "avg_launch_ms": round(sc_ms / sc_n, 4)}
