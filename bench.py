@@ -1032,7 +1032,7 @@ def run_exchange_device_side(a, json_out, lib, n, w):
     elapsed, kern, brk = timed_loop(a, lib, None, step)
     xb = dj.last_rows["S"][0]
     eb = row_bytes(xb)
-    lay = dj.last_layout
+    lay = res["x"][-1]  # the layout the attempt ended in
     # rows rank 0 keeps: the partitions it owns among G ranks
     F, U = 1 << pbits, used_parts(1, total, pbits)
     lo, hi = owned(F, G, 0, U)
