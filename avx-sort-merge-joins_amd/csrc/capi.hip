@@ -2170,6 +2170,41 @@ int smj_dev_partition_range_sampled(smj_workspace* wsp, const tuple_t* in, uint6
     return 1;
 }
 
+int smj_dev_partition_range_shards(smj_workspace* wsp, const tuple_t* in, uint64_t n,
+                                   void* out, uint32_t nbits, int64_t key_min, int64_t key_max,
+                                   int packed, int64_t* seg_start_out, int64_t* seg_cnt_out,
+                                   unsigned int* flags, smj_stream_t stream) {
+    Workspace* ws = (Workspace*)wsp;
+    hipStream_t st = (hipStream_t)stream;
+    if (nbits > 10 || n >= (1ull << 32)) return 0;  // the scatter's LDS carries
+    RangePlan h = make_plan(key_min, key_max, nbits, 0, 0, 0);
+#ifdef KEY_8B
+    if (packed && !LayPacked::usable(h)) return 0;
+#else
+    if (packed) return 0;
+#endif
+    const uint32_t nbins = 1u << nbits;
+    RangePlan* plan = (RangePlan*)ws->scratch("xp_plan", sizeof(RangePlan));
+    hipLaunchKernelGGL(k_setplan, dim3(1), dim3(1), 0, st, plan, h);
+    // exact (partition, shard) counts instead of a sample
+    unsigned int* counts =
+        (unsigned int*)ws->scratch("xp_shard_counts", (size_t)nbins * kShards * 4);
+    SMJ_CHECK(hipMemsetAsync(counts, 0, (size_t)nbins * kShards * 4, st));
+    SMJ_CHECK(hipMemsetAsync(flags, 0, 8, st));
+    uint64_t* starts = (uint64_t*)ws->scratch("xp_starts", (size_t)nbins * 8);
+    int64_t* hist = (int64_t*)ws->scratch("xp_hist", (size_t)nbins * 8);
+    const Tup* rels[1] = {(const Tup*)in};
+    const uint64_t ns[1] = {n};
+    void* outs[1] = {out};
+    uint64_t* st_[1] = {starts};
+    int64_t* h_[1] = {hist};
+    uint64_t* ss[1] = {(uint64_t*)seg_start_out};
+    int64_t* sc[1] = {seg_cnt_out};
+    sampled_partition(ws, 1, rels, ns, outs, plan, nbits, counts, st_, h_, ss, sc, flags, st,
+                      &h, packed != 0, packed ? flags + 1 : nullptr, 0, false, true);
+    return 1;
+}
+
 int smj_dev_partition_range_planes(smj_workspace* wsp, const tuple_t* in, uint64_t n,
                                    void* out, uint64_t stride, uint32_t nbits,
                                    int64_t key_min, int64_t key_max, int64_t* seg_start_out,

@@ -118,6 +118,11 @@ struct DevOps {
         return smj_dev_partition_range_sampled(w(), (const tuple_t*)in, n, out, nbits, kmin,
                                                kmax, packed, ss, sc, flags, st[0]);
     }
+    int part_shards(const void* in, uint64_t n, void* out, uint32_t nbits, int64_t kmin,
+                    int64_t kmax, int packed, int64_t* ss, int64_t* sc, uint32_t* flags) {
+        return smj_dev_partition_range_shards(w(), (const tuple_t*)in, n, out, nbits, kmin, kmax,
+                                              packed, ss, sc, flags, st[0]);
+    }
     void part_exact(const void* in, uint64_t n, void* out, uint32_t nbits, int64_t kmin,
                     int64_t kmax, int64_t* hist) {
         smj_dev_partition_range(w(), (const tuple_t*)in, n, (tuple_t*)out, nbits, kmin, kmax,

@@ -50,6 +50,8 @@
 //   uint32_t shards(); uint64_t sampled_capacity(uint64_t n, uint32_t nbits);
 //   int  part_planes(in, n, out, stride, nbits, kmin, kmax, ss, sc, flags);
 //   int  part_sampled(in, n, out, nbits, kmin, kmax, packed, ss, sc, flags);
+//   int  part_shards(in, n, out, nbits, kmin, kmax, packed, ss, sc, flags);
+//                                               exact shard regions, no slack
 //   void part_exact(in, n, out, nbits, kmin, kmax, hist);
 //   int  part_exact_packed(in, n, out, nbits, kmin, kmax, hist, bad);
 //   void hist_tables(hist, F, K, ss, sc);       exact partition -> shard-0 tables
@@ -494,6 +496,12 @@ struct Rank {
             done = ops->part_sampled(in[r], nn, xb, pbits, lr.base, kmax, lay == kWords ? 1 : 0,
                                      a.ss, a.sc, a.flags) != 0;
             if (!done) a.cap = nn;  // the exact form below
+        }
+        if (!done) {
+            // exact: the sampled scatter with exactly sized regions (one count
+            // pass, no slack to travel); else histogram + scatter
+            done = ops->part_shards(in[r], nn, xb, pbits, lr.base, kmax, lay == kWords ? 1 : 0,
+                                    a.ss, a.sc, a.flags) != 0;
         }
         if (!done) {
             ops->fill_u32(a.flags, 0, 2, kMain);

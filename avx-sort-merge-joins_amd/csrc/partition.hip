@@ -1291,6 +1291,74 @@ k_regions_done(RegionRel R, uint32_t nbins, unsigned int* __restrict__ flag) {
     }
 }
 
+// Exact shard regions (round 6): the exchange's range partition across ranks
+// takes the sampled scatter (k_scatter_res) with its regions sized from an
+// exact count of every (partition, shard) instead of a sample, laid out back
+// to back with no slack.  A shard is the scatter workgroup's blockIdx %
+// kShards, so the count follows the scatter's chunking (scatter_chunk).  The
+// partitions come out contiguous and exactly sized, as from the exact
+// partition (histogram + unstable scatter, plan_partition_packed), and no
+// region slack travels with the rows.
+template <int THREADS, int ITEMS, class Digit>
+__global__ void __launch_bounds__(THREADS)
+k_shard_hist(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, uint32_t split,
+             Digit dig_arg, uint32_t nbins, unsigned int* __restrict__ counts) {
+    const auto dig = dig_arg.load();
+    extern __shared__ unsigned int lh[];
+    for (uint32_t d = threadIdx.x; d < nbins; d += THREADS) lh[d] = 0;
+    __syncthreads();
+    // scatter chunk c is counted by `split` workgroups
+    const uint32_t c = blockIdx.x / split, s = blockIdx.x % split;
+    const uint64_t sub = (chunk + split - 1) / split;
+    const uint64_t beg = (uint64_t)c * chunk + (uint64_t)s * sub;
+    const uint64_t end = min(min(beg + sub, (uint64_t)(c + 1) * chunk), n);
+    constexpr int TILE = THREADS * ITEMS;
+    for (uint64_t base = beg; base < end; base += TILE) {
+        Tup v[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const uint64_t i = base + (uint64_t)j * THREADS + threadIdx.x;
+            v[j] = ld_stream(in + (i < end ? i : end - 1));  // clamped: all in flight
+        }
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++)
+            if (base + (uint64_t)j * THREADS + threadIdx.x < end) atomicAdd(&lh[dig(v[j])], 1u);
+    }
+    __syncthreads();
+    const uint32_t q = c % kShards;
+    for (uint32_t d = threadIdx.x; d < nbins; d += THREADS)
+        if (lh[d]) atomicAdd(&counts[(size_t)d * kShards + q], lh[d]);
+}
+
+// the regions of k_shard_hist's counts (R.sample: nbins * kShards each),
+// partition-major, shard-minor, back to back (blockIdx.x = relation)
+__global__ void __launch_bounds__(1024)
+k_regions_exact(RegionRel R, uint32_t nbins) {
+    const int r = blockIdx.x;
+    const unsigned int* __restrict__ cnt = R.sample[r];
+    __shared__ uint32_t scr[1024 / 64 + 1];
+    const uint32_t per = (nbins + 1023) / 1024;
+    const uint32_t b = threadIdx.x * per;
+    uint32_t loc = 0;
+    for (uint32_t k = 0; k < per; k++)
+        if (b + k < nbins)
+            for (uint32_t q = 0; q < kShards; q++) loc += cnt[(size_t)(b + k) * kShards + q];
+    uint32_t tot;
+    uint64_t e = block_exclusive_scan(loc, scr, &tot);
+    for (uint32_t k = 0; k < per; k++) {
+        const uint32_t d = b + k;
+        if (d >= nbins) break;
+        R.base[r][d] = e;
+        for (uint32_t q = 0; q < kShards; q++) {
+            const size_t i = (size_t)d * kShards + q;
+            R.seg_start[r][i] = e;
+            R.cursor[r][i] = e;
+            e += cnt[i];
+            R.cap_end[r][i] = e;
+        }
+    }
+}
+
 // lanes of the scatter write whole 64-byte segments: the complete segments
 // of a tile are numbered, segown[s] = the partition of segment s
 // (SB: bytes an element takes in the output's first plane: the segment is
@@ -1931,6 +1999,32 @@ uint64_t sampled_capacity(uint64_t n, uint32_t dbits) {
            ((uint64_t)1 << dbits) * kShards * (kRegionSlack + ALIGN);
 }
 
+// the sampled scatter's chunk of one workgroup (n > 0) and its workgroups
+static uint64_t scatter_chunk(uint64_t n, uint64_t tile, uint32_t* nwg_out) {
+    const uint64_t ntiles = (n + tile - 1) / tile;
+    const uint32_t maxwg = 256 * SMJ_SC_WG_PER_CU;
+    uint32_t nwg = (uint32_t)(ntiles < maxwg ? ntiles : maxwg);
+    const uint64_t tiles_per_wg = (ntiles + nwg - 1) / nwg;
+    *nwg_out = (uint32_t)((ntiles + tiles_per_wg - 1) / tiles_per_wg);
+    return tiles_per_wg * tile;
+}
+
+// items per thread of the sampled scatter for Pack at nbins partitions: the
+// widest tile whose LDS fits (0: none)
+template <class Pack>
+static int sampled_items(uint32_t nbins) {
+    constexpr int THREADS = SMJ_SC_THREADS;
+    constexpr int BIG = sizeof(Tup) == 16
+        ? (sizeof(typename Pack::OutT) <= 8 ? SMJ_SC_ITEMS16P : SMJ_SC_ITEMS16)
+        : SMJ_SC_ITEMS8;
+    constexpr int SMALL = sizeof(Tup) == 16 ? 4 : 8;
+    typedef typename Pack::OutT O;
+    if (ScatterGeom<THREADS, BIG, O, Pack::kStoreBytes>::lds_bytes(nbins) <= 160 * 1024) return BIG;
+    if (ScatterGeom<THREADS, SMALL, O, Pack::kStoreBytes>::lds_bytes(nbins) <= 160 * 1024)
+        return SMALL;
+    return 0;
+}
+
 template <int ITEMS, class Pack>
 static bool sampled_scatter_t(Workspace* ws, const Tup* in, uint64_t n, void* out,
                               uint64_t ostride, const PlanDigit1& dig, uint32_t nbins,
@@ -1941,12 +2035,8 @@ static bool sampled_scatter_t(Workspace* ws, const Tup* in, uint64_t n, void* ou
     const size_t lds = ScatterGeom<THREADS, ITEMS, typename Pack::OutT,
                                    Pack::kStoreBytes>::lds_bytes(nbins);
     if (lds > 160 * 1024) return false;
-    uint64_t ntiles = (n + TILE - 1) / TILE;
-    const uint32_t maxwg = 256 * SMJ_SC_WG_PER_CU;
-    uint32_t nwg = (uint32_t)(ntiles < maxwg ? ntiles : maxwg);
-    const uint64_t tiles_per_wg = (ntiles + nwg - 1) / nwg;
-    const uint64_t chunk = tiles_per_wg * TILE;
-    nwg = (uint32_t)((ntiles + tiles_per_wg - 1) / tiles_per_wg);
+    uint32_t nwg = 0;
+    const uint64_t chunk = scatter_chunk(n, TILE, &nwg);
     constexpr bool VEC_OK = sizeof(Tup) == 8 && ITEMS % 2 == 0;
     set_lds_attr((const void*)k_scatter_res<THREADS, ITEMS, PlanDigit1, Pack, false>, 160 * 1024);
     if constexpr (VEC_OK)
@@ -1985,11 +2075,13 @@ static void sampled_scatter(Workspace* ws, const Tup* in, uint64_t n, void* out,
         ? (sizeof(typename Pack::OutT) <= 8 ? SMJ_SC_ITEMS16P : SMJ_SC_ITEMS16)
         : SMJ_SC_ITEMS8;
     constexpr int SMALL = sizeof(Tup) == 16 ? 4 : 8;
-    if (sampled_scatter_t<BIG>(ws, in, n, out, ostride, dig, nbins, cursor, cap_end, pk,
-                               bad_flag, st))
+    // the choice sampled_items makes (k_shard_hist counts with its chunking)
+    const int items = sampled_items<Pack>(nbins);
+    if (items == BIG && sampled_scatter_t<BIG>(ws, in, n, out, ostride, dig, nbins, cursor,
+                                               cap_end, pk, bad_flag, st))
         return;
-    if (sampled_scatter_t<SMALL>(ws, in, n, out, ostride, dig, nbins, cursor, cap_end, pk,
-                                 bad_flag, st))
+    if (items == SMALL && sampled_scatter_t<SMALL>(ws, in, n, out, ostride, dig, nbins,
+                                                   cursor, cap_end, pk, bad_flag, st))
         return;
     fprintf(stderr, "[ERROR] smj: sampled scatter LDS exceeds 160 KiB (%u partitions)\n", nbins);
     abort();
@@ -2001,9 +2093,13 @@ void sampled_partition(Workspace* ws, int nrel, const Tup* const* in, const uint
                        int64_t* const* hist_out, uint64_t* const* seg_start,
                        int64_t* const* seg_cnt, unsigned int* flag_dev, hipStream_t st,
                        const RangePlan* host_plan, bool packed, unsigned int* bad,
-                       uint64_t p48_stride, bool p32) {
+                       uint64_t p48_stride, bool p32, bool exact) {
     PlanDigit1 dig{plan_dev};
     const uint32_t nbins = 1u << dbits;
+    if (exact && (p48_stride || p32)) {
+        fprintf(stderr, "[ERROR] smj: exact shard regions take tuples or 64-bit words\n");
+        abort();
+    }
 #ifndef KEY_8B
     // 8-byte tuples: no 64-bit packed words, but 48- and 32-bit ones
     packed = p48_stride != 0 || p32;
@@ -2030,7 +2126,7 @@ void sampled_partition(Workspace* ws, int nrel, const Tup* const* in, const uint
         const int rr = r < nrel ? r : 0;
         S.in[r] = in[rr];
         S.n[r] = n[rr];
-        S.hist[r] = sample + (size_t)rr * nbins;
+        S.hist[r] = sample + (size_t)rr * nbins * (exact ? kShards : 1);
         R.sample[r] = S.hist[r];
         R.base[r] = starts_dev[rr];
         R.seg_start[r] = seg_start[rr];
@@ -2045,7 +2141,34 @@ void sampled_partition(Workspace* ws, int nrel, const Tup* const* in, const uint
             R.cap_end[r] = R.cap_end[0];
         }
     }
-    {
+    if (exact) {
+        // exact (partition, shard) counts with the scatter's chunking, then
+        // regions back to back (`sample` holds nbins * kShards per relation)
+        TraceScope ts(ws, "k_hist", st);
+        for (int r = 0; r < nrel; r++) {
+            if (!n[r]) continue;
+            int items = 0;
+#ifdef KEY_8B
+            if (packed)
+                items = sampled_items<LayPacked::Pack>(nbins);
+            else
+#endif
+                items = sampled_items<PackRange>(nbins);
+            if (!items) {
+                fprintf(stderr, "[ERROR] smj: sampled scatter LDS exceeds 160 KiB (%u "
+                        "partitions)\n", nbins);
+                abort();
+            }
+            uint32_t nwg = 0;
+            const uint64_t chunk = scatter_chunk(n[r], (uint64_t)SMJ_SC_THREADS * items, &nwg);
+            constexpr int HI = sizeof(Tup) == 16 ? 8 : 16;
+            const uint32_t split = 4;  // workgroups counting one scatter chunk
+            hipLaunchKernelGGL((k_shard_hist<1024, HI, PlanDigit1>), dim3(nwg * split),
+                               dim3(1024), nbins * sizeof(unsigned int), st, in[r], n[r], chunk,
+                               split, dig, nbins, S.hist[r]);
+        }
+        hipLaunchKernelGGL(k_regions_exact, dim3(nrel), dim3(1024), 0, st, R, nbins);
+    } else {
         TraceScope ts(ws, "k_sample", st);
         const uint64_t npts = (nmax + 4 * kSampleStride - 1) / (4 * kSampleStride);
         uint32_t g = (uint32_t)((npts + 255) / 256);

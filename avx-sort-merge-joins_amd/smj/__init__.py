@@ -69,6 +69,7 @@ DEVICE_SYMBOLS = [
     "smj_mgpu_comm_init", "smj_mgpu_rank_join", "smj_mgpu_comm_destroy", "smj_mgpu_rank_sorted",
     "smj_mgpu_comm_workspace", "smj_workspace_last_layout", "smj_mgpu_join_slices",
     "smj_mgpu_last_stats", "smj_mgpu_last_sorted", "smj_mgpu_group_workspace",
+    "smj_dev_partition_range_shards",
 ]
 
 
@@ -267,6 +268,8 @@ class Library:
                                                      _P, _P]),
             "smj_dev_partition_range_sampled": (C.c_int, [_P, _P, _U64, _P, _U32, _I64, _I64,
                                                           C.c_int, _P, _P, _P, _P]),
+            "smj_dev_partition_range_shards": (C.c_int, [_P, _P, _U64, _P, _U32, _I64, _I64,
+                                                         C.c_int, _P, _P, _P, _P]),
             "smj_dev_partition_range_planes": (C.c_int, [_P, _P, _U64, _P, _U64, _U32, _I64,
                                                          _I64, _P, _P, _P, _P]),
             "smj_dev_join_segmented_planes": (None, [_P, _P, _U64, _U64, _P, _P, _P, _U64,
@@ -796,6 +799,16 @@ class Library:
         tensors of 2^nbits * shards, flags int32[2]; False when the form does
         not apply (nothing launched)."""
         return bool(self.lib.smj_dev_partition_range_sampled(
+            self.ws, inp.data_ptr(), inp.shape[0], out.data_ptr(), nbits, key_min, key_max,
+            1 if packed else 0, seg_start.data_ptr(), seg_cnt.data_ptr(), flags.data_ptr(),
+            self.stream_ptr()))
+
+    def dev_partition_range_shards(self, inp, out, nbits, key_min, key_max, packed,
+                                   seg_start, seg_cnt, flags):
+        """smj_dev_partition_range_shards: the sampled partition's tables with
+        exactly sized regions back to back (`out` holds n elements); False when
+        the form does not apply (nothing launched)."""
+        return bool(self.lib.smj_dev_partition_range_shards(
             self.ws, inp.data_ptr(), inp.shape[0], out.data_ptr(), nbits, key_min, key_max,
             1 if packed else 0, seg_start.data_ptr(), seg_cnt.data_ptr(), flags.data_ptr(),
             self.stream_ptr()))

@@ -342,6 +342,11 @@ class DeviceOps:
         return self.lib.dev_partition_range_sampled(inp, out, nbits, key_min, key_max, packed,
                                                     seg_start, seg_cnt, flags)
 
+    def partition_range_shards(self, inp, out, nbits, key_min, key_max, packed, seg_start,
+                               seg_cnt, flags):
+        return self.lib.dev_partition_range_shards(inp, out, nbits, key_min, key_max, packed,
+                                                   seg_start, seg_cnt, flags)
+
     def partition_range_planes(self, inp, out, nbits, key_min, key_max, seg_start, seg_cnt,
                                flags):
         return self.lib.dev_partition_range_planes(inp, out.buf, out.stride, nbits, key_min,
@@ -530,6 +535,23 @@ class DistributedJoin:
             return None
         return ss.view(F, K), sc.view(F, K), flags
 
+    def _shards(self, rel, part, packed, key):
+        """The exact partition across ranks (round 6): the sampled scatter
+        with exactly sized regions back to back (smj_dev_partition_range_shards:
+        one count pass, no slack to travel), tables in the sampled shape.
+        None when the ops have no such form or it does not apply."""
+        if not hasattr(self.ops, "partition_range_shards"):
+            return None
+        dev = rel.device
+        F, K = self.fanout, self.shards
+        ss = self._small("ss" + key, (F * K,), dev=dev)
+        sc = self._small("sc" + key, (F * K,), dev=dev)
+        flags = self._small("fl" + key, (2,), torch.int32, dev)
+        if not self.ops.partition_range_shards(rel, part, self.pbits, self.key_min,
+                                               self.key_max, packed, ss, sc, flags):
+            return None
+        return ss.view(F, K), sc.view(F, K), flags
+
     def _planes(self, rel, xb, key):
         """Sampled range partition of `rel` into the planes `xb` (48-bit
         words); where the form does not apply on this rank, empty tables
@@ -574,7 +596,9 @@ class DistributedJoin:
             res = self._sampled(rel, part, packed, key) if sampled else None
             if res is None:  # exact partition (the receivers read either form)
                 cap = n if sampled else cap
-                res = self._partition(rel, part[:n], packed)
+                res = self._shards(rel, part[:n], packed, key)
+                if res is None:
+                    res = self._partition(rel, part[:n], packed)
                 if res is None:
                     return None
         start, cnt, fl = res

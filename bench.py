@@ -133,6 +133,10 @@ def parse():
                         "of a world of this many GPUs would run it (its slice of the weak-scaled "
                         "relation, the exact range partition into that world's partitions and "
                         "layout, the table kernels; nothing crosses xGMI on one GPU)")
+    p.add_argument("--exchange-form", default="exact", choices=("exact", "sampled"),
+                   help="--op exchange on one GPU: the range partition form timed (exact: what "
+                        "ranks use across GPUs; sampled: the one-rank form, whose region slack "
+                        "would travel with the rows)")
     p.add_argument("--fanout-bits", type=int, default=8,
                    help="level-1 partitions (2^bits) of the join; the library raises it "
                         "as the relation size needs")
@@ -1023,8 +1027,9 @@ def run_exchange_device_side(a, json_out, lib, n, w):
     lib.dev_gen_fk(S, 0, total, total, 54321)
     torch.cuda.synchronize()
     pbits = partition_bits(a.fanout_bits, G, True, n, (1, total))
-    dj = DistributedJoin(DeviceOps(lib, sampled=False), a.fanout_bits, 1, total, n_hint=n,
-                         pbits=pbits)
+    sampled = a.exchange_form == "sampled"
+    dj = DistributedJoin(DeviceOps(lib, sampled=sampled, planes=False), a.fanout_bits, 1,
+                         total, n_hint=n, pbits=pbits)
     res = {}
 
     def step():
@@ -1043,7 +1048,7 @@ def run_exchange_device_side(a, json_out, lib, n, w):
     roof = None
     if sc_n:
         ach = alg_sc / (sc_ms / sc_n / 1e3) / 1e9
-        roof = {"bound": "hbm", "kernel": "k_scatter", "pass": "the exact range partition",
+        roof = {"bound": "hbm", "kernel": "k_scatter", "pass": f"the {a.exchange_form} range partition",
                 "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                 "alg_bytes_per_launch": alg_sc, "avg_launch_ms": round(sc_ms / sc_n, 4)}
@@ -1056,7 +1061,7 @@ def run_exchange_device_side(a, json_out, lib, n, w):
         "vs_baseline": None, "dtype": {"words": "int64", "planes": "u48"}.get(lay, "int64"),
         "data": "synthetic",
         "config": {"workload": f"the exchange's device side of S as rank 0 of {G} GPUs: {n} "
-                               f"{w}-byte FK tuples over keys 1..{total}, exact range partition "
+                               f"{w}-byte FK tuples over keys 1..{total}, {a.exchange_form} range partition "
                                f"into 2^{pbits} partitions as {lay} ({eb} B a row) + table kernels",
                    "tuples_per_gpu": n, "parallelism": f"one GPU, rank 0 of a simulated x{G}"},
         "roofline": roof,

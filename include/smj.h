@@ -754,6 +754,19 @@ int smj_dev_partition_range_planes(smj_workspace * ws, const tuple_t * in, uint6
                                    int64_t key_min, int64_t key_max, int64_t * seg_start,
                                    int64_t * seg_cnt, unsigned int * flags,
                                    smj_stream_t stream);
+/* The same partition with exactly sized regions (round 6; the multi-GPU
+ * exchange's form across ranks): one read pass counts every (partition,
+ * shard), the regions are laid out back to back with no slack, so `out` needs
+ * n elements and the partitions come out contiguous -- partition p is its
+ * smj_sampled_shards() shard regions one after the other.  Tables and flags
+ * as smj_dev_partition_range_sampled (the overflow flag stays 0).  Returns 0
+ * when it does not apply (nbits > 10, n >= 2^32, packed words the plan does
+ * not allow). */
+int smj_dev_partition_range_shards(smj_workspace * ws, const tuple_t * in, uint64_t n,
+                                   void * out, uint32_t nbits, int64_t key_min,
+                                   int64_t key_max, int packed, int64_t * seg_start,
+                                   int64_t * seg_cnt, unsigned int * flags,
+                                   smj_stream_t stream);
 uint64_t smj_sampled_capacity(uint64_t n, uint32_t nbits);
 uint32_t smj_sampled_shards(void);
 

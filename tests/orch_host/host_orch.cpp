@@ -135,7 +135,7 @@ struct HostOps {
     // the sampled layout: partition p = K consecutive shard regions (shard =
     // position * K / n), each followed by slack; element i goes to pos[i]
     void place(const Tup* in, uint64_t n, uint32_t nbits, const Range& rg, int64_t* ss,
-               int64_t* sc, uint32_t* flags, std::vector<uint64_t>& pos) {
+               int64_t* sc, uint32_t* flags, std::vector<uint64_t>& pos, bool slack = true) {
         const uint64_t FK = ((uint64_t)1 << nbits) * K;
         std::vector<uint64_t> cnt(FK, 0), start(FK, 0), fill(FK, 0);
         std::vector<uint64_t> idx(n);
@@ -146,14 +146,40 @@ struct HostOps {
         uint64_t acc = 0;
         for (uint64_t j = 0; j < FK; j++) {
             start[j] = acc;
-            acc += cnt[j] + cnt[j] / 8 + j % 5;
+            acc += cnt[j] + (slack ? cnt[j] / 8 + j % 5 : 0);
             ss[j] = (int64_t)start[j];
             sc[j] = (int64_t)cnt[j];
         }
         pos.resize(n);
         for (uint64_t i = 0; i < n; i++) pos[i] = start[idx[i]] + fill[idx[i]]++;
-        flags[0] = overflow ? 1u : 0u;
+        flags[0] = overflow && slack ? 1u : 0u;
     }
+    // smj_dev_partition_range_shards: the sampled layout with exactly sized
+    // regions back to back (no slack, never an overflow); `out` holds n
+    int part_shards(const void* inv, uint64_t n, void* out, uint32_t nbits, int64_t kmin,
+                    int64_t kmax, int packed, int64_t* ss, int64_t* sc, uint32_t* flags) {
+        const Tup* in = (const Tup*)inv;
+        Range rg(kmin, kmax, nbits);
+        shards_calls++;
+        if (not_applicable || nbits > 10) return 0;
+        if (packed && (!can_pack() || rg.s1 < 1 || rg.s1 > 32)) return 0;
+        std::vector<uint64_t> pos;
+        place(in, n, nbits, rg, ss, sc, flags, pos, false);
+        flags[1] = 0;
+        for (uint64_t i = 0; i < n; i++) {
+            CHECK(pos[i] < n, "shards position %llu of %llu", (unsigned long long)pos[i],
+                  (unsigned long long)n);
+            if (packed) {
+                uint32_t bad = 0;
+                ((uint64_t*)out)[pos[i]] = word64(in[i], rg, &bad);
+                flags[1] |= bad ? 1u : 0u;
+            } else {
+                ((Tup*)out)[pos[i]] = in[i];
+            }
+        }
+        return 1;
+    }
+    int shards_calls = 0;
     int part_sampled(const void* inv, uint64_t n, void* out, uint32_t nbits, int64_t kmin,
                      int64_t kmax, int packed, int64_t* ss, int64_t* sc, uint32_t* flags) {
         const Tup* in = (const Tup*)inv;

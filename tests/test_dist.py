@@ -26,8 +26,10 @@ class HostOps:
     can_pack = True
     K = 3  # shards of the sampled layout (the device uses smj_sampled_shards())
 
-    def __init__(self, orc, sampled=True, overflow=False, not_applicable=False, planes=True):
+    def __init__(self, orc, sampled=True, overflow=False, not_applicable=False, planes=True,
+                 shards=True):
         self.orc = orc
+        self.shards_ok = shards  # the exact form by exact shard regions (else histogram)
         self.can_sample = sampled
         self.can_planes = planes and sampled
         self.overflow = overflow  # report a region overflow from the sampled form
@@ -67,7 +69,34 @@ class HostOps:
         out[pos] = vals[order]
         return True
 
-    def _place(self, inp, nbits, key_min, key_max, seg_start, seg_cnt, flags):
+    def partition_range_shards(self, inp, out, nbits, key_min, key_max, packed, seg_start,
+                               seg_cnt, flags):
+        """smj_dev_partition_range_shards: the sampled layout with exactly
+        sized regions back to back (no slack, no overflow); `out` holds n."""
+        from smj.dist import range_digit
+        F, n = 1 << nbits, inp.shape[0]
+        if not self.shards_ok or self.not_applicable:
+            return False
+        flags.zero_()
+        if packed:
+            words = torch.empty(n, dtype=torch.int64)
+            hist = torch.zeros(F, dtype=torch.int64)
+            bad = torch.zeros(1, dtype=torch.int32)
+            if not self.partition_range_packed(inp, words, nbits, key_min, key_max, hist, bad):
+                return False
+            flags[1] = int(bad[0])
+            d = range_digit(inp[:, 1], key_min, key_max, nbits)
+            vals = torch.empty_like(words)
+            vals[torch.argsort(d, stable=True)] = words
+        else:
+            vals = inp
+        pos, order = self._place(inp, nbits, key_min, key_max, seg_start, seg_cnt, flags,
+                                 slack=False)
+        assert out.shape[0] >= n and (n == 0 or int(pos.max()) < n)
+        out[pos] = vals[order]
+        return True
+
+    def _place(self, inp, nbits, key_min, key_max, seg_start, seg_cnt, flags, slack=True):
         """The sampled layout's element positions: partition p is K
         consecutive shard regions (shard = position / n * K), each followed by
         slack; returns (positions, input order) and fills the tables."""
@@ -77,7 +106,7 @@ class HostOps:
         q = torch.arange(n) * K // max(n, 1)
         idx = d * K + q
         cnt = torch.bincount(idx, minlength=F * K)
-        cap = cnt + cnt // 8 + torch.arange(F * K) % 5
+        cap = cnt + (cnt // 8 + torch.arange(F * K) % 5 if slack else 0)
         start = torch.cumsum(cap, 0) - cap
         order = torch.argsort(idx, stable=True)
         first = torch.cumsum(cnt, 0) - cnt
@@ -85,7 +114,7 @@ class HostOps:
         pos = start[si] + torch.arange(n) - first[si]
         seg_start.copy_(start)
         seg_cnt.copy_(cnt)
-        if self.overflow:
+        if self.overflow and slack:
             flags[0] = 1
         return pos, order
 
@@ -245,7 +274,7 @@ class HostOps:
 
 
 def _worker(rank, world, port, n, q, s_payload="negative", mode="sampled", planes=True,
-            wide=False, chunk_mb=None, staged=True):
+            wide=False, chunk_mb=None, staged=True, shards=True):
     import sys
     for p in (ROOT, PKG):
         sys.path.insert(0, p)
@@ -282,7 +311,8 @@ def _worker(rank, world, port, n, q, s_payload="negative", mode="sampled", plane
         # others sampled: receivers read either form), "overflow" (rank 1's
         # sampled regions overflow: every rank repeats exactly)
         ops = HostOps(orc, sampled=mode != "exact", overflow=mode == "overflow" and rank == 1,
-                      not_applicable=mode == "mixed" and rank == 0, planes=planes)
+                      not_applicable=mode == "mixed" and rank == 0, planes=planes,
+                      shards=shards)
         if wide:  # 2^9 buckets per rank: planes take 2^9 partitions across ranks
             dj = DistributedJoin(ops, 9, 1, total, n_hint=n, staged=staged)
             assert dj.pbits == (9 if ops.can_planes else 9 + (world > 1))
@@ -424,7 +454,8 @@ def _free_port():
     (2, None, "rowid", "exact"), (3, None, "negative", "exact"),
     (3, None, "rowid", "mixed"), (2, None, "negative", "mixed"),
     (3, None, "rowid", "overflow"), (2, None, "rowid", "sampled-onecall"),
-    (3, None, "negative", "exact-onecall"),
+    (3, None, "negative", "exact-onecall"), (2, None, "rowid", "exact-hist"),
+    (3, None, "negative", "exact-hist"),
     (1, None, "wide48", "sampled"), (2, None, "wide48", "sampled"),
     (2, 0, "rowid", "sampled-noplanes"), (3, None, "rowid", "sampled-noplanes"),
     (1, None, "rowid", "sampled-noplanes"), (2, None, "rowid", "sampled-wide"),
@@ -440,6 +471,8 @@ def test_distributed_join_gloo(world, chunk_mb, s_payload, mode, oracles, monkey
     for both; "r_negative": R cannot be packed but S can (S goes again, as
     tuples); "wide48": S's payloads need 64-bit words (both go as words)."""
     staged = True
+    shards = not mode.endswith("-hist")  # the exact form by histogram + scatter
+    mode = mode.replace("-hist", "")
     if mode.endswith("-onecall"):  # the local join in one call (no staging)
         staged = False
         mode = mode[:-len("-onecall")]
@@ -451,7 +484,7 @@ def test_distributed_join_gloo(world, chunk_mb, s_payload, mode, oracles, monkey
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, 5000, q, s_payload, mode,
-                                               planes, wide, chunk_mb, staged))
+                                               planes, wide, chunk_mb, staged, shards))
              for r in range(world)]
     for p in procs:
         p.start()

@@ -668,6 +668,71 @@ def test_partition_range_sampled_small_bits(libs, oracles, width, nbits, n, pack
     assert np.array_equal(np.sort(np.concatenate(keys)), np.arange(1, n + 1))
 
 
+@pytest.mark.parametrize("nbits", [0, 3, 8, 10])
+@pytest.mark.parametrize("n", [1, 4097, 1 << 20, 3_000_017])
+@pytest.mark.parametrize("packed", [False, True])
+def test_partition_range_shards(libs, oracles, width, nbits, n, packed):
+    """smj_dev_partition_range_shards (the exchange's exact form across ranks,
+    round 6): regions exactly sized and back to back, covering [0, n) with no
+    gap, partition-major; every element in its partition's key range; the
+    partitions together are exactly the input (16-byte tuples: the (key,
+    payload) multiset; packed words: per partition the same sorted words as
+    smj_dev_partition_range_packed writes)."""
+    import torch
+    orc, lib = oracles[width], libs[width]
+    if packed and width != 16:
+        pytest.skip("packed words are the 16-byte layout")
+    orc.seed(7 + n + nbits)
+    t = orc.create_relation_fk(n, 5 * n)
+    t["payload"] = np.arange(n)
+    d_in = lib.to_device(t)
+    F, K = 1 << nbits, lib.sampled_shards()
+    canary = 4096
+    if packed:
+        buf = torch.full((n + canary,), -7, dtype=torch.int64, device="cuda")
+    else:
+        buf = lib.empty(n + canary)
+        buf.fill_(-7)
+    ss = torch.empty(F * K, dtype=torch.int64, device="cuda")
+    sc = torch.empty(F * K, dtype=torch.int64, device="cuda")
+    fl = torch.ones(2, dtype=torch.int32, device="cuda")
+    kmax = 5 * n
+    if not lib.dev_partition_range_shards(d_in, buf, nbits, 1, kmax, packed, ss, sc, fl):
+        assert packed and int(kmax - 1).bit_length() - nbits < 1
+        return
+    torch.cuda.synchronize()
+    assert fl.tolist() == [0, 0]
+    assert bool((buf[n:] == -7).all())  # nothing past n
+    ssh, sch = ss.cpu().numpy(), sc.cpu().numpy()
+    assert int(sch.sum()) == n
+    # back to back: region i starts where region i - 1 ends
+    assert ssh[0] == 0 and np.array_equal(ssh[1:], (ssh + sch)[:-1])
+    s1 = max(int(kmax - 1).bit_length() - nbits, 0)
+    if packed:
+        words = torch.empty(n, dtype=torch.int64, device="cuda")
+        hist = torch.zeros(F, dtype=torch.int64, device="cuda")
+        bad = torch.zeros(1, dtype=torch.int32, device="cuda")
+        assert lib.dev_partition_range_packed(d_in, words, nbits, 1, kmax, hist, bad)
+        torch.cuda.synchronize()
+        hs = hist.cpu().numpy()
+        got, want = buf[:n].cpu().numpy(), words.cpu().numpy()
+        pc = sch.reshape(F, K).sum(1)
+        assert np.array_equal(pc, hs)
+        o = 0
+        for p in range(F):
+            assert np.array_equal(np.sort(got[o:o + hs[p]]), np.sort(want[o:o + hs[p]])), p
+            o += hs[p]
+        return
+    h = lib.to_host(buf[:n])
+    for i in range(F * K):
+        seg = h[ssh[i]:ssh[i] + sch[i]]
+        rel = seg["key"].astype(np.int64) - 1
+        assert np.all(np.minimum(rel >> s1, F - 1) == i // K)
+    o = np.argsort(h["payload"], kind="stable")
+    assert np.array_equal(h["payload"][o], np.arange(n))
+    assert np.array_equal(h["key"][o], t["key"])
+
+
 @pytest.mark.parametrize("kind,n,maxid,skip,first", [
     ("nonunique", 1 << 20, 1 << 20, 0, 0), ("nonunique", 1 << 20, 1000, 17, 0),
     ("nonunique", 300001, 1 << 20, 0, 700000), ("zipf", 1 << 20, 1 << 20, 0, 0),
