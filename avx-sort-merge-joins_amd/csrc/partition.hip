@@ -507,12 +507,6 @@ constexpr int vmcnt_imm(int n) { return (n & 15) | ((n >> 4) << 14) | 0x0f70; }
 // tile's stores.  The loads thus fly under a whole tile of LDS work instead of
 // the stage phase alone.  Loads are non-temporal (NT; the input is read
 // once), 8-byte tuples leave in 16-byte pair stores.
-// tiles per block of the stable scatter's block-interleaved order (0: one
-// contiguous chunk per workgroup; k_scatter_swp)
-#ifndef SMJ_SWP_BLOCK_TILES
-#define SMJ_SWP_BLOCK_TILES 0
-#endif
-
 template <int THREADS, int ITEMS, class DigitL, bool NT>
 struct SwpTile {
     // info[d][3] = segment start (12 bits) | carry size (3) | emission + carry (17)
@@ -538,8 +532,7 @@ struct SwpTile {
     int lane, wid;
     bool owner;
     bool pairs;  // 8-byte tuples, 16-byte aligned output: pair stores
-    uint64_t end;    // end of the current block (tile counts)
-    uint64_t n_all;  // end of the input (load clamp)
+    uint64_t end;
     uint32_t pos[2], kc[2];
 
     // exclusive scan over the workgroup (v < 2^32 in total): wave scan by
@@ -569,14 +562,14 @@ struct SwpTile {
 #pragma unroll
         for (int j = 0; j < ITEMS; j++) {
             const uint64_t i = base + wbase + j * 64 + lane;
-            const uint64_t c = i < n_all ? i : n_all - 1;  // unconditional: a fixed count in flight
+            const uint64_t c = i < end ? i : end - 1;  // unconditional: a fixed count in flight
             v[j] = NT ? ld_nt(in + c) : in[c];
         }
     }
 
     __device__ __forceinline__ void tile(const Tup (&v)[ITEMS], Tup (&pre)[ITEMS],
-                                         uint64_t base, uint64_t pre_base) {
-        const uint32_t tcount = end > base ? (uint32_t)min((uint64_t)TILE, end - base) : 0u;
+                                         uint64_t base) {
+        const uint32_t tcount = (uint32_t)min((uint64_t)TILE, end - base);
         uint32_t dg[ITEMS], rk[ITEMS];
 #pragma unroll
         for (int j = 0; j < ITEMS; j++) {
@@ -635,7 +628,7 @@ struct SwpTile {
             }
         }
         // the next-but-one tile (its registers held the previous tile)
-        load(pre, pre_base);
+        load(pre, base + 2 * (uint64_t)TILE);
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < ITEMS; j++)
@@ -732,9 +725,8 @@ struct SwpTile {
 template <int THREADS, int ITEMS, class Digit, bool NT>
 __global__ void __launch_bounds__(THREADS)
 k_scatter_swp(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_arg,
-              uint32_t nbins, const uint32_t* __restrict__ counts, uint32_t nblk,
-              const uint64_t* __restrict__ starts, Tup* __restrict__ out, int pairs_ok,
-              int xcd_order) {
+              uint32_t nbins, const uint32_t* __restrict__ counts, uint32_t nwg,
+              const uint64_t* __restrict__ starts, Tup* __restrict__ out, int pairs_ok) {
     typedef SwpTile<THREADS, ITEMS, decltype(dig_arg.load()), NT> P;
     constexpr int W = P::W;
     constexpr int TILE = P::TILE;
@@ -758,69 +750,28 @@ k_scatter_swp(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
     s.owner = s.t2 < s.hb;
     s.pairs = sizeof(Tup) == 8 && pairs_ok && ((uintptr_t)out & 15) == 0;
     s.pos[0] = s.pos[1] = s.kc[0] = s.kc[1] = 0;
-    s.n_all = n;
-    // The input is cut into nblk blocks of `chunk` elements (whole tiles),
-    // and counts[d][blk] is block blk's start inside digit d.  Workgroup w
-    // takes blocks j * nwg + slot(w), j = 0, 1, ...: with one block per
-    // workgroup this is the chunked form (a contiguous chunk each); with
-    // several, the nwg workgroups work on nwg consecutive blocks at a time,
-    // those of one XCD (blockIdx % 8) on consecutive ones (xcd_order), so a
-    // digit's writes at any moment fall in one window of the output.  The
-    // carry holds within a block; its partial segments close at the block's end.
-    const uint32_t nwg = gridDim.x;
-    const uint32_t slot = xcd_order && nwg % 8 == 0 ? (blockIdx.x % 8) * (nwg / 8) + blockIdx.x / 8
-                                                    : blockIdx.x;
-    const uint32_t tpb = (uint32_t)(chunk / TILE);  // tiles per block
-    const uint32_t nbm = slot < nblk ? (nblk - slot + nwg - 1) / nwg : 0;  // blocks of mine
-    auto tile_base = [&](uint64_t t) -> uint64_t {
-        return ((t / tpb) * nwg + slot) * chunk + (t % tpb) * (uint64_t)TILE;
-    };
-    auto start_block = [&](uint32_t j) {
-        const uint64_t blk = (uint64_t)j * nwg + slot;
-        if (s.owner) {
+    if (s.owner) {
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
-                s.pos[h] = (uint32_t)(starts[2 * s.t2 + h] +
-                                      counts[(uint64_t)(2 * s.t2 + h) * nblk + blk]);
-                s.kc[h] = 0;
-            }
-        }
-        s.end = min(blk * chunk + chunk, n);
-    };
-    auto flush = [&]() {  // the partial last segment of every region of the block
-        if (s.owner) {
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const uint32_t d = 2 * s.t2 + h;
-                for (uint32_t e = 0; e < s.kc[h]; e++) out[s.pos[h] + e] = s.carry[d * CW + e];
-            }
-        }
-    };
+        for (int h = 0; h < 2; h++)
+            s.pos[h] = (uint32_t)(starts[2 * s.t2 + h] +
+                                  counts[(uint64_t)(2 * s.t2 + h) * nwg + blockIdx.x]);
+    }
     for (uint32_t q = threadIdx.x; q < W * s.hb; q += THREADS) s.w32[q] = 0;
+    const uint64_t beg = (uint64_t)blockIdx.x * chunk;
+    s.end = min(beg + chunk, n);
     s.wbase = s.wid * 64 * ITEMS;
-    const uint64_t nt = (uint64_t)nbm * tpb;  // tiles of mine (the last block's may be empty)
-    if (nt == 0) return;
-    start_block(0);
     Tup a[ITEMS], b[ITEMS], c[ITEMS];
-    s.load(a, tile_base(0));
-    s.load(b, tile_base(1));
+    s.load(a, beg);
+    s.load(b, beg + TILE);
     __builtin_amdgcn_s_waitcnt(vmcnt_imm(ITEMS));  // the first tile
     __syncthreads();
-    auto step = [&](const Tup (&v)[ITEMS], Tup (&pre)[ITEMS], uint64_t t) {
-        if (t && t % tpb == 0) {  // a new block (uniform): close the last one
-            __syncthreads();
-            flush();
-            start_block((uint32_t)(t / tpb));
-        }
-        s.tile(v, pre, tile_base(t), tile_base(t + 2));
-    };
-    for (uint64_t t = 0;;) {
-        step(a, c, t);
-        if (++t >= nt) break;
-        step(b, a, t);
-        if (++t >= nt) break;
-        step(c, b, t);
-        if (++t >= nt) break;
+    for (uint64_t base = beg;;) {
+        s.tile(a, c, base);
+        if ((base += TILE) >= s.end) break;
+        s.tile(b, a, base);
+        if ((base += TILE) >= s.end) break;
+        s.tile(c, b, base);
+        if ((base += TILE) >= s.end) break;
     }
     // the partial last segment of every region (carry slots are written by
     // every thread of the last tile's carry phase)
@@ -1819,42 +1770,30 @@ static void stable_partition_swp(Workspace* ws, const Tup* in, uint64_t n, Tup* 
     const uint32_t nbins = 1u << dbits;
     uint64_t ntiles = (n + G::TILE - 1) / G::TILE;
     if (ntiles == 0) ntiles = 1;
-    // blocks of SMJ_SWP_BLOCK_TILES tiles in XCD order over 256 workgroups,
-    // or (0) one contiguous chunk per workgroup
     uint32_t nwg = (uint32_t)(ntiles < 256 ? ntiles : 256);
-    uint64_t chunk;
-    uint32_t nblk;
-    const int xcd_order = SMJ_SWP_BLOCK_TILES > 0 && ntiles > 256 * (uint64_t)SMJ_SWP_BLOCK_TILES;
-    if (xcd_order) {
-        chunk = (uint64_t)SMJ_SWP_BLOCK_TILES * G::TILE;
-        nblk = (uint32_t)((ntiles + SMJ_SWP_BLOCK_TILES - 1) / SMJ_SWP_BLOCK_TILES);
-    } else {
-        const uint64_t tiles_per_wg = (ntiles + nwg - 1) / nwg;
-        chunk = tiles_per_wg * G::TILE;
-        nwg = (uint32_t)((ntiles + tiles_per_wg - 1) / tiles_per_wg);
-        nblk = nwg;
-    }
-    uint32_t* counts = (uint32_t*)ws->scratch("pt_counts", (size_t)nbins * nblk * 4);
+    const uint64_t tiles_per_wg = (ntiles + nwg - 1) / nwg;
+    const uint64_t chunk = tiles_per_wg * G::TILE;
+    nwg = (uint32_t)((ntiles + tiles_per_wg - 1) / tiles_per_wg);
+    uint32_t* counts = (uint32_t*)ws->scratch("pt_counts", (size_t)nbins * nwg * 4);
     uint64_t* totals = (uint64_t*)ws->scratch("pt_totals", (size_t)nbins * 8);
     {
-        // per block (the scatter's blocks)
         TraceScope ts(ws, "k_hist", st);
         bool vec = false;
         if constexpr (sizeof(Tup) == 8) {
             vec = ((uintptr_t)in & 15) == 0 && (chunk & 1) == 0;
             if (vec)
-                hipLaunchKernelGGL((k_hist_v<512, 8, Digit>), dim3(nblk), dim3(512),
+                hipLaunchKernelGGL((k_hist_v<512, 8, Digit>), dim3(nwg), dim3(512),
                                    nbins * sizeof(uint32_t), st, in, n, chunk, dig, nbins,
-                                   counts, nblk);
+                                   counts, nwg);
         }
         if (!vec)
-            hipLaunchKernelGGL((k_hist_p<512, 16, Digit, true>), dim3(nblk), dim3(512),
+            hipLaunchKernelGGL((k_hist_p<512, 16, Digit, true>), dim3(nwg), dim3(512),
                                nbins * sizeof(uint32_t), st, in, n, chunk, dig, nbins, counts,
-                               nblk);
+                               nwg);
     }
     {
         TraceScope ts(ws, "k_scan", st);
-        hipLaunchKernelGGL(k_scanrow, dim3(nbins), dim3(256), 0, st, counts, nblk, totals);
+        hipLaunchKernelGGL(k_scanrow, dim3(nbins), dim3(256), 0, st, counts, nwg, totals);
         hipLaunchKernelGGL(k_scandig, dim3(1), dim3(256), 0, st, totals, nbins, padded,
                            starts_dev, hist_out, off_out);
     }
@@ -1862,8 +1801,8 @@ static void stable_partition_swp(Workspace* ws, const Tup* in, uint64_t n, Tup* 
     set_lds_attr((const void*)k_scatter_swp<THREADS, ITEMS, Digit, true>, 160 * 1024);
     TraceScope ts(ws, "k_scatter", st);
     hipLaunchKernelGGL((k_scatter_swp<THREADS, ITEMS, Digit, true>), dim3(nwg), dim3(THREADS),
-                       G::lds_bytes(nbins), st, in, n, chunk, dig, nbins, counts, nblk,
-                       starts_dev, out, 1, xcd_order);
+                       G::lds_bytes(nbins), st, in, n, chunk, dig, nbins, counts, nwg,
+                       starts_dev, out, 1);
     SMJ_CHECK(hipGetLastError());
 }
 
