@@ -2212,9 +2212,9 @@ int smj_dev_partition_range_planes(smj_workspace* wsp, const tuple_t* in, uint64
                                    smj_stream_t stream) {
     Workspace* ws = (Workspace*)wsp;
     hipStream_t st = (hipStream_t)stream;
-    // the scatter's LDS carries hold 2^9 partitions of 48-bit words (the
-    // 1-GPU join's limit for this layout too)
-    if (nbits > 9 || n >= (1ull << 32)) return 0;
+    // the scatter's LDS carries hold 2^10 partitions of 48-bit words with its
+    // 16-byte segments (round 6; 2^9 was the limit of 64-byte segments)
+    if (nbits > 10 || n >= (1ull << 32)) return 0;
     RangePlan h = make_plan(key_min, key_max, nbits, 0, 0, 0);
     if (!LayP48::usable(h)) return 0;
     if (stride % 32 || stride < sampled_capacity(n, nbits)) {

@@ -85,7 +85,7 @@ namespace mg {
 // plan arithmetic (the same functions as smj/dist.py, which documents them)
 // ---------------------------------------------------------------------------
 constexpr uint32_t kMaxPartBits = 10;   // widest exchange partition (2^10)
-constexpr uint32_t kPlaneMaxBits = 9;   // the 48-bit scatter's LDS carries
+constexpr uint32_t kPlaneMaxBits = 10;  // the 48-bit scatter's LDS carries (16-byte segments)
 constexpr uint64_t kLocalBucketCap = 192ull * 16384;  // tiles of the tile pass
 constexpr uint32_t kHead = 4;           // message head (exchange.hip kXHead)
 constexpr uint32_t kBadPayload = 1, kBadRange = 2, kBadPayload48 = 4;

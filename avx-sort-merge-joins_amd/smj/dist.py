@@ -54,10 +54,11 @@ INT64_MAX = (1 << 63) - 1
 CHUNK_BYTES = 512 << 20
 # The exchange layouts, narrowest last: tuples, 64-bit packed words (16-byte
 # tuples only), 48-bit words in two planes (LayP48, both widths; the sampled
-# partition's LDS carries hold at most 2^9 partitions of them).  Both
-# relations of a step reach the local join in one layout.
+# partition's LDS carries hold at most 2^10 partitions of them with 16-byte
+# segments: round 6, 2^9 before).  Both relations of a step reach the local
+# join in one layout.
 LAYOUTS = ("tuples", "words", "planes")
-PLANE_MAX_BITS = 9
+PLANE_MAX_BITS = 10
 # a local bucket the tile pass / group pass take in stride: <= 192 tiles of
 # 16384 elements (choose_levels' bucket_cap in the library)
 LOCAL_BUCKET_CAP = 192 * 16384
@@ -168,8 +169,9 @@ def planes_hold(key_min: int, key_max: int, pbits: int) -> bool:
     payloads are taken to lie within the key span (the row ids of a PK
     relation, as in the benchmark).  Where they would not, every step would
     partition twice (planes, then 64-bit words once a rank reports a payload
-    too wide), so the exchange starts with words: 128M per rank at G = 4 is
-    such a case (keys 1..512M, 2^9 partitions: s1 = 20, payloads below 2^28)."""
+    too wide), so the exchange starts with words: 128M per rank at G = 8 is
+    such a case (keys 1..1024M, 2^10 partitions: s1 = 20, payloads below
+    2^28); at G = 4 (keys 1..512M, s1 = 19) row ids fit."""
     s1 = plan_shift(key_min, key_max, pbits)
     return 1 <= s1 <= 32 and key_max - key_min < (1 << (48 - s1))
 
@@ -178,7 +180,8 @@ def partition_bits(bucket_bits: int, world: int, planes: bool, n_hint=None,
                    key_range=None) -> int:
     """Exchange partition width: bucket_bits per rank (2^min(bucket_bits +
     log2 G, 10) partitions), unless the 48-bit planes are offered and one bit
-    less keeps them: 2^9 partitions, when every rank's share (n_hint elements
+    less keeps them (only where PLANE_MAX_BITS < MAX_PARTITION_BITS, as before
+    round 6): 2^9 partitions, when every rank's share (n_hint elements
     per relation, balanced) still splits into local buckets of at most
     LOCAL_BUCKET_CAP elements (at 128M per rank up to G = 8: 2^6 local
     buckets of 2M) and, given key_range, the words hold the payloads

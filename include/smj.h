@@ -748,7 +748,7 @@ int smj_dev_partition_range_sampled(smj_workspace * ws, const tuple_t * in, uint
  * stride >= smj_sampled_capacity(n, nbits), a multiple of 32.  flags[1]
  * gets 1 (payload wider than 64 - s1 bits), 2 (key outside the range) or 4
  * (payload wider than 48 - s1 bits), or-ed.  Returns 0 (nothing launched)
- * when the form does not apply: nbits > 9, n >= 2^32, or s1 outside 1..32. */
+ * when the form does not apply: nbits > 10, n >= 2^32, or s1 outside 1..32. */
 int smj_dev_partition_range_planes(smj_workspace * ws, const tuple_t * in, uint64_t n,
                                    void * out, uint64_t stride, uint32_t nbits,
                                    int64_t key_min, int64_t key_max, int64_t * seg_start,

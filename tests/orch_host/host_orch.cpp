@@ -214,7 +214,7 @@ struct HostOps {
                     int64_t kmin, int64_t kmax, int64_t* ss, int64_t* sc, uint32_t* flags) {
         const Tup* in = (const Tup*)inv;
         Range rg(kmin, kmax, nbits);
-        if (not_applicable || nbits > 9 || rg.s1 < 1 || rg.s1 > 32) return 0;
+        if (not_applicable || nbits > 10 || rg.s1 < 1 || rg.s1 > 32) return 0;
         CHECK(stride % 32 == 0 && stride >= sampled_capacity(n, nbits),
               "planes stride %llu", (unsigned long long)stride);
         std::vector<uint64_t> pos;

@@ -124,7 +124,7 @@ class HostOps:
         w = (key - base) mod 2^s1 << (48 - s1) | payload, lo 32 bits in
         out.lo, hi 16 in out.hi; flags[1] or-s 1 / 2 / 4 (payload over 64 -
         s1 bits / key outside the range / payload over 48 - s1 bits)."""
-        if self.not_applicable or nbits > 9:
+        if self.not_applicable or nbits > 10:
             return False
         s1 = self._s1(key_min, key_max, nbits)
         if not 1 <= s1 <= 32:
@@ -313,9 +313,9 @@ def _worker(rank, world, port, n, q, s_payload="negative", mode="sampled", plane
         ops = HostOps(orc, sampled=mode != "exact", overflow=mode == "overflow" and rank == 1,
                       not_applicable=mode == "mixed" and rank == 0, planes=planes,
                       shards=shards)
-        if wide:  # 2^9 buckets per rank: planes take 2^9 partitions across ranks
+        if wide:  # 2^9 buckets per rank: 2^10 partitions across ranks, planes too
             dj = DistributedJoin(ops, 9, 1, total, n_hint=n, staged=staged)
-            assert dj.pbits == (9 if ops.can_planes else 9 + (world > 1))
+            assert dj.pbits == 9 + (world > 1)
         else:
             dj = DistributedJoin(ops, 6, 1, total, staged=staged)
         # the layout both relations reach the local join in: planes when the
@@ -547,31 +547,29 @@ def test_local_range_int64_edges():
 
 
 def test_partition_bits():
-    """The exchange's partition width: bucket_bits + log2 G up to 2^10, or
-    2^9 where the 48-bit planes then fit and every rank's local buckets stay
-    within LOCAL_BUCKET_CAP (128M per rank: up to G = 8) and, given the key
-    range, 48-bit words hold payloads as wide as the key span."""
+    """The exchange's partition width: bucket_bits + log2 G up to 2^10.  Since
+    round 6 the 48-bit planes' scatter takes 2^10 partitions (16-byte
+    segments), so no bit is given up for them; whether the planes are tried
+    is planes_hold's: 48-bit words hold payloads as wide as the key span."""
     import sys
     sys.path.insert(0, PKG)
-    from smj.dist import partition_bits
+    from smj.dist import partition_bits, planes_hold
     n = 128_000_000
     assert partition_bits(9, 1, True, n) == 9
     assert partition_bits(9, 2, False, n) == 10
-    assert partition_bits(9, 2, True, None) == 10  # no hint: the default width
-    assert partition_bits(9, 2, True, n) == 9
-    assert partition_bits(9, 4, True, n) == 9
-    assert partition_bits(9, 8, True, n) == 9  # 2^6 buckets of 2M, within the cap
-    assert partition_bits(9, 8, True, 2 * n) == 10  # 4M a bucket: past it
-    assert partition_bits(9, 8, True, n, (1, 8 * n)) == 10  # 27 payload bits
+    assert partition_bits(9, 2, True, None) == 10
+    assert partition_bits(9, 2, True, n) == 10
+    assert partition_bits(9, 8, True, n) == 10
     assert partition_bits(6, 3, True, n) == 8
-    assert partition_bits(9, 16, True, 1000) == 10  # fewer than 2^6 local buckets
-    # payloads taken to lie within the key span (row ids): keys 1..512M at
-    # 2^9 partitions leave 28 payload bits, too few -> 64-bit words, 2^10
-    from smj.dist import planes_hold
+    assert partition_bits(9, 16, True, 1000) == 10
+    assert partition_bits(8, 2, True, n, (1, 2 * n)) == 9
     assert partition_bits(8, 4, True, n, (1, 4 * n)) == 10
-    assert partition_bits(8, 2, True, n, (1, 2 * n)) == 9  # 2^9 natively
-    assert partition_bits(9, 2, True, n, (1, 2 * n)) == 9  # 29 payload bits hold 256M
-    assert planes_hold(1, n, 8) and planes_hold(1, 2 * n, 9)
+    assert partition_bits(8, 8, True, n, (1, 8 * n)) == 10
+    # the benchmark's row ids (payloads within the key span): planes hold at
+    # G = 1, 2, 4 (keys 1..512M at 2^10: s1 = 19, 29 payload bits), not at
+    # G = 8 (keys 1..1024M: s1 = 20, 28 payload bits)
+    assert planes_hold(1, n, 8) and planes_hold(1, 2 * n, 9) and planes_hold(1, 4 * n, 10)
+    assert not planes_hold(1, 8 * n, 10)
     assert not planes_hold(1, 4 * n, 9) and not planes_hold(1, 8 * n, 9)
 
 
