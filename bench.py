@@ -1027,9 +1027,11 @@ def run_exchange_device_side(a, json_out, lib, n, w):
     lib.dev_gen_fk(S, 0, total, total, 54321)
     torch.cuda.synchronize()
     pbits = partition_bits(a.fanout_bits, G, True, n, (1, total))
-    sampled = a.exchange_form == "sampled"
-    dj = DistributedJoin(DeviceOps(lib, sampled=sampled, planes=False), a.fanout_bits, 1,
-                         total, n_hint=n, pbits=pbits)
+    # the ops a rank of G > 1 has: the 48-bit planes where they hold (always
+    # the sampled form), else words or tuples in the exact form
+    ops = DeviceOps(lib)
+    ops._sampled = a.exchange_form == "sampled"
+    dj = DistributedJoin(ops, a.fanout_bits, 1, total, n_hint=n, pbits=pbits)
     res = {}
 
     def step():
