@@ -351,7 +351,7 @@ def test_rccl_list_all_to_all_views(libs, monkeypatch):
 def test_partition_range_planes_flags(libs, width):
     """smj_dev_partition_range_planes' not-packable flags and its limits: a
     payload wider than 48 - s1 bits sets 4 (and 1 past 64 - s1 bits), a key
-    outside the range 2; more than 2^9 partitions: not applicable (False,
+    outside the range 2; more than 2^10 partitions: not applicable (False,
     nothing launched).  Clean input: every element comes back unpacked from
     its region (the words restated here)."""
     import torch
@@ -403,4 +403,7 @@ def test_partition_range_planes_flags(libs, width):
     out_of_range = keys.clone()
     out_of_range[3] = kmax + 5
     assert run(out_of_range, pays)[4][1] & 2
-    assert not run(keys, pays, bits=10)[0]
+    # 2^10 partitions apply since round 6 (16-byte segments), 2^11 do not
+    ok10, _, _, sc10, fl10 = run(keys, pays, bits=10)
+    assert ok10 and fl10 == [0, 0] and int(sc10.sum()) == n
+    assert not run(keys, pays, bits=11)[0]
