@@ -1037,7 +1037,7 @@ def run_exchange_device_side(a, json_out, lib, n, w):
     def step():
         res["x"] = dj._exchange(S, "S")
     elapsed, kern, brk = timed_loop(a, lib, None, step)
-    xb = dj.last_rows["S"][0]
+    xb, cap = dj.last_rows["S"][0], dj.last_rows["S"][1]
     eb = row_bytes(xb)
     lay = res["x"][-1]  # the layout the attempt ended in
     # rows rank 0 keeps: the partitions it owns among G ranks
@@ -1054,7 +1054,9 @@ def run_exchange_device_side(a, json_out, lib, n, w):
                 "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                 "alg_bytes_per_launch": alg_sc, "avg_launch_ms": round(sc_ms / sc_n, 4)}
-    leave = n * (G - 1) / G * eb  # uniform keys: (G-1)/G of the rows leave the rank
+    # uniform keys: (G-1)/G of the rows leave the rank, in chunks that carry
+    # the sampled form's region slack (cap elements for n; exact: cap = n)
+    leave = cap * (G - 1) / G * eb
     xgmi_peak = 7 * 153.0
     out = {
         "metric": "exchange (the join's row exchange) GB/s per GPU over xGMI",
@@ -1074,6 +1076,8 @@ def run_exchange_device_side(a, json_out, lib, n, w):
                     f"rank does for the exchange at {G} GPUs (HBM roofline of its partition)",
             "kernels_ms_per_step": {k: round(v[0], 4) for k, v in brk.items()},
             "exchange_layout": lay, "partition_bits": pbits, "owned_partitions_rank0": hi - lo,
+            "partition_form": "sampled (regions with slack)" if cap > n else "exact",
+            "elements_with_slack": int(cap),
             "xgmi_bytes_leaving_rank_per_step": int(leave),
             "xgmi_ms_at_link_peak": round(leave / (xgmi_peak * 1e9) * 1e3, 3),
             "xgmi_peak_GBps": xgmi_peak,
