@@ -2492,6 +2492,7 @@ bool bucket_sort(Workspace* ws, const BucketSortArgs& a, hipStream_t st) {
                 : bucket_sort_nosync<LayP48>(ws, a, st);
 #ifdef KEY_8B
         if (a.packed) return bucket_sort_nosync<LayPacked>(ws, a, st);
+        if (a.p96) return bucket_sort_nosync<LayP96>(ws, a, st);
 #endif
         return bucket_sort_nosync<LayTup>(ws, a, st);
     }

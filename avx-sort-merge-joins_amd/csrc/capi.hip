@@ -305,6 +305,10 @@ static bool use_p48(const Workspace* ws) { return !(ws->layouts_off & SMJ_LAYOUT
 // ... and 32-bit words before those (LayP32) where the payloads are tiny
 static bool use_p32(const Workspace* ws) { return !(ws->layouts_off & SMJ_LAYOUT_NO_P32); }
 
+// ... and, where no packed word holds the payloads, 12-byte elements (LayP96:
+// the payload and a 32-bit key offset) instead of the 16-byte tuples
+static bool use_p96(const Workspace* ws) { return !(ws->layouts_off & SMJ_LAYOUT_NO_P96); }
+
 // Sort of one relation (nrel 1) or sort + merge-join count of two (nrel 2):
 // range plan -> sampled level-1 partition -> tile pass -> group pass.  The
 // plan must be known on the host (no mid-pipeline synchronisation, and 16-byte
@@ -446,6 +450,15 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
         hinted = h > m;
         return h > m ? h : m;
     };
+    // the sampled tuples' attempt (mode 1) on 16-byte tuples: 12-byte
+    // elements where the plan spans at most 2^32 keys (LayP96)
+    auto p96_ok = [&]() {
+#ifdef KEY_8B
+        return sampled && plan_on_host && use_p96(ws) && LayP96::usable(hplan) && nb <= 1024;
+#else
+        return false;
+#endif
+    };
     int mode = hinted_mode(first_mode());
     const bool started_hinted = hinted;
     int payload_fb = -2;  // the mode a payload flag sent this call to
@@ -454,8 +467,9 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
         const bool p32 = mode == -2;
         const bool p48 = mode == -1;
         const bool packed = mode <= 0;
+        const bool p96 = mode == 1 && p96_ok();
         // the status word the tile and group passes exit on (sampled modes)
-        const bool check = packed || (guessed && mode == 1);
+        const bool check = packed || p96 || (guessed && mode == 1);
         hipLaunchKernelGGL(k_join_begin, dim3(1), dim3(256), 0, st, plan, hplan,
                            plan_on_host ? 1 : 0, cnt, status, sample,
                            mode < 2 ? (uint32_t)nrel * nb : 0u);
@@ -463,11 +477,11 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
         // rounded to 32 (the hi plane starts 16-byte aligned); the buffer
         // holds 16 bytes an element, the planes take 6
         uint64_t pstride[2] = {0, 0};
-        for (int r = 0; r < nrel && p48; r++)
+        for (int r = 0; r < nrel && (p48 || p96); r++)
             pstride[r] = (sampled_capacity(ns[r], D1) + 31) & ~31ull;
         if (mode < 2) {
             void* outs_v[2] = {part[0], part[nrel > 1 ? 1 : 0]};
-            if (p48 && nrel > 1 && pstride[0] != pstride[1]) {
+            if ((p48 || p96) && nrel > 1 && pstride[0] != pstride[1]) {
                 // one stride per launch: the two relations take turns.  Both
                 // calls use relation 0's region scratch (cursor, cap_end):
                 // correct because they run in order on the one stream `st`
@@ -481,12 +495,13 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
                     int64_t* sgc1[1] = {sgc[r]};
                     sampled_partition(ws, 1, rr1, nn1, oo1, plan, D1, sample + (size_t)r * nb,
                                       bs1, bh1, sgs1, sgc1, status, st, &hplan, true,
-                                      status + 1, pstride[r]);
+                                      status + 1, pstride[r], false, false, p96);
                 }
             } else {
                 sampled_partition(ws, nrel, rels, ns, outs_v, plan, D1, sample, bst, bh, sgs,
-                                  sgc, status, st, plan_on_host ? &hplan : nullptr, packed,
-                                  check ? status + 1 : nullptr, pstride[0], p32);
+                                  sgc, status, st, plan_on_host ? &hplan : nullptr,
+                                  packed || p96, check ? status + 1 : nullptr, pstride[0], p32,
+                                  false, p96);
             }
         } else {
             for (int r = 0; r < nrel; r++)
@@ -517,6 +532,7 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
         a.packed = packed;
         a.p48 = p48;
         a.p32 = p32;
+        a.p96 = p96;
         a.pstride[0] = pstride[0];
         a.pstride[1] = pstride[1];
         a.pack_bad = check ? status + 1 : nullptr;
@@ -568,7 +584,8 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
         mode++;
     }
     ws->last_layout = mode == -2 ? SMJ_LAYOUT_USED_P32 : mode == -1 ? SMJ_LAYOUT_USED_P48
-                    : mode == 0 ? SMJ_LAYOUT_USED_WORDS : SMJ_LAYOUT_USED_TUPLES;
+                    : mode == 0 ? SMJ_LAYOUT_USED_WORDS
+                    : mode == 1 && p96_ok() ? SMJ_LAYOUT_USED_P96 : SMJ_LAYOUT_USED_TUPLES;
     if (payload_fb >= 0)
         H.mode_hint = payload_fb;
     else if (!started_hinted)

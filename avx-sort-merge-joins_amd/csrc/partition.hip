@@ -2093,9 +2093,16 @@ void sampled_partition(Workspace* ws, int nrel, const Tup* const* in, const uint
                        int64_t* const* hist_out, uint64_t* const* seg_start,
                        int64_t* const* seg_cnt, unsigned int* flag_dev, hipStream_t st,
                        const RangePlan* host_plan, bool packed, unsigned int* bad,
-                       uint64_t p48_stride, bool p32, bool exact) {
+                       uint64_t p48_stride, bool p32, bool exact, bool p96) {
     PlanDigit1 dig{plan_dev};
     const uint32_t nbins = 1u << dbits;
+    // p96 (16-byte tuples): LayP96 elements in two planes of p48_stride
+    // elements (int64 payloads, then uint32 key offsets)
+    if (p96 && (sizeof(Tup) != 16 || !host_plan || !p48_stride || p32 || exact)) {
+        fprintf(stderr, "[ERROR] smj: the 96-bit layout needs 16-byte tuples, the host plan "
+                        "and a plane stride\n");
+        abort();
+    }
     if (exact && (p48_stride || p32)) {
         fprintf(stderr, "[ERROR] smj: exact shard regions take tuples or 64-bit words\n");
         abort();
@@ -2185,7 +2192,8 @@ void sampled_partition(Workspace* ws, int nrel, const Tup* const* in, const uint
         // elements, so the hi plane's regions start on 64 bytes)
         hipLaunchKernelGGL(k_regions, dim3(nrel), dim3(256), 0, st, R, nbins, kSampleStride,
                            kRegionSlack,
-                           p48_stride || p32 ? 4u : packed ? 8u : (uint32_t)sizeof(Tup));
+                           p96 ? 8u : p48_stride || p32 ? 4u : packed ? 8u
+                                                                     : (uint32_t)sizeof(Tup));
     }
     for (int r = 0; r < nrel; r++) {
         if (!n[r]) continue;
@@ -2198,6 +2206,16 @@ void sampled_partition(Workspace* ws, int nrel, const Tup* const* in, const uint
                             pk, bad, st);
             continue;
         }
+#ifdef KEY_8B
+        if (p96) {
+            LayP96::Pack pk;
+            pk.bu = key_u(host_plan->base);
+            pk.span = host_plan->span;
+            sampled_scatter(ws, in[r], n[r], out[r], p48_stride, dig, nbins, R.cursor[r],
+                            R.cap_end[r], pk, bad, st);
+            continue;
+        }
+#endif
         if (p48_stride) {
             LayP48::Pack pk;
             pk.bu = key_u(host_plan->base);

@@ -407,6 +407,154 @@ struct LayPacked {
 };
 #endif
 
+#ifdef KEY_8B
+// ---------------------------------------------------------------------------
+// LayP96 (round 6, 16-byte tuples whose payloads no packed word holds): the
+// full 64-bit payload and the key's offset in the plan range,
+//     rel = key_u(key) - key_u(base)      (< 2^32: plans spanning <= 2^32 keys)
+// stored as two planes of one buffer: pay = int64[stride], then rel =
+// uint32[stride].  12 bytes an element instead of the 16 of the tuple: the
+// level-1 scatter writes, the tile pass reads and writes and the group pass
+// reads a quarter fewer bytes.  In registers and LDS an element is a 16-byte
+// P96W ordered like (key, payload); the group pass writes the full tuples.  A
+// key outside the plan is flagged kBadRange by the partition (the join then
+// takes the 16-byte tuples).
+// ---------------------------------------------------------------------------
+struct __attribute__((aligned(16))) P96W {
+    int64_t pay;
+    uint32_t rel;
+    uint32_t pad;
+};
+typedef const __attribute__((address_space(1))) int64_t* G64c;
+typedef __attribute__((address_space(1))) int64_t* G64;
+typedef const __attribute__((address_space(1))) uint32_t* G32c96;
+typedef __attribute__((address_space(1))) uint32_t* G32w96;
+struct P96CView {
+    G64c pay;
+    G32c96 rel;
+    __device__ __forceinline__ P96W operator[](uint64_t i) const {
+        P96W w;
+        w.pay = pay[i];
+        w.rel = rel[i];
+        w.pad = 0;
+        return w;
+    }
+    __device__ __forceinline__ P96CView operator+(uint64_t k) const {
+        return P96CView{pay + k, rel + k};
+    }
+};
+struct P96View {
+    G64 pay;
+    G32w96 rel;
+    __device__ __forceinline__ P96View operator+(uint64_t k) const {
+        return P96View{pay + k, rel + k};
+    }
+};
+__device__ __forceinline__ void st_w(const P96View& p, const P96W& w) {
+#if SMJ_NT_STORES
+    __builtin_nontemporal_store(w.pay, (int64_t*)p.pay);
+    __builtin_nontemporal_store(w.rel, (uint32_t*)p.rel);
+#else
+    p.pay[0] = w.pay;
+    p.rel[0] = w.rel;
+#endif
+}
+
+struct LayP96 {
+    typedef P96W W;
+    static constexpr bool packed = true;
+    typedef P96CView CView;
+    typedef P96View View;
+    __device__ static __forceinline__ CView cview(const void* b, uint64_t stride) {
+        const int64_t* pay = static_cast<const int64_t*>(b);
+        return CView{(G64c)pay, (G32c96)(const uint32_t*)(pay + stride)};
+    }
+    __device__ static __forceinline__ View view(void* b, uint64_t stride) {
+        int64_t* pay = static_cast<int64_t*>(b);
+        return View{(G64)pay, (G32w96)(uint32_t*)(pay + stride)};
+    }
+    __device__ static __forceinline__ uint64_t rel(const RangePlan&, const W& w, uint32_t) {
+        return w.rel;
+    }
+    __device__ static __forceinline__ bool clamped(const RangePlan&, const W&) { return false; }
+    __device__ static __forceinline__ bool less(const W& a, const W& b) {
+        return a.rel < b.rel || (a.rel == b.rel && a.pay < b.pay);
+    }
+    __device__ static __forceinline__ uint64_t same_key_id(const W& w) {
+        return (uint64_t)w.pay;
+    }
+    // bits [sh, sh + width) of rel (sh + width <= 32)
+    __device__ static __forceinline__ uint32_t digit_fast(const W& w, uint32_t, uint32_t,
+                                                          uint32_t sh, uint32_t mask) {
+        return (w.rel >> sh) & mask;
+    }
+    __host__ static bool fast_ok(const RangePlan&, uint32_t sh, uint32_t width) {
+        return sh + width <= 32;
+    }
+    __device__ static __forceinline__ Tup unpack(const RangePlan& P, const W& w, uint32_t) {
+        Tup t;
+        t.payload = w.pay;
+        t.key = (int64_t)((key_u(P.base) + w.rel) ^ 0x8000000000000000ull);
+        return t;
+    }
+    struct FastDigit {
+        uint32_t sh, mask;
+        __device__ FastDigit(const RangePlan&, uint32_t s, uint32_t width)
+            : sh(s), mask((1u << width) - 1) {}
+        __device__ __forceinline__ uint32_t operator()(const W& w) const {
+            return (w.rel >> sh) & mask;
+        }
+    };
+    struct Unpack {
+        uint64_t kbu;
+        __device__ Unpack(const RangePlan& P, uint32_t) : kbu(key_u(P.base)) {}
+        __device__ __forceinline__ Tup operator()(const W& w) const {
+            Tup t;
+            t.payload = w.pay;
+            t.key = (int64_t)((kbu + w.rel) ^ 0x8000000000000000ull);
+            return t;
+        }
+    };
+    // the level-1 partition's element of tuple t: kBadRange when the key
+    // lies outside the plan (its offset would not be exact)
+    struct Pack {
+        typedef P96W OutT;
+        uint64_t bu, span;
+        __device__ __forceinline__ P96W operator()(const Tup& t, uint32_t& bad) const {
+            const uint64_t ku = key_u(t.key);
+            const uint64_t r = ku - bu;
+            bad |= (ku < bu || r > span) ? kBadRange : 0u;
+            P96W w;
+            w.pay = t.payload;
+            w.rel = (uint32_t)r;
+            w.pad = 0;
+            return w;
+        }
+        static constexpr uint32_t kStoreBytes = 8;  // the payload plane sets the segment
+        __device__ static __forceinline__ void store(void* out, uint64_t stride, uint64_t i,
+                                                     const P96W& x) {
+            int64_t* pay = static_cast<int64_t*>(out);
+            ((G64)pay)[i] = x.pay;
+            ((G32w96)(uint32_t*)(pay + stride))[i] = x.rel;
+        }
+        // elements i and i + 1 (i even): one 16-byte and one 8-byte store
+        static constexpr bool kPairs = true;
+        __device__ static __forceinline__ void store2(void* out, uint64_t stride, uint64_t i,
+                                                      const P96W& x0, const P96W& x1) {
+            typedef long long L2 __attribute__((ext_vector_type(2)));
+            typedef uint32_t U2 __attribute__((ext_vector_type(2)));
+            int64_t* pay = static_cast<int64_t*>(out);
+            L2 p = {x0.pay, x1.pay};
+            U2 r = {x0.rel, x1.rel};
+            *(__attribute__((address_space(1))) L2*)(pay + i) = p;
+            *(__attribute__((address_space(1))) U2*)((uint32_t*)(pay + stride) + i) = r;
+        }
+    };
+    // plans whose range spans at most 2^32 keys (rel fits 32 bits)
+    __host__ static bool usable(const RangePlan& P) { return P.span < (1ull << 32); }
+};
+#endif
+
 // ---------------------------------------------------------------------------
 // LayP48 (round 4, both tuple widths): the packed word of LayPacked cut to
 // 48 bits,

@@ -334,7 +334,7 @@ void sampled_partition(Workspace* ws, int nrel, const Tup* const* in, const uint
                        int64_t* const* seg_cnt, unsigned int* flag_dev, hipStream_t st,
                        const RangePlan* host_plan = nullptr, bool packed = false,
                        unsigned int* bad = nullptr, uint64_t p48_stride = 0,
-                       bool p32 = false, bool exact = false);
+                       bool p32 = false, bool exact = false, bool p96 = false);
 void hist_memcpy(Workspace* ws, const Tup* in, uint64_t n, Tup* out,
                  uint32_t dbits, hipStream_t st);
 // lane order of LDS atomic returns (k_scatter_swp's ranks): violations, 0 expected
@@ -372,6 +372,7 @@ struct BucketSortArgs {
     bool p48 = false;
     uint64_t pstride[2] = {0, 0};
     bool p32 = false;  // part/tmp hold LayP32 words (packed too, one plane)
+    bool p96 = false;  // part/tmp hold LayP96 elements (two planes of pstride[r])
     // optional 4-word block zeroed by the caller: [0] = part_flag, [1] =
     // pack_bad, [2] = the skew queue length (read back in one copy)
     unsigned int* status = nullptr;

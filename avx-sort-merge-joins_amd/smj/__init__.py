@@ -121,9 +121,9 @@ class MgpuStats(C.Structure):
 
 # smj_workspace_set_layouts bits (include/smj.h)
 LAYOUT_NO_P48, LAYOUT_NO_PACKED, LAYOUT_NO_SAMPLED, LAYOUT_SAMPLE_PLAN = 1, 2, 4, 8
-LAYOUT_NO_P32 = 16
+LAYOUT_NO_P32, LAYOUT_NO_P96 = 16, 32
 # smj_workspace_last_layout values
-LAYOUTS_USED = ("tuples", "words", "p48", "p32")
+LAYOUTS_USED = ("tuples", "words", "p48", "p32", "p96")
 # smj_mgpu_join flags (include/smj.h)
 MG_COPY, MG_NOPLANES, MG_ONECALL, MG_SAMPLED, MG_EXACT = 1, 2, 4, 8, 16
 MG_LAYOUTS = ("tuples", "words", "planes")

@@ -540,14 +540,19 @@ void smj_workspace_destroy(smj_workspace * ws);
 #define SMJ_LAYOUT_SAMPLE_PLAN 8u  /* without a key-range hint: plan from a device
                                       sample instead of from the relation size */
 #define SMJ_LAYOUT_NO_P32     16u  /* no 32-bit words (tiny payloads) */
+#define SMJ_LAYOUT_NO_P96     32u  /* no 12-byte elements (payloads no packed word
+                                      holds: 16-byte tuples instead) */
 void smj_workspace_set_layouts(smj_workspace * ws, uint32_t off);
 /* The intermediate layout the last device sort or join on `ws` (NULL: the
  * calling thread's workspace) finished in: tuples, 64-bit packed words,
- * 48-bit words in two planes, 32-bit words; -1 before the first call. */
+ * 48-bit words in two planes, 32-bit words, 12-byte elements (the full
+ * payload and a 32-bit key offset, in two planes); -1 before the first
+ * call. */
 #define SMJ_LAYOUT_USED_TUPLES 0
 #define SMJ_LAYOUT_USED_WORDS  1
 #define SMJ_LAYOUT_USED_P48    2
 #define SMJ_LAYOUT_USED_P32    3
+#define SMJ_LAYOUT_USED_P96    4
 int smj_workspace_last_layout(smj_workspace * ws);
 
 /* Stable radix partition, the device form of partition_relation*.

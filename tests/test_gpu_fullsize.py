@@ -142,12 +142,12 @@ def test_headline_join_full_bitexact(libs, oracles, width, dist_, fanout_bits):
     np.testing.assert_array_equal(gS, wS)
 
 
-@pytest.mark.parametrize("payload,layout", [("wide48", "words"), ("full64", "tuples")])
+@pytest.mark.parametrize("payload,layout", [("wide48", "words"), ("full64", "p96")])
 def test_headline_join_full_payload_layouts(libs, oracles, payload, layout):
     """The headline join (128M x 128M, 16-byte tuples, bench.py's plan) with
     payloads the 48-bit words cannot hold: 2^40 + row id (64-bit packed
-    words) and random 64-bit values, negative ones included (the 16-byte
-    tuples themselves, the persistent tile pass k_tilepass_p).  bench.py
+    words) and random 64-bit values, negative ones included (12-byte
+    elements, LayP96, through the persistent tile pass k_tilepass_p).  bench.py
     --payload sets the same payloads; sorted R, sorted S and the count
     against the oracle's full (key, payload) radix sort."""
     import torch

@@ -800,7 +800,7 @@ def test_sort_p32_words(libs, oracles, width, case):
     """Sorts whose payloads fit 32 - s1 bits (the sort benchmark's payload 0)
     carry 32-bit words through the intermediate passes (LayP32); a wider
     payload sends the call to the next layout that holds it (48-bit words,
-    or tuples for a negative 16-byte payload), and later calls of that shape
+    or 12-byte elements for a negative 16-byte payload), and later calls of that shape
     start there.  The result is the oracle's on every path."""
     import torch
     orc, lib = oracles[width], libs[width]
@@ -815,7 +815,7 @@ def test_sort_p32_words(libs, oracles, width, case):
     elif case == "negative":
         t["payload"][5] = -1
     want = {"pk": "p32", "tiny": "p32", "wide": "p48",
-            "negative": "p48" if width == 8 else "tuples"}[case]
+            "negative": "p48" if width == 8 else "p96"}[case]
     exp = orc.sort(t)
     lib.reset_workspace()  # no layout remembered
     d = lib.to_device(t)
@@ -864,6 +864,44 @@ def test_join_p32_words(libs, oracles, width, n):
         assert np.array_equal(lib.to_host(sR), eR)
         assert np.array_equal(lib.to_host(sS), eS)
         assert lib.last_layout() == ("p32" if n < 1_000_000 else "p48"), (call, lib.last_layout())
+
+
+@pytest.mark.parametrize("case", ["equal", "ragged", "wide_span", "no_p96"])
+def test_join_p96(libs, oracles, case):
+    """16-byte joins whose payloads no packed word holds (random 64-bit
+    values, negative ones included) carry 12-byte elements through the
+    intermediate passes (LayP96: the payload plane and a 32-bit key-offset
+    plane) where the plan spans < 2^32 keys; relations of different sizes
+    partition one at a time (one plane stride a launch).  A plan spanning
+    2^32 keys or more, or SMJ_LAYOUT_NO_P96, takes the 16-byte tuples.
+    Count and sorted relations as the oracle's on every path."""
+    import torch
+    import smj
+    orc, lib = oracles[16], libs[16]
+    nR, nS = {"ragged": (700_001, 1_300_003)}.get(case, (1_000_003, 1_000_003))
+    R, S = make_join_inputs(orc, 16, "pk_fk", nR, nS)
+    rng = np.random.default_rng(96)
+    R["payload"] = rng.integers(-(1 << 63), (1 << 63) - 1, nR, dtype=np.int64)
+    S["payload"] = rng.integers(-(1 << 63), (1 << 63) - 1, nS, dtype=np.int64)
+    if case == "wide_span":
+        R["key"][nR // 2] += np.int64(1) << 33  # one unmatched key far away
+    exp, eR, eS = orc.sortmergejoin(R, S)
+    lib.reset_workspace()
+    lib.set_layouts(smj.LAYOUT_NO_P96 if case == "no_p96" else 0)
+    try:
+        dR, dS = lib.to_device(R), lib.to_device(S)
+        sR, sS = lib.empty(nR), lib.empty(nS)
+        cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+        for call in range(2):
+            lib.dev_join(dR, dS, sR, sS, cnt, 8, 1, max(nR, nS))
+            torch.cuda.synchronize()
+            assert int(cnt.item()) == exp, call
+            assert np.array_equal(lib.to_host(sR), eR), call
+            assert np.array_equal(lib.to_host(sS), eS), call
+            want = "tuples" if case in ("wide_span", "no_p96") else "p96"
+            assert lib.last_layout() == want, (call, lib.last_layout())
+    finally:
+        lib.set_layouts(0)
 
 
 def test_layout_hints_per_shape(libs, oracles):
