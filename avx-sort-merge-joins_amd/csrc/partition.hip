@@ -1442,10 +1442,10 @@ k_scatter_res(const Tup* __restrict__ in, uint64_t n, uint64_t chunk, Digit dig_
         return VEC ? 2u * ((uint32_t)(j / 2) * THREADS + threadIdx.x) + (uint32_t)(j & 1)
                    : (uint32_t)j * THREADS + threadIdx.x;
     };
-    typedef unsigned long long V2 __attribute__((ext_vector_type(2)));
     // clamped loads of the tile at b0 (VEC: n and the chunks are even)
     auto load_tile = [&](Tup (&x)[ITEMS], uint64_t b0) {
 #ifndef KEY_8B
+        typedef unsigned long long V2 __attribute__((ext_vector_type(2)));
         if constexpr (VEC) {
             const V2* __restrict__ vin = reinterpret_cast<const V2*>(in);
             const uint64_t vl = end / 2 - 1;
