@@ -9,8 +9,6 @@
 * DistributedJoin itself runs over a one-rank NCCL (RCCL) group: the same
   code path bench.py --gpus N runs, with the collectives degenerate.
 """
-import os
-import socket
 
 import numpy as np
 import pytest
@@ -224,10 +222,11 @@ def test_sampled_exchange_simulated(libs, oracles, width, world, kind, layout, s
     assert got_total == total
 
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+def _init_one_rank(dist, torch):
+    """A one-rank RCCL group over an in-process store: no TCP port (a port
+    probed free can be taken by another process before the store binds it)."""
+    dist.init_process_group("nccl", rank=0, world_size=1, store=dist.HashStore(),
+                            device_id=torch.device("cuda", 0))
 
 
 @pytest.mark.parametrize("xsampled", ["1", "0"])
@@ -238,10 +237,7 @@ def test_distributed_join_one_rank_rccl(libs, width, xsampled, monkeypatch):
     import torch.distributed as dist
     from smj.dist import DeviceOps, DistributedJoin
     lib = libs[width]
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ["MASTER_PORT"] = str(_free_port())
-    dist.init_process_group("nccl", rank=0, world_size=1,
-                            device_id=torch.device("cuda", 0))
+    _init_one_rank(dist, torch)
     try:
         n = 4_000_000
         R, S = lib.empty(n), lib.empty(n)
@@ -319,9 +315,7 @@ def test_rccl_list_all_to_all_views(libs, monkeypatch):
     rounds): on a one-rank group the call shape and the view semantics."""
     import torch
     import torch.distributed as dist
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ["MASTER_PORT"] = str(_free_port())
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    _init_one_rank(dist, torch)
     try:
         buf = torch.arange(1000, dtype=torch.int64, device="cuda")
         out = torch.full((1000,), -1, dtype=torch.int64, device="cuda")

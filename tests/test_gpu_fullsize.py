@@ -14,7 +14,6 @@ sorts are its stable LSD radix sort (orc_sort_tuples_radix, checked against
 the qsort restatement in tests/test_oracle.py); the join's two run on two host
 threads (ctypes drops the GIL).
 """
-import os
 import time
 from concurrent.futures import ThreadPoolExecutor
 
@@ -238,18 +237,14 @@ def test_distributed_join_n1024_one_rank():
     join) on BASELINE configs[4]'s size, R = S = 1024M 16-byte tuples, S
     Zipf 0.75, over a one-rank RCCL group: count = |S|, both outputs sorted
     and permutations of their inputs (checksums), two steps (buffer reuse)."""
-    import socket
     import torch
     import torch.distributed as dist
     import smj
     from smj.dist import DeviceOps, DistributedJoin
     lib = smj.load(16)
-    with socket.socket() as so:
-        so.bind(("127.0.0.1", 0))
-        port = so.getsockname()[1]
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    # one rank: an in-process store (no TCP port to collide with)
+    dist.init_process_group("nccl", rank=0, world_size=1, store=dist.HashStore(),
+                            device_id=torch.device("cuda", 0))
     try:
         n = 1_024_000_000
         R, S = lib.empty(n), lib.empty(n)
