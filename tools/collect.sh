@@ -17,13 +17,16 @@ for d in "$I" "$I/nopmc"; do
     n=$(basename "$f" _noprof.json)
     t=$n
     # a second line of a config (the unprofiled pass of a later call): keep the first
-    [ "$d" = "$I/nopmc" ] && { [ -f "$I/${n}_noprof.json" ] || [ -f "$P/${R}_${n}_noprof.json" ]; } && t=${n}b
+    # (the first line: this call's PMC'd lines or PART=1's)
+    [ "$d" = "$I/nopmc" ] && { [ -f "$I/${n}_noprof.json" ] || [ -f "gpurun_out/${R}_fin/${n}_noprof.json" ]; } && t=${n}b
     cp "$f" "$P/${R}_${t}_noprof.json"
     [ -f "$d/$n.json" ] && cp "$d/$n.json" "$P/${R}_$t.json"
     s=$(stats "$d/trace_$n"); [ -n "$s" ] && cp "$s" "$P/${R}_${t}_kernel_stats.csv"
   done
 done
-[ -f "$I/roofcheck.json" ] && cp "$I/roofcheck.json" "$P/${R}_roofcheck.json"
+# the roofline checks per part: the join lines, the op lines (PART=2), 1024M (PART=3)
+case "$I" in *_fin2) rs=_ops ;; *_fin3) rs=_n1024 ;; *) rs= ;; esac
+[ -f "$I/roofcheck.json" ] && cp "$I/roofcheck.json" "$P/${R}_roofcheck$rs.json"
 [ -f "$I/nopmc/roofcheck.json" ] && cp "$I/nopmc/roofcheck.json" "$P/${R}_roofcheck_nopmc.json"
 [ -f "$I/pmc_traffic.json" ] && cp "$I/pmc_traffic.json" "$P/pmc_traffic.json"
 [ -f "$I/pytest_gpu.txt" ] && cp "$I/pytest_gpu.txt" "$P/${R}_pytest_gpu.txt"
