@@ -31,4 +31,5 @@ case "$I" in *_fin2) rs=_ops ;; *_fin3) rs=_n1024 ;; *) rs= ;; esac
 [ -f "$I/pmc_traffic.json" ] && cp "$I/pmc_traffic.json" "$P/pmc_traffic.json"
 [ -f "$I/pytest_gpu.txt" ] && cp "$I/pytest_gpu.txt" "$P/${R}_pytest_gpu.txt"
 [ -f "$I/smoke.txt" ] && cp "$I/smoke.txt" "$P/${R}_smoke.txt"
+[ -f "$I/sq_join8.txt" ] && cp "$I/sq_join8.txt" "$P/${R}_sq_join8.txt"
 ls -la "$P" | grep -c "${R}_"
