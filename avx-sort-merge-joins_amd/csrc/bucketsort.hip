@@ -117,6 +117,11 @@ constexpr int GS_THREADS = SMJ_GS_THREADS;      // one workgroup per group
 #ifndef SMJ_GS_WG_PER_CU8
 #define SMJ_GS_WG_PER_CU8 4
 #endif
+// 12-byte elements (LayP96): a workgroup's group buffer is 30 KB, so three
+// fit the 160 KB of LDS
+#ifndef SMJ_GS_WG_PER_CU12
+#define SMJ_GS_WG_PER_CU12 3
+#endif
 // 32-bit words (LayP32) in pair mode (one relation: the sort): the kernel
 // needs ~85 VGPRs and 26 KB of LDS a workgroup, so more fit
 #ifndef SMJ_GS_WG_PER_CU4P
@@ -125,6 +130,7 @@ constexpr int GS_THREADS = SMJ_GS_THREADS;      // one workgroup per group
 template <class W, bool PAIR = false>
 constexpr int gs_wg_per_cu() {
     return sizeof(W) == 16 ? SMJ_GS_WG_PER_CU
+         : sizeof(W) == 12 ? SMJ_GS_WG_PER_CU12
          : (sizeof(W) == 4 && PAIR) ? SMJ_GS_WG_PER_CU4P : SMJ_GS_WG_PER_CU8;
 }
 // 2560 elements per relation: the plan's groups average 2048, so a group's
@@ -2219,7 +2225,7 @@ static void launch_tilepass(const TilePassArgs& T, size_t lds, hipStream_t st) {
     // words (8-byte elements, two loads and two stores each for the 48-bit
     // planes) 0.65 -> 0.68-0.71 ms, the prefetch and the stores together
     // saturating the 63 outstanding memory operations; 32-bit words spill
-    if (SMJ_TP_PERSIST && sizeof(typename Lay::W) == 16) {
+    if (SMJ_TP_PERSIST && sizeof(typename Lay::W) >= 12) {
         hipLaunchKernelGGL((k_tilepass_p<Lay, LayO>), dim3(nblk < 256 ? nblk : 256),
                            dim3(TP_THREADS), lds, st, T);
     } else {

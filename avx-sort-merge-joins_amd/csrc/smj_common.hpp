@@ -415,16 +415,19 @@ struct LayPacked {
 // stored as two planes of one buffer: pay = int64[stride], then rel =
 // uint32[stride].  12 bytes an element instead of the 16 of the tuple: the
 // level-1 scatter writes, the tile pass reads and writes and the group pass
-// reads a quarter fewer bytes.  In registers and LDS an element is a 16-byte
-// P96W ordered like (key, payload); the group pass writes the full tuples.  A
+// reads a quarter fewer bytes.  In registers and LDS an element is a packed
+// 12-byte P96W (three dwords) ordered like (key, payload): a group-pass
+// workgroup's buffer is then 30 KB instead of 41, and three fit a CU instead
+// of two (round 6: the join 4.70 -> 4.33 ms, the group pass 1.81 -> 1.56 ms,
+// profiles/r06_lab/p12_ab.txt).  The group pass writes the full tuples.  A
 // key outside the plan is flagged kBadRange by the partition (the join then
 // takes the 16-byte tuples).
 // ---------------------------------------------------------------------------
-struct __attribute__((aligned(16))) P96W {
+struct __attribute__((packed, aligned(4))) P96W {
     int64_t pay;
     uint32_t rel;
-    uint32_t pad;
 };
+static_assert(sizeof(P96W) == 12, "12-byte element");
 typedef const __attribute__((address_space(1))) int64_t* G64c;
 typedef __attribute__((address_space(1))) int64_t* G64;
 typedef const __attribute__((address_space(1))) uint32_t* G32c96;
@@ -436,7 +439,6 @@ struct P96CView {
         P96W w;
         w.pay = pay[i];
         w.rel = rel[i];
-        w.pad = 0;
         return w;
     }
     __device__ __forceinline__ P96CView operator+(uint64_t k) const {
@@ -527,7 +529,6 @@ struct LayP96 {
             P96W w;
             w.pay = t.payload;
             w.rel = (uint32_t)r;
-            w.pad = 0;
             return w;
         }
         static constexpr uint32_t kStoreBytes = 8;  // the payload plane sets the segment

@@ -455,18 +455,24 @@ def _hot_inputs(orc, width, n, payload):
     S["key"][n // 2: n // 2 + n // 10] = 1000
     if payload == "equal":
         S["payload"] = 0
+    elif payload == "random64":  # no packed word holds them (16 B: LayP96)
+        info = np.iinfo(S["payload"].dtype)
+        rng = np.random.default_rng(64)
+        R["payload"] = rng.integers(info.min, info.max, n, dtype=S["payload"].dtype)
+        S["payload"] = rng.integers(info.min, info.max, n, dtype=S["payload"].dtype)
     else:  # descending payloads: equal-key runs come out of order
         S["payload"] = np.arange(n, 0, -1)
     return R, S
 
 
-@pytest.mark.parametrize("payload", ["equal", "descending"])
+@pytest.mark.parametrize("payload", ["equal", "descending", "random64"])
 @pytest.mark.parametrize("hint", [True, False])
 def test_device_join_hot_keys(libs, oracles, width, payload, hint):
     """Groups too large for LDS: counting-sorted on the device (exact last
     digit); equal-key runs out of payload order fall back to the segmented
     merge sort.  With the key-range hint the host-planned path runs, without
-    it the sampled plan."""
+    it the sampled plan.  Random full-width payloads take the skew kernels in
+    the 12-byte elements at 16 bytes (LayP96)."""
     import torch
     orc, lib = oracles[width], libs[width]
     n = 1 << 20
@@ -483,6 +489,8 @@ def test_device_join_hot_keys(libs, oracles, width, payload, hint):
     assert int(cnt.item()) == exp
     assert np.array_equal(lib.to_host(sR), eR)
     assert np.array_equal(lib.to_host(sS), eS)
+    if payload == "random64" and width == 16:
+        assert lib.last_layout() == "p96"
 
 
 def test_device_join_keys_outside_hint(libs, oracles, width):
