@@ -1964,6 +1964,10 @@ void plan_partition_packed(Workspace* ws, const Tup* in, uint64_t n, uint64_t* o
 #ifndef SMJ_SC_ITEMS16
 #define SMJ_SC_ITEMS16 4   // 16-byte tuples staged as tuples
 #endif
+#ifndef SMJ_SC_ITEMS16Q
+#define SMJ_SC_ITEMS16Q 6  // 16-byte tuples staged as 12-byte elements (LayP96): 4 items
+                           // 1.52 ms, 6 1.47, 8 1.47 (profiles/r06_lab/p12_ab.txt)
+#endif
 #ifndef SMJ_SC_ITEMS16P
 #define SMJ_SC_ITEMS16P 8  // 16-byte tuples staged as packed 8-byte words
 #endif
@@ -2015,7 +2019,9 @@ template <class Pack>
 static int sampled_items(uint32_t nbins) {
     constexpr int THREADS = SMJ_SC_THREADS;
     constexpr int BIG = sizeof(Tup) == 16
-        ? (sizeof(typename Pack::OutT) <= 8 ? SMJ_SC_ITEMS16P : SMJ_SC_ITEMS16)
+        ? (sizeof(typename Pack::OutT) <= 8    ? SMJ_SC_ITEMS16P
+           : sizeof(typename Pack::OutT) <= 12 ? SMJ_SC_ITEMS16Q
+                                               : SMJ_SC_ITEMS16)
         : SMJ_SC_ITEMS8;
     constexpr int SMALL = sizeof(Tup) == 16 ? 4 : 8;
     typedef typename Pack::OutT O;
@@ -2072,7 +2078,9 @@ static void sampled_scatter(Workspace* ws, const Tup* in, uint64_t n, void* out,
         abort();
     }
     constexpr int BIG = sizeof(Tup) == 16
-        ? (sizeof(typename Pack::OutT) <= 8 ? SMJ_SC_ITEMS16P : SMJ_SC_ITEMS16)
+        ? (sizeof(typename Pack::OutT) <= 8    ? SMJ_SC_ITEMS16P
+           : sizeof(typename Pack::OutT) <= 12 ? SMJ_SC_ITEMS16Q
+                                               : SMJ_SC_ITEMS16)
         : SMJ_SC_ITEMS8;
     constexpr int SMALL = sizeof(Tup) == 16 ? 4 : 8;
     // the choice sampled_items makes (k_shard_hist counts with its chunking)
