@@ -1977,6 +1977,11 @@ void plan_partition_packed(Workspace* ws, const Tup* in, uint64_t n, uint64_t* o
 // tools/ab_scvec.sh; 14 items with pair loads 3.12-3.17)
 #define SMJ_SC_ITEMS8 12
 #endif
+#ifndef SMJ_SC_ITEMS8W
+#define SMJ_SC_ITEMS8W 16  // 8-byte tuples staged as 32-bit words (LayP32): bench_sort
+                           // scatter 12 items 0.469 ms, 16 0.435, 20 0.639, 24 0.748
+                           // (profiles/r06_lab/scatter_items.txt)
+#endif
 #ifndef SMJ_SC_WG_PER_CU
 #define SMJ_SC_WG_PER_CU 1
 #endif
@@ -2022,7 +2027,7 @@ static int sampled_items(uint32_t nbins) {
         ? (sizeof(typename Pack::OutT) <= 8    ? SMJ_SC_ITEMS16P
            : sizeof(typename Pack::OutT) <= 12 ? SMJ_SC_ITEMS16Q
                                                : SMJ_SC_ITEMS16)
-        : SMJ_SC_ITEMS8;
+        : (sizeof(typename Pack::OutT) <= 4 ? SMJ_SC_ITEMS8W : SMJ_SC_ITEMS8);
     constexpr int SMALL = sizeof(Tup) == 16 ? 4 : 8;
     typedef typename Pack::OutT O;
     if (ScatterGeom<THREADS, BIG, O, Pack::kStoreBytes>::lds_bytes(nbins) <= 160 * 1024) return BIG;
@@ -2081,7 +2086,7 @@ static void sampled_scatter(Workspace* ws, const Tup* in, uint64_t n, void* out,
         ? (sizeof(typename Pack::OutT) <= 8    ? SMJ_SC_ITEMS16P
            : sizeof(typename Pack::OutT) <= 12 ? SMJ_SC_ITEMS16Q
                                                : SMJ_SC_ITEMS16)
-        : SMJ_SC_ITEMS8;
+        : (sizeof(typename Pack::OutT) <= 4 ? SMJ_SC_ITEMS8W : SMJ_SC_ITEMS8);
     constexpr int SMALL = sizeof(Tup) == 16 ? 4 : 8;
     // the choice sampled_items makes (k_shard_hist counts with its chunking)
     const int items = sampled_items<Pack>(nbins);
