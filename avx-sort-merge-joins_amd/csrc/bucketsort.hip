@@ -80,11 +80,23 @@ constexpr int TP_THREADS = SMJ_TP_THREADS;
 #ifndef SMJ_GS_ARGS_MEM
 #define SMJ_GS_ARGS_MEM 1
 #endif
-// elements a tile-pass thread holds: the stage of a tile is 128 KB of LDS
-// (16-byte elements: 16-byte tuples in their own layout take half the tile)
+// elements a tile-pass thread holds: the stage of a tile is 128 KB of LDS, one
+// tile a CU (16-byte elements: 16-byte tuples in their own layout take half
+// the tile), 64 KB for 32-bit words (two a CU)
+#ifndef SMJ_TP_STAGE4
+#define SMJ_TP_STAGE4 (64 * 1024)  // the stage of 32-bit words (LayP32): two tiles a CU;
+                                   // bench_sort tile pass 0.27 -> 0.19 ms, the step
+                                   // 1.215 -> 1.155 (profiles/r06_lab/tile_stage.txt)
+#endif
+#ifndef SMJ_TP_STAGE8
+#define SMJ_TP_STAGE8 (128 * 1024)  // the stage of 8-byte elements (words, tuples): 64 KB
+                                    // moves as much into the group pass as it saves
+                                    // (profiles/r06_lab/tile_stage.txt)
+#endif
 template <class W>
 constexpr int tp_items() {
-    return (int)(128 * 1024 / sizeof(W)) / TP_THREADS;
+    return (int)((sizeof(W) == 4 ? SMJ_TP_STAGE4 : sizeof(W) == 8 ? SMJ_TP_STAGE8 : 128 * 1024)
+                 / sizeof(W)) / TP_THREADS;
 }
 template <class W>
 constexpr uint32_t tile_elems() {
