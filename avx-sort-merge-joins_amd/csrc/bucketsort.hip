@@ -1522,7 +1522,7 @@ k_groupsort(GroupArgsParam Ap) {
 constexpr int SK_THREADS = SMJ_SK_THREADS;
 constexpr int SK_ITEMS = 8;
 constexpr int SK_CHUNK = SK_THREADS * SK_ITEMS;
-constexpr uint32_t kSkewSmall = 16384;  // tuples per relation, one workgroup
+constexpr uint32_t kSkewSmall = SK_THREADS * 64;  // tuples per relation, one workgroup
 #ifndef SMJ_SKEW_ITEM
 #define SMJ_SKEW_ITEM 8192  // tuples per work item of a large skew group (2048 measured slower)
 #endif
