@@ -35,7 +35,8 @@ def set_payloads(R, S, kind, first):
     the timed region).  wide48: 2^40 + global row id -- more than the 48 - s1
     bits a 48-bit word keeps at the headline plan, within the 64 - s1 of a
     packed 64-bit word; full64: a 64-bit avalanche hash of the global row id,
-    negative for half the rows -- unpackable, the join keeps 16-byte tuples."""
+    negative for half the rows -- no packed word holds them: the join moves
+    12-byte elements (payload + 32-bit key offset, LayP96)."""
     if kind == "rowid" or R.dtype != torch.int64:
         return
     for t, salt in ((R, 0), (S, 1 << 62)):
@@ -126,8 +127,8 @@ def parse():
                    help="join payloads: rowid = the generators' row ids (R: 5 + i; they "
                         "fit 48-bit words: the intermediates move 6 bytes an element); "
                         "wide48 = 2^40 + row id (64-bit packed words, 8 bytes); full64 = "
-                        "random 64-bit values, negative ones included (the 16-byte "
-                        "tuples themselves)")
+                        "random 64-bit values, negative ones included (12-byte "
+                        "elements: the payload and a 32-bit key offset)")
     p.add_argument("--sim-world", type=int, default=8,
                    help="--op exchange on ONE GPU: time the exchange's device side as rank 0 "
                         "of a world of this many GPUs would run it (its slice of the weak-scaled "
@@ -659,7 +660,7 @@ def main():
                                + {"rowid": ", row-id payloads (48-bit intermediates)",
                                   "wide48": ", payloads 2^40 + row id (64-bit packed "
                                             "intermediates)",
-                                  "full64": ", random 64-bit payloads (16-byte tuple "
+                                  "full64": ", random 64-bit payloads (12-byte "
                                             "intermediates)"}[a.payload if w == 16 else "rowid"],
                    "tuples_per_relation_per_gpu": n, "tuples_per_relation_total": total,
                    "tuple_bytes": w, "payload": a.payload if w == 16 else "rowid",
