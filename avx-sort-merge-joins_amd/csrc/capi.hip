@@ -454,7 +454,10 @@ static void device_bucket(Workspace* ws, const Tup* const* rels, const uint64_t*
     // elements where the plan spans at most 2^32 keys (LayP96)
     auto p96_ok = [&]() {
 #ifdef KEY_8B
-        return sampled && plan_on_host && use_p96(ws) && LayP96::usable(hplan) && nb <= 1024;
+        // (16-element segments: the scatter's carries fit LDS up to 512
+        // partitions, as for the 48-bit words)
+        return sampled && plan_on_host && use_p96(ws) && LayP96::usable(hplan) &&
+               nb <= (LayP96::Pack::kStoreBytes < 8 ? 512u : 1024u);
 #else
         return false;
 #endif

@@ -2205,7 +2205,7 @@ void sampled_partition(Workspace* ws, int nrel, const Tup* const* in, const uint
         // elements, so the hi plane's regions start on 64 bytes)
         hipLaunchKernelGGL(k_regions, dim3(nrel), dim3(256), 0, st, R, nbins, kSampleStride,
                            kRegionSlack,
-                           p96 ? 8u : p48_stride || p32 ? 4u : packed ? 8u
+                           p96 ? (uint32_t)SMJ_P96_SEGB : p48_stride || p32 ? 4u : packed ? 8u
                                                                      : (uint32_t)sizeof(Tup));
     }
     for (int r = 0; r < nrel; r++) {

@@ -407,6 +407,9 @@ struct LayPacked {
 };
 #endif
 
+#ifndef SMJ_P96_SEGB
+#define SMJ_P96_SEGB 8  // LayP96::Pack::kStoreBytes
+#endif
 #ifdef KEY_8B
 // ---------------------------------------------------------------------------
 // LayP96 (round 6, 16-byte tuples whose payloads no packed word holds): the
@@ -531,7 +534,9 @@ struct LayP96 {
             w.rel = (uint32_t)r;
             return w;
         }
-        static constexpr uint32_t kStoreBytes = 8;  // the payload plane sets the segment
+        // the plane whose 64 bytes make a segment: 8, the payload plane (8
+        // elements); 4, the offset plane (16)
+        static constexpr uint32_t kStoreBytes = SMJ_P96_SEGB;
         __device__ static __forceinline__ void store(void* out, uint64_t stride, uint64_t i,
                                                      const P96W& x) {
             int64_t* pay = static_cast<int64_t*>(out);
