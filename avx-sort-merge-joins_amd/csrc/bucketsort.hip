@@ -103,6 +103,31 @@ constexpr uint32_t tile_elems() {
     return (uint32_t)(TP_THREADS * tp_items<W>());
 }
 static_assert(tile_elems<uint64_t>() <= 65535 + 1, "u16 prefix rows");
+// 48-bit words staged in LDS as two planes (u32 lo, u16 hi: 6 bytes an
+// element) instead of uint64_t: SMJ_TP_STAGE6 bytes of them a tile (0: off).
+// 72 KB (12288 elements) puts two tiles on a CU instead of one 16384-element
+// tile: the tile pass 0.645 -> 0.570 ms, the group pass +0.05 (runs 3/4 as
+// long); the 16-byte join 3.123 -> 3.100 ms, the 8-byte and the Zipf joins
+// within noise (profiles/r06_lab/tile_stage.txt)
+#ifndef SMJ_TP_STAGE6
+#define SMJ_TP_STAGE6 (72 * 1024)
+#endif
+template <class Lay>
+struct TileStage {
+    static constexpr bool kSplit = false;
+    static constexpr uint32_t kBytes = sizeof(typename Lay::W);
+    static constexpr int kItems = tp_items<typename Lay::W>();
+};
+template <>
+struct TileStage<LayP48> {
+    static constexpr bool kSplit = SMJ_TP_STAGE6 > 0;
+    static constexpr uint32_t kBytes = kSplit ? 6 : 8;
+    static constexpr int kItems = kSplit ? SMJ_TP_STAGE6 / 6 / TP_THREADS : tp_items<uint64_t>();
+};
+template <class Lay>
+constexpr uint32_t tile_elems_l() {
+    return (uint32_t)(TP_THREADS * TileStage<Lay>::kItems);
+}
 // the bucket-size unit of the plan (choose_levels): a level-1 bucket stays
 // within 192 of these (the group pass takes up to 256 tiles of a bucket).
 // 16384, the tile of 8-byte elements: the 1024M x 1024M join then plans 2^9
@@ -242,13 +267,17 @@ __global__ void __launch_bounds__(TP_THREADS)
 k_tilepass(TilePassArgs A) {
     typedef typename Lay::W W;
     static_assert(std::is_same<W, typename LayO::W>::value, "one element type");
-    constexpr int TP_ITEMS = tp_items<W>();
+    typedef TileStage<Lay> TS;
+    constexpr int TP_ITEMS = TS::kItems;
+    constexpr uint32_t TSZ = tile_elems_l<Lay>();
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     if (A.pack_bad && *A.pack_bad) return;
     const RangePlan& P = A.plan;
     const uint32_t nb2 = A.nb2;
     W* stage = reinterpret_cast<W*>(lds_raw);
-    uint32_t* hist = reinterpret_cast<uint32_t*>(lds_raw + tile_elems<W>() * sizeof(W));
+    uint32_t* stage_lo = reinterpret_cast<uint32_t*>(lds_raw);        // kSplit
+    uint16_t* stage_hi = reinterpret_cast<uint16_t*>(lds_raw + TSZ * 4);
+    uint32_t* hist = reinterpret_cast<uint32_t*>(lds_raw + ((TSZ * TS::kBytes + 15) & ~15u));
     uint32_t* scr = hist + nb2;
 
     const int r = blockIdx.x < A.nt[0] ? 0 : 1;
@@ -321,14 +350,23 @@ k_tilepass(TilePassArgs A) {
         uint32_t i = j * TP_THREADS + threadIdx.x;
         if (i < len) {
             uint32_t pos = atomicAdd(&hist[dg[j]], 1u);
-            stage[pos] = v[j];
+            if constexpr (TS::kSplit) {
+                stage_lo[pos] = (uint32_t)v[j];
+                stage_hi[pos] = (uint16_t)(v[j] >> 32);
+            } else {
+                stage[pos] = v[j];
+            }
         }
     }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < TP_ITEMS; j++) {
         uint32_t i = j * TP_THREADS + threadIdx.x;
-        if (i < len) st_w(tmp + off + i, stage[i]);
+        if constexpr (TS::kSplit) {
+            if (i < len) st_w(tmp + off + i, (W)stage_lo[i] | ((W)stage_hi[i] << 32));
+        } else {
+            if (i < len) st_w(tmp + off + i, stage[i]);
+        }
     }
 }
 
@@ -2336,7 +2374,7 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
     const int nrel = a.nrel;
     const uint32_t nb2 = 1u << a.host_plan->D2;
     const uint64_t nmax = nrel > 1 && a.n[1] > a.n[0] ? a.n[1] : a.n[0];
-    const uint32_t tsz = tile_elems<W>();
+    const uint32_t tsz = tile_elems_l<Lay>();
     TileTable tt[2];
     static const char* names[2][8] = {
         {"bs_off0", "bs_len0", "bs_bkt0", "bs_bt00", "bs_pref0", "bs_ost0", "bs_nt0", "bs_preft0"},
@@ -2436,7 +2474,8 @@ static bool bucket_sort_nosync(Workspace* ws, const BucketSortArgs& a, hipStream
     if (ns) {
         {
             TraceScope ts(ws, "k_tilepass", st);
-            const size_t tp_lds = (size_t)tsz * sizeof(W) + nb2 * 4 + 64;
+            const size_t tp_lds =
+                (((size_t)tsz * TileStage<Lay>::kBytes + 15) & ~(size_t)15) + nb2 * 4 + 64;
             launch_tilepass<Lay, LayG>(T, tp_lds, st);
         }
         const uint32_t ubs[2] = {T.nt[0], T.nt[1]};
