@@ -108,9 +108,11 @@ static_assert(tile_elems<uint64_t>() <= 65535 + 1, "u16 prefix rows");
 // 72 KB (12288 elements) puts two tiles on a CU instead of one 16384-element
 // tile: the tile pass 0.645 -> 0.570 ms, the group pass +0.05 (runs 3/4 as
 // long); the 16-byte join 3.123 -> 3.100 ms, the 8-byte and the Zipf joins
-// within noise (profiles/r06_lab/tile_stage.txt)
+// within noise, and the group pass becomes the join's longest kernel at 0.82
+// of its credit instead of the scatter at 0.86 (profiles/r06_lab/tile_stage.txt).
+// Off: within the noise between boxes
 #ifndef SMJ_TP_STAGE6
-#define SMJ_TP_STAGE6 (72 * 1024)
+#define SMJ_TP_STAGE6 0
 #endif
 template <class Lay>
 struct TileStage {
